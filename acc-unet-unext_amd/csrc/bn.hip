@@ -1,0 +1,473 @@
+// Training-mode BatchNorm2d (+LeakyReLU) on NHWC fp32, split into streaming
+// passes whose per-channel statistics are reduced deterministically
+// (per-block partials -> fixed-order reduction, fp64 final accumulation).
+//
+// Reference semantics (torch.nn.BatchNorm2d as used throughout
+// ACC_UNet/ACC_UNet.py, e.g. :235-262): normalise with the biased batch
+// variance, update running_mean / running_var with momentum 0.1 using the
+// UNBIASED variance, eps = 1e-5; eval mode uses the running statistics.
+#include "common.h"
+#include "kernels.h"
+
+// --------------------------------------------------------------------------
+// Channel-tiled streaming geometry: thread t of a 256-thread block owns channel
+// vector cq = t % TCQ (V = 4 or 1 channels) of channel group blockIdx.y and walks
+// rows rg, rg + RG, ... of the block's row range.
+// --------------------------------------------------------------------------
+struct ChanTile {
+  int CQ, TCQ, RG, cq, rg, c0;
+  bool active;
+};
+
+template <int V>
+ACC_DEV ChanTile chan_tile(int C) {
+  ChanTile t;
+  t.CQ = C / V;
+  t.TCQ = t.CQ < 64 ? t.CQ : 64;
+  t.RG = 256 / t.TCQ;
+  int tid = threadIdx.x;
+  t.cq = blockIdx.y * 64 + tid % t.TCQ;
+  t.rg = tid / t.TCQ;
+  t.c0 = t.cq * V;
+  t.active = (t.rg < t.RG) && (t.cq < t.CQ) && (tid % t.TCQ) < t.TCQ;
+  return t;
+}
+
+template <int V>
+ACC_DEV void ldv(const float* p, float (&v)[V]) {
+  if (V == 4) {
+    float4 q = ld4(p);
+    v[0] = q.x; v[1] = q.y; v[2 % V] = q.z; v[3 % V] = q.w;
+  } else {
+    v[0] = p[0];
+  }
+}
+template <int V>
+ACC_DEV void stv(float* p, const float (&v)[V]) {
+  if (V == 4) {
+    st4(p, make_float4(v[0], v[1 % V], v[2 % V], v[3 % V]));
+  } else {
+    p[0] = v[0];
+  }
+}
+
+// Reduce per-thread (a[V], b[V]) across the RG row-groups of the block and write
+// the block's partial row out[(row)*2*C + {0,C} + c].
+template <int V>
+ACC_DEV void block_chan_reduce2(const ChanTile& t, float (&a)[V], float (&b)[V], float* out,
+                                long row, int C) {
+  __shared__ float red[2][256 * 4];
+  int tid = threadIdx.x;
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    red[0][tid * V + j] = a[j];
+    red[1][tid * V + j] = b[j];
+  }
+  __syncthreads();
+  if (t.rg == 0 && t.cq < t.CQ) {
+    int lt = tid % t.TCQ;
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      float sa = 0.f, sb = 0.f;
+      for (int g = 0; g < t.RG; ++g) {
+        sa += red[0][(g * t.TCQ + lt) * V + j];
+        sb += red[1][(g * t.TCQ + lt) * V + j];
+      }
+      out[row * 2 * C + t.c0 + j] = sa;
+      out[row * 2 * C + C + t.c0 + j] = sb;
+    }
+  }
+}
+
+
+__global__ void inc_i64_kernel(long long* p) { *p += 1; }
+
+// out[c] = sum_r part[r*stride + c], fp64 accumulation, c < ncols
+__global__ void __launch_bounds__(256)
+sum_rows_kernel(const float* __restrict__ part, int R, int stride, int ncols,
+                float* __restrict__ out) {
+  __shared__ double red[4][64];
+  int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
+  int c = blockIdx.x * 64 + cl;
+  double s1 = 0.0;
+  if (c < ncols)
+    for (int r = g; r < R; r += 4) s1 += (double)part[(long)r * stride + c];
+  red[g][cl] = s1;
+  __syncthreads();
+  if (g == 0 && c < ncols) out[c] = (float)(red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl]);
+}
+
+// ---------------------------------------------------------------------------
+// colreduce: out[r/RB][w] = sum of in[r][w] over RB consecutive rows (stage 1 of
+// the partial-statistics reduction when there are many partial rows).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+colreduce_kernel(const float* __restrict__ in, float* __restrict__ out, int R, int Wd, int RB) {
+  __shared__ float red[4][64];
+  int c = blockIdx.y * 64 + (threadIdx.x & 63);
+  int g = threadIdx.x >> 6;
+  int r0 = blockIdx.x * RB;
+  int r1 = min(R, r0 + RB);
+  float s = 0.f;
+  if (c < Wd)
+    for (int r = r0 + g; r < r1; r += 4) s += in[(long)r * Wd + c];
+  red[g][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (g == 0 && c < Wd) out[(long)blockIdx.x * Wd + c] = red[0][threadIdx.x] + red[1][threadIdx.x] +
+                                                     red[2][threadIdx.x] + red[3][threadIdx.x];
+}
+
+// Reduce [R][Wd] partial rows into at most 64 rows using ws; returns pointer+rows.
+const float* reduce_partials(const float* part, int R, int Wd, float* ws, int* Rout,
+                                    hipStream_t s) {
+  const float* cur = part;
+  int rows = R;
+  float* bufs[2] = {ws, ws + (size_t)ceil_div(R, 256) * Wd};
+  int which = 0;
+  while (rows > 64) {
+    int RB = 256;
+    int nb = ceil_div(rows, RB);
+    hipLaunchKernelGGL(colreduce_kernel, dim3(nb, ceil_div(Wd, 64)), dim3(256), 0, s, cur,
+                       bufs[which], rows, Wd, RB);
+    cur = bufs[which];
+    which ^= 1;
+    rows = nb;
+  }
+  *Rout = rows;
+  return cur;
+}
+
+size_t accunet_partials_ws_elems(int R, int Wd) {
+  return (size_t)(ceil_div(R, 256) + ceil_div(ceil_div(R, 256), 256) + 2) * Wd;
+}
+
+// ---------------------------------------------------------------------------
+// bn_finalize: partial (sum, sumsq) rows -> mean, rstd, scale, shift; running
+// statistics update (training) or running-stat normalisation (eval).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+bn_finalize_kernel(const float* __restrict__ part, int R, int C, double count,
+                   const float* __restrict__ gamma, const float* __restrict__ beta,
+                   float* __restrict__ rmean, float* __restrict__ rvar, float momentum, float eps,
+                   int training, float* __restrict__ st) {
+  __shared__ double red[2][4][64];
+  int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
+  int c = blockIdx.x * 64 + cl;
+  double s1 = 0.0, s2 = 0.0;
+  if (training && c < C) {
+    for (int r = g; r < R; r += 4) {
+      s1 += (double)part[(long)r * 2 * C + c];
+      s2 += (double)part[(long)r * 2 * C + C + c];
+    }
+  }
+  red[0][g][cl] = s1;
+  red[1][g][cl] = s2;
+  __syncthreads();
+  if (g != 0 || c >= C) return;
+  float mean, var;
+  if (training) {
+    s1 = red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
+    s2 = red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl];
+    double m = s1 / count;
+    double v = s2 / count - m * m;
+    if (v < 0.0) v = 0.0;
+    mean = (float)m;
+    var = (float)v;
+    if (rmean) rmean[c] = (1.f - momentum) * rmean[c] + momentum * mean;
+    if (rvar) {
+      double unb = count > 1.0 ? v * count / (count - 1.0) : v;
+      rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unb;
+    }
+  } else {
+    mean = rmean[c];
+    var = rvar[c];
+  }
+  float rstd = 1.0f / sqrtf(var + eps);
+  float ga = gamma ? gamma[c] : 1.f;
+  float be = beta ? beta[c] : 0.f;
+  float sc = ga * rstd;
+  st[BN_MEAN * C + c] = mean;
+  st[BN_RSTD * C + c] = rstd;
+  st[BN_SCALE * C + c] = sc;
+  st[BN_SHIFT * C + c] = be - mean * sc;
+}
+
+extern "C" int accunet_bn_finalize(const float* part, int R, int C, double count,
+                                   const float* gamma, const float* beta, float* rmean,
+                                   float* rvar, long long* nbt, float momentum, float eps,
+                                   int training, float* st, float* ws, void* stream_) {
+  hipStream_t s = (hipStream_t)stream_;
+  if (C <= 0) return ACC_EBADSHAPE;
+  int rows = R;
+  const float* p = part;
+  if (training) p = reduce_partials(part, R, 2 * C, ws, &rows, s);
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(C, 64)), dim3(256), 0, s, p, rows, C,
+                     count, gamma, beta, rmean, rvar, momentum, eps, training, st);
+  if (training && nbt) {
+    // num_batches_tracked += 1 (int64 buffer)
+    hipLaunchKernelGGL(inc_i64_kernel, dim3(1), dim3(1), 0, s, nbt);
+  }
+  return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+}
+
+
+// ---------------------------------------------------------------------------
+// affine_act: y = act(x*scale[c] + shift[c]) (+ res), optional partial stats of y
+// ---------------------------------------------------------------------------
+template <int V>
+__global__ void __launch_bounds__(256)
+affine_act_kernel(const float* __restrict__ x, const float* __restrict__ sc,
+                  const float* __restrict__ sh, int act, const float* __restrict__ res,
+                  float* __restrict__ y, long P, int C, float* __restrict__ stats) {
+  ChanTile t = chan_tile<V>(C);
+  long rows_per = (P + gridDim.x - 1) / gridDim.x;
+  long r0 = blockIdx.x * rows_per, r1 = min(P, r0 + rows_per);
+  float a[V], b[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) { a[j] = 0.f; b[j] = 0.f; }
+  if (t.active) {
+    float s[V], h[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      s[j] = sc ? sc[t.c0 + j] : 1.f;
+      h[j] = sh ? sh[t.c0 + j] : 0.f;
+    }
+    for (long r = r0 + t.rg; r < r1; r += t.RG) {
+      long off = r * C + t.c0;
+      float v[V];
+      ldv<V>(x + off, v);
+#pragma unroll
+      for (int j = 0; j < V; ++j) v[j] = apply_act(v[j] * s[j] + h[j], act);
+      if (res) {
+        float q[V];
+        ldv<V>(res + off, q);
+#pragma unroll
+        for (int j = 0; j < V; ++j) v[j] += q[j];
+      }
+      stv<V>(y + off, v);
+#pragma unroll
+      for (int j = 0; j < V; ++j) { a[j] += v[j]; b[j] += v[j] * v[j]; }
+    }
+  }
+  if (stats) block_chan_reduce2<V>(t, a, b, stats, blockIdx.x, C);
+}
+
+int stream_rowblocks(long P, int C) {
+  long elems = P * (long)C;
+  long want = elems / (256 * 16);  // ~16 elements per thread
+  if (want < 1) want = 1;
+  if (want > 1024) want = 1024;
+  if (want > P) want = P;
+  return (int)want;
+}
+
+extern "C" int accunet_affine_act_fwd(const float* x, const float* sc, const float* sh, int act,
+                                      const float* res, float* y, long P, int C, float* stats,
+                                      int* stats_rows, void* stream_) {
+  hipStream_t s = (hipStream_t)stream_;
+  int V = (C % 4 == 0) ? 4 : 1;
+  int CQ = C / V;
+  int nb = stream_rowblocks(P, C);
+  if (stats_rows) *stats_rows = nb;
+  dim3 grid(nb, ceil_div(CQ, 64));
+  if (V == 4)
+    hipLaunchKernelGGL(affine_act_kernel<4>, grid, dim3(256), 0, s, x, sc, sh, act, res, y, P, C,
+                       stats);
+  else
+    hipLaunchKernelGGL(affine_act_kernel<1>, grid, dim3(256), 0, s, x, sc, sh, act, res, y, P, C,
+                       stats);
+  return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+}
+
+extern "C" int accunet_stream_rows(long P, int C) { return stream_rowblocks(P, C); }
+
+// ---------------------------------------------------------------------------
+// BatchNorm(+act) backward.
+//   pre = x*scale + shift, g = dy * act'(pre), xhat = (x-mean)*rstd
+//   reduce:   partial (sum g, sum g*xhat) per channel
+//   finalize: dgamma, dbeta, dx = k1*g + k2*x + k3
+//   apply:    dx (optionally accumulated), optional partial column sums of dx
+// ---------------------------------------------------------------------------
+template <int V>
+__global__ void __launch_bounds__(256)
+bn_bwd_reduce_kernel(const float* __restrict__ x, const float* __restrict__ dy,
+                     const float* __restrict__ st, int act, long P, int C,
+                     float* __restrict__ part) {
+  ChanTile t = chan_tile<V>(C);
+  long rows_per = (P + gridDim.x - 1) / gridDim.x;
+  long r0 = blockIdx.x * rows_per, r1 = min(P, r0 + rows_per);
+  float a[V], b[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) { a[j] = 0.f; b[j] = 0.f; }
+  if (t.active) {
+    float mu[V], rs[V], s[V], h[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      mu[j] = st[BN_MEAN * C + t.c0 + j];
+      rs[j] = st[BN_RSTD * C + t.c0 + j];
+      s[j] = st[BN_SCALE * C + t.c0 + j];
+      h[j] = st[BN_SHIFT * C + t.c0 + j];
+    }
+    for (long r = r0 + t.rg; r < r1; r += t.RG) {
+      long off = r * C + t.c0;
+      float xv[V], dv[V];
+      ldv<V>(x + off, xv);
+      ldv<V>(dy + off, dv);
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        float g = dv[j];
+        if (act == ACT_LRELU) g *= lrelu_d(xv[j] * s[j] + h[j]);
+        a[j] += g;
+        b[j] += g * (xv[j] - mu[j]) * rs[j];
+      }
+    }
+  }
+  block_chan_reduce2<V>(t, a, b, part, blockIdx.x, C);
+}
+
+__global__ void __launch_bounds__(256)
+bn_bwd_finalize_kernel(const float* __restrict__ part, int R, int C, double count,
+                       const float* __restrict__ st, const float* __restrict__ gamma,
+                       int training, float* __restrict__ dgamma, float* __restrict__ dbeta,
+                       float* __restrict__ coef) {
+  __shared__ double red[2][4][64];
+  int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
+  int c = blockIdx.x * 64 + cl;
+  double s1 = 0.0, s2 = 0.0;
+  if (c < C)
+    for (int r = g; r < R; r += 4) {
+      s1 += (double)part[(long)r * 2 * C + c];
+      s2 += (double)part[(long)r * 2 * C + C + c];
+    }
+  red[0][g][cl] = s1;
+  red[1][g][cl] = s2;
+  __syncthreads();
+  if (g != 0 || c >= C) return;
+  s1 = red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
+  s2 = red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl];
+  if (dgamma) dgamma[c] = (float)s2;
+  if (dbeta) dbeta[c] = (float)s1;
+  float ga = gamma ? gamma[c] : 1.f;
+  float rstd = st[BN_RSTD * C + c];
+  float mean = st[BN_MEAN * C + c];
+  float k1 = ga * rstd;
+  float k2 = 0.f, k3 = 0.f;
+  if (training) {
+    float mg = (float)(s1 / count), mgx = (float)(s2 / count);
+    k2 = -k1 * rstd * mgx;
+    k3 = -k1 * mg + k1 * mean * rstd * mgx;
+  }
+  coef[c] = k1;
+  coef[C + c] = k2;
+  coef[2 * C + c] = k3;
+}
+
+template <int V>
+__global__ void __launch_bounds__(256)
+bn_bwd_apply_kernel(const float* __restrict__ x, const float* __restrict__ dy,
+                    const float* __restrict__ st, const float* __restrict__ coef, int act,
+                    long P, int C, float* __restrict__ dx, int accumulate,
+                    float* __restrict__ colsum) {
+  ChanTile t = chan_tile<V>(C);
+  long rows_per = (P + gridDim.x - 1) / gridDim.x;
+  long r0 = blockIdx.x * rows_per, r1 = min(P, r0 + rows_per);
+  float a[V], b[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) { a[j] = 0.f; b[j] = 0.f; }
+  if (t.active) {
+    float s[V], h[V], k1[V], k2[V], k3[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      s[j] = st[BN_SCALE * C + t.c0 + j];
+      h[j] = st[BN_SHIFT * C + t.c0 + j];
+      k1[j] = coef[t.c0 + j];
+      k2[j] = coef[C + t.c0 + j];
+      k3[j] = coef[2 * C + t.c0 + j];
+    }
+    for (long r = r0 + t.rg; r < r1; r += t.RG) {
+      long off = r * C + t.c0;
+      float xv[V], dv[V], o[V];
+      ldv<V>(x + off, xv);
+      ldv<V>(dy + off, dv);
+      if (accumulate) ldv<V>(dx + off, o);
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        float g = dv[j];
+        if (act == ACT_LRELU) g *= lrelu_d(xv[j] * s[j] + h[j]);
+        float d = k1[j] * g + k2[j] * xv[j] + k3[j];
+        a[j] += d;
+        o[j] = accumulate ? o[j] + d : d;
+      }
+      stv<V>(dx + off, o);
+    }
+  }
+  if (colsum) block_chan_reduce2<V>(t, a, b, colsum, blockIdx.x, C);
+}
+
+extern "C" int accunet_bn_bwd(const float* x, const float* dy, const float* st,
+                              const float* gamma, int act, int training, long P, int C,
+                              float* dx, int accumulate, float* dgamma, float* dbeta,
+                              float* colsum, int* colsum_rows, float* ws, size_t ws_elems,
+                              void* stream_) {
+  hipStream_t s = (hipStream_t)stream_;
+  int V = (C % 4 == 0) ? 4 : 1;
+  int nb = stream_rowblocks(P, C);
+  if (colsum_rows) *colsum_rows = nb;
+  dim3 grid(nb, ceil_div(C / V, 64));
+  // ws layout: [nb][2][C] partials | coef [3][C] | reduce scratch
+  float* part = ws;
+  float* coef = ws + (size_t)nb * 2 * C;
+  float* scratch = coef + 3 * (size_t)C;
+  if ((size_t)nb * 2 * C + 3 * (size_t)C + accunet_partials_ws_elems(nb, 2 * C) > ws_elems)
+    return ACC_EBADARG;
+  if (V == 4)
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<4>, grid, dim3(256), 0, s, x, dy, st, act, P, C, part);
+  else
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<1>, grid, dim3(256), 0, s, x, dy, st, act, P, C, part);
+  int rows;
+  const float* pr = reduce_partials(part, nb, 2 * C, scratch, &rows, s);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(C, 64)), dim3(256), 0, s, pr, rows, C,
+                     (double)P, st, gamma, training, dgamma, dbeta, coef);
+  if (V == 4)
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<4>, grid, dim3(256), 0, s, x, dy, st, coef, act, P, C,
+                       dx, accumulate, colsum);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<1>, grid, dim3(256), 0, s, x, dy, st, coef, act, P, C,
+                       dx, accumulate, colsum);
+  return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+}
+
+// ---------------------------------------------------------------------------
+// Column sums (conv bias gradients when no BN-backward pass precedes them).
+// ---------------------------------------------------------------------------
+extern "C" int accunet_colsum(const float* x, long P, int C, float* out, float* ws,
+                              size_t ws_elems, void* stream_) {
+  hipStream_t s = (hipStream_t)stream_;
+  int V = (C % 4 == 0) ? 4 : 1;
+  int nb = stream_rowblocks(P, C);
+  dim3 grid(nb, ceil_div(C / V, 64));
+  float* part = ws;
+  float* scratch = ws + (size_t)nb * 2 * C;
+  if ((size_t)nb * 2 * C + accunet_partials_ws_elems(nb, 2 * C) > ws_elems) return ACC_EBADARG;
+  if (V == 4)
+    hipLaunchKernelGGL(affine_act_kernel<4>, grid, dim3(256), 0, s, x, nullptr, nullptr, ACT_NONE,
+                       nullptr, nullptr, P, C, part);
+  else
+    hipLaunchKernelGGL(affine_act_kernel<1>, grid, dim3(256), 0, s, x, nullptr, nullptr, ACT_NONE,
+                       nullptr, nullptr, P, C, part);
+  int rows;
+  const float* pr = reduce_partials(part, nb, 2 * C, scratch, &rows, s);
+  hipLaunchKernelGGL(sum_rows_kernel, dim3(ceil_div(C, 64)), dim3(256), 0, s, pr, rows, 2 * C, C, out);
+  return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+}
+
+// Reduce a partial-stats block [R][2][C] to totals [2][C] (fp32 out).
+extern "C" int accunet_reduce_stats(const float* part, int R, int C, float* out2C, float* ws,
+                                    void* stream_) {
+  hipStream_t s = (hipStream_t)stream_;
+  int rows;
+  const float* pr = reduce_partials(part, R, 2 * C, ws, &rows, s);
+  hipLaunchKernelGGL(sum_rows_kernel, dim3(ceil_div(2 * C, 64)), dim3(256), 0, s, pr, rows, 2 * C,
+                     2 * C, out2C);
+  return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+}

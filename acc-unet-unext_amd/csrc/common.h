@@ -1,0 +1,71 @@
+// Shared device helpers for the ACC-UNet gfx950 kernels.
+//
+// Layout convention for every activation tensor handed to this library:
+// NHWC (channels-last), fp32, contiguous, viewed as a row-major matrix
+// [P = B*H*W pixels][C channels]. A "pixel row" is therefore C contiguous
+// floats, which makes 1x1 convolutions plain row-major GEMMs and keeps the
+// per-channel BatchNorm / SE statistics coalesced along the fast axis.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/accunet.h"
+
+#define ACC_DEV __device__ __forceinline__
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float floatx4v __attribute__((ext_vector_type(4)));
+
+// LeakyReLU slope used everywhere in the reference (torch default 0.01).
+#define LRELU_SLOPE 0.01f
+
+// status codes returned through the C ABI
+#define ACC_OK 0
+#define ACC_EBADSHAPE -1
+#define ACC_EBADARG -2
+#define ACC_ELAUNCH -3
+
+// Fast unsigned division by a runtime-constant divisor (n < 2^31).
+struct FastDiv {
+  uint32_t d, m, s;
+};
+
+static inline FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  uint32_t s = 0;
+  while ((1ull << s) < d) ++s;
+  f.s = s;
+  uint64_t m = ((1ull << 32) * ((1ull << s) - d)) / d + 1;
+  f.m = (uint32_t)m;
+  return f;
+}
+
+ACC_DEV uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  uint32_t t = __umulhi(n, f.m);
+  return (t + n) >> f.s;
+}
+
+ACC_DEV float lrelu(float x) { return x > 0.f ? x : x * LRELU_SLOPE; }
+// torch LeakyReLU backward: grad * (input > 0 ? 1 : slope)
+ACC_DEV float lrelu_d(float pre) { return pre > 0.f ? 1.f : LRELU_SLOPE; }
+
+ACC_DEV float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+ACC_DEV void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+
+ACC_DEV float f4get(const float4& v, int i) {
+  return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
+}
+
+
+ACC_DEV float apply_act(float v, int act) { return act == ACT_LRELU ? lrelu(v) : v; }
+
+// Per-channel BatchNorm state block produced by bn_finalize:
+//   st[0*C + c] = mean, st[1*C + c] = rstd, st[2*C + c] = scale (= gamma*rstd),
+//   st[3*C + c] = shift (= beta - mean*scale)
+// so that bn(x) = x*scale + shift.
+#define BN_MEAN 0
+#define BN_RSTD 1
+#define BN_SCALE 2
+#define BN_SHIFT 3
+
+static inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }

@@ -1,0 +1,49 @@
+// Tile selection + template dispatch for gemm_f32_kernel.
+#pragma once
+#include "gemm_f32.h"
+
+// Tile configurations (WM, TM, TN) -> (BM, BN):
+//   T_A 128x128 (2,2,2)  T_B 128x64 (2,2,1)  T_C 128x32 (4,1,1)
+//   T_D 32x128  (1,1,1)  T_E 64x64  (2,1,1)
+enum { TILE_A = 0, TILE_B, TILE_C, TILE_D, TILE_E, TILE_COUNT };
+
+static inline int tile_bm(int t) {
+  switch (t) { case TILE_A: case TILE_B: case TILE_C: return 128; case TILE_D: return 32; default: return 64; }
+}
+static inline int tile_bn(int t) {
+  switch (t) { case TILE_A: case TILE_D: return 128; case TILE_B: case TILE_E: return 64; default: return 32; }
+}
+
+typedef void (*gemm_kfn)(const GemmParams);
+
+// One translation unit per (AMODE,BMODE,PRO_A,PRO_B) defines this table.
+#define GEMM_DECLARE_TABLE(NAME) extern gemm_kfn NAME[2][TILE_COUNT];
+
+#define GEMM_DEFINE_TABLE(NAME, AM, BMo, PA, PB)                                          \
+  gemm_kfn NAME[2][TILE_COUNT] = {                                                        \
+      {gemm_f32_kernel<AM, BMo, PA, PB, false, false, 2, 2, 2>,                           \
+       gemm_f32_kernel<AM, BMo, PA, PB, false, false, 2, 2, 1>,                           \
+       gemm_f32_kernel<AM, BMo, PA, PB, false, false, 4, 1, 1>,                           \
+       gemm_f32_kernel<AM, BMo, PA, PB, false, false, 1, 1, 1>,                           \
+       gemm_f32_kernel<AM, BMo, PA, PB, false, false, 2, 1, 1>},                          \
+      {gemm_f32_kernel<AM, BMo, PA, PB, true, true, 2, 2, 2>,                             \
+       gemm_f32_kernel<AM, BMo, PA, PB, true, true, 2, 2, 1>,                             \
+       gemm_f32_kernel<AM, BMo, PA, PB, true, true, 4, 1, 1>,                             \
+       gemm_f32_kernel<AM, BMo, PA, PB, true, true, 1, 1, 1>,                             \
+       gemm_f32_kernel<AM, BMo, PA, PB, true, true, 2, 1, 1>}};
+
+GEMM_DECLARE_TABLE(g_gemm_row_nt_p0)
+GEMM_DECLARE_TABLE(g_gemm_row_nt_p1)
+GEMM_DECLARE_TABLE(g_gemm_row_nt_p2)
+GEMM_DECLARE_TABLE(g_gemm_sh3_nt)
+GEMM_DECLARE_TABLE(g_gemm_row_nn)
+GEMM_DECLARE_TABLE(g_gemm_col_nn_p0)
+GEMM_DECLARE_TABLE(g_gemm_col_nn_p1)
+GEMM_DECLARE_TABLE(g_gemm_col_nn_p2)
+GEMM_DECLARE_TABLE(g_gemm_col_nnsh3)
+
+// Host-side driver: picks a tile, split-K factor and launches. ws (workspace,
+// may be null) is used for split-K partial slabs; if the split would not fit it
+// falls back to no split. Returns ACC_OK or an error code.
+int gemm_run(GemmParams p, int amode, int bmode, int pro_a, int pro_b, bool allow_split,
+             float* ws, size_t ws_elems, hipStream_t stream);

@@ -1,0 +1,447 @@
+// fp32 MFMA GEMM engine for every convolution on the ACC-UNet path.
+//
+//   C[M,N] = sum_k A(m,k) * B(k,n)  (+ bias[n]) (+ nearest-upsampled adds) ,
+//   with optional per-column BatchNorm partial statistics in the epilogue.
+//
+// The 1x1 convolutions of HANCBlock / HANCLayer / MLFC / Conv2d_batchnorm
+// (reference ACC_UNet/ACC_UNet.py:229-286, :77-142, :146-186, :338-527), the
+// dense 3x3 ResPath convolutions (:290-328) and their data / weight gradients
+// all map onto this one kernel through operand "modes":
+//   A: AM_ROW    A(m,k) = A[m*lda + k]          (pixels x channels, NHWC; up to 4
+//                                                 channel-concatenated sources)
+//      AM_COL    A(m,k) = A[k*lda + m]          (dY^T for weight gradients)
+//      AM_SHIFT3 A(m,k) = X[shift_tap(m)*lda+ci] (implicit 3x3 conv, k = tap*cin+ci,
+//                                                 zero padding 1)
+//   B: BM_NT     B(k,n) = B[n*ldb + k]          (weights [N][K])
+//      BM_NN     B(k,n) = B[k*ldb + n]          (weights [K][N] / activations for dW)
+//      BM_NN_SHIFT3 B(k=p, n=tap*cin+ci) = X[shift_tap(p)*ldb + ci]  (3x3 dW)
+// Optional operand prologue y = act(x*scale[ch] + shift[ch]) applies a pending
+// BatchNorm(+LeakyReLU) to A's channel axis (AM_ROW) or B's channel axis (BM_NN)
+// so the normalised activation never has to be written to HBM.
+//
+// Matrix core: v_mfma_f32_32x32x2_f32 (exact fp32 fma chain, 64 cyc/SIMD), 4 waves
+// (64-wide) per 256-thread workgroup laid out WM x WN, each wave owning TM x TN
+// 32x32 accumulator tiles (16 regs each). K is staged 16 at a time through a
+// double-buffered, padded, k-major LDS image so every MFMA operand read is a
+// conflict-free ds_read_b32 (lanes 0-31 and 32-63 sit in different bank groups).
+#pragma once
+#include "common.h"
+
+enum { AM_ROW = 0, AM_COL = 1, AM_SHIFT3 = 2 };
+enum { BM_NT = 0, BM_NN = 1, BM_NN_SHIFT3 = 2 };
+
+#define GEMM_BK 16
+#define GEMM_PAD 4
+#define GEMM_THREADS 256
+
+struct GemmParams {
+  int M, N, K;
+  const float* A[4];
+  int lda[4];
+  int kbeg[5];  // A source s covers k in [kbeg[s], kbeg[s+1])
+  int nsrc;
+  const float* a_scale;
+  const float* a_shift;
+  const float* B;
+  int ldb;
+  const float* b_scale;
+  const float* b_shift;
+  int H, W;  // pixel grid of the "pixel" operand (SHIFT3 modes, up-adds)
+  FastDiv fW, fH;
+  int cin;  // channels per tap for the SHIFT3 modes
+  float* C;
+  int ldc;
+  const float* bias;
+  int nup;
+  const float* up[3];
+  int upld[3];
+  int uplog[3];  // log2 of the nearest-upsample factor of each added source
+  float* stats;  // [gridDim.x][2][N] partial column (sum, sumsq) of final C, or null
+  int kchunk;    // K range per blockIdx.z (split-K); >= K means no split
+  size_t zstride;  // element stride between split-K partial slabs
+};
+
+template <int PRO>
+ACC_DEV float pro_apply(float v, float sc, float sh) {
+  if (PRO == PRO_NONE) return v;
+  float y = v * sc + sh;
+  if (PRO == PRO_AFFINE_LRELU) y = lrelu(y);
+  return y;
+}
+
+template <int AMODE, int BMODE, int PRO_A, int PRO_B, bool VA, bool VB, int WM, int TM, int TN>
+__global__ void __launch_bounds__(GEMM_THREADS)
+gemm_f32_kernel(const GemmParams p) {
+  constexpr int WN = 4 / WM;
+  constexpr int BM = WM * TM * 32;
+  constexpr int BN = WN * TN * 32;
+  constexpr int BK = GEMM_BK;
+  constexpr int SA = BM + GEMM_PAD;
+  constexpr int SB = BN + GEMM_PAD;
+  constexpr int NPA = (BM * 4 + GEMM_THREADS - 1) / GEMM_THREADS;
+  constexpr int NPB = (BN * 4 + GEMM_THREADS - 1) / GEMM_THREADS;
+
+  __shared__ __attribute__((aligned(16))) float smem[2 * BK * SA + 2 * BK * SB];
+  float* As = smem;
+  float* Bs = smem + 2 * BK * SA;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave % WM;
+  const int wn = wave / WM;
+  const int l31 = lane & 31;
+  const int lh = lane >> 5;
+
+  const int m0 = blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+  const int M = p.M, N = p.N, K = p.K;
+
+  int kstart = 0, kend = K;
+  if (gridDim.z > 1) {
+    kstart = blockIdx.z * p.kchunk;
+    kend = min(K, kstart + p.kchunk);
+  }
+  const int nkt = kend > kstart ? (kend - kstart + BK - 1) / BK : 0;
+
+  // ---- per-thread A row geometry for the implicit 3x3 conv -----------------
+  int a_h[NPA], a_w[NPA];
+  if (AMODE == AM_SHIFT3) {
+#pragma unroll
+    for (int i = 0; i < NPA; ++i) {
+      int idx = tid + i * GEMM_THREADS;
+      int r = idx >> 2;
+      uint32_t g = (uint32_t)(m0 + r);
+      uint32_t q = fdiv(g, p.fW);
+      a_w[i] = (int)(g - q * p.W);
+      a_h[i] = (int)(q - fdiv(q, p.fH) * p.H);
+    }
+  }
+
+  float4 ra[NPA], rb[NPB];
+
+  auto load_tiles = [&](int k0) {
+    // ------------------------------ A ---------------------------------------
+    if (AMODE == AM_ROW || AMODE == AM_SHIFT3) {
+      int s = 0;
+      if (AMODE == AM_ROW) {
+#pragma unroll
+        for (int j = 1; j < 4; ++j)
+          if (j < p.nsrc && k0 >= p.kbeg[j]) s = j;
+      }
+      const float* Ab = p.A[s];
+      const int lda = p.lda[s];
+      const int kb = p.kbeg[s];
+      const int kend_s = (AMODE == AM_ROW) ? min(p.kbeg[s + 1], K) : K;
+      int tap = 0, cbase = 0, dh = 0, dw = 0;
+      if (AMODE == AM_SHIFT3) {
+        tap = k0 / p.cin;
+        cbase = k0 - tap * p.cin;
+        dh = tap / 3 - 1;
+        dw = tap % 3 - 1;
+      }
+#pragma unroll
+      for (int i = 0; i < NPA; ++i) {
+        int idx = tid + i * GEMM_THREADS;
+        int r = idx >> 2, q = idx & 3;
+        int g = m0 + r;
+        int k = k0 + 4 * q;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        bool rowok = (idx < BM * 4) && (g < M);
+        long src = g;
+        if (AMODE == AM_SHIFT3) {
+          int hh = a_h[i] + dh, ww = a_w[i] + dw;
+          rowok = rowok && hh >= 0 && hh < p.H && ww >= 0 && ww < p.W;
+          src = (long)g + dh * p.W + dw;
+        }
+        if (rowok) {
+          const float* ptr = (AMODE == AM_SHIFT3) ? Ab + src * lda + cbase + 4 * q
+                                                  : Ab + src * lda + (k - kb);
+          if (VA) {
+            if (k < kend_s) v = ld4(ptr);
+          } else {
+            if (k + 0 < kend_s) v.x = ptr[0];
+            if (k + 1 < kend_s) v.y = ptr[1];
+            if (k + 2 < kend_s) v.z = ptr[2];
+            if (k + 3 < kend_s) v.w = ptr[3];
+          }
+          if (PRO_A != PRO_NONE) {
+            // prologue on the channel axis; padding zeros stay zero
+            if (k + 0 < kend_s) v.x = pro_apply<PRO_A>(v.x, p.a_scale[k + 0], p.a_shift[k + 0]);
+            if (k + 1 < kend_s) v.y = pro_apply<PRO_A>(v.y, p.a_scale[k + 1], p.a_shift[k + 1]);
+            if (k + 2 < kend_s) v.z = pro_apply<PRO_A>(v.z, p.a_scale[k + 2], p.a_shift[k + 2]);
+            if (k + 3 < kend_s) v.w = pro_apply<PRO_A>(v.w, p.a_scale[k + 3], p.a_shift[k + 3]);
+          }
+        }
+        ra[i] = v;
+      }
+    } else {  // AM_COL: A(m,k) = A[k*lda + m]
+      const float* Ab = p.A[0];
+      const int lda = p.lda[0];
+#pragma unroll
+      for (int i = 0; i < NPA; ++i) {
+        int idx = tid + i * GEMM_THREADS;
+        int kr = idx / (BM / 4), q = idx % (BM / 4);
+        int k = k0 + kr;
+        int m = m0 + 4 * q;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (idx < BM * 4 && k < kend) {
+          const float* ptr = Ab + (long)k * lda + m;
+          if (VA) {
+            if (m < M) v = ld4(ptr);
+          } else {
+            if (m + 0 < M) v.x = ptr[0];
+            if (m + 1 < M) v.y = ptr[1];
+            if (m + 2 < M) v.z = ptr[2];
+            if (m + 3 < M) v.w = ptr[3];
+          }
+        }
+        ra[i] = v;
+      }
+    }
+    // ------------------------------ B ---------------------------------------
+    if (BMODE == BM_NT) {
+#pragma unroll
+      for (int i = 0; i < NPB; ++i) {
+        int idx = tid + i * GEMM_THREADS;
+        int r = idx >> 2, q = idx & 3;
+        int n = n0 + r;
+        int k = k0 + 4 * q;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (idx < BN * 4 && n < N) {
+          const float* ptr = p.B + (long)n * p.ldb + k;
+          if (VB) {
+            if (k < kend) v = ld4(ptr);
+          } else {
+            if (k + 0 < kend) v.x = ptr[0];
+            if (k + 1 < kend) v.y = ptr[1];
+            if (k + 2 < kend) v.z = ptr[2];
+            if (k + 3 < kend) v.w = ptr[3];
+          }
+        }
+        rb[i] = v;
+      }
+    } else {  // BM_NN / BM_NN_SHIFT3: B(k,n) = B[row(k)*ldb + n]
+      int tap = 0, ncb = n0, dh = 0, dw = 0;
+      if (BMODE == BM_NN_SHIFT3) {
+        tap = n0 / p.cin;
+        ncb = n0 - tap * p.cin;
+        dh = tap / 3 - 1;
+        dw = tap % 3 - 1;
+      }
+#pragma unroll
+      for (int i = 0; i < NPB; ++i) {
+        int idx = tid + i * GEMM_THREADS;
+        int kr = idx / (BN / 4), q = idx % (BN / 4);
+        int k = k0 + kr;
+        int n = n0 + 4 * q;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        bool ok = idx < BN * 4 && k < kend;
+        long row = k;
+        if (BMODE == BM_NN_SHIFT3 && ok) {
+          uint32_t qq = fdiv((uint32_t)k, p.fW);
+          int ww = k - (int)qq * p.W;
+          int hh = (int)(qq - fdiv(qq, p.fH) * p.H);
+          ok = (hh + dh) >= 0 && (hh + dh) < p.H && (ww + dw) >= 0 && (ww + dw) < p.W;
+          row = (long)k + dh * p.W + dw;
+        }
+        if (ok) {
+          const float* ptr = p.B + row * p.ldb + (BMODE == BM_NN_SHIFT3 ? ncb + 4 * q : n);
+          if (VB) {
+            if (n < N) v = ld4(ptr);
+          } else {
+            if (n + 0 < N) v.x = ptr[0];
+            if (n + 1 < N) v.y = ptr[1];
+            if (n + 2 < N) v.z = ptr[2];
+            if (n + 3 < N) v.w = ptr[3];
+          }
+          if (PRO_B != PRO_NONE) {
+            if (n + 0 < N) v.x = pro_apply<PRO_B>(v.x, p.b_scale[n + 0], p.b_shift[n + 0]);
+            if (n + 1 < N) v.y = pro_apply<PRO_B>(v.y, p.b_scale[n + 1], p.b_shift[n + 1]);
+            if (n + 2 < N) v.z = pro_apply<PRO_B>(v.z, p.b_scale[n + 2], p.b_shift[n + 2]);
+            if (n + 3 < N) v.w = pro_apply<PRO_B>(v.w, p.b_scale[n + 3], p.b_shift[n + 3]);
+          }
+        }
+        rb[i] = v;
+      }
+    }
+  };
+
+  auto store_tiles = [&](int buf) {
+    float* as = As + buf * BK * SA;
+    float* bs = Bs + buf * BK * SB;
+    if (AMODE == AM_COL) {
+#pragma unroll
+      for (int i = 0; i < NPA; ++i) {
+        int idx = tid + i * GEMM_THREADS;
+        if (idx < BM * 4) {
+          int kr = idx / (BM / 4), q = idx % (BM / 4);
+          st4(as + kr * SA + 4 * q, ra[i]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NPA; ++i) {
+        int idx = tid + i * GEMM_THREADS;
+        if (idx < BM * 4) {
+          int r = idx >> 2, q = idx & 3;
+          as[(4 * q + 0) * SA + r] = ra[i].x;
+          as[(4 * q + 1) * SA + r] = ra[i].y;
+          as[(4 * q + 2) * SA + r] = ra[i].z;
+          as[(4 * q + 3) * SA + r] = ra[i].w;
+        }
+      }
+    }
+    if (BMODE == BM_NT) {
+#pragma unroll
+      for (int i = 0; i < NPB; ++i) {
+        int idx = tid + i * GEMM_THREADS;
+        if (idx < BN * 4) {
+          int r = idx >> 2, q = idx & 3;
+          bs[(4 * q + 0) * SB + r] = rb[i].x;
+          bs[(4 * q + 1) * SB + r] = rb[i].y;
+          bs[(4 * q + 2) * SB + r] = rb[i].z;
+          bs[(4 * q + 3) * SB + r] = rb[i].w;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NPB; ++i) {
+        int idx = tid + i * GEMM_THREADS;
+        if (idx < BN * 4) {
+          int kr = idx / (BN / 4), q = idx % (BN / 4);
+          st4(bs + kr * SB + 4 * q, rb[i]);
+        }
+      }
+    }
+  };
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int am_off = wm * TM * 32 + l31;
+  const int bn_off = wn * TN * 32 + l31;
+
+  if (nkt > 0) {
+    load_tiles(kstart);
+    store_tiles(0);
+    __syncthreads();
+    for (int kt = 0; kt < nkt; ++kt) {
+      const int buf = kt & 1;
+      if (kt + 1 < nkt) load_tiles(kstart + (kt + 1) * BK);
+      const float* as = As + buf * BK * SA;
+      const float* bs = Bs + buf * BK * SB;
+#pragma unroll
+      for (int kk = 0; kk < BK / 2; ++kk) {
+        float a[TM], b[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) a[i] = as[(2 * kk + lh) * SA + am_off + i * 32];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) b[j] = bs[(2 * kk + lh) * SB + bn_off + j * 32];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+      }
+      if (kt + 1 < nkt) store_tiles(buf ^ 1);
+      __syncthreads();
+    }
+  }
+
+  // ------------------------------- epilogue ---------------------------------
+  if (gridDim.z > 1) {
+    float* Cz = p.C + (size_t)blockIdx.z * p.zstride;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        int n = n0 + wn * TN * 32 + j * 32 + l31;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          if (m < M && n < N) Cz[(size_t)m * p.ldc + n] = acc[i][j][r];
+        }
+      }
+    return;
+  }
+
+  float s1[TN], s2[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
+
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      if (m >= M) continue;
+      long upoff[3] = {0, 0, 0};
+      if (p.nup > 0) {
+        uint32_t q = fdiv((uint32_t)m, p.fW);
+        int w = m - (int)q * p.W;
+        uint32_t b = fdiv(q, p.fH);
+        int h = (int)(q - b * p.H);
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+          if (u < p.nup) {
+            int lg = p.uplog[u];
+            int Hs = p.H >> lg, Ws = p.W >> lg;
+            upoff[u] = (((long)b * Hs + (h >> lg)) * Ws + (w >> lg)) * p.upld[u];
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        int n = n0 + wn * TN * 32 + j * 32 + l31;
+        if (n >= N) continue;
+        float v = acc[i][j][r];
+        if (p.bias) v += p.bias[n];
+#pragma unroll
+        for (int u = 0; u < 3; ++u)
+          if (u < p.nup) v += p.up[u][upoff[u] + n];
+        p.C[(size_t)m * p.ldc + n] = v;
+        s1[j] += v;
+        s2[j] += v * v;
+      }
+    }
+  }
+
+  if (p.stats) {
+    // reduce over the two half-waves, then across the WM waves sharing columns
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      s1[j] += __shfl_xor(s1[j], 32);
+      s2[j] += __shfl_xor(s2[j], 32);
+    }
+    __syncthreads();  // smem reuse
+    float* red = smem;  // [WM][2][BN]
+    if (lh == 0) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        int c = wn * TN * 32 + j * 32 + l31;
+        red[(wm * 2 + 0) * BN + c] = s1[j];
+        red[(wm * 2 + 1) * BN + c] = s2[j];
+      }
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += GEMM_THREADS) {
+      int n = n0 + c;
+      if (n < N) {
+        float a = 0.f, b = 0.f;
+#pragma unroll
+        for (int w = 0; w < WM; ++w) {
+          a += red[(w * 2 + 0) * BN + c];
+          b += red[(w * 2 + 1) * BN + c];
+        }
+        p.stats[((size_t)blockIdx.x * 2 + 0) * N + n] = a;
+        p.stats[((size_t)blockIdx.x * 2 + 1) * N + n] = b;
+      }
+    }
+  }
+}

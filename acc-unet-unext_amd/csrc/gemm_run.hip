@@ -1,0 +1,176 @@
+// Host driver for the fp32 MFMA GEMM: tile choice, split-K, deterministic
+// split-K reduction (fixed slab order, no float atomics).
+#include "gemm_dispatch.h"
+#include <string.h>
+
+__global__ void __launch_bounds__(256)
+splitk_reduce_kernel(const float* __restrict__ ws, float* __restrict__ C, int M, int N, int ldc,
+                     int S, size_t zstride) {
+  long total = (long)M * N;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    float acc = 0.f;
+    for (int z = 0; z < S; ++z) acc += ws[z * zstride + i];
+    int m = (int)(i / N), n = (int)(i - (long)m * N);
+    C[(size_t)m * ldc + n] = acc;
+  }
+}
+
+static gemm_kfn* table_for(int amode, int bmode, int pro_a, int pro_b) {
+  if (amode == AM_ROW && bmode == BM_NT && pro_b == PRO_NONE) {
+    if (pro_a == PRO_NONE) return g_gemm_row_nt_p0[0];
+    if (pro_a == PRO_AFFINE) return g_gemm_row_nt_p1[0];
+    if (pro_a == PRO_AFFINE_LRELU) return g_gemm_row_nt_p2[0];
+  }
+  if (amode == AM_SHIFT3 && bmode == BM_NT && pro_a == PRO_NONE && pro_b == PRO_NONE)
+    return g_gemm_sh3_nt[0];
+  if (amode == AM_ROW && bmode == BM_NN && pro_a == PRO_NONE && pro_b == PRO_NONE)
+    return g_gemm_row_nn[0];
+  if (amode == AM_COL && bmode == BM_NN && pro_a == PRO_NONE) {
+    if (pro_b == PRO_NONE) return g_gemm_col_nn_p0[0];
+    if (pro_b == PRO_AFFINE) return g_gemm_col_nn_p1[0];
+    if (pro_b == PRO_AFFINE_LRELU) return g_gemm_col_nn_p2[0];
+  }
+  if (amode == AM_COL && bmode == BM_NN_SHIFT3 && pro_a == PRO_NONE && pro_b == PRO_NONE)
+    return g_gemm_col_nnsh3[0];
+  return nullptr;
+}
+
+static gemm_kfn* table_v(int amode, int bmode, int pro_a, int pro_b, int v) {
+  // the tables are [2][TILE_COUNT]; table_for returns row 0
+  gemm_kfn* t0 = table_for(amode, bmode, pro_a, pro_b);
+  return t0 ? t0 + v * TILE_COUNT : nullptr;
+}
+
+static int pick_tile(int M, int N, int bmode, int cin) {
+  int t;
+  if (M <= 32) t = TILE_D;
+  else if (M <= 64) t = TILE_E;
+  else if (N <= 32) t = TILE_C;
+  else if (N <= 64) t = TILE_B;
+  else t = TILE_A;
+  if (bmode == BM_NN_SHIFT3) {
+    // the n-tile must not straddle two taps
+    if (cin % tile_bn(t) != 0) {
+      if (tile_bn(t) == 128) t = (t == TILE_D) ? TILE_E : TILE_B;
+    }
+    if (cin % tile_bn(t) != 0) t = TILE_C;
+  }
+  return t;
+}
+
+int gemm_run(GemmParams p, int amode, int bmode, int pro_a, int pro_b, bool allow_split,
+             float* ws, size_t ws_elems, hipStream_t stream) {
+  if (p.M <= 0 || p.N <= 0) return ACC_OK;
+  if (amode == AM_SHIFT3 && (p.cin % GEMM_BK) != 0) return ACC_EBADSHAPE;
+  if (bmode == BM_NN_SHIFT3 && (p.cin % 32) != 0) return ACC_EBADSHAPE;
+  // vectorised (float4) operand loads need every contiguous extent % 4 == 0
+  bool vec = true;
+  if (amode == AM_ROW) {
+    for (int s = 0; s < p.nsrc; ++s) {
+      int w = p.kbeg[s + 1] - p.kbeg[s];
+      if ((w & 3) || (p.lda[s] & 3) || ((uintptr_t)p.A[s] & 15)) vec = false;
+      if (s + 1 < p.nsrc && (w % GEMM_BK) != 0) return ACC_EBADSHAPE;  // source seams on k-tiles
+    }
+    if (p.K & 3) vec = false;
+  } else if (amode == AM_SHIFT3) {
+    if ((p.lda[0] & 3) || ((uintptr_t)p.A[0] & 15)) vec = false;
+  } else {  // AM_COL
+    if ((p.M & 3) || (p.lda[0] & 3) || ((uintptr_t)p.A[0] & 15)) vec = false;
+  }
+  if (bmode == BM_NT) {
+    if ((p.K & 3) || (p.ldb & 3) || ((uintptr_t)p.B & 15)) vec = false;
+  } else {
+    if ((p.N & 3) || (p.ldb & 3) || ((uintptr_t)p.B & 15)) vec = false;
+  }
+  if (amode == AM_ROW && p.nsrc == 1) { p.kbeg[0] = 0; p.kbeg[1] = p.K; }
+  gemm_kfn* tab = table_v(amode, bmode, pro_a, pro_b, vec ? 1 : 0);
+  if (!tab) return ACC_EBADARG;
+  int t = pick_tile(p.M, p.N, bmode, p.cin);
+  int BM = tile_bm(t), BN = tile_bn(t);
+  int gx = ceil_div(p.M, BM), gy = ceil_div(p.N, BN);
+
+  int S = 1;
+  p.kchunk = p.K;
+  p.zstride = 0;
+  float* Cfinal = p.C;
+  int ldc_final = p.ldc;
+  if (allow_split && ws != nullptr && p.bias == nullptr && p.nup == 0 && p.stats == nullptr) {
+    long tiles = (long)gx * gy;
+    long target = 1024;
+    long maxS = p.K / (GEMM_BK * 4);
+    long want = (target + tiles - 1) / tiles;
+    S = (int)(want < maxS ? want : maxS);
+    if (S < 1) S = 1;
+    while (S > 1 && (size_t)S * p.M * p.N > ws_elems) --S;
+    if (S > 1) {
+      int kt = ceil_div(p.K, S);
+      kt = ceil_div(kt, GEMM_BK) * GEMM_BK;
+      S = ceil_div(p.K, kt);
+      p.kchunk = kt;
+      p.zstride = (size_t)p.M * p.N;
+      p.C = ws;
+      p.ldc = p.N;
+    }
+  }
+  dim3 grid(gx, gy, S);
+  hipLaunchKernelGGL(tab[t], grid, dim3(GEMM_THREADS), 0, stream, p);
+  if (S > 1) {
+    long total = (long)p.M * p.N;
+    int blocks = (int)((total + 255) / 256);
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, stream, ws, Cfinal, p.M,
+                       p.N, ldc_final, S, p.zstride);
+  }
+  return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+}
+
+// ----------------------------------------------------------------------------
+// C ABI (include/accunet.h: AccGemmDesc / accunet_gemm)
+// ----------------------------------------------------------------------------
+#include "../../include/accunet.h"
+
+extern "C" int accunet_gemm(const AccGemmDesc* d, float* ws, size_t ws_elems, void* stream) {
+  if (!d) return ACC_EBADARG;
+  GemmParams p;
+  memset(&p, 0, sizeof(p));
+  p.M = d->M;
+  p.N = d->N;
+  p.K = d->K;
+  p.nsrc = d->nsrc < 1 ? 1 : d->nsrc;
+  if (p.nsrc > 4) return ACC_EBADARG;
+  for (int s = 0; s < 4; ++s) {
+    p.A[s] = d->a[s];
+    p.lda[s] = d->lda[s];
+  }
+  for (int s = 0; s < 5; ++s) p.kbeg[s] = d->kbeg[s];
+  p.a_scale = d->a_scale;
+  p.a_shift = d->a_shift;
+  p.B = d->b;
+  p.ldb = d->ldb;
+  p.b_scale = d->b_scale;
+  p.b_shift = d->b_shift;
+  p.H = d->H > 0 ? d->H : 1;
+  p.W = d->W > 0 ? d->W : 1;
+  p.fW = make_fastdiv((uint32_t)p.W);
+  p.fH = make_fastdiv((uint32_t)p.H);
+  p.cin = d->cin;
+  p.C = d->c;
+  p.ldc = d->ldc;
+  p.bias = d->bias;
+  p.nup = d->nup;
+  if (p.nup < 0 || p.nup > 3) return ACC_EBADARG;
+  for (int u = 0; u < 3; ++u) {
+    p.up[u] = d->up[u];
+    p.upld[u] = d->upld[u];
+    p.uplog[u] = d->uplog[u];
+  }
+  p.stats = d->stats;
+  return gemm_run(p, d->amode, d->bmode, d->pro_a, d->pro_b, d->allow_split != 0, ws, ws_elems,
+                  (hipStream_t)stream);
+}
+
+extern "C" int accunet_gemm_stats_rows(int M, int N, int amode, int bmode, int cin) {
+  int t = pick_tile(M, N, bmode, cin);
+  return ceil_div(M, tile_bm(t));
+}

@@ -1,0 +1,469 @@
+"""ORACLE — test infrastructure only, never on the product path.
+
+CPU restatement (plain PyTorch-CPU functional ops, fp32 or fp64) of the ACC-UNet
+hot path of prashantkul366/ACC-UNet-Unext, used by tests/, __graft_entry__.smoke()
+and bench.py's `cpu_baseline` leg as the CHECKER. The product path
+(acc-unet-unext_amd/accunet) never imports this module.
+
+Parity pinning: this restatement is checked against golden vectors produced by
+importing the reference modules in the build container
+(tests/golden/make_golden.py -> tests/golden/*.npz, test tests/test_oracle_golden.py).
+
+Every function cites the reference file:line whose behaviour it restates
+(paths relative to the reference repository root):
+  ACC_UNet/ACC_UNet.py        canonical model (inv_fctr 34 at cnv72, Sigmoid head)
+  Experiments/nets/ACC_UNet.py  script variant (inv_fctr 3 at cnv72, raw logits)
+  ACC_UNet/ACC_UNet_lite.py   Lite (MLFC reduced to its 4 SE layers)
+  ACC_UNet/ACC_UNet_w.py      W (learnable MLFC merge weight)
+  Experiments/utils.py        WeightedDiceBCE / dice metrics
+"""
+from __future__ import annotations
+
+import math
+from collections import OrderedDict
+from typing import Dict, List, Tuple
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+VARIANTS = ("canonical", "script", "lite", "w")
+SLOPE = 0.01  # torch.nn.LeakyReLU() default, used at ACC_UNet.py:30,73,170,250,312,416
+EPS = 1e-5
+MOMENTUM = 0.1
+
+# --------------------------------------------------------------------------
+# Parameter specification: names / shapes exactly as the reference state_dict.
+# --------------------------------------------------------------------------
+
+
+def _bn_spec(prefix: str, c: int, out: list):
+    # torch.nn.BatchNorm2d(c): weight, bias, running_mean, running_var, num_batches_tracked
+    out += [(prefix + ".weight", (c,)), (prefix + ".bias", (c,)),
+            (prefix + ".running_mean", (c,)), (prefix + ".running_var", (c,)),
+            (prefix + ".num_batches_tracked", ())]
+
+
+def _conv_spec(prefix, cout, cin, kh, kw, out, groups=1):
+    out += [(prefix + ".weight", (cout, cin // groups, kh, kw)), (prefix + ".bias", (cout,))]
+
+
+def _se_spec(prefix, c, out):
+    # ChannelSELayer ACC_UNet/ACC_UNet.py:14-34 (fc1, fc2, bn; r = 8)
+    cr = c // 8
+    out += [(prefix + ".fc1.weight", (cr, c)), (prefix + ".fc1.bias", (cr,)),
+            (prefix + ".fc2.weight", (c, cr)), (prefix + ".fc2.bias", (c,))]
+    _bn_spec(prefix + ".bn", c, out)
+
+
+def _hanc_block_spec(prefix, n_filts, out_ch, k, inv, out):
+    # HANCBlock.__init__ ACC_UNet/ACC_UNet.py:229-264 (registration order)
+    h = n_filts * inv
+    _conv_spec(prefix + ".conv1", h, n_filts, 1, 1, out)
+    _bn_spec(prefix + ".norm1", h, out)
+    _conv_spec(prefix + ".conv2", h, h, 3, 3, out, groups=h)
+    _bn_spec(prefix + ".norm2", h, out)
+    _conv_spec(prefix + ".hnc.cnv", n_filts, (2 * k - 1) * h, 1, 1, out)
+    _bn_spec(prefix + ".hnc.bn", n_filts, out)
+    _bn_spec(prefix + ".norm", n_filts, out)
+    _conv_spec(prefix + ".conv3", out_ch, n_filts, 1, 1, out)
+    _bn_spec(prefix + ".norm3", out_ch, out)
+    _se_spec(prefix + ".sqe", out_ch, out)
+
+
+def _respath_spec(prefix, c, n_lvl, out):
+    # ResPath.__init__ ACC_UNet/ACC_UNet.py:296-320: the (initially empty) ModuleLists
+    # convs/bns/sqes are registered before bn/sqe, so their entries come first
+    convs, bns, sqes = [], [], []
+    for i in range(n_lvl):
+        _conv_spec(f"{prefix}.convs.{i}", c, c, 3, 3, convs)
+        _bn_spec(f"{prefix}.bns.{i}", c, bns)
+        _se_spec(f"{prefix}.sqes.{i}", c, sqes)
+    out += convs + bns + sqes
+    _bn_spec(prefix + ".bn", c, out)
+    _bn_spec(prefix + ".sqe", c, out)
+
+
+def _cbn_spec(prefix, cin, cout, out):
+    # Conv2d_batchnorm ACC_UNet/ACC_UNet.py:151-179
+    _conv_spec(prefix + ".conv1", cout, cin, 1, 1, out)
+    _bn_spec(prefix + ".batchnorm", cout, out)
+    _se_spec(prefix + ".sqe", cout, out)
+
+
+def _mlfc_spec(prefix, f1, f2, f3, f4, out, weighted=False):
+    # MLFC.__init__ ACC_UNet/ACC_UNet.py:338-417 (ModuleList registration order)
+    fs = (f1, f2, f3, f4)
+    tot = sum(fs)
+    if weighted:  # ACC_UNet/ACC_UNet_w.py:354 registers W first
+        out.append((prefix + ".W", (1,)))
+    groups = {k: [] for k in ("blks", "mrg", "bns", "bns_mrg")}
+    # the ModuleLists are registered blks1..4, mrg1..4, bns1..4, bns_mrg1..4 (:363-381)
+    for lvl, f in enumerate(fs, 1):
+        _cbn_spec(f"{prefix}.cnv_blks{lvl}.0", tot, f, groups["blks"])
+    for lvl, f in enumerate(fs, 1):
+        _cbn_spec(f"{prefix}.cnv_mrg{lvl}.0", 2 * f, f, groups["mrg"])
+    for lvl, f in enumerate(fs, 1):
+        _bn_spec(f"{prefix}.bns{lvl}.0", f, groups["bns"])
+    for lvl, f in enumerate(fs, 1):
+        _bn_spec(f"{prefix}.bns_mrg{lvl}.0", f, groups["bns_mrg"])
+    out += groups["blks"] + groups["mrg"] + groups["bns"] + groups["bns_mrg"]
+    for lvl, f in enumerate(fs, 1):
+        _se_spec(f"{prefix}.sqe{lvl}", f, out)
+
+
+def cnv72_inv(variant: str) -> int:
+    # ACC_UNet/ACC_UNet.py:584 (34) vs Experiments/nets/ACC_UNet.py:584 (3)
+    return 3 if variant == "script" else 34
+
+
+def block_table(variant: str, n_channels: int, n_filts: int):
+    """(name, n_filts_in, out_ch, k, inv) for the 18 HANC blocks (ACC_UNet.py:554-592)."""
+    f = n_filts
+    return [
+        ("cnv11", n_channels, f, 3, 3), ("cnv12", f, f, 3, 3),
+        ("cnv21", f, 2 * f, 3, 3), ("cnv22", 2 * f, 2 * f, 3, 3),
+        ("cnv31", 2 * f, 4 * f, 3, 3), ("cnv32", 4 * f, 4 * f, 3, 3),
+        ("cnv41", 4 * f, 8 * f, 2, 3), ("cnv42", 8 * f, 8 * f, 2, 3),
+        ("cnv51", 8 * f, 16 * f, 1, 3), ("cnv52", 16 * f, 16 * f, 1, 3),
+        ("cnv61", 16 * f, 8 * f, 2, 3), ("cnv62", 8 * f, 8 * f, 2, 3),
+        ("cnv71", 8 * f, 4 * f, 3, 3), ("cnv72", 4 * f, 4 * f, 3, cnv72_inv(variant)),
+        ("cnv81", 4 * f, 2 * f, 3, 3), ("cnv82", 2 * f, 2 * f, 3, 3),
+        ("cnv91", 2 * f, f, 3, 3), ("cnv92", f, f, 3, 3),
+    ]
+
+
+def param_spec(variant: str, n_channels: int = 3, n_classes: int = 1, n_filts: int = 32
+               ) -> List[Tuple[str, tuple]]:
+    """Ordered state_dict (name, shape) list of the reference model."""
+    assert variant in VARIANTS
+    f = n_filts
+    out: list = []
+    blocks = {b[0]: b for b in block_table(variant, n_channels, n_filts)}
+
+    def hb(name):
+        _, nf, oc, k, inv = blocks[name]
+        _hanc_block_spec(name, nf, oc, k, inv, out)
+
+    # ACC_UNet.__init__ attribute order, ACC_UNet/ACC_UNet.py:549-599
+    for n in ("cnv11", "cnv12", "cnv21", "cnv22", "cnv31", "cnv32", "cnv41", "cnv42",
+              "cnv51", "cnv52"):
+        hb(n)
+    for i, (c, nl) in enumerate(((f, 4), (2 * f, 3), (4 * f, 2), (8 * f, 1)), 1):
+        _respath_spec(f"rspth{i}", c, nl, out)
+    for i in (1, 2, 3):
+        _mlfc_spec(f"mlfc{i}", f, 2 * f, 4 * f, 8 * f, out, weighted=(variant == "w"))
+    for up, cin, cout, blks in (("up6", 16 * f, 8 * f, ("cnv61", "cnv62")),
+                                ("up7", 8 * f, 4 * f, ("cnv71", "cnv72")),
+                                ("up8", 4 * f, 2 * f, ("cnv81", "cnv82")),
+                                ("up9", 2 * f, f, ("cnv91", "cnv92"))):
+        # ConvTranspose2d weight is (in, out, kh, kw)
+        out += [(up + ".weight", (cin, cout, 2, 2)), (up + ".bias", (cout,))]
+        for b in blks:
+            hb(b)
+    nout = n_classes if n_classes == 1 else n_classes + 1
+    _conv_spec("out", nout, f, 1, 1, out)
+    return out
+
+
+# --------------------------------------------------------------------------
+# Deterministic, version-independent parameter / input fill (counter hash).
+# --------------------------------------------------------------------------
+_M64 = (1 << 64) - 1
+
+
+def _fnv1a(s: str) -> int:
+    h = 0xCBF29CE484222325
+    for ch in s.encode():
+        h ^= ch
+        h = (h * 0x100000001B3) & _M64
+    return h
+
+
+def hash_uniform(key: str, n: int) -> np.ndarray:
+    """n values uniform in [-1, 1) from splitmix64(fnv1a(key) + i)."""
+    with np.errstate(over="ignore"):
+        z = (np.arange(n, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)
+             + np.uint64(_fnv1a(key)))
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    u = (z >> np.uint64(40)).astype(np.float64) / float(1 << 24)
+    return (2.0 * u - 1.0)
+
+
+def fan_in(shape) -> int:
+    if len(shape) <= 1:
+        return 1
+    return int(np.prod(shape[1:]))
+
+
+def det_state_dict(spec, seed: int = 0) -> "OrderedDict[str, torch.Tensor]":
+    """Deterministic, version-independent fill of every state_dict entry, in the
+    ranges PyTorch's default init uses (U(-1/sqrt(fan_in), 1/sqrt(fan_in)) for conv /
+    linear weights and biases); BatchNorm affine and running statistics are
+    perturbed away from (1, 0, 0, 1) so parity tests exercise them."""
+    names = {n for n, _ in spec}
+    shapes = dict(spec)
+    sd = OrderedDict()
+    for name, shape in spec:
+        prefix, leaf = name.rsplit(".", 1)
+        n = int(np.prod(shape)) if len(shape) else 1
+        if leaf == "num_batches_tracked":
+            sd[name] = torch.tensor(0, dtype=torch.long)
+            continue
+        u = torch.from_numpy(hash_uniform(f"{seed}:{name}", n).reshape(shape))
+        if leaf == "running_mean":
+            v = 0.1 * u
+        elif leaf == "running_var":
+            v = 1.0 + 0.5 * u.abs()
+        elif prefix + ".running_mean" in names:  # BatchNorm affine
+            v = (1.0 + 0.2 * u) if leaf == "weight" else 0.1 * u
+        elif leaf == "W":  # ACC_UNet_W merge weight (zeros in the reference init)
+            v = 0.3 + 0.2 * u
+        else:
+            wshape = shapes[prefix + ".weight"]
+            fi = fan_in(wshape)
+            if prefix.startswith("up"):  # ConvTranspose2d (in, out, kh, kw): fan_in = dim 1
+                fi = wshape[1] * wshape[2] * wshape[3]
+            v = u / math.sqrt(max(fi, 1))
+        sd[name] = v.float()
+    return sd
+
+
+def det_input(shape, key="x") -> torch.Tensor:
+    n = int(np.prod(shape))
+    # approximately N(0,1): sum of 4 uniforms scaled
+    u = sum(hash_uniform(f"{key}:{j}", n) for j in range(4)) * math.sqrt(3.0 / 4.0)
+    return torch.from_numpy(u.reshape(shape)).float()
+
+
+def det_mask(shape, key="mask", p=0.5) -> torch.Tensor:
+    n = int(np.prod(shape))
+    u = 0.5 * (hash_uniform(key, n) + 1.0)
+    return torch.from_numpy((u < p).astype(np.float32).reshape(shape))
+
+
+# --------------------------------------------------------------------------
+# Functional forward (NCHW, CPU). State dict entries for running stats are
+# updated in place in training mode, exactly like the reference modules.
+# --------------------------------------------------------------------------
+def lrelu(x):
+    return F.leaky_relu(x, SLOPE)
+
+
+def bn(x, sd, p, training):
+    # torch.nn.BatchNorm2d semantics (momentum 0.1, eps 1e-5, unbiased running var)
+    if training:
+        sd[p + ".num_batches_tracked"] += 1
+    return F.batch_norm(x, sd[p + ".running_mean"], sd[p + ".running_var"],
+                        sd[p + ".weight"], sd[p + ".bias"], training, MOMENTUM, EPS)
+
+
+def conv(x, sd, p, padding=0, groups=1):
+    return F.conv2d(x, sd[p + ".weight"], sd[p + ".bias"], padding=padding, groups=groups)
+
+
+def se(x, sd, p, training):
+    """ChannelSELayer.forward, ACC_UNet/ACC_UNet.py:37-49."""
+    b, c = x.shape[:2]
+    s = F.adaptive_avg_pool2d(x, 1).view(b, c)
+    s = lrelu(F.linear(s, sd[p + ".fc1.weight"], sd[p + ".fc1.bias"]))
+    s = torch.sigmoid(F.linear(s, sd[p + ".fc2.weight"], sd[p + ".fc2.bias"]))
+    y = x * s.view(b, c, 1, 1)
+    return lrelu(bn(y, sd, p + ".bn", training))
+
+
+def _up(x, f):
+    return F.interpolate(x, scale_factor=f, mode="nearest")
+
+
+def hanc_layer(x, sd, p, k, training):
+    """HANCLayer.forward, ACC_UNet/ACC_UNet.py:77-142: neighbourhood pyramid
+    concatenated along H then viewed as channels (interleave c*(2k-1)+j)."""
+    b, c, h, w = x.shape
+    parts = [x]
+    if k >= 2:
+        parts.append(_up(F.avg_pool2d(x, 2), 2))
+    if k >= 3:
+        parts.append(_up(F.avg_pool2d(x, 4), 4))
+    if k >= 2:
+        parts.append(_up(F.max_pool2d(x, 2), 2))
+    if k >= 3:
+        parts.append(_up(F.max_pool2d(x, 4), 4))
+    z = torch.cat(parts, dim=2).view(b, c * (2 * k - 1), h, w)
+    return lrelu(bn(conv(z, sd, p + ".cnv"), sd, p + ".bn", training))
+
+
+def hanc_block(x, sd, p, k, training):
+    """HANCBlock.forward, ACC_UNet/ACC_UNet.py:267-286."""
+    inp = x
+    x = lrelu(bn(conv(x, sd, p + ".conv1"), sd, p + ".norm1", training))
+    c = x.shape[1]
+    x = lrelu(bn(conv(x, sd, p + ".conv2", padding=1, groups=c), sd, p + ".norm2", training))
+    x = hanc_layer(x, sd, p + ".hnc", k, training)
+    x = bn(x + inp, sd, p + ".norm", training)
+    x = lrelu(bn(conv(x, sd, p + ".conv3"), sd, p + ".norm3", training))
+    return se(x, sd, p + ".sqe", training)
+
+
+def respath(x, sd, p, n_lvl, training):
+    """ResPath.forward, ACC_UNet/ACC_UNet.py:323-328."""
+    for i in range(n_lvl):
+        y = lrelu(bn(conv(x, sd, f"{p}.convs.{i}", padding=1), sd, f"{p}.bns.{i}", training))
+        x = x + se(y, sd, f"{p}.sqes.{i}", training)
+    return bn(lrelu(bn(x, sd, p + ".bn", training)), sd, p + ".sqe", training)
+
+
+def conv_bn_se(x, sd, p, training):
+    """Conv2d_batchnorm.forward, ACC_UNet/ACC_UNet.py:182-186."""
+    x = bn(conv(x, sd, p + ".conv1"), sd, p + ".batchnorm", training)
+    return se(lrelu(x), sd, p + ".sqe", training)
+
+
+def mlfc(xs, sd, p, training, variant):
+    """MLFC.forward, ACC_UNet/ACC_UNet.py:420-527 (W variant: ACC_UNet_w.py:497-522;
+    Lite: ACC_UNet_lite.py:422-429)."""
+    x1, x2, x3, x4 = xs
+    if variant == "lite":
+        return tuple(se(x, sd, f"{p}.sqe{i}", training) for i, x in enumerate(xs, 1))
+    down = lambda t: F.avg_pool2d(t, 2)
+    up = lambda t: _up(t, 2)
+    b = x1.shape[0]
+    cats = [
+        [x1, up(x2), up(up(x3)), up(up(up(x4)))],
+        [down(x1), x2, up(x3), up(up(x4))],
+        [down(down(x1)), down(x2), x3, up(x4)],
+        [down(down(down(x1))), down(down(x2)), down(x3), x4],
+    ]
+    xc = []
+    for lvl in range(4):
+        z = conv_bn_se(torch.cat(cats[lvl], dim=1), sd, f"{p}.cnv_blks{lvl + 1}.0", training)
+        xc.append(lrelu(bn(z, sd, f"{p}.bns{lvl + 1}.0", training)))
+    outs = []
+    for lvl, xl in enumerate(xs):
+        c, h, w = xl.shape[1:]
+        merged = torch.cat([xc[lvl], xl], dim=2).view(b, 2 * c, h, w)
+        m = conv_bn_se(merged, sd, f"{p}.cnv_mrg{lvl + 1}.0", training)
+        if variant == "w":
+            wgt = sd[p + ".W"]
+            m = m * wgt + xl * (1 - wgt)
+        else:
+            m = m + xl
+        outs.append(lrelu(bn(m, sd, f"{p}.bns_mrg{lvl + 1}.0", training)))
+    return tuple(se(o, sd, f"{p}.sqe{i}", training) for i, o in enumerate(outs, 1))
+
+
+def convT(x, sd, p):
+    return F.conv_transpose2d(x, sd[p + ".weight"], sd[p + ".bias"], stride=2)
+
+
+def forward(sd, x, variant="canonical", training=True, n_classes=1):
+    """ACC_UNet.forward, ACC_UNet/ACC_UNet.py:601-659 (script variant returns logits,
+    Experiments/nets/ACC_UNet.py:654-655)."""
+    t = training
+    x2 = hanc_block(hanc_block(x, sd, "cnv11", 3, t), sd, "cnv12", 3, t)
+    x3 = hanc_block(hanc_block(F.max_pool2d(x2, 2), sd, "cnv21", 3, t), sd, "cnv22", 3, t)
+    x4 = hanc_block(hanc_block(F.max_pool2d(x3, 2), sd, "cnv31", 3, t), sd, "cnv32", 3, t)
+    x5 = hanc_block(hanc_block(F.max_pool2d(x4, 2), sd, "cnv41", 2, t), sd, "cnv42", 2, t)
+    x6 = hanc_block(hanc_block(F.max_pool2d(x5, 2), sd, "cnv51", 1, t), sd, "cnv52", 1, t)
+    x2 = respath(x2, sd, "rspth1", 4, t)
+    x3 = respath(x3, sd, "rspth2", 3, t)
+    x4 = respath(x4, sd, "rspth3", 2, t)
+    x5 = respath(x5, sd, "rspth4", 1, t)
+    xs = (x2, x3, x4, x5)
+    for i in (1, 2, 3):
+        xs = mlfc(xs, sd, f"mlfc{i}", t, variant)
+    x2, x3, x4, x5 = xs
+    x7 = hanc_block(torch.cat([convT(x6, sd, "up6"), x5], 1), sd, "cnv61", 2, t)
+    x7 = hanc_block(x7, sd, "cnv62", 2, t)
+    x8 = hanc_block(torch.cat([convT(x7, sd, "up7"), x4], 1), sd, "cnv71", 3, t)
+    x8 = hanc_block(x8, sd, "cnv72", 3, t)
+    x9 = hanc_block(torch.cat([convT(x8, sd, "up8"), x3], 1), sd, "cnv81", 3, t)
+    x9 = hanc_block(x9, sd, "cnv82", 3, t)
+    x10 = hanc_block(torch.cat([convT(x9, sd, "up9"), x2], 1), sd, "cnv91", 3, t)
+    x10 = hanc_block(x10, sd, "cnv92", 3, t)
+    logits = conv(x10, sd, "out")
+    if variant != "script" and n_classes == 1:
+        return torch.sigmoid(logits)
+    return logits
+
+
+# --------------------------------------------------------------------------
+# Loss and metrics, Experiments/utils.py
+# --------------------------------------------------------------------------
+def weighted_bce(logit, truth, weights=(0.5, 0.5)):
+    """WeightedBCE.forward, Experiments/utils.py:28-74 (logits version)."""
+    logit = logit.float()
+    truth = truth.float().view_as(logit)
+    if truth.max() > 1.0:
+        truth = (truth > 0).float()
+    loss = F.binary_cross_entropy_with_logits(logit, truth, reduction="none")
+    pos = (truth > 0.5).float()
+    neg = 1.0 - pos
+    pw = pos.sum().clamp(min=1.0)
+    nw = neg.sum().clamp(min=1.0)
+    return (weights[0] * pos * loss / pw + weights[1] * neg * loss / nw).sum()
+
+
+def weighted_dice(logit, truth, weights=(0.5, 0.5), smooth=1e-5):
+    """WeightedDiceLoss.forward, Experiments/utils.py:115-138."""
+    b = len(logit)
+    p = torch.sigmoid(logit.reshape(b, -1))
+    t = truth.reshape(b, -1)
+    w = truth.detach().reshape(b, -1) * (weights[1] - weights[0]) + weights[0]
+    p = w * p
+    t = w * t
+    inter = (p * t).sum(-1)
+    union = (p * p).sum(-1) + (t * t).sum(-1)
+    return (1 - (2 * inter + smooth) / (union + smooth)).mean()
+
+
+def dice_bce_loss(logit, truth, dice_weight=0.5, bce_weight=0.5):
+    """WeightedDiceBCE(0.5, 0.5).forward, Experiments/utils.py:160-171 (train_model.py:719)."""
+    return dice_weight * weighted_dice(logit, truth) + bce_weight * weighted_bce(logit, truth)
+
+
+def show_dice(inputs, targets):
+    """WeightedDiceBCE._show_dice, Experiments/utils.py:149-158 (sigmoid applied, then
+    sigmoid again inside WeightedDiceLoss; mutates targets)."""
+    hard = (torch.sigmoid(inputs) >= 0.5).float()
+    targets[targets > 0] = 1
+    targets[targets <= 0] = 0
+    return 1.0 - weighted_dice(hard, targets)
+
+
+def dice_on_batch(masks, pred):
+    """dice_on_batch, Experiments/utils.py:503-519 (numpy hard Dice, smooth 1e-5)."""
+    dices = []
+    for i in range(pred.shape[0]):
+        p = torch.sigmoid(pred[i][0]).detach().cpu().numpy()
+        m = masks[i].detach().cpu().numpy().copy()
+        p[p >= 0.5] = 1
+        p[p < 0.5] = 0
+        m[m > 0] = 1
+        m[m <= 0] = 0
+        yt, yp = m.flatten(), p.flatten()
+        inter = np.sum(yt * yp)
+        dices.append((2.0 * inter + 1e-5) / (np.sum(yt) + np.sum(yp) + 1e-5))
+    return float(np.mean(dices))
+
+
+def iou_on_batch(masks, pred):
+    """iou_on_batch, Experiments/utils.py:478-494 (jaccard of hard masks)."""
+    ious = []
+    for i in range(pred.shape[0]):
+        p = torch.sigmoid(pred[i][0]).detach().cpu().numpy()
+        m = masks[i].detach().cpu().numpy().copy()
+        p = (p >= 0.5).astype(np.float64).flatten()
+        m = (m > 0).astype(np.float64).flatten()
+        inter = np.sum(p * m)
+        union = np.sum(np.maximum(p, m))
+        ious.append(inter / union if union > 0 else 0.0)
+    return float(np.mean(ious))
+
+
+def cosine_warm_restarts_lr(base_lr, eta_min, T_0, epoch):
+    """CosineAnnealingWarmRestarts.get_lr with T_mult=1, Experiments/utils.py:668-784."""
+    t_cur = epoch % T_0
+    return eta_min + (base_lr - eta_min) * (1 + math.cos(math.pi * t_cur / T_0)) / 2

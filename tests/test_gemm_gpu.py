@@ -1,0 +1,132 @@
+"""GEMM engine parity (fp32 MFMA) against float64 torch references."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from accunet import kern  # noqa: E402
+from accunet import _lib  # noqa: E402
+
+DEV = "cuda"
+
+
+def rel(a, b):
+    return ((a.double() - b.double()).abs().max() / (b.double().abs().max() + 1e-30)).item()
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 128, 96), (1000, 64, 45), (777, 32, 18),
+                                   (2048, 9, 3), (300, 200, 256), (64, 512, 1536)])
+def test_row_nt_bias_stats(M, N, K):
+    torch.manual_seed(0)
+    A = torch.randn(M, K, device=DEV)
+    Wt = torch.randn(N, K, device=DEV)
+    b = torch.randn(N, device=DEV)
+    C = torch.empty(M, N, device=DEV)
+    rows = kern.gemm_stats_rows(M, N)
+    st = torch.zeros(rows, 2, N, device=DEV)
+    kern.gemm(M, N, K, a=[A], lda=[K], b=Wt, ldb=K, c=C, ldc=N, bias=b, stats=st)
+    ref = A.double() @ Wt.double().t() + b.double()
+    assert rel(C, ref) < 1e-5
+    s = st.double().sum(0)
+    assert torch.allclose(s[0], ref.sum(0), rtol=1e-4, atol=1e-2)
+    assert torch.allclose(s[1], (ref * ref).sum(0), rtol=1e-4, atol=1e-1)
+
+
+def test_row_nt_prologue_multisrc_ups():
+    torch.manual_seed(1)
+    B, H, W = 2, 16, 32
+    P = B * H * W
+    K1, K2 = 32, 16
+    N = 48
+    A1 = torch.randn(P, K1, device=DEV)
+    A2 = torch.randn(P, 40, device=DEV)[:, 8:24]  # column slice with ld=40
+    Wt = torch.randn(N, K1 + K2, device=DEV)
+    g2 = torch.randn(B * (H // 2) * (W // 2), N, device=DEV)
+    g4 = torch.randn(B * (H // 4) * (W // 4), 64, device=DEV)
+    C = torch.empty(P, N, device=DEV)
+    A2full = A2.contiguous()
+    base = torch.randn(P, 40, device=DEV)
+    base[:, 8:24] = A2full
+    kern.gemm(P, N, K1 + K2, a=[A1, base], lda=[K1, 40], a_offsets=[0, 8], kbeg=[0, K1, K1 + K2],
+              b=Wt, ldb=K1 + K2, c=C, ldc=N, H=H, W=W,
+              ups=[(g2, N, 1, 0), (g4, 64, 2, 16)])
+    X = torch.cat([A1, A2full], 1).double()
+    ref = X @ Wt.double().t()
+    up2 = g2.view(B, H // 2, W // 2, N).repeat_interleave(2, 1).repeat_interleave(2, 2).reshape(P, N)
+    up4 = g4[:, 16:16 + N].reshape(B, H // 4, W // 4, N).repeat_interleave(4, 1).repeat_interleave(4, 2).reshape(P, N)
+    ref = ref + up2.double() + up4.double()
+    assert rel(C, ref) < 1e-5
+
+    # prologue (affine + lrelu) on A
+    sc = torch.rand(K1, device=DEV) + 0.5
+    sh = torch.randn(K1, device=DEV)
+    C2 = torch.empty(P, N, device=DEV)
+    kern.gemm(P, N, K1, a=[A1], lda=[K1], b=Wt, ldb=K1 + K2, c=C2, ldc=N,
+              pro_a=_lib.PRO_AFFINE_LRELU, a_scale=sc, a_shift=sh)
+    Xp = F.leaky_relu(A1.double() * sc.double() + sh.double(), 0.01)
+    assert rel(C2, Xp @ Wt[:, :K1].double().t()) < 1e-5
+
+
+@pytest.mark.parametrize("P,N,K", [(5000, 96, 32), (4096, 3, 32), (1024, 1536, 512)])
+def test_row_nn_dgrad(P, N, K):
+    # dX[P,K] = dZ[P,N] @ W[N,K]  -> GEMM M=P, N=K, K=N with B = W as [K][N] (NN)
+    torch.manual_seed(2)
+    dZ = torch.randn(P, N, device=DEV)
+    Wt = torch.randn(N, K, device=DEV)
+    dX = torch.empty(P, K, device=DEV)
+    kern.gemm(P, K, N, a=[dZ], lda=[N], b=Wt, ldb=K, bmode=_lib.BMODE_NN, c=dX, ldc=K)
+    assert rel(dX, dZ.double() @ Wt.double()) < 1e-5
+
+
+@pytest.mark.parametrize("P,Co,Ci,pro", [(65536, 96, 32, 0), (20000, 32, 96, 2), (4096, 512, 1536, 1),
+                                         (3000, 9, 3, 0)])
+def test_col_nn_wgrad_splitk(P, Co, Ci, pro):
+    torch.manual_seed(3)
+    dZ = torch.randn(P, Co, device=DEV)
+    X = torch.randn(P, Ci, device=DEV)
+    sc = torch.rand(Ci, device=DEV) + 0.5
+    sh = torch.randn(Ci, device=DEV)
+    dW = torch.empty(Co, Ci, device=DEV)
+    kern.gemm(Co, Ci, P, a=[dZ], lda=[Co], amode=_lib.AMODE_COL, b=X, ldb=Ci,
+              bmode=_lib.BMODE_NN, c=dW, ldc=Ci, pro_b=pro,
+              b_scale=sc if pro else None, b_shift=sh if pro else None, allow_split=True)
+    Xd = X.double()
+    if pro == 1:
+        Xd = Xd * sc.double() + sh.double()
+    elif pro == 2:
+        Xd = F.leaky_relu(Xd * sc.double() + sh.double(), 0.01)
+    ref = dZ.double().t() @ Xd
+    assert rel(dW, ref) < 1e-5
+
+
+@pytest.mark.parametrize("B,H,W,Ci,Co", [(2, 32, 32, 32, 32), (1, 16, 64, 64, 64), (2, 8, 8, 256, 256)])
+def test_conv3x3_fwd_dgrad_wgrad(B, H, W, Ci, Co):
+    torch.manual_seed(4)
+    x = torch.randn(B, Ci, H, W, device=DEV, dtype=torch.float64, requires_grad=True)
+    w = torch.randn(Co, Ci, 3, 3, device=DEV, dtype=torch.float64, requires_grad=True)
+    bias = torch.randn(Co, device=DEV, dtype=torch.float64)
+    y = F.conv2d(x, w, bias, padding=1)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    P = B * H * W
+    xn = x.detach().permute(0, 2, 3, 1).reshape(P, Ci).float().contiguous()
+    wr = w.detach().permute(0, 2, 3, 1).reshape(Co, 9 * Ci).float().contiguous()  # [co][tap][ci]
+    out = torch.empty(P, Co, device=DEV)
+    kern.gemm(P, Co, 9 * Ci, a=[xn], lda=[Ci], amode=_lib.AMODE_SHIFT3, b=wr, ldb=9 * Ci,
+              c=out, ldc=Co, bias=bias.float(), H=H, W=W, cin=Ci)
+    ref = y.detach().permute(0, 2, 3, 1).reshape(P, Co)
+    assert rel(out, ref) < 1e-5
+    # dgrad: conv with flipped, transposed weights W'[ci][tap'][co] = W[co][ci][8-tap']
+    gyn = gy.permute(0, 2, 3, 1).reshape(P, Co).float().contiguous()
+    wf = w.detach().flip(2, 3).permute(1, 2, 3, 0).reshape(Ci, 9 * Co).float().contiguous()
+    dx = torch.empty(P, Ci, device=DEV)
+    kern.gemm(P, Ci, 9 * Co, a=[gyn], lda=[Co], amode=_lib.AMODE_SHIFT3, b=wf, ldb=9 * Co,
+              c=dx, ldc=Ci, H=H, W=W, cin=Co)
+    assert rel(dx, x.grad.permute(0, 2, 3, 1).reshape(P, Ci)) < 1e-5
+    # wgrad: dW[co][tap][ci] = sum_p gy[p,co] x[shift_tap(p), ci]
+    dw = torch.empty(Co, 9 * Ci, device=DEV)
+    kern.gemm(Co, 9 * Ci, P, a=[gyn], lda=[Co], amode=_lib.AMODE_COL, b=xn, ldb=Ci,
+              bmode=_lib.BMODE_NN_SHIFT3, c=dw, ldc=9 * Ci, H=H, W=W, cin=Ci, allow_split=True)
+    refw = w.grad.permute(0, 2, 3, 1).reshape(Co, 9 * Ci)
+    assert rel(dw, refw) < 1e-5
