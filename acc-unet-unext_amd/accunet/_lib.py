@@ -62,7 +62,39 @@ _SIGS = {
     "accunet_bn_bwd": [P, P, P, P, I, I, L, I, P, I, P, P, P, IP, P, S, P],
     "accunet_colsum": [P, L, I, P, P, S, P],
     "accunet_reduce_stats": [P, I, I, P, P, P],
+    "accunet_dw3x3_rows": [I, I, I, I],
+    "accunet_dw3x3_fwd": [P, P, P, P, P, I, I, P, P, I, I, I, I, P],
+    "accunet_dw3x3_wgrad_ws": [I, I, I, I],
+    "accunet_dw3x3_wgrad": [P, P, P, P, I, P, P, I, I, I, I, P, S, P],
+    "accunet_hanc_pyramid_fwd": [P, P, P, I, I, I, I, I, I, P, P, P],
+    "accunet_hanc_pyramid_bwd": [P, P, P, I, I, I, I, I, I, P, P, P, P, P, P],
+    "accunet_pool2_fwd": [P, P, I, I, I, I, I, P],
+    "accunet_pool2_bwd": [P, P, P, P, I, I, I, I, I, I, P],
+    "accunet_upsample_bwd": [P, I, I, P, I, I, I, I, I, I, I, P],
+    "accunet_slice_copy": [P, I, I, P, I, I, L, I, I, P],
+    "accunet_pixel_shuffle2": [P, P, P, I, I, I, I, I, P],
+    "accunet_permute4": [P, P, IP, POINTER(c_longlong), IP, I, P],
+    "accunet_group_relayout": [P, P, I, I, I, IP, I, P],
+    "accunet_se_save_elems": [I, I, I],
+    "accunet_se_ws_elems": [I, I, I, I],
+    "accunet_se_fwd": [P, P, P, I, I, I, I, I, P, P, P, P, P, P, P, P, P, F, F, I, P, P, P, P, S, P],
+    "accunet_se_stats_rows": [I, I, I],
+    "accunet_se_bwd": [P, P, P, P, I, I, I, I, I, P, P, P, I, P, P, P, P, P, P, P, P, P, S, P],
+    "accunet_head_fwd": [P, P, P, I, P, L, I, P],
+    "accunet_head_ws_elems": [L, I],
+    "accunet_head_bwd": [P, P, P, P, I, P, P, P, L, I, P, S, P],
+    "accunet_loss_ws_elems": [I],
+    "accunet_loss_fwd": [P, P, I, L, F, F, P, P, S, P],
+    "accunet_loss_bwd": [P, P, I, L, F, F, P, P, P, P],
+    "accunet_adam_chunk_elems": [],
+    "accunet_adam_step": [P, P, P, I, F, F, F, F, F, I, P],
+    "accunet_dotdiff": [P, P, P, L, P, I, P, P],
+    "accunet_wmerge_fwd": [P, P, P, P, L, I, P, P],
+    "accunet_wmerge_bwd": [P, P, P, P, L, P],
 }
+# entry points returning a size/count rather than a status
+_SIZE_FNS = {"accunet_dw3x3_wgrad_ws", "accunet_se_save_elems", "accunet_se_ws_elems",
+             "accunet_head_ws_elems", "accunet_loss_ws_elems"}
 
 _lib = None
 
@@ -83,7 +115,7 @@ def load():
     for name, args in _SIGS.items():
         fn = getattr(lib, name)
         fn.argtypes = args
-        fn.restype = c_int
+        fn.restype = c_size_t if name in _SIZE_FNS else c_int
     _lib = lib
     return lib
 
@@ -100,6 +132,16 @@ def check(status: int, what: str):
         raise AccError(f"{what} failed: {_ERRS.get(status, status)}")
 
 
+_DEBUG = os.environ.get("ACCUNET_DEBUG", "0") not in ("", "0")
+
+
 def call(name: str, *args):
     lib = load()
+    if _DEBUG:  # serialise + trace every entry point (debug builds of a run only)
+        import sys
+        import torch
+        sys.stderr.write(f"[accunet] {name}\n")
+        sys.stderr.flush()
     check(getattr(lib, name)(*args), name)
+    if _DEBUG:
+        torch.cuda.synchronize()

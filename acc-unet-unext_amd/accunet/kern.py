@@ -155,3 +155,156 @@ def reduce_stats(part, R: int, C: int, out2C):
     ws = workspace(partial_ws_elems(R, 2 * C), part.device)
     call("accunet_reduce_stats", _p(part), int(R), int(C), _p(out2C), _p(ws), _stream())
     return ws
+
+
+def _lib_raw():
+    return _lib.load()
+
+
+def dw3x3_rows(B, H, W, C) -> int:
+    return int(_lib_raw().accunet_dw3x3_rows(B, H, W, C))
+
+
+def dw3x3_fwd(x, wt, bias, sc, sh, act, flip, z, stats, B, H, W, C):
+    call("accunet_dw3x3_fwd", _p(x), _p(wt), _p(bias), _p(sc), _p(sh), int(act), int(flip), _p(z),
+         _p(stats), B, H, W, C, _stream())
+
+
+def dw3x3_wgrad(x, dz, sc, sh, act, dw, db, B, H, W, C):
+    n = int(_lib_raw().accunet_dw3x3_wgrad_ws(B, H, W, C))
+    ws = workspace(n, x.device)
+    call("accunet_dw3x3_wgrad", _p(x), _p(dz), _p(sc), _p(sh), int(act), _p(dw), _p(db), B, H, W,
+         C, _p(ws), n, _stream())
+    return ws
+
+
+def hanc_pyramid_fwd(x, sc, sh, act, B, H, W, C, k, p2, p4):
+    call("accunet_hanc_pyramid_fwd", _p(x), _p(sc), _p(sh), int(act), B, H, W, C, k, _p(p2),
+         _p(p4), _stream())
+
+
+def hanc_pyramid_bwd(x, sc, sh, act, B, H, W, C, k, p2, p4, dp2, dp4, da):
+    call("accunet_hanc_pyramid_bwd", _p(x), _p(sc), _p(sh), int(act), B, H, W, C, k, _p(p2),
+         _p(p4), _p(dp2), _p(dp4), _p(da), _stream())
+
+
+POOL_MAX, POOL_AVG = 0, 1
+
+
+def pool2_fwd(x, y, B, H, W, C, mode):
+    call("accunet_pool2_fwd", _p(x), _p(y), B, H, W, C, mode, _stream())
+
+
+def pool2_bwd(x, y, dy, dx, B, H, W, C, mode, accumulate=False):
+    call("accunet_pool2_bwd", _p(x), _p(y), _p(dy), _p(dx), B, H, W, C, mode,
+         1 if accumulate else 0, _stream())
+
+
+def upsample_bwd(inp, ld_in, in_off, out, ld_out, B, H, W, C, f, accumulate=False):
+    call("accunet_upsample_bwd", _p(inp), int(ld_in), int(in_off), _p(out), int(ld_out), B, H, W,
+         C, int(f), 1 if accumulate else 0, _stream())
+
+
+def slice_copy(src, ld_src, src_off, dst, ld_dst, dst_off, P, C, accumulate=False):
+    call("accunet_slice_copy", _p(src), int(ld_src), int(src_off), _p(dst), int(ld_dst),
+         int(dst_off), int(P), int(C), 1 if accumulate else 0, _stream())
+
+
+def pixel_shuffle2(t, bias, y, B, Hi, Wi, Cout, inverse=False):
+    call("accunet_pixel_shuffle2", _p(t), _p(bias), _p(y), B, Hi, Wi, Cout, 1 if inverse else 0,
+         _stream())
+
+
+def permute4(inp, out, dims, strides, flips=None, accumulate=False):
+    d = (ctypes.c_int * 4)(*[int(v) for v in dims])
+    s = (ctypes.c_longlong * 4)(*[int(v) for v in strides])
+    f = (ctypes.c_int * 4)(*[int(v) for v in (flips or (0, 0, 0, 0))])
+    call("accunet_permute4", _p(inp), _p(out), d, s, f, 1 if accumulate else 0, _stream())
+
+
+def group_relayout(inp, out, N, C, J, order, inverse=False):
+    o = (ctypes.c_int * 8)(*([int(v) for v in order] + [0] * (8 - len(order))))
+    call("accunet_group_relayout", _p(inp), _p(out), int(N), int(C), int(J), o,
+         1 if inverse else 0, _stream())
+
+
+def se_save_elems(B, C, Cr) -> int:
+    return int(_lib_raw().accunet_se_save_elems(B, C, Cr))
+
+
+def se_ws_elems(B, HW, C, Cr) -> int:
+    return int(_lib_raw().accunet_se_ws_elems(B, HW, C, Cr))
+
+
+def se_stats_rows(B, HW, C) -> int:
+    return int(_lib_raw().accunet_se_stats_rows(B, HW, C))
+
+
+def se_fwd(z, sc, sh, act, B, HW, C, Cr, w1, b1, w2, b2, gamma, beta, rmean, rvar, nbt, momentum,
+           eps, training, out, save, ostats=None):
+    n = se_ws_elems(B, HW, C, Cr)
+    ws = workspace(n, z.device)
+    call("accunet_se_fwd", _p(z), _p(sc), _p(sh), int(act), B, HW, C, Cr, _p(w1), _p(b1), _p(w2),
+         _p(b2), _p(gamma), _p(beta), _p(rmean), _p(rvar), _p(nbt), float(momentum), float(eps),
+         1 if training else 0, _p(out), _p(save), _p(ostats), _p(ws), n, _stream())
+    return ws
+
+
+def se_bwd(z, dout, sc, sh, act, B, HW, C, Cr, w1, w2, gamma, training, save, da, dw1, db1, dw2,
+           db2, dgamma, dbeta):
+    n = se_ws_elems(B, HW, C, Cr)
+    ws = workspace(n, z.device)
+    call("accunet_se_bwd", _p(z), _p(dout), _p(sc), _p(sh), int(act), B, HW, C, Cr, _p(w1),
+         _p(w2), _p(gamma), 1 if training else 0, _p(save), _p(da), _p(dw1), _p(db1), _p(dw2),
+         _p(db2), _p(dgamma), _p(dbeta), _p(ws), n, _stream())
+    return ws
+
+
+def head_fwd(x, w, b, sigm, y, P, C):
+    call("accunet_head_fwd", _p(x), _p(w), _p(b), 1 if sigm else 0, _p(y), int(P), int(C),
+         _stream())
+
+
+def head_bwd(x, w, y, dy, sigm, dx, dw, db, P, C):
+    n = int(_lib_raw().accunet_head_ws_elems(int(P), int(C)))
+    ws = workspace(n, x.device)
+    call("accunet_head_bwd", _p(x), _p(w), _p(y), _p(dy), 1 if sigm else 0, _p(dx), _p(dw),
+         _p(db), int(P), int(C), _p(ws), n, _stream())
+    return ws
+
+
+def loss_fwd(x, t, B, N, dice_w, bce_w, res):
+    n = int(_lib_raw().accunet_loss_ws_elems(int(B)))
+    ws = workspace(n, x.device)
+    call("accunet_loss_fwd", _p(x), _p(t), int(B), int(N), float(dice_w), float(bce_w), _p(res),
+         _p(ws), n, _stream())
+    return ws
+
+
+def loss_bwd(x, t, B, N, dice_w, bce_w, res, gout, dx):
+    call("accunet_loss_bwd", _p(x), _p(t), int(B), int(N), float(dice_w), float(bce_w), _p(res),
+         _p(gout), _p(dx), _stream())
+
+
+def adam_chunk_elems() -> int:
+    return int(_lib_raw().accunet_adam_chunk_elems())
+
+
+def adam_step(table, chunk_t, chunk_s, nchunks, lr, b1, b2, eps, wd, step):
+    call("accunet_adam_step", _p(table), _p(chunk_t), _p(chunk_s), int(nchunks), float(lr),
+         float(b1), float(b2), float(eps), float(wd), int(step), _stream())
+
+
+def dotdiff(g, a, b, n, out, accumulate=False):
+    ws = workspace(1024, g.device)
+    call("accunet_dotdiff", _p(g), _p(a), _p(b), int(n), _p(out), 1 if accumulate else 0, _p(ws),
+         _stream())
+    return ws
+
+
+def wmerge_fwd(a, b, w, y, P, C, stats=None):
+    call("accunet_wmerge_fwd", _p(a), _p(b), _p(w), _p(y), int(P), int(C), _p(stats), _stream())
+
+
+def wmerge_bwd(g, w, da, db, n):
+    call("accunet_wmerge_bwd", _p(g), _p(w), _p(da), _p(db), int(n), _stream())

@@ -1,0 +1,958 @@
+"""Fused ACC-UNet operators as autograd Functions over the HIP C ABI.
+
+Activations are NHWC fp32 tensors [B, H, W, C]. A BatchNorm2d(+LeakyReLU) whose
+statistics are known but which has not been applied yet travels as a `Pending`
+(tensor z + the BatchNorm module + the partial statistics its producer's epilogue
+wrote); the op that consumes it finalises the statistics (running-stat update
+happens there, exactly once per forward, as in torch) and applies the
+normalisation in registers while loading. The reference applies every
+BatchNorm as a separate ATen pass (ACC_UNet/ACC_UNet.py, e.g. :269-284).
+
+Every forward / backward below calls only `kern.*` (libaccunet_hip.so); torch is
+used for allocation, views and autograd bookkeeping.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import torch
+
+from . import kern
+from . import profile as _prof
+from ._lib import (ACT_LRELU, ACT_NONE, AMODE_COL, AMODE_SHIFT3, BMODE_NN, BMODE_NN_SHIFT3,
+                   PRO_AFFINE, PRO_AFFINE_LRELU, PRO_NONE)
+
+__all__ = ["Pending", "pw_conv", "dw_conv", "hanc_layer", "bn_act_add", "se", "conv3x3",
+           "conv_transpose2x2", "pool2", "cat_channels", "head", "wmerge", "group_relayout",
+           "to_nhwc", "weighted_dice_bce"]
+
+
+def _empty(shape, like):
+    return torch.empty(shape, dtype=torch.float32, device=like.device)
+
+
+def _flat_off(t: torch.Tensor, off: int) -> torch.Tensor:
+    """1-D view of t starting `off` elements in (pointer offset for kernels)."""
+    f = t.view(-1)
+    return f.narrow(0, off, f.numel() - off)
+
+
+# --------------------------------------------------------------------------
+# Pending BatchNorm(+act)
+# --------------------------------------------------------------------------
+class Pending:
+    """value = act(bn(z)); bn None -> value = z (already materialised)."""
+
+    __slots__ = ("z", "bn", "act", "part", "rows")
+
+    def __init__(self, z: torch.Tensor, bn=None, act: int = ACT_NONE, part=None, rows: int = 0):
+        self.z = z
+        self.bn = bn
+        self.act = act
+        self.part = part
+        self.rows = rows
+
+    @property
+    def shape(self):
+        return self.z.shape
+
+
+def as_pending(x) -> Pending:
+    return x if isinstance(x, Pending) else Pending(x)
+
+
+@dataclass
+class _Pro:
+    """Finalised BatchNorm prologue for one consumer (non-tensor context)."""
+    active: bool
+    st: Optional[torch.Tensor] = None   # [4, C] mean, rstd, scale, shift
+    act: int = ACT_NONE
+    training: bool = False
+
+
+def _finalize(p: Pending) -> _Pro:
+    if p.bn is None:
+        return _Pro(False)
+    bn = p.bn
+    z = p.z
+    C = z.shape[-1]
+    P = z.numel() // C
+    training = bn.training or not bn.track_running_stats
+    st = _empty((4, C), z)
+    if training and p.part is None:
+        raise RuntimeError("pending BatchNorm in training mode without producer statistics")
+    mom = bn.momentum if bn.momentum is not None else 0.1
+    kern.bn_finalize(p.part, p.rows, C, float(P), bn.weight, bn.bias,
+                     bn.running_mean if bn.track_running_stats else None,
+                     bn.running_var if bn.track_running_stats else None,
+                     bn.num_batches_tracked if (training and bn.track_running_stats) else None,
+                     mom, bn.eps, training, st)
+    return _Pro(True, st, p.act, training)
+
+
+def _pro_mode(pro: _Pro) -> int:
+    if not pro.active:
+        return PRO_NONE
+    return PRO_AFFINE_LRELU if pro.act == ACT_LRELU else PRO_AFFINE
+
+
+def _pro_bwd(pro: _Pro, z, gamma, dA, need_z=True, need_params=True):
+    """Backward of a BatchNorm(+act) prologue: returns (dz, dgamma, dbeta)."""
+    if not pro.active:
+        return dA, None, None
+    C = z.shape[-1]
+    P = z.numel() // C
+    dz = torch.empty_like(z)
+    dg = _empty((C,), z) if need_params else None
+    db = _empty((C,), z) if need_params else None
+    kern.bn_bwd(z, dA, pro.st, gamma, pro.act, pro.training, P, C, dz, False, dg, db)
+    return dz, dg, db
+
+
+def _bn_params(p: Pending):
+    if p.bn is None:
+        return None, None
+    return p.bn.weight, p.bn.bias
+
+
+def _want_stats(consumer_bn) -> bool:
+    return consumer_bn is not None and (consumer_bn.training or not consumer_bn.track_running_stats)
+
+
+# --------------------------------------------------------------------------
+# 1x1 convolution (multi-source, optional BN prologue on source 0, nearest-up adds)
+# --------------------------------------------------------------------------
+@dataclass
+class _PWCfg:
+    nsrc: int
+    src_ch: List[int]
+    pro: _Pro
+    w_off: int
+    w_ld: int
+    N: int
+    B: int
+    H: int
+    W: int
+    ups: List[tuple] = field(default_factory=list)  # (log2f, col_off, ld)
+    want_stats: bool = False
+    has_bias: bool = True
+
+
+class _PWConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, cfg: _PWCfg, weight, bias, pro_g, pro_b, *tens):
+        srcs = tens[:cfg.nsrc]
+        ups = tens[cfg.nsrc:]
+        B, H, W, N = cfg.B, cfg.H, cfg.W, cfg.N
+        P = B * H * W
+        kbeg = [0]
+        for c in cfg.src_ch:
+            kbeg.append(kbeg[-1] + c)
+        K = kbeg[-1]
+        Z = _empty((B, H, W, N), weight)
+        stats = None
+        rows = 0
+        if cfg.want_stats:
+            rows = kern.gemm_stats_rows(P, N)
+            stats = _empty((rows, 2, N), weight)
+        pro = cfg.pro
+        kern.gemm(P, N, K, a=list(srcs), lda=cfg.src_ch, kbeg=kbeg, b=weight, ldb=cfg.w_ld,
+                  b_offset=cfg.w_off, c=Z, ldc=N, bias=bias if cfg.has_bias else None,
+                  pro_a=_pro_mode(pro), a_scale=pro.st[2] if pro.active else None,
+                  a_shift=pro.st[3] if pro.active else None, H=H, W=W,
+                  ups=[(u, ld, lg, off) for u, (lg, off, ld) in zip(ups, cfg.ups)], stats=stats)
+        ctx.cfg = cfg
+        ctx.kbeg = kbeg
+        ctx.save_for_backward(weight, pro_g, *srcs)
+        ctx.up_shapes = [u.shape for u in ups]
+        if stats is None:
+            stats = _empty((0,), weight)
+        ctx.mark_non_differentiable(stats)
+        ctx.rows = rows
+        return Z, stats
+
+    @staticmethod
+    def backward(ctx, dZ, _dstats):
+        cfg = ctx.cfg
+        weight, pro_g, *srcs = ctx.saved_tensors
+        dZ = dZ.contiguous()
+        B, H, W, N = cfg.B, cfg.H, cfg.W, cfg.N
+        P = B * H * W
+        kbeg = ctx.kbeg
+        nig = ctx.needs_input_grad  # (cfg, weight, bias, pro_g, pro_b, *srcs, *ups)
+        pro = cfg.pro
+        keep = []
+        d_srcs = []
+        dpro_g = dpro_b = None
+        for s, (x, C) in enumerate(zip(srcs, cfg.src_ch)):
+            need = nig[5 + s] or (s == 0 and pro.active and (nig[3] or nig[4]))
+            if not need:
+                d_srcs.append(None)
+                continue
+            dA = _empty((B, H, W, C), dZ)
+            keep.append(kern.gemm(P, C, N, a=[dZ], lda=[N], b=weight, ldb=cfg.w_ld,
+                                  bmode=BMODE_NN, b_offset=cfg.w_off + kbeg[s], c=dA, ldc=C))
+            if s == 0 and pro.active:
+                dA, dpro_g, dpro_b = _pro_bwd(pro, x, pro_g, dA)
+            d_srcs.append(dA)
+        dW = None
+        if nig[1]:
+            full = (cfg.w_off == 0 and kbeg[-1] == cfg.w_ld)
+            dW = torch.zeros_like(weight) if not full else torch.empty_like(weight)
+            for s, (x, C) in enumerate(zip(srcs, cfg.src_ch)):
+                use_pro = (s == 0 and pro.active)
+                keep.append(kern.gemm(N, C, P, a=[dZ], lda=[N], amode=AMODE_COL, b=x, ldb=C,
+                                      bmode=BMODE_NN, c=dW, ldc=cfg.w_ld,
+                                      c_offset=cfg.w_off + kbeg[s],
+                                      pro_b=_pro_mode(pro) if use_pro else PRO_NONE,
+                                      b_scale=pro.st[2] if use_pro else None,
+                                      b_shift=pro.st[3] if use_pro else None, allow_split=True))
+        dbias = None
+        if cfg.has_bias and nig[2]:
+            dbias = _empty((N,), dZ)
+            keep.append(kern.colsum(dZ, P, N, dbias))
+        d_ups = []
+        for i, ((lg, off, ld), shp) in enumerate(zip(cfg.ups, ctx.up_shapes)):
+            if not nig[5 + cfg.nsrc + i]:
+                d_ups.append(None)
+                continue
+            dG = torch.zeros(shp, dtype=torch.float32, device=dZ.device) if ld != N else \
+                torch.empty(shp, dtype=torch.float32, device=dZ.device)
+            kern.upsample_bwd(dZ, N, 0, _flat_off(dG, off), ld, B, H, W, N, 1 << lg)
+            d_ups.append(dG)
+        return (None, dW, dbias, dpro_g, dpro_b, *d_srcs, *d_ups)
+
+
+def pw_conv(srcs: Sequence, weight, bias, *, w_off: int = 0, ups: Sequence = (),
+            consumer_bn=None, want_stats: Optional[bool] = None):
+    """Z = sum_s src_s @ W[:, w_off + kbeg_s : ...]^T (+bias) (+ nearest-up adds).
+
+    srcs[0] may be a Pending (its BatchNorm(+act) is applied in the GEMM prologue).
+    ups: sequence of (G tensor [B, H>>lg, W>>lg, ld], log2 factor, column offset).
+    Returns Pending(Z, consumer_bn, ...) carrying Z's partial statistics.
+    """
+    srcs = [as_pending(s) for s in srcs]
+    for s in srcs[1:]:
+        if s.bn is not None:
+            raise ValueError("only the first source may carry a pending BatchNorm")
+    pro = _finalize(srcs[0])
+    z0 = srcs[0].z
+    B, H, W = z0.shape[:3]
+    w2 = weight.reshape(weight.shape[0], -1)
+    N, w_ld = w2.shape
+    if want_stats is None:
+        want_stats = _want_stats(consumer_bn)
+    cfg = _PWCfg(nsrc=len(srcs), src_ch=[s.z.shape[-1] for s in srcs], pro=pro, w_off=w_off,
+                 w_ld=w_ld, N=N, B=B, H=H, W=W,
+                 ups=[(lg, off, g.shape[-1]) for g, lg, off in ups], want_stats=want_stats,
+                 has_bias=bias is not None)
+    pg, pb = _bn_params(srcs[0])
+    Z, stats = _PWConvFn.apply(cfg, w2, bias, pg, pb, *[s.z for s in srcs],
+                               *[g for g, _, _ in ups])
+    return Pending(Z, consumer_bn, ACT_LRELU, stats if want_stats else None,
+                   kern.gemm_stats_rows(B * H * W, N) if want_stats else 0)
+
+
+# --------------------------------------------------------------------------
+# depthwise 3x3 (HANCBlock.conv2) with the norm1+LReLU prologue
+# --------------------------------------------------------------------------
+@dataclass
+class _DWCfg:
+    pro: _Pro
+    B: int
+    H: int
+    W: int
+    C: int
+    want_stats: bool
+
+
+class _DWConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, cfg: _DWCfg, z, pro_g, pro_b, weight, bias):
+        B, H, W, C = cfg.B, cfg.H, cfg.W, cfg.C
+        Z = _empty((B, H, W, C), z)
+        stats = None
+        if cfg.want_stats:
+            stats = _empty((kern.dw3x3_rows(B, H, W, C), 2, C), z)
+        pro = cfg.pro
+        with _prof.region(f"dw3x3_fwd B{B} {H}x{W} C{C}", kernel="dw3x3_fwd_kernel",
+                          shape=f"{B}x{H}x{W}x{C}", bytes_alg=2.0 * 4 * B * H * W * C):
+            kern.dw3x3_fwd(z, weight, bias, pro.st[2] if pro.active else None,
+                           pro.st[3] if pro.active else None, pro.act, 0, Z, stats, B, H, W, C)
+        ctx.cfg = cfg
+        ctx.save_for_backward(z, pro_g, weight)
+        if stats is None:
+            stats = _empty((0,), z)
+        ctx.mark_non_differentiable(stats)
+        return Z, stats
+
+    @staticmethod
+    def backward(ctx, dZ, _ds):
+        cfg = ctx.cfg
+        z, pro_g, weight = ctx.saved_tensors
+        dZ = dZ.contiguous()
+        B, H, W, C = cfg.B, cfg.H, cfg.W, cfg.C
+        pro = cfg.pro
+        dA = torch.empty_like(z)
+        kern.dw3x3_fwd(dZ, weight, None, None, None, ACT_NONE, 1, dA, None, B, H, W, C)
+        dW = torch.empty_like(weight)
+        db = _empty((C,), z)
+        ws = kern.dw3x3_wgrad(z, dZ, pro.st[2] if pro.active else None,
+                              pro.st[3] if pro.active else None, pro.act, dW, db, B, H, W, C)
+        dz, dg, dbeta = _pro_bwd(pro, z, pro_g, dA)
+        del ws
+        return None, dz, dg, dbeta, dW, db
+
+
+def dw_conv(x, weight, bias, *, consumer_bn=None):
+    x = as_pending(x)
+    pro = _finalize(x)
+    B, H, W, C = x.z.shape
+    want = _want_stats(consumer_bn)
+    cfg = _DWCfg(pro, B, H, W, C, want)
+    pg, pb = _bn_params(x)
+    Z, stats = _DWConvFn.apply(cfg, x.z, pg, pb, weight.reshape(C, 9), bias)
+    return Pending(Z, consumer_bn, ACT_LRELU, stats if want else None,
+                   kern.dw3x3_rows(B, H, W, C) if want else 0)
+
+
+# --------------------------------------------------------------------------
+# HANCLayer (ACC_UNet/ACC_UNet.py:77-142), restructured exactly:
+#   cnv(view(cat_H[a, up2 avg2 a, up4 avg4 a, up2 max2 a, up4 max4 a]))
+#   = W0 a + up2(W_{avg2,max2} [avg2 a | max2 a]) + up4(W_{avg4,max4} [avg4 a | max4 a]) + b
+# --------------------------------------------------------------------------
+# branch j of input channel c sits at column c*(2k-1)+j (j: 0 x, 1 avg2, 2 avg4, 3 max2,
+# 4 max4 for k = 3; 0 x, 1 avg2, 2 max2 for k = 2). Relayout order groups the columns as
+# [x | avg2 max2 | avg4 max4] so each GEMM reads one contiguous column block.
+_HANC_ORDER = {1: [0], 2: [0, 1, 2], 3: [0, 1, 3, 2, 4]}
+
+
+@dataclass
+class _HancCfg:
+    pro: _Pro
+    k: int
+    B: int
+    H: int
+    W: int
+    C: int
+    N: int
+    want_stats: bool
+
+
+class _HancLayerFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, cfg: _HancCfg, z, pro_g, pro_b, weight, bias):
+        B, H, W, C, N, k = cfg.B, cfg.H, cfg.W, cfg.C, cfg.N, cfg.k
+        J = 2 * k - 1
+        P = B * H * W
+        pro = cfg.pro
+        sc = pro.st[2] if pro.active else None
+        sh = pro.st[3] if pro.active else None
+        Wp = _empty((N, J * C), z)
+        kern.group_relayout(weight, Wp, N, C, J, _HANC_ORDER[k])
+        ups = []
+        p2 = p4 = g2 = g4 = None
+        if k >= 2:
+            p2 = _empty((B, H // 2, W // 2, 2 * C), z)
+            p4 = _empty((B, H // 4, W // 4, 2 * C), z) if k == 3 else None
+            kern.hanc_pyramid_fwd(z, sc, sh, pro.act, B, H, W, C, k, p2, p4)
+            g2 = _empty((B, H // 2, W // 2, N), z)
+            kern.gemm(P // 4, N, 2 * C, a=[p2], lda=[2 * C], b=Wp, ldb=J * C, b_offset=C, c=g2,
+                      ldc=N)
+            ups.append((g2, N, 1, 0))
+            if k == 3:
+                g4 = _empty((B, H // 4, W // 4, N), z)
+                kern.gemm(P // 16, N, 2 * C, a=[p4], lda=[2 * C], b=Wp, ldb=J * C,
+                          b_offset=3 * C, c=g4, ldc=N)
+                ups.append((g4, N, 2, 0))
+        Z = _empty((B, H, W, N), z)
+        stats = None
+        if cfg.want_stats:
+            stats = _empty((kern.gemm_stats_rows(P, N), 2, N), z)
+        with _prof.region(f"hanc_gemm P{P} N{N} K{C}", kernel="gemm_f32_kernel (HANC x-branch)",
+                          shape=f"M{P} N{N} K{C}", flops=2.0 * P * N * C):
+            kern.gemm(P, N, C, a=[z], lda=[C], b=Wp, ldb=J * C, c=Z, ldc=N, bias=bias,
+                      pro_a=_pro_mode(pro), a_scale=sc, a_shift=sh, H=H, W=W, ups=ups,
+                      stats=stats)
+        ctx.cfg = cfg
+        saved = [z, pro_g, Wp]
+        ctx.has_p = k >= 2
+        if k >= 2:
+            saved.append(p2)
+            if k == 3:
+                saved.append(p4)
+        ctx.save_for_backward(*saved)
+        if stats is None:
+            stats = _empty((0,), z)
+        ctx.mark_non_differentiable(stats)
+        return Z, stats
+
+    @staticmethod
+    def backward(ctx, dZ, _ds):
+        cfg = ctx.cfg
+        B, H, W, C, N, k = cfg.B, cfg.H, cfg.W, cfg.C, cfg.N, cfg.k
+        J = 2 * k - 1
+        P = B * H * W
+        saved = ctx.saved_tensors
+        z, pro_g, Wp = saved[:3]
+        p2 = saved[3] if k >= 2 else None
+        p4 = saved[4] if k == 3 else None
+        dZ = dZ.contiguous()
+        pro = cfg.pro
+        sc = pro.st[2] if pro.active else None
+        sh = pro.st[3] if pro.active else None
+        keep = []
+        dWp = _empty((N, J * C), z)
+        # x branch
+        dA = torch.empty_like(z)
+        keep.append(kern.gemm(P, C, N, a=[dZ], lda=[N], b=Wp, ldb=J * C, bmode=BMODE_NN, c=dA,
+                              ldc=C))
+        keep.append(kern.gemm(N, C, P, a=[dZ], lda=[N], amode=AMODE_COL, b=z, ldb=C,
+                              bmode=BMODE_NN, c=dWp, ldc=J * C, c_offset=0,
+                              pro_b=_pro_mode(pro), b_scale=sc, b_shift=sh, allow_split=True))
+        if k >= 2:
+            dG2 = _empty((B, H // 2, W // 2, N), z)
+            kern.upsample_bwd(dZ, N, 0, dG2, N, B, H, W, N, 2)
+            dP2 = _empty(p2.shape, z)
+            keep.append(kern.gemm(P // 4, 2 * C, N, a=[dG2], lda=[N], b=Wp, ldb=J * C,
+                                  bmode=BMODE_NN, b_offset=C, c=dP2, ldc=2 * C))
+            keep.append(kern.gemm(N, 2 * C, P // 4, a=[dG2], lda=[N], amode=AMODE_COL, b=p2,
+                                  ldb=2 * C, bmode=BMODE_NN, c=dWp, ldc=J * C, c_offset=C,
+                                  allow_split=True))
+            dP4 = None
+            if k == 3:
+                dG4 = _empty((B, H // 4, W // 4, N), z)
+                kern.upsample_bwd(dZ, N, 0, dG4, N, B, H, W, N, 4)
+                dP4 = _empty(p4.shape, z)
+                keep.append(kern.gemm(P // 16, 2 * C, N, a=[dG4], lda=[N], b=Wp, ldb=J * C,
+                                      bmode=BMODE_NN, b_offset=3 * C, c=dP4, ldc=2 * C))
+                keep.append(kern.gemm(N, 2 * C, P // 16, a=[dG4], lda=[N], amode=AMODE_COL,
+                                      b=p4, ldb=2 * C, bmode=BMODE_NN, c=dWp, ldc=J * C,
+                                      c_offset=3 * C, allow_split=True))
+            kern.hanc_pyramid_bwd(z, sc, sh, pro.act, B, H, W, C, k, p2, p4, dP2, dP4, dA)
+        dW = _empty((N, J * C), z)
+        kern.group_relayout(dWp, dW, N, C, J, _HANC_ORDER[k], inverse=True)
+        db = _empty((N,), z)
+        keep.append(kern.colsum(dZ, P, N, db))
+        dz, dg, dbeta = _pro_bwd(pro, z, pro_g, dA)
+        return None, dz, dg, dbeta, dW, db
+
+
+def hanc_layer(x, weight, bias, k: int, *, consumer_bn=None):
+    x = as_pending(x)
+    pro = _finalize(x)
+    B, H, W, C = x.z.shape
+    w2 = weight.reshape(weight.shape[0], -1)
+    N = w2.shape[0]
+    assert w2.shape[1] == (2 * k - 1) * C
+    if k >= 2 and (H % (2 if k == 2 else 4) or W % (2 if k == 2 else 4)):
+        raise ValueError("HANCLayer: spatial size must be divisible by the pooling factor")
+    want = _want_stats(consumer_bn)
+    cfg = _HancCfg(pro, k, B, H, W, C, N, want)
+    pg, pb = _bn_params(x)
+    Z, stats = _HancLayerFn.apply(cfg, x.z, pg, pb, w2, bias)
+    return Pending(Z, consumer_bn, ACT_LRELU, stats if want else None,
+                   kern.gemm_stats_rows(B * H * W, N) if want else 0)
+
+
+# --------------------------------------------------------------------------
+# y = act(bn(z)) (+ res), materialised, optional statistics of y
+# --------------------------------------------------------------------------
+@dataclass
+class _BAACfg:
+    pro: _Pro
+    has_res: bool
+    want_stats: bool
+
+
+class _BnActAddFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, cfg: _BAACfg, z, pro_g, pro_b, res):
+        C = z.shape[-1]
+        P = z.numel() // C
+        y = torch.empty_like(z)
+        stats = _empty((kern.stream_rows(P, C), 2, C), z) if cfg.want_stats else None
+        pro = cfg.pro
+        kern.affine_act(z, pro.st[2] if pro.active else None, pro.st[3] if pro.active else None,
+                        pro.act if pro.active else ACT_NONE, res if cfg.has_res else None, y, P,
+                        C, stats)
+        ctx.cfg = cfg
+        ctx.save_for_backward(z, pro_g)
+        if stats is None:
+            stats = _empty((0,), z)
+        ctx.mark_non_differentiable(stats)
+        return y, stats
+
+    @staticmethod
+    def backward(ctx, dy, _ds):
+        cfg = ctx.cfg
+        z, pro_g = ctx.saved_tensors
+        dy = dy.contiguous()
+        dz, dg, db = _pro_bwd(cfg.pro, z, pro_g, dy)
+        dres = dy if cfg.has_res else None
+        return None, dz, dg, db, dres
+
+
+def bn_act_add(x, res=None, *, consumer_bn=None, act_after=ACT_LRELU, want_stats=None):
+    """Materialise act(bn(x)) (+res); returns Pending(y, consumer_bn) with y's stats."""
+    x = as_pending(x)
+    pro = _finalize(x)
+    if want_stats is None:
+        want_stats = _want_stats(consumer_bn)
+    cfg = _BAACfg(pro, res is not None, want_stats)
+    pg, pb = _bn_params(x)
+    y, stats = _BnActAddFn.apply(cfg, x.z, pg, pb, res)
+    C = y.shape[-1]
+    return Pending(y, consumer_bn, act_after, stats if want_stats else None,
+                   kern.stream_rows(y.numel() // C, C) if want_stats else 0)
+
+
+# --------------------------------------------------------------------------
+# ChannelSELayer (ACC_UNet/ACC_UNet.py:37-49) fused with its preceding BN(+act)
+# --------------------------------------------------------------------------
+@dataclass
+class _SECfg:
+    pro: _Pro
+    bn: object  # the SE's own BatchNorm2d (running stats updated in forward)
+    training: bool
+    B: int
+    HW: int
+    C: int
+    Cr: int
+    want_stats: bool = False
+
+
+class _SEFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, cfg: _SECfg, z, pro_g, pro_b, w1, b1, w2, b2, g, b):
+        B, HW, C, Cr = cfg.B, cfg.HW, cfg.C, cfg.Cr
+        pro = cfg.pro
+        out = torch.empty_like(z)
+        ostats = _empty((kern.se_stats_rows(B, HW, C), 2, C), z) if cfg.want_stats else None
+        save = _empty((kern.se_save_elems(B, C, Cr),), z)
+        bn = cfg.bn
+        mom = bn.momentum if bn.momentum is not None else 0.1
+        tr = cfg.training
+        with _prof.region(f"se_fwd B{B} HW{HW} C{C}", kernel="se_reduce+se_mid+se_apply",
+                          shape=f"{B}x{HW}x{C}", bytes_alg=2.0 * 4 * B * HW * C):
+            kern.se_fwd(z, pro.st[2] if pro.active else None,
+                        pro.st[3] if pro.active else None, pro.act, B, HW, C, Cr, w1, b1, w2,
+                        b2, g, b, bn.running_mean if bn.track_running_stats else None,
+                        bn.running_var if bn.track_running_stats else None,
+                        bn.num_batches_tracked if (tr and bn.track_running_stats) else None,
+                        mom, bn.eps, tr, out, save, ostats)
+        ctx.cfg = cfg
+        ctx.save_for_backward(z, pro_g, w1, w2, g, save)
+        if ostats is None:
+            ostats = _empty((0,), z)
+        ctx.mark_non_differentiable(ostats)
+        return out, ostats
+
+    @staticmethod
+    def backward(ctx, dout, _dst):
+        cfg = ctx.cfg
+        z, pro_g, w1, w2, g, save = ctx.saved_tensors
+        dout = dout.contiguous()
+        B, HW, C, Cr = cfg.B, cfg.HW, cfg.C, cfg.Cr
+        pro = cfg.pro
+        da = torch.empty_like(z)
+        dw1 = torch.empty_like(w1)
+        db1 = _empty((Cr,), z)
+        dw2 = torch.empty_like(w2)
+        db2 = _empty((C,), z)
+        dg = _empty((C,), z)
+        dbeta = _empty((C,), z)
+        kern.se_bwd(z, dout, pro.st[2] if pro.active else None,
+                    pro.st[3] if pro.active else None, pro.act, B, HW, C, Cr, w1, w2, g,
+                    cfg.training, save, da, dw1, db1, dw2, db2, dg, dbeta)
+        dz, dpg, dpb = _pro_bwd(pro, z, pro_g, da)
+        return None, dz, dpg, dpb, dw1, db1, dw2, db2, dg, dbeta
+
+
+def se(x, mod, *, consumer_bn=None):
+    """ChannelSELayer `mod` (fc1, fc2, bn) applied to x (Pending or tensor).
+
+    Returns the materialised output tensor, or (when consumer_bn is given) a
+    Pending(out, consumer_bn) carrying the output's statistics."""
+    x = as_pending(x)
+    pro = _finalize(x)
+    B, H, W, C = x.z.shape
+    Cr = mod.fc1.weight.shape[0]
+    bn = mod.bn
+    tr = bn.training or not bn.track_running_stats
+    want = _want_stats(consumer_bn)
+    cfg = _SECfg(pro, bn, tr, B, H * W, C, Cr, want)
+    pg, pb = _bn_params(x)
+    out, ostats = _SEFn.apply(cfg, x.z, pg, pb, mod.fc1.weight, mod.fc1.bias, mod.fc2.weight,
+                              mod.fc2.bias, bn.weight, bn.bias)
+    if consumer_bn is None:
+        return out
+    return Pending(out, consumer_bn, ACT_LRELU, ostats if want else None,
+                   kern.se_stats_rows(B, H * W, C) if want else 0)
+
+
+# --------------------------------------------------------------------------
+# dense 3x3 conv, padding 1 (ResPath.convs, ACC_UNet/ACC_UNet.py:317-318,326)
+# --------------------------------------------------------------------------
+@dataclass
+class _C3Cfg:
+    B: int
+    H: int
+    W: int
+    Cin: int
+    Cout: int
+    want_stats: bool
+
+
+class _Conv3x3Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, cfg: _C3Cfg, x, weight, bias):
+        B, H, W, Ci, Co = cfg.B, cfg.H, cfg.W, cfg.Cin, cfg.Cout
+        P = B * H * W
+        Wr = _empty((Co, 9 * Ci), x)  # [co][tap][ci]
+        kern.permute4(weight, Wr, (Co, 3, 3, Ci), (9 * Ci, 3, 1, 9))
+        Z = _empty((B, H, W, Co), x)
+        stats = _empty((kern.gemm_stats_rows(P, Co), 2, Co), x) if cfg.want_stats else None
+        kern.gemm(P, Co, 9 * Ci, a=[x], lda=[Ci], amode=AMODE_SHIFT3, b=Wr, ldb=9 * Ci, c=Z,
+                  ldc=Co, bias=bias, H=H, W=W, cin=Ci, stats=stats)
+        ctx.cfg = cfg
+        ctx.save_for_backward(x, weight)
+        if stats is None:
+            stats = _empty((0,), x)
+        ctx.mark_non_differentiable(stats)
+        return Z, stats
+
+    @staticmethod
+    def backward(ctx, dZ, _ds):
+        cfg = ctx.cfg
+        x, weight = ctx.saved_tensors
+        dZ = dZ.contiguous()
+        B, H, W, Ci, Co = cfg.B, cfg.H, cfg.W, cfg.Cin, cfg.Cout
+        P = B * H * W
+        keep = []
+        dx = None
+        if ctx.needs_input_grad[1]:
+            Wf = _empty((Ci, 9 * Co), x)  # [ci][tap'][co] = W[co][ci][8-tap']
+            kern.permute4(weight, Wf, (Ci, 3, 3, Co), (9, 3, 1, 9 * Ci), flips=(0, 1, 1, 0))
+            dx = torch.empty_like(x)
+            keep.append(kern.gemm(P, Ci, 9 * Co, a=[dZ], lda=[Co], amode=AMODE_SHIFT3, b=Wf,
+                                  ldb=9 * Co, c=dx, ldc=Ci, H=H, W=W, cin=Co))
+        dWr = _empty((Co, 9 * Ci), x)
+        keep.append(kern.gemm(Co, 9 * Ci, P, a=[dZ], lda=[Co], amode=AMODE_COL, b=x, ldb=Ci,
+                              bmode=BMODE_NN_SHIFT3, c=dWr, ldc=9 * Ci, H=H, W=W, cin=Ci,
+                              allow_split=True))
+        dW = torch.empty_like(weight)
+        kern.permute4(dWr, dW, (Co, Ci, 3, 3), (9 * Ci, 1, 3 * Ci, Ci))
+        db = _empty((Co,), x)
+        keep.append(kern.colsum(dZ, P, Co, db))
+        return None, dx, dW, db
+
+
+def conv3x3(x: torch.Tensor, weight, bias, *, consumer_bn=None):
+    B, H, W, Ci = x.shape
+    Co = weight.shape[0]
+    want = _want_stats(consumer_bn)
+    cfg = _C3Cfg(B, H, W, Ci, Co, want)
+    Z, stats = _Conv3x3Fn.apply(cfg, x, weight, bias)
+    return Pending(Z, consumer_bn, ACT_LRELU, stats if want else None,
+                   kern.gemm_stats_rows(B * H * W, Co) if want else 0)
+
+
+# --------------------------------------------------------------------------
+# ConvTranspose2d(k=2, s=2) (ACC_UNet/ACC_UNet.py:578-590,637-648)
+# --------------------------------------------------------------------------
+class _ConvT2Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        B, H, W, Ci = x.shape
+        Co = weight.shape[1]
+        P = B * H * W
+        Wr = _empty((Ci, 4 * Co), x)  # [ci][d][co], d = di*2+dj
+        kern.permute4(weight, Wr, (Ci, 2, 2, Co), (4 * Co, 2, 1, 4))
+        T = _empty((B, H, W, 4 * Co), x)
+        kern.gemm(P, 4 * Co, Ci, a=[x], lda=[Ci], b=Wr, ldb=4 * Co, bmode=BMODE_NN, c=T,
+                  ldc=4 * Co)
+        Y = _empty((B, 2 * H, 2 * W, Co), x)
+        kern.pixel_shuffle2(T, bias, Y, B, H, W, Co)
+        ctx.save_for_backward(x, Wr)
+        ctx.shape = (B, H, W, Ci, Co)
+        return Y
+
+    @staticmethod
+    def backward(ctx, dY):
+        x, Wr = ctx.saved_tensors
+        B, H, W, Ci, Co = ctx.shape
+        P = B * H * W
+        dY = dY.contiguous()
+        dT = _empty((B, H, W, 4 * Co), x)
+        kern.pixel_shuffle2(dT, None, dY, B, H, W, Co, inverse=True)
+        keep = []
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            keep.append(kern.gemm(P, Ci, 4 * Co, a=[dT], lda=[4 * Co], b=Wr, ldb=4 * Co, c=dx,
+                                  ldc=Ci))
+        dWr = _empty((Ci, 4 * Co), x)
+        keep.append(kern.gemm(Ci, 4 * Co, P, a=[x], lda=[Ci], amode=AMODE_COL, b=dT,
+                              ldb=4 * Co, bmode=BMODE_NN, c=dWr, ldc=4 * Co, allow_split=True))
+        dW = _empty((Ci, Co, 2, 2), x)
+        kern.permute4(dWr, dW, (Ci, Co, 2, 2), (4 * Co, 1, 2 * Co, Co))
+        db = _empty((Co,), x)
+        keep.append(kern.colsum(dY, B * 4 * H * W, Co, db))
+        return dx, dW, db
+
+
+def conv_transpose2x2(x, weight, bias):
+    return _ConvT2Fn.apply(x, weight, bias)
+
+
+# --------------------------------------------------------------------------
+# MaxPool2d(2) / AvgPool2d(2)
+# --------------------------------------------------------------------------
+class _Pool2Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, mode):
+        B, H, W, C = x.shape
+        if H % 2 or W % 2:
+            raise ValueError("pool2: spatial size must be even")
+        y = _empty((B, H // 2, W // 2, C), x)
+        kern.pool2_fwd(x, y, B, H, W, C, mode)
+        ctx.mode = mode
+        if mode == kern.POOL_MAX:
+            ctx.save_for_backward(x, y)
+        else:
+            ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        saved = ctx.saved_tensors
+        x = saved[0]
+        y = saved[1] if ctx.mode == kern.POOL_MAX else x
+        B, H, W, C = x.shape
+        dx = torch.empty_like(x)
+        kern.pool2_bwd(x, y, dy.contiguous(), dx, B, H, W, C, ctx.mode)
+        return dx, None
+
+
+def pool2(x, mode=kern.POOL_MAX):
+    return _Pool2Fn.apply(x, mode)
+
+
+# --------------------------------------------------------------------------
+# channel concat (decoder torch.cat([up, skip], dim=1))
+# --------------------------------------------------------------------------
+class _CatFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b):
+        B, H, W, Ca = a.shape
+        Cb = b.shape[-1]
+        P = B * H * W
+        y = _empty((B, H, W, Ca + Cb), a)
+        kern.slice_copy(a, Ca, 0, y, Ca + Cb, 0, P, Ca)
+        kern.slice_copy(b, Cb, 0, y, Ca + Cb, Ca, P, Cb)
+        ctx.dims = (P, Ca, Cb)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        P, Ca, Cb = ctx.dims
+        dy = dy.contiguous()
+        da = db = None
+        if ctx.needs_input_grad[0]:
+            da = _empty(dy.shape[:-1] + (Ca,), dy)
+            kern.slice_copy(dy, Ca + Cb, 0, da, Ca, 0, P, Ca)
+        if ctx.needs_input_grad[1]:
+            db = _empty(dy.shape[:-1] + (Cb,), dy)
+            kern.slice_copy(dy, Ca + Cb, Ca, db, Cb, 0, P, Cb)
+        return da, db
+
+
+def cat_channels(a, b):
+    return _CatFn.apply(a, b)
+
+
+# --------------------------------------------------------------------------
+# head: 1x1 conv to one channel (+ Sigmoid) (ACC_UNet/ACC_UNet.py:594-599,653-659)
+# --------------------------------------------------------------------------
+class _HeadFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, sigm):
+        B, H, W, C = x.shape
+        y = _empty((B, H, W, 1), x)
+        kern.head_fwd(x, w, b, sigm, y, B * H * W, C)
+        ctx.sigm = sigm
+        ctx.save_for_backward(x, w, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, y = ctx.saved_tensors
+        B, H, W, C = x.shape
+        dx = torch.empty_like(x)
+        dw = torch.empty_like(w)
+        db = _empty((1,), x)
+        ws = kern.head_bwd(x, w, y, dy.contiguous(), ctx.sigm, dx, dw, db, B * H * W, C)
+        del ws
+        return dx, dw, db, None
+
+
+def head(x, weight, bias, sigmoid: bool):
+    C = x.shape[-1]
+    return _HeadFn.apply(x, weight.reshape(C), bias, bool(sigmoid))
+
+
+# --------------------------------------------------------------------------
+# ACC_UNet_W learnable merge y = m*W + x*(1-W) (ACC_UNet/ACC_UNet_w.py:497-522)
+# --------------------------------------------------------------------------
+class _WMergeFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b, w, want_stats):
+        C = a.shape[-1]
+        P = a.numel() // C
+        y = torch.empty_like(a)
+        stats = _empty((kern.stream_rows(P, C), 2, C), a) if want_stats else None
+        kern.wmerge_fwd(a, b, w, y, P, C, stats)
+        ctx.save_for_backward(a, b, w)
+        if stats is None:
+            stats = _empty((0,), a)
+        ctx.mark_non_differentiable(stats)
+        return y, stats
+
+    @staticmethod
+    def backward(ctx, dy, _ds):
+        a, b, w = ctx.saved_tensors
+        dy = dy.contiguous()
+        da = torch.empty_like(a)
+        db = torch.empty_like(b)
+        kern.wmerge_bwd(dy, w, da, db, a.numel())
+        dw = _empty((1,), a)
+        ws = kern.dotdiff(dy, a, b, a.numel(), dw)
+        del ws
+        return da, db, dw, None
+
+
+def wmerge(m, x, w, *, consumer_bn=None):
+    want = _want_stats(consumer_bn)
+    y, stats = _WMergeFn.apply(m, x, w, want)
+    C = y.shape[-1]
+    return Pending(y, consumer_bn, ACT_LRELU, stats if want else None,
+                   kern.stream_rows(y.numel() // C, C) if want else 0)
+
+
+# --------------------------------------------------------------------------
+# weight column relayout (MLFC merge: channel 2c = x_c, 2c+1 = x, ACC_UNet.py:492)
+# --------------------------------------------------------------------------
+class _GroupRelayoutFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, w2, J, order):
+        N, K = w2.shape
+        C = K // J
+        out = _empty((N, K), w2)
+        kern.group_relayout(w2, out, N, C, J, order)
+        ctx.meta = (N, C, J, list(order))
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        N, C, J, order = ctx.meta
+        out = _empty((N, J * C), g)
+        kern.group_relayout(g.contiguous(), out, N, C, J, order, inverse=True)
+        return out, None, None
+
+
+def group_relayout(w2, J, order):
+    return _GroupRelayoutFn.apply(w2, J, tuple(order))
+
+
+# --------------------------------------------------------------------------
+# NCHW <-> NHWC at the module boundary
+# --------------------------------------------------------------------------
+class _ToNHWCFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        B, C, H, W = x.shape
+        y = _empty((B, H, W, C), x)
+        kern.permute4(x, y, (B, H, W, C), (C * H * W, W, 1, H * W))
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        B, H, W, C = dy.shape
+        dx = _empty((B, C, H, W), dy)
+        kern.permute4(dy.contiguous(), dx, (B, C, H, W), (H * W * C, 1, W * C, C))
+        return dx
+
+
+def to_nhwc(x):
+    x = x.contiguous()
+    if x.dtype != torch.float32:
+        x = x.float()
+    return _ToNHWCFn.apply(x)
+
+
+class _ToNCHWFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, y):
+        B, H, W, C = y.shape
+        x = _empty((B, C, H, W), y)
+        kern.permute4(y, x, (B, C, H, W), (H * W * C, 1, W * C, C))
+        return x
+
+    @staticmethod
+    def backward(ctx, dx):
+        B, C, H, W = dx.shape
+        dy = _empty((B, H, W, C), dx)
+        kern.permute4(dx.contiguous(), dy, (B, H, W, C), (C * H * W, W, 1, H * W))
+        return dy
+
+
+def nhwc_to_nchw(y):
+    B, H, W, C = y.shape
+    if C == 1:
+        return y.view(B, 1, H, W)
+    return _ToNCHWFn.apply(y.contiguous())
+
+
+# --------------------------------------------------------------------------
+# WeightedDiceBCE(0.5, 0.5) (Experiments/utils.py:140-171)
+# --------------------------------------------------------------------------
+class _LossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, t, dice_w, bce_w):
+        B = x.shape[0]
+        N = x.numel() // B
+        res = torch.zeros(8 + 2 * B, dtype=torch.float32, device=x.device)
+        ws = kern.loss_fwd(x, t, B, N, dice_w, bce_w, res)
+        del ws
+        ctx.save_for_backward(x, t, res)
+        ctx.w = (dice_w, bce_w)
+        return res[0].clone(), res[1].clone(), res[2].clone()
+
+    @staticmethod
+    def backward(ctx, gl, _gd, _gb):
+        x, t, res = ctx.saved_tensors
+        B = x.shape[0]
+        N = x.numel() // B
+        dx = torch.empty_like(x)
+        g = gl.reshape(1).contiguous().float() if gl is not None else None
+        kern.loss_bwd(x, t, B, N, ctx.w[0], ctx.w[1], res, g, dx)
+        return dx, None, None, None
+
+
+def weighted_dice_bce(logits, truth, dice_weight=1.0, bce_weight=1.0):
+    x = logits.contiguous().float()
+    t = truth.contiguous().float().reshape(x.shape)
+    loss, _, _ = _LossFn.apply(x, t, float(dice_weight), float(bce_weight))
+    return loss
+
+
+def weighted_dice_terms(logits, truth):
+    """WeightedDiceLoss value (Experiments/utils.py:115-138) from the same kernel."""
+    x = logits.contiguous().float()
+    t = truth.contiguous().float().reshape(x.shape)
+    B = x.shape[0]
+    res = torch.zeros(8 + 2 * B, dtype=torch.float32, device=x.device)
+    kern.loss_fwd(x, t, B, x.numel() // B, 1.0, 1.0, res)
+    return res[1]

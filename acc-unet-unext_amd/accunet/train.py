@@ -1,0 +1,49 @@
+"""Training-step harness: the counterpart of Experiments/Train_one_epoch.py:48-201
+and train_model.py:269-833 for the ACC-UNet path, without the per-step host
+syncs of the reference loop (sklearn IoU on CPU, torch.cuda.empty_cache twice per
+step, Train_one_epoch.py:134,167,185): metrics stay on the device and are read
+only when logged.
+
+    step = TrainStep(model, lr=1e-3)            # Adam(lr 1e-3), WeightedDiceBCE(0.5, 0.5)
+    loss = step(images, masks)                  # fwd + loss + bwd (+ RCCL all-reduce) + Adam
+"""
+from __future__ import annotations
+
+import torch
+
+from .loss import WeightedDiceBCE
+from .optim import FusedAdam
+
+
+class TrainStep:
+    def __init__(self, model, lr=1e-3, reducer=None, dice_weight=0.5, bce_weight=0.5):
+        self.model = model
+        self.reducer = reducer
+        self.criterion = WeightedDiceBCE(dice_weight, bce_weight)
+        params = [p for p in model.parameters() if p.requires_grad]
+        if reducer is None:
+            # persistent gradient storage (stable pointers for the fused optimizer)
+            total = sum(p.numel() for p in params)
+            self.flat = torch.zeros(total, dtype=torch.float32, device=params[0].device)
+            o = 0
+            for p in params:
+                p.grad = self.flat[o:o + p.numel()].view_as(p)
+                o += p.numel()
+        self.opt = FusedAdam(params, lr=lr)
+
+    def zero_grad(self):
+        if self.reducer is not None:
+            self.reducer.zero_grad()
+        else:
+            self.flat.zero_()
+
+    def __call__(self, images, masks):
+        self.model.train(True)
+        self.zero_grad()
+        if self.reducer is not None:
+            self.reducer.prepare()
+        preds = self.model(images)
+        loss = self.criterion(preds, masks)
+        loss.backward()
+        self.opt.step()
+        return loss.detach()

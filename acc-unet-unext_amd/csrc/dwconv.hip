@@ -1,0 +1,331 @@
+// Depthwise 3x3 convolution (stride 1, zero padding 1, +bias) on NHWC fp32:
+// HANCBlock.conv2 + norm2 statistics, reference ACC_UNet/ACC_UNet.py:240-247,273-275.
+//
+// K1 (forward): z[b,h,w,c] = bias[c] + sum_tap W[c][tap] * a[b,h+dh,w+dw,c] where the
+// input a = act(x*scale[c] + shift[c]) is the pending BatchNorm(norm1)+LeakyReLU of the
+// conv1 output x, applied in registers (a is never written to HBM). The epilogue
+// writes per-block per-channel (sum z, sum z^2) partials for norm2.
+//
+// Mapping: a 256-thread block owns TCQ channel vectors (4 channels each) x (256/TCQ)
+// consecutive pixels of one image row-strip of TR rows. Each thread slides a 3x3
+// register window down its pixel column: per output row it issues 3 new 16-byte
+// loads (its own column + the two neighbours, which are L1/L2 hits shared with the
+// adjacent threads) and one 16-byte store, so HBM sees ~1 read + 1 write per element.
+#include "common.h"
+#include "kernels.h"
+
+#define DW_TR 8  // output rows per thread strip
+
+template <int V>
+struct VecT;
+template <>
+struct VecT<4> {
+  typedef float4 T;
+};
+template <>
+struct VecT<1> {
+  typedef float T;
+};
+
+template <int V>
+ACC_DEV void vload(const float* p, float (&v)[V]) {
+  if (V == 4) {
+    float4 q = ld4(p);
+    v[0] = q.x; v[1 % V] = q.y; v[2 % V] = q.z; v[3 % V] = q.w;
+  } else {
+    v[0] = p[0];
+  }
+}
+template <int V>
+ACC_DEV void vstore(float* p, const float (&v)[V]) {
+  if (V == 4) st4(p, make_float4(v[0], v[1 % V], v[2 % V], v[3 % V]));
+  else p[0] = v[0];
+}
+
+struct DwGeom {
+  int B, H, W, C;
+  int TCQ;      // channel vectors per block
+  int TW;       // pixels per block row
+  int tilesW, tilesH;
+};
+
+// flip != 0: use W[c][8-tap] (data gradient = correlation with the flipped kernel)
+template <int V>
+__global__ void __launch_bounds__(256)
+dw3x3_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
+                 const float* __restrict__ bias, const float* __restrict__ sc,
+                 const float* __restrict__ sh, int act, int flip, float* __restrict__ z,
+                 float* __restrict__ stats, DwGeom g) {
+  const int tid = threadIdx.x;
+  const int cql = tid % g.TCQ;
+  const int px = tid / g.TCQ;
+  const int cq = blockIdx.y * g.TCQ + cql;
+  const int c0 = cq * V;
+  int t = blockIdx.x;
+  const int tw = t % g.tilesW;
+  t /= g.tilesW;
+  const int th = t % g.tilesH;
+  const int b = t / g.tilesH;
+  const int w = tw * g.TW + px;
+  const int h0 = th * DW_TR;
+  const bool active = (px < g.TW) && (w < g.W) && (c0 < g.C);
+  const int C = g.C;
+
+  float s1[V], s2[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
+
+  if (active) {
+    float k[9][V], bi[V], psc[V], psh[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+#pragma unroll
+      for (int tp = 0; tp < 9; ++tp) k[tp][j] = wt[(c0 + j) * 9 + (flip ? 8 - tp : tp)];
+      bi[j] = bias ? bias[c0 + j] : 0.f;
+      psc[j] = sc ? sc[c0 + j] : 1.f;
+      psh[j] = sh ? sh[c0 + j] : 0.f;
+    }
+    const bool pro = sc != nullptr;
+    // window rows r0 (h-1), r1 (h), r2 (h+1); columns w-1, w, w+1
+    float win[3][3][V];
+    auto load_row = [&](int hh, float (&row)[3][V]) {
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) {
+        int ww = w + dx - 1;
+        if (hh >= 0 && hh < g.H && ww >= 0 && ww < g.W) {
+          vload<V>(x + (((long)b * g.H + hh) * g.W + ww) * C + c0, row[dx]);
+          if (pro) {
+#pragma unroll
+            for (int j = 0; j < V; ++j) row[dx][j] = apply_act(row[dx][j] * psc[j] + psh[j], act);
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < V; ++j) row[dx][j] = 0.f;
+        }
+      }
+    };
+    load_row(h0 - 1, win[0]);
+    load_row(h0, win[1]);
+    const int h1 = min(g.H, h0 + DW_TR);
+    for (int h = h0; h < h1; ++h) {
+      load_row(h + 1, win[2]);
+      float o[V];
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        float acc = bi[j];
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+          for (int dx = 0; dx < 3; ++dx) acc = fmaf(k[dy * 3 + dx][j], win[dy][dx][j], acc);
+        o[j] = acc;
+        s1[j] += acc;
+        s2[j] += acc * acc;
+      }
+      vstore<V>(z + (((long)b * g.H + h) * g.W + w) * C + c0, o);
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          win[0][dx][j] = win[1][dx][j];
+          win[1][dx][j] = win[2][dx][j];
+        }
+    }
+  }
+
+  if (stats) {
+    __shared__ float red[2][256 * 4];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      red[0][tid * V + j] = s1[j];
+      red[1][tid * V + j] = s2[j];
+    }
+    __syncthreads();
+    if (px == 0 && c0 < C) {
+      int npx = 256 / g.TCQ;
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        float a = 0.f, q = 0.f;
+        for (int i = 0; i < npx; ++i) {
+          a += red[0][(i * g.TCQ + cql) * V + j];
+          q += red[1][(i * g.TCQ + cql) * V + j];
+        }
+        stats[(long)blockIdx.x * 2 * C + c0 + j] = a;
+        stats[(long)blockIdx.x * 2 * C + C + c0 + j] = q;
+      }
+    }
+  }
+}
+
+// Weight + bias gradient: dW[c][tap] = sum_p dz[p,c] * a[shift_tap(p), c],
+// db[c] = sum_p dz[p,c]; a = act(x*scale+shift) recomputed. Output partials
+// [block][10][C] (taps 0..8, then bias).
+template <int V>
+__global__ void __launch_bounds__(256)
+dw3x3_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dz,
+                   const float* __restrict__ sc, const float* __restrict__ sh, int act,
+                   float* __restrict__ part, DwGeom g) {
+  const int tid = threadIdx.x;
+  const int cql = tid % g.TCQ;
+  const int px = tid / g.TCQ;
+  const int cq = blockIdx.y * g.TCQ + cql;
+  const int c0 = cq * V;
+  int t = blockIdx.x;
+  const int tw = t % g.tilesW;
+  t /= g.tilesW;
+  const int th = t % g.tilesH;
+  const int b = t / g.tilesH;
+  const int w = tw * g.TW + px;
+  const int h0 = th * DW_TR;
+  const bool active = (px < g.TW) && (w < g.W) && (c0 < g.C);
+  const int C = g.C;
+
+  float acc[10][V];
+#pragma unroll
+  for (int i = 0; i < 10; ++i)
+#pragma unroll
+    for (int j = 0; j < V; ++j) acc[i][j] = 0.f;
+
+  if (active) {
+    float psc[V], psh[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      psc[j] = sc ? sc[c0 + j] : 1.f;
+      psh[j] = sh ? sh[c0 + j] : 0.f;
+    }
+    const bool pro = sc != nullptr;
+    float win[3][3][V];
+    auto load_row = [&](int hh, float (&row)[3][V]) {
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) {
+        int ww = w + dx - 1;
+        if (hh >= 0 && hh < g.H && ww >= 0 && ww < g.W) {
+          vload<V>(x + (((long)b * g.H + hh) * g.W + ww) * C + c0, row[dx]);
+          if (pro) {
+#pragma unroll
+            for (int j = 0; j < V; ++j) row[dx][j] = apply_act(row[dx][j] * psc[j] + psh[j], act);
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < V; ++j) row[dx][j] = 0.f;
+        }
+      }
+    };
+    load_row(h0 - 1, win[0]);
+    load_row(h0, win[1]);
+    const int h1 = min(g.H, h0 + DW_TR);
+    for (int h = h0; h < h1; ++h) {
+      load_row(h + 1, win[2]);
+      float d[V];
+      vload<V>(dz + (((long)b * g.H + h) * g.W + w) * C + c0, d);
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+          for (int dx = 0; dx < 3; ++dx) acc[dy * 3 + dx][j] = fmaf(d[j], win[dy][dx][j], acc[dy * 3 + dx][j]);
+        acc[9][j] += d[j];
+      }
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          win[0][dx][j] = win[1][dx][j];
+          win[1][dx][j] = win[2][dx][j];
+        }
+    }
+  }
+
+  __shared__ float red[256 * 4];
+  const int npx = 256 / g.TCQ;
+  for (int i = 0; i < 10; ++i) {
+#pragma unroll
+    for (int j = 0; j < V; ++j) red[tid * V + j] = acc[i][j];
+    __syncthreads();
+    if (px == 0 && c0 < C) {
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        float a = 0.f;
+        for (int k = 0; k < npx; ++k) a += red[(k * g.TCQ + cql) * V + j];
+        part[((long)blockIdx.x * 10 + i) * C + c0 + j] = a;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// [10][C] sums -> dW[c][tap] (torch layout [C][1][3][3]) and db[c]
+__global__ void dw_wgrad_finish_kernel(const float* __restrict__ sums, int C, float* __restrict__ dw,
+                                       float* __restrict__ db) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+#pragma unroll
+  for (int tp = 0; tp < 9; ++tp) dw[c * 9 + tp] = sums[tp * C + c];
+  if (db) db[c] = sums[9 * C + c];
+}
+
+static DwGeom dw_geom(int B, int H, int W, int C, int V, dim3* grid) {
+  DwGeom g;
+  g.B = B; g.H = H; g.W = W; g.C = C;
+  int CQ = C / V;
+  if (CQ % 8 == 0) g.TCQ = 8;
+  else if (CQ <= 64) g.TCQ = CQ;
+  else g.TCQ = 8;  // (not hit on the ACC-UNet shapes)
+  g.TW = 256 / g.TCQ;
+  g.tilesW = ceil_div(W, g.TW);
+  g.tilesH = ceil_div(H, DW_TR);
+  *grid = dim3(B * g.tilesH * g.tilesW, ceil_div(CQ, g.TCQ));
+  return g;
+}
+
+extern "C" int accunet_dw3x3_rows(int B, int H, int W, int C) {
+  dim3 grid;
+  dw_geom(B, H, W, C, (C % 4 == 0) ? 4 : 1, &grid);
+  return (int)grid.x;
+}
+
+extern "C" int accunet_dw3x3_fwd(const float* x, const float* wt, const float* bias,
+                                 const float* sc, const float* sh, int act, int flip, float* z,
+                                 float* stats, int B, int H, int W, int C, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  int V = (C % 4 == 0) ? 4 : 1;
+  dim3 grid;
+  DwGeom g = dw_geom(B, H, W, C, V, &grid);
+  if (V == 4)
+    hipLaunchKernelGGL(dw3x3_fwd_kernel<4>, grid, dim3(256), 0, s, x, wt, bias, sc, sh, act, flip,
+                       z, stats, g);
+  else
+    hipLaunchKernelGGL(dw3x3_fwd_kernel<1>, grid, dim3(256), 0, s, x, wt, bias, sc, sh, act, flip,
+                       z, stats, g);
+  return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+}
+
+size_t dw_wgrad_ws(int B, int H, int W, int C) {
+  int R = accunet_dw3x3_rows(B, H, W, C);
+  return (size_t)R * 10 * C + accunet_partials_ws_elems(R, 10 * C) + 10 * (size_t)C;
+}
+
+extern "C" size_t accunet_dw3x3_wgrad_ws(int B, int H, int W, int C) { return dw_wgrad_ws(B, H, W, C); }
+
+extern "C" int accunet_dw3x3_wgrad(const float* x, const float* dz, const float* sc,
+                                   const float* sh, int act, float* dw, float* db, int B, int H,
+                                   int W, int C, float* ws, size_t ws_elems, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  int V = (C % 4 == 0) ? 4 : 1;
+  dim3 grid;
+  DwGeom g = dw_geom(B, H, W, C, V, &grid);
+  int R = (int)grid.x;
+  if (ws_elems < dw_wgrad_ws(B, H, W, C)) return ACC_EBADARG;
+  float* part = ws;
+  float* scratch = ws + (size_t)R * 10 * C;
+  float* sums = scratch + accunet_partials_ws_elems(R, 10 * C);
+  if (V == 4)
+    hipLaunchKernelGGL(dw3x3_wgrad_kernel<4>, grid, dim3(256), 0, s, x, dz, sc, sh, act, part, g);
+  else
+    hipLaunchKernelGGL(dw3x3_wgrad_kernel<1>, grid, dim3(256), 0, s, x, dz, sc, sh, act, part, g);
+  int rows;
+  const float* pr = reduce_partials(part, R, 10 * C, scratch, &rows, s);
+  hipLaunchKernelGGL(sum_rows_kernel, dim3(ceil_div(10 * C, 64)), dim3(256), 0, s, pr, rows, 10 * C,
+                     10 * C, sums);
+  hipLaunchKernelGGL(dw_wgrad_finish_kernel, dim3(ceil_div(C, 256)), dim3(256), 0, s, sums, C, dw, db);
+  return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+}

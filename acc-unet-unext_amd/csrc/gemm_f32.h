@@ -47,7 +47,7 @@ struct GemmParams {
   const float* b_scale;
   const float* b_shift;
   int H, W;  // pixel grid of the "pixel" operand (SHIFT3 modes, up-adds)
-  FastDiv fW, fH;
+  FastDiv fW, fH, fC;
   int cin;  // channels per tap for the SHIFT3 modes
   float* C;
   int ldc;
@@ -122,24 +122,9 @@ gemm_f32_kernel(const GemmParams p) {
 
   auto load_tiles = [&](int k0) {
     // ------------------------------ A ---------------------------------------
-    if (AMODE == AM_ROW || AMODE == AM_SHIFT3) {
-      int s = 0;
-      if (AMODE == AM_ROW) {
-#pragma unroll
-        for (int j = 1; j < 4; ++j)
-          if (j < p.nsrc && k0 >= p.kbeg[j]) s = j;
-      }
-      const float* Ab = p.A[s];
-      const int lda = p.lda[s];
-      const int kb = p.kbeg[s];
-      const int kend_s = (AMODE == AM_ROW) ? min(p.kbeg[s + 1], K) : K;
-      int tap = 0, cbase = 0, dh = 0, dw = 0;
-      if (AMODE == AM_SHIFT3) {
-        tap = k0 / p.cin;
-        cbase = k0 - tap * p.cin;
-        dh = tap / 3 - 1;
-        dw = tap % 3 - 1;
-      }
+    if (AMODE == AM_ROW) {
+      // up to 4 channel-concatenated sources; source seams may fall anywhere (a
+      // float4 never straddles one in the vectorised path: widths are % 4 == 0)
 #pragma unroll
       for (int i = 0; i < NPA; ++i) {
         int idx = tid + i * GEMM_THREADS;
@@ -147,30 +132,79 @@ gemm_f32_kernel(const GemmParams p) {
         int g = m0 + r;
         int k = k0 + 4 * q;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        bool rowok = (idx < BM * 4) && (g < M);
-        long src = g;
-        if (AMODE == AM_SHIFT3) {
-          int hh = a_h[i] + dh, ww = a_w[i] + dw;
-          rowok = rowok && hh >= 0 && hh < p.H && ww >= 0 && ww < p.W;
-          src = (long)g + dh * p.W + dw;
-        }
-        if (rowok) {
-          const float* ptr = (AMODE == AM_SHIFT3) ? Ab + src * lda + cbase + 4 * q
-                                                  : Ab + src * lda + (k - kb);
+        if ((idx < BM * 4) && (g < M)) {
           if (VA) {
-            if (k < kend_s) v = ld4(ptr);
+            if (k < K) {
+              int s = 0;
+#pragma unroll
+              for (int j = 1; j < 4; ++j)
+                if (j < p.nsrc && k >= p.kbeg[j]) s = j;
+              v = ld4(p.A[s] + (long)g * p.lda[s] + (k - p.kbeg[s]));
+              if (PRO_A != PRO_NONE && s == 0) {
+                v.x = pro_apply<PRO_A>(v.x, p.a_scale[k + 0], p.a_shift[k + 0]);
+                v.y = pro_apply<PRO_A>(v.y, p.a_scale[k + 1], p.a_shift[k + 1]);
+                v.z = pro_apply<PRO_A>(v.z, p.a_scale[k + 2], p.a_shift[k + 2]);
+                v.w = pro_apply<PRO_A>(v.w, p.a_scale[k + 3], p.a_shift[k + 3]);
+              }
+            }
           } else {
-            if (k + 0 < kend_s) v.x = ptr[0];
-            if (k + 1 < kend_s) v.y = ptr[1];
-            if (k + 2 < kend_s) v.z = ptr[2];
-            if (k + 3 < kend_s) v.w = ptr[3];
+            float e[4];
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+              int kk = k + jj;
+              e[jj] = 0.f;
+              if (kk < K) {
+                int s = 0;
+#pragma unroll
+                for (int j = 1; j < 4; ++j)
+                  if (j < p.nsrc && kk >= p.kbeg[j]) s = j;
+                float x = p.A[s][(long)g * p.lda[s] + (kk - p.kbeg[s])];
+                if (PRO_A != PRO_NONE && s == 0) x = pro_apply<PRO_A>(x, p.a_scale[kk], p.a_shift[kk]);
+                e[jj] = x;
+              }
+            }
+            v = make_float4(e[0], e[1], e[2], e[3]);
           }
-          if (PRO_A != PRO_NONE) {
-            // prologue on the channel axis; padding zeros stay zero
-            if (k + 0 < kend_s) v.x = pro_apply<PRO_A>(v.x, p.a_scale[k + 0], p.a_shift[k + 0]);
-            if (k + 1 < kend_s) v.y = pro_apply<PRO_A>(v.y, p.a_scale[k + 1], p.a_shift[k + 1]);
-            if (k + 2 < kend_s) v.z = pro_apply<PRO_A>(v.z, p.a_scale[k + 2], p.a_shift[k + 2]);
-            if (k + 3 < kend_s) v.w = pro_apply<PRO_A>(v.w, p.a_scale[k + 3], p.a_shift[k + 3]);
+        }
+        ra[i] = v;
+      }
+    } else if (AMODE == AM_SHIFT3) {
+      // implicit 3x3: k = tap*cin + ci; zero padding outside the image
+      const float* Ab = p.A[0];
+      const int lda = p.lda[0];
+#pragma unroll
+      for (int i = 0; i < NPA; ++i) {
+        int idx = tid + i * GEMM_THREADS;
+        int r = idx >> 2, q = idx & 3;
+        int g = m0 + r;
+        int k = k0 + 4 * q;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if ((idx < BM * 4) && (g < M)) {
+          if (VA) {  // cin % 4 == 0: the quad shares one tap
+            if (k < K) {
+              int tap = (int)fdiv((uint32_t)k, p.fC);
+              int ci = k - tap * p.cin;
+              int dh = tap / 3 - 1, dw = tap - (tap / 3) * 3 - 1;
+              int hh = a_h[i] + dh, ww = a_w[i] + dw;
+              if (hh >= 0 && hh < p.H && ww >= 0 && ww < p.W)
+                v = ld4(Ab + ((long)g + dh * p.W + dw) * lda + ci);
+            }
+          } else {
+            float e[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              e[j] = 0.f;
+              int kk = k + j;
+              if (kk < K) {
+                int tap = (int)fdiv((uint32_t)kk, p.fC);
+                int ci = kk - tap * p.cin;
+                int dh = tap / 3 - 1, dw = tap - (tap / 3) * 3 - 1;
+                int hh = a_h[i] + dh, ww = a_w[i] + dw;
+                if (hh >= 0 && hh < p.H && ww >= 0 && ww < p.W)
+                  e[j] = Ab[((long)g + dh * p.W + dw) * lda + ci];
+              }
+            }
+            v = make_float4(e[0], e[1], e[2], e[3]);
           }
         }
         ra[i] = v;
@@ -221,14 +255,7 @@ gemm_f32_kernel(const GemmParams p) {
         }
         rb[i] = v;
       }
-    } else {  // BM_NN / BM_NN_SHIFT3: B(k,n) = B[row(k)*ldb + n]
-      int tap = 0, ncb = n0, dh = 0, dw = 0;
-      if (BMODE == BM_NN_SHIFT3) {
-        tap = n0 / p.cin;
-        ncb = n0 - tap * p.cin;
-        dh = tap / 3 - 1;
-        dw = tap % 3 - 1;
-      }
+    } else if (BMODE == BM_NN) {  // B(k,n) = B[k*ldb + n]
 #pragma unroll
       for (int i = 0; i < NPB; ++i) {
         int idx = tid + i * GEMM_THREADS;
@@ -236,17 +263,8 @@ gemm_f32_kernel(const GemmParams p) {
         int k = k0 + kr;
         int n = n0 + 4 * q;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        bool ok = idx < BN * 4 && k < kend;
-        long row = k;
-        if (BMODE == BM_NN_SHIFT3 && ok) {
-          uint32_t qq = fdiv((uint32_t)k, p.fW);
-          int ww = k - (int)qq * p.W;
-          int hh = (int)(qq - fdiv(qq, p.fH) * p.H);
-          ok = (hh + dh) >= 0 && (hh + dh) < p.H && (ww + dw) >= 0 && (ww + dw) < p.W;
-          row = (long)k + dh * p.W + dw;
-        }
-        if (ok) {
-          const float* ptr = p.B + row * p.ldb + (BMODE == BM_NN_SHIFT3 ? ncb + 4 * q : n);
+        if (idx < BN * 4 && k < kend) {
+          const float* ptr = p.B + (long)k * p.ldb + n;
           if (VB) {
             if (n < N) v = ld4(ptr);
           } else {
@@ -260,6 +278,45 @@ gemm_f32_kernel(const GemmParams p) {
             if (n + 1 < N) v.y = pro_apply<PRO_B>(v.y, p.b_scale[n + 1], p.b_shift[n + 1]);
             if (n + 2 < N) v.z = pro_apply<PRO_B>(v.z, p.b_scale[n + 2], p.b_shift[n + 2]);
             if (n + 3 < N) v.w = pro_apply<PRO_B>(v.w, p.b_scale[n + 3], p.b_shift[n + 3]);
+          }
+        }
+        rb[i] = v;
+      }
+    } else {  // BM_NN_SHIFT3: B(k = pixel p, n = tap*cin + ci) = X[shift_tap(p)*ldb + ci]
+#pragma unroll
+      for (int i = 0; i < NPB; ++i) {
+        int idx = tid + i * GEMM_THREADS;
+        int kr = idx / (BN / 4), q = idx % (BN / 4);
+        int k = k0 + kr;
+        int n = n0 + 4 * q;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (idx < BN * 4 && k < kend) {
+          uint32_t qq = fdiv((uint32_t)k, p.fW);
+          int ww0 = k - (int)qq * p.W;
+          int hh0 = (int)(qq - fdiv(qq, p.fH) * p.H);
+          if (VB) {  // cin % 4 == 0: the quad shares one tap
+            if (n < N) {
+              int tap = (int)fdiv((uint32_t)n, p.fC);
+              int ci = n - tap * p.cin;
+              int dh = tap / 3 - 1, dw = tap - (tap / 3) * 3 - 1;
+              if (hh0 + dh >= 0 && hh0 + dh < p.H && ww0 + dw >= 0 && ww0 + dw < p.W)
+                v = ld4(p.B + ((long)k + dh * p.W + dw) * p.ldb + ci);
+            }
+          } else {
+            float e[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              e[j] = 0.f;
+              int nn = n + j;
+              if (nn < N) {
+                int tap = (int)fdiv((uint32_t)nn, p.fC);
+                int ci = nn - tap * p.cin;
+                int dh = tap / 3 - 1, dw = tap - (tap / 3) * 3 - 1;
+                if (hh0 + dh >= 0 && hh0 + dh < p.H && ww0 + dw >= 0 && ww0 + dw < p.W)
+                  e[j] = p.B[((long)k + dh * p.W + dw) * p.ldb + ci];
+              }
+            }
+            v = make_float4(e[0], e[1], e[2], e[3]);
           }
         }
         rb[i] = v;

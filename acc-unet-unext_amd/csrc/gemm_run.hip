@@ -49,32 +49,25 @@ static int pick_tile(int M, int N, int bmode, int cin) {
   else if (N <= 32) t = TILE_C;
   else if (N <= 64) t = TILE_B;
   else t = TILE_A;
-  if (bmode == BM_NN_SHIFT3) {
-    // the n-tile must not straddle two taps
-    if (cin % tile_bn(t) != 0) {
-      if (tile_bn(t) == 128) t = (t == TILE_D) ? TILE_E : TILE_B;
-    }
-    if (cin % tile_bn(t) != 0) t = TILE_C;
-  }
+  (void)bmode;
+  (void)cin;
   return t;
 }
 
 int gemm_run(GemmParams p, int amode, int bmode, int pro_a, int pro_b, bool allow_split,
              float* ws, size_t ws_elems, hipStream_t stream) {
   if (p.M <= 0 || p.N <= 0) return ACC_OK;
-  if (amode == AM_SHIFT3 && (p.cin % GEMM_BK) != 0) return ACC_EBADSHAPE;
-  if (bmode == BM_NN_SHIFT3 && (p.cin % 32) != 0) return ACC_EBADSHAPE;
+  if ((amode == AM_SHIFT3 || bmode == BM_NN_SHIFT3) && p.cin <= 0) return ACC_EBADSHAPE;
   // vectorised (float4) operand loads need every contiguous extent % 4 == 0
   bool vec = true;
   if (amode == AM_ROW) {
     for (int s = 0; s < p.nsrc; ++s) {
       int w = p.kbeg[s + 1] - p.kbeg[s];
       if ((w & 3) || (p.lda[s] & 3) || ((uintptr_t)p.A[s] & 15)) vec = false;
-      if (s + 1 < p.nsrc && (w % GEMM_BK) != 0) return ACC_EBADSHAPE;  // source seams on k-tiles
     }
     if (p.K & 3) vec = false;
   } else if (amode == AM_SHIFT3) {
-    if ((p.lda[0] & 3) || ((uintptr_t)p.A[0] & 15)) vec = false;
+    if ((p.cin & 3) || (p.lda[0] & 3) || ((uintptr_t)p.A[0] & 15)) vec = false;
   } else {  // AM_COL
     if ((p.M & 3) || (p.lda[0] & 3) || ((uintptr_t)p.A[0] & 15)) vec = false;
   }
@@ -82,6 +75,7 @@ int gemm_run(GemmParams p, int amode, int bmode, int pro_a, int pro_b, bool allo
     if ((p.K & 3) || (p.ldb & 3) || ((uintptr_t)p.B & 15)) vec = false;
   } else {
     if ((p.N & 3) || (p.ldb & 3) || ((uintptr_t)p.B & 15)) vec = false;
+    if (bmode == BM_NN_SHIFT3 && (p.cin & 3)) vec = false;
   }
   if (amode == AM_ROW && p.nsrc == 1) { p.kbeg[0] = 0; p.kbeg[1] = p.K; }
   gemm_kfn* tab = table_v(amode, bmode, pro_a, pro_b, vec ? 1 : 0);
@@ -155,6 +149,7 @@ extern "C" int accunet_gemm(const AccGemmDesc* d, float* ws, size_t ws_elems, vo
   p.fW = make_fastdiv((uint32_t)p.W);
   p.fH = make_fastdiv((uint32_t)p.H);
   p.cin = d->cin;
+  p.fC = make_fastdiv((uint32_t)(p.cin > 0 ? p.cin : 1));
   p.C = d->c;
   p.ldc = d->ldc;
   p.bias = d->bias;

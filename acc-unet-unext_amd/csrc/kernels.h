@@ -14,3 +14,5 @@ size_t accunet_partials_ws_elems(int R, int Wd);
 
 __global__ void sum_rows_kernel(const float* __restrict__ part, int R, int stride, int ncols,
                                 float* __restrict__ out);
+
+__global__ void inc_i64_kernel(long long* p);

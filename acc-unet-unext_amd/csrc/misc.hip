@@ -1,0 +1,399 @@
+// Head, loss and optimizer kernels on the training step.
+//
+//  - head: 1x1 conv n_filts -> 1 (+bias) with optional Sigmoid
+//    (ACC_UNet.out / last_activation, ACC_UNet/ACC_UNet.py:594-599,653-659).
+//  - WeightedDiceBCE(dice 0.5, BCE 0.5) forward/backward
+//    (Experiments/utils.py:21-74 WeightedBCE, :109-138 WeightedDiceLoss,
+//    :140-171 WeightedDiceBCE) on the logits [B, N].
+//  - Adam (torch.optim.Adam, lr 1e-3, betas (0.9, 0.999), eps 1e-8, no weight decay;
+//    Experiments/train_model.py:647) as one multi-tensor launch over every parameter.
+#include "common.h"
+#include "chan.h"
+#include "kernels.h"
+
+// ---------------------------------------------------------------------------
+// head
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+head_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ b,
+                int sigm, float* __restrict__ y, long P, int C) {
+  for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < P; p += (long)gridDim.x * blockDim.x) {
+    const float* xr = x + p * C;
+    float acc = 0.f;
+    for (int c = 0; c < C; ++c) acc = fmaf(xr[c], w[c], acc);
+    acc += b[0];
+    y[p] = sigm ? 1.f / (1.f + expf(-acc)) : acc;
+  }
+}
+
+// dx[p,c] = g[p]*w[c]; partial dw/db per block: part[blk][C+1]
+__global__ void __launch_bounds__(256)
+head_bwd_kernel(const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ y,
+                const float* __restrict__ dy, int sigm, float* __restrict__ dx, long P, int C,
+                float* __restrict__ part) {
+  __shared__ float red[256][33];
+  float acc[33];
+  for (int c = 0; c <= C && c < 33; ++c) acc[c] = 0.f;
+  long per = (P + gridDim.x - 1) / gridDim.x;
+  long p0 = blockIdx.x * per, p1 = min(P, p0 + per);
+  for (long p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
+    float g = dy[p];
+    if (sigm) {
+      float yy = y[p];
+      g *= yy * (1.f - yy);
+    }
+    const float* xr = x + p * C;
+    float* dr = dx + p * C;
+    for (int c = 0; c < C; ++c) {
+      dr[c] = g * w[c];
+      acc[c] = fmaf(g, xr[c], acc[c]);
+    }
+    acc[C] += g;
+  }
+  for (int c = 0; c <= C; ++c) red[threadIdx.x][c] = acc[c];
+  __syncthreads();
+  for (int c = threadIdx.x; c <= C; c += blockDim.x) {
+    float s = 0.f;
+    for (int t = 0; t < 256; ++t) s += red[t][c];
+    part[(long)blockIdx.x * (C + 1) + c] = s;
+  }
+}
+
+extern "C" int accunet_head_fwd(const float* x, const float* w, const float* b, int sigm, float* y,
+                                long P, int C, void* stream) {
+  long blocks = (P + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(head_fwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, w, b,
+                     sigm, y, P, C);
+  return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+}
+
+extern "C" size_t accunet_head_ws_elems(long P, int C) { return (size_t)512 * (C + 1) + 2 * (C + 1) + 64; }
+
+extern "C" int accunet_head_bwd(const float* x, const float* w, const float* y, const float* dy,
+                                int sigm, float* dx, float* dw, float* db, long P, int C, float* ws,
+                                size_t ws_elems, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (C > 32) return ACC_EBADSHAPE;
+  const int nb = 512;
+  if (ws_elems < accunet_head_ws_elems(P, C)) return ACC_EBADARG;
+  float* part = ws;
+  float* sums = ws + (size_t)nb * (C + 1);
+  hipLaunchKernelGGL(head_bwd_kernel, dim3(nb), dim3(256), 0, s, x, w, y, dy, sigm, dx, P, C, part);
+  hipLaunchKernelGGL(sum_rows_kernel, dim3(ceil_div(C + 1, 64)), dim3(256), 0, s, part, nb, C + 1,
+                     C + 1, sums);
+  hipMemcpyAsync(dw, sums, sizeof(float) * C, hipMemcpyDeviceToDevice, s);
+  hipMemcpyAsync(db, sums + C, sizeof(float), hipMemcpyDeviceToDevice, s);
+  return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+}
+
+// ---------------------------------------------------------------------------
+// WeightedDiceBCE
+//   partial row per block (block covers a chunk of one sample b):
+//   [0] sum p*t'  [1] sum p^2  [2] sum tw^2  [3] n_pos  [4] sum pos*l  [5] sum neg*l
+//   (p = w*sigmoid(x), tw = w*t, w = t*(w1-w0)+w0 ; BCE on t_b = normalised truth)
+// ---------------------------------------------------------------------------
+#define LOSS_NCH 64
+
+__global__ void __launch_bounds__(256)
+max_kernel(const float* __restrict__ t, long n, float* __restrict__ out) {
+  __shared__ float red[256];
+  float m = -INFINITY;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    m = fmaxf(m, t[i]);
+  red[threadIdx.x] = m;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + s]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[blockIdx.x] = red[0];
+}
+
+ACC_DEV float bce_logits(float x, float t) {
+  // max(x,0) - x*t + log(1 + exp(-|x|))  (torch binary_cross_entropy_with_logits)
+  return fmaxf(x, 0.f) - x * t + log1pf(expf(-fabsf(x)));
+}
+
+__global__ void __launch_bounds__(256)
+loss_reduce_kernel(const float* __restrict__ x, const float* __restrict__ t, int B, long N,
+                   const float* __restrict__ tmax_part, int nmax, float dw0, float dw1,
+                   float* __restrict__ part) {
+  __shared__ float red[6][256];
+  const int b = blockIdx.x / LOSS_NCH, ch = blockIdx.x % LOSS_NCH;
+  float tmax = -INFINITY;
+  for (int i = 0; i < nmax; ++i) tmax = fmaxf(tmax, tmax_part[i]);
+  const bool binarize = tmax > 1.f;
+  long per = (N + LOSS_NCH - 1) / LOSS_NCH;
+  long i0 = ch * per, i1 = min(N, i0 + per);
+  float a[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (long i = i0 + threadIdx.x; i < i1; i += 256) {
+    float xv = x[(long)b * N + i], tv = t[(long)b * N + i];
+    float w = tv * (dw1 - dw0) + dw0;
+    float p = w * (1.f / (1.f + expf(-xv)));
+    float tw = w * tv;
+    a[0] += p * tw;
+    a[1] += p * p;
+    a[2] += tw * tw;
+    float tb = binarize ? (tv > 0.f ? 1.f : 0.f) : tv;
+    float l = bce_logits(xv, tb);
+    float pos = tb > 0.5f ? 1.f : 0.f;
+    a[3] += pos;
+    a[4] += pos * l;
+    a[5] += (1.f - pos) * l;
+  }
+  for (int k = 0; k < 6; ++k) red[k][threadIdx.x] = a[k];
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s)
+      for (int k = 0; k < 6; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x < 6) part[(long)blockIdx.x * 6 + threadIdx.x] = red[threadIdx.x][0];
+}
+
+// res layout: [0] loss [1] dice [2] bce [3] pw [4] nw [5] binarize flag, then per b: I, U
+__global__ void loss_finalize_kernel(const float* __restrict__ part, int B, long N,
+                                     const float* __restrict__ tmax_part, int nmax, float bw0,
+                                     float bw1, float dice_w, float bce_w, float smooth,
+                                     float* __restrict__ res) {
+  if (threadIdx.x != 0) return;
+  double dice = 0.0, npos = 0.0, spos = 0.0, sneg = 0.0;
+  for (int b = 0; b < B; ++b) {
+    double I = 0, P2 = 0, T2 = 0;
+    for (int ch = 0; ch < LOSS_NCH; ++ch) {
+      const float* pr = part + ((long)b * LOSS_NCH + ch) * 6;
+      I += pr[0];
+      P2 += pr[1];
+      T2 += pr[2];
+      npos += pr[3];
+      spos += pr[4];
+      sneg += pr[5];
+    }
+    double U = P2 + T2;
+    dice += 1.0 - (2.0 * I + smooth) / (U + smooth);
+    res[8 + 2 * b] = (float)I;
+    res[8 + 2 * b + 1] = (float)U;
+  }
+  dice /= B;
+  double nneg = (double)B * N - npos;
+  double pw = npos < 1.0 ? 1.0 : npos;
+  double nw = nneg < 1.0 ? 1.0 : nneg;
+  double bce = bw0 * spos / pw + bw1 * sneg / nw;
+  float tmax = -INFINITY;
+  for (int i = 0; i < nmax; ++i) tmax = fmaxf(tmax, tmax_part[i]);
+  res[0] = (float)(dice_w * dice + bce_w * bce);
+  res[1] = (float)dice;
+  res[2] = (float)bce;
+  res[3] = (float)pw;
+  res[4] = (float)nw;
+  res[5] = tmax > 1.f ? 1.f : 0.f;
+}
+
+__global__ void __launch_bounds__(256)
+loss_bwd_kernel(const float* __restrict__ x, const float* __restrict__ t, int B, long N,
+                const float* __restrict__ res, const float* __restrict__ gout, float dw0, float dw1,
+                float bw0, float bw1, float dice_w, float bce_w, float smooth,
+                float* __restrict__ dx) {
+  const float g0 = gout ? gout[0] : 1.f;
+  const float pw = res[3], nw = res[4];
+  const bool binarize = res[5] > 0.5f;
+  long total = (long)B * N;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    int b = (int)(i / N);
+    float I = res[8 + 2 * b], U = res[8 + 2 * b + 1];
+    float xv = x[i], tv = t[i];
+    float sg = 1.f / (1.f + expf(-xv));
+    float w = tv * (dw1 - dw0) + dw0;
+    float p = w * sg, tw = w * tv;
+    float den = U + smooth;
+    float dD_dp = -(2.f * tw * den - (2.f * I + smooth) * 2.f * p) / (den * den);
+    float gd = dD_dp * w * sg * (1.f - sg) * (dice_w / B);
+    float tb = binarize ? (tv > 0.f ? 1.f : 0.f) : tv;
+    float pos = tb > 0.5f ? 1.f : 0.f;
+    float gb = (sg - tb) * (pos * bw0 / pw + (1.f - pos) * bw1 / nw) * bce_w;
+    dx[i] = g0 * (gd + gb);
+  }
+}
+
+extern "C" size_t accunet_loss_ws_elems(int B) { return (size_t)B * LOSS_NCH * 6 + 256 + 8 + 2 * (size_t)B; }
+
+// res (device, >= 8 + 2B floats) receives [loss, dice, bce, pw, nw, binarize, -, -, (I,U) per b]
+extern "C" int accunet_loss_fwd(const float* x, const float* t, int B, long N, float dice_w,
+                                float bce_w, float* res, float* ws, size_t ws_elems, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (ws_elems < accunet_loss_ws_elems(B)) return ACC_EBADARG;
+  float* part = ws;
+  float* tmax = ws + (size_t)B * LOSS_NCH * 6;
+  const int nmax = 256;
+  hipLaunchKernelGGL(max_kernel, dim3(nmax), dim3(256), 0, s, t, (long)B * N, tmax);
+  hipLaunchKernelGGL(loss_reduce_kernel, dim3(B * LOSS_NCH), dim3(256), 0, s, x, t, B, N, tmax,
+                     nmax, 0.5f, 0.5f, part);
+  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(64), 0, s, part, B, N, tmax, nmax, 0.5f,
+                     0.5f, dice_w, bce_w, 1e-5f, res);
+  return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+}
+
+extern "C" int accunet_loss_bwd(const float* x, const float* t, int B, long N, float dice_w,
+                                float bce_w, const float* res, const float* gout, float* dx,
+                                void* stream) {
+  long total = (long)B * N;
+  long blocks = (total + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(loss_bwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, t, B, N,
+                     res, gout, 0.5f, 0.5f, 0.5f, 0.5f, dice_w, bce_w, 1e-5f, dx);
+  return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+}
+
+// ---------------------------------------------------------------------------
+// Multi-tensor Adam: one launch over every parameter tensor.
+// table: per tensor {p, g, m, v} device pointers + numel; chunks map blocks to
+// (tensor, start). Same arithmetic order as torch.optim.Adam (foreach path):
+//   m = m + (1-b1)*(g-m);  v = v*b2 + (1-b2)*g*g;
+//   p = p - step_size * m / (sqrt(v)/bc2_sqrt + eps)
+// ---------------------------------------------------------------------------
+struct AdamTensor {
+  float* p;
+  const float* g;
+  float* m;
+  float* v;
+  long long n;
+};
+
+#define ADAM_CHUNK 16384
+
+__global__ void __launch_bounds__(256)
+adam_kernel(const AdamTensor* __restrict__ tab, const int* __restrict__ chunk_t,
+            const long long* __restrict__ chunk_s, float b1, float b2, float eps, float step_size,
+            float bc2_sqrt, float wd) {
+  const int c = blockIdx.x;
+  const AdamTensor T = tab[chunk_t[c]];
+  long long s0 = chunk_s[c];
+  long long s1 = min(T.n, s0 + (long long)ADAM_CHUNK);
+  for (long long i = s0 + threadIdx.x; i < s1; i += blockDim.x) {
+    float g = T.g[i];
+    float p = T.p[i];
+    if (wd != 0.f) g = g + wd * p;
+    float m = T.m[i];
+    m = m + (1.f - b1) * (g - m);
+    float v = T.v[i] * b2 + (1.f - b2) * g * g;
+    float denom = sqrtf(v) / bc2_sqrt + eps;
+    T.m[i] = m;
+    T.v[i] = v;
+    T.p[i] = p - step_size * (m / denom);
+  }
+}
+
+extern "C" int accunet_adam_chunk_elems() { return ADAM_CHUNK; }
+
+extern "C" int accunet_adam_step(const void* table, const int* chunk_t, const long long* chunk_s,
+                                 int nchunks, float lr, float b1, float b2, float eps, float wd,
+                                 int step, void* stream) {
+  if (nchunks <= 0) return ACC_OK;
+  double bc1 = 1.0 - pow((double)b1, step);
+  double bc2 = 1.0 - pow((double)b2, step);
+  float step_size = (float)(lr / bc1);
+  float bc2_sqrt = (float)sqrt(bc2);
+  hipLaunchKernelGGL(adam_kernel, dim3(nchunks), dim3(256), 0, (hipStream_t)stream,
+                     (const AdamTensor*)table, chunk_t, chunk_s, b1, b2, eps, step_size, bc2_sqrt,
+                     wd);
+  return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+}
+
+// ---------------------------------------------------------------------------
+// out[0] = sum_i g[i] * (a[i] - b[i])  (gradient of ACC_UNet_W's scalar merge weight,
+// ACC_UNet/ACC_UNet_w.py:497-522: y = m*W + x*(1-W)); deterministic two-level sum.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+dotdiff_kernel(const float* __restrict__ g, const float* __restrict__ a, const float* __restrict__ b,
+               long n, float* __restrict__ part) {
+  __shared__ float red[256];
+  float s = 0.f;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    s += g[i] * (a[i] - b[i]);
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+__global__ void finish_sum_kernel(const float* __restrict__ part, int n, float* __restrict__ out,
+                                  int accumulate) {
+  if (threadIdx.x != 0) return;
+  double s = 0.0;
+  for (int i = 0; i < n; ++i) s += part[i];
+  out[0] = accumulate ? out[0] + (float)s : (float)s;
+}
+
+extern "C" int accunet_dotdiff(const float* g, const float* a, const float* b, long n, float* out,
+                               int accumulate, float* ws, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(dotdiff_kernel, dim3(1024), dim3(256), 0, s, g, a, b, n, ws);
+  hipLaunchKernelGGL(finish_sum_kernel, dim3(1), dim3(64), 0, s, ws, 1024, out, accumulate);
+  return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+}
+
+// y = a*w + b*(1-w) (w device scalar), with optional partial channel stats of y
+template <int V>
+__global__ void __launch_bounds__(256)
+wmerge_kernel(const float* __restrict__ a, const float* __restrict__ b, const float* __restrict__ w,
+              float* __restrict__ y, long P, int C, float* __restrict__ stats) {
+  ChanTile t = chan_tile<V>(C);
+  long rows_per = (P + gridDim.x - 1) / gridDim.x;
+  long r0 = blockIdx.x * rows_per, r1 = min(P, r0 + rows_per);
+  float s1[V], s2[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
+  const float wv = w[0];
+  if (t.active) {
+    for (long r = r0 + t.rg; r < r1; r += t.RG) {
+      float va[V], vb[V];
+      ldv<V>(a + r * C + t.c0, va);
+      ldv<V>(b + r * C + t.c0, vb);
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        va[j] = va[j] * wv + vb[j] * (1.f - wv);
+        s1[j] += va[j];
+        s2[j] += va[j] * va[j];
+      }
+      stv<V>(y + r * C + t.c0, va);
+    }
+  }
+  if (stats) block_chan_reduce2<V>(t, s1, s2, stats, blockIdx.x, C);
+}
+
+extern "C" int accunet_wmerge_fwd(const float* a, const float* b, const float* w, float* y, long P,
+                                  int C, float* stats, void* stream) {
+  int V = (C % 4 == 0) ? 4 : 1;
+  int nb = stream_rowblocks(P, C);
+  dim3 grid(nb, ceil_div(C / V, 64));
+  if (V == 4)
+    hipLaunchKernelGGL(wmerge_kernel<4>, grid, dim3(256), 0, (hipStream_t)stream, a, b, w, y, P, C, stats);
+  else
+    hipLaunchKernelGGL(wmerge_kernel<1>, grid, dim3(256), 0, (hipStream_t)stream, a, b, w, y, P, C, stats);
+  return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+}
+
+// dA = w*g, dB = (1-w)*g (B gradient optionally accumulated)
+__global__ void __launch_bounds__(256)
+wmerge_bwd_kernel(const float* __restrict__ g, const float* __restrict__ w, float* __restrict__ da,
+                  float* __restrict__ db, long n) {
+  const float wv = w[0];
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float gv = g[i];
+    da[i] = wv * gv;
+    db[i] = (1.f - wv) * gv;
+  }
+}
+
+extern "C" int accunet_wmerge_bwd(const float* g, const float* w, float* da, float* db, long n,
+                                  void* stream) {
+  long blocks = (n + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(wmerge_bwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, g, w, da, db, n);
+  return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+}

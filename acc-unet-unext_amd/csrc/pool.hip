@@ -1,0 +1,432 @@
+// Pooling / resampling / layout kernels on NHWC fp32.
+//
+//  - HANC neighbourhood pyramid (HANCLayer, ACC_UNet/ACC_UNet.py:86-106): from the
+//    pending-BN input a = act(x*scale+shift) produce at 1/2 resolution
+//    P2 = [avg2(a) | max2(a)] and at 1/4 resolution P4 = [avg4(a) | max4(a)]
+//    (2C channels each) in ONE read of x. Backward routes avg gradients uniformly and
+//    max gradients to the first maximal element of the window (row-major scan,
+//    torch CPU max_pool2d tie rule), recomputing the argmax from x.
+//  - MaxPool2d(2) between encoder levels (ACC_UNet.py:552,608-623), AvgPool2d(2)
+//    chain of MLFC (:361), nearest-upsample backward (block sums), channel concat /
+//    slice copies (decoder torch.cat, :639-648), ConvTranspose2d(2,2) pixel
+//    shuffle (:578-590), and generic 4-D permutes for weight / boundary layouts.
+#include "common.h"
+#include "kernels.h"
+
+// ---------------------------------------------------------------------------
+// pyramid forward: one thread per (low-res 4x4 cell or 2x2 cell, channel)
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+hanc_pyramid_fwd_kernel(const float* __restrict__ x, const float* __restrict__ sc,
+                        const float* __restrict__ sh, int act, int B, int H, int W, int C, int k,
+                        float* __restrict__ p2, float* __restrict__ p4) {
+  // k == 3: cell = 4x4 (one P4 pixel, four P2 pixels); k == 2: cell = 2x2 (one P2 pixel)
+  const int cs = (k == 3) ? 4 : 2;
+  const int Hc = H / cs, Wc = W / cs;
+  long total = (long)B * Hc * Wc * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    int c = (int)(i % C);
+    long cell = i / C;
+    int wc = (int)(cell % Wc);
+    long t = cell / Wc;
+    int hc = (int)(t % Hc);
+    int b = (int)(t / Hc);
+    float s = sc ? sc[c] : 1.f, h = sh ? sh[c] : 0.f;
+    const bool pro = sc != nullptr;
+    float v[4][4];
+#pragma unroll
+    for (int dy = 0; dy < 4; ++dy)
+#pragma unroll
+      for (int dx = 0; dx < 4; ++dx) {
+        if (dy < cs && dx < cs) {
+          float q = x[(((long)b * H + hc * cs + dy) * W + wc * cs + dx) * C + c];
+          v[dy][dx] = pro ? apply_act(q * s + h, act) : q;
+        }
+      }
+    const int H2 = H / 2, W2 = W / 2;
+    float s4 = 0.f, m4 = -INFINITY;
+    const int n2 = cs / 2;
+    for (int qy = 0; qy < n2; ++qy)
+      for (int qx = 0; qx < n2; ++qx) {
+        float a0 = v[2 * qy][2 * qx], a1 = v[2 * qy][2 * qx + 1];
+        float a2 = v[2 * qy + 1][2 * qx], a3 = v[2 * qy + 1][2 * qx + 1];
+        float sum = ((a0 + a1) + a2) + a3;  // torch CPU avg_pool2d summation order
+        float mx = fmaxf(fmaxf(a0, a1), fmaxf(a2, a3));
+        long o = (((long)b * H2 + hc * n2 + qy) * W2 + wc * n2 + qx) * (2 * C);
+        p2[o + c] = sum * 0.25f;
+        p2[o + C + c] = mx;
+      }
+    if (k == 3) {
+#pragma unroll
+      for (int dy = 0; dy < 4; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 4; ++dx) {
+          s4 += v[dy][dx];
+          m4 = fmaxf(m4, v[dy][dx]);
+        }
+      long o = (((long)b * Hc + hc) * Wc + wc) * (2 * C);
+      p4[o + c] = s4 * (1.f / 16.f);
+      p4[o + C + c] = m4;
+    }
+  }
+}
+
+// pyramid backward: da (+)= spread(dP2) + spread(dP4); accumulate into da
+__global__ void __launch_bounds__(256)
+hanc_pyramid_bwd_kernel(const float* __restrict__ x, const float* __restrict__ sc,
+                        const float* __restrict__ sh, int act, int B, int H, int W, int C, int k,
+                        const float* __restrict__ p2, const float* __restrict__ p4,
+                        const float* __restrict__ dp2, const float* __restrict__ dp4,
+                        float* __restrict__ da) {
+  const int cs = (k == 3) ? 4 : 2;
+  const int Hc = H / cs, Wc = W / cs;
+  long total = (long)B * Hc * Wc * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    int c = (int)(i % C);
+    long cell = i / C;
+    int wc = (int)(cell % Wc);
+    long t = cell / Wc;
+    int hc = (int)(t % Hc);
+    int b = (int)(t / Hc);
+    float s = sc ? sc[c] : 1.f, h = sh ? sh[c] : 0.f;
+    const bool pro = sc != nullptr;
+    float v[4][4], g[4][4];
+#pragma unroll
+    for (int dy = 0; dy < 4; ++dy)
+#pragma unroll
+      for (int dx = 0; dx < 4; ++dx) {
+        g[dy][dx] = 0.f;
+        if (dy < cs && dx < cs) {
+          float q = x[(((long)b * H + hc * cs + dy) * W + wc * cs + dx) * C + c];
+          v[dy][dx] = pro ? apply_act(q * s + h, act) : q;
+        }
+      }
+    const int H2 = H / 2, W2 = W / 2;
+    const int n2 = cs / 2;
+    for (int qy = 0; qy < n2; ++qy)
+      for (int qx = 0; qx < n2; ++qx) {
+        long o = (((long)b * H2 + hc * n2 + qy) * W2 + wc * n2 + qx) * (2 * C);
+        float gav = dp2[o + c] * 0.25f;
+        float gmx = dp2[o + C + c];
+        float mx = p2[o + C + c];
+        bool done = false;
+        for (int dy = 0; dy < 2; ++dy)
+          for (int dx = 0; dx < 2; ++dx) {
+            int yy = 2 * qy + dy, xx = 2 * qx + dx;
+            g[yy][xx] += gav;
+            if (!done && v[yy][xx] == mx) {
+              g[yy][xx] += gmx;
+              done = true;
+            }
+          }
+      }
+    if (k == 3) {
+      long o = (((long)b * Hc + hc) * Wc + wc) * (2 * C);
+      float gav = dp4[o + c] * (1.f / 16.f);
+      float gmx = dp4[o + C + c];
+      float mx = p4[o + C + c];
+      bool done = false;
+#pragma unroll
+      for (int dy = 0; dy < 4; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 4; ++dx) {
+          g[dy][dx] += gav;
+          if (!done && v[dy][dx] == mx) {
+            g[dy][dx] += gmx;
+            done = true;
+          }
+        }
+    }
+#pragma unroll
+    for (int dy = 0; dy < 4; ++dy)
+#pragma unroll
+      for (int dx = 0; dx < 4; ++dx)
+        if (dy < cs && dx < cs) da[(((long)b * H + hc * cs + dy) * W + wc * cs + dx) * C + c] += g[dy][dx];
+  }
+}
+
+static int grid_for(long total) {
+  long b = (total + 255) / 256;
+  if (b > 8192) b = 8192;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+extern "C" int accunet_hanc_pyramid_fwd(const float* x, const float* sc, const float* sh, int act,
+                                        int B, int H, int W, int C, int k, float* p2, float* p4,
+                                        void* stream) {
+  if (k < 2 || k > 3) return ACC_EBADARG;
+  int cs = (k == 3) ? 4 : 2;
+  if (H % cs || W % cs) return ACC_EBADSHAPE;
+  long total = (long)B * (H / cs) * (W / cs) * C;
+  hipLaunchKernelGGL(hanc_pyramid_fwd_kernel, dim3(grid_for(total)), dim3(256), 0,
+                     (hipStream_t)stream, x, sc, sh, act, B, H, W, C, k, p2, p4);
+  return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+}
+
+extern "C" int accunet_hanc_pyramid_bwd(const float* x, const float* sc, const float* sh, int act,
+                                        int B, int H, int W, int C, int k, const float* p2,
+                                        const float* p4, const float* dp2, const float* dp4,
+                                        float* da, void* stream) {
+  if (k < 2 || k > 3) return ACC_EBADARG;
+  int cs = (k == 3) ? 4 : 2;
+  long total = (long)B * (H / cs) * (W / cs) * C;
+  hipLaunchKernelGGL(hanc_pyramid_bwd_kernel, dim3(grid_for(total)), dim3(256), 0,
+                     (hipStream_t)stream, x, sc, sh, act, B, H, W, C, k, p2, p4, dp2, dp4, da);
+  return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+}
+
+// ---------------------------------------------------------------------------
+// 2x2 pooling (stride 2): mode 0 = max, 1 = avg. Backward recomputes argmax.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+pool2_fwd_kernel(const float* __restrict__ x, float* __restrict__ y, int B, int H, int W, int C,
+                 int mode) {
+  const int Ho = H / 2, Wo = W / 2;
+  long total = (long)B * Ho * Wo * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    int c = (int)(i % C);
+    long pix = i / C;
+    int wo = (int)(pix % Wo);
+    long t = pix / Wo;
+    int ho = (int)(t % Ho);
+    int b = (int)(t / Ho);
+    const float* p = x + (((long)b * H + 2 * ho) * W + 2 * wo) * C + c;
+    float a0 = p[0], a1 = p[C], a2 = p[(long)W * C], a3 = p[(long)W * C + C];
+    y[i] = mode == 0 ? fmaxf(fmaxf(a0, a1), fmaxf(a2, a3)) : (((a0 + a1) + a2) + a3) * 0.25f;
+  }
+}
+
+__global__ void __launch_bounds__(256)
+pool2_bwd_kernel(const float* __restrict__ x, const float* __restrict__ y,
+                 const float* __restrict__ dy, float* __restrict__ dx, int B, int H, int W, int C,
+                 int mode, int accumulate) {
+  const int Ho = H / 2, Wo = W / 2;
+  long total = (long)B * Ho * Wo * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    int c = (int)(i % C);
+    long pix = i / C;
+    int wo = (int)(pix % Wo);
+    long t = pix / Wo;
+    int ho = (int)(t % Ho);
+    int b = (int)(t / Ho);
+    long base = (((long)b * H + 2 * ho) * W + 2 * wo) * C + c;
+    long off[4] = {base, base + C, base + (long)W * C, base + (long)W * C + C};
+    float g = dy[i];
+    float gv[4];
+    if (mode == 0) {
+      float m = y[i];
+      bool done = false;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        gv[j] = 0.f;
+        if (!done && x[off[j]] == m) {
+          gv[j] = g;
+          done = true;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) gv[j] = 0.25f * g;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dx[off[j]] = accumulate ? dx[off[j]] + gv[j] : gv[j];
+  }
+}
+
+extern "C" int accunet_pool2_fwd(const float* x, float* y, int B, int H, int W, int C, int mode,
+                                 void* stream) {
+  if (H % 2 || W % 2) return ACC_EBADSHAPE;
+  long total = (long)B * (H / 2) * (W / 2) * C;
+  hipLaunchKernelGGL(pool2_fwd_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, x,
+                     y, B, H, W, C, mode);
+  return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+}
+
+extern "C" int accunet_pool2_bwd(const float* x, const float* y, const float* dy, float* dx, int B,
+                                 int H, int W, int C, int mode, int accumulate, void* stream) {
+  long total = (long)B * (H / 2) * (W / 2) * C;
+  hipLaunchKernelGGL(pool2_bwd_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, x,
+                     y, dy, dx, B, H, W, C, mode, accumulate);
+  return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+}
+
+// ---------------------------------------------------------------------------
+// Nearest-upsample backward: out[b,hs,ws,c] (+)= sum over the f x f block of
+// in[b, hs*f+dy, ws*f+dx, in_off + c] (in has ld_in channels per pixel).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+blocksum_kernel(const float* __restrict__ in, int ld_in, int in_off, float* __restrict__ out,
+                int ld_out, int B, int H, int W, int C, int f, int accumulate) {
+  const int Hs = H / f, Ws = W / f;
+  long total = (long)B * Hs * Ws * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    int c = (int)(i % C);
+    long pix = i / C;
+    int ws = (int)(pix % Ws);
+    long t = pix / Ws;
+    int hs = (int)(t % Hs);
+    int b = (int)(t / Hs);
+    float s = 0.f;
+    for (int dy = 0; dy < f; ++dy)
+      for (int dx = 0; dx < f; ++dx)
+        s += in[(((long)b * H + hs * f + dy) * W + ws * f + dx) * ld_in + in_off + c];
+    float* o = out + pix * ld_out + c;
+    *o = accumulate ? *o + s : s;
+  }
+}
+
+extern "C" int accunet_upsample_bwd(const float* in, int ld_in, int in_off, float* out, int ld_out,
+                                    int B, int H, int W, int C, int f, int accumulate,
+                                    void* stream) {
+  if (H % f || W % f) return ACC_EBADSHAPE;
+  long total = (long)B * (H / f) * (W / f) * C;
+  hipLaunchKernelGGL(blocksum_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, in,
+                     ld_in, in_off, out, ld_out, B, H, W, C, f, accumulate);
+  return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+}
+
+// ---------------------------------------------------------------------------
+// Strided channel-slice copy: dst[p, dst_off + c] (+)= src[p, src_off + c], c < C
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+slice_copy_kernel(const float* __restrict__ src, int ld_src, int src_off, float* __restrict__ dst,
+                  int ld_dst, int dst_off, long P, int C, int accumulate) {
+  long total = P * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    long p = i / C;
+    int c = (int)(i - p * C);
+    float v = src[p * ld_src + src_off + c];
+    float* d = dst + p * ld_dst + dst_off + c;
+    *d = accumulate ? *d + v : v;
+  }
+}
+
+extern "C" int accunet_slice_copy(const float* src, int ld_src, int src_off, float* dst,
+                                  int ld_dst, int dst_off, long P, int C, int accumulate,
+                                  void* stream) {
+  hipLaunchKernelGGL(slice_copy_kernel, dim3(grid_for(P * C)), dim3(256), 0, (hipStream_t)stream,
+                     src, ld_src, src_off, dst, ld_dst, dst_off, P, C, accumulate);
+  return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+}
+
+// ---------------------------------------------------------------------------
+// ConvTranspose2d(k=2,s=2) pixel shuffle. GEMM output T[b,i,j,(d*Cout+co)],
+// d = di*2+dj  ->  Y[b,2i+di,2j+dj,co] (+bias). Inverse for the backward.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+pixel_shuffle2_kernel(const float* __restrict__ t, const float* __restrict__ bias,
+                      float* __restrict__ y, int B, int Hi, int Wi, int Cout, int inverse) {
+  const int Ho = 2 * Hi, Wo = 2 * Wi;
+  long total = (long)B * Ho * Wo * Cout;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    int co = (int)(i % Cout);
+    long pix = i / Cout;
+    int wo = (int)(pix % Wo);
+    long q = pix / Wo;
+    int ho = (int)(q % Ho);
+    int b = (int)(q / Ho);
+    int d = (ho & 1) * 2 + (wo & 1);
+    long ti = (((long)b * Hi + (ho >> 1)) * Wi + (wo >> 1)) * (4 * Cout) + d * Cout + co;
+    if (!inverse) {
+      y[i] = t[ti] + (bias ? bias[co] : 0.f);
+    } else {
+      // here y is the gradient dY (input), t is dT (output)
+      const_cast<float*>(t)[ti] = y[i];
+    }
+  }
+}
+
+extern "C" int accunet_pixel_shuffle2(const float* t, const float* bias, float* y, int B, int Hi,
+                                      int Wi, int Cout, int inverse, void* stream) {
+  long total = (long)B * 4 * Hi * Wi * Cout;
+  hipLaunchKernelGGL(pixel_shuffle2_kernel, dim3(grid_for(total)), dim3(256), 0,
+                     (hipStream_t)stream, t, bias, y, B, Hi, Wi, Cout, inverse);
+  return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+}
+
+// ---------------------------------------------------------------------------
+// Generic 4-D permute: out[i0,i1,i2,i3] (out dims d) = in[...] with in strides
+// given per OUTPUT axis (so any permutation / flip is expressed by strides and
+// per-axis flip flags). accumulate adds into out.
+// ---------------------------------------------------------------------------
+struct Perm4 {
+  int d[4];
+  long s[4];
+  int flip[4];
+};
+
+__global__ void __launch_bounds__(256)
+permute4_kernel(const float* __restrict__ in, float* __restrict__ out, Perm4 p, int accumulate) {
+  long total = (long)p.d[0] * p.d[1] * p.d[2] * p.d[3];
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    long r = i;
+    long off = 0;
+    for (int a = 3; a >= 0; --a) {
+      int ia = (int)(r % p.d[a]);
+      r /= p.d[a];
+      if (p.flip[a]) ia = p.d[a] - 1 - ia;
+      off += ia * p.s[a];
+    }
+    out[i] = accumulate ? out[i] + in[off] : in[off];
+  }
+}
+
+extern "C" int accunet_permute4(const float* in, float* out, const int* dims, const long long* strides,
+                                const int* flips, int accumulate, void* stream) {
+  Perm4 p;
+  for (int a = 0; a < 4; ++a) {
+    p.d[a] = dims[a];
+    p.s[a] = strides[a];
+    p.flip[a] = flips ? flips[a] : 0;
+  }
+  long total = (long)p.d[0] * p.d[1] * p.d[2] * p.d[3];
+  hipLaunchKernelGGL(permute4_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, in,
+                     out, p, accumulate);
+  return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+}
+
+// ---------------------------------------------------------------------------
+// Grouped-column weight relayout for the channel-interleaved concats:
+//   HANCLayer: input channel c*J + j of hnc.cnv is branch j of channel c
+//   (ACC_UNet/ACC_UNet.py:96-106,138); MLFC merge: 2c = x_c, 2c+1 = x (:492)
+// out[n][jj][c] = W[n][c*J + order[jj]]   (inverse: scatter back, accumulate opt.)
+// ---------------------------------------------------------------------------
+struct JOrder {
+  int o[8];
+};
+
+__global__ void __launch_bounds__(256)
+group_relayout_kernel(const float* __restrict__ in, float* __restrict__ out, int N, int C, int J,
+                      JOrder ord, int inverse) {
+  long total = (long)N * J * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    int c = (int)(i % C);
+    long t = i / C;
+    int jj = (int)(t % J);
+    int n = (int)(t / J);
+    long src = (long)n * C * J + (long)c * J + ord.o[jj];
+    if (!inverse) out[i] = in[src];
+    else out[src] = in[i];
+  }
+}
+
+extern "C" int accunet_group_relayout(const float* in, float* out, int N, int C, int J,
+                                      const int* order, int inverse, void* stream) {
+  if (J < 1 || J > 8) return ACC_EBADARG;
+  JOrder o;
+  for (int j = 0; j < 8; ++j) o.o[j] = (order && j < J) ? order[j] : j;
+  long total = (long)N * J * C;
+  hipLaunchKernelGGL(group_relayout_kernel, dim3(grid_for(total)), dim3(256), 0,
+                     (hipStream_t)stream, in, out, N, C, J, o, inverse);
+  return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+}

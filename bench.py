@@ -1,0 +1,163 @@
+#!/usr/bin/env python3
+"""ACC-UNet training-throughput benchmark (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 16] [--size 256]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+One step = forward + WeightedDiceBCE(0.5, 0.5) + backward (+ RCCL bucketed
+all-reduce for N > 1) + Adam(lr 1e-3) step of the canonical ACC_UNet (16.77 M
+params, ACC_UNet/ACC_UNet.py) on a per-GPU batch of 16 x 3 x 256 x 256 fp32
+synthetic images resident in HBM (BASELINE configs[1]; configs[2] at N = 8).
+Rank 0 prints one JSON line; `value` = images/s over all ranks (weak scaling).
+
+Extra objects on the line:
+  roofline     — the HANC depthwise stage (K1, `dw3x3_fwd` of cnv12, B x 96 x 256^2)
+                 and the other tracked kernels timed live with HIP events on the
+                 stream they run on; algorithmic bytes / average launch time vs the
+                 8 TB/s HBM3E peak;
+  cpu_baseline — the CPU oracle (oracle/accunet_oracle.py, plain PyTorch-CPU, same op
+                 sequence as the reference) timed on this host on a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "acc-unet-unext_amd"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "images/sec fwd+bwd, ACC-UNet 3×256×256 bs=16/GPU, 1→8 MI355X"
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--variant", default="canonical")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=1, help="images in the CPU sample")
+    return ap.parse_args()
+
+
+def cpu_baseline(variant, size, n_img):
+    """Time the CPU oracle (fwd + loss + bwd) on n_img images of the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import accunet_oracle as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
+    torch.set_num_threads(threads)
+    spec = O.param_spec(variant, 3, 1, 32)
+    sd = O.det_state_dict(spec, seed=0)
+    params = [v.requires_grad_(True) for k, v in sd.items()
+              if not k.endswith(("running_mean", "running_var", "num_batches_tracked"))]
+    x = O.det_input((n_img, 3, size, size), "bench-cpu-x")
+    m = O.det_mask((n_img, 1, size, size), "bench-cpu-mask", p=0.3)
+    t0 = time.perf_counter()
+    out = O.forward(sd, x, variant, training=True)
+    loss = O.dice_bce_loss(out, m)
+    loss.backward()
+    dt = time.perf_counter() - t0
+    del params
+    cpu = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": n_img / dt, "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{n_img} image(s) {variant} 3x{size}x{size} fwd+loss+bwd (no optimizer), "
+                      f"fp32, torch-CPU oracle, {dt:.1f} s", "cpu_model": cpu}
+
+
+def main():
+    args = parse()
+    from accunet import dist as adist
+    from accunet import model as M
+    from accunet import profile as prof
+    from accunet.train import TrainStep
+
+    rank, world = adist.init_from_env()
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    torch.manual_seed(0)
+    model = M.VARIANTS[args.variant](3, 1, n_filts=32).to(dev).train()
+    reducer = adist.GradBucketReducer(model) if world > 1 else None
+    step = TrainStep(model, lr=1e-3, reducer=reducer)
+
+    g = torch.Generator(device="cpu").manual_seed(1000 + rank)
+    B, S = args.batch, args.size
+    x = torch.randn(B, 3, S, S, generator=g).to(dev)
+    mask = (torch.rand(B, 1, S, S, generator=g) < 0.3).float().to(dev)
+
+    for _ in range(args.warmup):
+        step(x, mask)
+    torch.cuda.synchronize()
+
+    prof.enable(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step(x, mask)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    prof.enable(False)
+    dt = t1 - t0
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    imgs = B * world * args.steps
+    line = {
+        "metric": METRIC,
+        "value": imgs / dt,
+        "unit": "images/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1000.0 * dt / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (x ~ N(0,1), mask ~ Bernoulli(0.3), per-rank seed 1000+rank); "
+                "torch.manual_seed(0) default init",
+        "config": {"workload": f"ACC_UNet {args.variant} fwd+WeightedDiceBCE+bwd+Adam, "
+                               f"{B}x3x{S}x{S} per GPU",
+                   "model": "ACC_UNet (16.77M)" if args.variant == "canonical" else args.variant,
+                   "global_batch": B * world, "per_gpu_batch": B, "image": [3, S, S],
+                   "parallelism": f"dp{world}"},
+        "final_loss": float(loss.item()),
+    }
+    rl = prof.rooflines(HBM_PEAK_GBS)
+    if rl:
+        line["roofline"] = rl[0]
+        line["rooflines"] = rl
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(args.variant, S, args.cpu_sample)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

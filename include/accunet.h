@@ -93,6 +93,122 @@ int accunet_colsum(const float* x, long P, int C, float* out, float* ws, size_t 
                    void* stream);
 int accunet_reduce_stats(const float* part, int R, int C, float* out2C, float* ws, void* stream);
 
+/* ------------------------------------------------------------------------- *
+ * HANCBlock.conv2 — depthwise 3x3 (+bias), pad 1, groups = C
+ * (ACC_UNet/ACC_UNet.py:240-247, forward :273). Input may carry a pending
+ * BatchNorm+LeakyReLU (sc/sh/act, norm1 :236) applied on load; `stats` receives
+ * per-block (sum, sumsq) of z for norm2. flip=1 runs the kernel with W[c][8-tap]
+ * (the data gradient). wgrad writes dW [C][1][3][3] and db [C].
+ * ------------------------------------------------------------------------- */
+int accunet_dw3x3_rows(int B, int H, int W, int C);
+int accunet_dw3x3_fwd(const float* x, const float* wt, const float* bias, const float* sc,
+                      const float* sh, int act, int flip, float* z, float* stats, int B, int H,
+                      int W, int C, void* stream);
+size_t accunet_dw3x3_wgrad_ws(int B, int H, int W, int C);
+int accunet_dw3x3_wgrad(const float* x, const float* dz, const float* sc, const float* sh,
+                        int act, float* dw, float* db, int B, int H, int W, int C, float* ws,
+                        size_t ws_elems, void* stream);
+
+/* ------------------------------------------------------------------------- *
+ * HANCLayer neighbourhood pyramid (ACC_UNet/ACC_UNet.py:86-106): from
+ * a = act(x*sc+sh): P2 = [avg2 a | max2 a] at H/2, P4 = [avg4 a | max4 a] at H/4
+ * (k = 3) in one read. Backward accumulates into da (max: first max in window).
+ * ------------------------------------------------------------------------- */
+int accunet_hanc_pyramid_fwd(const float* x, const float* sc, const float* sh, int act, int B,
+                             int H, int W, int C, int k, float* p2, float* p4, void* stream);
+int accunet_hanc_pyramid_bwd(const float* x, const float* sc, const float* sh, int act, int B,
+                             int H, int W, int C, int k, const float* p2, const float* p4,
+                             const float* dp2, const float* dp4, float* da, void* stream);
+/* HANCLayer / MLFC-merge channel interleave (ACC_UNet.py:138, :492):
+ * out[n][jj][c] = W[n][c*J + order[jj]]  (inverse scatters back) */
+int accunet_group_relayout(const float* in, float* out, int N, int C, int J, const int* order,
+                           int inverse, void* stream);
+
+/* ------------------------------------------------------------------------- *
+ * Resampling / layout: MaxPool2d(2) (ACC_UNet.py:552), AvgPool2d(2) (MLFC :361),
+ * nearest Upsample backward (block sums, :360), channel concat slices
+ * (torch.cat dim=1, :639-648), ConvTranspose2d(2,2,s2) pixel shuffle (:578-590),
+ * generic 4-D permute (weights, NCHW<->NHWC at the module boundary).
+ * mode: 0 = max, 1 = avg.
+ * ------------------------------------------------------------------------- */
+int accunet_pool2_fwd(const float* x, float* y, int B, int H, int W, int C, int mode,
+                      void* stream);
+int accunet_pool2_bwd(const float* x, const float* y, const float* dy, float* dx, int B, int H,
+                      int W, int C, int mode, int accumulate, void* stream);
+int accunet_upsample_bwd(const float* in, int ld_in, int in_off, float* out, int ld_out, int B,
+                         int H, int W, int C, int f, int accumulate, void* stream);
+int accunet_slice_copy(const float* src, int ld_src, int src_off, float* dst, int ld_dst,
+                       int dst_off, long P, int C, int accumulate, void* stream);
+int accunet_pixel_shuffle2(const float* t, const float* bias, float* y, int B, int Hi, int Wi,
+                           int Cout, int inverse, void* stream);
+int accunet_permute4(const float* in, float* out, const int* dims, const long long* strides,
+                     const int* flips, int accumulate, void* stream);
+
+/* ------------------------------------------------------------------------- *
+ * ChannelSELayer (ACC_UNet/ACC_UNet.py:9-49) fused with the BatchNorm(+LReLU)
+ * that precedes it (sc/sh/act) and its own BN + LeakyReLU; the BN statistics of
+ * a*s are derived from per-(b,c) sums, so the input is read twice and the output
+ * written once. `save` (accunet_se_save_elems) holds the forward state for
+ * accunet_se_bwd, which returns da (gradient w.r.t. the SE input a) and the fc /
+ * BN parameter gradients. ostats (optional) = statistics of the output.
+ * ------------------------------------------------------------------------- */
+size_t accunet_se_save_elems(int B, int C, int Cr);
+size_t accunet_se_ws_elems(int B, int HW, int C, int Cr);
+int accunet_se_stats_rows(int B, int HW, int C);
+int accunet_se_fwd(const float* z, const float* sc, const float* sh, int act, int B, int HW,
+                   int C, int Cr, const float* w1, const float* b1, const float* w2,
+                   const float* b2, const float* gamma, const float* beta, float* rmean,
+                   float* rvar, long long* nbt, float momentum, float eps, int training,
+                   float* out, float* save, float* ostats, float* ws, size_t ws_elems,
+                   void* stream);
+int accunet_se_bwd(const float* z, const float* dout, const float* sc, const float* sh, int act,
+                   int B, int HW, int C, int Cr, const float* w1, const float* w2,
+                   const float* gamma, int training, const float* save, float* da, float* dw1,
+                   float* db1, float* dw2, float* db2, float* dgamma, float* dbeta, float* ws,
+                   size_t ws_elems, void* stream);
+
+/* ------------------------------------------------------------------------- *
+ * Head: out 1x1 conv n_filts -> 1 (+ Sigmoid when sigm) (ACC_UNet.py:594-599,653-659)
+ * ------------------------------------------------------------------------- */
+int accunet_head_fwd(const float* x, const float* w, const float* b, int sigm, float* y, long P,
+                     int C, void* stream);
+size_t accunet_head_ws_elems(long P, int C);
+int accunet_head_bwd(const float* x, const float* w, const float* y, const float* dy, int sigm,
+                     float* dx, float* dw, float* db, long P, int C, float* ws, size_t ws_elems,
+                     void* stream);
+
+/* ------------------------------------------------------------------------- *
+ * WeightedDiceBCE (Experiments/utils.py:140-171; WeightedBCE :21-74 with the
+ * truth.max() > 1 binarisation, WeightedDiceLoss :109-138), weights [0.5, 0.5].
+ * res (device, 8 + 2B floats): [loss, dice, bce, pos_w, neg_w, binarised, -, -, (I,U)/b]
+ * ------------------------------------------------------------------------- */
+size_t accunet_loss_ws_elems(int B);
+int accunet_loss_fwd(const float* x, const float* t, int B, long N, float dice_w, float bce_w,
+                     float* res, float* ws, size_t ws_elems, void* stream);
+int accunet_loss_bwd(const float* x, const float* t, int B, long N, float dice_w, float bce_w,
+                     const float* res, const float* gout, float* dx, void* stream);
+
+/* ------------------------------------------------------------------------- *
+ * Adam (torch.optim.Adam as used at Experiments/train_model.py:647) over every
+ * parameter in one launch. table: device array of {float* p; const float* g;
+ * float* m; float* v; long long n;}; chunk_t / chunk_s map each block to
+ * (tensor, first element), accunet_adam_chunk_elems() elements per chunk.
+ * ------------------------------------------------------------------------- */
+int accunet_adam_chunk_elems(void);
+int accunet_adam_step(const void* table, const int* chunk_t, const long long* chunk_s,
+                      int nchunks, float lr, float b1, float b2, float eps, float wd, int step,
+                      void* stream);
+
+/* ------------------------------------------------------------------------- *
+ * ACC_UNet_W learnable merge y = a*w + b*(1-w) (ACC_UNet/ACC_UNet_w.py:497-522)
+ * ------------------------------------------------------------------------- */
+int accunet_wmerge_fwd(const float* a, const float* b, const float* w, float* y, long P, int C,
+                       float* stats, void* stream);
+int accunet_wmerge_bwd(const float* g, const float* w, float* da, float* db, long n,
+                       void* stream);
+int accunet_dotdiff(const float* g, const float* a, const float* b, long n, float* out,
+                    int accumulate, float* ws, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

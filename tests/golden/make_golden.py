@@ -73,13 +73,20 @@ def main():
     U = ref_utils()
     meta = {}
 
-    # 1) state_dict key/shape lists at the default size (n_filts=32, n_channels=3)
+    # 1) state_dict key/shape lists at the default size (n_filts=32, n_channels=3) and a
+    #    digest of the seeded default initialisation (torch.manual_seed(0); cls(3, 1))
+    import hashlib
     for v, cls in models.items():
+        torch.manual_seed(0)
         m = cls(3, 1)
         keys = [[k, list(t.shape)] for k, t in m.state_dict().items()]
         nparams = sum(p.numel() for p in m.parameters())
+        h = hashlib.sha256()
+        for k, t in m.state_dict().items():
+            h.update(t.detach().contiguous().numpy().tobytes())
         with open(os.path.join(HERE, f"keys_{v}.json"), "w") as f:
-            json.dump({"n_params": nparams, "keys": keys}, f)
+            json.dump({"n_params": nparams, "keys": keys, "init_sha256_seed0": h.hexdigest(),
+                       "torch": torch.__version__}, f)
         meta[f"n_params_{v}"] = nparams
         print(v, nparams, len(keys))
 
