@@ -39,7 +39,7 @@ class AccGemmDesc(Structure):
         ("up", c_void_p * 3),
         ("upld", c_int * 3),
         ("uplog", c_int * 3),
-        ("stats", c_void_p),
+        ("stats", c_void_p),  # double*
         ("allow_split", c_int),
     ]
 
@@ -59,6 +59,7 @@ _SIGS = {
     "accunet_stream_rows": [L, I],
     "accunet_bn_finalize": [P, I, I, D, P, P, P, P, P, F, F, I, P, P, P],
     "accunet_affine_act_fwd": [P, P, P, I, P, P, L, I, P, IP, P],
+    "accunet_bn_bwd_ws_elems": [L, I],
     "accunet_bn_bwd": [P, P, P, P, I, I, L, I, P, I, P, P, P, IP, P, S, P],
     "accunet_colsum": [P, L, I, P, P, S, P],
     "accunet_reduce_stats": [P, I, I, P, P, P],
@@ -93,7 +94,7 @@ _SIGS = {
     "accunet_wmerge_bwd": [P, P, P, P, L, P],
 }
 # entry points returning a size/count rather than a status
-_SIZE_FNS = {"accunet_dw3x3_wgrad_ws", "accunet_se_save_elems", "accunet_se_ws_elems",
+_SIZE_FNS = {"accunet_bn_bwd_ws_elems", "accunet_dw3x3_wgrad_ws", "accunet_se_save_elems", "accunet_se_ws_elems",
              "accunet_head_ws_elems", "accunet_loss_ws_elems"}
 
 _lib = None

@@ -32,12 +32,12 @@ def _check(t: torch.Tensor, name: str):
         raise _lib.AccError(f"{name}: expected float32, got {t.dtype}")
 
 
-def workspace(n_elems: int, device) -> torch.Tensor:
-    return torch.empty(max(int(n_elems), 1), dtype=torch.float32, device=device)
+def workspace(n_elems: int, device, dtype=torch.float32) -> torch.Tensor:
+    return torch.empty(max(int(n_elems), 1), dtype=dtype, device=device)
 
 
 def stats_buffer(rows: int, C: int, device) -> torch.Tensor:
-    return torch.empty(rows, 2, C, dtype=torch.float32, device=device)
+    return torch.empty(rows, 2, C, dtype=torch.float64, device=device)
 
 
 def gemm(M: int, N: int, K: int, *, a: Sequence[torch.Tensor], lda: Sequence[int],
@@ -87,6 +87,8 @@ def gemm(M: int, N: int, K: int, *, a: Sequence[torch.Tensor], lda: Sequence[int
         d.up[i] = t.data_ptr() + 4 * int(off)
         d.upld[i] = int(ld)
         d.uplog[i] = int(lg)
+    if stats is not None and stats.dtype != torch.float64:
+        raise _lib.AccError("gemm.stats: fp64 partial-statistics buffer expected")
     d.stats = stats.data_ptr() if stats is not None else None
     d.allow_split = 1 if allow_split else 0
     ws = None
@@ -116,7 +118,7 @@ def partial_ws_elems(R: int, Wd: int) -> int:
 def bn_finalize(part: Optional[torch.Tensor], R: int, C: int, count: float, gamma, beta,
                 rmean, rvar, nbt, momentum: float, eps: float, training: bool,
                 st: torch.Tensor):
-    ws = workspace(partial_ws_elems(R, 2 * C), st.device) if training else None
+    ws = workspace(partial_ws_elems(R, 2 * C), st.device, torch.float64) if training else None
     call("accunet_bn_finalize", _p(part), int(R), int(C), float(count), _p(gamma), _p(beta),
          _p(rmean), _p(rvar), _p(nbt), float(momentum), float(eps), 1 if training else 0,
          _p(st), _p(ws), _stream())
@@ -133,8 +135,7 @@ def affine_act(x: torch.Tensor, sc, sh, act: int, res, y: torch.Tensor, P: int, 
 
 def bn_bwd(x, dy, st, gamma, act: int, training: bool, P: int, C: int, dx, accumulate: bool,
            dgamma, dbeta, colsum=None):
-    nb = stream_rows(P, C)
-    ws_elems = nb * 2 * C + 3 * C + partial_ws_elems(nb, 2 * C)
+    ws_elems = int(_lib.load().accunet_bn_bwd_ws_elems(int(P), int(C)))
     ws = workspace(ws_elems, x.device)
     rows = ctypes.c_int(0)
     call("accunet_bn_bwd", _p(x), _p(dy), _p(st), _p(gamma), int(act), 1 if training else 0,
@@ -146,13 +147,13 @@ def bn_bwd(x, dy, st, gamma, act: int, training: bool, P: int, C: int, dx, accum
 def colsum(x, P: int, C: int, out):
     nb = stream_rows(P, C)
     ws_elems = nb * 2 * C + partial_ws_elems(nb, 2 * C)
-    ws = workspace(ws_elems, x.device)
+    ws = workspace(ws_elems, x.device, torch.float64)
     call("accunet_colsum", _p(x), int(P), int(C), _p(out), _p(ws), ws_elems, _stream())
     return ws
 
 
 def reduce_stats(part, R: int, C: int, out2C):
-    ws = workspace(partial_ws_elems(R, 2 * C), part.device)
+    ws = workspace(partial_ws_elems(R, 2 * C), part.device, torch.float64)
     call("accunet_reduce_stats", _p(part), int(R), int(C), _p(out2C), _p(ws), _stream())
     return ws
 

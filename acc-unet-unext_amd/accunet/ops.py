@@ -32,6 +32,11 @@ def _empty(shape, like):
     return torch.empty(shape, dtype=torch.float32, device=like.device)
 
 
+def _stats(shape, like):
+    """fp64 partial-statistics block [rows, 2, C] (see include/accunet.h)."""
+    return torch.empty(shape, dtype=torch.float64, device=like.device)
+
+
 def _flat_off(t: torch.Tensor, off: int) -> torch.Tensor:
     """1-D view of t starting `off` elements in (pointer offset for kernels)."""
     f = t.view(-1)
@@ -155,7 +160,7 @@ class _PWConvFn(torch.autograd.Function):
         rows = 0
         if cfg.want_stats:
             rows = kern.gemm_stats_rows(P, N)
-            stats = _empty((rows, 2, N), weight)
+            stats = _stats((rows, 2, N), weight)
         pro = cfg.pro
         kern.gemm(P, N, K, a=list(srcs), lda=cfg.src_ch, kbeg=kbeg, b=weight, ldb=cfg.w_ld,
                   b_offset=cfg.w_off, c=Z, ldc=N, bias=bias if cfg.has_bias else None,
@@ -274,7 +279,7 @@ class _DWConvFn(torch.autograd.Function):
         Z = _empty((B, H, W, C), z)
         stats = None
         if cfg.want_stats:
-            stats = _empty((kern.dw3x3_rows(B, H, W, C), 2, C), z)
+            stats = _stats((kern.dw3x3_rows(B, H, W, C), 2, C), z)
         pro = cfg.pro
         with _prof.region(f"dw3x3_fwd B{B} {H}x{W} C{C}", kernel="dw3x3_fwd_kernel",
                           shape=f"{B}x{H}x{W}x{C}", bytes_alg=2.0 * 4 * B * H * W * C):
@@ -369,7 +374,7 @@ class _HancLayerFn(torch.autograd.Function):
         Z = _empty((B, H, W, N), z)
         stats = None
         if cfg.want_stats:
-            stats = _empty((kern.gemm_stats_rows(P, N), 2, N), z)
+            stats = _stats((kern.gemm_stats_rows(P, N), 2, N), z)
         with _prof.region(f"hanc_gemm P{P} N{N} K{C}", kernel="gemm_f32_kernel (HANC x-branch)",
                           shape=f"M{P} N{N} K{C}", flops=2.0 * P * N * C):
             kern.gemm(P, N, C, a=[z], lda=[C], b=Wp, ldb=J * C, c=Z, ldc=N, bias=bias,
@@ -472,7 +477,7 @@ class _BnActAddFn(torch.autograd.Function):
         C = z.shape[-1]
         P = z.numel() // C
         y = torch.empty_like(z)
-        stats = _empty((kern.stream_rows(P, C), 2, C), z) if cfg.want_stats else None
+        stats = _stats((kern.stream_rows(P, C), 2, C), z) if cfg.want_stats else None
         pro = cfg.pro
         kern.affine_act(z, pro.st[2] if pro.active else None, pro.st[3] if pro.active else None,
                         pro.act if pro.active else ACT_NONE, res if cfg.has_res else None, y, P,
@@ -529,7 +534,7 @@ class _SEFn(torch.autograd.Function):
         B, HW, C, Cr = cfg.B, cfg.HW, cfg.C, cfg.Cr
         pro = cfg.pro
         out = torch.empty_like(z)
-        ostats = _empty((kern.se_stats_rows(B, HW, C), 2, C), z) if cfg.want_stats else None
+        ostats = _stats((kern.se_stats_rows(B, HW, C), 2, C), z) if cfg.want_stats else None
         save = _empty((kern.se_save_elems(B, C, Cr),), z)
         bn = cfg.bn
         mom = bn.momentum if bn.momentum is not None else 0.1
@@ -613,7 +618,7 @@ class _Conv3x3Fn(torch.autograd.Function):
         Wr = _empty((Co, 9 * Ci), x)  # [co][tap][ci]
         kern.permute4(weight, Wr, (Co, 3, 3, Ci), (9 * Ci, 3, 1, 9))
         Z = _empty((B, H, W, Co), x)
-        stats = _empty((kern.gemm_stats_rows(P, Co), 2, Co), x) if cfg.want_stats else None
+        stats = _stats((kern.gemm_stats_rows(P, Co), 2, Co), x) if cfg.want_stats else None
         kern.gemm(P, Co, 9 * Ci, a=[x], lda=[Ci], amode=AMODE_SHIFT3, b=Wr, ldb=9 * Ci, c=Z,
                   ldc=Co, bias=bias, H=H, W=W, cin=Ci, stats=stats)
         ctx.cfg = cfg
@@ -812,7 +817,7 @@ class _WMergeFn(torch.autograd.Function):
         C = a.shape[-1]
         P = a.numel() // C
         y = torch.empty_like(a)
-        stats = _empty((kern.stream_rows(P, C), 2, C), a) if want_stats else None
+        stats = _stats((kern.stream_rows(P, C), 2, C), a) if want_stats else None
         kern.wmerge_fwd(a, b, w, y, P, C, stats)
         ctx.save_for_backward(a, b, w)
         if stats is None:

@@ -28,18 +28,34 @@ sum_rows_kernel(const float* __restrict__ part, int R, int stride, int ncols,
   if (g == 0 && c < ncols) out[c] = (float)(red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl]);
 }
 
+template <typename TOUT>
+__global__ void __launch_bounds__(256)
+sum_rows_d_kernel(const double* __restrict__ part, int R, int stride, int ncols,
+                  TOUT* __restrict__ out) {
+  __shared__ double red[4][64];
+  int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
+  int c = blockIdx.x * 64 + cl;
+  double s1 = 0.0;
+  if (c < ncols)
+    for (int r = g; r < R; r += 4) s1 += part[(long)r * stride + c];
+  red[g][cl] = s1;
+  __syncthreads();
+  if (g == 0 && c < ncols) out[c] = (TOUT)(red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl]);
+}
+
 // ---------------------------------------------------------------------------
 // colreduce: out[r/RB][w] = sum of in[r][w] over RB consecutive rows (stage 1 of
 // the partial-statistics reduction when there are many partial rows).
 // ---------------------------------------------------------------------------
+template <typename T>
 __global__ void __launch_bounds__(256)
-colreduce_kernel(const float* __restrict__ in, float* __restrict__ out, int R, int Wd, int RB) {
-  __shared__ float red[4][64];
+colreduce_kernel(const T* __restrict__ in, T* __restrict__ out, int R, int Wd, int RB) {
+  __shared__ T red[4][64];
   int c = blockIdx.y * 64 + (threadIdx.x & 63);
   int g = threadIdx.x >> 6;
   int r0 = blockIdx.x * RB;
   int r1 = min(R, r0 + RB);
-  float s = 0.f;
+  T s = 0;
   if (c < Wd)
     for (int r = r0 + g; r < r1; r += 4) s += in[(long)r * Wd + c];
   red[g][threadIdx.x & 63] = s;
@@ -49,16 +65,16 @@ colreduce_kernel(const float* __restrict__ in, float* __restrict__ out, int R, i
 }
 
 // Reduce [R][Wd] partial rows into at most 64 rows using ws; returns pointer+rows.
-const float* reduce_partials(const float* part, int R, int Wd, float* ws, int* Rout,
-                                    hipStream_t s) {
-  const float* cur = part;
+template <typename T>
+const T* reduce_partials_t(const T* part, int R, int Wd, T* ws, int* Rout, hipStream_t s) {
+  const T* cur = part;
   int rows = R;
-  float* bufs[2] = {ws, ws + (size_t)ceil_div(R, 256) * Wd};
+  T* bufs[2] = {ws, ws + (size_t)ceil_div(R, 256) * Wd};
   int which = 0;
   while (rows > 64) {
     int RB = 256;
     int nb = ceil_div(rows, RB);
-    hipLaunchKernelGGL(colreduce_kernel, dim3(nb, ceil_div(Wd, 64)), dim3(256), 0, s, cur,
+    hipLaunchKernelGGL(colreduce_kernel<T>, dim3(nb, ceil_div(Wd, 64)), dim3(256), 0, s, cur,
                        bufs[which], rows, Wd, RB);
     cur = bufs[which];
     which ^= 1;
@@ -66,6 +82,11 @@ const float* reduce_partials(const float* part, int R, int Wd, float* ws, int* R
   }
   *Rout = rows;
   return cur;
+}
+
+const float* reduce_partials(const float* part, int R, int Wd, float* ws, int* Rout,
+                             hipStream_t s) {
+  return reduce_partials_t<float>(part, R, Wd, ws, Rout, s);
 }
 
 size_t accunet_partials_ws_elems(int R, int Wd) {
@@ -77,7 +98,7 @@ size_t accunet_partials_ws_elems(int R, int Wd) {
 // statistics update (training) or running-stat normalisation (eval).
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256)
-bn_finalize_kernel(const float* __restrict__ part, int R, int C, double count,
+bn_finalize_kernel(const double* __restrict__ part, int R, int C, double count,
                    const float* __restrict__ gamma, const float* __restrict__ beta,
                    float* __restrict__ rmean, float* __restrict__ rvar, float momentum, float eps,
                    int training, float* __restrict__ st) {
@@ -87,8 +108,8 @@ bn_finalize_kernel(const float* __restrict__ part, int R, int C, double count,
   double s1 = 0.0, s2 = 0.0;
   if (training && c < C) {
     for (int r = g; r < R; r += 4) {
-      s1 += (double)part[(long)r * 2 * C + c];
-      s2 += (double)part[(long)r * 2 * C + C + c];
+      s1 += part[(long)r * 2 * C + c];
+      s2 += part[(long)r * 2 * C + C + c];
     }
   }
   red[0][g][cl] = s1;
@@ -123,15 +144,15 @@ bn_finalize_kernel(const float* __restrict__ part, int R, int C, double count,
   st[BN_SHIFT * C + c] = be - mean * sc;
 }
 
-extern "C" int accunet_bn_finalize(const float* part, int R, int C, double count,
+extern "C" int accunet_bn_finalize(const double* part, int R, int C, double count,
                                    const float* gamma, const float* beta, float* rmean,
                                    float* rvar, long long* nbt, float momentum, float eps,
-                                   int training, float* st, float* ws, void* stream_) {
+                                   int training, float* st, double* ws, void* stream_) {
   hipStream_t s = (hipStream_t)stream_;
   if (C <= 0) return ACC_EBADSHAPE;
   int rows = R;
-  const float* p = part;
-  if (training) p = reduce_partials(part, R, 2 * C, ws, &rows, s);
+  const double* p = part;
+  if (training) p = reduce_partials_t<double>(part, R, 2 * C, ws, &rows, s);
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(C, 64)), dim3(256), 0, s, p, rows, C,
                      count, gamma, beta, rmean, rvar, momentum, eps, training, st);
   if (training && nbt) {
@@ -149,13 +170,13 @@ template <int V>
 __global__ void __launch_bounds__(256)
 affine_act_kernel(const float* __restrict__ x, const float* __restrict__ sc,
                   const float* __restrict__ sh, int act, const float* __restrict__ res,
-                  float* __restrict__ y, long P, int C, float* __restrict__ stats) {
+                  float* __restrict__ y, long P, int C, double* __restrict__ stats) {
   ChanTile t = chan_tile<V>(C);
   long rows_per = (P + gridDim.x - 1) / gridDim.x;
   long r0 = blockIdx.x * rows_per, r1 = min(P, r0 + rows_per);
-  float a[V], b[V];
+  double a[V], b[V];
 #pragma unroll
-  for (int j = 0; j < V; ++j) { a[j] = 0.f; b[j] = 0.f; }
+  for (int j = 0; j < V; ++j) { a[j] = 0.0; b[j] = 0.0; }
   if (t.active) {
     float s[V], h[V];
 #pragma unroll
@@ -177,7 +198,7 @@ affine_act_kernel(const float* __restrict__ x, const float* __restrict__ sc,
       }
       if (y) stv<V>(y + off, v);  // y == nullptr: statistics only (accunet_colsum)
 #pragma unroll
-      for (int j = 0; j < V; ++j) { a[j] += v[j]; b[j] += v[j] * v[j]; }
+      for (int j = 0; j < V; ++j) { a[j] += v[j]; b[j] += (double)v[j] * v[j]; }
     }
   }
   if (stats) block_chan_reduce2<V>(t, a, b, stats, blockIdx.x, C);
@@ -193,7 +214,7 @@ int stream_rowblocks(long P, int C) {
 }
 
 extern "C" int accunet_affine_act_fwd(const float* x, const float* sc, const float* sh, int act,
-                                      const float* res, float* y, long P, int C, float* stats,
+                                      const float* res, float* y, long P, int C, double* stats,
                                       int* stats_rows, void* stream_) {
   hipStream_t s = (hipStream_t)stream_;
   int V = (C % 4 == 0) ? 4 : 1;
@@ -223,13 +244,14 @@ template <int V>
 __global__ void __launch_bounds__(256)
 bn_bwd_reduce_kernel(const float* __restrict__ x, const float* __restrict__ dy,
                      const float* __restrict__ st, int act, long P, int C,
-                     float* __restrict__ part) {
+                     double* __restrict__ part) {
+  // fp64 accumulation, as ATen's CPU batch_norm backward (acc_type<float> = double)
   ChanTile t = chan_tile<V>(C);
   long rows_per = (P + gridDim.x - 1) / gridDim.x;
   long r0 = blockIdx.x * rows_per, r1 = min(P, r0 + rows_per);
-  float a[V], b[V];
+  double a[V], b[V];
 #pragma unroll
-  for (int j = 0; j < V; ++j) { a[j] = 0.f; b[j] = 0.f; }
+  for (int j = 0; j < V; ++j) { a[j] = 0.0; b[j] = 0.0; }
   if (t.active) {
     float mu[V], rs[V], s[V], h[V];
 #pragma unroll
@@ -249,7 +271,7 @@ bn_bwd_reduce_kernel(const float* __restrict__ x, const float* __restrict__ dy,
         float g = dv[j];
         if (act == ACT_LRELU) g *= lrelu_d(xv[j] * s[j] + h[j]);
         a[j] += g;
-        b[j] += g * (xv[j] - mu[j]) * rs[j];
+        b[j] += (double)g * ((double)xv[j] - mu[j]) * rs[j];
       }
     }
   }
@@ -257,7 +279,7 @@ bn_bwd_reduce_kernel(const float* __restrict__ x, const float* __restrict__ dy,
 }
 
 __global__ void __launch_bounds__(256)
-bn_bwd_finalize_kernel(const float* __restrict__ part, int R, int C, double count,
+bn_bwd_finalize_kernel(const double* __restrict__ part, int R, int C, double count,
                        const float* __restrict__ st, const float* __restrict__ gamma,
                        int training, float* __restrict__ dgamma, float* __restrict__ dbeta,
                        float* __restrict__ coef) {
@@ -267,8 +289,8 @@ bn_bwd_finalize_kernel(const float* __restrict__ part, int R, int C, double coun
   double s1 = 0.0, s2 = 0.0;
   if (c < C)
     for (int r = g; r < R; r += 4) {
-      s1 += (double)part[(long)r * 2 * C + c];
-      s2 += (double)part[(long)r * 2 * C + C + c];
+      s1 += part[(long)r * 2 * C + c];
+      s2 += part[(long)r * 2 * C + C + c];
     }
   red[0][g][cl] = s1;
   red[1][g][cl] = s2;
@@ -283,10 +305,12 @@ bn_bwd_finalize_kernel(const float* __restrict__ part, int R, int C, double coun
   float mean = st[BN_MEAN * C + c];
   float k1 = ga * rstd;
   float k2 = 0.f, k3 = 0.f;
+  (void)mean;
   if (training) {
+    // dx = k1*(g - mean(g) - xhat*mean(g*xhat)) = k1*g + k2*(x - mean) + k3
     float mg = (float)(s1 / count), mgx = (float)(s2 / count);
     k2 = -k1 * rstd * mgx;
-    k3 = -k1 * mg + k1 * mean * rstd * mgx;
+    k3 = -k1 * mg;
   }
   coef[c] = k1;
   coef[C + c] = k2;
@@ -306,9 +330,10 @@ bn_bwd_apply_kernel(const float* __restrict__ x, const float* __restrict__ dy,
 #pragma unroll
   for (int j = 0; j < V; ++j) { a[j] = 0.f; b[j] = 0.f; }
   if (t.active) {
-    float s[V], h[V], k1[V], k2[V], k3[V];
+    float s[V], h[V], k1[V], k2[V], k3[V], mu[V];
 #pragma unroll
     for (int j = 0; j < V; ++j) {
+      mu[j] = st[BN_MEAN * C + t.c0 + j];
       s[j] = st[BN_SCALE * C + t.c0 + j];
       h[j] = st[BN_SHIFT * C + t.c0 + j];
       k1[j] = coef[t.c0 + j];
@@ -325,7 +350,7 @@ bn_bwd_apply_kernel(const float* __restrict__ x, const float* __restrict__ dy,
       for (int j = 0; j < V; ++j) {
         float g = dv[j];
         if (act == ACT_LRELU) g *= lrelu_d(xv[j] * s[j] + h[j]);
-        float d = k1[j] * g + k2[j] * xv[j] + k3[j];
+        float d = k1[j] * g + k2[j] * (xv[j] - mu[j]) + k3[j];
         a[j] += d;
         o[j] = accumulate ? o[j] + d : d;
       }
@@ -333,6 +358,11 @@ bn_bwd_apply_kernel(const float* __restrict__ x, const float* __restrict__ dy,
     }
   }
   if (colsum) block_chan_reduce2<V>(t, a, b, colsum, blockIdx.x, C);
+}
+
+extern "C" size_t accunet_bn_bwd_ws_elems(long P, int C) {
+  int nb = stream_rowblocks(P, C);
+  return (size_t)nb * 2 * C * 2 + accunet_partials_ws_elems(nb, 2 * C) * 2 + 3 * (size_t)C;
 }
 
 extern "C" int accunet_bn_bwd(const float* x, const float* dy, const float* st,
@@ -345,18 +375,20 @@ extern "C" int accunet_bn_bwd(const float* x, const float* dy, const float* st,
   int nb = stream_rowblocks(P, C);
   if (colsum_rows) *colsum_rows = nb;
   dim3 grid(nb, ceil_div(C / V, 64));
-  // ws layout: [nb][2][C] partials | coef [3][C] | reduce scratch
-  float* part = ws;
-  float* coef = ws + (size_t)nb * 2 * C;
-  float* scratch = coef + 3 * (size_t)C;
-  if ((size_t)nb * 2 * C + 3 * (size_t)C + accunet_partials_ws_elems(nb, 2 * C) > ws_elems)
-    return ACC_EBADARG;
+  // ws layout (floats): fp64 partials [nb][2][C] | fp64 reduce scratch | coef [3][C]
+  size_t part_f = (size_t)nb * 2 * C * 2;
+  size_t scr_f = accunet_partials_ws_elems(nb, 2 * C) * 2;
+  if (part_f + scr_f + 3 * (size_t)C > ws_elems) return ACC_EBADARG;
+  if ((uintptr_t)ws & 7) return ACC_EBADARG;
+  double* part = reinterpret_cast<double*>(ws);
+  double* scratch = reinterpret_cast<double*>(ws + part_f);
+  float* coef = ws + part_f + scr_f;
   if (V == 4)
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<4>, grid, dim3(256), 0, s, x, dy, st, act, P, C, part);
   else
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<1>, grid, dim3(256), 0, s, x, dy, st, act, P, C, part);
   int rows;
-  const float* pr = reduce_partials(part, nb, 2 * C, scratch, &rows, s);
+  const double* pr = reduce_partials_t<double>(part, nb, 2 * C, scratch, &rows, s);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(C, 64)), dim3(256), 0, s, pr, rows, C,
                      (double)P, st, gamma, training, dgamma, dbeta, coef);
   if (V == 4)
@@ -371,14 +403,14 @@ extern "C" int accunet_bn_bwd(const float* x, const float* dy, const float* st,
 // ---------------------------------------------------------------------------
 // Column sums (conv bias gradients when no BN-backward pass precedes them).
 // ---------------------------------------------------------------------------
-extern "C" int accunet_colsum(const float* x, long P, int C, float* out, float* ws,
+extern "C" int accunet_colsum(const float* x, long P, int C, float* out, double* ws,
                               size_t ws_elems, void* stream_) {
   hipStream_t s = (hipStream_t)stream_;
   int V = (C % 4 == 0) ? 4 : 1;
   int nb = stream_rowblocks(P, C);
   dim3 grid(nb, ceil_div(C / V, 64));
-  float* part = ws;
-  float* scratch = ws + (size_t)nb * 2 * C;
+  double* part = ws;
+  double* scratch = ws + (size_t)nb * 2 * C;
   if ((size_t)nb * 2 * C + accunet_partials_ws_elems(nb, 2 * C) > ws_elems) return ACC_EBADARG;
   if (V == 4)
     hipLaunchKernelGGL(affine_act_kernel<4>, grid, dim3(256), 0, s, x, nullptr, nullptr, ACT_NONE,
@@ -387,18 +419,19 @@ extern "C" int accunet_colsum(const float* x, long P, int C, float* out, float* 
     hipLaunchKernelGGL(affine_act_kernel<1>, grid, dim3(256), 0, s, x, nullptr, nullptr, ACT_NONE,
                        nullptr, nullptr, P, C, part);
   int rows;
-  const float* pr = reduce_partials(part, nb, 2 * C, scratch, &rows, s);
-  hipLaunchKernelGGL(sum_rows_kernel, dim3(ceil_div(C, 64)), dim3(256), 0, s, pr, rows, 2 * C, C, out);
+  const double* pr = reduce_partials_t<double>(part, nb, 2 * C, scratch, &rows, s);
+  hipLaunchKernelGGL(sum_rows_d_kernel<float>, dim3(ceil_div(C, 64)), dim3(256), 0, s, pr, rows,
+                     2 * C, C, out);
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 
-// Reduce a partial-stats block [R][2][C] to totals [2][C] (fp32 out).
-extern "C" int accunet_reduce_stats(const float* part, int R, int C, float* out2C, float* ws,
+// Reduce a partial-stats block [R][2][C] to totals [2][C] (fp64).
+extern "C" int accunet_reduce_stats(const double* part, int R, int C, double* out2C, double* ws,
                                     void* stream_) {
   hipStream_t s = (hipStream_t)stream_;
   int rows;
-  const float* pr = reduce_partials(part, R, 2 * C, ws, &rows, s);
-  hipLaunchKernelGGL(sum_rows_kernel, dim3(ceil_div(2 * C, 64)), dim3(256), 0, s, pr, rows, 2 * C,
-                     2 * C, out2C);
+  const double* pr = reduce_partials_t<double>(part, R, 2 * C, ws, &rows, s);
+  hipLaunchKernelGGL(sum_rows_d_kernel<double>, dim3(ceil_div(2 * C, 64)), dim3(256), 0, s, pr,
+                     rows, 2 * C, 2 * C, out2C);
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }

@@ -46,10 +46,10 @@ ACC_DEV void stv(float* p, const float (&v)[V]) {
 
 // Reduce per-thread (a[V], b[V]) across the RG row-groups of the block and write
 // the block's partial row out[(row)*2*C + {0,C} + c].
-template <int V>
-ACC_DEV void block_chan_reduce2(const ChanTile& t, float (&a)[V], float (&b)[V], float* out,
-                                long row, int C) {
-  __shared__ float red[2][256 * 4];
+template <int V, typename T>
+ACC_DEV void block_chan_reduce2(const ChanTile& t, T (&a)[V], T (&b)[V], T* out, long row,
+                                int C) {
+  __shared__ T red[2][256 * 4];
   int tid = threadIdx.x;
 #pragma unroll
   for (int j = 0; j < V; ++j) {
@@ -61,7 +61,7 @@ ACC_DEV void block_chan_reduce2(const ChanTile& t, float (&a)[V], float (&b)[V],
     int lt = tid % t.TCQ;
 #pragma unroll
     for (int j = 0; j < V; ++j) {
-      float sa = 0.f, sb = 0.f;
+      T sa = 0, sb = 0;
       for (int g = 0; g < t.RG; ++g) {
         sa += red[0][(g * t.TCQ + lt) * V + j];
         sb += red[1][(g * t.TCQ + lt) * V + j];
@@ -71,5 +71,3 @@ ACC_DEV void block_chan_reduce2(const ChanTile& t, float (&a)[V], float (&b)[V],
     }
   }
 }
-
-

@@ -55,7 +55,7 @@ __global__ void __launch_bounds__(256)
 dw3x3_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
                  const float* __restrict__ bias, const float* __restrict__ sc,
                  const float* __restrict__ sh, int act, int flip, float* __restrict__ z,
-                 float* __restrict__ stats, DwGeom g) {
+                 double* __restrict__ stats, DwGeom g) {
   const int tid = threadIdx.x;
   const int cql = tid % g.TCQ;
   const int px = tid / g.TCQ;
@@ -71,9 +71,9 @@ dw3x3_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
   const bool active = (px < g.TW) && (w < g.W) && (c0 < g.C);
   const int C = g.C;
 
-  float s1[V], s2[V];
+  double s1[V], s2[V];
 #pragma unroll
-  for (int j = 0; j < V; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
+  for (int j = 0; j < V; ++j) { s1[j] = 0.0; s2[j] = 0.0; }
 
   if (active) {
     float k[9][V], bi[V], psc[V], psh[V];
@@ -119,7 +119,7 @@ dw3x3_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
           for (int dx = 0; dx < 3; ++dx) acc = fmaf(k[dy * 3 + dx][j], win[dy][dx][j], acc);
         o[j] = acc;
         s1[j] += acc;
-        s2[j] += acc * acc;
+        s2[j] += (double)acc * acc;
       }
       vstore<V>(z + (((long)b * g.H + h) * g.W + w) * C + c0, o);
 #pragma unroll
@@ -133,7 +133,7 @@ dw3x3_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
   }
 
   if (stats) {
-    __shared__ float red[2][256 * 4];
+    __shared__ double red[2][256 * 4];
 #pragma unroll
     for (int j = 0; j < V; ++j) {
       red[0][tid * V + j] = s1[j];
@@ -144,7 +144,7 @@ dw3x3_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
       int npx = 256 / g.TCQ;
 #pragma unroll
       for (int j = 0; j < V; ++j) {
-        float a = 0.f, q = 0.f;
+        double a = 0.0, q = 0.0;
         for (int i = 0; i < npx; ++i) {
           a += red[0][(i * g.TCQ + cql) * V + j];
           q += red[1][(i * g.TCQ + cql) * V + j];
@@ -285,7 +285,7 @@ extern "C" int accunet_dw3x3_rows(int B, int H, int W, int C) {
 
 extern "C" int accunet_dw3x3_fwd(const float* x, const float* wt, const float* bias,
                                  const float* sc, const float* sh, int act, int flip, float* z,
-                                 float* stats, int B, int H, int W, int C, void* stream) {
+                                 double* stats, int B, int H, int W, int C, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   int V = (C % 4 == 0) ? 4 : 1;
   dim3 grid;

@@ -56,7 +56,7 @@ struct GemmParams {
   const float* up[3];
   int upld[3];
   int uplog[3];  // log2 of the nearest-upsample factor of each added source
-  float* stats;  // [gridDim.x][2][N] partial column (sum, sumsq) of final C, or null
+  double* stats;  // [gridDim.x][2][N] fp64 partial column (sum, sumsq) of final C, or null
   int kchunk;    // K range per blockIdx.z (split-K); >= K means no split
   size_t zstride;  // element stride between split-K partial slabs
 };
@@ -428,9 +428,9 @@ gemm_f32_kernel(const GemmParams p) {
     return;
   }
 
-  float s1[TN], s2[TN];
+  double s1[TN], s2[TN];  // BatchNorm statistics accumulate in fp64 (as ATen's CPU BN)
 #pragma unroll
-  for (int j = 0; j < TN; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
+  for (int j = 0; j < TN; ++j) { s1[j] = 0.0; s2[j] = 0.0; }
 
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
@@ -464,7 +464,7 @@ gemm_f32_kernel(const GemmParams p) {
           if (u < p.nup) v += p.up[u][upoff[u] + n];
         p.C[(size_t)m * p.ldc + n] = v;
         s1[j] += v;
-        s2[j] += v * v;
+        s2[j] += (double)v * v;
       }
     }
   }
@@ -477,7 +477,7 @@ gemm_f32_kernel(const GemmParams p) {
       s2[j] += __shfl_xor(s2[j], 32);
     }
     __syncthreads();  // smem reuse
-    float* red = smem;  // [WM][2][BN]
+    double* red = reinterpret_cast<double*>(smem);  // [WM][2][BN]
     if (lh == 0) {
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
@@ -490,7 +490,7 @@ gemm_f32_kernel(const GemmParams p) {
     for (int c = tid; c < BN; c += GEMM_THREADS) {
       int n = n0 + c;
       if (n < N) {
-        float a = 0.f, b = 0.f;
+        double a = 0.0, b = 0.0;
 #pragma unroll
         for (int w = 0; w < WM; ++w) {
           a += red[(w * 2 + 0) * BN + c];

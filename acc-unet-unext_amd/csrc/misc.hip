@@ -341,13 +341,13 @@ extern "C" int accunet_dotdiff(const float* g, const float* a, const float* b, l
 template <int V>
 __global__ void __launch_bounds__(256)
 wmerge_kernel(const float* __restrict__ a, const float* __restrict__ b, const float* __restrict__ w,
-              float* __restrict__ y, long P, int C, float* __restrict__ stats) {
+              float* __restrict__ y, long P, int C, double* __restrict__ stats) {
   ChanTile t = chan_tile<V>(C);
   long rows_per = (P + gridDim.x - 1) / gridDim.x;
   long r0 = blockIdx.x * rows_per, r1 = min(P, r0 + rows_per);
-  float s1[V], s2[V];
+  double s1[V], s2[V];
 #pragma unroll
-  for (int j = 0; j < V; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
+  for (int j = 0; j < V; ++j) { s1[j] = 0.0; s2[j] = 0.0; }
   const float wv = w[0];
   if (t.active) {
     for (long r = r0 + t.rg; r < r1; r += t.RG) {
@@ -358,7 +358,7 @@ wmerge_kernel(const float* __restrict__ a, const float* __restrict__ b, const fl
       for (int j = 0; j < V; ++j) {
         va[j] = va[j] * wv + vb[j] * (1.f - wv);
         s1[j] += va[j];
-        s2[j] += va[j] * va[j];
+        s2[j] += (double)va[j] * va[j];
       }
       stv<V>(y + r * C + t.c0, va);
     }
@@ -367,7 +367,7 @@ wmerge_kernel(const float* __restrict__ a, const float* __restrict__ b, const fl
 }
 
 extern "C" int accunet_wmerge_fwd(const float* a, const float* b, const float* w, float* y, long P,
-                                  int C, float* stats, void* stream) {
+                                  int C, double* stats, void* stream) {
   int V = (C % 4 == 0) ? 4 : 1;
   int nb = stream_rowblocks(P, C);
   dim3 grid(nb, ceil_div(C / V, 64));

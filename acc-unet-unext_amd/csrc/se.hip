@@ -27,6 +27,36 @@ struct SeGeom {
   long rows_per;  // rows per chunk
 };
 
+// Forward state saved for the backward (one float buffer, doubles first):
+//   S[B*C], Q[B*C] (fp64: per-(b,c) sum a, sum a^2), then fp32 hpre[B*Cr], s[B*C],
+//   mean[C], rstd[C], alpha[B*C], betap[C]
+struct SeSave {
+  double* S;
+  double* Q;
+  float *hpre, *sg, *mean, *rstd, *alpha, *betap;
+};
+
+ACC_DEV SeSave se_save_view(float* base, int B, int C, int Cr) {
+  SeSave v;
+  v.S = reinterpret_cast<double*>(base);
+  v.Q = v.S + (size_t)B * C;
+  float* f = reinterpret_cast<float*>(v.Q + (size_t)B * C);
+  v.hpre = f;
+  v.sg = v.hpre + (size_t)B * Cr;
+  v.mean = v.sg + (size_t)B * C;
+  v.rstd = v.mean + C;
+  v.alpha = v.rstd + C;
+  v.betap = v.alpha + (size_t)B * C;
+  return v;
+}
+
+static size_t se_save_floats(int B, int C, int Cr) {
+  return (size_t)B * C * 4 + (size_t)B * Cr + (size_t)B * C * 2 + 3 * (size_t)C;
+}
+static size_t se_alpha_offset(int B, int C, int Cr) {  // floats
+  return (size_t)B * C * 4 + (size_t)B * Cr + (size_t)B * C + 2 * (size_t)C;
+}
+
 static SeGeom se_geom(int B, int HW, int C) {
   SeGeom g;
   g.B = B;
@@ -45,14 +75,14 @@ static SeGeom se_geom(int B, int HW, int C) {
 template <int V>
 __global__ void __launch_bounds__(256)
 se_reduce_kernel(const float* __restrict__ z, const float* __restrict__ sc,
-                 const float* __restrict__ sh, int act, SeGeom g, float* __restrict__ part) {
+                 const float* __restrict__ sh, int act, SeGeom g, double* __restrict__ part) {
   ChanTile t = chan_tile<V>(g.C);
   const int b = blockIdx.x / g.NCH, ch = blockIdx.x % g.NCH;
   long r0 = (long)b * g.HW + ch * g.rows_per;
   long r1 = min((long)b * g.HW + g.HW, r0 + g.rows_per);
-  float a[V], q[V];
+  double a[V], q[V];
 #pragma unroll
-  for (int j = 0; j < V; ++j) { a[j] = 0.f; q[j] = 0.f; }
+  for (int j = 0; j < V; ++j) { a[j] = 0.0; q[j] = 0.0; }
   if (t.active) {
     float s[V], h[V];
 #pragma unroll
@@ -66,7 +96,7 @@ se_reduce_kernel(const float* __restrict__ z, const float* __restrict__ sc,
       ldv<V>(z + r * g.C + t.c0, v);
 #pragma unroll
       for (int j = 0; j < V; ++j) {
-        float x = pro ? apply_act(v[j] * s[j] + h[j], act) : v[j];
+        double x = pro ? apply_act(v[j] * s[j] + h[j], act) : v[j];
         a[j] += x;
         q[j] += x * x;
       }
@@ -75,46 +105,37 @@ se_reduce_kernel(const float* __restrict__ z, const float* __restrict__ sc,
   block_chan_reduce2<V>(t, a, q, part, blockIdx.x, g.C);
 }
 
-// mid forward. One block of 256 threads. save layout (floats):
-//   S[B*C] Q[B*C] hpre[B*Cr] s[B*C] mean[C] rstd[C] alpha[B*C] betap[C]
+// mid forward. One block of 256 threads. Writes the SeSave state.
 __global__ void __launch_bounds__(256)
-se_mid_kernel(const float* __restrict__ part, SeGeom g, int Cr, const float* __restrict__ w1,
+se_mid_kernel(const double* __restrict__ part, SeGeom g, int Cr, const float* __restrict__ w1,
               const float* __restrict__ b1, const float* __restrict__ w2,
               const float* __restrict__ b2, const float* __restrict__ gamma,
               const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar,
               float momentum, float eps, int training, float* __restrict__ save) {
   const int B = g.B, C = g.C;
-  float* S = save;
-  float* Q = S + B * C;
-  float* hpre = Q + B * C;
-  float* sg = hpre + B * Cr;
-  float* mean = sg + B * C;
-  float* rstd = mean + C;
-  float* alpha = rstd + C;
-  float* betap = alpha + B * C;
+  SeSave sv = se_save_view(save, B, C, Cr);
   const int tid = threadIdx.x;
-  const float inv_hw = 1.f / (float)g.HW;
-  // 1) S, Q
+  // 1) S, Q (fp64)
   for (int i = tid; i < B * C; i += 256) {
     int b = i / C, c = i % C;
     double s1 = 0.0, s2 = 0.0;
     for (int k = 0; k < g.NCH; ++k) {
-      const float* pr = part + ((long)(b * g.NCH + k) * 2) * C;
+      const double* pr = part + ((long)(b * g.NCH + k) * 2) * C;
       s1 += pr[c];
       s2 += pr[C + c];
     }
-    S[i] = (float)s1;
-    Q[i] = (float)s2;
+    sv.S[i] = s1;
+    sv.Q[i] = s2;
   }
   __syncthreads();
-  // 2) fc1 + lrelu (pre-activation saved)
+  // 2) fc1 on the channel means (pre-activation saved)
   for (int i = tid; i < B * Cr; i += 256) {
     int b = i / Cr, j = i % Cr;
     float acc = b1[j];
     const float* wr = w1 + (long)j * C;
-    const float* Sb = S + b * C;
-    for (int c = 0; c < C; ++c) acc = fmaf(wr[c], Sb[c] / (float)g.HW, acc);
-    hpre[i] = acc;
+    const double* Sb = sv.S + (size_t)b * C;
+    for (int c = 0; c < C; ++c) acc = fmaf(wr[c], (float)(Sb[c] / g.HW), acc);
+    sv.hpre[i] = acc;
   }
   __syncthreads();
   // 3) fc2 + sigmoid
@@ -122,21 +143,21 @@ se_mid_kernel(const float* __restrict__ part, SeGeom g, int Cr, const float* __r
     int b = i / C, c = i % C;
     float acc = b2[c];
     const float* wr = w2 + (long)c * Cr;
-    const float* hb = hpre + b * Cr;
+    const float* hb = sv.hpre + (size_t)b * Cr;
     for (int j = 0; j < Cr; ++j) acc = fmaf(wr[j], lrelu(hb[j]), acc);
-    sg[i] = 1.f / (1.f + expf(-acc));
+    sv.sg[i] = 1.f / (1.f + expf(-acc));
   }
   __syncthreads();
-  // 4) BN statistics of y = a*s, running update, coefficients
+  // 4) BN statistics of y = a*s from (S, Q, s), running update, coefficients
   const double n = (double)B * g.HW;
   for (int c = tid; c < C; c += 256) {
     float mu, var;
     if (training) {
       double m1 = 0.0, m2 = 0.0;
       for (int b = 0; b < B; ++b) {
-        double s = sg[b * C + c];
-        m1 += s * S[b * C + c];
-        m2 += s * s * Q[b * C + c];
+        double s = sv.sg[b * C + c];
+        m1 += s * sv.S[b * C + c];
+        m2 += s * s * sv.Q[b * C + c];
       }
       m1 /= n;
       m2 = m2 / n - m1 * m1;
@@ -151,10 +172,10 @@ se_mid_kernel(const float* __restrict__ part, SeGeom g, int Cr, const float* __r
     }
     float rs = 1.f / sqrtf(var + eps);
     float k = gamma[c] * rs;
-    mean[c] = mu;
-    rstd[c] = rs;
-    betap[c] = beta[c] - k * mu;
-    for (int b = 0; b < B; ++b) alpha[b * C + c] = k * sg[b * C + c];
+    sv.mean[c] = mu;
+    sv.rstd[c] = rs;
+    sv.betap[c] = beta[c] - k * mu;
+    for (int b = 0; b < B; ++b) sv.alpha[b * C + c] = k * sv.sg[b * C + c];
   }
 }
 
@@ -164,14 +185,14 @@ __global__ void __launch_bounds__(256)
 se_apply_kernel(const float* __restrict__ z, const float* __restrict__ sc,
                 const float* __restrict__ sh, int act, SeGeom g, const float* __restrict__ alpha,
                 const float* __restrict__ betap, float* __restrict__ out,
-                float* __restrict__ ostats) {
+                double* __restrict__ ostats) {
   ChanTile t = chan_tile<V>(g.C);
   const int b = blockIdx.x / g.NCH, ch = blockIdx.x % g.NCH;
   long r0 = (long)b * g.HW + ch * g.rows_per;
   long r1 = min((long)b * g.HW + g.HW, r0 + g.rows_per);
-  float o1[V], o2[V];
+  double o1[V], o2[V];
 #pragma unroll
-  for (int j = 0; j < V; ++j) { o1[j] = 0.f; o2[j] = 0.f; }
+  for (int j = 0; j < V; ++j) { o1[j] = 0.0; o2[j] = 0.0; }
   if (t.active) {
     float s[V], h[V], al[V], be[V];
 #pragma unroll
@@ -190,7 +211,7 @@ se_apply_kernel(const float* __restrict__ z, const float* __restrict__ sc,
         float x = pro ? apply_act(v[j] * s[j] + h[j], act) : v[j];
         v[j] = lrelu(al[j] * x + be[j]);
         o1[j] += v[j];
-        o2[j] += v[j] * v[j];
+        o2[j] += (double)v[j] * v[j];
       }
       stv<V>(out + r * g.C + t.c0, v);
     }
@@ -205,14 +226,14 @@ __global__ void __launch_bounds__(256)
 se_bwd_reduce_kernel(const float* __restrict__ z, const float* __restrict__ dout,
                      const float* __restrict__ sc, const float* __restrict__ sh, int act,
                      SeGeom g, const float* __restrict__ alpha, const float* __restrict__ betap,
-                     float* __restrict__ part) {
+                     double* __restrict__ part) {
   ChanTile t = chan_tile<V>(g.C);
   const int b = blockIdx.x / g.NCH, ch = blockIdx.x % g.NCH;
   long r0 = (long)b * g.HW + ch * g.rows_per;
   long r1 = min((long)b * g.HW + g.HW, r0 + g.rows_per);
-  float t1[V], t2[V];
+  double t1[V], t2[V];
 #pragma unroll
-  for (int j = 0; j < V; ++j) { t1[j] = 0.f; t2[j] = 0.f; }
+  for (int j = 0; j < V; ++j) { t1[j] = 0.0; t2[j] = 0.0; }
   if (t.active) {
     float s[V], h[V], al[V], be[V];
 #pragma unroll
@@ -232,127 +253,123 @@ se_bwd_reduce_kernel(const float* __restrict__ z, const float* __restrict__ dout
         float x = pro ? apply_act(v[j] * s[j] + h[j], act) : v[j];
         float g2 = d[j] * lrelu_d(al[j] * x + be[j]);
         t1[j] += g2;
-        t2[j] += g2 * x;
+        t2[j] += (double)g2 * x;
       }
     }
   }
   block_chan_reduce2<V>(t, t1, t2, part, blockIdx.x, g.C);
 }
 
-// backward mid. One block. coef layout: A[B*C] Bc[B*C] Cc[B*C]
+// backward mid. One block. coef layout (fp32): A[B*C] Bc[B*C] Cc[B*C] with
+//   da = A*g2 + Bc*(a*s - mean) + Cc
+// scratch (fp64): T1[B*C] T2[B*C] G[C] GY[C] du[B*C] dh[B*Cr]
 __global__ void __launch_bounds__(256)
-se_bwd_mid_kernel(const float* __restrict__ part, SeGeom g, int Cr, const float* __restrict__ w1,
+se_bwd_mid_kernel(const double* __restrict__ part, SeGeom g, int Cr, const float* __restrict__ w1,
                   const float* __restrict__ w2, const float* __restrict__ gamma, int training,
-                  const float* __restrict__ save, float* __restrict__ dw1, float* __restrict__ db1,
+                  float* __restrict__ save, float* __restrict__ dw1, float* __restrict__ db1,
                   float* __restrict__ dw2, float* __restrict__ db2, float* __restrict__ dgamma,
-                  float* __restrict__ dbeta, float* __restrict__ scratch, float* __restrict__ coef) {
+                  float* __restrict__ dbeta, double* __restrict__ scratch,
+                  float* __restrict__ coef) {
   const int B = g.B, C = g.C;
-  const float* S = save;
-  const float* Q = S + B * C;
-  const float* hpre = Q + B * C;
-  const float* sg = hpre + B * Cr;
-  const float* mean = sg + B * C;
-  const float* rstd = mean + C;
-  float* T1 = scratch;
-  float* T2 = T1 + B * C;
-  float* G = T2 + B * C;   // [C]
-  float* GY = G + C;       // [C]
-  float* du = GY + C;      // [B*C]
-  float* dh = du + B * C;  // [B*Cr]
+  SeSave sv = se_save_view(save, B, C, Cr);
+  double* T1 = scratch;
+  double* T2 = T1 + (size_t)B * C;
+  double* G = T2 + (size_t)B * C;
+  double* GY = G + C;
+  double* du = GY + C;
+  double* dh = du + (size_t)B * C;
   float* A = coef;
-  float* Bc = A + B * C;
-  float* Cc = Bc + B * C;
+  float* Bc = A + (size_t)B * C;
+  float* Cc = Bc + (size_t)B * C;
   const int tid = threadIdx.x;
-  const float inv_hw = 1.f / (float)g.HW;
   const double n = (double)B * g.HW;
   for (int i = tid; i < B * C; i += 256) {
     int b = i / C, c = i % C;
     double s1 = 0.0, s2 = 0.0;
     for (int k = 0; k < g.NCH; ++k) {
-      const float* pr = part + ((long)(b * g.NCH + k) * 2) * C;
+      const double* pr = part + ((long)(b * g.NCH + k) * 2) * C;
       s1 += pr[c];
       s2 += pr[C + c];
     }
-    T1[i] = (float)s1;
-    T2[i] = (float)s2;
+    T1[i] = s1;
+    T2[i] = s2;
   }
   __syncthreads();
+  // per-channel BN sums: G = sum g2, GY = sum g2*yhat = rstd * sum_b (s*T2 - mean*T1)
   for (int c = tid; c < C; c += 256) {
     double gs = 0.0, gy = 0.0;
     for (int b = 0; b < B; ++b) {
       gs += T1[b * C + c];
-      gy += (double)sg[b * C + c] * T2[b * C + c] - (double)mean[c] * T1[b * C + c];
+      gy += (double)sv.sg[b * C + c] * T2[b * C + c] - (double)sv.mean[c] * T1[b * C + c];
     }
-    gy *= rstd[c];
-    G[c] = (float)gs;
-    GY[c] = (float)gy;
+    gy *= sv.rstd[c];
+    G[c] = gs;
+    GY[c] = gy;
     if (dgamma) dgamma[c] = (float)gy;
     if (dbeta) dbeta[c] = (float)gs;
   }
   __syncthreads();
-  // ds -> du = ds * s * (1 - s)
+  // ds = sum_hw dy*a; du = ds * s * (1 - s)
   for (int i = tid; i < B * C; i += 256) {
     int c = i % C;
-    float k = gamma[c] * rstd[c];
-    float s = sg[i];
-    float ds;
+    double k = (double)gamma[c] * sv.rstd[c];
+    double s = sv.sg[i];
+    double ds;
     if (training) {
-      float yhx = rstd[c] * (s * Q[i] - mean[c] * S[i]);  // sum_hw yhat * a
-      ds = k * (T2[i] - (float)(G[c] / n) * S[i] - (float)(GY[c] / n) * yhx);
+      double yha = (double)sv.rstd[c] * (s * sv.Q[i] - (double)sv.mean[c] * sv.S[i]);
+      ds = k * (T2[i] - (G[c] / n) * sv.S[i] - (GY[c] / n) * yha);
     } else {
       ds = k * T2[i];
     }
-    du[i] = ds * s * (1.f - s);
+    du[i] = ds * s * (1.0 - s);
   }
   __syncthreads();
-  // fc2 backward: dw2[c][j] = sum_b du[b,c] * lrelu(hpre[b,j]); db2[c] = sum_b du[b,c]
+  // fc2 backward
   for (int i = tid; i < C * Cr; i += 256) {
     int c = i / Cr, j = i % Cr;
-    float acc = 0.f;
-    for (int b = 0; b < B; ++b) acc += du[b * C + c] * lrelu(hpre[b * Cr + j]);
-    dw2[i] = acc;
+    double acc = 0.0;
+    for (int b = 0; b < B; ++b) acc += du[b * C + c] * lrelu(sv.hpre[b * Cr + j]);
+    dw2[i] = (float)acc;
   }
   for (int c = tid; c < C; c += 256) {
-    float acc = 0.f;
+    double acc = 0.0;
     for (int b = 0; b < B; ++b) acc += du[b * C + c];
-    db2[c] = acc;
+    db2[c] = (float)acc;
   }
   // dh[b,j] = lrelu'(hpre) * sum_c w2[c][j] du[b,c]
   for (int i = tid; i < B * Cr; i += 256) {
     int b = i / Cr, j = i % Cr;
-    float acc = 0.f;
-    for (int c = 0; c < C; ++c) acc = fmaf(w2[(long)c * Cr + j], du[b * C + c], acc);
-    dh[i] = acc * lrelu_d(hpre[i]);
+    double acc = 0.0;
+    for (int c = 0; c < C; ++c) acc += (double)w2[(long)c * Cr + j] * du[b * C + c];
+    dh[i] = acc * lrelu_d(sv.hpre[i]);
   }
   __syncthreads();
-  // fc1 backward: dw1[j][c] = sum_b dh[b,j] * m[b,c]; db1[j] = sum_b dh[b,j]
+  // fc1 backward (input = channel means S/HW)
   for (int i = tid; i < Cr * C; i += 256) {
     int j = i / C, c = i % C;
-    float acc = 0.f;
-    for (int b = 0; b < B; ++b) acc += dh[b * Cr + j] * (S[b * C + c] * inv_hw);
-    dw1[i] = acc;
+    double acc = 0.0;
+    for (int b = 0; b < B; ++b) acc += dh[b * Cr + j] * (sv.S[b * C + c] / g.HW);
+    dw1[i] = (float)acc;
   }
   for (int j = tid; j < Cr; j += 256) {
-    float acc = 0.f;
+    double acc = 0.0;
     for (int b = 0; b < B; ++b) acc += dh[b * Cr + j];
-    db1[j] = acc;
+    db1[j] = (float)acc;
   }
-  // coefficients: da = A*g2 + Bc*a + Cc
+  // coefficients: da = A*g2 + Bc*(a*s - mean) + Cc
   for (int i = tid; i < B * C; i += 256) {
     int b = i / C, c = i % C;
-    float dm = 0.f;
-    for (int j = 0; j < Cr; ++j) dm = fmaf(w1[(long)j * C + c], dh[b * Cr + j], dm);
-    float k = gamma[c] * rstd[c];
-    float s = sg[i];
+    double dm = 0.0;
+    for (int j = 0; j < Cr; ++j) dm += (double)w1[(long)j * C + c] * dh[b * Cr + j];
+    double k = (double)gamma[c] * sv.rstd[c];
+    double s = sv.sg[i];
+    A[i] = (float)(s * k);
     if (training) {
-      float gn = (float)(G[c] / n), gyn = (float)(GY[c] / n);
-      A[i] = s * k;
-      Bc[i] = -s * s * k * rstd[c] * gyn;
-      Cc[i] = -s * k * gn + s * k * rstd[c] * mean[c] * gyn + dm * inv_hw;
+      Bc[i] = (float)(-s * k * sv.rstd[c] * (GY[c] / n));
+      Cc[i] = (float)(-s * k * (G[c] / n) + dm / g.HW);
     } else {
-      A[i] = s * k;
       Bc[i] = 0.f;
-      Cc[i] = dm * inv_hw;
+      Cc[i] = (float)(dm / g.HW);
     }
   }
 }
@@ -362,6 +379,7 @@ __global__ void __launch_bounds__(256)
 se_bwd_apply_kernel(const float* __restrict__ z, const float* __restrict__ dout,
                     const float* __restrict__ sc, const float* __restrict__ sh, int act, SeGeom g,
                     const float* __restrict__ alpha, const float* __restrict__ betap,
+                    const float* __restrict__ sgate, const float* __restrict__ mean,
                     const float* __restrict__ coef, float* __restrict__ da) {
   ChanTile t = chan_tile<V>(g.C);
   if (!t.active) return;
@@ -369,10 +387,12 @@ se_bwd_apply_kernel(const float* __restrict__ z, const float* __restrict__ dout,
   long r0 = (long)b * g.HW + ch * g.rows_per;
   long r1 = min((long)b * g.HW + g.HW, r0 + g.rows_per);
   const int BC = g.B * g.C;
-  float s[V], h[V], al[V], be[V], A[V], Bc[V], Cc[V];
+  float s[V], h[V], al[V], be[V], A[V], Bc[V], Cc[V], sgv[V], mu[V];
 #pragma unroll
   for (int j = 0; j < V; ++j) {
     int i = b * g.C + t.c0 + j;
+    sgv[j] = sgate[i];
+    mu[j] = mean[t.c0 + j];
     s[j] = sc ? sc[t.c0 + j] : 1.f;
     h[j] = sh ? sh[t.c0 + j] : 0.f;
     al[j] = alpha[i];
@@ -390,7 +410,7 @@ se_bwd_apply_kernel(const float* __restrict__ z, const float* __restrict__ dout,
     for (int j = 0; j < V; ++j) {
       float x = pro ? apply_act(v[j] * s[j] + h[j], act) : v[j];
       float g2 = d[j] * lrelu_d(al[j] * x + be[j]);
-      d[j] = A[j] * g2 + Bc[j] * x + Cc[j];
+      d[j] = A[j] * g2 + Bc[j] * (x * sgv[j] - mu[j]) + Cc[j];
     }
     stv<V>(da + r * g.C + t.c0, d);
   }
@@ -399,9 +419,7 @@ se_bwd_apply_kernel(const float* __restrict__ z, const float* __restrict__ dout,
 // ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------
-extern "C" size_t accunet_se_save_elems(int B, int C, int Cr) {
-  return (size_t)B * C * 4 + (size_t)B * Cr + 3 * (size_t)C;
-}
+extern "C" size_t accunet_se_save_elems(int B, int C, int Cr) { return se_save_floats(B, C, Cr); }
 
 // rows of the optional SE-output statistics block written by accunet_se_fwd
 extern "C" int accunet_se_stats_rows(int B, int HW, int C) {
@@ -409,12 +427,15 @@ extern "C" int accunet_se_stats_rows(int B, int HW, int C) {
   return B * g.NCH;
 }
 
+// workspace (floats): fp64 partials [B*NCH][2][C] | fp64 scratch | fp32 coef [3][B*C]
+static size_t se_part_floats(const SeGeom& g) { return (size_t)g.B * g.NCH * 2 * g.C * 2; }
+static size_t se_scratch_floats(int B, int C, int Cr) {
+  return ((size_t)B * C * 3 + 2 * (size_t)C + (size_t)B * Cr) * 2;
+}
+
 extern "C" size_t accunet_se_ws_elems(int B, int HW, int C, int Cr) {
   SeGeom g = se_geom(B, HW, C);
-  size_t part = (size_t)B * g.NCH * 2 * C;
-  size_t scratch = (size_t)B * C * 3 + 2 * (size_t)C + (size_t)B * Cr;
-  size_t coef = (size_t)B * C * 3;
-  return part + scratch + coef;
+  return se_part_floats(g) + se_scratch_floats(B, C, Cr) + (size_t)B * C * 3 + 4;
 }
 
 extern "C" int accunet_se_fwd(const float* z, const float* sc, const float* sh, int act, int B,
@@ -422,13 +443,14 @@ extern "C" int accunet_se_fwd(const float* z, const float* sc, const float* sh, 
                               const float* w2, const float* b2, const float* gamma,
                               const float* beta, float* rmean, float* rvar, long long* nbt,
                               float momentum, float eps, int training, float* out, float* save,
-                              float* ostats, float* ws, size_t ws_elems, void* stream) {
+                              double* ostats, float* ws, size_t ws_elems, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (ws_elems < accunet_se_ws_elems(B, HW, C, Cr)) return ACC_EBADARG;
+  if (((uintptr_t)ws & 7) || ((uintptr_t)save & 7)) return ACC_EBADARG;
   SeGeom g = se_geom(B, HW, C);
   int V = (C % 4 == 0) ? 4 : 1;
   dim3 grid(B * g.NCH, ceil_div(C / V, 64));
-  float* part = ws;
+  double* part = reinterpret_cast<double*>(ws);
   if (V == 4)
     hipLaunchKernelGGL(se_reduce_kernel<4>, grid, dim3(256), 0, s, z, sc, sh, act, g, part);
   else
@@ -436,7 +458,7 @@ extern "C" int accunet_se_fwd(const float* z, const float* sc, const float* sh, 
   hipLaunchKernelGGL(se_mid_kernel, dim3(1), dim3(256), 0, s, part, g, Cr, w1, b1, w2, b2, gamma,
                      beta, rmean, rvar, momentum, eps, training, save);
   if (training && nbt) hipLaunchKernelGGL(inc_i64_kernel, dim3(1), dim3(1), 0, s, nbt);
-  const float* alpha = save + (size_t)B * C * 3 + (size_t)B * Cr + 2 * (size_t)C;
+  const float* alpha = save + se_alpha_offset(B, C, Cr);
   const float* betap = alpha + (size_t)B * C;
   if (V == 4)
     hipLaunchKernelGGL(se_apply_kernel<4>, grid, dim3(256), 0, s, z, sc, sh, act, g, alpha, betap,
@@ -455,14 +477,17 @@ extern "C" int accunet_se_bwd(const float* z, const float* dout, const float* sc
                               void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (ws_elems < accunet_se_ws_elems(B, HW, C, Cr)) return ACC_EBADARG;
+  if (((uintptr_t)ws & 7) || ((uintptr_t)save & 7)) return ACC_EBADARG;
   SeGeom g = se_geom(B, HW, C);
   int V = (C % 4 == 0) ? 4 : 1;
   dim3 grid(B * g.NCH, ceil_div(C / V, 64));
-  float* part = ws;
-  float* scratch = part + (size_t)B * g.NCH * 2 * C;
-  float* coef = scratch + (size_t)B * C * 3 + 2 * (size_t)C + (size_t)B * Cr;
-  const float* alpha = save + (size_t)B * C * 3 + (size_t)B * Cr + 2 * (size_t)C;
+  double* part = reinterpret_cast<double*>(ws);
+  double* scratch = reinterpret_cast<double*>(ws + se_part_floats(g));
+  float* coef = ws + se_part_floats(g) + se_scratch_floats(B, C, Cr);
+  const float* alpha = save + se_alpha_offset(B, C, Cr);
   const float* betap = alpha + (size_t)B * C;
+  const float* sgate = save + (size_t)B * C * 4 + (size_t)B * Cr;
+  const float* mean = sgate + (size_t)B * C;
   if (V == 4)
     hipLaunchKernelGGL(se_bwd_reduce_kernel<4>, grid, dim3(256), 0, s, z, dout, sc, sh, act, g,
                        alpha, betap, part);
@@ -470,12 +495,13 @@ extern "C" int accunet_se_bwd(const float* z, const float* dout, const float* sc
     hipLaunchKernelGGL(se_bwd_reduce_kernel<1>, grid, dim3(256), 0, s, z, dout, sc, sh, act, g,
                        alpha, betap, part);
   hipLaunchKernelGGL(se_bwd_mid_kernel, dim3(1), dim3(256), 0, s, part, g, Cr, w1, w2, gamma,
-                     training, save, dw1, db1, dw2, db2, dgamma, dbeta, scratch, coef);
+                     training, const_cast<float*>(save), dw1, db1, dw2, db2, dgamma, dbeta,
+                     scratch, coef);
   if (V == 4)
     hipLaunchKernelGGL(se_bwd_apply_kernel<4>, grid, dim3(256), 0, s, z, dout, sc, sh, act, g,
-                       alpha, betap, coef, da);
+                       alpha, betap, sgate, mean, coef, da);
   else
     hipLaunchKernelGGL(se_bwd_apply_kernel<1>, grid, dim3(256), 0, s, z, dout, sc, sh, act, g,
-                       alpha, betap, coef, da);
+                       alpha, betap, sgate, mean, coef, da);
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }

@@ -61,7 +61,7 @@ typedef struct AccGemmDesc {
   const float* up[3];
   int upld[3];
   int uplog[3];
-  float* stats;             /* [rows][2][N] partial (sum,sumsq) of C, or NULL */
+  double* stats;            /* [rows][2][N] fp64 partial (sum,sumsq) of C, or NULL */
   int allow_split;          /* split-K through ws (weight gradients) */
 } AccGemmDesc;
 
@@ -76,22 +76,26 @@ int accunet_gemm_stats_rows(int M, int N, int amode, int bmode, int cin);
  * :235-262 (HANCBlock norms), :73-74 (HANCLayer), :172-184 (Conv2d_batchnorm),
  * :309-325 (ResPath), :393-414 (MLFC).
  * st = [4][C]: mean, rstd, scale(=gamma*rstd), shift(=beta-mean*scale)
+ * Statistics partial blocks ("stats"/"part": [rows][2][C] sum, sum of squares) are
+ * fp64 everywhere (ATen's CPU BatchNorm also accumulates in double).
  * ------------------------------------------------------------------------- */
 int accunet_stream_rows(long P, int C);
-int accunet_bn_finalize(const float* part, int R, int C, double count, const float* gamma,
+int accunet_bn_finalize(const double* part, int R, int C, double count, const float* gamma,
                         const float* beta, float* rmean, float* rvar, long long* nbt,
-                        float momentum, float eps, int training, float* st, float* ws,
+                        float momentum, float eps, int training, float* st, double* ws,
                         void* stream);
 int accunet_affine_act_fwd(const float* x, const float* sc, const float* sh, int act,
-                           const float* res, float* y, long P, int C, float* stats,
+                           const float* res, float* y, long P, int C, double* stats,
                            int* stats_rows, void* stream);
+size_t accunet_bn_bwd_ws_elems(long P, int C);
 int accunet_bn_bwd(const float* x, const float* dy, const float* st, const float* gamma, int act,
                    int training, long P, int C, float* dx, int accumulate, float* dgamma,
                    float* dbeta, float* colsum, int* colsum_rows, float* ws, size_t ws_elems,
                    void* stream);
-int accunet_colsum(const float* x, long P, int C, float* out, float* ws, size_t ws_elems,
+int accunet_colsum(const float* x, long P, int C, float* out, double* ws, size_t ws_elems,
                    void* stream);
-int accunet_reduce_stats(const float* part, int R, int C, float* out2C, float* ws, void* stream);
+int accunet_reduce_stats(const double* part, int R, int C, double* out2C, double* ws,
+                         void* stream);
 
 /* ------------------------------------------------------------------------- *
  * HANCBlock.conv2 — depthwise 3x3 (+bias), pad 1, groups = C
@@ -102,7 +106,7 @@ int accunet_reduce_stats(const float* part, int R, int C, float* out2C, float* w
  * ------------------------------------------------------------------------- */
 int accunet_dw3x3_rows(int B, int H, int W, int C);
 int accunet_dw3x3_fwd(const float* x, const float* wt, const float* bias, const float* sc,
-                      const float* sh, int act, int flip, float* z, float* stats, int B, int H,
+                      const float* sh, int act, int flip, float* z, double* stats, int B, int H,
                       int W, int C, void* stream);
 size_t accunet_dw3x3_wgrad_ws(int B, int H, int W, int C);
 int accunet_dw3x3_wgrad(const float* x, const float* dz, const float* sc, const float* sh,
@@ -159,7 +163,7 @@ int accunet_se_fwd(const float* z, const float* sc, const float* sh, int act, in
                    int C, int Cr, const float* w1, const float* b1, const float* w2,
                    const float* b2, const float* gamma, const float* beta, float* rmean,
                    float* rvar, long long* nbt, float momentum, float eps, int training,
-                   float* out, float* save, float* ostats, float* ws, size_t ws_elems,
+                   float* out, float* save, double* ostats, float* ws, size_t ws_elems,
                    void* stream);
 int accunet_se_bwd(const float* z, const float* dout, const float* sc, const float* sh, int act,
                    int B, int HW, int C, int Cr, const float* w1, const float* w2,
@@ -203,7 +207,7 @@ int accunet_adam_step(const void* table, const int* chunk_t, const long long* ch
  * ACC_UNet_W learnable merge y = a*w + b*(1-w) (ACC_UNet/ACC_UNet_w.py:497-522)
  * ------------------------------------------------------------------------- */
 int accunet_wmerge_fwd(const float* a, const float* b, const float* w, float* y, long P, int C,
-                       float* stats, void* stream);
+                       double* stats, void* stream);
 int accunet_wmerge_bwd(const float* g, const float* w, float* da, float* db, long n,
                        void* stream);
 int accunet_dotdiff(const float* g, const float* a, const float* b, long n, float* out,

@@ -1,6 +1,7 @@
-"""Diagnostic driver (GPU box): HIP model vs fp64 oracle, prints per-check errors.
+"""Diagnostic driver (GPU box): HIP model vs fp64 oracle, with the reference's own
+fp32 error (fp32 oracle) as the yardstick. Prints the worst tensors by ratio.
 
-    python tests/gpu_diag.py [variant ...]
+    python tests/gpu_diag.py variant nf B H
 """
 import os
 import sys
@@ -13,62 +14,82 @@ sys.path.insert(0, os.path.join(os.path.dirname(HERE), "acc-unet-unext_amd"))
 sys.path.insert(0, HERE)
 import parity_util as PU  # noqa: E402
 from parity_util import O  # noqa: E402
-from accunet.model import VARIANTS  # noqa: E402
+from accunet import model as M  # noqa: E402
 from accunet.loss import WeightedDiceBCE  # noqa: E402
 
 
-def run(variant, nf=8, B=2, H=32, W=32):
+def run_model(variant, nf, B, H):
     spec = O.param_spec(variant, 3, 1, nf)
     sd = O.det_state_dict(spec, seed=0)
-    x = O.det_input((B, 3, H, W), "golden-x")
-    mask = O.det_mask((B, 1, H, W), "golden-mask", p=0.4)
-    t0 = time.time()
-    ref_out, ref_loss, ref_grads, ref_sd = PU.oracle_run(variant, sd, x, mask)
-    t1 = time.time()
-    m = VARIANTS[variant](3, 1, n_filts=nf)
+    x = O.det_input((B, 3, H, H), "golden-x")
+    mask = O.det_mask((B, 1, H, H), "golden-mask", p=0.4)
+    r64 = PU.oracle_run(variant, sd, x, mask)
+    r32 = PU.oracle_run(variant, sd, x, mask, dtype=torch.float32)
+    m = M.VARIANTS[variant](3, 1, n_filts=nf)
     m.load_state_dict(sd)
     m = m.cuda().train()
     out = m(x.cuda())
     loss = WeightedDiceBCE(0.5, 0.5)(out, mask.cuda())
     loss.backward()
     torch.cuda.synchronize()
-    t2 = time.time()
-    oerr = (out.detach().double().cpu() - ref_out).abs().max().item()
-    lerr = abs(loss.item() - ref_loss.item())
-    print(f"[{variant}] oracle {t1 - t0:.2f}s hip {t2 - t1:.2f}s  out max|d|={oerr:.3e} "
-          f"loss {loss.item():.6f} vs {ref_loss.item():.6f} d={lerr:.2e}")
-    hip_grads = {k: p.grad if p.grad is not None else torch.zeros_like(p)
-                 for k, p in m.named_parameters()}
-    rows = PU.compare_grads(hip_grads, ref_grads)
-    bad = [r for r in rows if not r[4]]
-    rows.sort(key=lambda r: -(r[1] / (r[3] + 1e-30)))
-    for r in rows[:12]:
-        print("   %-45s err=%.3e scale=%.3e tol=%.3e %s" % (r[0], r[1], r[2], r[3], "ok" if r[4] else "BAD"))
-    print(f"   grads: {len(rows) - len(bad)}/{len(rows)} ok")
-    # running stats
-    msd = m.state_dict()
-    worst = 0.0
-    wname = ""
-    for k, v in ref_sd.items():
-        if k.endswith("running_mean") or k.endswith("running_var"):
-            d = (msd[k].double().cpu() - v.double()).abs().max().item()
-            if d > worst:
-                worst, wname = d, k
-        if k.endswith("num_batches_tracked"):
-            assert int(msd[k]) == int(v), k
-    print(f"   running stats worst |d| = {worst:.3e} ({wname})")
-    # eval mode forward
-    m.eval()
-    with torch.no_grad():
-        oe = m(x.cuda()).double().cpu()
-    ref_e, _, _, _ = PU.oracle_run(variant, ref_sd, x, None, training=False)
-    print(f"   eval out max|d| = {(oe - ref_e).abs().max().item():.3e}")
-    return len(bad)
+    hip = {"out": out}
+    a64 = {"out": r64[0]}
+    a32 = {"out": r32[0]}
+    for k, p in m.named_parameters():
+        hip[k] = p.grad
+        a64[k] = r64[2][k]
+        a32[k] = r32[2][k]
+    rows = PU.compare_vs_reference_fp32(hip, a64, a32)
+    rows.sort(key=lambda r: -(r[1] / (r[2] + 1e-30)))
+    print(f"== {variant} nf{nf} B{B} {H}x{H}: loss hip {loss.item():.7f} r64 {r64[1].item():.7f} "
+          f"r32 {r32[1].item():.7f}")
+    for r in rows[:25]:
+        sc = a64[r[0]].abs().max().item()
+        print("   %-42s hip %.2e ref32 %.2e ratio %6.1f  scale %.2e %s" %
+              (r[0], r[1], r[2], r[1] / (r[2] + 1e-30), sc, "" if r[4] else "BAD"))
+    print("   bad:", sum(1 for r in rows if not r[4]), "/", len(rows))
+
+
+def run_se(C, B, H, pre):
+    torch.manual_seed(0)
+    se = M.ChannelSELayer(C)
+    spec = [(n, tuple(t.shape)) for n, t in se.state_dict().items()]
+    sd = O.det_state_dict([("s." + n, s) for n, s in spec], seed=3)
+    se.load_state_dict({n[2:]: v for n, v in sd.items()})
+    se = se.cuda().train()
+    x = O.det_input((B, C, H, H), "se-x") * 2 + 0.5
+    go = O.det_input((B, C, H, H), "se-go")
+    res = {}
+    for dt in (torch.float64, torch.float32):
+        sdo = {n: (v.to(dt).requires_grad_(not n.endswith(PU.BUFFER_LEAVES)) if v.is_floating_point() else v.clone())
+               for n, v in sd.items()}
+        xr = x.detach().clone().to(dt).requires_grad_(True)
+        y = O.se(xr, sdo, "s", True)
+        (y * go.to(dt)).sum().backward()
+        res[dt] = (y.detach(), xr.grad, {n[2:]: v.grad for n, v in sdo.items() if v.grad is not None})
+    xh = x.detach().cuda().requires_grad_(True)
+    y = se(xh)
+    (y * go.cuda()).sum().backward()
+    print(f"== SE C{C} B{B} {H}x{H}")
+    hip = {"out": y, "dx": xh.grad}
+    a64 = {"out": res[torch.float64][0], "dx": res[torch.float64][1]}
+    a32 = {"out": res[torch.float32][0], "dx": res[torch.float32][1]}
+    for n, p in se.named_parameters():
+        hip[n] = p.grad
+        a64[n] = res[torch.float64][2][n]
+        a32[n] = res[torch.float32][2][n]
+    for r in PU.compare_vs_reference_fp32(hip, a64, a32):
+        print("   %-20s hip %.2e ref32 %.2e ratio %6.1f %s" % (r[0], r[1], r[2], r[1] / (r[2] + 1e-30),
+                                                            "" if r[4] else "BAD"))
 
 
 if __name__ == "__main__":
-    vs = sys.argv[1:] or ["canonical", "script", "lite", "w"]
-    nbad = 0
-    for v in vs:
-        nbad += run(v)
-    print("TOTAL BAD", nbad)
+    a = sys.argv[1:]
+    if a and a[0] == "se":
+        run_se(int(a[1]), int(a[2]), int(a[3]), None)
+    else:
+        variant = a[0] if a else "canonical"
+        nf = int(a[1]) if len(a) > 1 else 8
+        B = int(a[2]) if len(a) > 2 else 2
+        H = int(a[3]) if len(a) > 3 else 32
+        run_model(variant, nf, B, H)

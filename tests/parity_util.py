@@ -58,3 +58,38 @@ def compare_grads(hip_grads: dict, ref_grads: dict, rtol=2e-3, floor_frac=2e-3):
             ok = err <= tol
         rows.append((k, err, scale, tol, ok))
     return rows
+
+
+def compare_vs_reference_fp32(hip: dict, ref64: dict, ref32: dict, factor=4.0, rel_floor=1e-4,
+                              abs_floor=None):
+    """Per-tensor check that the HIP fp32 result is as close to the fp64 oracle as the
+    reference's own fp32 arithmetic is (oracle run in fp32 = same ATen ops as the
+    reference): max|hip - ref64| <= factor * max|ref32 - ref64| + rel_floor * max|ref64|.
+    Returns rows (name, err_hip, err_ref32, tol, ok)."""
+    rows = []
+    for k, r64 in ref64.items():
+        r64 = r64.detach().double().cpu()
+        h = hip[k].detach().double().cpu()
+        r32 = ref32[k].detach().double().cpu()
+        e_h = (h - r64).abs().max().item() if r64.numel() else 0.0
+        e_r = (r32 - r64).abs().max().item() if r64.numel() else 0.0
+        scale = r64.abs().max().item() if r64.numel() else 0.0
+        tol = factor * e_r + rel_floor * scale + 1e-9
+        if abs_floor is not None:
+            tol += abs_floor.get(k, 0.0) if isinstance(abs_floor, dict) else abs_floor
+        rows.append((k, e_h, e_r, tol, e_h <= tol))
+    return rows
+
+
+def global_rel_err(hip: dict, ref: dict, keys):
+    num = sum(float((hip[k].detach().double().cpu() - ref[k].detach().double().cpu()).norm() ** 2)
+              for k in keys)
+    den = sum(float(ref[k].detach().double().cpu().norm() ** 2) for k in keys)
+    return (num / max(den, 1e-300)) ** 0.5
+
+
+def median_live_grad(ref_grads: dict) -> float:
+    per = [g.abs().mean().item() for k, g in ref_grads.items()
+           if g.numel() and not structurally_zero(k)]
+    per = [v for v in per if v > 0]
+    return float(np.median(per)) if per else 0.0

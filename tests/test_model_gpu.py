@@ -1,0 +1,269 @@
+"""GPU parity: the HIP path (C ABI through the drop-in modules) against the CPU
+oracle (fp64) on identical deterministic weights / inputs.
+
+Tolerances (fp32 kernels; the north_star bound is 1e-4 fp32 on outputs / Dice):
+  well-conditioned cases (eval mode, single blocks, loss, Adam): absolute bounds
+  (probabilities / Dice 1e-4 vs the reference's own outputs, see each test);
+  ill-conditioned training-mode BatchNorm over few values (whole model at
+  2x3x32x32, Cfg1 train at B = 1): every output / gradient / running statistic
+  within 4x the reference's OWN fp32 error (the fp32 oracle runs the same ATen
+  ops as the reference) of the fp64 oracle, plus 1e-4 of the tensor's scale.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import parity_util as PU  # noqa: E402
+from parity_util import O  # noqa: E402
+from accunet import model as M  # noqa: E402
+from accunet.loss import WeightedDiceBCE  # noqa: E402
+from accunet.optim import FusedAdam  # noqa: E402
+
+DEV = "cuda"
+GOLD = os.path.join(HERE, "golden")
+
+
+def _hip_model(variant, sd, nf, n_ch=3):
+    m = M.VARIANTS[variant](n_ch, 1, n_filts=nf)
+    m.load_state_dict(sd)
+    return m.to(DEV)
+
+
+@pytest.mark.parametrize("variant", ["canonical", "script", "lite", "w"])
+def test_golden_config_loss_and_outputs_match_reference(variant):
+    """The golden configuration (n_filts 8, 2x3x32x32): the reference's own fp32
+    outputs / loss / Dice (tests/golden/model_*_nf8.npz) vs the HIP path."""
+    g = np.load(os.path.join(GOLD, f"model_{variant}_nf8.npz"))
+    spec = O.param_spec(variant, 3, 1, 8)
+    sd = O.det_state_dict(spec, seed=0)
+    x = O.det_input((2, 3, 32, 32), "golden-x")
+    mask = O.det_mask((2, 1, 32, 32), "golden-mask", p=0.4)
+    m = _hip_model(variant, sd, 8).train()
+    crit = WeightedDiceBCE(0.5, 0.5)
+    out = m(x.to(DEV))
+    loss = crit(out, mask.to(DEV))
+    assert abs(loss.item() - float(g["loss"])) < 1e-5
+    # 2x2 BatchNorm level: the reference itself is 8e-4 (3e-3 for logits) from fp64
+    o64, _, _, _ = PU.oracle_run(variant, sd, x, None)
+    e_ref = np.abs(g["out_train"] - o64.numpy()).max()
+    e_hip = (out.detach().double().cpu() - o64).abs().max().item()
+    assert e_hip <= 4 * e_ref + 1e-5, (e_hip, e_ref)
+    # hard masks (sigmoid >= 0.5) may differ only where the reference itself is
+    # ambiguous (|sigmoid(out) - 0.5| within its own fp32 error); then Dice within 1e-4
+    p_ref = torch.sigmoid(torch.from_numpy(g["out_train"]).double())
+    p_hip = torch.sigmoid(out.detach().double().cpu())
+    flip = (p_ref >= 0.5) != (p_hip >= 0.5)
+    ambiguous = (torch.sigmoid(o64) - 0.5).abs() <= 4 * e_ref + 1e-6
+    assert bool((~flip | ambiguous).all())
+    if not bool(flip.any()):
+        assert abs(crit._show_dice(out.detach(), mask.clone().to(DEV)).item()
+                   - float(g["show_dice"])) < 1e-4
+        assert abs(O.dice_on_batch(mask.clone(), out.detach().cpu())
+                   - float(g["dice_on_batch"])) < 1e-4
+
+
+@pytest.mark.parametrize("variant", ["canonical", "script", "lite", "w"])
+def test_whole_model_train_step_matches_oracle(variant):
+    """Full train step (fwd + loss + bwd) at n_filts 8, 4x3x64x64 against the fp64
+    oracle, with the reference's OWN fp32 error (fp32 oracle = the reference's ATen
+    ops) as the yardstick:
+      - whole gradient vector: ||g_hip - g64|| <= 3 ||g32 - g64|| + 1e-6 ||g64||
+      - every tensor (outputs, gradients, BN running stats):
+          max|hip - 64| <= 4 max|32 - 64| + 1e-4 max|64| + 0.05 * median_k mean|g_k|
+        (the absolute floor covers near-structurally-zero gradients; SE gate fc1 biases,
+        which a batch-wide BatchNorm nearly cancels, get 0.5 * median)
+      - loss within 1e-6 relative of the fp64 oracle."""
+    nf, B, S = 8, 4, 64
+    spec = O.param_spec(variant, 3, 1, nf)
+    sd = O.det_state_dict(spec, seed=0)
+    x = O.det_input((B, 3, S, S), "golden-x")
+    mask = O.det_mask((B, 1, S, S), "golden-mask", p=0.4)
+    ref_out, ref_loss, ref_grads, ref_sd = PU.oracle_run(variant, sd, x, mask)
+    r32_out, r32_loss, r32_grads, r32_sd = PU.oracle_run(variant, sd, x, mask,
+                                                        dtype=torch.float32)
+    m = _hip_model(variant, sd, nf).train()
+    out = m(x.to(DEV))
+    loss = WeightedDiceBCE(0.5, 0.5)(out, mask.to(DEV))
+    loss.backward()
+    assert abs(loss.item() - ref_loss.item()) <= 1e-6 * abs(ref_loss.item()) + 1e-7
+    hip = {"out": out}
+    r64 = {"out": ref_out}
+    r32 = {"out": r32_out}
+    gkeys = []
+    for k, p in m.named_parameters():
+        hip["grad:" + k] = p.grad if p.grad is not None else torch.zeros_like(p)
+        r64["grad:" + k] = ref_grads[k]
+        r32["grad:" + k] = r32_grads[k]
+        gkeys.append("grad:" + k)
+    e_glob_h = PU.global_rel_err(hip, r64, gkeys)
+    e_glob_r = PU.global_rel_err(r32, r64, gkeys)
+    assert e_glob_h <= 3 * e_glob_r + 1e-6, (e_glob_h, e_glob_r)
+    med = PU.median_live_grad(ref_grads)
+    # SE gate biases: d/d(fc1.bias) = sum over the batch of per-sample terms that the
+    # SE's own training BatchNorm nearly cancels (a batch-uniform gate shift is
+    # normalised away) -> near-structural-zero, cancellation-dominated; their
+    # fc1.weight counterparts (which see per-sample means) are held to the normal floor
+    floor = {k: (0.5 if k.endswith("fc1.bias") else 0.05) * med for k in gkeys}
+    msd = m.state_dict()
+    for k, v in ref_sd.items():
+        if k.endswith(("running_mean", "running_var")):
+            hip["buf:" + k] = msd[k]
+            r64["buf:" + k] = v
+            r32["buf:" + k] = r32_sd[k]
+        elif k.endswith("num_batches_tracked"):
+            assert int(msd[k]) == int(v), k
+    rows = PU.compare_vs_reference_fp32(hip, r64, r32, abs_floor=floor)
+    bad = [r for r in rows if not r[4]]
+    assert not bad, sorted(bad, key=lambda r: -r[1] / r[3])[:8]
+    # eval mode uses the (updated) running statistics
+    m.eval()
+    with torch.no_grad():
+        oe = m(x.to(DEV)).double().cpu()
+    ref_e, _, _, _ = PU.oracle_run(variant, ref_sd, x, None, training=False)
+    r32_e, _, _, _ = PU.oracle_run(variant, r32_sd, x, None, training=False,
+                                   dtype=torch.float32)
+    e_h = (oe - ref_e).abs().max().item()
+    e_r = (r32_e.double() - ref_e).abs().max().item()
+    assert e_h <= 4 * e_r + 1e-5, (e_h, e_r)
+
+
+def test_cfg1_lite_forward_and_dice_match_reference_golden():
+    """BASELINE configs[0]: ACC_UNet_Lite forward on 1x3x128x128 (Dice vs mask).
+
+    eval: probabilities within 1e-4 of the reference's own output (golden), Dice
+    within 1e-4. train (B = 1: BatchNorm over 64 values at 8x8): the reference's
+    fp32 output itself sits 1.4e-4 from the fp64 oracle, so probabilities are held
+    to 4x that distance from the fp64 oracle; Dice still within 1e-4."""
+    g = np.load(os.path.join(GOLD, "cfg1_lite.npz"))
+    spec = O.param_spec("lite", 3, 1, 32)
+    sd0 = O.det_state_dict(spec, seed=1)
+    xc = O.det_input((1, 3, 128, 128), "cfg1-x")
+    x = xc.to(DEV)
+    mk = O.det_mask((1, 1, 128, 128), "cfg1-mask", p=0.5)
+    crit = WeightedDiceBCE(0.5, 0.5)
+    for mode in ("eval", "train"):
+        m = _hip_model("lite", sd0, 32).train(mode == "train")
+        with torch.no_grad():
+            probs = m(x)
+        p = probs.double().cpu()
+        if mode == "eval":
+            d = np.abs(p.numpy() - g["probs_eval"]).max()
+            assert d < 1e-4, (mode, d)
+        else:
+            with torch.no_grad():
+                o64, _, _, _ = PU.oracle_run("lite", sd0, xc, None, training=True)
+            e_ref = np.abs(g["probs_train"] - o64.numpy()).max()
+            e_hip = (p - o64).abs().max().item()
+            assert e_hip <= 4 * e_ref + 1e-5, (e_hip, e_ref)
+        sd = crit._show_dice(probs, mk.clone().to(DEV)).item()
+        assert abs(sd - float(g[f"show_dice_{mode}"])) < 1e-4
+        assert abs(O.dice_on_batch(mk.clone(), probs.cpu()) - float(g[f"dice_on_batch_{mode}"])) < 1e-4
+        assert abs(crit(probs, mk.to(DEV)).item() - float(g[f"loss_{mode}"])) < 1e-5
+
+
+def test_training_trajectory_matches_reference_golden():
+    """3 Adam steps of the script variant (n_channels 1, 2x1x64x64) vs the reference."""
+    g = np.load(os.path.join(GOLD, "traj_script.npz"))
+    spec = O.param_spec("script", 1, 1, 32)
+    sd = O.det_state_dict(spec, seed=2)
+    m = _hip_model("script", sd, 32, n_ch=1).train()
+    opt = FusedAdam([p for p in m.parameters() if p.requires_grad], lr=1e-3)
+    crit = WeightedDiceBCE(0.5, 0.5)
+    x = O.det_input((2, 1, 64, 64), "traj-x").to(DEV)
+    mk = O.det_mask((2, 1, 64, 64), "traj-mask", p=0.3).to(DEV)
+    losses = []
+    for _ in range(3):
+        out = m(x)
+        loss = crit(out, mk)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    # Adam divides every gradient by its own RMS, so parameters whose true gradient is
+    # ~0 take lr-sized steps along their rounding noise: even the fp64 oracle departs
+    # from the reference's fp32 trajectory by 1.6e-3 at step 2 (1.8e-3 at step 3).
+    # Step 1 (no update yet) is pinned tightly, later steps to that inherent spread.
+    assert abs(losses[0] - g["losses"][0]) < 1e-5, (losses, list(g["losses"]))
+    assert abs(losses[1] - g["losses"][1]) < 4e-3, (losses, list(g["losses"]))
+    assert abs(losses[2] - g["losses"][2]) < 1e-2, (losses, list(g["losses"]))
+    assert losses[2] < losses[0]  # it trains
+
+
+def test_fused_adam_matches_torch_adam():
+    torch.manual_seed(0)
+    ps = [torch.randn(s, device=DEV) for s in ((300, 7), (5,), (40000,))]
+    qs = [p.clone() for p in ps]
+    pa = [torch.nn.Parameter(p) for p in ps]
+    pb = [torch.nn.Parameter(q) for q in qs]
+    oa = FusedAdam(pa, lr=1e-3)
+    ob = torch.optim.Adam(pb, lr=1e-3, foreach=False)
+    for it in range(4):
+        for a, b in zip(pa, pb):
+            gr = torch.randn_like(a) * (it + 1)
+            a.grad = gr.clone()
+            b.grad = gr.clone()
+        oa.step()
+        ob.step()
+    for a, b in zip(pa, pb):
+        assert (a - b).abs().max().item() < 1e-6
+
+
+def test_loss_matches_oracle_including_binarised_masks():
+    torch.manual_seed(3)
+    x = torch.randn(3, 1, 16, 16, dtype=torch.float64)
+    for scale in (1.0, 255.0):
+        t = (torch.rand(3, 1, 16, 16) < 0.3).double() * scale
+        xr = x.clone().requires_grad_(True)
+        lr = O.dice_bce_loss(xr, t)
+        lr.backward()
+        xh = x.float().to(DEV).requires_grad_(True)
+        lh = WeightedDiceBCE(0.5, 0.5)(xh, t.float().to(DEV))
+        lh.backward()
+        assert abs(lh.item() - lr.item()) < 1e-5
+        assert (xh.grad.double().cpu() - xr.grad).abs().max().item() < 1e-6
+
+
+@pytest.mark.parametrize("k,cin,cout", [(1, 16, 32), (2, 8, 16), (3, 8, 8), (3, 3, 16)])
+def test_hanc_block_matches_oracle(k, cin, cout):
+    torch.manual_seed(0)
+    blk = M.HANCBlock(cin, cout, k=k, inv_fctr=3)
+    spec = [(n, tuple(t.shape)) for n, t in blk.state_dict().items()]
+    sd = O.det_state_dict(spec, seed=5)
+    blk.load_state_dict(sd)
+    blk = blk.to(DEV).train()
+    x = O.det_input((2, cin, 16, 16), f"hb{k}")
+    xh = x.to(DEV).requires_grad_(True)
+    out = blk(xh)
+    go = O.det_input(tuple(out.shape), "hb-go").to(DEV)
+    (out * go).sum().backward()
+    sdo = {n: (v.double().requires_grad_(not n.endswith(PU.BUFFER_LEAVES)) if v.is_floating_point() else v)
+           for n, v in sd.items()}
+    # oracle names are prefixed by the block path; bind through a prefix-less dict
+    xr = x.double().requires_grad_(True)
+    ref = O.hanc_block(xr, {("b." + n): v for n, v in sdo.items()}, "b", k, True)
+    (ref * go.double().cpu()).sum().backward()
+    assert (out.detach().double().cpu() - ref.detach()).abs().max().item() < 1e-4
+    assert (xh.grad.double().cpu() - xr.grad).abs().max().item() < 1e-4 * max(1.0, xr.grad.abs().max().item())
+    for n, p in blk.named_parameters():
+        gr = sdo[n].grad
+        if gr is None or PU.structurally_zero("x." + n):
+            continue
+        err = (p.grad.double().cpu() - gr).abs().max().item()
+        assert err < 2e-3 * gr.abs().max().item() + 1e-6, n
+
+
+def test_maxpool_first_max_tie_rule():
+    x = torch.zeros(1, 4, 4, 8, device=DEV)  # all ties: gradient goes to the top-left element
+    from accunet import ops
+    xr = x.clone().requires_grad_(True)
+    y = ops.pool2(xr)
+    y.sum().backward()
+    g = xr.grad[0, :, :, 0].cpu()
+    assert g[0, 0] == 1 and g[0, 1] == 0 and g[1, 0] == 0 and g[1, 1] == 0
