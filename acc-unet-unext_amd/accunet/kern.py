@@ -94,7 +94,8 @@ def gemm(M: int, N: int, K: int, *, a: Sequence[torch.Tensor], lda: Sequence[int
     ws = None
     ws_elems = 0
     if allow_split:
-        ws_elems = min(64, max(1, K // 64)) * M * N
+        # room for up to 1024 K-slabs (the driver targets ~1024 workgroups), capped at 256 MB
+        ws_elems = min(1024, max(1, K // 64)) * M * N
         ws_elems = min(ws_elems, 1 << 26)
         ws = workspace(ws_elems, c.device)
     call("accunet_gemm", ctypes.byref(d), _p(ws), ws_elems, _stream())
@@ -110,9 +111,10 @@ def stream_rows(P: int, C: int) -> int:
 
 
 def partial_ws_elems(R: int, Wd: int) -> int:
+    """mirror of accunet_partials_ws_elems (csrc/bn.hip)."""
     import math
-    r1 = math.ceil(R / 256)
-    return (r1 + math.ceil(r1 / 256) + 2) * Wd
+    r1 = math.ceil(R / 32)
+    return (r1 + math.ceil(r1 / 32) + 2) * Wd
 
 
 def bn_finalize(part: Optional[torch.Tensor], R: int, C: int, count: float, gamma, beta,

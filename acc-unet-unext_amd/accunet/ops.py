@@ -281,7 +281,9 @@ class _DWConvFn(torch.autograd.Function):
         if cfg.want_stats:
             stats = _stats((kern.dw3x3_rows(B, H, W, C), 2, C), z)
         pro = cfg.pro
-        with _prof.region(f"dw3x3_fwd B{B} {H}x{W} C{C}", kernel="dw3x3_fwd_kernel",
+        # csrc/dwconv.hip picks the LDS-tiled kernel whenever C % 32 == 0
+        kname = "dw3x3_tile_fwd_kernel" if C % 32 == 0 else "dw3x3_fwd_kernel"
+        with _prof.region(f"dw3x3_fwd B{B} {H}x{W} C{C}", kernel=kname,
                           shape=f"{B}x{H}x{W}x{C}", bytes_alg=2.0 * 4 * B * H * W * C):
             kern.dw3x3_fwd(z, weight, bias, pro.st[2] if pro.active else None,
                            pro.st[3] if pro.active else None, pro.act, 0, Z, stats, B, H, W, C)

@@ -25,10 +25,20 @@ class FusedAdam(torch.optim.Optimizer):
         self._tables = {}
 
     def _table(self, group_idx, params):
-        key = (group_idx, tuple(p.data_ptr() for p in params),
-               tuple(p.grad.data_ptr() for p in params))
+        # The chunk map depends only on the parameter set; gradient pointers change
+        # every step when autograd hands over fresh gradient tensors, so only the
+        # pointer table is re-uploaded (pinned, async: no host sync).
+        key = (group_idx, tuple(p.data_ptr() for p in params))
+        gkey = tuple(p.grad.data_ptr() for p in params)
         t = self._tables.get(group_idx)
         if t is not None and t[0] == key:
+            tab, ct, cs, n = t[1]
+            if t[2] != gkey:
+                rows = [[p.data_ptr(), p.grad.data_ptr(), self.state[p]["exp_avg"].data_ptr(),
+                         self.state[p]["exp_avg_sq"].data_ptr(), p.numel()] for p in params]
+                host = torch.tensor(rows, dtype=torch.int64).pin_memory()
+                tab.copy_(host, non_blocking=True)
+                self._tables[group_idx] = (key, t[1], gkey)
             return t[1]
         dev = params[0].device
         rows = []
@@ -45,7 +55,7 @@ class FusedAdam(torch.optim.Optimizer):
         ct = torch.tensor(chunk_t, dtype=torch.int32).to(dev)
         cs = torch.tensor(chunk_s, dtype=torch.int64).to(dev)
         entry = (tab, ct, cs, len(chunk_t))
-        self._tables[group_idx] = (key, entry)
+        self._tables[group_idx] = (key, entry, gkey)
         return entry
 
     @torch.no_grad()

@@ -21,21 +21,17 @@ class TrainStep:
         self.reducer = reducer
         self.criterion = WeightedDiceBCE(dice_weight, bce_weight)
         params = [p for p in model.parameters() if p.requires_grad]
-        if reducer is None:
-            # persistent gradient storage (stable pointers for the fused optimizer)
-            total = sum(p.numel() for p in params)
-            self.flat = torch.zeros(total, dtype=torch.float32, device=params[0].device)
-            o = 0
-            for p in params:
-                p.grad = self.flat[o:o + p.numel()].view_as(p)
-                o += p.numel()
+        # single GPU: gradients are the tensors the backward kernels produce
+        # (AccumulateGrad steals them, no per-parameter add); with a reducer they
+        # are views of its flat all-reduce buffer.
         self.opt = FusedAdam(params, lr=lr)
 
     def zero_grad(self):
         if self.reducer is not None:
             self.reducer.zero_grad()
         else:
-            self.flat.zero_()
+            for p in self.opt.param_groups[0]["params"]:
+                p.grad = None
 
     def __call__(self, images, masks):
         self.model.train(True)

@@ -69,10 +69,10 @@ template <typename T>
 const T* reduce_partials_t(const T* part, int R, int Wd, T* ws, int* Rout, hipStream_t s) {
   const T* cur = part;
   int rows = R;
-  T* bufs[2] = {ws, ws + (size_t)ceil_div(R, 256) * Wd};
+  T* bufs[2] = {ws, ws + (size_t)ceil_div(R, 32) * Wd};
   int which = 0;
   while (rows > 64) {
-    int RB = 256;
+    const int RB = 32;  // many small blocks: the reduction is latency-, not bandwidth-bound
     int nb = ceil_div(rows, RB);
     hipLaunchKernelGGL(colreduce_kernel<T>, dim3(nb, ceil_div(Wd, 64)), dim3(256), 0, s, cur,
                        bufs[which], rows, Wd, RB);
@@ -90,7 +90,8 @@ const float* reduce_partials(const float* part, int R, int Wd, float* ws, int* R
 }
 
 size_t accunet_partials_ws_elems(int R, int Wd) {
-  return (size_t)(ceil_div(R, 256) + ceil_div(ceil_div(R, 256), 256) + 2) * Wd;
+  int r1 = ceil_div(R, 32);
+  return (size_t)(r1 + ceil_div(r1, 32) + 2) * Wd;
 }
 
 // ---------------------------------------------------------------------------

@@ -263,6 +263,287 @@ __global__ void dw_wgrad_finish_kernel(const float* __restrict__ sums, int C, fl
   if (db) db[c] = sums[9 * C + c];
 }
 
+// ----------------------------------------------------------------------------
+// LDS-tiled kernels (C % 32 == 0: every ACC-UNet HANC width except cnv11's 9).
+// A block owns TR=8 output rows x TP pixels x TCQ channel quads; it first pulls the
+// whole (TR+2) x (TP+2) x TCQ input halo tile into LDS with ~11 independent 16-byte
+// loads per thread (prologue BN+act applied on the way, zero padding after the
+// activation), so each CU keeps >100 KB of HBM reads in flight instead of the
+// ~3 dependent loads per row of the register-window kernel above; then every
+// thread slides its 3x3 window down LDS. Tiles are handed out XCD-contiguously
+// (consecutive workgroup ids land on different XCDs; the remap gives each XCD a
+// contiguous run of tiles so halo rows/columns shared by neighbours hit its L2).
+// ----------------------------------------------------------------------------
+struct DwTGeom {
+  int B, H, W, C;
+  int tilesW, tilesH;
+  int remap;  // ntiles % 8 == 0: XCD-contiguous tile order
+};
+
+ACC_DEV int dw_tile_id(const DwTGeom& g) {
+  int bid = blockIdx.x;
+  if (g.remap) {
+    int per = gridDim.x >> 3;
+    bid = (bid & 7) * per + (bid >> 3);
+  }
+  return bid;
+}
+
+template <int TCQ>
+struct DwT {
+  static constexpr int TP = 256 / TCQ;  // output pixels per tile row
+  static constexpr int IP = TP + 2;
+  static constexpr int IR = DW_TR + 2;
+  static constexpr int N4 = IR * IP * TCQ;  // float4 elements of the input tile
+  static constexpr int NK = (N4 + 255) / 256;
+};
+
+// load the activated input tile a = act(x*sc+sh) (zero outside the image) into LDS
+template <int TCQ>
+ACC_DEV void dw_fill_tile(float4* __restrict__ tile, const float* __restrict__ x,
+                          const float* __restrict__ sc, const float* __restrict__ sh, int act,
+                          const DwTGeom& g, int b, int h0, int w0, int c0) {
+  typedef DwT<TCQ> T;
+  const int tid = threadIdx.x;
+  const int q = tid % TCQ;  // 256 % TCQ == 0: a thread always loads the same quad
+  float4 ps = make_float4(1.f, 1.f, 1.f, 1.f), pb = make_float4(0.f, 0.f, 0.f, 0.f);
+  const bool pro = sc != nullptr;
+  if (pro) {
+    ps = ld4(sc + c0 + 4 * q);
+    pb = ld4(sh + c0 + 4 * q);
+  }
+  float4 v[T::NK];
+  bool in[T::NK];
+#pragma unroll
+  for (int k = 0; k < T::NK; ++k) {
+    const int i = tid + 256 * k;
+    const int rp = i / TCQ;
+    const int p = rp % T::IP, r = rp / T::IP;
+    const int hh = h0 - 1 + r, ww = w0 - 1 + p;
+    in[k] = (i < T::N4) && hh >= 0 && hh < g.H && ww >= 0 && ww < g.W;
+    v[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (in[k]) v[k] = ld4(x + (((long)b * g.H + hh) * g.W + ww) * g.C + c0 + 4 * q);
+  }
+#pragma unroll
+  for (int k = 0; k < T::NK; ++k) {
+    const int i = tid + 256 * k;
+    if (i < T::N4) {
+      float4 a = v[k];
+      if (pro && in[k]) {
+        a.x = apply_act(a.x * ps.x + pb.x, act);
+        a.y = apply_act(a.y * ps.y + pb.y, act);
+        a.z = apply_act(a.z * ps.z + pb.z, act);
+        a.w = apply_act(a.w * ps.w + pb.w, act);
+      }
+      tile[i] = a;
+    }
+  }
+}
+
+template <int TCQ>
+__global__ void __launch_bounds__(256)
+dw3x3_tile_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
+                      const float* __restrict__ bias, const float* __restrict__ sc,
+                      const float* __restrict__ sh, int act, int flip, float* __restrict__ z,
+                      double* __restrict__ stats, DwTGeom g) {
+  typedef DwT<TCQ> T;
+  __shared__ float4 tile[T::N4 > 1024 ? T::N4 : 1024];
+  const int tid = threadIdx.x;
+  const int q = tid % TCQ, p = tid / TCQ;
+  const int c0 = blockIdx.y * TCQ * 4;
+  const int c = c0 + 4 * q;
+  int t = dw_tile_id(g);
+  const int tw = t % g.tilesW;
+  t /= g.tilesW;
+  const int th = t % g.tilesH;
+  const int b = t / g.tilesH;
+  const int h0 = th * DW_TR, w0 = tw * T::TP;
+  dw_fill_tile<TCQ>(tile, x, sc, sh, act, g, b, h0, w0, c0);
+
+  float k[9][4], bi[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+#pragma unroll
+    for (int tp = 0; tp < 9; ++tp) k[tp][j] = wt[(c + j) * 9 + (flip ? 8 - tp : tp)];
+    bi[j] = bias ? bias[c + j] : 0.f;
+  }
+  __syncthreads();
+  double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+  const int w = w0 + p;
+  if (w < g.W) {
+    float win[3][3][4];
+    auto rd = [&](int r, float (&row)[3][4]) {
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) {
+        float4 a = tile[(r * T::IP + p + dx) * TCQ + q];
+        row[dx][0] = a.x; row[dx][1] = a.y; row[dx][2] = a.z; row[dx][3] = a.w;
+      }
+    };
+    rd(0, win[0]);
+    rd(1, win[1]);
+    const int nr = min(DW_TR, g.H - h0);
+#pragma unroll
+    for (int r = 0; r < DW_TR; ++r) {
+      if (r < nr) {
+        rd(r + 2, win[2]);
+        float o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float acc = bi[j];
+#pragma unroll
+          for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx) acc = fmaf(k[dy * 3 + dx][j], win[dy][dx][j], acc);
+          o[j] = acc;
+          s1[j] += acc;
+          s2[j] += (double)acc * acc;
+        }
+        st4(z + (((long)b * g.H + h0 + r) * g.W + w) * g.C + c, make_float4(o[0], o[1], o[2], o[3]));
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            win[0][dx][j] = win[1][dx][j];
+            win[1][dx][j] = win[2][dx][j];
+          }
+      }
+    }
+  }
+  if (stats) {
+    __syncthreads();  // the tile is reused as the reduction buffer
+    double* red = reinterpret_cast<double*>(tile);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      red[tid * 4 + j] = s1[j];
+      red[1024 + tid * 4 + j] = s2[j];
+    }
+    __syncthreads();
+    if (p == 0) {
+      const long row = (long)(blockIdx.x) * 2 * g.C;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        double a = 0.0, qq = 0.0;
+        for (int i = 0; i < T::TP; ++i) {
+          a += red[(i * TCQ + q) * 4 + j];
+          qq += red[1024 + (i * TCQ + q) * 4 + j];
+        }
+        stats[row + c + j] = a;
+        stats[row + g.C + c + j] = qq;
+      }
+    }
+  }
+}
+
+template <int TCQ>
+__global__ void __launch_bounds__(256)
+dw3x3_tile_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dz,
+                        const float* __restrict__ sc, const float* __restrict__ sh, int act,
+                        float* __restrict__ part, DwTGeom g) {
+  typedef DwT<TCQ> T;
+  __shared__ float4 tile[T::N4 > 1024 ? T::N4 : 1024];
+  const int tid = threadIdx.x;
+  const int q = tid % TCQ, p = tid / TCQ;
+  const int c0 = blockIdx.y * TCQ * 4;
+  const int c = c0 + 4 * q;
+  int t = dw_tile_id(g);
+  const int tw = t % g.tilesW;
+  t /= g.tilesW;
+  const int th = t % g.tilesH;
+  const int b = t / g.tilesH;
+  const int h0 = th * DW_TR, w0 = tw * T::TP;
+  const int w = w0 + p;
+  const int nr = min(DW_TR, g.H - h0);
+  // this thread's dz column (independent loads issued before the tile fill completes)
+  float4 d[DW_TR];
+#pragma unroll
+  for (int r = 0; r < DW_TR; ++r) {
+    d[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (w < g.W && r < nr) d[r] = ld4(dz + (((long)b * g.H + h0 + r) * g.W + w) * g.C + c);
+  }
+  dw_fill_tile<TCQ>(tile, x, sc, sh, act, g, b, h0, w0, c0);
+  __syncthreads();
+  float acc[10][4];
+#pragma unroll
+  for (int i = 0; i < 10; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+  if (w < g.W) {
+    float win[3][3][4];
+    auto rd = [&](int r, float (&row)[3][4]) {
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) {
+        float4 a = tile[(r * T::IP + p + dx) * TCQ + q];
+        row[dx][0] = a.x; row[dx][1] = a.y; row[dx][2] = a.z; row[dx][3] = a.w;
+      }
+    };
+    rd(0, win[0]);
+    rd(1, win[1]);
+#pragma unroll
+    for (int r = 0; r < DW_TR; ++r) {
+      if (r < nr) {
+        rd(r + 2, win[2]);
+        const float dv[4] = {d[r].x, d[r].y, d[r].z, d[r].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+#pragma unroll
+          for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx)
+              acc[dy * 3 + dx][j] = fmaf(dv[j], win[dy][dx][j], acc[dy * 3 + dx][j]);
+          acc[9][j] += dv[j];
+        }
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            win[0][dx][j] = win[1][dx][j];
+            win[1][dx][j] = win[2][dx][j];
+          }
+      }
+    }
+  }
+  __syncthreads();  // tile -> reduction buffer [256][4] per tap (two taps per pass)
+  float* red = reinterpret_cast<float*>(tile);
+  for (int i = 0; i < 10; i += 2) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      red[tid * 4 + j] = acc[i][j];
+      red[1024 + tid * 4 + j] = acc[i + 1][j];
+    }
+    __syncthreads();
+    if (p < 2) {  // p = 0: tap i, p = 1: tap i+1
+      float a4[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float a = 0.f;
+        for (int k2 = 0; k2 < T::TP; ++k2) a += red[p * 1024 + (k2 * TCQ + q) * 4 + j];
+        a4[j] = a;
+      }
+      st4(part + ((long)blockIdx.x * 10 + i + p) * g.C + c, make_float4(a4[0], a4[1], a4[2], a4[3]));
+    }
+    __syncthreads();
+  }
+}
+
+// tile-kernel selection: 0 = none (register-window kernel), else TCQ
+static int dw_tile_tcq(int W, int C) {
+  if (C % 32) return 0;
+  int CQ = C / 4;
+  if (W <= 16 && CQ % 16 == 0) return 16;
+  return 8;
+}
+
+static DwTGeom dw_tgeom(int B, int H, int W, int C, int tcq, dim3* grid) {
+  DwTGeom g;
+  g.B = B; g.H = H; g.W = W; g.C = C;
+  g.tilesW = ceil_div(W, 256 / tcq);
+  g.tilesH = ceil_div(H, DW_TR);
+  long nt = (long)B * g.tilesH * g.tilesW;
+  g.remap = (nt % 8 == 0) ? 1 : 0;
+  *grid = dim3((unsigned)nt, C / 4 / tcq);
+  return g;
+}
+
 static DwGeom dw_geom(int B, int H, int W, int C, int V, dim3* grid) {
   DwGeom g;
   g.B = B; g.H = H; g.W = W; g.C = C;
@@ -279,7 +560,9 @@ static DwGeom dw_geom(int B, int H, int W, int C, int V, dim3* grid) {
 
 extern "C" int accunet_dw3x3_rows(int B, int H, int W, int C) {
   dim3 grid;
-  dw_geom(B, H, W, C, (C % 4 == 0) ? 4 : 1, &grid);
+  int tcq = dw_tile_tcq(W, C);
+  if (tcq) dw_tgeom(B, H, W, C, tcq, &grid);
+  else dw_geom(B, H, W, C, (C % 4 == 0) ? 4 : 1, &grid);
   return (int)grid.x;
 }
 
@@ -287,8 +570,19 @@ extern "C" int accunet_dw3x3_fwd(const float* x, const float* wt, const float* b
                                  const float* sc, const float* sh, int act, int flip, float* z,
                                  double* stats, int B, int H, int W, int C, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  int V = (C % 4 == 0) ? 4 : 1;
   dim3 grid;
+  int tcq = dw_tile_tcq(W, C);
+  if (tcq) {
+    DwTGeom tg = dw_tgeom(B, H, W, C, tcq, &grid);
+    if (tcq == 16)
+      hipLaunchKernelGGL(dw3x3_tile_fwd_kernel<16>, grid, dim3(256), 0, s, x, wt, bias, sc, sh, act,
+                         flip, z, stats, tg);
+    else
+      hipLaunchKernelGGL(dw3x3_tile_fwd_kernel<8>, grid, dim3(256), 0, s, x, wt, bias, sc, sh, act,
+                         flip, z, stats, tg);
+    return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+  }
+  int V = (C % 4 == 0) ? 4 : 1;
   DwGeom g = dw_geom(B, H, W, C, V, &grid);
   if (V == 4)
     hipLaunchKernelGGL(dw3x3_fwd_kernel<4>, grid, dim3(256), 0, s, x, wt, bias, sc, sh, act, flip,
@@ -299,6 +593,7 @@ extern "C" int accunet_dw3x3_fwd(const float* x, const float* wt, const float* b
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 
+extern "C" int accunet_dw3x3_rows(int B, int H, int W, int C);
 size_t dw_wgrad_ws(int B, int H, int W, int C) {
   int R = accunet_dw3x3_rows(B, H, W, C);
   return (size_t)R * 10 * C + accunet_partials_ws_elems(R, 10 * C) + 10 * (size_t)C;
@@ -312,13 +607,21 @@ extern "C" int accunet_dw3x3_wgrad(const float* x, const float* dz, const float*
   hipStream_t s = (hipStream_t)stream;
   int V = (C % 4 == 0) ? 4 : 1;
   dim3 grid;
-  DwGeom g = dw_geom(B, H, W, C, V, &grid);
+  int tcq = dw_tile_tcq(W, C);
+  DwTGeom tg;
+  DwGeom g;
+  if (tcq) tg = dw_tgeom(B, H, W, C, tcq, &grid);
+  else g = dw_geom(B, H, W, C, V, &grid);
   int R = (int)grid.x;
   if (ws_elems < dw_wgrad_ws(B, H, W, C)) return ACC_EBADARG;
   float* part = ws;
   float* scratch = ws + (size_t)R * 10 * C;
   float* sums = scratch + accunet_partials_ws_elems(R, 10 * C);
-  if (V == 4)
+  if (tcq == 16)
+    hipLaunchKernelGGL(dw3x3_tile_wgrad_kernel<16>, grid, dim3(256), 0, s, x, dz, sc, sh, act, part, tg);
+  else if (tcq == 8)
+    hipLaunchKernelGGL(dw3x3_tile_wgrad_kernel<8>, grid, dim3(256), 0, s, x, dz, sc, sh, act, part, tg);
+  else if (V == 4)
     hipLaunchKernelGGL(dw3x3_wgrad_kernel<4>, grid, dim3(256), 0, s, x, dz, sc, sh, act, part, g);
   else
     hipLaunchKernelGGL(dw3x3_wgrad_kernel<1>, grid, dim3(256), 0, s, x, dz, sc, sh, act, part, g);

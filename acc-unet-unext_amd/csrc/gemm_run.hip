@@ -3,16 +3,43 @@
 #include "gemm_dispatch.h"
 #include <string.h>
 
-__global__ void __launch_bounds__(256)
+// One block = 64 consecutive outputs x 16 slab groups (1024 threads): thread
+// (c, g) sums slabs g, g+16, ... in order, then the 16 group sums are added in
+// fixed order -> deterministic, and S-way parallel enough that a 32x32 weight
+// gradient split 1024 ways does not serialise on one thread per output.
+#define SPLITK_COLS 64
+#define SPLITK_GROUPS 16
+__global__ void __launch_bounds__(1024)
 splitk_reduce_kernel(const float* __restrict__ ws, float* __restrict__ C, int M, int N, int ldc,
                      int S, size_t zstride) {
-  long total = (long)M * N;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
-       i += (long)gridDim.x * blockDim.x) {
-    float acc = 0.f;
-    for (int z = 0; z < S; ++z) acc += ws[z * zstride + i];
+  __shared__ float part[SPLITK_GROUPS][SPLITK_COLS];
+  const int c = threadIdx.x & (SPLITK_COLS - 1), g = threadIdx.x / SPLITK_COLS;
+  const long total = (long)M * N;
+  const long i = (long)blockIdx.x * SPLITK_COLS + c;
+  float acc = 0.f;
+  if (i < total) {
+    const float* src = ws + i;
+    int z = g;
+    for (; z + 3 * SPLITK_GROUPS < S; z += 4 * SPLITK_GROUPS) {
+      float a0 = src[(size_t)z * zstride];
+      float a1 = src[(size_t)(z + SPLITK_GROUPS) * zstride];
+      float a2 = src[(size_t)(z + 2 * SPLITK_GROUPS) * zstride];
+      float a3 = src[(size_t)(z + 3 * SPLITK_GROUPS) * zstride];
+      acc += a0;
+      acc += a1;
+      acc += a2;
+      acc += a3;
+    }
+    for (; z < S; z += SPLITK_GROUPS) acc += src[(size_t)z * zstride];
+  }
+  part[g][c] = acc;
+  __syncthreads();
+  if (g == 0 && i < total) {
+    float s = part[0][c];
+#pragma unroll
+    for (int k = 1; k < SPLITK_GROUPS; ++k) s += part[k][c];
     int m = (int)(i / N), n = (int)(i - (long)m * N);
-    C[(size_t)m * ldc + n] = acc;
+    C[(size_t)m * ldc + n] = s;
   }
 }
 
@@ -111,9 +138,9 @@ int gemm_run(GemmParams p, int amode, int bmode, int pro_a, int pro_b, bool allo
   hipLaunchKernelGGL(tab[t], grid, dim3(GEMM_THREADS), 0, stream, p);
   if (S > 1) {
     long total = (long)p.M * p.N;
-    int blocks = (int)((total + 255) / 256);
-    if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, stream, ws, Cfinal, p.M,
+    long blocks = (total + SPLITK_COLS - 1) / SPLITK_COLS;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)blocks), dim3(SPLITK_COLS * SPLITK_GROUPS),
+                       0, stream, ws, Cfinal, p.M,
                        p.N, ldc_final, S, p.zstride);
   }
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;

@@ -105,78 +105,105 @@ se_reduce_kernel(const float* __restrict__ z, const float* __restrict__ sc,
   block_chan_reduce2<V>(t, a, q, part, blockIdx.x, g.C);
 }
 
-// mid forward. One block of 256 threads. Writes the SeSave state.
+// chunk partials -> per-(b,c) sums: block = 64 channels x 4 chunk groups of one
+// sample; each group sums its chunks in order, the 4 group sums are added in order.
 __global__ void __launch_bounds__(256)
-se_mid_kernel(const double* __restrict__ part, SeGeom g, int Cr, const float* __restrict__ w1,
-              const float* __restrict__ b1, const float* __restrict__ w2,
-              const float* __restrict__ b2, const float* __restrict__ gamma,
-              const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar,
-              float momentum, float eps, int training, float* __restrict__ save) {
-  const int B = g.B, C = g.C;
-  SeSave sv = se_save_view(save, B, C, Cr);
-  const int tid = threadIdx.x;
-  // 1) S, Q (fp64)
-  for (int i = tid; i < B * C; i += 256) {
-    int b = i / C, c = i % C;
-    double s1 = 0.0, s2 = 0.0;
-    for (int k = 0; k < g.NCH; ++k) {
+se_part_sum_kernel(const double* __restrict__ part, SeGeom g, double* __restrict__ o1,
+                   double* __restrict__ o2) {
+  __shared__ double r1[4][64], r2[4][64];
+  const int C = g.C, b = blockIdx.y, t = threadIdx.x;
+  const int c = blockIdx.x * 64 + (t & 63), grp = t >> 6;
+  double s1 = 0.0, s2 = 0.0;
+  if (c < C) {
+    for (int k = grp; k < g.NCH; k += 4) {
       const double* pr = part + ((long)(b * g.NCH + k) * 2) * C;
       s1 += pr[c];
       s2 += pr[C + c];
     }
-    sv.S[i] = s1;
-    sv.Q[i] = s2;
   }
+  r1[grp][t & 63] = s1;
+  r2[grp][t & 63] = s2;
   __syncthreads();
-  // 2) fc1 on the channel means (pre-activation saved)
-  for (int i = tid; i < B * Cr; i += 256) {
-    int b = i / Cr, j = i % Cr;
-    float acc = b1[j];
+  if (grp == 0 && c < C) {
+    o1[b * C + c] = ((r1[0][t] + r1[1][t]) + r1[2][t]) + r1[3][t];
+    o2[b * C + c] = ((r2[0][t] + r2[1][t]) + r2[2][t]) + r2[3][t];
+  }
+}
+
+// mid forward, part 1: one block per sample b — the channel means (from the
+// per-(b,c) sums S), fc1 (+LeakyReLU) and fc2 (+sigmoid) of that sample.
+__global__ void __launch_bounds__(256)
+se_mid_gate_kernel(SeGeom g, int Cr,
+                   const float* __restrict__ w1, const float* __restrict__ b1,
+                   const float* __restrict__ w2, const float* __restrict__ b2,
+                   float* __restrict__ save) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];  // m[C] | h'[Cr]
+  const int B = g.B, C = g.C, b = blockIdx.x, tid = threadIdx.x;
+  SeSave sv = se_save_view(save, B, C, Cr);
+  float* m = sm;
+  float* hp = sm + C;
+  for (int c = tid; c < C; c += 256) m[c] = (float)(sv.S[b * C + c] / g.HW);
+  __syncthreads();
+  // fc1: 4 threads per output, interleaved over the input channels
+  for (int o = tid; o < Cr * 4; o += 256) {
+    int j = o >> 2, part_i = o & 3;
+    float acc = 0.f;
     const float* wr = w1 + (long)j * C;
-    const double* Sb = sv.S + (size_t)b * C;
-    for (int c = 0; c < C; ++c) acc = fmaf(wr[c], (float)(Sb[c] / g.HW), acc);
-    sv.hpre[i] = acc;
+    for (int c = part_i; c < C; c += 4) acc = fmaf(wr[c], m[c], acc);
+    acc += __shfl_xor(acc, 1);
+    acc += __shfl_xor(acc, 2);
+    if (part_i == 0) {
+      acc += b1[j];
+      sv.hpre[b * Cr + j] = acc;
+      hp[j] = lrelu(acc);
+    }
   }
   __syncthreads();
-  // 3) fc2 + sigmoid
-  for (int i = tid; i < B * C; i += 256) {
-    int b = i / C, c = i % C;
+  for (int c = tid; c < C; c += 256) {
     float acc = b2[c];
     const float* wr = w2 + (long)c * Cr;
-    const float* hb = sv.hpre + (size_t)b * Cr;
-    for (int j = 0; j < Cr; ++j) acc = fmaf(wr[j], lrelu(hb[j]), acc);
-    sv.sg[i] = 1.f / (1.f + expf(-acc));
+    for (int j = 0; j < Cr; ++j) acc = fmaf(wr[j], hp[j], acc);
+    sv.sg[b * C + c] = 1.f / (1.f + expf(-acc));
   }
-  __syncthreads();
-  // 4) BN statistics of y = a*s from (S, Q, s), running update, coefficients
+}
+
+// mid forward, part 2: one thread per channel — BatchNorm statistics of y = a*s
+// derived from (S, Q, s), running-stat update, per-(b,c) coefficients.
+__global__ void __launch_bounds__(256)
+se_mid_bn_kernel(SeGeom g, int Cr, const float* __restrict__ gamma,
+                 const float* __restrict__ beta, float* __restrict__ rmean,
+                 float* __restrict__ rvar, float momentum, float eps, int training,
+                 float* __restrict__ save) {
+  const int B = g.B, C = g.C;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  SeSave sv = se_save_view(save, B, C, Cr);
   const double n = (double)B * g.HW;
-  for (int c = tid; c < C; c += 256) {
-    float mu, var;
-    if (training) {
-      double m1 = 0.0, m2 = 0.0;
-      for (int b = 0; b < B; ++b) {
-        double s = sv.sg[b * C + c];
-        m1 += s * sv.S[b * C + c];
-        m2 += s * s * sv.Q[b * C + c];
-      }
-      m1 /= n;
-      m2 = m2 / n - m1 * m1;
-      if (m2 < 0.0) m2 = 0.0;
-      mu = (float)m1;
-      var = (float)m2;
-      if (rmean) rmean[c] = (1.f - momentum) * rmean[c] + momentum * mu;
-      if (rvar) rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)(m2 * n / (n - 1.0));
-    } else {
-      mu = rmean[c];
-      var = rvar[c];
+  float mu, var;
+  if (training) {
+    double m1 = 0.0, m2 = 0.0;
+    for (int b = 0; b < B; ++b) {
+      double s = sv.sg[b * C + c];
+      m1 += s * sv.S[b * C + c];
+      m2 += s * s * sv.Q[b * C + c];
     }
-    float rs = 1.f / sqrtf(var + eps);
-    float k = gamma[c] * rs;
-    sv.mean[c] = mu;
-    sv.rstd[c] = rs;
-    sv.betap[c] = beta[c] - k * mu;
-    for (int b = 0; b < B; ++b) sv.alpha[b * C + c] = k * sv.sg[b * C + c];
+    m1 /= n;
+    m2 = m2 / n - m1 * m1;
+    if (m2 < 0.0) m2 = 0.0;
+    mu = (float)m1;
+    var = (float)m2;
+    if (rmean) rmean[c] = (1.f - momentum) * rmean[c] + momentum * mu;
+    if (rvar) rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)(m2 * n / (n - 1.0));
+  } else {
+    mu = rmean[c];
+    var = rvar[c];
   }
+  float rs = 1.f / sqrtf(var + eps);
+  float k = gamma[c] * rs;
+  sv.mean[c] = mu;
+  sv.rstd[c] = rs;
+  sv.betap[c] = beta[c] - k * mu;
+  for (int b = 0; b < B; ++b) sv.alpha[b * C + c] = k * sv.sg[b * C + c];
 }
 
 // pass 2 forward: out = lrelu(alpha[b,c]*a + betap[c])
@@ -260,109 +287,89 @@ se_bwd_reduce_kernel(const float* __restrict__ z, const float* __restrict__ dout
   block_chan_reduce2<V>(t, t1, t2, part, blockIdx.x, g.C);
 }
 
-// backward mid. One block. coef layout (fp32): A[B*C] Bc[B*C] Cc[B*C] with
+// backward mid (three small launches). coef (fp32): A[B*C] Bc[B*C] Cc[B*C] with
 //   da = A*g2 + Bc*(a*s - mean) + Cc
-// scratch (fp64): T1[B*C] T2[B*C] G[C] GY[C] du[B*C] dh[B*Cr]
+// scratch (fp64): G[C] GY[C] du[B*C] dh[B*Cr] T1[B*C] T2[B*C]
+// part 1: one thread per channel — BN backward sums and du = ds * s * (1 - s)
 __global__ void __launch_bounds__(256)
-se_bwd_mid_kernel(const double* __restrict__ part, SeGeom g, int Cr, const float* __restrict__ w1,
-                  const float* __restrict__ w2, const float* __restrict__ gamma, int training,
-                  float* __restrict__ save, float* __restrict__ dw1, float* __restrict__ db1,
-                  float* __restrict__ dw2, float* __restrict__ db2, float* __restrict__ dgamma,
-                  float* __restrict__ dbeta, double* __restrict__ scratch,
-                  float* __restrict__ coef) {
+se_bwd_chan_kernel(SeGeom g, int Cr,
+                   const float* __restrict__ gamma, int training, float* __restrict__ save,
+                   float* __restrict__ dgamma, float* __restrict__ dbeta,
+                   double* __restrict__ scratch) {
   const int B = g.B, C = g.C;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
   SeSave sv = se_save_view(save, B, C, Cr);
-  double* T1 = scratch;
-  double* T2 = T1 + (size_t)B * C;
-  double* G = T2 + (size_t)B * C;
+  double* G = scratch;
+  double* GY = G + C;
+  double* du = GY + C;
+  const double* T1 = du + (size_t)B * C + (size_t)B * Cr;
+  const double* T2 = T1 + (size_t)B * C;
+  const double n = (double)B * g.HW;
+  const double mean = sv.mean[c], rstd = sv.rstd[c];
+  double gs = 0.0, gy = 0.0;
+  // per-(b,c) T1 = sum g2, T2 = sum g2*a (se_part_sum_kernel)
+  for (int b = 0; b < B; ++b) {
+    double t1 = T1[b * C + c];
+    gs += t1;
+    gy += (double)sv.sg[b * C + c] * T2[b * C + c] - mean * t1;
+  }
+  gy *= rstd;
+  G[c] = gs;
+  GY[c] = gy;
+  if (dgamma) dgamma[c] = (float)gy;
+  if (dbeta) dbeta[c] = (float)gs;
+  const double k = (double)gamma[c] * rstd;
+  for (int b = 0; b < B; ++b) {
+    double s = sv.sg[b * C + c];
+    double t2 = T2[b * C + c];
+    double ds;
+    if (training) {
+      double yha = rstd * (s * sv.Q[b * C + c] - mean * sv.S[b * C + c]);
+      ds = k * (t2 - (gs / n) * sv.S[b * C + c] - (gy / n) * yha);
+    } else {
+      ds = k * t2;
+    }
+    du[b * C + c] = ds * s * (1.0 - s);
+  }
+}
+
+// part 2: one block per sample — dh = lrelu'(hpre) * W2^T du, dm = W1^T dh, coefficients
+__global__ void __launch_bounds__(256)
+se_bwd_sample_kernel(SeGeom g, int Cr, const float* __restrict__ w1,
+                     const float* __restrict__ w2, const float* __restrict__ gamma, int training,
+                     float* __restrict__ save, double* __restrict__ scratch,
+                     float* __restrict__ coef) {
+  extern __shared__ __attribute__((aligned(16))) double smd[];  // dh[Cr]
+  const int B = g.B, C = g.C, b = blockIdx.x, tid = threadIdx.x;
+  SeSave sv = se_save_view(save, B, C, Cr);
+  double* G = scratch;
   double* GY = G + C;
   double* du = GY + C;
   double* dh = du + (size_t)B * C;
+  for (int o = tid; o < Cr * 4; o += 256) {
+    int j = o >> 2, part_i = o & 3;
+    double acc = 0.0;
+    for (int c = part_i; c < C; c += 4) acc += (double)w2[(long)c * Cr + j] * du[b * C + c];
+    acc += __shfl_xor(acc, 1);
+    acc += __shfl_xor(acc, 2);
+    if (part_i == 0) {
+      double v = acc * lrelu_d(sv.hpre[b * Cr + j]);
+      smd[j] = v;
+      dh[b * Cr + j] = v;
+    }
+  }
+  __syncthreads();
+  const double n = (double)B * g.HW;
   float* A = coef;
   float* Bc = A + (size_t)B * C;
   float* Cc = Bc + (size_t)B * C;
-  const int tid = threadIdx.x;
-  const double n = (double)B * g.HW;
-  for (int i = tid; i < B * C; i += 256) {
-    int b = i / C, c = i % C;
-    double s1 = 0.0, s2 = 0.0;
-    for (int k = 0; k < g.NCH; ++k) {
-      const double* pr = part + ((long)(b * g.NCH + k) * 2) * C;
-      s1 += pr[c];
-      s2 += pr[C + c];
-    }
-    T1[i] = s1;
-    T2[i] = s2;
-  }
-  __syncthreads();
-  // per-channel BN sums: G = sum g2, GY = sum g2*yhat = rstd * sum_b (s*T2 - mean*T1)
   for (int c = tid; c < C; c += 256) {
-    double gs = 0.0, gy = 0.0;
-    for (int b = 0; b < B; ++b) {
-      gs += T1[b * C + c];
-      gy += (double)sv.sg[b * C + c] * T2[b * C + c] - (double)sv.mean[c] * T1[b * C + c];
-    }
-    gy *= sv.rstd[c];
-    G[c] = gs;
-    GY[c] = gy;
-    if (dgamma) dgamma[c] = (float)gy;
-    if (dbeta) dbeta[c] = (float)gs;
-  }
-  __syncthreads();
-  // ds = sum_hw dy*a; du = ds * s * (1 - s)
-  for (int i = tid; i < B * C; i += 256) {
-    int c = i % C;
-    double k = (double)gamma[c] * sv.rstd[c];
-    double s = sv.sg[i];
-    double ds;
-    if (training) {
-      double yha = (double)sv.rstd[c] * (s * sv.Q[i] - (double)sv.mean[c] * sv.S[i]);
-      ds = k * (T2[i] - (G[c] / n) * sv.S[i] - (GY[c] / n) * yha);
-    } else {
-      ds = k * T2[i];
-    }
-    du[i] = ds * s * (1.0 - s);
-  }
-  __syncthreads();
-  // fc2 backward
-  for (int i = tid; i < C * Cr; i += 256) {
-    int c = i / Cr, j = i % Cr;
-    double acc = 0.0;
-    for (int b = 0; b < B; ++b) acc += du[b * C + c] * lrelu(sv.hpre[b * Cr + j]);
-    dw2[i] = (float)acc;
-  }
-  for (int c = tid; c < C; c += 256) {
-    double acc = 0.0;
-    for (int b = 0; b < B; ++b) acc += du[b * C + c];
-    db2[c] = (float)acc;
-  }
-  // dh[b,j] = lrelu'(hpre) * sum_c w2[c][j] du[b,c]
-  for (int i = tid; i < B * Cr; i += 256) {
-    int b = i / Cr, j = i % Cr;
-    double acc = 0.0;
-    for (int c = 0; c < C; ++c) acc += (double)w2[(long)c * Cr + j] * du[b * C + c];
-    dh[i] = acc * lrelu_d(sv.hpre[i]);
-  }
-  __syncthreads();
-  // fc1 backward (input = channel means S/HW)
-  for (int i = tid; i < Cr * C; i += 256) {
-    int j = i / C, c = i % C;
-    double acc = 0.0;
-    for (int b = 0; b < B; ++b) acc += dh[b * Cr + j] * (sv.S[b * C + c] / g.HW);
-    dw1[i] = (float)acc;
-  }
-  for (int j = tid; j < Cr; j += 256) {
-    double acc = 0.0;
-    for (int b = 0; b < B; ++b) acc += dh[b * Cr + j];
-    db1[j] = (float)acc;
-  }
-  // coefficients: da = A*g2 + Bc*(a*s - mean) + Cc
-  for (int i = tid; i < B * C; i += 256) {
-    int b = i / C, c = i % C;
     double dm = 0.0;
-    for (int j = 0; j < Cr; ++j) dm += (double)w1[(long)j * C + c] * dh[b * Cr + j];
+    for (int j = 0; j < Cr; ++j) dm += (double)w1[(long)j * C + c] * smd[j];
     double k = (double)gamma[c] * sv.rstd[c];
-    double s = sv.sg[i];
+    double s = sv.sg[b * C + c];
+    int i = b * C + c;
     A[i] = (float)(s * k);
     if (training) {
       Bc[i] = (float)(-s * k * sv.rstd[c] * (GY[c] / n));
@@ -371,6 +378,41 @@ se_bwd_mid_kernel(const double* __restrict__ part, SeGeom g, int Cr, const float
       Bc[i] = 0.f;
       Cc[i] = (float)(dm / g.HW);
     }
+  }
+}
+
+// part 3: parameter gradients of fc1 / fc2 (sums over the batch)
+__global__ void __launch_bounds__(256)
+se_bwd_param_kernel(SeGeom g, int Cr, float* __restrict__ save, const double* __restrict__ scratch,
+                    float* __restrict__ dw1, float* __restrict__ db1, float* __restrict__ dw2,
+                    float* __restrict__ db2) {
+  const int B = g.B, C = g.C;
+  SeSave sv = se_save_view(save, B, C, Cr);
+  const double* du = scratch + 2 * (size_t)C;
+  const double* dh = du + (size_t)B * C;
+  const long nW = (long)C * Cr;
+  const long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (i < nW) {  // dw2[c][j] = sum_b du[b,c] * lrelu(hpre[b,j])
+    int c = (int)(i / Cr), j = (int)(i % Cr);
+    double acc = 0.0;
+    for (int b = 0; b < B; ++b) acc += du[b * C + c] * lrelu(sv.hpre[b * Cr + j]);
+    dw2[i] = (float)acc;
+  } else if (i < 2 * nW) {  // dw1[j][c] = sum_b dh[b,j] * m[b,c]
+    long t = i - nW;
+    int j = (int)(t / C), c = (int)(t % C);
+    double acc = 0.0;
+    for (int b = 0; b < B; ++b) acc += dh[b * Cr + j] * (sv.S[b * C + c] / g.HW);
+    dw1[t] = (float)acc;
+  } else if (i < 2 * nW + C) {
+    int c = (int)(i - 2 * nW);
+    double acc = 0.0;
+    for (int b = 0; b < B; ++b) acc += du[b * C + c];
+    db2[c] = (float)acc;
+  } else if (i < 2 * nW + C + Cr) {
+    int j = (int)(i - 2 * nW - C);
+    double acc = 0.0;
+    for (int b = 0; b < B; ++b) acc += dh[b * Cr + j];
+    db1[j] = (float)acc;
   }
 }
 
@@ -455,8 +497,15 @@ extern "C" int accunet_se_fwd(const float* z, const float* sc, const float* sh, 
     hipLaunchKernelGGL(se_reduce_kernel<4>, grid, dim3(256), 0, s, z, sc, sh, act, g, part);
   else
     hipLaunchKernelGGL(se_reduce_kernel<1>, grid, dim3(256), 0, s, z, sc, sh, act, g, part);
-  hipLaunchKernelGGL(se_mid_kernel, dim3(1), dim3(256), 0, s, part, g, Cr, w1, b1, w2, b2, gamma,
-                     beta, rmean, rvar, momentum, eps, training, save);
+  {
+    double* S = reinterpret_cast<double*>(save);  // SeSave: S[B*C] then Q[B*C]
+    hipLaunchKernelGGL(se_part_sum_kernel, dim3(ceil_div(C, 64), B), dim3(256), 0, s, part, g, S,
+                       S + (size_t)B * C);
+  }
+  hipLaunchKernelGGL(se_mid_gate_kernel, dim3(B), dim3(256), (C + Cr) * sizeof(float), s, g, Cr, w1,
+                     b1, w2, b2, save);
+  hipLaunchKernelGGL(se_mid_bn_kernel, dim3(ceil_div(C, 256)), dim3(256), 0, s, g, Cr, gamma, beta,
+                     rmean, rvar, momentum, eps, training, save);
   if (training && nbt) hipLaunchKernelGGL(inc_i64_kernel, dim3(1), dim3(1), 0, s, nbt);
   const float* alpha = save + se_alpha_offset(B, C, Cr);
   const float* betap = alpha + (size_t)B * C;
@@ -494,9 +543,19 @@ extern "C" int accunet_se_bwd(const float* z, const float* dout, const float* sc
   else
     hipLaunchKernelGGL(se_bwd_reduce_kernel<1>, grid, dim3(256), 0, s, z, dout, sc, sh, act, g,
                        alpha, betap, part);
-  hipLaunchKernelGGL(se_bwd_mid_kernel, dim3(1), dim3(256), 0, s, part, g, Cr, w1, w2, gamma,
-                     training, const_cast<float*>(save), dw1, db1, dw2, db2, dgamma, dbeta,
-                     scratch, coef);
+  float* sv = const_cast<float*>(save);
+  {
+    double* T1 = scratch + 2 * (size_t)C + (size_t)B * C + (size_t)B * Cr;
+    hipLaunchKernelGGL(se_part_sum_kernel, dim3(ceil_div(C, 64), B), dim3(256), 0, s, part, g, T1,
+                       T1 + (size_t)B * C);
+  }
+  hipLaunchKernelGGL(se_bwd_chan_kernel, dim3(ceil_div(C, 256)), dim3(256), 0, s, g, Cr, gamma,
+                     training, sv, dgamma, dbeta, scratch);
+  hipLaunchKernelGGL(se_bwd_sample_kernel, dim3(B), dim3(256), (Cr > 0 ? Cr : 1) * sizeof(double),
+                     s, g, Cr, w1, w2, gamma, training, sv, scratch, coef);
+  long nparam = 2L * C * Cr + C + Cr;
+  hipLaunchKernelGGL(se_bwd_param_kernel, dim3(ceil_div(nparam, 256)), dim3(256), 0, s, g, Cr, sv,
+                     scratch, dw1, db1, dw2, db2);
   if (V == 4)
     hipLaunchKernelGGL(se_bwd_apply_kernel<4>, grid, dim3(256), 0, s, z, dout, sc, sh, act, g,
                        alpha, betap, sgate, mean, coef, da);

@@ -149,7 +149,11 @@ def main():
     }
     rl = prof.rooflines(HBM_PEAK_GBS)
     if rl:
-        line["roofline"] = rl[0]
+        # primary: K1, the HANC depthwise stage at the north-star instance (cnv12's
+        # dw3x3 over B x 256^2 x 96; cnv92 has the same shape), SURVEY.md 8(d)
+        k1 = f"{B}x{S}x{S}x{3 * 32}"
+        prim = [r for r in rl if r["kernel"].startswith("dw3x3") and r["shape"] == k1]
+        line["roofline"] = prim[0] if prim else rl[0]
         line["rooflines"] = rl
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.variant, S, args.cpu_sample)

@@ -10,7 +10,7 @@ import time
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, os.path.join(os.path.dirname(HERE), "acc-unet-unext_amd"))
+sys.path.insert(0, os.environ.get("ACCUNET_PKG_DIR", os.path.join(os.path.dirname(HERE), "acc-unet-unext_amd")))
 sys.path.insert(0, HERE)
 import parity_util as PU  # noqa: E402
 from parity_util import O  # noqa: E402

@@ -1,0 +1,132 @@
+"""Kernel-level parity of the streaming HANC kernels against fp64 torch restatements
+of the reference ops (the depthwise conv + norm2 statistics of HANCBlock,
+ACC_UNet/ACC_UNet.py:240-247,273-275, and ChannelSELayer :37-49), called through
+the C ABI (accunet.kern) so every tile variant / fallback path is exercised:
+    dw3x3: LDS-tiled TCQ=8 (C % 32 == 0), TCQ=16 (W <= 16), register-window
+           fallback (C % 32 != 0, incl. cnv11's C = 9), ragged tiles (H % 8, W % TP)."""
+import os
+import sys
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "acc-unet-unext_amd"))
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _kern():
+    from accunet import kern
+    return kern
+
+
+def _lrelu(t):
+    return torch.where(t > 0, t, 0.01 * t)
+
+
+DW_SHAPES = [
+    (2, 16, 16, 96),     # TCQ 16 tile, W = TP
+    (2, 24, 40, 64),     # TCQ 8 tile, ragged H (24 = 3 x 8) and W (40 = 32 + 8)
+    (1, 13, 35, 32),     # ragged everything
+    (3, 8, 8, 128),      # W < TP
+    (2, 17, 19, 36),     # fallback register-window kernel, V = 4
+    (2, 12, 12, 9),      # fallback, V = 1 (cnv11's hidden width)
+]
+
+
+@pytest.mark.parametrize("B,H,W,C", DW_SHAPES)
+@pytest.mark.parametrize("pro", [False, True])
+def test_dw3x3_fwd_stats_wgrad_vs_fp64(B, H, W, C, pro):
+    kern = _kern()
+    g = torch.Generator().manual_seed(B * 1000 + H * 10 + C)
+    x = torch.randn(B, H, W, C, generator=g, dtype=torch.float64)
+    wt = torch.randn(C, 1, 3, 3, generator=g, dtype=torch.float64) * 0.3
+    bias = torch.randn(C, generator=g, dtype=torch.float64) * 0.1
+    sc = torch.rand(C, generator=g, dtype=torch.float64) + 0.5
+    sh = torch.randn(C, generator=g, dtype=torch.float64) * 0.2
+    dz = torch.randn(B, H, W, C, generator=g, dtype=torch.float64)
+    a = _lrelu(x * sc + sh) if pro else x
+    a_nchw = a.permute(0, 3, 1, 2)
+    z_ref = F.conv2d(a_nchw, wt, bias, padding=1, groups=C).permute(0, 2, 3, 1)
+    # flipped-kernel correlation = data gradient of the conv
+    zf_ref = F.conv2d(a_nchw, wt.flip(-1).flip(-2), None, padding=1, groups=C).permute(0, 2, 3, 1)
+    # weight / bias gradient for upstream dz
+    a_req = a_nchw.clone().requires_grad_(False)
+    w_req = wt.clone().requires_grad_(True)
+    b_req = bias.clone().requires_grad_(True)
+    zz = F.conv2d(a_req, w_req, b_req, padding=1, groups=C)
+    (zz * dz.permute(0, 3, 1, 2)).sum().backward()
+
+    f = lambda t: t.float().contiguous().to(DEV)  # noqa: E731
+    xd, wd, bd, scd, shd, dzd = f(x), f(wt), f(bias), f(sc), f(sh), f(dz)
+    rows = kern.dw3x3_rows(B, H, W, C)
+    st = torch.zeros(rows, 2 * C, dtype=torch.float64, device=DEV)
+    z = torch.empty(B, H, W, C, device=DEV)
+    act = 1 if pro else 0
+    kern.dw3x3_fwd(xd, wd, bd, scd if pro else None, shd if pro else None, act, 0, z, st, B, H, W, C)
+    zf = torch.empty_like(z)
+    kern.dw3x3_fwd(xd, wd, None, scd if pro else None, shd if pro else None, act, 1, zf, None,
+                   B, H, W, C)
+    dw = torch.empty(C, 1, 3, 3, device=DEV)
+    db = torch.empty(C, device=DEV)
+    kern.dw3x3_wgrad(xd, dzd, scd if pro else None, shd if pro else None, act, dw, db, B, H, W, C)
+    torch.cuda.synchronize()
+    scale = z_ref.abs().max().item()
+    assert (z.double().cpu() - z_ref).abs().max().item() <= 2e-6 * scale
+    assert (zf.double().cpu() - zf_ref).abs().max().item() <= 2e-6 * scale
+    s = st.sum(0).cpu()
+    zr = z_ref.reshape(-1, C)
+    assert torch.allclose(s[:C], zr.sum(0), rtol=1e-6, atol=1e-6 * zr.abs().sum(0).max().item())
+    assert torch.allclose(s[C:], (zr * zr).sum(0), rtol=1e-6)
+    gw = w_req.grad
+    assert (dw.double().cpu() - gw).abs().max().item() <= 1e-5 * gw.abs().max().item() + 1e-5
+    gb = b_req.grad
+    assert (db.double().cpu() - gb).abs().max().item() <= 1e-5 * gb.abs().max().item() + 1e-5
+
+
+@pytest.mark.parametrize("B,H,C", [(4, 16, 64), (2, 8, 32), (16, 32, 256), (3, 5, 40)])
+def test_se_layer_vs_fp64_oracle(B, H, C):
+    """ChannelSELayer (fused GAP / gate / BN-of-gated / LeakyReLU, and its backward) vs
+    the fp64 oracle; tolerance relative to the reference's own fp32 error."""
+    sys.path.insert(0, HERE)
+    import parity_util as PU
+    from parity_util import O
+    from accunet import model as M
+    torch.manual_seed(0)
+    se = M.ChannelSELayer(C)
+    spec = [("s." + n, tuple(t.shape)) for n, t in se.state_dict().items()]
+    sd = O.det_state_dict(spec, seed=3)
+    se.load_state_dict({n[2:]: v for n, v in sd.items()})
+    se = se.to(DEV).train()
+    x = O.det_input((B, C, H, H), "se-x") * 2 + 0.5
+    go = O.det_input((B, C, H, H), "se-go")
+    res = {}
+    for dt in (torch.float64, torch.float32):
+        sdo = {n: (v.to(dt).requires_grad_(not n.endswith(PU.BUFFER_LEAVES))
+                   if v.is_floating_point() else v.clone()) for n, v in sd.items()}
+        xr = x.detach().clone().to(dt).requires_grad_(True)
+        y = O.se(xr, sdo, "s", True)
+        (y * go.to(dt)).sum().backward()
+        res[dt] = (y.detach(), xr.grad, {n[2:]: v.grad for n, v in sdo.items() if v.grad is not None},
+                   {n[2:]: v for n, v in sdo.items()})
+    xh = x.detach().to(DEV).requires_grad_(True)
+    y = se(xh)
+    (y * go.to(DEV)).sum().backward()
+    hip = {"out": y, "dx": xh.grad}
+    a64 = {"out": res[torch.float64][0], "dx": res[torch.float64][1]}
+    a32 = {"out": res[torch.float32][0], "dx": res[torch.float32][1]}
+    for n, p in se.named_parameters():
+        hip[n] = p.grad
+        a64[n] = res[torch.float64][2][n]
+        a32[n] = res[torch.float32][2][n]
+    sdh = se.state_dict()
+    for n in ("bn.running_mean", "bn.running_var"):
+        hip[n] = sdh[n]
+        a64[n] = res[torch.float64][3][n]
+        a32[n] = res[torch.float32][3][n]
+    rows = PU.compare_vs_reference_fp32(hip, a64, a32, factor=4.0, rel_floor=1e-5)
+    bad = [r for r in rows if not r[4]]
+    assert not bad, bad
