@@ -71,3 +71,39 @@ ACC_DEV void block_chan_reduce2(const ChanTile& t, T (&a)[V], T (&b)[V], T* out,
     }
   }
 }
+
+// Deterministic block reduction for power-of-two slot counts: thread t contributes
+// v[0..N) to slot t % TCQ (TCQ | 256). Lanes of one wave sharing a slot are summed
+// with xor shuffles (offsets TCQ, 2*TCQ, ..., 32), the per-wave sums go through LDS
+// ([waves][slot][N]) and threads t < TCQ add them in wave order. Returns true in
+// the threads that hold a slot's total (t < TCQ), whose v[] then holds the sums.
+// `lds` must hold 4 * min(TCQ, 64) * N elements; the caller syncs before reusing it.
+template <int TCQ, int N, typename T>
+ACC_DEV bool block_slot_reduce(T (&v)[N], T* lds) {
+  static_assert(TCQ > 0 && (TCQ & (TCQ - 1)) == 0 && TCQ <= 256, "TCQ: power of two <= 256");
+  constexpr int WL = TCQ < 64 ? TCQ : 64;  // slots per wave
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int off = TCQ; off < 64; off <<= 1)
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] += __shfl_xor(v[i], off);
+  if (lane < WL) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) lds[(wave * WL + lane) * N + i] = v[i];
+  }
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t >= TCQ) return false;
+  constexpr int WPS = 4 * WL / TCQ;  // waves holding each slot
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    T s = 0;
+#pragma unroll
+    for (int k = 0; k < WPS; ++k) {
+      const int w = (t / 64) + k * (TCQ / WL);  // TCQ <= 64: w = k; TCQ = 128: t/64, +2
+      s += lds[(w * WL + (t % WL)) * N + i];
+    }
+    v[i] = s;
+  }
+  return true;
+}

@@ -13,6 +13,8 @@
 // adjacent threads) and one 16-byte store, so HBM sees ~1 read + 1 write per element.
 #include "common.h"
 #include "kernels.h"
+#include "chan.h"
+#include <stdlib.h>
 
 #define DW_TR 8  // output rows per thread strip
 
@@ -277,6 +279,8 @@ __global__ void dw_wgrad_finish_kernel(const float* __restrict__ sums, int C, fl
 struct DwTGeom {
   int B, H, W, C;
   int tilesW, tilesH;
+  int rch;    // 8-row chunks per block (forward kernel: a vertical strip of 8*rch rows)
+  int ntl;    // non-temporal input loads (tuning knob ACCUNET_DW_NTL)
   int remap;  // ntiles % 8 == 0: XCD-contiguous tile order
 };
 
@@ -296,7 +300,60 @@ struct DwT {
   static constexpr int IR = DW_TR + 2;
   static constexpr int N4 = IR * IP * TCQ;  // float4 elements of the input tile
   static constexpr int NK = (N4 + 255) / 256;
+  static constexpr int CR = 4;                 // strip pipeline: rows per chunk
+  static constexpr int N8 = CR * IP * TCQ;     // float4 elements of CR new input rows
+  static constexpr int NK8 = (N8 + 255) / 256;
 };
+
+// Strip pipeline helpers: input rows live in a 10-slot LDS ring, row h of the
+// block's strip (which starts at output row hbeg) in slot (h - hbeg + 1) % 10.
+// Fetch `n` float4 elements of consecutive input rows starting at row hA into
+// registers (zero outside the image).
+template <int TCQ, int NKK>
+ACC_DEV void dw_fetch_rows(float4 (&v)[NKK], const float* __restrict__ x, const DwTGeom& g, int b,
+                           int hA, int n, int w0, int c0) {
+  typedef DwT<TCQ> T;
+  const int tid = threadIdx.x, q = tid % TCQ;
+#pragma unroll
+  for (int k = 0; k < NKK; ++k) {
+    const int i = tid + 256 * k;
+    const int rp = i / TCQ;
+    const int p = rp % T::IP, r = rp / T::IP;
+    const int hh = hA + r, ww = w0 - 1 + p;
+    v[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (i < n && hh >= 0 && hh < g.H && ww >= 0 && ww < g.W) {
+      const float* src = x + (((long)b * g.H + hh) * g.W + ww) * g.C + c0 + 4 * q;
+      v[k] = g.ntl ? ld4_nt(src) : ld4(src);
+    }
+  }
+}
+
+// Activate (prologue BN+act, in-image elements only) and park fetched rows in the ring.
+template <int TCQ, int NKK>
+ACC_DEV void dw_park_rows(float4* __restrict__ ring, const float4 (&v)[NKK], const DwTGeom& g,
+                          int hA, int n, int w0, int hbeg, bool pro, float4 ps, float4 pb,
+                          int act) {
+  typedef DwT<TCQ> T;
+  const int tid = threadIdx.x, q = tid % TCQ;
+#pragma unroll
+  for (int k = 0; k < NKK; ++k) {
+    const int i = tid + 256 * k;
+    if (i < n) {
+      const int rp = i / TCQ;
+      const int p = rp % T::IP, r = rp / T::IP;
+      const int hh = hA + r, ww = w0 - 1 + p;
+      float4 a = v[k];
+      if (pro && hh >= 0 && hh < g.H && ww >= 0 && ww < g.W) {
+        a.x = apply_act(a.x * ps.x + pb.x, act);
+        a.y = apply_act(a.y * ps.y + pb.y, act);
+        a.z = apply_act(a.z * ps.z + pb.z, act);
+        a.w = apply_act(a.w * ps.w + pb.w, act);
+      }
+      const int slot = (hh - hbeg + 1) % T::IR;
+      ring[(slot * T::IP + p) * TCQ + q] = a;
+    }
+  }
+}
 
 // load the activated input tile a = act(x*sc+sh) (zero outside the image) into LDS
 template <int TCQ>
@@ -340,13 +397,20 @@ ACC_DEV void dw_fill_tile(float4* __restrict__ tile, const float* __restrict__ x
   }
 }
 
+// Forward: a block owns a vertical strip of 8*rch output rows x TP pixels x TCQ
+// channel quads and walks it in CR=4-row chunks over a 10-slot LDS ring that holds
+// input rows r0-1 .. r0+8 at the start of the chunk at row r0. The CR rows the
+// NEXT chunk adds (r0+9 .. r0+12) are fetched into registers before this chunk is
+// computed and parked afterwards in the slots of rows r0-1 .. r0+2 (dead by then),
+// so HBM reads stay in flight through the compute (software pipeline).
 template <int TCQ>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
 dw3x3_tile_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
                       const float* __restrict__ bias, const float* __restrict__ sc,
                       const float* __restrict__ sh, int act, int flip, float* __restrict__ z,
                       double* __restrict__ stats, DwTGeom g) {
   typedef DwT<TCQ> T;
+  constexpr int CR = T::CR;
   __shared__ float4 tile[T::N4 > 1024 ? T::N4 : 1024];
   const int tid = threadIdx.x;
   const int q = tid % TCQ, p = tid / TCQ;
@@ -357,9 +421,20 @@ dw3x3_tile_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
   t /= g.tilesW;
   const int th = t % g.tilesH;
   const int b = t / g.tilesH;
-  const int h0 = th * DW_TR, w0 = tw * T::TP;
-  dw_fill_tile<TCQ>(tile, x, sc, sh, act, g, b, h0, w0, c0);
-
+  const int hbeg = th * DW_TR * g.rch, w0 = tw * T::TP;
+  const int hend = min(g.H, hbeg + DW_TR * g.rch);
+  const int nch = (hend - hbeg + CR - 1) / CR;
+  const bool pro = sc != nullptr;
+  float4 ps = make_float4(1.f, 1.f, 1.f, 1.f), pb = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (pro) {
+    ps = ld4(sc + c);
+    pb = ld4(sh + c);
+  }
+  {
+    float4 v[T::NK];
+    dw_fetch_rows<TCQ, T::NK>(v, x, g, b, hbeg - 1, T::N4, w0, c0);
+    dw_park_rows<TCQ, T::NK>(tile, v, g, hbeg - 1, T::N4, w0, hbeg, pro, ps, pb, act);
+  }
   float k[9][4], bi[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -370,65 +445,70 @@ dw3x3_tile_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
   __syncthreads();
   double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
   const int w = w0 + p;
-  if (w < g.W) {
-    float win[3][3][4];
-    auto rd = [&](int r, float (&row)[3][4]) {
+  for (int kc = 0; kc < nch; ++kc) {
+    const int r0 = hbeg + CR * kc;
+    // rows r0+9 .. are needed only if the strip's last input row (hend) lies there
+    const bool more = kc + 1 < nch && r0 + 9 <= hend;
+    float4 nx[T::NK8];
+    if (more) dw_fetch_rows<TCQ, T::NK8>(nx, x, g, b, r0 + 9, T::N8, w0, c0);
+    if (w < g.W) {
+      const int base = (CR * kc) % T::IR;  // slot of input row r0 - 1
+      float win[3][3][4];
+      auto rd = [&](int j, float (&row)[3][4]) {
+        int sl = base + j;
+        sl = sl >= T::IR ? sl - T::IR : sl;
 #pragma unroll
-      for (int dx = 0; dx < 3; ++dx) {
-        float4 a = tile[(r * T::IP + p + dx) * TCQ + q];
-        row[dx][0] = a.x; row[dx][1] = a.y; row[dx][2] = a.z; row[dx][3] = a.w;
-      }
-    };
-    rd(0, win[0]);
-    rd(1, win[1]);
-    const int nr = min(DW_TR, g.H - h0);
-#pragma unroll
-    for (int r = 0; r < DW_TR; ++r) {
-      if (r < nr) {
-        rd(r + 2, win[2]);
-        float o[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          float acc = bi[j];
-#pragma unroll
-          for (int dy = 0; dy < 3; ++dy)
-#pragma unroll
-            for (int dx = 0; dx < 3; ++dx) acc = fmaf(k[dy * 3 + dx][j], win[dy][dx][j], acc);
-          o[j] = acc;
-          s1[j] += acc;
-          s2[j] += (double)acc * acc;
+        for (int dx = 0; dx < 3; ++dx) {
+          float4 a = tile[(sl * T::IP + p + dx) * TCQ + q];
+          row[dx][0] = a.x; row[dx][1] = a.y; row[dx][2] = a.z; row[dx][3] = a.w;
         }
-        st4(z + (((long)b * g.H + h0 + r) * g.W + w) * g.C + c, make_float4(o[0], o[1], o[2], o[3]));
+      };
+      rd(0, win[0]);
+      rd(1, win[1]);
+      const int nr = min(CR, hend - r0);
 #pragma unroll
-        for (int dx = 0; dx < 3; ++dx)
+      for (int r = 0; r < CR; ++r) {
+        if (r < nr) {
+          rd(r + 2, win[2]);
+          float o[4];
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            win[0][dx][j] = win[1][dx][j];
-            win[1][dx][j] = win[2][dx][j];
+            float acc = bi[j];
+#pragma unroll
+            for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+              for (int dx = 0; dx < 3; ++dx) acc = fmaf(k[dy * 3 + dx][j], win[dy][dx][j], acc);
+            o[j] = acc;
+            s1[j] += acc;
+            s2[j] += (double)acc * acc;
           }
+          st4_nt(z + (((long)b * g.H + r0 + r) * g.W + w) * g.C + c, make_float4(o[0], o[1], o[2], o[3]));
+#pragma unroll
+          for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              win[0][dx][j] = win[1][dx][j];
+              win[1][dx][j] = win[2][dx][j];
+            }
+        }
       }
+    }
+    if (more) {
+      __syncthreads();  // every thread is done with rows r0-1 .. r0+CR-2
+      dw_park_rows<TCQ, T::NK8>(tile, nx, g, r0 + 9, T::N8, w0, hbeg, pro, ps, pb, act);
+      __syncthreads();
     }
   }
   if (stats) {
     __syncthreads();  // the tile is reused as the reduction buffer
-    double* red = reinterpret_cast<double*>(tile);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      red[tid * 4 + j] = s1[j];
-      red[1024 + tid * 4 + j] = s2[j];
-    }
-    __syncthreads();
-    if (p == 0) {
+    double v[8] = {s1[0], s1[1], s1[2], s1[3], s2[0], s2[1], s2[2], s2[3]};
+    if (block_slot_reduce<TCQ, 8, double>(v, reinterpret_cast<double*>(tile))) {
       const long row = (long)(blockIdx.x) * 2 * g.C;
+      const int cc = c0 + 4 * threadIdx.x;  // slot = quad index q
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        double a = 0.0, qq = 0.0;
-        for (int i = 0; i < T::TP; ++i) {
-          a += red[(i * TCQ + q) * 4 + j];
-          qq += red[1024 + (i * TCQ + q) * 4 + j];
-        }
-        stats[row + c + j] = a;
-        stats[row + g.C + c + j] = qq;
+        stats[row + cc + j] = v[j];
+        stats[row + g.C + cc + j] = v[4 + j];
       }
     }
   }
@@ -502,26 +582,18 @@ dw3x3_tile_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ d
       }
     }
   }
-  __syncthreads();  // tile -> reduction buffer [256][4] per tap (two taps per pass)
-  float* red = reinterpret_cast<float*>(tile);
-  for (int i = 0; i < 10; i += 2) {
+  __syncthreads();  // the tile is reused as the reduction buffer
+  float v[40];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      red[tid * 4 + j] = acc[i][j];
-      red[1024 + tid * 4 + j] = acc[i + 1][j];
-    }
-    __syncthreads();
-    if (p < 2) {  // p = 0: tap i, p = 1: tap i+1
-      float a4[4];
+  for (int i = 0; i < 10; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float a = 0.f;
-        for (int k2 = 0; k2 < T::TP; ++k2) a += red[p * 1024 + (k2 * TCQ + q) * 4 + j];
-        a4[j] = a;
-      }
-      st4(part + ((long)blockIdx.x * 10 + i + p) * g.C + c, make_float4(a4[0], a4[1], a4[2], a4[3]));
-    }
-    __syncthreads();
+    for (int j = 0; j < 4; ++j) v[i * 4 + j] = acc[i][j];
+  if (block_slot_reduce<TCQ, 40, float>(v, reinterpret_cast<float*>(tile))) {
+    const int cc = c0 + 4 * threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < 10; ++i)
+      st4(part + ((long)blockIdx.x * 10 + i) * g.C + cc,
+          make_float4(v[i * 4], v[i * 4 + 1], v[i * 4 + 2], v[i * 4 + 3]));
   }
 }
 
@@ -533,11 +605,37 @@ static int dw_tile_tcq(int W, int C) {
   return 8;
 }
 
-static DwTGeom dw_tgeom(int B, int H, int W, int C, int tcq, dim3* grid) {
+static int dw_ntl() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ACCUNET_DW_NTL");
+    v = e ? atoi(e) : 0;
+  }
+  return v;
+}
+
+static int dw_rch_max() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ACCUNET_DW_RCH");  // tuning knob (tools/kbench); default 4
+    v = e ? atoi(e) : 4;
+    if (v < 1) v = 1;
+  }
+  return v;
+}
+
+// rch_max > 1 (forward only): strips of up to 8*rch_max rows, as long as the grid
+// keeps >= ~2048 workgroups (8 per CU); the weight-gradient kernel uses 1.
+static DwTGeom dw_tgeom(int B, int H, int W, int C, int tcq, dim3* grid, int rch_max = 1) {
   DwTGeom g;
   g.B = B; g.H = H; g.W = W; g.C = C;
   g.tilesW = ceil_div(W, 256 / tcq);
-  g.tilesH = ceil_div(H, DW_TR);
+  long cols = (long)B * g.tilesW * (C / 4 / tcq);
+  int rch = 1;
+  while (rch * 2 <= rch_max && cols * ceil_div(H, DW_TR * rch * 2) >= 2048) rch *= 2;
+  g.rch = rch;
+  g.ntl = dw_ntl();
+  g.tilesH = ceil_div(H, DW_TR * rch);
   long nt = (long)B * g.tilesH * g.tilesW;
   g.remap = (nt % 8 == 0) ? 1 : 0;
   *grid = dim3((unsigned)nt, C / 4 / tcq);
@@ -561,7 +659,7 @@ static DwGeom dw_geom(int B, int H, int W, int C, int V, dim3* grid) {
 extern "C" int accunet_dw3x3_rows(int B, int H, int W, int C) {
   dim3 grid;
   int tcq = dw_tile_tcq(W, C);
-  if (tcq) dw_tgeom(B, H, W, C, tcq, &grid);
+  if (tcq) dw_tgeom(B, H, W, C, tcq, &grid, dw_rch_max());
   else dw_geom(B, H, W, C, (C % 4 == 0) ? 4 : 1, &grid);
   return (int)grid.x;
 }
@@ -573,7 +671,7 @@ extern "C" int accunet_dw3x3_fwd(const float* x, const float* wt, const float* b
   dim3 grid;
   int tcq = dw_tile_tcq(W, C);
   if (tcq) {
-    DwTGeom tg = dw_tgeom(B, H, W, C, tcq, &grid);
+    DwTGeom tg = dw_tgeom(B, H, W, C, tcq, &grid, dw_rch_max());
     if (tcq == 16)
       hipLaunchKernelGGL(dw3x3_tile_fwd_kernel<16>, grid, dim3(256), 0, s, x, wt, bias, sc, sh, act,
                          flip, z, stats, tg);
@@ -593,9 +691,16 @@ extern "C" int accunet_dw3x3_fwd(const float* x, const float* wt, const float* b
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 
-extern "C" int accunet_dw3x3_rows(int B, int H, int W, int C);
+static int dw_wgrad_rows(int B, int H, int W, int C) {
+  dim3 grid;
+  int tcq = dw_tile_tcq(W, C);
+  if (tcq) dw_tgeom(B, H, W, C, tcq, &grid);
+  else dw_geom(B, H, W, C, (C % 4 == 0) ? 4 : 1, &grid);
+  return (int)grid.x;
+}
+
 size_t dw_wgrad_ws(int B, int H, int W, int C) {
-  int R = accunet_dw3x3_rows(B, H, W, C);
+  int R = dw_wgrad_rows(B, H, W, C);
   return (size_t)R * 10 * C + accunet_partials_ws_elems(R, 10 * C) + 10 * (size_t)C;
 }
 

@@ -11,11 +11,17 @@ params, ACC_UNet/ACC_UNet.py) on a per-GPU batch of 16 x 3 x 256 x 256 fp32
 synthetic images resident in HBM (BASELINE configs[1]; configs[2] at N = 8).
 Rank 0 prints one JSON line; `value` = images/s over all ranks (weak scaling).
 
+Each step replays one HIP graph holding forward + loss + backward (captured on the
+first call, accunet/train.py), then the RCCL all-reduce (N > 1) and the fused Adam
+launch; --eager launches every kernel from Python instead.
+
 Extra objects on the line:
-  roofline     — the HANC depthwise stage (K1, `dw3x3_fwd` of cnv12, B x 96 x 256^2)
-                 and the other tracked kernels timed live with HIP events on the
-                 stream they run on; algorithmic bytes / average launch time vs the
-                 8 TB/s HBM3E peak (see DESIGN.md §Measurement);
+  roofline     — the HANC depthwise stage (K1, `dw3x3_tile_fwd_kernel` of cnv12,
+                 B x 256^2 x 96) re-launched back-to-back at its in-model shape after
+                 the timed steps, timed with HIP events on its launch stream;
+                 algorithmic bytes (2 x B*H*W*C*4) / average launch time vs the 8 TB/s
+                 HBM3E peak; `rooflines` adds K3 (cnv12's SE) and the largest MFMA
+                 GEMM (cnv72's HANC x-branch) (see DESIGN.md 3, accunet/probe.py);
   cpu_baseline — the CPU oracle (oracle/accunet_oracle.py, plain PyTorch-CPU, same op
                  sequence as the reference) timed on this host on a bounded sample.
 """
@@ -46,6 +52,9 @@ def parse():
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--variant", default="canonical")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--eager", action="store_true",
+                    help="launch every kernel from Python (default: replay one HIP graph per step)")
+    ap.add_argument("--no-probe", action="store_true", help="skip the roofline probes")
     ap.add_argument("--cpu-sample", type=int, default=1, help="images in the CPU sample")
     return ap.parse_args()
 
@@ -96,8 +105,11 @@ def main():
 
     torch.manual_seed(0)
     model = M.VARIANTS[args.variant](3, 1, n_filts=32).to(dev).train()
-    reducer = adist.GradBucketReducer(model) if world > 1 else None
-    step = TrainStep(model, lr=1e-3, reducer=reducer)
+    if args.eager:
+        reducer = adist.GradBucketReducer(model) if world > 1 else None
+        step = TrainStep(model, lr=1e-3, reducer=reducer)
+    else:
+        step = TrainStep(model, lr=1e-3, graph=True)
 
     g = torch.Generator(device="cpu").manual_seed(1000 + rank)
     B, S = args.batch, args.size
@@ -108,7 +120,7 @@ def main():
         step(x, mask)
     torch.cuda.synchronize()
 
-    prof.enable(True)
+    prof.enable(args.eager)  # per-launch events only make sense for eager launches
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -147,14 +159,22 @@ def main():
                    "parallelism": f"dp{world}"},
         "final_loss": float(loss.item()),
     }
-    rl = prof.rooflines(HBM_PEAK_GBS)
-    if rl:
-        # primary: K1, the HANC depthwise stage at the north-star instance (cnv12's
-        # dw3x3 over B x 256^2 x 96; cnv92 has the same shape), SURVEY.md 8(d)
-        k1 = f"{B}x{S}x{S}x{3 * 32}"
-        prim = [r for r in rl if r["kernel"].startswith("dw3x3") and r["shape"] == k1]
-        line["roofline"] = prim[0] if prim else rl[0]
+    # roofline: K1, the HANC depthwise stage at the north-star instance (cnv12's
+    # dw3x3 over B x 256^2 x 96; cnv92 has the same shape), SURVEY.md 8(d), plus K3
+    # (cnv12's SE) and the largest MFMA GEMM, each re-launched back-to-back at its
+    # in-model shape right after the timed steps (accunet/probe.py)
+    if not args.no_probe:
+        from accunet import probe
+        blk = model.cnv12
+        rl = [probe.k1_dw3x3(B, S, S, blk.conv2.weight.shape[0], blk.conv2.weight, blk.conv2.bias),
+              probe.k3_se(B, S, S, blk.sqe.fc2.weight.shape[0], blk.sqe),
+              probe.hanc_gemm(B * (S // 4) ** 2, model.cnv72.hnc.cnv.weight.shape[0],
+                              model.cnv72.conv1.weight.shape[0])]
+        line["roofline"] = rl[0]
         line["rooflines"] = rl
+    if args.eager:
+        line["rooflines_in_model"] = prof.rooflines(HBM_PEAK_GBS)
+    line["mode"] = "eager" if args.eager else "hipgraph"
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.variant, S, args.cpu_sample)
     if rank == 0:

@@ -272,3 +272,25 @@ def test_maxpool_first_max_tie_rule():
     y.sum().backward()
     g = xr.grad[0, :, :, 0].cpu()
     assert g[0, 0] == 1 and g[0, 1] == 0 and g[1, 0] == 0 and g[1, 1] == 0
+
+
+@pytest.mark.parametrize("variant", ["canonical", "lite"])
+def test_hip_graph_train_step_equals_eager(variant):
+    """bench.py's mode: forward + loss + backward captured once into a HIP graph and
+    replayed, then the fused Adam launch. Every kernel is deterministic (no float
+    atomics), so 3 graph steps must reproduce 3 eager steps bit for bit: losses,
+    parameters, BatchNorm running statistics and num_batches_tracked."""
+    from accunet.train import TrainStep
+    nf, B, S = 8, 2, 64
+    sd = O.det_state_dict(O.param_spec(variant, 3, 1, nf), seed=0)
+    x = O.det_input((B, 3, S, S), "golden-x").to(DEV)
+    mask = O.det_mask((B, 1, S, S), "golden-mask", p=0.4).to(DEV)
+    runs = {}
+    for graph in (False, True):
+        m = _hip_model(variant, sd, nf).train()
+        step = TrainStep(m, lr=1e-3, graph=graph)
+        losses = [float(step(x, mask).item()) for _ in range(3)]
+        runs[graph] = (losses, {k: v.detach().clone() for k, v in m.state_dict().items()})
+    assert runs[False][0] == runs[True][0], (runs[False][0], runs[True][0])
+    for k, v in runs[False][1].items():
+        assert torch.equal(v, runs[True][1][k]), k

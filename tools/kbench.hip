@@ -1,0 +1,189 @@
+// Standalone kernel microbenchmark for the streaming hot kernels, linked against
+// libaccunet_hip.so through the public C ABI (include/accunet.h). No torch, so a
+// GPU box runs it in seconds:
+//   make -C tools kbench && tools/kbench [iters]
+// Reports per-launch average (hipEvent over `iters` back-to-back launches) and
+// algorithmic GB/s next to a float4 copy of the same byte count (the practical
+// HBM ceiling for this footprint).
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <vector>
+
+#include "../include/accunet.h"
+
+#define CK(x)                                                                   \
+  do {                                                                          \
+    hipError_t e_ = (x);                                                        \
+    if (e_ != hipSuccess) {                                                     \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(1);                                                                  \
+    }                                                                           \
+  } while (0)
+#define CA(x)                                                 \
+  do {                                                        \
+    int r_ = (x);                                             \
+    if (r_ != 0) {                                            \
+      fprintf(stderr, "%s:%d accunet rc %d\n", __FILE__, __LINE__, r_); \
+      exit(1);                                                \
+    }                                                         \
+  } while (0)
+
+__global__ void copy4(const float4* __restrict__ a, float4* __restrict__ b, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    b[i] = a[i];
+}
+
+typedef float v4f __attribute__((ext_vector_type(4)));
+__global__ void copy4_nt(const float4* __restrict__ a0, float4* __restrict__ b0, long n) {
+  const v4f* a = (const v4f*)a0;
+  v4f* b = (v4f*)b0;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    __builtin_nontemporal_store(a[i], &b[i]);
+}
+__global__ void copy4_flat(const float4* __restrict__ a, float4* __restrict__ b, long n) {
+  long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (i < n) b[i] = a[i];
+}
+// 4 independent float4 per thread per iteration (block-contiguous)
+__global__ void copy4_x4(const float4* __restrict__ a, float4* __restrict__ b, long n) {
+  long base = (long)blockIdx.x * 1024 + threadIdx.x;
+  float4 v[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) if (base + 256 * k < n) v[k] = a[base + 256 * k];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) if (base + 256 * k < n) b[base + 256 * k] = v[k];
+}
+__global__ void copy4_x4_nt(const float4* __restrict__ a0, float4* __restrict__ b0, long n) {
+  const v4f* a = (const v4f*)a0;
+  v4f* b = (v4f*)b0;
+  long base = (long)blockIdx.x * 1024 + threadIdx.x;
+  v4f v[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) if (base + 256 * k < n) v[k] = __builtin_nontemporal_load(&a[base + 256 * k]);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) if (base + 256 * k < n) __builtin_nontemporal_store(v[k], &b[base + 256 * k]);
+}
+
+__global__ void fill(float* p, long n, float s) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    p[i] = s * (float)((i * 2654435761u) % 1000) / 1000.f - 0.5f * s;
+}
+
+static float* dalloc(size_t n, float s = 1.f) {
+  float* p;
+  CK(hipMalloc(&p, n * sizeof(float)));
+  hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, p, (long)n, s);
+  return p;
+}
+
+template <class F>
+static double timeit(F f, int iters) {
+  f();
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  CK(hipEventRecord(a, 0));
+  for (int i = 0; i < iters; ++i) f();
+  CK(hipEventRecord(b, 0));
+  CK(hipEventSynchronize(b));
+  float ms;
+  CK(hipEventElapsedTime(&ms, a, b));
+  return 1000.0 * ms / iters;
+}
+
+static void report(const char* name, double us, double bytes) {
+  printf("%-44s %9.2f us  %8.1f GB/s  (%.1f%% of 8 TB/s)\n", name, us, bytes / us / 1e3,
+         100.0 * bytes / us / 1e3 / 8000.0);
+}
+
+int main(int argc, char** argv) {
+  int iters = argc > 1 ? atoi(argv[1]) : 30;
+  const int B = 16, H = 256, W = 256;
+  // ---- K1: cnv12 depthwise, C = 96 ----
+  {
+    const int C = 96;
+    size_t n = (size_t)B * H * W * C;
+    float *x = dalloc(n), *z = dalloc(n), *wt = dalloc(9 * C, 0.3f), *bi = dalloc(C, 0.1f);
+    float *sc = dalloc(C, 1.f), *sh = dalloc(C, 0.1f);
+    int rows = accunet_dw3x3_rows(B, H, W, C);
+    double* st;
+    CK(hipMalloc(&st, (size_t)rows * 2 * C * sizeof(double)));
+    double bytes = 2.0 * 4 * n;
+    report("copy float4 (same bytes as K1)",
+           timeit([&] { hipLaunchKernelGGL(copy4, dim3(8192), dim3(256), 0, 0, (const float4*)x,
+                                           (float4*)z, (long)(n / 4)); }, iters), bytes);
+    long n4 = (long)(n / 4);
+    report("copy float4 nt-store grid-stride",
+           timeit([&] { hipLaunchKernelGGL(copy4_nt, dim3(8192), dim3(256), 0, 0, (const float4*)x,
+                                           (float4*)z, n4); }, iters), bytes);
+    report("copy float4 flat (1/thread)",
+           timeit([&] { hipLaunchKernelGGL(copy4_flat, dim3((n4 + 255) / 256), dim3(256), 0, 0,
+                                           (const float4*)x, (float4*)z, n4); }, iters), bytes);
+    report("copy float4 x4/thread",
+           timeit([&] { hipLaunchKernelGGL(copy4_x4, dim3((n4 + 1023) / 1024), dim3(256), 0, 0,
+                                           (const float4*)x, (float4*)z, n4); }, iters), bytes);
+    report("copy float4 x4/thread nt",
+           timeit([&] { hipLaunchKernelGGL(copy4_x4_nt, dim3((n4 + 1023) / 1024), dim3(256), 0, 0,
+                                           (const float4*)x, (float4*)z, n4); }, iters), bytes);
+    report("K1 dw3x3_fwd 16x256x256x96 pro+stats",
+           timeit([&] { CA(accunet_dw3x3_fwd(x, wt, bi, sc, sh, 1, 0, z, st, B, H, W, C, 0)); }, iters),
+           bytes);
+    report("K1 dw3x3_fwd flip (dgrad) no pro/stats",
+           timeit([&] { CA(accunet_dw3x3_fwd(x, wt, nullptr, nullptr, nullptr, 0, 1, z, nullptr, B, H, W, C, 0)); }, iters),
+           bytes);
+    size_t wse = accunet_dw3x3_wgrad_ws(B, H, W, C);
+    float* ws = dalloc(wse);
+    float *dw = dalloc(9 * C), *db = dalloc(C);
+    report("K1' dw3x3_wgrad 16x256x256x96 pro",
+           timeit([&] { CA(accunet_dw3x3_wgrad(x, z, sc, sh, 1, dw, db, B, H, W, C, ws, wse, 0)); }, iters),
+           bytes);
+    CK(hipFree(x)); CK(hipFree(z)); CK(hipFree(ws)); CK(hipFree(st));
+  }
+  // ---- K1 channel-width sweep (1..6 channel groups of 32) ----
+  if (getenv("KB_SWEEP")) {
+    for (int C : {32, 64, 96, 128, 192}) {
+      size_t n = (size_t)B * H * W * C;
+      float *x = dalloc(n), *z = dalloc(n), *wt = dalloc(9 * C, 0.3f), *bi = dalloc(C, 0.1f);
+      float *sc = dalloc(C, 1.f), *sh = dalloc(C, 0.1f);
+      int rows = accunet_dw3x3_rows(B, H, W, C);
+      double* st;
+      CK(hipMalloc(&st, (size_t)rows * 2 * C * sizeof(double)));
+      char name[96];
+      snprintf(name, sizeof name, "K1 sweep 16x256x256x%d", C);
+      report(name, timeit([&] { CA(accunet_dw3x3_fwd(x, wt, bi, sc, sh, 1, 0, z, st, B, H, W, C, 0)); }, iters),
+             2.0 * 4 * n);
+      CK(hipFree(x)); CK(hipFree(z)); CK(hipFree(st)); CK(hipFree(wt)); CK(hipFree(bi));
+      CK(hipFree(sc)); CK(hipFree(sh));
+    }
+  }
+  // ---- K3: cnv12 SE, C = 32 ----
+  {
+    const int C = 32, Cr = 4, HW = H * W;
+    size_t n = (size_t)B * HW * C;
+    float *z = dalloc(n), *out = dalloc(n), *dout = dalloc(n), *da = dalloc(n);
+    float *sc = dalloc(C, 1.f), *sh = dalloc(C, 0.1f);
+    float *w1 = dalloc(Cr * C, 0.3f), *b1 = dalloc(Cr, 0.1f), *w2 = dalloc(C * Cr, 0.3f),
+          *b2 = dalloc(C, 0.1f), *g = dalloc(C, 1.f), *be = dalloc(C, 0.1f), *rm = dalloc(C),
+          *rv = dalloc(C);
+    float *dw1 = dalloc(Cr * C), *db1 = dalloc(Cr), *dw2 = dalloc(C * Cr), *db2 = dalloc(C),
+          *dg = dalloc(C), *dbe = dalloc(C);
+    float* save = dalloc(accunet_se_save_elems(B, C, Cr));
+    size_t wse = accunet_se_ws_elems(B, HW, C, Cr);
+    float* ws = dalloc(wse);
+    double bytes = 2.0 * 4 * n;
+    report("copy float4 (same bytes as K3)",
+           timeit([&] { hipLaunchKernelGGL(copy4, dim3(8192), dim3(256), 0, 0, (const float4*)z,
+                                           (float4*)out, (long)(n / 4)); }, iters), bytes);
+    report("K3 se_fwd 16x65536x32 pro",
+           timeit([&] { CA(accunet_se_fwd(z, sc, sh, 1, B, HW, C, Cr, w1, b1, w2, b2, g, be, rm, rv,
+                                          nullptr, 0.1f, 1e-5f, 1, out, save, nullptr, ws, wse, 0)); }, iters),
+           bytes);
+    report("K3' se_bwd 16x65536x32 pro (2 rd + 1 rd/wr)",
+           timeit([&] { CA(accunet_se_bwd(z, dout, sc, sh, 1, B, HW, C, Cr, w1, w2, g, 1, save, da,
+                                          dw1, db1, dw2, db2, dg, dbe, ws, wse, 0)); }, iters),
+           4.0 * 4 * n);
+  }
+  CK(hipDeviceSynchronize());
+  return 0;
+}
