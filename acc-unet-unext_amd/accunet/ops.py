@@ -365,13 +365,15 @@ class _HancLayerFn(torch.autograd.Function):
             p4 = _empty((B, H // 4, W // 4, 2 * C), z) if k == 3 else None
             kern.hanc_pyramid_fwd(z, sc, sh, pro.act, B, H, W, C, k, p2, p4)
             g2 = _empty((B, H // 2, W // 2, N), z)
-            kern.gemm(P // 4, N, 2 * C, a=[p2], lda=[2 * C], b=Wp, ldb=J * C, b_offset=C, c=g2,
-                      ldc=N)
+            # coarse branches: few output tiles, long K (2C) -> split-K
+            keep_f = [kern.gemm(P // 4, N, 2 * C, a=[p2], lda=[2 * C], b=Wp, ldb=J * C,
+                                b_offset=C, c=g2, ldc=N, allow_split=True)]
             ups.append((g2, N, 1, 0))
             if k == 3:
                 g4 = _empty((B, H // 4, W // 4, N), z)
-                kern.gemm(P // 16, N, 2 * C, a=[p4], lda=[2 * C], b=Wp, ldb=J * C,
-                          b_offset=3 * C, c=g4, ldc=N)
+                keep_f.append(kern.gemm(P // 16, N, 2 * C, a=[p4], lda=[2 * C], b=Wp,
+                                        ldb=J * C, b_offset=3 * C, c=g4, ldc=N,
+                                        allow_split=True))
                 ups.append((g4, N, 2, 0))
         Z = _empty((B, H, W, N), z)
         stats = None

@@ -617,27 +617,46 @@ static int dw_ntl() {
 static int dw_rch_max() {
   static int v = -1;
   if (v < 0) {
-    const char* e = getenv("ACCUNET_DW_RCH");  // tuning knob (tools/kbench); default 4
-    v = e ? atoi(e) : 4;
+    const char* e = getenv("ACCUNET_DW_RCH");  // tuning knob (tools/kbench); default 32
+    v = e ? atoi(e) : 32;
     if (v < 1) v = 1;
   }
   return v;
 }
 
 // rch_max > 1 (forward only): strips of up to 8*rch_max rows, as long as the grid
-// keeps >= ~2048 workgroups (8 per CU); the weight-gradient kernel uses 1.
+// keeps >= 768 workgroups (3 per CU); the weight-gradient kernel uses 1.
 static DwTGeom dw_tgeom(int B, int H, int W, int C, int tcq, dim3* grid, int rch_max = 1) {
   DwTGeom g;
   g.B = B; g.H = H; g.W = W; g.C = C;
   g.tilesW = ceil_div(W, 256 / tcq);
   long cols = (long)B * g.tilesW * (C / 4 / tcq);
   int rch = 1;
-  while (rch * 2 <= rch_max && cols * ceil_div(H, DW_TR * rch * 2) >= 2048) rch *= 2;
+  static const char* force = getenv("ACCUNET_DW_RCH_FORCE");  // tuning knob (tools/kbench)
+  if (force && rch_max > 1) {
+    rch = atoi(force) > 0 ? atoi(force) : 1;
+  } else {
+      // pick the strip length by a wave-quantised cost model: a block costs its rows
+      // plus ~3 rows of unoverlapped prologue, and the grid runs in waves of
+      // 256 CUs x 3 resident blocks (measured on 16x256x256xC, tools/kbench)
+      long best = -1;
+      for (int r = 1; r <= rch_max; r *= 2) {
+        long nb = cols * ceil_div(H, DW_TR * r);
+        long waves = (nb + 767) / 768;
+        long cost = waves * (min(DW_TR * r, H) + 3);
+        if (best < 0 || cost < best) {
+          best = cost;
+          rch = r;
+        }
+        if (DW_TR * r >= H) break;
+      }
+  }
   g.rch = rch;
   g.ntl = dw_ntl();
   g.tilesH = ceil_div(H, DW_TR * rch);
   long nt = (long)B * g.tilesH * g.tilesW;
-  g.remap = (nt % 8 == 0) ? 1 : 0;
+  static const char* noremap = getenv("ACCUNET_DW_NOREMAP");  // tuning knob (tools/kbench)
+  g.remap = (nt % 8 == 0 && !noremap) ? 1 : 0;
   *grid = dim3((unsigned)nt, C / 4 / tcq);
   return g;
 }

@@ -1,0 +1,72 @@
+"""GEMM census of one training step: every accunet_gemm call of the canonical
+ACC_UNet at B16 256^2 timed in isolation (synchronise before/after), grouped by
+shape and mode, with achieved TFLOP/s against the 157.3 TFLOP/s fp32 MFMA peak.
+
+    python tools/gemm_census.py [--batch 16] [--size 256] [--top 40]
+"""
+import argparse
+import collections
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "acc-unet-unext_amd"))
+
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--top", type=int, default=40)
+    a = ap.parse_args()
+    from accunet import kern
+    from accunet import model as M
+    from accunet.train import TrainStep
+
+    torch.manual_seed(0)
+    dev = torch.device("cuda", 0)
+    model = M.VARIANTS["canonical"](3, 1, n_filts=32).to(dev).train()
+    step = TrainStep(model, lr=1e-3)
+    x = torch.randn(a.batch, 3, a.size, a.size, device=dev)
+    m = (torch.rand(a.batch, 1, a.size, a.size, device=dev) < 0.3).float()
+    step(x, m)
+    torch.cuda.synchronize()
+
+    rec = collections.defaultdict(list)
+    orig = kern.gemm
+
+    def timed(M_, N_, K_, **kw):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        r = orig(M_, N_, K_, **kw)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        key = (M_, N_, K_, kw.get("amode", 0), kw.get("bmode", 0), kw.get("pro_a", 0),
+               kw.get("pro_b", 0), len(kw.get("a", [])), len(kw.get("ups", ())),
+               bool(kw.get("allow_split")), kw.get("stats") is not None)
+        rec[key].append(dt)
+        return r
+
+    kern.gemm = timed
+    try:
+        step(x, m)
+    finally:
+        kern.gemm = orig
+    rows = []
+    for k, v in rec.items():
+        t = sum(v) / len(v)
+        fl = 2.0 * k[0] * k[1] * k[2]
+        rows.append((t * len(v), len(v), t, fl / t / 1e12, k))
+    rows.sort(key=lambda r: -r[0])
+    tot = sum(r[0] for r in rows)
+    print(f"total GEMM time (isolated, incl. launch) {tot * 1e3:.2f} ms over {sum(r[1] for r in rows)} calls")
+    print(f"{'ms':>8} {'n':>3} {'us/call':>9} {'TF/s':>7}  M N K amode bmode proA proB nsrc nup split stats")
+    for tt, n, t, tf, k in rows[:a.top]:
+        print(f"{tt * 1e3:8.3f} {n:3d} {t * 1e6:9.1f} {tf:7.1f}  {k}")
+
+
+if __name__ == "__main__":
+    main()
