@@ -78,8 +78,10 @@ gemm_f32_kernel(const GemmParams p) {
   constexpr int BK = GEMM_BK;
   constexpr int SA = BM + GEMM_PAD;
   constexpr int SB = BN + GEMM_PAD;
-  constexpr int NPA = (BM * 4 + GEMM_THREADS - 1) / GEMM_THREADS;
-  constexpr int NPB = (BN * 4 + GEMM_THREADS - 1) / GEMM_THREADS;
+  constexpr int QPR = BK / 4;  // float4 quads per BK-slice of one row
+  constexpr int NA4 = BM * QPR, NB4 = BN * QPR;  // float4 elements per stage
+  constexpr int NPA = (NA4 + GEMM_THREADS - 1) / GEMM_THREADS;
+  constexpr int NPB = (NB4 + GEMM_THREADS - 1) / GEMM_THREADS;
 
   __shared__ __attribute__((aligned(16))) float smem[2 * BK * SA + 2 * BK * SB];
   float* As = smem;
@@ -110,7 +112,7 @@ gemm_f32_kernel(const GemmParams p) {
 #pragma unroll
     for (int i = 0; i < NPA; ++i) {
       int idx = tid + i * GEMM_THREADS;
-      int r = idx >> 2;
+      int r = idx / QPR;
       uint32_t g = (uint32_t)(m0 + r);
       uint32_t q = fdiv(g, p.fW);
       a_w[i] = (int)(g - q * p.W);
@@ -128,11 +130,11 @@ gemm_f32_kernel(const GemmParams p) {
 #pragma unroll
       for (int i = 0; i < NPA; ++i) {
         int idx = tid + i * GEMM_THREADS;
-        int r = idx >> 2, q = idx & 3;
+        int r = idx / QPR, q = idx % QPR;
         int g = m0 + r;
         int k = k0 + 4 * q;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if ((idx < BM * 4) && (g < M)) {
+        if ((idx < NA4) && (g < M)) {
           if (VA) {
             if (k < K) {
               int s = 0;
@@ -175,11 +177,11 @@ gemm_f32_kernel(const GemmParams p) {
 #pragma unroll
       for (int i = 0; i < NPA; ++i) {
         int idx = tid + i * GEMM_THREADS;
-        int r = idx >> 2, q = idx & 3;
+        int r = idx / QPR, q = idx % QPR;
         int g = m0 + r;
         int k = k0 + 4 * q;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if ((idx < BM * 4) && (g < M)) {
+        if ((idx < NA4) && (g < M)) {
           if (VA) {  // cin % 4 == 0: the quad shares one tap
             if (k < K) {
               int tap = (int)fdiv((uint32_t)k, p.fC);
@@ -219,7 +221,7 @@ gemm_f32_kernel(const GemmParams p) {
         int k = k0 + kr;
         int m = m0 + 4 * q;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (idx < BM * 4 && k < kend) {
+        if (idx < NA4 && k < kend) {
           const float* ptr = Ab + (long)k * lda + m;
           if (VA) {
             if (m < M) v = ld4(ptr);
@@ -238,11 +240,11 @@ gemm_f32_kernel(const GemmParams p) {
 #pragma unroll
       for (int i = 0; i < NPB; ++i) {
         int idx = tid + i * GEMM_THREADS;
-        int r = idx >> 2, q = idx & 3;
+        int r = idx / QPR, q = idx % QPR;
         int n = n0 + r;
         int k = k0 + 4 * q;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (idx < BN * 4 && n < N) {
+        if (idx < NB4 && n < N) {
           const float* ptr = p.B + (long)n * p.ldb + k;
           if (VB) {
             if (k < kend) v = ld4(ptr);
@@ -263,7 +265,7 @@ gemm_f32_kernel(const GemmParams p) {
         int k = k0 + kr;
         int n = n0 + 4 * q;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (idx < BN * 4 && k < kend) {
+        if (idx < NB4 && k < kend) {
           const float* ptr = p.B + (long)k * p.ldb + n;
           if (VB) {
             if (n < N) v = ld4(ptr);
@@ -290,7 +292,7 @@ gemm_f32_kernel(const GemmParams p) {
         int k = k0 + kr;
         int n = n0 + 4 * q;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (idx < BN * 4 && k < kend) {
+        if (idx < NB4 && k < kend) {
           uint32_t qq = fdiv((uint32_t)k, p.fW);
           int ww0 = k - (int)qq * p.W;
           int hh0 = (int)(qq - fdiv(qq, p.fH) * p.H);
@@ -331,7 +333,7 @@ gemm_f32_kernel(const GemmParams p) {
 #pragma unroll
       for (int i = 0; i < NPA; ++i) {
         int idx = tid + i * GEMM_THREADS;
-        if (idx < BM * 4) {
+        if (idx < NA4) {
           int kr = idx / (BM / 4), q = idx % (BM / 4);
           st4(as + kr * SA + 4 * q, ra[i]);
         }
@@ -340,8 +342,8 @@ gemm_f32_kernel(const GemmParams p) {
 #pragma unroll
       for (int i = 0; i < NPA; ++i) {
         int idx = tid + i * GEMM_THREADS;
-        if (idx < BM * 4) {
-          int r = idx >> 2, q = idx & 3;
+        if (idx < NA4) {
+          int r = idx / QPR, q = idx % QPR;
           as[(4 * q + 0) * SA + r] = ra[i].x;
           as[(4 * q + 1) * SA + r] = ra[i].y;
           as[(4 * q + 2) * SA + r] = ra[i].z;
@@ -353,8 +355,8 @@ gemm_f32_kernel(const GemmParams p) {
 #pragma unroll
       for (int i = 0; i < NPB; ++i) {
         int idx = tid + i * GEMM_THREADS;
-        if (idx < BN * 4) {
-          int r = idx >> 2, q = idx & 3;
+        if (idx < NB4) {
+          int r = idx / QPR, q = idx % QPR;
           bs[(4 * q + 0) * SB + r] = rb[i].x;
           bs[(4 * q + 1) * SB + r] = rb[i].y;
           bs[(4 * q + 2) * SB + r] = rb[i].z;
@@ -365,7 +367,7 @@ gemm_f32_kernel(const GemmParams p) {
 #pragma unroll
       for (int i = 0; i < NPB; ++i) {
         int idx = tid + i * GEMM_THREADS;
-        if (idx < BN * 4) {
+        if (idx < NB4) {
           int kr = idx / (BN / 4), q = idx % (BN / 4);
           st4(bs + kr * SB + 4 * q, rb[i]);
         }

@@ -55,7 +55,7 @@ def parse():
     ap.add_argument("--eager", action="store_true",
                     help="launch every kernel from Python (default: replay one HIP graph per step)")
     ap.add_argument("--no-probe", action="store_true", help="skip the roofline probes")
-    ap.add_argument("--cpu-sample", type=int, default=1, help="images in the CPU sample")
+    ap.add_argument("--cpu-sample", type=int, default=3, help="images in the CPU sample")
     return ap.parse_args()
 
 
@@ -170,6 +170,15 @@ def main():
               probe.k3_se(B, S, S, blk.sqe.fc2.weight.shape[0], blk.sqe),
               probe.hanc_gemm(B * (S // 4) ** 2, model.cnv72.hnc.cnv.weight.shape[0],
                               model.cnv72.conv1.weight.shape[0])]
+        # HBM traffic of K1 from the committed PMC passes of this same bench command
+        # (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate runs; tools/pmc_traffic.py)
+        tf = os.path.join(ROOT, "profiles", "k1_traffic.json")
+        if os.path.exists(tf):
+            with open(tf) as f:
+                t = json.load(f)
+            if t.get("shape") == rl[0]["shape"]:
+                rl[0]["traffic"] = t["traffic_bytes"]
+                rl[0]["traffic_source"] = t.get("source", tf)
         line["roofline"] = rl[0]
         line["rooflines"] = rl
     if args.eager:
