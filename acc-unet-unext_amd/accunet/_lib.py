@@ -41,6 +41,8 @@ class AccGemmDesc(Structure):
         ("uplog", c_int * 3),
         ("stats", c_void_p),  # double*
         ("allow_split", c_int),
+        ("pd2", c_void_p), ("pd4", c_void_p),  # fused pyramid backward (float*)
+        ("mk2", c_void_p), ("mk4", c_void_p),  # first-max codes (uint8*)
     ]
 
 
@@ -67,7 +69,7 @@ _SIGS = {
     "accunet_dw3x3_fwd": [P, P, P, P, P, I, I, P, P, I, I, I, I, P],
     "accunet_dw3x3_wgrad_ws": [I, I, I, I],
     "accunet_dw3x3_wgrad": [P, P, P, P, I, P, P, I, I, I, I, P, S, P],
-    "accunet_hanc_pyramid_fwd": [P, P, P, I, I, I, I, I, I, P, P, P],
+    "accunet_hanc_pyramid_fwd": [P, P, P, I, I, I, I, I, I, P, P, P, P, P],
     "accunet_hanc_pyramid_bwd": [P, P, P, I, I, I, I, I, I, P, P, P, P, P, P],
     "accunet_pool2_fwd": [P, P, I, I, I, I, I, P],
     "accunet_pool2_bwd": [P, P, P, P, I, I, I, I, I, I, P],

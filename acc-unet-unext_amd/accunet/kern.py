@@ -49,11 +49,13 @@ def gemm(M: int, N: int, K: int, *, a: Sequence[torch.Tensor], lda: Sequence[int
          H: int = 1, W: int = 1, cin: int = 0,
          ups: Sequence = (), stats: Optional[torch.Tensor] = None,
          allow_split: bool = False, a_offsets: Optional[Sequence[int]] = None,
-         b_offset: int = 0, c_offset: int = 0):
+         b_offset: int = 0, c_offset: int = 0, pyr: Optional[Sequence] = None):
     """C[M,N] = A(M,K) B(K,N) (+bias) (+ups) on the current stream.
 
     `ups` is a sequence of (tensor, ld, log2_factor, col_offset) nearest-upsample addends.
     Offsets are element offsets into the respective tensors (column slices).
+    `pyr` = (dP2, dP4 or None, mk2, mk4 or None): HANCLayer pyramid backward fused into
+    the epilogue (H, W = image size; see AccGemmDesc.pd2).
     """
     d = AccGemmDesc()
     d.M, d.N, d.K = int(M), int(N), int(K)
@@ -91,6 +93,15 @@ def gemm(M: int, N: int, K: int, *, a: Sequence[torch.Tensor], lda: Sequence[int
         raise _lib.AccError("gemm.stats: fp64 partial-statistics buffer expected")
     d.stats = stats.data_ptr() if stats is not None else None
     d.allow_split = 1 if allow_split else 0
+    if pyr is not None:
+        pd2, pd4, mk2, mk4 = pyr
+        _check(pd2, "gemm.pd2")
+        if mk2.dtype != torch.uint8 or (mk4 is not None and mk4.dtype != torch.uint8):
+            raise _lib.AccError("gemm.pyr: uint8 first-max codes expected")
+        d.pd2 = pd2.data_ptr()
+        d.pd4 = pd4.data_ptr() if pd4 is not None else None
+        d.mk2 = mk2.data_ptr()
+        d.mk4 = mk4.data_ptr() if mk4 is not None else None
     ws = None
     ws_elems = 0
     if allow_split:
@@ -181,9 +192,10 @@ def dw3x3_wgrad(x, dz, sc, sh, act, dw, db, B, H, W, C):
     return ws
 
 
-def hanc_pyramid_fwd(x, sc, sh, act, B, H, W, C, k, p2, p4):
+def hanc_pyramid_fwd(x, sc, sh, act, B, H, W, C, k, p2, p4, mk2=None, mk4=None):
     call("accunet_hanc_pyramid_fwd", _p(x), _p(sc), _p(sh), int(act), B, H, W, C, k, _p(p2),
-         _p(p4), _stream())
+         _p(p4), None if mk2 is None else mk2.data_ptr(),
+         None if mk4 is None else mk4.data_ptr(), _stream())
 
 
 def hanc_pyramid_bwd(x, sc, sh, act, B, H, W, C, k, p2, p4, dp2, dp4, da):

@@ -359,11 +359,16 @@ class _HancLayerFn(torch.autograd.Function):
         Wp = _empty((N, J * C), z)
         kern.group_relayout(weight, Wp, N, C, J, _HANC_ORDER[k])
         ups = []
-        p2 = p4 = g2 = g4 = None
+        p2 = p4 = g2 = g4 = mk2 = mk4 = None
         if k >= 2:
             p2 = _empty((B, H // 2, W // 2, 2 * C), z)
             p4 = _empty((B, H // 4, W // 4, 2 * C), z) if k == 3 else None
-            kern.hanc_pyramid_fwd(z, sc, sh, pro.act, B, H, W, C, k, p2, p4)
+            # first-max codes: the backward routes max-pool gradients with them inside
+            # the x-branch data-gradient GEMM (no re-read of the activation)
+            mk2 = torch.empty((B, H // 2, W // 2, C), dtype=torch.uint8, device=z.device)
+            mk4 = (torch.empty((B, H // 4, W // 4, C), dtype=torch.uint8, device=z.device)
+                   if k == 3 else None)
+            kern.hanc_pyramid_fwd(z, sc, sh, pro.act, B, H, W, C, k, p2, p4, mk2, mk4)
             g2 = _empty((B, H // 2, W // 2, N), z)
             # coarse branches: few output tiles, long K (2C) -> split-K
             keep_f = [kern.gemm(P // 4, N, 2 * C, a=[p2], lda=[2 * C], b=Wp, ldb=J * C,
@@ -388,9 +393,9 @@ class _HancLayerFn(torch.autograd.Function):
         saved = [z, pro_g, Wp]
         ctx.has_p = k >= 2
         if k >= 2:
-            saved.append(p2)
+            saved += [p2, mk2]
             if k == 3:
-                saved.append(p4)
+                saved += [p4, mk4]
         ctx.save_for_backward(*saved)
         if stats is None:
             stats = _empty((0,), z)
@@ -405,21 +410,15 @@ class _HancLayerFn(torch.autograd.Function):
         P = B * H * W
         saved = ctx.saved_tensors
         z, pro_g, Wp = saved[:3]
-        p2 = saved[3] if k >= 2 else None
-        p4 = saved[4] if k == 3 else None
+        p2, mk2 = (saved[3], saved[4]) if k >= 2 else (None, None)
+        p4, mk4 = (saved[5], saved[6]) if k == 3 else (None, None)
         dZ = dZ.contiguous()
         pro = cfg.pro
         sc = pro.st[2] if pro.active else None
         sh = pro.st[3] if pro.active else None
         keep = []
         dWp = _empty((N, J * C), z)
-        # x branch
-        dA = torch.empty_like(z)
-        keep.append(kern.gemm(P, C, N, a=[dZ], lda=[N], b=Wp, ldb=J * C, bmode=BMODE_NN, c=dA,
-                              ldc=C))
-        keep.append(kern.gemm(N, C, P, a=[dZ], lda=[N], amode=AMODE_COL, b=z, ldb=C,
-                              bmode=BMODE_NN, c=dWp, ldc=J * C, c_offset=0,
-                              pro_b=_pro_mode(pro), b_scale=sc, b_shift=sh, allow_split=True))
+        dP2 = dP4 = None
         if k >= 2:
             dG2 = _empty((B, H // 2, W // 2, N), z)
             kern.upsample_bwd(dZ, N, 0, dG2, N, B, H, W, N, 2)
@@ -429,7 +428,6 @@ class _HancLayerFn(torch.autograd.Function):
             keep.append(kern.gemm(N, 2 * C, P // 4, a=[dG2], lda=[N], amode=AMODE_COL, b=p2,
                                   ldb=2 * C, bmode=BMODE_NN, c=dWp, ldc=J * C, c_offset=C,
                                   allow_split=True))
-            dP4 = None
             if k == 3:
                 dG4 = _empty((B, H // 4, W // 4, N), z)
                 kern.upsample_bwd(dZ, N, 0, dG4, N, B, H, W, N, 4)
@@ -439,7 +437,15 @@ class _HancLayerFn(torch.autograd.Function):
                 keep.append(kern.gemm(N, 2 * C, P // 16, a=[dG4], lda=[N], amode=AMODE_COL,
                                       b=p4, ldb=2 * C, bmode=BMODE_NN, c=dWp, ldc=J * C,
                                       c_offset=3 * C, allow_split=True))
-            kern.hanc_pyramid_bwd(z, sc, sh, pro.act, B, H, W, C, k, p2, p4, dP2, dP4, dA)
+        # x branch data gradient; for k >= 2 its epilogue adds the pyramid's backward
+        # (avg spread + first-max routing), so dA is written exactly once
+        dA = torch.empty_like(z)
+        keep.append(kern.gemm(P, C, N, a=[dZ], lda=[N], b=Wp, ldb=J * C, bmode=BMODE_NN, c=dA,
+                              ldc=C, H=H, W=W,
+                              pyr=(dP2, dP4, mk2, mk4) if k >= 2 else None))
+        keep.append(kern.gemm(N, C, P, a=[dZ], lda=[N], amode=AMODE_COL, b=z, ldb=C,
+                              bmode=BMODE_NN, c=dWp, ldc=J * C, c_offset=0,
+                              pro_b=_pro_mode(pro), b_scale=sc, b_shift=sh, allow_split=True))
         dW = _empty((N, J * C), z)
         kern.group_relayout(dWp, dW, N, C, J, _HANC_ORDER[k], inverse=True)
         db = _empty((N,), z)

@@ -185,21 +185,33 @@ affine_act_kernel(const float* __restrict__ x, const float* __restrict__ sc,
       s[j] = sc ? sc[t.c0 + j] : 1.f;
       h[j] = sh ? sh[t.c0 + j] : 0.f;
     }
-    for (long r = r0 + t.rg; r < r1; r += t.RG) {
-      long off = r * C + t.c0;
-      float v[V];
-      ldv<V>(x + off, v);
+    // rows are processed U at a time with all their loads issued first, so each
+    // thread keeps 2U-4U 16-byte loads in flight (latency hiding at 4 blocks/CU)
+    constexpr int U = 4;
+    for (long rb = r0 + t.rg; rb < r1; rb += U * t.RG) {
+      float v[U][V], q[U][V];
 #pragma unroll
-      for (int j = 0; j < V; ++j) v[j] = apply_act(v[j] * s[j] + h[j], act);
-      if (res) {
-        float q[V];
-        ldv<V>(res + off, q);
-#pragma unroll
-        for (int j = 0; j < V; ++j) v[j] += q[j];
+      for (int u = 0; u < U; ++u) {
+        long r = rb + (long)u * t.RG;
+        if (r < r1) {
+          ldv<V>(x + r * C + t.c0, v[u]);
+          if (res) ldv<V>(res + r * C + t.c0, q[u]);
+        }
       }
-      if (y) stv<V>(y + off, v);  // y == nullptr: statistics only (accunet_colsum)
 #pragma unroll
-      for (int j = 0; j < V; ++j) { a[j] += v[j]; b[j] += (double)v[j] * v[j]; }
+      for (int u = 0; u < U; ++u) {
+        long r = rb + (long)u * t.RG;
+        if (r < r1) {
+#pragma unroll
+          for (int j = 0; j < V; ++j) {
+            v[u][j] = apply_act(v[u][j] * s[j] + h[j], act);
+            if (res) v[u][j] += q[u][j];
+          }
+          if (y) stv<V>(y + r * C + t.c0, v[u]);  // y == nullptr: statistics only (accunet_colsum)
+#pragma unroll
+          for (int j = 0; j < V; ++j) { a[j] += v[u][j]; b[j] += (double)v[u][j] * v[u][j]; }
+        }
+      }
     }
   }
   if (stats) block_chan_reduce2<V>(t, a, b, stats, blockIdx.x, C);
@@ -262,17 +274,28 @@ bn_bwd_reduce_kernel(const float* __restrict__ x, const float* __restrict__ dy,
       s[j] = st[BN_SCALE * C + t.c0 + j];
       h[j] = st[BN_SHIFT * C + t.c0 + j];
     }
-    for (long r = r0 + t.rg; r < r1; r += t.RG) {
-      long off = r * C + t.c0;
-      float xv[V], dv[V];
-      ldv<V>(x + off, xv);
-      ldv<V>(dy + off, dv);
+    constexpr int U = 4;  // see affine_act_kernel
+    for (long rb = r0 + t.rg; rb < r1; rb += U * t.RG) {
+      float xv[U][V], dv[U][V];
 #pragma unroll
-      for (int j = 0; j < V; ++j) {
-        float g = dv[j];
-        if (act == ACT_LRELU) g *= lrelu_d(xv[j] * s[j] + h[j]);
-        a[j] += g;
-        b[j] += (double)g * ((double)xv[j] - mu[j]) * rs[j];
+      for (int u = 0; u < U; ++u) {
+        long r = rb + (long)u * t.RG;
+        if (r < r1) {
+          ldv<V>(x + r * C + t.c0, xv[u]);
+          ldv<V>(dy + r * C + t.c0, dv[u]);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (rb + (long)u * t.RG < r1) {
+#pragma unroll
+          for (int j = 0; j < V; ++j) {
+            float g = dv[u][j];
+            if (act == ACT_LRELU) g *= lrelu_d(xv[u][j] * s[j] + h[j]);
+            a[j] += g;
+            b[j] += (double)g * ((double)xv[u][j] - mu[j]) * rs[j];
+          }
+        }
       }
     }
   }
@@ -341,21 +364,33 @@ bn_bwd_apply_kernel(const float* __restrict__ x, const float* __restrict__ dy,
       k2[j] = coef[C + t.c0 + j];
       k3[j] = coef[2 * C + t.c0 + j];
     }
-    for (long r = r0 + t.rg; r < r1; r += t.RG) {
-      long off = r * C + t.c0;
-      float xv[V], dv[V], o[V];
-      ldv<V>(x + off, xv);
-      ldv<V>(dy + off, dv);
-      if (accumulate) ldv<V>(dx + off, o);
+    constexpr int U = 4;  // see affine_act_kernel
+    for (long rb = r0 + t.rg; rb < r1; rb += U * t.RG) {
+      float xv[U][V], dv[U][V], o[U][V];
 #pragma unroll
-      for (int j = 0; j < V; ++j) {
-        float g = dv[j];
-        if (act == ACT_LRELU) g *= lrelu_d(xv[j] * s[j] + h[j]);
-        float d = k1[j] * g + k2[j] * (xv[j] - mu[j]) + k3[j];
-        a[j] += d;
-        o[j] = accumulate ? o[j] + d : d;
+      for (int u = 0; u < U; ++u) {
+        long r = rb + (long)u * t.RG;
+        if (r < r1) {
+          ldv<V>(x + r * C + t.c0, xv[u]);
+          ldv<V>(dy + r * C + t.c0, dv[u]);
+          if (accumulate) ldv<V>(dx + r * C + t.c0, o[u]);
+        }
       }
-      stv<V>(dx + off, o);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        long r = rb + (long)u * t.RG;
+        if (r < r1) {
+#pragma unroll
+          for (int j = 0; j < V; ++j) {
+            float g = dv[u][j];
+            if (act == ACT_LRELU) g *= lrelu_d(xv[u][j] * s[j] + h[j]);
+            float d = k1[j] * g + k2[j] * (xv[u][j] - mu[j]) + k3[j];
+            a[j] += d;
+            o[u][j] = accumulate ? o[u][j] + d : d;
+          }
+          stv<V>(dx + r * C + t.c0, o[u]);
+        }
+      }
     }
   }
   if (colsum) block_chan_reduce2<V>(t, a, b, colsum, blockIdx.x, C);

@@ -51,6 +51,39 @@ ACC_DEV void block_chan_reduce2(const ChanTile& t, T (&a)[V], T (&b)[V], T* out,
                                 int C) {
   __shared__ T red[2][256 * 4];
   int tid = threadIdx.x;
+  if ((t.TCQ & (t.TCQ - 1)) == 0) {
+    // power-of-two slot count: lanes sharing a channel vector are xor partners;
+    // reduce within the wave, then the 4 wave sums in order (deterministic)
+    for (int off = t.TCQ; off < 64; off <<= 1) {
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        a[j] += __shfl_xor(a[j], off);
+        b[j] += __shfl_xor(b[j], off);
+      }
+    }
+    const int lane = tid & 63, wave = tid >> 6;
+    if (lane < t.TCQ) {
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        red[0][(wave * 64 + lane) * V + j] = a[j];
+        red[1][(wave * 64 + lane) * V + j] = b[j];
+      }
+    }
+    __syncthreads();
+    if (tid < t.TCQ && t.cq < t.CQ) {
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        T sa = 0, sb = 0;
+        for (int w = 0; w < 4; ++w) {
+          sa += red[0][(w * 64 + tid) * V + j];
+          sb += red[1][(w * 64 + tid) * V + j];
+        }
+        out[row * 2 * C + t.c0 + j] = sa;
+        out[row * 2 * C + C + t.c0 + j] = sb;
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < V; ++j) {
     red[0][tid * V + j] = a[j];

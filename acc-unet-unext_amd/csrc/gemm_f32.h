@@ -26,6 +26,7 @@
 // conflict-free ds_read_b32 (lanes 0-31 and 32-63 sit in different bank groups).
 #pragma once
 #include "common.h"
+#include "chan.h"
 
 enum { AM_ROW = 0, AM_COL = 1, AM_SHIFT3 = 2 };
 enum { BM_NT = 0, BM_NN = 1, BM_NN_SHIFT3 = 2 };
@@ -57,8 +58,14 @@ struct GemmParams {
   int upld[3];
   int uplog[3];  // log2 of the nearest-upsample factor of each added source
   double* stats;  // [gridDim.x][2][N] fp64 partial column (sum, sumsq) of final C, or null
+  // fused HANCLayer pyramid backward (see AccGemmDesc in include/accunet.h)
+  const float* pd2;
+  const float* pd4;
+  const unsigned char* mk2;
+  const unsigned char* mk4;
   int kchunk;    // K range per blockIdx.z (split-K); >= K means no split
   size_t zstride;  // element stride between split-K partial slabs
+  int evec;      // epilogue may use 16-byte accesses (host-checked alignment)
 };
 
 template <int PRO>
@@ -414,92 +421,149 @@ gemm_f32_kernel(const GemmParams p) {
   }
 
   // ------------------------------- epilogue ---------------------------------
-  if (gridDim.z > 1) {
-    float* Cz = p.C + (size_t)blockIdx.z * p.zstride;
+  // The accumulators are staged through LDS one 32-row subtile per wave at a time
+  // (pass i of TM) and re-read by a row-major thread layout: thread (rr, cq) owns
+  // column quad cq of tile rows rr, rr + RPP, ... so bias / up-adds / pyramid
+  // terms / stores are 16-byte, row-contiguous accesses (a tile row is BN*4 bytes
+  // of one C row) and the per-column fp64 statistics stay per thread until one
+  // deterministic block reduction at the end.
+  constexpr int CQN = BN / 4;               // column quads per tile row
+  constexpr int RPP = GEMM_THREADS / CQN;   // tile rows per sweep
+  constexpr int PR = WM * 32;               // tile rows staged per pass
+  constexpr int SC = BN + 4;                // LDS row stride (floats)
+  static_assert(PR * SC <= 2 * BK * SA + 2 * BK * SB, "epilogue staging exceeds the LDS tile");
+  static_assert(GEMM_THREADS % CQN == 0, "BN/4 must divide the block");
+  const bool split = gridDim.z > 1;
+  float* Cout = split ? p.C + (size_t)blockIdx.z * p.zstride : p.C;
+  const int cq = tid % CQN, rr0 = tid / CQN;
+  const int nq = n0 + 4 * cq;
+  const bool evec = p.evec && (nq + 3 < N);
+  float bq[4] = {0.f, 0.f, 0.f, 0.f};
+  if (!split && p.bias) {
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        int n = n0 + wn * TN * 32 + j * 32 + l31;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-          if (m < M && n < N) Cz[(size_t)m * p.ldc + n] = acc[i][j][r];
-        }
-      }
-    return;
+    for (int e = 0; e < 4; ++e) bq[e] = (nq + e < N) ? p.bias[nq + e] : 0.f;
   }
-
-  double s1[TN], s2[TN];  // BatchNorm statistics accumulate in fp64 (as ATen's CPU BN)
-#pragma unroll
-  for (int j = 0; j < TN; ++j) { s1[j] = 0.0; s2[j] = 0.0; }
-
+  double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+  const bool need_pix = !split && (p.nup > 0 || p.pd2);
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
+    __syncthreads();  // LDS free (main loop / previous pass)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-      if (m >= M) continue;
-      long upoff[3] = {0, 0, 0};
-      if (p.nup > 0) {
-        uint32_t q = fdiv((uint32_t)m, p.fW);
-        int w = m - (int)q * p.W;
-        uint32_t b = fdiv(q, p.fH);
-        int h = (int)(q - b * p.H);
+    for (int j = 0; j < TN; ++j)
 #pragma unroll
-        for (int u = 0; u < 3; ++u) {
-          if (u < p.nup) {
-            int lg = p.uplog[u];
-            int Hs = p.H >> lg, Ws = p.W >> lg;
-            upoff[u] = (((long)b * Hs + (h >> lg)) * Ws + (w >> lg)) * p.upld[u];
+      for (int r = 0; r < 16; ++r)
+        smem[(wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * SC + wn * TN * 32 + j * 32 + l31] =
+            acc[i][j][r];
+    __syncthreads();
+    for (int rr = rr0; rr < PR; rr += RPP) {
+      const int m = m0 + (rr >> 5) * TM * 32 + i * 32 + (rr & 31);
+      if (m >= M || nq >= N) continue;
+      float4 a4 = *reinterpret_cast<const float4*>(smem + rr * SC + 4 * cq);
+      float v[4] = {a4.x, a4.y, a4.z, a4.w};
+      if (!split) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += bq[e];
+        if (need_pix) {
+          uint32_t q = fdiv((uint32_t)m, p.fW);
+          const int w = m - (int)q * p.W;
+          const uint32_t b = fdiv(q, p.fH);
+          const int h = (int)(q - b * p.H);
+          for (int u = 0; u < p.nup; ++u) {
+            const int lg = p.uplog[u];
+            const long uo = (((long)b * (p.H >> lg) + (h >> lg)) * (p.W >> lg) + (w >> lg)) *
+                                p.upld[u] + nq;
+            if (evec) {
+              float4 t4 = ld4(p.up[u] + uo);
+              v[0] += t4.x; v[1] += t4.y; v[2] += t4.z; v[3] += t4.w;
+            } else {
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                if (nq + e < N) v[e] += p.up[u][uo + e];
+            }
+          }
+          if (p.pd2) {
+            // same accumulation order as the standalone pyramid backward:
+            // g = (avg2/4 [+ max2]) + avg4/16 [+ max4]; C += g
+            const long q2 = ((long)b * (p.H >> 1) + (h >> 1)) * (p.W >> 1) + (w >> 1);
+            const long q4 = ((long)b * (p.H >> 2) + (h >> 2)) * (p.W >> 2) + (w >> 2);
+            const int pos2 = (h & 1) * 2 + (w & 1), pos4 = (h & 3) * 4 + (w & 3);
+            float av2[4], mx2[4], av4[4] = {0.f, 0.f, 0.f, 0.f}, mx4[4] = {0.f, 0.f, 0.f, 0.f};
+            unsigned c2[4], c4[4] = {255u, 255u, 255u, 255u};
+            if (evec) {  // 16-byte rows of dP, 4-byte rows of codes
+              float4 t = ld4(p.pd2 + q2 * 2 * N + nq);
+              av2[0] = t.x; av2[1] = t.y; av2[2] = t.z; av2[3] = t.w;
+              t = ld4(p.pd2 + q2 * 2 * N + N + nq);
+              mx2[0] = t.x; mx2[1] = t.y; mx2[2] = t.z; mx2[3] = t.w;
+              unsigned k2 = *reinterpret_cast<const unsigned*>(p.mk2 + q2 * N + nq);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) c2[e] = (k2 >> (8 * e)) & 255u;
+              if (p.pd4) {
+                t = ld4(p.pd4 + q4 * 2 * N + nq);
+                av4[0] = t.x; av4[1] = t.y; av4[2] = t.z; av4[3] = t.w;
+                t = ld4(p.pd4 + q4 * 2 * N + N + nq);
+                mx4[0] = t.x; mx4[1] = t.y; mx4[2] = t.z; mx4[3] = t.w;
+                unsigned k4 = *reinterpret_cast<const unsigned*>(p.mk4 + q4 * N + nq);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) c4[e] = (k4 >> (8 * e)) & 255u;
+              }
+            } else {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const int n = nq + e < N ? nq + e : N - 1;
+                av2[e] = p.pd2[q2 * 2 * N + n];
+                mx2[e] = p.pd2[q2 * 2 * N + N + n];
+                c2[e] = p.mk2[q2 * N + n];
+                if (p.pd4) {
+                  av4[e] = p.pd4[q4 * 2 * N + n];
+                  mx4[e] = p.pd4[q4 * 2 * N + N + n];
+                  c4[e] = p.mk4[q4 * N + n];
+                }
+              }
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              float g = av2[e] * 0.25f;
+              if (c2[e] == (unsigned)pos2) g += mx2[e];
+              if (p.pd4) {
+                g += av4[e] * (1.f / 16.f);
+                if (c4[e] == (unsigned)pos4) g += mx4[e];
+              }
+              v[e] += g;
+            }
           }
         }
+        if (p.stats) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (nq + e < N) {
+              s1[e] += v[e];
+              s2[e] += (double)v[e] * v[e];
+            }
+        }
       }
+      float* dst = Cout + (size_t)m * (split ? N : p.ldc) + nq;
+      if (evec) {
+        st4(dst, make_float4(v[0], v[1], v[2], v[3]));
+      } else {
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        int n = n0 + wn * TN * 32 + j * 32 + l31;
-        if (n >= N) continue;
-        float v = acc[i][j][r];
-        if (p.bias) v += p.bias[n];
-#pragma unroll
-        for (int u = 0; u < 3; ++u)
-          if (u < p.nup) v += p.up[u][upoff[u] + n];
-        p.C[(size_t)m * p.ldc + n] = v;
-        s1[j] += v;
-        s2[j] += (double)v * v;
+        for (int e = 0; e < 4; ++e)
+          if (nq + e < N) dst[e] = v[e];
       }
     }
   }
 
-  if (p.stats) {
-    // reduce over the two half-waves, then across the WM waves sharing columns
+  if (!split && p.stats) {
+    __syncthreads();  // LDS reused as the reduction buffer
+    double vv[8] = {s1[0], s1[1], s1[2], s1[3], s2[0], s2[1], s2[2], s2[3]};
+    if (block_slot_reduce<CQN, 8, double>(vv, reinterpret_cast<double*>(smem))) {
+      // thread tid (< CQN) holds column quad tid
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      s1[j] += __shfl_xor(s1[j], 32);
-      s2[j] += __shfl_xor(s2[j], 32);
-    }
-    __syncthreads();  // smem reuse
-    double* red = reinterpret_cast<double*>(smem);  // [WM][2][BN]
-    if (lh == 0) {
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        int c = wn * TN * 32 + j * 32 + l31;
-        red[(wm * 2 + 0) * BN + c] = s1[j];
-        red[(wm * 2 + 1) * BN + c] = s2[j];
-      }
-    }
-    __syncthreads();
-    for (int c = tid; c < BN; c += GEMM_THREADS) {
-      int n = n0 + c;
-      if (n < N) {
-        double a = 0.0, b = 0.0;
-#pragma unroll
-        for (int w = 0; w < WM; ++w) {
-          a += red[(w * 2 + 0) * BN + c];
-          b += red[(w * 2 + 1) * BN + c];
+      for (int e = 0; e < 4; ++e) {
+        const int n = n0 + 4 * tid + e;
+        if (n < N) {
+          p.stats[((size_t)blockIdx.x * 2 + 0) * N + n] = vv[e];
+          p.stats[((size_t)blockIdx.x * 2 + 1) * N + n] = vv[4 + e];
         }
-        p.stats[((size_t)blockIdx.x * 2 + 0) * N + n] = a;
-        p.stats[((size_t)blockIdx.x * 2 + 1) * N + n] = b;
       }
     }
   }

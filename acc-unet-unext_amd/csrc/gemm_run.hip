@@ -116,7 +116,8 @@ int gemm_run(GemmParams p, int amode, int bmode, int pro_a, int pro_b, bool allo
   p.zstride = 0;
   float* Cfinal = p.C;
   int ldc_final = p.ldc;
-  if (allow_split && ws != nullptr && p.bias == nullptr && p.nup == 0 && p.stats == nullptr) {
+  if (allow_split && ws != nullptr && p.bias == nullptr && p.nup == 0 && p.stats == nullptr &&
+      p.pd2 == nullptr) {
     long tiles = (long)gx * gy;
     long target = 1024;
     long maxS = p.K / (GEMM_BK * 4);
@@ -133,6 +134,13 @@ int gemm_run(GemmParams p, int amode, int bmode, int pro_a, int pro_b, bool allo
       p.C = ws;
       p.ldc = p.N;
     }
+  }
+  {
+    // 16-byte epilogue accesses: C rows, up-add rows and pyramid rows all 4-float aligned
+    bool ev = (p.N % 4 == 0) && (p.ldc % 4 == 0) && (((uintptr_t)p.C & 15) == 0);
+    for (int u = 0; u < p.nup; ++u)
+      if ((p.upld[u] % 4) || ((uintptr_t)p.up[u] & 15)) ev = false;
+    p.evec = ev ? 1 : 0;
   }
   dim3 grid(gx, gy, S);
   hipLaunchKernelGGL(tab[t], grid, dim3(GEMM_THREADS), 0, stream, p);
@@ -188,6 +196,13 @@ extern "C" int accunet_gemm(const AccGemmDesc* d, float* ws, size_t ws_elems, vo
     p.uplog[u] = d->uplog[u];
   }
   p.stats = d->stats;
+  p.pd2 = d->pd2;
+  p.pd4 = d->pd4;
+  p.mk2 = d->mk2;
+  p.mk4 = d->mk4;
+  if (p.pd2 && (!p.mk2 || (p.pd4 && !p.mk4) || (p.H & 1) || (p.W & 1) ||
+                (p.pd4 && ((p.H & 3) || (p.W & 3))) || p.ldc != p.N))
+    return ACC_EBADARG;
   return gemm_run(p, d->amode, d->bmode, d->pro_a, d->pro_b, d->allow_split != 0, ws, ws_elems,
                   (hipStream_t)stream);
 }

@@ -19,7 +19,8 @@
 __global__ void __launch_bounds__(256)
 hanc_pyramid_fwd_kernel(const float* __restrict__ x, const float* __restrict__ sc,
                         const float* __restrict__ sh, int act, int B, int H, int W, int C, int k,
-                        float* __restrict__ p2, float* __restrict__ p4) {
+                        float* __restrict__ p2, float* __restrict__ p4,
+                        unsigned char* __restrict__ mk2, unsigned char* __restrict__ mk4) {
   // k == 3: cell = 4x4 (one P4 pixel, four P2 pixels); k == 2: cell = 2x2 (one P2 pixel)
   const int cs = (k == 3) ? 4 : 2;
   const int Hc = H / cs, Wc = W / cs;
@@ -53,9 +54,14 @@ hanc_pyramid_fwd_kernel(const float* __restrict__ x, const float* __restrict__ s
         float a2 = v[2 * qy + 1][2 * qx], a3 = v[2 * qy + 1][2 * qx + 1];
         float sum = ((a0 + a1) + a2) + a3;  // torch CPU avg_pool2d summation order
         float mx = fmaxf(fmaxf(a0, a1), fmaxf(a2, a3));
-        long o = (((long)b * H2 + hc * n2 + qy) * W2 + wc * n2 + qx) * (2 * C);
+        long q2 = ((long)b * H2 + hc * n2 + qy) * W2 + wc * n2 + qx;
+        long o = q2 * (2 * C);
         p2[o + c] = sum * 0.25f;
         p2[o + C + c] = mx;
+        if (mk2) {  // first maximum in window order (0,0) (0,1) (1,0) (1,1)
+          unsigned char code = a0 == mx ? 0 : a1 == mx ? 1 : a2 == mx ? 2 : a3 == mx ? 3 : 255;
+          mk2[q2 * C + c] = code;
+        }
       }
     if (k == 3) {
 #pragma unroll
@@ -65,9 +71,17 @@ hanc_pyramid_fwd_kernel(const float* __restrict__ x, const float* __restrict__ s
           s4 += v[dy][dx];
           m4 = fmaxf(m4, v[dy][dx]);
         }
-      long o = (((long)b * Hc + hc) * Wc + wc) * (2 * C);
+      long q4 = ((long)b * Hc + hc) * Wc + wc;
+      long o = q4 * (2 * C);
       p4[o + c] = s4 * (1.f / 16.f);
       p4[o + C + c] = m4;
+      if (mk4) {
+        unsigned char code = 255;
+#pragma unroll
+        for (int e = 15; e >= 0; --e)
+          if (v[e >> 2][e & 3] == m4) code = (unsigned char)e;
+        mk4[q4 * C + c] = code;
+      }
     }
   }
 }
@@ -156,13 +170,14 @@ static int grid_for(long total) {
 
 extern "C" int accunet_hanc_pyramid_fwd(const float* x, const float* sc, const float* sh, int act,
                                         int B, int H, int W, int C, int k, float* p2, float* p4,
-                                        void* stream) {
+                                        unsigned char* mk2, unsigned char* mk4, void* stream) {
   if (k < 2 || k > 3) return ACC_EBADARG;
   int cs = (k == 3) ? 4 : 2;
   if (H % cs || W % cs) return ACC_EBADSHAPE;
   long total = (long)B * (H / cs) * (W / cs) * C;
   hipLaunchKernelGGL(hanc_pyramid_fwd_kernel, dim3(grid_for(total)), dim3(256), 0,
-                     (hipStream_t)stream, x, sc, sh, act, B, H, W, C, k, p2, p4);
+                     (hipStream_t)stream, x, sc, sh, act, B, H, W, C, k, p2, p4, mk2,
+                     k == 3 ? mk4 : nullptr);
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 

@@ -63,6 +63,16 @@ typedef struct AccGemmDesc {
   int uplog[3];
   double* stats;            /* [rows][2][N] fp64 partial (sum,sumsq) of C, or NULL */
   int allow_split;          /* split-K through ws (weight gradients) */
+  /* HANCLayer pyramid backward fused into the x-branch data-gradient epilogue
+   * (ACC_UNet/ACC_UNet.py:86-106 pooling + nearest upsample, differentiated):
+   * C[m,n] += dP2avg/4 + [argmax2 == pos] dP2max + dP4avg/16 + [argmax4 == pos] dP4max
+   * with dP2 = pd2 [P/4][2N] ([avg | max] columns), dP4 = pd4 [P/16][2N] (or NULL),
+   * mk2 [P/4][N], mk4 [P/16][N] the first-max codes written by
+   * accunet_hanc_pyramid_fwd. pd2 == NULL disables it. */
+  const float* pd2;
+  const float* pd4;
+  const unsigned char* mk2;
+  const unsigned char* mk4;
 } AccGemmDesc;
 
 int accunet_gemm(const AccGemmDesc* d, float* ws, size_t ws_elems, void* stream);
@@ -116,10 +126,14 @@ int accunet_dw3x3_wgrad(const float* x, const float* dz, const float* sc, const 
 /* ------------------------------------------------------------------------- *
  * HANCLayer neighbourhood pyramid (ACC_UNet/ACC_UNet.py:86-106): from
  * a = act(x*sc+sh): P2 = [avg2 a | max2 a] at H/2, P4 = [avg4 a | max4 a] at H/4
- * (k = 3) in one read. Backward accumulates into da (max: first max in window).
+ * (k = 3) in one read. mk2 / mk4 (optional, uint8 [P/4][C] / [P/16][C]) receive the
+ * index of the first maximum in each window (row-major, 255 if none), which the
+ * x-branch data-gradient GEMM uses to route the max-pool gradient (AccGemmDesc.pd2).
+ * Backward (standalone form) accumulates into da (max: first max in window).
  * ------------------------------------------------------------------------- */
 int accunet_hanc_pyramid_fwd(const float* x, const float* sc, const float* sh, int act, int B,
-                             int H, int W, int C, int k, float* p2, float* p4, void* stream);
+                             int H, int W, int C, int k, float* p2, float* p4,
+                             unsigned char* mk2, unsigned char* mk4, void* stream);
 int accunet_hanc_pyramid_bwd(const float* x, const float* sc, const float* sh, int act, int B,
                              int H, int W, int C, int k, const float* p2, const float* p4,
                              const float* dp2, const float* dp4, float* da, void* stream);

@@ -175,6 +175,21 @@ int main(int argc, char** argv) {
     report("copy float4 (same bytes as K3)",
            timeit([&] { hipLaunchKernelGGL(copy4, dim3(8192), dim3(256), 0, 0, (const float4*)z,
                                            (float4*)out, (long)(n / 4)); }, iters), bytes);
+    {
+      int rows = accunet_stream_rows((long)B * HW, C);
+      double* st2;
+      CK(hipMalloc(&st2, (size_t)rows * 2 * C * sizeof(double)));
+      report("affine_act+stats 16x65536x32 (1 rd + 1 wr)",
+             timeit([&] { CA(accunet_affine_act_fwd(z, sc, sh, 1, nullptr, out, (long)B * HW, C, st2,
+                                                    nullptr, 0)); }, iters), bytes);
+      float* stb = dalloc(4 * C, 1.f);
+      size_t bws = accunet_bn_bwd_ws_elems((long)B * HW, C);
+      float* bw = dalloc(bws);
+      report("bn_bwd 16x65536x32 (rd 2 + rd 2 + wr 1)",
+             timeit([&] { CA(accunet_bn_bwd(z, dout, stb, g, 1, 1, (long)B * HW, C, da, 0, dg, dbe,
+                                            nullptr, nullptr, bw, bws, 0)); }, iters),
+             5.0 * 4 * n);
+    }
     report("K3 se_fwd 16x65536x32 pro",
            timeit([&] { CA(accunet_se_fwd(z, sc, sh, 1, B, HW, C, Cr, w1, b1, w2, b2, g, be, rm, rv,
                                           nullptr, 0.1f, 1e-5f, 1, out, save, nullptr, ws, wse, 0)); }, iters),
