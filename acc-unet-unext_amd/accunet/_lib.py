@@ -83,6 +83,8 @@ _SIGS = {
     "accunet_se_fwd": [P, P, P, I, I, I, I, I, P, P, P, P, P, P, P, P, P, F, F, I, P, P, P, P, S, P],
     "accunet_se_stats_rows": [I, I, I],
     "accunet_se_bwd": [P, P, P, P, I, I, I, I, I, P, P, P, I, P, P, P, P, P, P, P, P, P, S, P],
+    "accunet_se_bwd_pro": [P, P, P, I, P, I, I, I, I, I, P, P, P, I, P, P, P, P, P, P, P, P, P, P,
+                           P, S, P],
     "accunet_head_fwd": [P, P, P, I, P, L, I, P],
     "accunet_head_ws_elems": [L, I],
     "accunet_head_bwd": [P, P, P, P, I, P, P, P, L, I, P, S, P],

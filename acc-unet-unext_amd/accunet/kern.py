@@ -275,6 +275,19 @@ def se_bwd(z, dout, sc, sh, act, B, HW, C, Cr, w1, w2, gamma, training, save, da
     return ws
 
 
+def se_bwd_pro(z, dout, pst, act, pgamma, ptraining, B, HW, C, Cr, w1, w2, gamma, training, save,
+               dz, dpgamma, dpbeta, dw1, db1, dw2, db2, dgamma, dbeta):
+    """SE backward fused with the backward of its BatchNorm(+act) prologue (pst = [4][C]
+    mean, rstd, scale, shift of that BatchNorm): writes dz and the prologue's dgamma/dbeta."""
+    n = se_ws_elems(B, HW, C, Cr)
+    ws = workspace(n, z.device)
+    call("accunet_se_bwd_pro", _p(z), _p(dout), _p(pst), int(act), _p(pgamma),
+         1 if ptraining else 0, B, HW, C, Cr, _p(w1), _p(w2), _p(gamma), 1 if training else 0,
+         _p(save), _p(dz), _p(dpgamma), _p(dpbeta), _p(dw1), _p(db1), _p(dw2), _p(db2),
+         _p(dgamma), _p(dbeta), _p(ws), n, _stream())
+    return ws
+
+
 def head_fwd(x, w, b, sigm, y, P, C):
     call("accunet_head_fwd", _p(x), _p(w), _p(b), 1 if sigm else 0, _p(y), int(P), int(C),
          _stream())

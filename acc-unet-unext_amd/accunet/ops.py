@@ -174,11 +174,14 @@ class _PWConvFn(torch.autograd.Function):
         if stats is None:
             stats = _empty((0,), weight)
         ctx.mark_non_differentiable(stats)
+        ctx.set_materialize_grads(False)
         ctx.rows = rows
         return Z, stats
 
     @staticmethod
     def backward(ctx, dZ, _dstats):
+        if dZ is None:  # output unused: every input gradient is zero
+            return (None,) * (5 + ctx.cfg.nsrc + len(ctx.up_shapes))
         cfg = ctx.cfg
         weight, pro_g, *srcs = ctx.saved_tensors
         dZ = dZ.contiguous()
@@ -292,10 +295,13 @@ class _DWConvFn(torch.autograd.Function):
         if stats is None:
             stats = _empty((0,), z)
         ctx.mark_non_differentiable(stats)
+        ctx.set_materialize_grads(False)
         return Z, stats
 
     @staticmethod
     def backward(ctx, dZ, _ds):
+        if dZ is None:  # output unused: every input gradient is zero
+            return (None,) * 6
         cfg = ctx.cfg
         z, pro_g, weight = ctx.saved_tensors
         dZ = dZ.contiguous()
@@ -400,10 +406,13 @@ class _HancLayerFn(torch.autograd.Function):
         if stats is None:
             stats = _empty((0,), z)
         ctx.mark_non_differentiable(stats)
+        ctx.set_materialize_grads(False)
         return Z, stats
 
     @staticmethod
     def backward(ctx, dZ, _ds):
+        if dZ is None:  # output unused: every input gradient is zero
+            return (None,) * 6
         cfg = ctx.cfg
         B, H, W, C, N, k = cfg.B, cfg.H, cfg.W, cfg.C, cfg.N, cfg.k
         J = 2 * k - 1
@@ -497,10 +506,13 @@ class _BnActAddFn(torch.autograd.Function):
         if stats is None:
             stats = _empty((0,), z)
         ctx.mark_non_differentiable(stats)
+        ctx.set_materialize_grads(False)
         return y, stats
 
     @staticmethod
     def backward(ctx, dy, _ds):
+        if dy is None:  # output unused: every input gradient is zero
+            return (None,) * 5
         cfg = ctx.cfg
         z, pro_g = ctx.saved_tensors
         dy = dy.contiguous()
@@ -562,27 +574,37 @@ class _SEFn(torch.autograd.Function):
         if ostats is None:
             ostats = _empty((0,), z)
         ctx.mark_non_differentiable(ostats)
+        ctx.set_materialize_grads(False)
         return out, ostats
 
     @staticmethod
     def backward(ctx, dout, _dst):
+        if dout is None:  # output unused: every input gradient is zero
+            return (None,) * 10
         cfg = ctx.cfg
         z, pro_g, w1, w2, g, save = ctx.saved_tensors
         dout = dout.contiguous()
         B, HW, C, Cr = cfg.B, cfg.HW, cfg.C, cfg.Cr
         pro = cfg.pro
-        da = torch.empty_like(z)
         dw1 = torch.empty_like(w1)
         db1 = _empty((Cr,), z)
         dw2 = torch.empty_like(w2)
         db2 = _empty((C,), z)
         dg = _empty((C,), z)
         dbeta = _empty((C,), z)
-        kern.se_bwd(z, dout, pro.st[2] if pro.active else None,
-                    pro.st[3] if pro.active else None, pro.act, B, HW, C, Cr, w1, w2, g,
-                    cfg.training, save, da, dw1, db1, dw2, db2, dg, dbeta)
-        dz, dpg, dpb = _pro_bwd(pro, z, pro_g, da)
-        return None, dz, dpg, dpb, dw1, db1, dw2, db2, dg, dbeta
+        if pro.active:
+            # the preceding BatchNorm(+act)'s backward rides on the SE's two passes
+            dz = torch.empty_like(z)
+            dpg = _empty((C,), z)
+            dpb = _empty((C,), z)
+            kern.se_bwd_pro(z, dout, pro.st, pro.act, pro_g, pro.training, B, HW, C, Cr, w1,
+                            w2, g, cfg.training, save, dz, dpg, dpb, dw1, db1, dw2, db2, dg,
+                            dbeta)
+            return None, dz, dpg, dpb, dw1, db1, dw2, db2, dg, dbeta
+        da = torch.empty_like(z)
+        kern.se_bwd(z, dout, None, None, pro.act, B, HW, C, Cr, w1, w2, g, cfg.training, save,
+                    da, dw1, db1, dw2, db2, dg, dbeta)
+        return None, da, None, None, dw1, db1, dw2, db2, dg, dbeta
 
 
 def se(x, mod, *, consumer_bn=None):
@@ -636,10 +658,13 @@ class _Conv3x3Fn(torch.autograd.Function):
         if stats is None:
             stats = _empty((0,), x)
         ctx.mark_non_differentiable(stats)
+        ctx.set_materialize_grads(False)
         return Z, stats
 
     @staticmethod
     def backward(ctx, dZ, _ds):
+        if dZ is None:  # output unused: every input gradient is zero
+            return (None,) * 4
         cfg = ctx.cfg
         x, weight = ctx.saved_tensors
         dZ = dZ.contiguous()
@@ -833,10 +858,13 @@ class _WMergeFn(torch.autograd.Function):
         if stats is None:
             stats = _empty((0,), a)
         ctx.mark_non_differentiable(stats)
+        ctx.set_materialize_grads(False)
         return y, stats
 
     @staticmethod
     def backward(ctx, dy, _ds):
+        if dy is None:  # output unused: every input gradient is zero
+            return (None,) * 4
         a, b, w = ctx.saved_tensors
         dy = dy.contiguous()
         da = torch.empty_like(a)

@@ -102,10 +102,11 @@ __global__ void __launch_bounds__(256)
 bn_finalize_kernel(const double* __restrict__ part, int R, int C, double count,
                    const float* __restrict__ gamma, const float* __restrict__ beta,
                    float* __restrict__ rmean, float* __restrict__ rvar, float momentum, float eps,
-                   int training, float* __restrict__ st) {
+                   int training, float* __restrict__ st, long long* __restrict__ nbt) {
   __shared__ double red[2][4][64];
   int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
   int c = blockIdx.x * 64 + cl;
+  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;  // num_batches_tracked
   double s1 = 0.0, s2 = 0.0;
   if (training && c < C) {
     for (int r = g; r < R; r += 4) {
@@ -155,11 +156,8 @@ extern "C" int accunet_bn_finalize(const double* part, int R, int C, double coun
   const double* p = part;
   if (training) p = reduce_partials_t<double>(part, R, 2 * C, ws, &rows, s);
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(C, 64)), dim3(256), 0, s, p, rows, C,
-                     count, gamma, beta, rmean, rvar, momentum, eps, training, st);
-  if (training && nbt) {
-    // num_batches_tracked += 1 (int64 buffer)
-    hipLaunchKernelGGL(inc_i64_kernel, dim3(1), dim3(1), 0, s, nbt);
-  }
+                     count, gamma, beta, rmean, rvar, momentum, eps, training, st,
+                     training ? nbt : nullptr);
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 

@@ -105,6 +105,53 @@ ACC_DEV void block_chan_reduce2(const ChanTile& t, T (&a)[V], T (&b)[V], T* out,
   }
 }
 
+// N-quantity version of block_chan_reduce2: per-thread v[i][V] (i < N) reduced over
+// the block's row groups into out[(row*N + i)*C + c], one quantity at a time through
+// one LDS buffer (same deterministic order as block_chan_reduce2).
+template <int V, int N, typename T>
+ACC_DEV void block_chan_reduceN(const ChanTile& t, T (&v)[N][V], T* out, long row, int C) {
+  __shared__ T red[256 * 4];
+  const int tid = threadIdx.x;
+  const bool p2 = (t.TCQ & (t.TCQ - 1)) == 0;
+  const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    if (p2) {
+      for (int off = t.TCQ; off < 64; off <<= 1) {
+#pragma unroll
+        for (int j = 0; j < V; ++j) v[i][j] += __shfl_xor(v[i][j], off);
+      }
+      if (lane < t.TCQ) {
+#pragma unroll
+        for (int j = 0; j < V; ++j) red[(wave * 64 + lane) * V + j] = v[i][j];
+      }
+      __syncthreads();
+      if (tid < t.TCQ && t.cq < t.CQ) {
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          T s = 0;
+          for (int w = 0; w < 4; ++w) s += red[(w * 64 + tid) * V + j];
+          out[(row * N + i) * C + t.c0 + j] = s;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < V; ++j) red[tid * V + j] = v[i][j];
+      __syncthreads();
+      if (t.rg == 0 && t.cq < t.CQ) {
+        const int lt = tid % t.TCQ;
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          T s = 0;
+          for (int g = 0; g < t.RG; ++g) s += red[(g * t.TCQ + lt) * V + j];
+          out[(row * N + i) * C + t.c0 + j] = s;
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // Deterministic block reduction for power-of-two slot counts: thread t contributes
 // v[0..N) to slot t % TCQ (TCQ | 256). Lanes of one wave sharing a slot are summed
 // with xor shuffles (offsets TCQ, 2*TCQ, ..., 32), the per-wave sums go through LDS

@@ -105,28 +105,33 @@ se_reduce_kernel(const float* __restrict__ z, const float* __restrict__ sc,
   block_chan_reduce2<V>(t, a, q, part, blockIdx.x, g.C);
 }
 
-// chunk partials -> per-(b,c) sums: block = 64 channels x 4 chunk groups of one
-// sample; each group sums its chunks in order, the 4 group sums are added in order.
+// chunk partials [B*NCH][N][C] -> per-(b,c) sums out[i][B*C] (i < N): block = 64
+// channels x 4 chunk groups of one sample; each group sums its chunks in order, the 4
+// group sums are added in order.
+template <int N>
 __global__ void __launch_bounds__(256)
-se_part_sum_kernel(const double* __restrict__ part, SeGeom g, double* __restrict__ o1,
-                   double* __restrict__ o2) {
-  __shared__ double r1[4][64], r2[4][64];
+se_part_sum_kernel(const double* __restrict__ part, SeGeom g, double* __restrict__ out) {
+  __shared__ double r[N][4][64];
   const int C = g.C, b = blockIdx.y, t = threadIdx.x;
   const int c = blockIdx.x * 64 + (t & 63), grp = t >> 6;
-  double s1 = 0.0, s2 = 0.0;
+  double s[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) s[i] = 0.0;
   if (c < C) {
     for (int k = grp; k < g.NCH; k += 4) {
-      const double* pr = part + ((long)(b * g.NCH + k) * 2) * C;
-      s1 += pr[c];
-      s2 += pr[C + c];
+      const double* pr = part + ((long)(b * g.NCH + k) * N) * C;
+#pragma unroll
+      for (int i = 0; i < N; ++i) s[i] += pr[(long)i * C + c];
     }
   }
-  r1[grp][t & 63] = s1;
-  r2[grp][t & 63] = s2;
+#pragma unroll
+  for (int i = 0; i < N; ++i) r[i][grp][t & 63] = s[i];
   __syncthreads();
   if (grp == 0 && c < C) {
-    o1[b * C + c] = ((r1[0][t] + r1[1][t]) + r1[2][t]) + r1[3][t];
-    o2[b * C + c] = ((r2[0][t] + r2[1][t]) + r2[2][t]) + r2[3][t];
+    const long BC = (long)g.B * C;
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      out[i * BC + b * C + c] = ((r[i][0][t] + r[i][1][t]) + r[i][2][t]) + r[i][3][t];
   }
 }
 
@@ -173,9 +178,10 @@ __global__ void __launch_bounds__(256)
 se_mid_bn_kernel(SeGeom g, int Cr, const float* __restrict__ gamma,
                  const float* __restrict__ beta, float* __restrict__ rmean,
                  float* __restrict__ rvar, float momentum, float eps, int training,
-                 float* __restrict__ save) {
+                 float* __restrict__ save, long long* __restrict__ nbt) {
   const int B = g.B, C = g.C;
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (nbt && c == 0) *nbt += 1;  // num_batches_tracked (training only; null otherwise)
   if (c >= C) return;
   SeSave sv = se_save_view(save, B, C, Cr);
   const double n = (double)B * g.HW;
@@ -459,6 +465,184 @@ se_bwd_apply_kernel(const float* __restrict__ z, const float* __restrict__ dout,
 }
 
 // ---------------------------------------------------------------------------
+// SE backward fused with the backward of the BatchNorm(+act) prologue that feeds it
+// (the preceding layer's BN: HANCBlock.norm3 :281-283, ResPath.bns[i] :326,
+// Conv2d_batchnorm.batchnorm :183-185, MLFC.bns_mrg :520).
+//
+// With pre = z*sc1 + sh1, a = act(pre), l' = act'(pre), xc = z - mean1, the SE
+// backward gives da = A*g2 + Bc*(a*s - mean) + Cc (per-(b,c) A, Bc, Cc); the
+// prologue BN backward needs g = da*l' reduced per channel:
+//   sum_p g      = A*U1 + Bc*s*U2 + (Cc - Bc*mean)*U3
+//   sum_p g*xc   = A*W1 + Bc*s*W2 + (Cc - Bc*mean)*W3
+// with U1 = sum l'g2, U2 = sum l'a, U3 = sum l', W1 = sum l'g2*xc, W2 = sum l'a*xc,
+// W3 = sum l'*xc: per-(b,c) sums the SE's own first backward pass can collect. So
+// the pair costs 2 read passes of (z, dout) + 1 write of dz, instead of 4 read
+// passes + 2 writes (da is never materialised).
+// ---------------------------------------------------------------------------
+#define SE_PRO_NQ 8  // T1, T2, U1, U2, U3, W1, W2, W3
+
+template <int V>
+__global__ void __launch_bounds__(256)
+se_bwd_reduce_pro_kernel(const float* __restrict__ z, const float* __restrict__ dout,
+                         const float* __restrict__ pst, int act, SeGeom g,
+                         const float* __restrict__ alpha, const float* __restrict__ betap,
+                         double* __restrict__ part) {
+  ChanTile t = chan_tile<V>(g.C);
+  const int C = g.C;
+  const int b = blockIdx.x / g.NCH, ch = blockIdx.x % g.NCH;
+  long r0 = (long)b * g.HW + ch * g.rows_per;
+  long r1 = min((long)b * g.HW + g.HW, r0 + g.rows_per);
+  double acc[SE_PRO_NQ][V];
+#pragma unroll
+  for (int i = 0; i < SE_PRO_NQ; ++i)
+#pragma unroll
+    for (int j = 0; j < V; ++j) acc[i][j] = 0.0;
+  if (t.active) {
+    float s[V], h[V], mu[V], al[V], be[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      mu[j] = pst[BN_MEAN * C + t.c0 + j];
+      s[j] = pst[BN_SCALE * C + t.c0 + j];
+      h[j] = pst[BN_SHIFT * C + t.c0 + j];
+      al[j] = alpha[b * C + t.c0 + j];
+      be[j] = betap[t.c0 + j];
+    }
+    for (long r = r0 + t.rg; r < r1; r += t.RG) {
+      float v[V], d[V];
+      ldv<V>(z + r * C + t.c0, v);
+      ldv<V>(dout + r * C + t.c0, d);
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const float pre = v[j] * s[j] + h[j];
+        const float x = apply_act(pre, act);
+        const float lp = act == ACT_LRELU ? lrelu_d(pre) : 1.f;
+        const float g2 = d[j] * lrelu_d(al[j] * x + be[j]);
+        const double xc = (double)v[j] - mu[j];
+        const double lg = (double)lp * g2, la = (double)lp * x;
+        acc[0][j] += g2;
+        acc[1][j] += (double)g2 * x;
+        acc[2][j] += lg;
+        acc[3][j] += la;
+        acc[4][j] += lp;
+        acc[5][j] += lg * xc;
+        acc[6][j] += la * xc;
+        acc[7][j] += lp * xc;
+      }
+    }
+  }
+  block_chan_reduceN<V, SE_PRO_NQ>(t, acc, part, blockIdx.x, C);
+}
+
+// one thread per channel: the prologue BN's backward coefficients
+//   dz = k1*g + k2*(z - mean1) + k3, dgamma1 = sum g*xhat, dbeta1 = sum g
+// from the per-(b,c) sums (UW[i][B*C], i = 0..5 -> U1 U2 U3 W1 W2 W3) and the SE
+// coefficients A, Bc, Cc.
+__global__ void __launch_bounds__(256)
+se_pro_coef_kernel(SeGeom g, int Cr, const float* __restrict__ save,
+                   const double* __restrict__ UW, const float* __restrict__ coef,
+                   const float* __restrict__ pst, const float* __restrict__ pgamma,
+                   int ptraining, float* __restrict__ dpg, float* __restrict__ dpb,
+                   float* __restrict__ pcoef) {
+  const int B = g.B, C = g.C;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  SeSave sv = se_save_view(const_cast<float*>(save), B, C, Cr);
+  const long BC = (long)B * C;
+  const float* A = coef;
+  const float* Bc = A + BC;
+  const float* Cc = Bc + BC;
+  const double mean = sv.mean[c];
+  double sg = 0.0, sgx = 0.0;
+  for (int b = 0; b < B; ++b) {
+    const long i = (long)b * C + c;
+    const double a = A[i], bb = Bc[i], s = sv.sg[i];
+    const double cst = (double)Cc[i] - bb * mean;
+    sg += a * UW[0 * BC + i] + bb * s * UW[1 * BC + i] + cst * UW[2 * BC + i];
+    sgx += a * UW[3 * BC + i] + bb * s * UW[4 * BC + i] + cst * UW[5 * BC + i];
+  }
+  const float rstd1 = pst[BN_RSTD * C + c];
+  sgx *= rstd1;  // sum g*xhat
+  if (dpg) dpg[c] = (float)sgx;
+  if (dpb) dpb[c] = (float)sg;
+  const double n = (double)B * g.HW;
+  const float ga = pgamma ? pgamma[c] : 1.f;
+  const float k1 = ga * rstd1;
+  float k2 = 0.f, k3 = 0.f;
+  if (ptraining) {  // same coefficients as bn_bwd_finalize_kernel (csrc/bn.hip)
+    const float mg = (float)(sg / n), mgx = (float)(sgx / n);
+    k2 = -k1 * rstd1 * mgx;
+    k3 = -k1 * mg;
+  }
+  pcoef[c] = k1;
+  pcoef[C + c] = k2;
+  pcoef[2 * C + c] = k3;
+}
+
+template <int V>
+__global__ void __launch_bounds__(256)
+se_bwd_apply_pro_kernel(const float* __restrict__ z, const float* __restrict__ dout,
+                        const float* __restrict__ pst, int act, SeGeom g,
+                        const float* __restrict__ alpha, const float* __restrict__ betap,
+                        const float* __restrict__ sgate, const float* __restrict__ mean,
+                        const float* __restrict__ coef, const float* __restrict__ pcoef,
+                        float* __restrict__ dz) {
+  ChanTile t = chan_tile<V>(g.C);
+  if (!t.active) return;
+  const int C = g.C;
+  const int b = blockIdx.x / g.NCH, ch = blockIdx.x % g.NCH;
+  long r0 = (long)b * g.HW + ch * g.rows_per;
+  long r1 = min((long)b * g.HW + g.HW, r0 + g.rows_per);
+  const int BC = g.B * C;
+  float s[V], h[V], mu1[V], al[V], be[V], A[V], Bc[V], Cc[V], sgv[V], mu[V], k1[V], k2[V],
+      k3[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    const int c = t.c0 + j, i = b * C + c;
+    sgv[j] = sgate[i];
+    mu[j] = mean[c];
+    mu1[j] = pst[BN_MEAN * C + c];
+    s[j] = pst[BN_SCALE * C + c];
+    h[j] = pst[BN_SHIFT * C + c];
+    al[j] = alpha[i];
+    be[j] = betap[c];
+    A[j] = coef[i];
+    Bc[j] = coef[BC + i];
+    Cc[j] = coef[2 * BC + i];
+    k1[j] = pcoef[c];
+    k2[j] = pcoef[C + c];
+    k3[j] = pcoef[2 * C + c];
+  }
+  constexpr int U = 2;  // rows per iteration with all loads issued first
+  for (long rb = r0 + t.rg; rb < r1; rb += U * t.RG) {
+    float v[U][V], d[U][V];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long r = rb + (long)u * t.RG;
+      if (r < r1) {
+        ldv<V>(z + r * C + t.c0, v[u]);
+        ldv<V>(dout + r * C + t.c0, d[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long r = rb + (long)u * t.RG;
+      if (r < r1) {
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          const float pre = v[u][j] * s[j] + h[j];
+          const float x = apply_act(pre, act);
+          const float g2 = d[u][j] * lrelu_d(al[j] * x + be[j]);
+          float da = A[j] * g2 + Bc[j] * (x * sgv[j] - mu[j]) + Cc[j];
+          if (act == ACT_LRELU) da *= lrelu_d(pre);
+          d[u][j] = k1[j] * da + k2[j] * (v[u][j] - mu1[j]) + k3[j];
+        }
+        stv<V>(dz + r * C + t.c0, d[u]);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------
 extern "C" size_t accunet_se_save_elems(int B, int C, int Cr) { return se_save_floats(B, C, Cr); }
@@ -469,15 +653,19 @@ extern "C" int accunet_se_stats_rows(int B, int HW, int C) {
   return B * g.NCH;
 }
 
-// workspace (floats): fp64 partials [B*NCH][2][C] | fp64 scratch | fp32 coef [3][B*C]
-static size_t se_part_floats(const SeGeom& g) { return (size_t)g.B * g.NCH * 2 * g.C * 2; }
+// workspace (floats): fp64 partials [B*NCH][SE_PRO_NQ][C] | fp64 scratch | fp32 coef [3][B*C]
+// | fp32 prologue coefficients [3][C]
+static size_t se_part_floats(const SeGeom& g) {
+  return (size_t)g.B * g.NCH * SE_PRO_NQ * g.C * 2;
+}
+// fp64 scratch: G[C] GY[C] du[B*C] dh[B*Cr] T1 T2 U1 U2 U3 W1 W2 W3 [B*C each]
 static size_t se_scratch_floats(int B, int C, int Cr) {
-  return ((size_t)B * C * 3 + 2 * (size_t)C + (size_t)B * Cr) * 2;
+  return ((size_t)B * C * (1 + SE_PRO_NQ) + 2 * (size_t)C + (size_t)B * Cr) * 2;
 }
 
 extern "C" size_t accunet_se_ws_elems(int B, int HW, int C, int Cr) {
   SeGeom g = se_geom(B, HW, C);
-  return se_part_floats(g) + se_scratch_floats(B, C, Cr) + (size_t)B * C * 3 + 4;
+  return se_part_floats(g) + se_scratch_floats(B, C, Cr) + (size_t)B * C * 3 + 3 * (size_t)C + 4;
 }
 
 extern "C" int accunet_se_fwd(const float* z, const float* sc, const float* sh, int act, int B,
@@ -497,16 +685,13 @@ extern "C" int accunet_se_fwd(const float* z, const float* sc, const float* sh, 
     hipLaunchKernelGGL(se_reduce_kernel<4>, grid, dim3(256), 0, s, z, sc, sh, act, g, part);
   else
     hipLaunchKernelGGL(se_reduce_kernel<1>, grid, dim3(256), 0, s, z, sc, sh, act, g, part);
-  {
-    double* S = reinterpret_cast<double*>(save);  // SeSave: S[B*C] then Q[B*C]
-    hipLaunchKernelGGL(se_part_sum_kernel, dim3(ceil_div(C, 64), B), dim3(256), 0, s, part, g, S,
-                       S + (size_t)B * C);
-  }
+  // SeSave: S[B*C] then Q[B*C]
+  hipLaunchKernelGGL(se_part_sum_kernel<2>, dim3(ceil_div(C, 64), B), dim3(256), 0, s, part, g,
+                     reinterpret_cast<double*>(save));
   hipLaunchKernelGGL(se_mid_gate_kernel, dim3(B), dim3(256), (C + Cr) * sizeof(float), s, g, Cr, w1,
                      b1, w2, b2, save);
   hipLaunchKernelGGL(se_mid_bn_kernel, dim3(ceil_div(C, 256)), dim3(256), 0, s, g, Cr, gamma, beta,
-                     rmean, rvar, momentum, eps, training, save);
-  if (training && nbt) hipLaunchKernelGGL(inc_i64_kernel, dim3(1), dim3(1), 0, s, nbt);
+                     rmean, rvar, momentum, eps, training, save, training ? nbt : nullptr);
   const float* alpha = save + se_alpha_offset(B, C, Cr);
   const float* betap = alpha + (size_t)B * C;
   if (V == 4)
@@ -516,6 +701,29 @@ extern "C" int accunet_se_fwd(const float* z, const float* sc, const float* sh, 
     hipLaunchKernelGGL(se_apply_kernel<1>, grid, dim3(256), 0, s, z, sc, sh, act, g, alpha, betap,
                        out, ostats);
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+}
+
+// shared by accunet_se_bwd / accunet_se_bwd_pro: the per-(b,c) sums in scratch (from
+// part) -> BN / gate / fc backward, coef (A, Bc, Cc), fc parameter gradients
+static void se_bwd_mid(const SeGeom& g, int Cr, const double* part, int nq, const float* w1,
+                       const float* w2, const float* gamma, int training, float* sv,
+                       double* scratch, float* coef, float* dw1, float* db1, float* dw2,
+                       float* db2, float* dgamma, float* dbeta, hipStream_t s) {
+  const int B = g.B, C = g.C;
+  double* T1 = scratch + 2 * (size_t)C + (size_t)B * C + (size_t)B * Cr;
+  if (nq == 2)
+    hipLaunchKernelGGL(se_part_sum_kernel<2>, dim3(ceil_div(C, 64), B), dim3(256), 0, s, part, g,
+                       T1);
+  else
+    hipLaunchKernelGGL(se_part_sum_kernel<SE_PRO_NQ>, dim3(ceil_div(C, 64), B), dim3(256), 0, s,
+                       part, g, T1);
+  hipLaunchKernelGGL(se_bwd_chan_kernel, dim3(ceil_div(C, 256)), dim3(256), 0, s, g, Cr, gamma,
+                     training, sv, dgamma, dbeta, scratch);
+  hipLaunchKernelGGL(se_bwd_sample_kernel, dim3(B), dim3(256), (Cr > 0 ? Cr : 1) * sizeof(double),
+                     s, g, Cr, w1, w2, gamma, training, sv, scratch, coef);
+  long nparam = 2L * C * Cr + C + Cr;
+  hipLaunchKernelGGL(se_bwd_param_kernel, dim3(ceil_div(nparam, 256)), dim3(256), 0, s, g, Cr, sv,
+                     scratch, dw1, db1, dw2, db2);
 }
 
 extern "C" int accunet_se_bwd(const float* z, const float* dout, const float* sc, const float* sh,
@@ -544,23 +752,56 @@ extern "C" int accunet_se_bwd(const float* z, const float* dout, const float* sc
     hipLaunchKernelGGL(se_bwd_reduce_kernel<1>, grid, dim3(256), 0, s, z, dout, sc, sh, act, g,
                        alpha, betap, part);
   float* sv = const_cast<float*>(save);
-  {
-    double* T1 = scratch + 2 * (size_t)C + (size_t)B * C + (size_t)B * Cr;
-    hipLaunchKernelGGL(se_part_sum_kernel, dim3(ceil_div(C, 64), B), dim3(256), 0, s, part, g, T1,
-                       T1 + (size_t)B * C);
-  }
-  hipLaunchKernelGGL(se_bwd_chan_kernel, dim3(ceil_div(C, 256)), dim3(256), 0, s, g, Cr, gamma,
-                     training, sv, dgamma, dbeta, scratch);
-  hipLaunchKernelGGL(se_bwd_sample_kernel, dim3(B), dim3(256), (Cr > 0 ? Cr : 1) * sizeof(double),
-                     s, g, Cr, w1, w2, gamma, training, sv, scratch, coef);
-  long nparam = 2L * C * Cr + C + Cr;
-  hipLaunchKernelGGL(se_bwd_param_kernel, dim3(ceil_div(nparam, 256)), dim3(256), 0, s, g, Cr, sv,
-                     scratch, dw1, db1, dw2, db2);
+  se_bwd_mid(g, Cr, part, 2, w1, w2, gamma, training, sv, scratch, coef, dw1, db1, dw2, db2,
+             dgamma, dbeta, s);
   if (V == 4)
     hipLaunchKernelGGL(se_bwd_apply_kernel<4>, grid, dim3(256), 0, s, z, dout, sc, sh, act, g,
                        alpha, betap, sgate, mean, coef, da);
   else
     hipLaunchKernelGGL(se_bwd_apply_kernel<1>, grid, dim3(256), 0, s, z, dout, sc, sh, act, g,
                        alpha, betap, sgate, mean, coef, da);
+  return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+}
+
+extern "C" int accunet_se_bwd_pro(const float* z, const float* dout, const float* pst, int act,
+                                  const float* pgamma, int ptraining, int B, int HW, int C,
+                                  int Cr, const float* w1, const float* w2, const float* gamma,
+                                  int training, const float* save, float* dz, float* dpgamma,
+                                  float* dpbeta, float* dw1, float* db1, float* dw2, float* db2,
+                                  float* dgamma, float* dbeta, float* ws, size_t ws_elems,
+                                  void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (ws_elems < accunet_se_ws_elems(B, HW, C, Cr)) return ACC_EBADARG;
+  if (((uintptr_t)ws & 7) || ((uintptr_t)save & 7)) return ACC_EBADARG;
+  if (!pst || !dz) return ACC_EBADARG;
+  SeGeom g = se_geom(B, HW, C);
+  int V = (C % 4 == 0) ? 4 : 1;
+  dim3 grid(B * g.NCH, ceil_div(C / V, 64));
+  double* part = reinterpret_cast<double*>(ws);
+  double* scratch = reinterpret_cast<double*>(ws + se_part_floats(g));
+  float* coef = ws + se_part_floats(g) + se_scratch_floats(B, C, Cr);
+  float* pcoef = coef + (size_t)B * C * 3;
+  const float* alpha = save + se_alpha_offset(B, C, Cr);
+  const float* betap = alpha + (size_t)B * C;
+  const float* sgate = save + (size_t)B * C * 4 + (size_t)B * Cr;
+  const float* mean = sgate + (size_t)B * C;
+  if (V == 4)
+    hipLaunchKernelGGL(se_bwd_reduce_pro_kernel<4>, grid, dim3(256), 0, s, z, dout, pst, act, g,
+                       alpha, betap, part);
+  else
+    hipLaunchKernelGGL(se_bwd_reduce_pro_kernel<1>, grid, dim3(256), 0, s, z, dout, pst, act, g,
+                       alpha, betap, part);
+  float* sv = const_cast<float*>(save);
+  se_bwd_mid(g, Cr, part, SE_PRO_NQ, w1, w2, gamma, training, sv, scratch, coef, dw1, db1, dw2,
+             db2, dgamma, dbeta, s);
+  const double* UW = scratch + 2 * (size_t)C + (size_t)B * C + (size_t)B * Cr + 2 * (size_t)B * C;
+  hipLaunchKernelGGL(se_pro_coef_kernel, dim3(ceil_div(C, 256)), dim3(256), 0, s, g, Cr, save, UW,
+                     coef, pst, pgamma, ptraining, dpgamma, dpbeta, pcoef);
+  if (V == 4)
+    hipLaunchKernelGGL(se_bwd_apply_pro_kernel<4>, grid, dim3(256), 0, s, z, dout, pst, act, g,
+                       alpha, betap, sgate, mean, coef, pcoef, dz);
+  else
+    hipLaunchKernelGGL(se_bwd_apply_pro_kernel<1>, grid, dim3(256), 0, s, z, dout, pst, act, g,
+                       alpha, betap, sgate, mean, coef, pcoef, dz);
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }

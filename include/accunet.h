@@ -184,6 +184,18 @@ int accunet_se_bwd(const float* z, const float* dout, const float* sc, const flo
                    const float* gamma, int training, const float* save, float* da, float* dw1,
                    float* db1, float* dw2, float* db2, float* dgamma, float* dbeta, float* ws,
                    size_t ws_elems, void* stream);
+/* accunet_se_bwd fused with the backward of the BatchNorm(+act) prologue that feeds
+ * the SE (HANCBlock.norm3 :281-283, ResPath.bns :326, Conv2d_batchnorm.batchnorm
+ * :183-185, MLFC.bns_mrg :520): pst = that BatchNorm's [4][C] (mean, rstd, scale,
+ * shift) block, pgamma its weight, ptraining its mode. Returns dz (gradient w.r.t.
+ * the pre-BN input z) and the prologue's dgamma/dbeta directly: 2 read passes over
+ * (z, dout) and one write, da is never materialised. */
+int accunet_se_bwd_pro(const float* z, const float* dout, const float* pst, int act,
+                       const float* pgamma, int ptraining, int B, int HW, int C, int Cr,
+                       const float* w1, const float* w2, const float* gamma, int training,
+                       const float* save, float* dz, float* dpgamma, float* dpbeta, float* dw1,
+                       float* db1, float* dw2, float* db2, float* dgamma, float* dbeta, float* ws,
+                       size_t ws_elems, void* stream);
 
 /* ------------------------------------------------------------------------- *
  * Head: out 1x1 conv n_filts -> 1 (+ Sigmoid when sigm) (ACC_UNet.py:594-599,653-659)
