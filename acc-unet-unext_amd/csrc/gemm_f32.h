@@ -128,6 +128,22 @@ gemm_f32_kernel(const GemmParams p) {
   }
 
   float4 ra[NPA], rb[NPB];
+  // BM_NN prologue coefficients: thread i-slot always loads the same column quad
+  float4 bsc[NPB], bsh[NPB];
+  if (BMODE == BM_NN && PRO_B != PRO_NONE) {
+#pragma unroll
+    for (int i = 0; i < NPB; ++i) {
+      const int n = n0 + 4 * ((tid + i * GEMM_THREADS) % (BN / 4));
+      float e[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        e[j] = (n + j < N) ? p.b_scale[n + j] : 1.f;
+        e[4 + j] = (n + j < N) ? p.b_shift[n + j] : 0.f;
+      }
+      bsc[i] = make_float4(e[0], e[1], e[2], e[3]);
+      bsh[i] = make_float4(e[4], e[5], e[6], e[7]);
+    }
+  }
 
   auto load_tiles = [&](int k0) {
     // ------------------------------ A ---------------------------------------
@@ -144,16 +160,24 @@ gemm_f32_kernel(const GemmParams p) {
         if ((idx < NA4) && (g < M)) {
           if (VA) {
             if (k < K) {
-              int s = 0;
-#pragma unroll
-              for (int j = 1; j < 4; ++j)
-                if (j < p.nsrc && k >= p.kbeg[j]) s = j;
-              v = ld4(p.A[s] + (long)g * p.lda[s] + (k - p.kbeg[s]));
-              if (PRO_A != PRO_NONE && s == 0) {
-                v.x = pro_apply<PRO_A>(v.x, p.a_scale[k + 0], p.a_shift[k + 0]);
-                v.y = pro_apply<PRO_A>(v.y, p.a_scale[k + 1], p.a_shift[k + 1]);
-                v.z = pro_apply<PRO_A>(v.z, p.a_scale[k + 2], p.a_shift[k + 2]);
-                v.w = pro_apply<PRO_A>(v.w, p.a_scale[k + 3], p.a_shift[k + 3]);
+              // source of this quad (a float4 never straddles a seam): explicit selects
+              // over the kernel arguments keep base / ld / kbeg in SGPRs -> v_cndmask,
+              // instead of a lane-indexed p.A[s] that hipcc turns into dependent
+              // global loads of the argument block inside the k-loop
+              const float* base = p.A[0];
+              int ld = p.lda[0], kb = 0;
+              if (p.nsrc > 1) {
+                if (k >= p.kbeg[1]) { base = p.A[1]; ld = p.lda[1]; kb = p.kbeg[1]; }
+                if (p.nsrc > 2 && k >= p.kbeg[2]) { base = p.A[2]; ld = p.lda[2]; kb = p.kbeg[2]; }
+                if (p.nsrc > 3 && k >= p.kbeg[3]) { base = p.A[3]; ld = p.lda[3]; kb = p.kbeg[3]; }
+              }
+              v = ld4(base + (long)g * ld + (k - kb));
+              if (PRO_A != PRO_NONE && kb == 0) {  // the pending BatchNorm sits on source 0
+                const float4 sc = ld4(p.a_scale + k), sh = ld4(p.a_shift + k);
+                v.x = pro_apply<PRO_A>(v.x, sc.x, sh.x);
+                v.y = pro_apply<PRO_A>(v.y, sc.y, sh.y);
+                v.z = pro_apply<PRO_A>(v.z, sc.z, sh.z);
+                v.w = pro_apply<PRO_A>(v.w, sc.w, sh.w);
               }
             }
           } else {
@@ -282,11 +306,11 @@ gemm_f32_kernel(const GemmParams p) {
             if (n + 2 < N) v.z = ptr[2];
             if (n + 3 < N) v.w = ptr[3];
           }
-          if (PRO_B != PRO_NONE) {
-            if (n + 0 < N) v.x = pro_apply<PRO_B>(v.x, p.b_scale[n + 0], p.b_shift[n + 0]);
-            if (n + 1 < N) v.y = pro_apply<PRO_B>(v.y, p.b_scale[n + 1], p.b_shift[n + 1]);
-            if (n + 2 < N) v.z = pro_apply<PRO_B>(v.z, p.b_scale[n + 2], p.b_shift[n + 2]);
-            if (n + 3 < N) v.w = pro_apply<PRO_B>(v.w, p.b_scale[n + 3], p.b_shift[n + 3]);
+          if (PRO_B != PRO_NONE) {  // per-column coefficients, loaded once (bsc/bsh)
+            if (n + 0 < N) v.x = pro_apply<PRO_B>(v.x, bsc[i].x, bsh[i].x);
+            if (n + 1 < N) v.y = pro_apply<PRO_B>(v.y, bsc[i].y, bsh[i].y);
+            if (n + 2 < N) v.z = pro_apply<PRO_B>(v.z, bsc[i].z, bsh[i].z);
+            if (n + 3 < N) v.w = pro_apply<PRO_B>(v.w, bsc[i].w, bsh[i].w);
           }
         }
         rb[i] = v;
@@ -402,18 +426,26 @@ gemm_f32_kernel(const GemmParams p) {
       if (kt + 1 < nkt) load_tiles(kstart + (kt + 1) * BK);
       const float* as = As + buf * BK * SA;
       const float* bs = Bs + buf * BK * SB;
+      // fragments for step kk+1 are read from LDS before the MFMAs of step kk issue
+      float a[2][TM], b[2][TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[0][i] = as[lh * SA + am_off + i * 32];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b[0][j] = bs[lh * SB + bn_off + j * 32];
 #pragma unroll
       for (int kk = 0; kk < BK / 2; ++kk) {
-        float a[TM], b[TN];
+        const int cur = kk & 1;
+        if (kk + 1 < BK / 2) {
 #pragma unroll
-        for (int i = 0; i < TM; ++i) a[i] = as[(2 * kk + lh) * SA + am_off + i * 32];
+          for (int i = 0; i < TM; ++i) a[cur ^ 1][i] = as[(2 * kk + 2 + lh) * SA + am_off + i * 32];
 #pragma unroll
-        for (int j = 0; j < TN; ++j) b[j] = bs[(2 * kk + lh) * SB + bn_off + j * 32];
+          for (int j = 0; j < TN; ++j) b[cur ^ 1][j] = bs[(2 * kk + 2 + lh) * SB + bn_off + j * 32];
+        }
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[cur][i], b[cur][j], acc[i][j], 0, 0, 0);
       }
       if (kt + 1 < nkt) store_tiles(buf ^ 1);
       __syncthreads();
