@@ -463,6 +463,9 @@ gemm_f32_kernel(const GemmParams p) {
   constexpr int RPP = GEMM_THREADS / CQN;   // tile rows per sweep
   constexpr int PR = WM * 32;               // tile rows staged per pass
   constexpr int SC = BN + 4;                // LDS row stride (floats)
+  constexpr int NR = PR / RPP;              // rows per thread per pass
+  constexpr int EC = NR < 2 ? NR : 2;       // rows per load chunk
+  static_assert(PR % RPP == 0, "pass rows must split evenly over the sweeps");
   static_assert(PR * SC <= 2 * BK * SA + 2 * BK * SB, "epilogue staging exceeds the LDS tile");
   static_assert(GEMM_THREADS % CQN == 0, "BN/4 must divide the block");
   const bool split = gridDim.z > 1;
@@ -487,99 +490,153 @@ gemm_f32_kernel(const GemmParams p) {
         smem[(wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * SC + wn * TN * 32 + j * 32 + l31] =
             acc[i][j][r];
     __syncthreads();
-    for (int rr = rr0; rr < PR; rr += RPP) {
-      const int m = m0 + (rr >> 5) * TM * 32 + i * 32 + (rr & 31);
-      if (m >= M || nq >= N) continue;
-      float4 a4 = *reinterpret_cast<const float4*>(smem + rr * SC + 4 * cq);
-      float v[4] = {a4.x, a4.y, a4.z, a4.w};
-      if (!split) {
+    // rows of this pass are handled EC at a time: first every global load of the
+    // chunk (nearest-up addends / pyramid terms) is issued, then the rows are combined
+    // and stored, so a chunk costs one L2 round trip instead of one per row (the
+    // compiler cannot hoist those loads above the previous row's C stores itself)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] += bq[e];
-        if (need_pix) {
-          uint32_t q = fdiv((uint32_t)m, p.fW);
-          const int w = m - (int)q * p.W;
-          const uint32_t b = fdiv(q, p.fH);
-          const int h = (int)(q - b * p.H);
-          for (int u = 0; u < p.nup; ++u) {
-            const int lg = p.uplog[u];
-            const long uo = (((long)b * (p.H >> lg) + (h >> lg)) * (p.W >> lg) + (w >> lg)) *
-                                p.upld[u] + nq;
-            if (evec) {
-              float4 t4 = ld4(p.up[u] + uo);
-              v[0] += t4.x; v[1] += t4.y; v[2] += t4.z; v[3] += t4.w;
-            } else {
+    for (int r0 = 0; r0 < NR; r0 += EC) {
+      int mrow[EC];
+      bool ok[EC];
+      float v[EC][4];
 #pragma unroll
-              for (int e = 0; e < 4; ++e)
-                if (nq + e < N) v[e] += p.up[u][uo + e];
-            }
-          }
-          if (p.pd2) {
-            // same accumulation order as the standalone pyramid backward:
-            // g = (avg2/4 [+ max2]) + avg4/16 [+ max4]; C += g
+      for (int c = 0; c < EC; ++c) {
+        const int rr = rr0 + (r0 + c) * RPP;
+        mrow[c] = m0 + (rr >> 5) * TM * 32 + i * 32 + (rr & 31);
+        ok[c] = (r0 + c < NR) && mrow[c] < M && nq < N;
+        const float4 a4 = *reinterpret_cast<const float4*>(smem + (ok[c] ? rr : 0) * SC + 4 * cq);
+        v[c][0] = a4.x; v[c][1] = a4.y; v[c][2] = a4.z; v[c][3] = a4.w;
+        if (!split) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[c][e] += bq[e];
+        }
+      }
+      if (need_pix && p.pd2) {
+        // fused HANCLayer pyramid backward: same accumulation order as the standalone
+        // pyramid backward, g = (avg2/4 [+ max2]) + avg4/16 [+ max4]; C += g
+        float4 av2[EC], mx2[EC], av4[EC], mx4[EC];
+        unsigned k2[EC], k4[EC];
+        int pos2[EC], pos4[EC];
+#pragma unroll
+        for (int c = 0; c < EC; ++c) {
+          av2[c] = mx2[c] = av4[c] = mx4[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+          k2[c] = 0u;
+          k4[c] = 0xffffffffu;
+          pos2[c] = pos4[c] = 0;
+          if (ok[c]) {
+            const int m = mrow[c];
+            const uint32_t q = fdiv((uint32_t)m, p.fW);
+            const int w = m - (int)q * p.W;
+            const uint32_t b = fdiv(q, p.fH);
+            const int h = (int)(q - b * p.H);
             const long q2 = ((long)b * (p.H >> 1) + (h >> 1)) * (p.W >> 1) + (w >> 1);
             const long q4 = ((long)b * (p.H >> 2) + (h >> 2)) * (p.W >> 2) + (w >> 2);
-            const int pos2 = (h & 1) * 2 + (w & 1), pos4 = (h & 3) * 4 + (w & 3);
-            float av2[4], mx2[4], av4[4] = {0.f, 0.f, 0.f, 0.f}, mx4[4] = {0.f, 0.f, 0.f, 0.f};
-            unsigned c2[4], c4[4] = {255u, 255u, 255u, 255u};
+            pos2[c] = (h & 1) * 2 + (w & 1);
+            pos4[c] = (h & 3) * 4 + (w & 3);
             if (evec) {  // 16-byte rows of dP, 4-byte rows of codes
-              float4 t = ld4(p.pd2 + q2 * 2 * N + nq);
-              av2[0] = t.x; av2[1] = t.y; av2[2] = t.z; av2[3] = t.w;
-              t = ld4(p.pd2 + q2 * 2 * N + N + nq);
-              mx2[0] = t.x; mx2[1] = t.y; mx2[2] = t.z; mx2[3] = t.w;
-              unsigned k2 = *reinterpret_cast<const unsigned*>(p.mk2 + q2 * N + nq);
-#pragma unroll
-              for (int e = 0; e < 4; ++e) c2[e] = (k2 >> (8 * e)) & 255u;
+              av2[c] = ld4(p.pd2 + q2 * 2 * N + nq);
+              mx2[c] = ld4(p.pd2 + q2 * 2 * N + N + nq);
+              k2[c] = *reinterpret_cast<const unsigned*>(p.mk2 + q2 * N + nq);
               if (p.pd4) {
-                t = ld4(p.pd4 + q4 * 2 * N + nq);
-                av4[0] = t.x; av4[1] = t.y; av4[2] = t.z; av4[3] = t.w;
-                t = ld4(p.pd4 + q4 * 2 * N + N + nq);
-                mx4[0] = t.x; mx4[1] = t.y; mx4[2] = t.z; mx4[3] = t.w;
-                unsigned k4 = *reinterpret_cast<const unsigned*>(p.mk4 + q4 * N + nq);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) c4[e] = (k4 >> (8 * e)) & 255u;
+                av4[c] = ld4(p.pd4 + q4 * 2 * N + nq);
+                mx4[c] = ld4(p.pd4 + q4 * 2 * N + N + nq);
+                k4[c] = *reinterpret_cast<const unsigned*>(p.mk4 + q4 * N + nq);
               }
             } else {
+              float t[4][4];
+              unsigned u2 = 0u, u4 = 0u;
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
                 const int n = nq + e < N ? nq + e : N - 1;
-                av2[e] = p.pd2[q2 * 2 * N + n];
-                mx2[e] = p.pd2[q2 * 2 * N + N + n];
-                c2[e] = p.mk2[q2 * N + n];
+                t[0][e] = p.pd2[q2 * 2 * N + n];
+                t[1][e] = p.pd2[q2 * 2 * N + N + n];
+                u2 |= (unsigned)p.mk2[q2 * N + n] << (8 * e);
+                t[2][e] = t[3][e] = 0.f;
                 if (p.pd4) {
-                  av4[e] = p.pd4[q4 * 2 * N + n];
-                  mx4[e] = p.pd4[q4 * 2 * N + N + n];
-                  c4[e] = p.mk4[q4 * N + n];
+                  t[2][e] = p.pd4[q4 * 2 * N + n];
+                  t[3][e] = p.pd4[q4 * 2 * N + N + n];
+                  u4 |= (unsigned)p.mk4[q4 * N + n] << (8 * e);
                 }
               }
-            }
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              float g = av2[e] * 0.25f;
-              if (c2[e] == (unsigned)pos2) g += mx2[e];
-              if (p.pd4) {
-                g += av4[e] * (1.f / 16.f);
-                if (c4[e] == (unsigned)pos4) g += mx4[e];
-              }
-              v[e] += g;
+              av2[c] = make_float4(t[0][0], t[0][1], t[0][2], t[0][3]);
+              mx2[c] = make_float4(t[1][0], t[1][1], t[1][2], t[1][3]);
+              av4[c] = make_float4(t[2][0], t[2][1], t[2][2], t[2][3]);
+              mx4[c] = make_float4(t[3][0], t[3][1], t[3][2], t[3][3]);
+              k2[c] = u2;
+              k4[c] = p.pd4 ? u4 : 0xffffffffu;
             }
           }
         }
-        if (p.stats) {
+#pragma unroll
+        for (int c = 0; c < EC; ++c) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float g = f4get(av2[c], e) * 0.25f;
+            if (((k2[c] >> (8 * e)) & 255u) == (unsigned)pos2[c]) g += f4get(mx2[c], e);
+            if (p.pd4) {
+              g += f4get(av4[c], e) * (1.f / 16.f);
+              if (((k4[c] >> (8 * e)) & 255u) == (unsigned)pos4[c]) g += f4get(mx4[c], e);
+            }
+            v[c][e] += g;
+          }
+        }
+      } else if (need_pix) {
+        // nearest-upsampled addends (HANCLayer coarse branches, MLFC coarse sources),
+        // added in source order
+        float4 up4[EC][3];
+#pragma unroll
+        for (int c = 0; c < EC; ++c) {
+          const int m = mrow[c];
+          const uint32_t q = fdiv((uint32_t)m, p.fW);
+          const int w = m - (int)q * p.W;
+          const uint32_t b = fdiv(q, p.fH);
+          const int h = (int)(q - b * p.H);
+#pragma unroll
+          for (int u = 0; u < 3; ++u) {
+            up4[c][u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (u < p.nup && ok[c]) {
+              const int lg = p.uplog[u];
+              const long uo = (((long)b * (p.H >> lg) + (h >> lg)) * (p.W >> lg) + (w >> lg)) *
+                                  p.upld[u] + nq;
+              if (evec) {
+                up4[c][u] = ld4(p.up[u] + uo);
+              } else {
+                float t[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) t[e] = (nq + e < N) ? p.up[u][uo + e] : 0.f;
+                up4[c][u] = make_float4(t[0], t[1], t[2], t[3]);
+              }
+            }
+          }
+        }
+#pragma unroll
+        for (int c = 0; c < EC; ++c)
+#pragma unroll
+          for (int u = 0; u < 3; ++u)
+            if (u < p.nup) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[c][e] += f4get(up4[c][u], e);
+            }
+      }
+#pragma unroll
+      for (int c = 0; c < EC; ++c) {
+        if (!ok[c]) continue;
+        if (!split && p.stats) {
 #pragma unroll
           for (int e = 0; e < 4; ++e)
             if (nq + e < N) {
-              s1[e] += v[e];
-              s2[e] += (double)v[e] * v[e];
+              s1[e] += v[c][e];
+              s2[e] += (double)v[c][e] * v[c][e];
             }
         }
-      }
-      float* dst = Cout + (size_t)m * (split ? N : p.ldc) + nq;
-      if (evec) {
-        st4(dst, make_float4(v[0], v[1], v[2], v[3]));
-      } else {
+        float* dst = Cout + (size_t)mrow[c] * (split ? N : p.ldc) + nq;
+        if (evec) {
+          st4(dst, make_float4(v[c][0], v[c][1], v[c][2], v[c][3]));
+        } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (nq + e < N) dst[e] = v[e];
+          for (int e = 0; e < 4; ++e)
+            if (nq + e < N) dst[e] = v[c][e];
+        }
       }
     }
   }

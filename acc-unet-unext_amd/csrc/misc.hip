@@ -14,9 +14,33 @@
 // ---------------------------------------------------------------------------
 // head
 // ---------------------------------------------------------------------------
+// Forward: TQ = C/4 lanes per pixel (a power of two <= 64) each load one 16-byte
+// channel quad (coalesced rows), dot with w, xor-shuffle sum over the TQ lanes.
 __global__ void __launch_bounds__(256)
 head_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ b,
-                int sigm, float* __restrict__ y, long P, int C) {
+                int sigm, float* __restrict__ y, long P, int C, int TQ) {
+  const int q = threadIdx.x % TQ;
+  const int ppb = 256 / TQ;  // pixels per block sweep
+  const float4 wq = ld4(w + 4 * q);
+  const float bias = b[0];
+  for (long p = (long)blockIdx.x * ppb + threadIdx.x / TQ; p < P; p += (long)gridDim.x * ppb) {
+    const float4 xv = ld4(x + p * C + 4 * q);
+    float acc = xv.x * wq.x;
+    acc = fmaf(xv.y, wq.y, acc);
+    acc = fmaf(xv.z, wq.z, acc);
+    acc = fmaf(xv.w, wq.w, acc);
+    for (int off = 1; off < TQ; off <<= 1) acc += __shfl_xor(acc, off);
+    if (q == 0) {
+      acc += bias;
+      y[p] = sigm ? 1.f / (1.f + expf(-acc)) : acc;
+    }
+  }
+}
+
+// generic fallback (C % 4 != 0 or C/4 not a power of two): one thread per pixel
+__global__ void __launch_bounds__(256)
+head_fwd_scalar_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                       const float* __restrict__ b, int sigm, float* __restrict__ y, long P, int C) {
   for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < P; p += (long)gridDim.x * blockDim.x) {
     const float* xr = x + p * C;
     float acc = 0.f;
@@ -26,11 +50,41 @@ head_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w, const 
   }
 }
 
-// dx[p,c] = g[p]*w[c]; partial dw/db per block: part[blk][C+1]
+// Backward (C % 4 == 0, C/4 a power of two <= 64): dx[p,c] = g[p]*w[c],
+// g = dy (* y(1-y) for the Sigmoid); per-block partials part[blk][2][C] of
+// (sum g*x[c], sum g) through the channel-tiled deterministic block reduction.
 __global__ void __launch_bounds__(256)
 head_bwd_kernel(const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ y,
                 const float* __restrict__ dy, int sigm, float* __restrict__ dx, long P, int C,
                 float* __restrict__ part) {
+  ChanTile t = chan_tile<4>(C);
+  float a[4] = {0.f, 0.f, 0.f, 0.f}, gs[4] = {0.f, 0.f, 0.f, 0.f};
+  long per = (P + gridDim.x - 1) / gridDim.x;
+  long p0 = blockIdx.x * per, p1 = min(P, p0 + per);
+  if (t.active) {
+    const float4 wq = ld4(w + t.c0);
+    for (long p = p0 + t.rg; p < p1; p += t.RG) {
+      float g = dy[p];
+      if (sigm) {
+        const float yy = y[p];
+        g *= yy * (1.f - yy);
+      }
+      const float4 xv = ld4(x + p * C + t.c0);
+      st4(dx + p * C + t.c0, make_float4(g * wq.x, g * wq.y, g * wq.z, g * wq.w));
+      a[0] = fmaf(g, xv.x, a[0]);
+      a[1] = fmaf(g, xv.y, a[1]);
+      a[2] = fmaf(g, xv.z, a[2]);
+      a[3] = fmaf(g, xv.w, a[3]);
+      gs[0] += g;
+    }
+  }
+  block_chan_reduce2<4>(t, a, gs, part, blockIdx.x, C);
+}
+
+__global__ void __launch_bounds__(256)
+head_bwd_scalar_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                       const float* __restrict__ y, const float* __restrict__ dy, int sigm,
+                       float* __restrict__ dx, long P, int C, float* __restrict__ part) {
   __shared__ float red[256][33];
   float acc[33];
   for (int c = 0; c <= C && c < 33; ++c) acc[c] = 0.f;
@@ -52,38 +106,73 @@ head_bwd_kernel(const float* __restrict__ x, const float* __restrict__ w, const 
   }
   for (int c = 0; c <= C; ++c) red[threadIdx.x][c] = acc[c];
   __syncthreads();
+  // same [blk][2][C] layout as head_bwd_kernel: row 0 = sum g*x[c], row 1 col 0 = sum g
   for (int c = threadIdx.x; c <= C; c += blockDim.x) {
     float s = 0.f;
     for (int t = 0; t < 256; ++t) s += red[t][c];
-    part[(long)blockIdx.x * (C + 1) + c] = s;
+    part[(long)blockIdx.x * 2 * C + c] = s;  // c == C lands on row 1, column 0
   }
+}
+
+// [R][2][C] partial rows -> dw[c] = sum row0, db = sum row1[0]
+__global__ void head_bwd_finish_kernel(const float* __restrict__ sums, int C, float* __restrict__ dw,
+                                       float* __restrict__ db) {
+  const int c = threadIdx.x;
+  if (c < C) dw[c] = sums[c];
+  if (c == 0) db[0] = sums[C];
+}
+
+static int head_tq(int C) {
+  if (C % 4) return 0;
+  const int q = C / 4;
+  return (q & (q - 1)) == 0 && q <= 64 ? q : 0;
 }
 
 extern "C" int accunet_head_fwd(const float* x, const float* w, const float* b, int sigm, float* y,
                                 long P, int C, void* stream) {
-  long blocks = (P + 255) / 256;
-  if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(head_fwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, w, b,
-                     sigm, y, P, C);
+  const int tq = head_tq(C);
+  if (tq) {
+    long blocks = (P * tq + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(head_fwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, w, b,
+                       sigm, y, P, C, tq);
+  } else {
+    long blocks = (P + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(head_fwd_scalar_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x,
+                       w, b, sigm, y, P, C);
+  }
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 
-extern "C" size_t accunet_head_ws_elems(long P, int C) { return (size_t)512 * (C + 1) + 2 * (C + 1) + 64; }
+#define HEAD_NB 1024
+extern "C" size_t accunet_head_ws_elems(long P, int C) {
+  return (size_t)HEAD_NB * 2 * C + accunet_partials_ws_elems(HEAD_NB, 2 * C) + 2 * (size_t)C + 64;
+}
 
 extern "C" int accunet_head_bwd(const float* x, const float* w, const float* y, const float* dy,
                                 int sigm, float* dx, float* dw, float* db, long P, int C, float* ws,
                                 size_t ws_elems, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  if (C > 32) return ACC_EBADSHAPE;
-  const int nb = 512;
+  const int tq = head_tq(C);
+  if (!tq && C > 32) return ACC_EBADSHAPE;
   if (ws_elems < accunet_head_ws_elems(P, C)) return ACC_EBADARG;
+  long nb = (P + 255) / 256;
+  if (nb > HEAD_NB) nb = HEAD_NB;
   float* part = ws;
-  float* sums = ws + (size_t)nb * (C + 1);
-  hipLaunchKernelGGL(head_bwd_kernel, dim3(nb), dim3(256), 0, s, x, w, y, dy, sigm, dx, P, C, part);
-  hipLaunchKernelGGL(sum_rows_kernel, dim3(ceil_div(C + 1, 64)), dim3(256), 0, s, part, nb, C + 1,
-                     C + 1, sums);
-  hipMemcpyAsync(dw, sums, sizeof(float) * C, hipMemcpyDeviceToDevice, s);
-  hipMemcpyAsync(db, sums + C, sizeof(float), hipMemcpyDeviceToDevice, s);
+  float* scratch = ws + (size_t)HEAD_NB * 2 * C;
+  float* sums = scratch + accunet_partials_ws_elems(HEAD_NB, 2 * C);
+  if (tq)
+    hipLaunchKernelGGL(head_bwd_kernel, dim3((unsigned)nb, ceil_div(C / 4, 64)), dim3(256), 0, s, x,
+                       w, y, dy, sigm, dx, P, C, part);
+  else
+    hipLaunchKernelGGL(head_bwd_scalar_kernel, dim3((unsigned)nb), dim3(256), 0, s, x, w, y, dy,
+                       sigm, dx, P, C, part);
+  int rows;
+  const float* pr = reduce_partials(part, (int)nb, 2 * C, scratch, &rows, s);
+  hipLaunchKernelGGL(sum_rows_kernel, dim3(ceil_div(2 * C, 64)), dim3(256), 0, s, pr, rows, 2 * C,
+                     2 * C, sums);
+  hipLaunchKernelGGL(head_bwd_finish_kernel, dim3(1), dim3(64), 0, s, sums, C, dw, db);
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 
@@ -153,27 +242,43 @@ loss_reduce_kernel(const float* __restrict__ x, const float* __restrict__ t, int
 }
 
 // res layout: [0] loss [1] dice [2] bce [3] pw [4] nw [5] binarize flag, then per b: I, U
-__global__ void loss_finalize_kernel(const float* __restrict__ part, int B, long N,
-                                     const float* __restrict__ tmax_part, int nmax, float bw0,
-                                     float bw1, float dice_w, float bce_w, float smooth,
-                                     float* __restrict__ res) {
-  if (threadIdx.x != 0) return;
-  double dice = 0.0, npos = 0.0, spos = 0.0, sneg = 0.0;
-  for (int b = 0; b < B; ++b) {
-    double I = 0, P2 = 0, T2 = 0;
+// One block: thread b (< B) sums sample b's LOSS_NCH chunk rows; the per-sample Dice
+// terms and the BCE counts are then added over b in fixed order by thread 0.
+__global__ void __launch_bounds__(256)
+loss_finalize_kernel(const float* __restrict__ part, int B, long N,
+                     const float* __restrict__ tmax_part, int nmax, float bw0, float bw1,
+                     float dice_w, float bce_w, float smooth, float* __restrict__ res) {
+  __shared__ double red[4][256];
+  __shared__ float tm[256];
+  const int t = threadIdx.x;
+  tm[t] = t < nmax ? tmax_part[t] : -INFINITY;
+  for (int b = t; b < B; b += 256) {
+    double I = 0, P2 = 0, T2 = 0, np = 0, sp = 0, sn = 0;
     for (int ch = 0; ch < LOSS_NCH; ++ch) {
       const float* pr = part + ((long)b * LOSS_NCH + ch) * 6;
       I += pr[0];
       P2 += pr[1];
       T2 += pr[2];
-      npos += pr[3];
-      spos += pr[4];
-      sneg += pr[5];
+      np += pr[3];
+      sp += pr[4];
+      sn += pr[5];
     }
-    double U = P2 + T2;
-    dice += 1.0 - (2.0 * I + smooth) / (U + smooth);
+    const double U = P2 + T2;
     res[8 + 2 * b] = (float)I;
     res[8 + 2 * b + 1] = (float)U;
+    red[0][b] = 1.0 - (2.0 * I + smooth) / (U + smooth);
+    red[1][b] = np;
+    red[2][b] = sp;
+    red[3][b] = sn;
+  }
+  __syncthreads();
+  if (t != 0) return;
+  double dice = 0.0, npos = 0.0, spos = 0.0, sneg = 0.0;
+  for (int b = 0; b < B && b < 256; ++b) {
+    dice += red[0][b];
+    npos += red[1][b];
+    spos += red[2][b];
+    sneg += red[3][b];
   }
   dice /= B;
   double nneg = (double)B * N - npos;
@@ -181,7 +286,7 @@ __global__ void loss_finalize_kernel(const float* __restrict__ part, int B, long
   double nw = nneg < 1.0 ? 1.0 : nneg;
   double bce = bw0 * spos / pw + bw1 * sneg / nw;
   float tmax = -INFINITY;
-  for (int i = 0; i < nmax; ++i) tmax = fmaxf(tmax, tmax_part[i]);
+  for (int i = 0; i < nmax && i < 256; ++i) tmax = fmaxf(tmax, tm[i]);
   res[0] = (float)(dice_w * dice + bce_w * bce);
   res[1] = (float)dice;
   res[2] = (float)bce;
@@ -224,13 +329,14 @@ extern "C" int accunet_loss_fwd(const float* x, const float* t, int B, long N, f
                                 float bce_w, float* res, float* ws, size_t ws_elems, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (ws_elems < accunet_loss_ws_elems(B)) return ACC_EBADARG;
+  if (B < 1 || B > 256) return ACC_EBADSHAPE;  // loss_finalize_kernel: one thread per sample
   float* part = ws;
   float* tmax = ws + (size_t)B * LOSS_NCH * 6;
   const int nmax = 256;
   hipLaunchKernelGGL(max_kernel, dim3(nmax), dim3(256), 0, s, t, (long)B * N, tmax);
   hipLaunchKernelGGL(loss_reduce_kernel, dim3(B * LOSS_NCH), dim3(256), 0, s, x, t, B, N, tmax,
                      nmax, 0.5f, 0.5f, part);
-  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(64), 0, s, part, B, N, tmax, nmax, 0.5f,
+  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), 0, s, part, B, N, tmax, nmax, 0.5f,
                      0.5f, dice_w, bce_w, 1e-5f, res);
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }

@@ -11,3 +11,5 @@ timeout -k 10 300 python tools/gemm_census.py --top 80 > gpurun_out/census.txt 2
 head -2 gpurun_out/census.txt | tail -1
 timeout -k 10 400 python bench.py --no-cpu-baseline > gpurun_out/bench_iter.log 2>&1
 grep '^{"metric' gpurun_out/bench_iter.log | cut -c1-260
+timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/prof_iter -o run -- python bench.py --steps 6 --warmup 2 --no-cpu-baseline --no-probe > gpurun_out/prof_iter.log 2>&1
+echo "trace done"
