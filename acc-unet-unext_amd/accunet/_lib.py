@@ -43,6 +43,7 @@ class AccGemmDesc(Structure):
         ("allow_split", c_int),
         ("pd2", c_void_p), ("pd4", c_void_p),  # fused pyramid backward (float*)
         ("mk2", c_void_p), ("mk4", c_void_p),  # first-max codes (uint8*)
+        ("bz", c_void_p), ("bst", c_void_p), ("bact", c_int),  # BN-backward epilogue stats
     ]
 
 
@@ -66,7 +67,9 @@ _SIGS = {
     "accunet_colsum": [P, L, I, P, P, S, P],
     "accunet_reduce_stats": [P, I, I, P, P, P],
     "accunet_dw3x3_rows": [I, I, I, I],
-    "accunet_dw3x3_fwd": [P, P, P, P, P, I, I, P, P, I, I, I, I, P],
+    "accunet_dw3x3_fwd": [P, P, P, P, P, I, I, P, P, I, I, I, I, P, P, I, P],
+    "accunet_bn_bwd_part_ws_elems": [I, I],
+    "accunet_bn_bwd_part": [P, P, P, P, I, I, L, I, P, I, P, P, P, P, S, P],
     "accunet_dw3x3_wgrad_ws": [I, I, I, I],
     "accunet_dw3x3_wgrad": [P, P, P, P, I, P, P, I, I, I, I, P, S, P],
     "accunet_hanc_pyramid_fwd": [P, P, P, I, I, I, I, I, I, P, P, P, P, P],
@@ -98,7 +101,7 @@ _SIGS = {
     "accunet_wmerge_bwd": [P, P, P, P, L, P],
 }
 # entry points returning a size/count rather than a status
-_SIZE_FNS = {"accunet_bn_bwd_ws_elems", "accunet_dw3x3_wgrad_ws", "accunet_se_save_elems", "accunet_se_ws_elems",
+_SIZE_FNS = {"accunet_bn_bwd_ws_elems", "accunet_bn_bwd_part_ws_elems","accunet_dw3x3_wgrad_ws", "accunet_se_save_elems", "accunet_se_ws_elems",
              "accunet_head_ws_elems", "accunet_loss_ws_elems"}
 
 _lib = None

@@ -49,13 +49,16 @@ def gemm(M: int, N: int, K: int, *, a: Sequence[torch.Tensor], lda: Sequence[int
          H: int = 1, W: int = 1, cin: int = 0,
          ups: Sequence = (), stats: Optional[torch.Tensor] = None,
          allow_split: bool = False, a_offsets: Optional[Sequence[int]] = None,
-         b_offset: int = 0, c_offset: int = 0, pyr: Optional[Sequence] = None):
+         b_offset: int = 0, c_offset: int = 0, pyr: Optional[Sequence] = None,
+         bnb: Optional[Sequence] = None):
     """C[M,N] = A(M,K) B(K,N) (+bias) (+ups) on the current stream.
 
     `ups` is a sequence of (tensor, ld, log2_factor, col_offset) nearest-upsample addends.
     Offsets are element offsets into the respective tensors (column slices).
     `pyr` = (dP2, dP4 or None, mk2, mk4 or None): HANCLayer pyramid backward fused into
     the epilogue (H, W = image size; see AccGemmDesc.pd2).
+    `bnb` = (z, st, act): `stats` receives the BatchNorm-backward partials of the
+    BatchNorm(+act) whose pre-BN input is z [M][ldc] (see AccGemmDesc.bz).
     """
     d = AccGemmDesc()
     d.M, d.N, d.K = int(M), int(N), int(K)
@@ -102,6 +105,14 @@ def gemm(M: int, N: int, K: int, *, a: Sequence[torch.Tensor], lda: Sequence[int
         d.pd4 = pd4.data_ptr() if pd4 is not None else None
         d.mk2 = mk2.data_ptr()
         d.mk4 = mk4.data_ptr() if mk4 is not None else None
+    if bnb is not None:
+        bz, bst, bact = bnb
+        _check(bz, "gemm.bz")
+        if stats is None:
+            raise _lib.AccError("gemm.bnb needs a stats buffer")
+        d.bz = bz.data_ptr()
+        d.bst = bst.data_ptr()
+        d.bact = int(bact)
     ws = None
     ws_elems = 0
     if allow_split:
@@ -157,6 +168,17 @@ def bn_bwd(x, dy, st, gamma, act: int, training: bool, P: int, C: int, dx, accum
     return ws
 
 
+def bn_bwd_part(x, dy, st, gamma, act: int, training: bool, P: int, C: int, part, R: int, dx,
+                dgamma, dbeta):
+    """BatchNorm backward from producer-side partials part [R][2][C] (fp64)."""
+    ws_elems = int(_lib.load().accunet_bn_bwd_part_ws_elems(int(R), int(C)))
+    ws = workspace(ws_elems, x.device)
+    call("accunet_bn_bwd_part", _p(x), _p(dy), _p(st), _p(gamma), int(act), 1 if training else 0,
+         int(P), int(C), _p(part), int(R), _p(dx), _p(dgamma), _p(dbeta), _p(ws), ws_elems,
+         _stream())
+    return ws
+
+
 def colsum(x, P: int, C: int, out):
     nb = stream_rows(P, C)
     ws_elems = nb * 2 * C + partial_ws_elems(nb, 2 * C)
@@ -179,9 +201,12 @@ def dw3x3_rows(B, H, W, C) -> int:
     return int(_lib_raw().accunet_dw3x3_rows(B, H, W, C))
 
 
-def dw3x3_fwd(x, wt, bias, sc, sh, act, flip, z, stats, B, H, W, C):
+def dw3x3_fwd(x, wt, bias, sc, sh, act, flip, z, stats, B, H, W, C, bnb=None):
+    """bnb = (bz, bst, bact): `stats` receives BatchNorm-backward partials (see
+    accunet_dw3x3_fwd in include/accunet.h)."""
+    bz, bst, bact = bnb if bnb is not None else (None, None, 0)
     call("accunet_dw3x3_fwd", _p(x), _p(wt), _p(bias), _p(sc), _p(sh), int(act), int(flip), _p(z),
-         _p(stats), B, H, W, C, _stream())
+         _p(stats), B, H, W, C, _p(bz), _p(bst), int(bact), _stream())
 
 
 def dw3x3_wgrad(x, dz, sc, sh, act, dw, db, B, H, W, C):

@@ -115,6 +115,25 @@ def _pro_bwd(pro: _Pro, z, gamma, dA, need_z=True, need_params=True):
     return dz, dg, db
 
 
+def _pro_bwd_part(pro: _Pro, z, gamma, dA, part, R):
+    """_pro_bwd whose reduce pass already ran in dA's producer (`part` = [R][2][C]
+    partials of (sum g, sum g*(z - mean)) from a GEMM / depthwise epilogue)."""
+    C = z.shape[-1]
+    P = z.numel() // C
+    dz = torch.empty_like(z)
+    dg = _empty((C,), z)
+    db = _empty((C,), z)
+    kern.bn_bwd_part(z, dA, pro.st, gamma, pro.act, pro.training, P, C, part, R, dz, dg, db)
+    return dz, dg, db
+
+
+def _bnb_part(pro: _Pro, P: int, C: int, like, rows: int):
+    """partials buffer + the (z-independent part of the) epilogue request, or None."""
+    if not pro.active:
+        return None
+    return _stats((rows, 2, C), like)
+
+
 def _bn_params(p: Pending):
     if p.bn is None:
         return None, None
@@ -199,10 +218,17 @@ class _PWConvFn(torch.autograd.Function):
                 d_srcs.append(None)
                 continue
             dA = _empty((B, H, W, C), dZ)
-            keep.append(kern.gemm(P, C, N, a=[dZ], lda=[N], b=weight, ldb=cfg.w_ld,
-                                  bmode=BMODE_NN, b_offset=cfg.w_off + kbeg[s], c=dA, ldc=C))
             if s == 0 and pro.active:
-                dA, dpro_g, dpro_b = _pro_bwd(pro, x, pro_g, dA)
+                # the prologue BatchNorm's backward reduce rides in this GEMM's epilogue
+                R = kern.gemm_stats_rows(P, C)
+                part = _bnb_part(pro, P, C, dZ, R)
+                keep.append(kern.gemm(P, C, N, a=[dZ], lda=[N], b=weight, ldb=cfg.w_ld,
+                                      bmode=BMODE_NN, b_offset=cfg.w_off + kbeg[s], c=dA, ldc=C,
+                                      stats=part, bnb=(x, pro.st, pro.act)))
+                dA, dpro_g, dpro_b = _pro_bwd_part(pro, x, pro_g, dA, part, R)
+            else:
+                keep.append(kern.gemm(P, C, N, a=[dZ], lda=[N], b=weight, ldb=cfg.w_ld,
+                                      bmode=BMODE_NN, b_offset=cfg.w_off + kbeg[s], c=dA, ldc=C))
             d_srcs.append(dA)
         dW = None
         if nig[1]:
@@ -308,12 +334,23 @@ class _DWConvFn(torch.autograd.Function):
         B, H, W, C = cfg.B, cfg.H, cfg.W, cfg.C
         pro = cfg.pro
         dA = torch.empty_like(z)
-        kern.dw3x3_fwd(dZ, weight, None, None, None, ACT_NONE, 1, dA, None, B, H, W, C)
+        part = R = None
+        if pro.active:
+            # norm1's backward reduce rides in the data-gradient kernel's epilogue
+            R = kern.dw3x3_rows(B, H, W, C)
+            part = _bnb_part(pro, B * H * W, C, z, R)
+            kern.dw3x3_fwd(dZ, weight, None, None, None, ACT_NONE, 1, dA, part, B, H, W, C,
+                           bnb=(z, pro.st, pro.act))
+        else:
+            kern.dw3x3_fwd(dZ, weight, None, None, None, ACT_NONE, 1, dA, None, B, H, W, C)
         dW = torch.empty_like(weight)
         db = _empty((C,), z)
         ws = kern.dw3x3_wgrad(z, dZ, pro.st[2] if pro.active else None,
                               pro.st[3] if pro.active else None, pro.act, dW, db, B, H, W, C)
-        dz, dg, dbeta = _pro_bwd(pro, z, pro_g, dA)
+        if pro.active:
+            dz, dg, dbeta = _pro_bwd_part(pro, z, pro_g, dA, part, R)
+        else:
+            dz, dg, dbeta = dA, None, None
         del ws
         return None, dz, dg, dbeta, dW, db
 
@@ -449,9 +486,14 @@ class _HancLayerFn(torch.autograd.Function):
         # x branch data gradient; for k >= 2 its epilogue adds the pyramid's backward
         # (avg spread + first-max routing), so dA is written exactly once
         dA = torch.empty_like(z)
+        part = R = None
+        if pro.active:  # norm2's backward reduce rides in this epilogue too
+            R = kern.gemm_stats_rows(P, C)
+            part = _bnb_part(pro, P, C, z, R)
         keep.append(kern.gemm(P, C, N, a=[dZ], lda=[N], b=Wp, ldb=J * C, bmode=BMODE_NN, c=dA,
                               ldc=C, H=H, W=W,
-                              pyr=(dP2, dP4, mk2, mk4) if k >= 2 else None))
+                              pyr=(dP2, dP4, mk2, mk4) if k >= 2 else None, stats=part,
+                              bnb=(z, pro.st, pro.act) if pro.active else None))
         keep.append(kern.gemm(N, C, P, a=[dZ], lda=[N], amode=AMODE_COL, b=z, ldb=C,
                               bmode=BMODE_NN, c=dWp, ldc=J * C, c_offset=0,
                               pro_b=_pro_mode(pro), b_scale=sc, b_shift=sh, allow_split=True))
@@ -459,7 +501,10 @@ class _HancLayerFn(torch.autograd.Function):
         kern.group_relayout(dWp, dW, N, C, J, _HANC_ORDER[k], inverse=True)
         db = _empty((N,), z)
         keep.append(kern.colsum(dZ, P, N, db))
-        dz, dg, dbeta = _pro_bwd(pro, z, pro_g, dA)
+        if pro.active:
+            dz, dg, dbeta = _pro_bwd_part(pro, z, pro_g, dA, part, R)
+        else:
+            dz, dg, dbeta = dA, None, None
         return None, dz, dg, dbeta, dW, db
 
 

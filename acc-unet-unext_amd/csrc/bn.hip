@@ -304,7 +304,7 @@ __global__ void __launch_bounds__(256)
 bn_bwd_finalize_kernel(const double* __restrict__ part, int R, int C, double count,
                        const float* __restrict__ st, const float* __restrict__ gamma,
                        int training, float* __restrict__ dgamma, float* __restrict__ dbeta,
-                       float* __restrict__ coef) {
+                       float* __restrict__ coef, int xc_form) {
   __shared__ double red[2][4][64];
   int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
   int c = blockIdx.x * 64 + cl;
@@ -320,6 +320,8 @@ bn_bwd_finalize_kernel(const double* __restrict__ part, int R, int C, double cou
   if (g != 0 || c >= C) return;
   s1 = red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
   s2 = red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl];
+  // producer-side partials carry sum g*(x - mean): scale to sum g*xhat
+  if (xc_form) s2 *= (double)st[BN_RSTD * C + c];
   if (dgamma) dgamma[c] = (float)s2;
   if (dbeta) dbeta[c] = (float)s1;
   float ga = gamma ? gamma[c] : 1.f;
@@ -424,13 +426,45 @@ extern "C" int accunet_bn_bwd(const float* x, const float* dy, const float* st,
   int rows;
   const double* pr = reduce_partials_t<double>(part, nb, 2 * C, scratch, &rows, s);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(C, 64)), dim3(256), 0, s, pr, rows, C,
-                     (double)P, st, gamma, training, dgamma, dbeta, coef);
+                     (double)P, st, gamma, training, dgamma, dbeta, coef, 0);
   if (V == 4)
     hipLaunchKernelGGL(bn_bwd_apply_kernel<4>, grid, dim3(256), 0, s, x, dy, st, coef, act, P, C,
                        dx, accumulate, colsum);
   else
     hipLaunchKernelGGL(bn_bwd_apply_kernel<1>, grid, dim3(256), 0, s, x, dy, st, coef, act, P, C,
                        dx, accumulate, colsum);
+  return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+}
+
+// BatchNorm backward whose reduce pass ran in the producer of dy (GEMM / depthwise
+// data-gradient epilogues): part = [R][2][C] (sum g, sum g*(x - mean)).
+extern "C" size_t accunet_bn_bwd_part_ws_elems(int R, int C) {
+  return accunet_partials_ws_elems(R, 2 * C) * 2 + 3 * (size_t)C + 2;
+}
+
+extern "C" int accunet_bn_bwd_part(const float* x, const float* dy, const float* st,
+                                   const float* gamma, int act, int training, long P, int C,
+                                   const double* part, int R, float* dx, float* dgamma,
+                                   float* dbeta, float* ws, size_t ws_elems, void* stream_) {
+  hipStream_t s = (hipStream_t)stream_;
+  if (C <= 0 || R <= 0) return ACC_EBADSHAPE;
+  if (ws_elems < accunet_bn_bwd_part_ws_elems(R, C) || ((uintptr_t)ws & 7)) return ACC_EBADARG;
+  const int V = (C % 4 == 0) ? 4 : 1;
+  const int nb = stream_rowblocks(P, C);
+  dim3 grid(nb, ceil_div(C / V, 64));
+  const size_t scr_f = accunet_partials_ws_elems(R, 2 * C) * 2;
+  double* scratch = reinterpret_cast<double*>(ws);
+  float* coef = ws + scr_f;
+  int rows;
+  const double* pr = reduce_partials_t<double>(part, R, 2 * C, scratch, &rows, s);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(C, 64)), dim3(256), 0, s, pr, rows, C,
+                     (double)P, st, gamma, training, dgamma, dbeta, coef, 1);
+  if (V == 4)
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<4>, grid, dim3(256), 0, s, x, dy, st, coef, act, P, C,
+                       dx, 0, nullptr);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<1>, grid, dim3(256), 0, s, x, dy, st, coef, act, P, C,
+                       dx, 0, nullptr);
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 

@@ -57,7 +57,9 @@ __global__ void __launch_bounds__(256)
 dw3x3_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
                  const float* __restrict__ bias, const float* __restrict__ sc,
                  const float* __restrict__ sh, int act, int flip, float* __restrict__ z,
-                 double* __restrict__ stats, DwGeom g) {
+                 double* __restrict__ stats, DwGeom g, const float* __restrict__ bz,
+                 const float* __restrict__ bst, int bact) {
+  const bool bnb = stats != nullptr && bz != nullptr;  // see dw3x3_tile_fwd_kernel
   const int tid = threadIdx.x;
   const int cql = tid % g.TCQ;
   const int px = tid / g.TCQ;
@@ -120,8 +122,17 @@ dw3x3_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
 #pragma unroll
           for (int dx = 0; dx < 3; ++dx) acc = fmaf(k[dy * 3 + dx][j], win[dy][dx][j], acc);
         o[j] = acc;
-        s1[j] += acc;
-        s2[j] += (double)acc * acc;
+        if (bnb) {
+          const float zz = bz[(((long)b * g.H + h) * g.W + w) * C + c0 + j];
+          float gg = acc;
+          if (bact == ACT_LRELU)
+            gg *= lrelu_d(zz * bst[BN_SCALE * C + c0 + j] + bst[BN_SHIFT * C + c0 + j]);
+          s1[j] += gg;
+          s2[j] += (double)gg * ((double)zz - bst[BN_MEAN * C + c0 + j]);
+        } else {
+          s1[j] += acc;
+          s2[j] += (double)acc * acc;
+        }
       }
       vstore<V>(z + (((long)b * g.H + h) * g.W + w) * C + c0, o);
 #pragma unroll
@@ -403,15 +414,19 @@ ACC_DEV void dw_fill_tile(float4* __restrict__ tile, const float* __restrict__ x
 // NEXT chunk adds (r0+9 .. r0+12) are fetched into registers before this chunk is
 // computed and parked afterwards in the slots of rows r0-1 .. r0+2 (dead by then),
 // so HBM reads stay in flight through the compute (software pipeline).
-template <int TCQ>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
+template <int TCQ, bool BNB>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BNB ? 2 : 3)))
 dw3x3_tile_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
                       const float* __restrict__ bias, const float* __restrict__ sc,
                       const float* __restrict__ sh, int act, int flip, float* __restrict__ z,
-                      double* __restrict__ stats, DwTGeom g) {
+                      double* __restrict__ stats, DwTGeom g, const float* __restrict__ bz,
+                      const float* __restrict__ bst, int bact) {
   typedef DwT<TCQ> T;
   constexpr int CR = T::CR;
   __shared__ float4 tile[T::N4 > 1024 ? T::N4 : 1024];
+  // bz != null (data gradient, flip = 1): stats receive the BatchNorm-backward partials
+  // (sum g, sum g*(bz - mean)) of g = out * act'(bz*scale + shift) instead of (sum, sumsq)
+  const bool bnb = BNB && stats != nullptr && bz != nullptr;
   const int tid = threadIdx.x;
   const int q = tid % TCQ, p = tid / TCQ;
   const int c0 = blockIdx.y * TCQ * 4;
@@ -442,15 +457,35 @@ dw3x3_tile_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
     for (int tp = 0; tp < 9; ++tp) k[tp][j] = wt[(c + j) * 9 + (flip ? 8 - tp : tp)];
     bi[j] = bias ? bias[c + j] : 0.f;
   }
+  float bmu[4] = {0.f, 0.f, 0.f, 0.f}, bsc[4] = {0.f, 0.f, 0.f, 0.f}, bsh[4] = {0.f, 0.f, 0.f, 0.f};
+  if (bnb) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bmu[j] = bst[BN_MEAN * g.C + c + j];
+      bsc[j] = bst[BN_SCALE * g.C + c + j];
+      bsh[j] = bst[BN_SHIFT * g.C + c + j];
+    }
+  }
   __syncthreads();
   double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
   const int w = w0 + p;
+  // BNB: the bz rows of a chunk are fetched one chunk ahead (registers), like the input rows
+  float4 zcur[CR], znext[CR];
+  auto fetch_z = [&](float4 (&zz)[CR], int rbase) {
+#pragma unroll
+    for (int r = 0; r < CR; ++r)
+      zz[r] = (w < g.W && rbase + r < hend)
+                  ? ld4(bz + (((long)b * g.H + rbase + r) * g.W + w) * g.C + c)
+                  : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  if (bnb) fetch_z(zcur, hbeg);
   for (int kc = 0; kc < nch; ++kc) {
     const int r0 = hbeg + CR * kc;
     // rows r0+9 .. are needed only if the strip's last input row (hend) lies there
     const bool more = kc + 1 < nch && r0 + 9 <= hend;
     float4 nx[T::NK8];
     if (more) dw_fetch_rows<TCQ, T::NK8>(nx, x, g, b, r0 + 9, T::N8, w0, c0);
+    if (bnb && kc + 1 < nch) fetch_z(znext, r0 + CR);
     if (w < g.W) {
       const int base = (CR * kc) % T::IR;  // slot of input row r0 - 1
       float win[3][3][4];
@@ -479,8 +514,16 @@ dw3x3_tile_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
 #pragma unroll
               for (int dx = 0; dx < 3; ++dx) acc = fmaf(k[dy * 3 + dx][j], win[dy][dx][j], acc);
             o[j] = acc;
-            s1[j] += acc;
-            s2[j] += (double)acc * acc;
+            if (bnb) {
+              const float zz = f4get(zcur[r], j);
+              float gg = acc;
+              if (bact == ACT_LRELU) gg *= lrelu_d(zz * bsc[j] + bsh[j]);
+              s1[j] += gg;
+              s2[j] += (double)gg * ((double)zz - bmu[j]);
+            } else {
+              s1[j] += acc;
+              s2[j] += (double)acc * acc;
+            }
           }
           st4_nt(z + (((long)b * g.H + r0 + r) * g.W + w) * g.C + c, make_float4(o[0], o[1], o[2], o[3]));
 #pragma unroll
@@ -497,6 +540,10 @@ dw3x3_tile_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
       __syncthreads();  // every thread is done with rows r0-1 .. r0+CR-2
       dw_park_rows<TCQ, T::NK8>(tile, nx, g, r0 + 9, T::N8, w0, hbeg, pro, ps, pb, act);
       __syncthreads();
+    }
+    if (bnb) {
+#pragma unroll
+      for (int r = 0; r < CR; ++r) zcur[r] = znext[r];
     }
   }
   if (stats) {
@@ -685,28 +732,38 @@ extern "C" int accunet_dw3x3_rows(int B, int H, int W, int C) {
 
 extern "C" int accunet_dw3x3_fwd(const float* x, const float* wt, const float* bias,
                                  const float* sc, const float* sh, int act, int flip, float* z,
-                                 double* stats, int B, int H, int W, int C, void* stream) {
+                                 double* stats, int B, int H, int W, int C, const float* bz,
+                                 const float* bst, int bact, void* stream) {
   hipStream_t s = (hipStream_t)stream;
+  if (bz && (!bst || !stats)) return ACC_EBADARG;
   dim3 grid;
   int tcq = dw_tile_tcq(W, C);
   if (tcq) {
     DwTGeom tg = dw_tgeom(B, H, W, C, tcq, &grid, dw_rch_max());
-    if (tcq == 16)
-      hipLaunchKernelGGL(dw3x3_tile_fwd_kernel<16>, grid, dim3(256), 0, s, x, wt, bias, sc, sh, act,
-                         flip, z, stats, tg);
-    else
-      hipLaunchKernelGGL(dw3x3_tile_fwd_kernel<8>, grid, dim3(256), 0, s, x, wt, bias, sc, sh, act,
-                         flip, z, stats, tg);
+    if (bz) {
+      if (tcq == 16)
+        hipLaunchKernelGGL((dw3x3_tile_fwd_kernel<16, true>), grid, dim3(256), 0, s, x, wt, bias, sc,
+                           sh, act, flip, z, stats, tg, bz, bst, bact);
+      else
+        hipLaunchKernelGGL((dw3x3_tile_fwd_kernel<8, true>), grid, dim3(256), 0, s, x, wt, bias, sc,
+                           sh, act, flip, z, stats, tg, bz, bst, bact);
+    } else if (tcq == 16) {
+      hipLaunchKernelGGL((dw3x3_tile_fwd_kernel<16, false>), grid, dim3(256), 0, s, x, wt, bias, sc,
+                         sh, act, flip, z, stats, tg, bz, bst, bact);
+    } else {
+      hipLaunchKernelGGL((dw3x3_tile_fwd_kernel<8, false>), grid, dim3(256), 0, s, x, wt, bias, sc,
+                         sh, act, flip, z, stats, tg, bz, bst, bact);
+    }
     return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
   }
   int V = (C % 4 == 0) ? 4 : 1;
   DwGeom g = dw_geom(B, H, W, C, V, &grid);
   if (V == 4)
     hipLaunchKernelGGL(dw3x3_fwd_kernel<4>, grid, dim3(256), 0, s, x, wt, bias, sc, sh, act, flip,
-                       z, stats, g);
+                       z, stats, g, bz, bst, bact);
   else
     hipLaunchKernelGGL(dw3x3_fwd_kernel<1>, grid, dim3(256), 0, s, x, wt, bias, sc, sh, act, flip,
-                       z, stats, g);
+                       z, stats, g, bz, bst, bact);
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 

@@ -19,24 +19,26 @@ typedef void (*gemm_kfn)(const GemmParams);
 // One translation unit per (AMODE,BMODE,PRO_A,PRO_B) defines this table.
 #define GEMM_DECLARE_TABLE(NAME) extern gemm_kfn NAME[2][TILE_COUNT];
 
-#define GEMM_DEFINE_TABLE(NAME, AM, BMo, PA, PB)                                          \
+#define GEMM_DEFINE_TABLE_E(NAME, AM, BMo, PA, PB, EPI)                                   \
   gemm_kfn NAME[2][TILE_COUNT] = {                                                        \
-      {gemm_f32_kernel<AM, BMo, PA, PB, false, false, 2, 2, 2>,                           \
-       gemm_f32_kernel<AM, BMo, PA, PB, false, false, 2, 2, 1>,                           \
-       gemm_f32_kernel<AM, BMo, PA, PB, false, false, 4, 1, 1>,                           \
-       gemm_f32_kernel<AM, BMo, PA, PB, false, false, 1, 1, 1>,                           \
-       gemm_f32_kernel<AM, BMo, PA, PB, false, false, 2, 1, 1>},                          \
-      {gemm_f32_kernel<AM, BMo, PA, PB, true, true, 2, 2, 2>,                             \
-       gemm_f32_kernel<AM, BMo, PA, PB, true, true, 2, 2, 1>,                             \
-       gemm_f32_kernel<AM, BMo, PA, PB, true, true, 4, 1, 1>,                             \
-       gemm_f32_kernel<AM, BMo, PA, PB, true, true, 1, 1, 1>,                             \
-       gemm_f32_kernel<AM, BMo, PA, PB, true, true, 2, 1, 1>}};
+      {gemm_f32_kernel<AM, BMo, PA, PB, false, false, 2, 2, 2, EPI>,                      \
+       gemm_f32_kernel<AM, BMo, PA, PB, false, false, 2, 2, 1, EPI>,                      \
+       gemm_f32_kernel<AM, BMo, PA, PB, false, false, 4, 1, 1, EPI>,                      \
+       gemm_f32_kernel<AM, BMo, PA, PB, false, false, 1, 1, 1, EPI>,                      \
+       gemm_f32_kernel<AM, BMo, PA, PB, false, false, 2, 1, 1, EPI>},                     \
+      {gemm_f32_kernel<AM, BMo, PA, PB, true, true, 2, 2, 2, EPI>,                        \
+       gemm_f32_kernel<AM, BMo, PA, PB, true, true, 2, 2, 1, EPI>,                        \
+       gemm_f32_kernel<AM, BMo, PA, PB, true, true, 4, 1, 1, EPI>,                        \
+       gemm_f32_kernel<AM, BMo, PA, PB, true, true, 1, 1, 1, EPI>,                        \
+       gemm_f32_kernel<AM, BMo, PA, PB, true, true, 2, 1, 1, EPI>}};
+#define GEMM_DEFINE_TABLE(NAME, AM, BMo, PA, PB) GEMM_DEFINE_TABLE_E(NAME, AM, BMo, PA, PB, 0)
 
 GEMM_DECLARE_TABLE(g_gemm_row_nt_p0)
 GEMM_DECLARE_TABLE(g_gemm_row_nt_p1)
 GEMM_DECLARE_TABLE(g_gemm_row_nt_p2)
 GEMM_DECLARE_TABLE(g_gemm_sh3_nt)
 GEMM_DECLARE_TABLE(g_gemm_row_nn)
+GEMM_DECLARE_TABLE(g_gemm_row_nn_bnb)
 GEMM_DECLARE_TABLE(g_gemm_col_nn_p0)
 GEMM_DECLARE_TABLE(g_gemm_col_nn_p1)
 GEMM_DECLARE_TABLE(g_gemm_col_nn_p2)

@@ -63,6 +63,10 @@ struct GemmParams {
   const float* pd4;
   const unsigned char* mk2;
   const unsigned char* mk4;
+  // BatchNorm-backward statistics in the epilogue (see AccGemmDesc.bz)
+  const float* bz;
+  const float* bst;
+  int bact;
   int kchunk;    // K range per blockIdx.z (split-K); >= K means no split
   size_t zstride;  // element stride between split-K partial slabs
   int evec;      // epilogue may use 16-byte accesses (host-checked alignment)
@@ -76,7 +80,9 @@ ACC_DEV float pro_apply(float v, float sc, float sh) {
   return y;
 }
 
-template <int AMODE, int BMODE, int PRO_A, int PRO_B, bool VA, bool VB, int WM, int TM, int TN>
+// EPI = 1: BatchNorm-backward statistics epilogue (GemmParams.bz; data gradients only)
+template <int AMODE, int BMODE, int PRO_A, int PRO_B, bool VA, bool VB, int WM, int TM, int TN,
+          int EPI = 0>
 __global__ void __launch_bounds__(GEMM_THREADS)
 gemm_f32_kernel(const GemmParams p) {
   constexpr int WN = 4 / WM;
@@ -479,6 +485,18 @@ gemm_f32_kernel(const GemmParams p) {
     for (int e = 0; e < 4; ++e) bq[e] = (nq + e < N) ? p.bias[nq + e] : 0.f;
   }
   double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+  // BatchNorm-backward statistics mode: this thread's column-quad state
+  const bool bnb = EPI == 1 && !split && p.stats && p.bz;
+  float bmu[4] = {0.f, 0.f, 0.f, 0.f}, bsc4[4] = {0.f, 0.f, 0.f, 0.f}, bsh4[4] = {0.f, 0.f, 0.f, 0.f};
+  if (bnb) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int n = nq + e < N ? nq + e : N - 1;
+      bmu[e] = p.bst[BN_MEAN * N + n];
+      bsc4[e] = p.bst[BN_SCALE * N + n];
+      bsh4[e] = p.bst[BN_SHIFT * N + n];
+    }
+  }
   const bool need_pix = !split && (p.nup > 0 || p.pd2);
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
@@ -499,11 +517,24 @@ gemm_f32_kernel(const GemmParams p) {
       int mrow[EC];
       bool ok[EC];
       float v[EC][4];
+      float4 zb[EC];
 #pragma unroll
       for (int c = 0; c < EC; ++c) {
         const int rr = rr0 + (r0 + c) * RPP;
         mrow[c] = m0 + (rr >> 5) * TM * 32 + i * 32 + (rr & 31);
         ok[c] = (r0 + c < NR) && mrow[c] < M && nq < N;
+        zb[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (bnb && ok[c]) {  // pre-BN input of the BatchNorm whose backward this feeds
+          const float* zr = p.bz + (size_t)mrow[c] * p.ldc + nq;
+          if (evec) {
+            zb[c] = ld4(zr);
+          } else {
+            float t[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) t[e] = (nq + e < N) ? zr[e] : 0.f;
+            zb[c] = make_float4(t[0], t[1], t[2], t[3]);
+          }
+        }
         const float4 a4 = *reinterpret_cast<const float4*>(smem + (ok[c] ? rr : 0) * SC + 4 * cq);
         v[c][0] = a4.x; v[c][1] = a4.y; v[c][2] = a4.z; v[c][3] = a4.w;
         if (!split) {
@@ -621,7 +652,18 @@ gemm_f32_kernel(const GemmParams p) {
 #pragma unroll
       for (int c = 0; c < EC; ++c) {
         if (!ok[c]) continue;
-        if (!split && p.stats) {
+        if (bnb) {
+          // g = dC * act'(z*scale + shift); (sum g, sum g*(z - mean)) as bn_bwd_reduce_kernel
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (nq + e < N) {
+              const float z = f4get(zb[c], e);
+              float g = v[c][e];
+              if (p.bact == ACT_LRELU) g *= lrelu_d(z * bsc4[e] + bsh4[e]);
+              s1[e] += g;
+              s2[e] += (double)g * ((double)z - bmu[e]);
+            }
+        } else if (!split && p.stats) {
 #pragma unroll
           for (int e = 0; e < 4; ++e)
             if (nq + e < N) {

@@ -43,7 +43,12 @@ splitk_reduce_kernel(const float* __restrict__ ws, float* __restrict__ C, int M,
   }
 }
 
-static gemm_kfn* table_for(int amode, int bmode, int pro_a, int pro_b) {
+static gemm_kfn* table_for(int amode, int bmode, int pro_a, int pro_b, bool bnb) {
+  if (bnb) {  // BatchNorm-backward statistics epilogue: data gradients only
+    if (amode == AM_ROW && bmode == BM_NN && pro_a == PRO_NONE && pro_b == PRO_NONE)
+      return g_gemm_row_nn_bnb[0];
+    return nullptr;
+  }
   if (amode == AM_ROW && bmode == BM_NT && pro_b == PRO_NONE) {
     if (pro_a == PRO_NONE) return g_gemm_row_nt_p0[0];
     if (pro_a == PRO_AFFINE) return g_gemm_row_nt_p1[0];
@@ -63,9 +68,9 @@ static gemm_kfn* table_for(int amode, int bmode, int pro_a, int pro_b) {
   return nullptr;
 }
 
-static gemm_kfn* table_v(int amode, int bmode, int pro_a, int pro_b, int v) {
+static gemm_kfn* table_v(int amode, int bmode, int pro_a, int pro_b, bool bnb, int v) {
   // the tables are [2][TILE_COUNT]; table_for returns row 0
-  gemm_kfn* t0 = table_for(amode, bmode, pro_a, pro_b);
+  gemm_kfn* t0 = table_for(amode, bmode, pro_a, pro_b, bnb);
   return t0 ? t0 + v * TILE_COUNT : nullptr;
 }
 
@@ -105,7 +110,7 @@ int gemm_run(GemmParams p, int amode, int bmode, int pro_a, int pro_b, bool allo
     if (bmode == BM_NN_SHIFT3 && (p.cin & 3)) vec = false;
   }
   if (amode == AM_ROW && p.nsrc == 1) { p.kbeg[0] = 0; p.kbeg[1] = p.K; }
-  gemm_kfn* tab = table_v(amode, bmode, pro_a, pro_b, vec ? 1 : 0);
+  gemm_kfn* tab = table_v(amode, bmode, pro_a, pro_b, p.bz != nullptr, vec ? 1 : 0);
   if (!tab) return ACC_EBADARG;
   int t = pick_tile(p.M, p.N, bmode, p.cin);
   int BM = tile_bm(t), BN = tile_bn(t);
@@ -200,6 +205,10 @@ extern "C" int accunet_gemm(const AccGemmDesc* d, float* ws, size_t ws_elems, vo
   p.pd4 = d->pd4;
   p.mk2 = d->mk2;
   p.mk4 = d->mk4;
+  p.bz = d->bz;
+  p.bst = d->bst;
+  p.bact = d->bact;
+  if (p.bz && (!p.bst || !p.stats)) return ACC_EBADARG;
   if (p.pd2 && (!p.mk2 || (p.pd4 && !p.mk4) || (p.H & 1) || (p.W & 1) ||
                 (p.pd4 && ((p.H & 3) || (p.W & 3))) || p.ldc != p.N))
     return ACC_EBADARG;

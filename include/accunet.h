@@ -73,6 +73,14 @@ typedef struct AccGemmDesc {
   const float* pd4;
   const unsigned char* mk2;
   const unsigned char* mk4;
+  /* BatchNorm backward statistics in the epilogue (data gradients whose input went
+   * through a pending BatchNorm(+LeakyReLU) prologue in the forward): with bz the
+   * pre-BN input z [M][ldc] and bst its [4][N] state block, `stats` receives per-row-
+   * block (sum g, sum g*(z - mean)) of g = C * act'(z*scale + shift) instead of
+   * (sum C, sum C^2); accunet_bn_bwd_part finishes the BatchNorm backward. */
+  const float* bz;
+  const float* bst;
+  int bact;
 } AccGemmDesc;
 
 int accunet_gemm(const AccGemmDesc* d, float* ws, size_t ws_elems, void* stream);
@@ -102,6 +110,15 @@ int accunet_bn_bwd(const float* x, const float* dy, const float* st, const float
                    int training, long P, int C, float* dx, int accumulate, float* dgamma,
                    float* dbeta, float* colsum, int* colsum_rows, float* ws, size_t ws_elems,
                    void* stream);
+/* BatchNorm backward from producer-side partials: part = [R][2][C] (sum g,
+ * sum g*(x - mean)) written by a data-gradient epilogue (AccGemmDesc.bz,
+ * accunet_dw3x3_fwd bz) -> dgamma, dbeta, dx = k1*g + k2*(x - mean) + k3 in one
+ * streaming pass (the reduce pass of accunet_bn_bwd is skipped). */
+size_t accunet_bn_bwd_part_ws_elems(int R, int C);
+int accunet_bn_bwd_part(const float* x, const float* dy, const float* st, const float* gamma,
+                        int act, int training, long P, int C, const double* part, int R,
+                        float* dx, float* dgamma, float* dbeta, float* ws, size_t ws_elems,
+                        void* stream);
 int accunet_colsum(const float* x, long P, int C, float* out, double* ws, size_t ws_elems,
                    void* stream);
 int accunet_reduce_stats(const double* part, int R, int C, double* out2C, double* ws,
@@ -112,12 +129,14 @@ int accunet_reduce_stats(const double* part, int R, int C, double* out2C, double
  * (ACC_UNet/ACC_UNet.py:240-247, forward :273). Input may carry a pending
  * BatchNorm+LeakyReLU (sc/sh/act, norm1 :236) applied on load; `stats` receives
  * per-block (sum, sumsq) of z for norm2. flip=1 runs the kernel with W[c][8-tap]
- * (the data gradient). wgrad writes dW [C][1][3][3] and db [C].
+ * (the data gradient); with bz/bst/bact (the pre-BN input of norm1 and its state)
+ * `stats` then receives the BatchNorm-backward partials (sum g, sum g*(bz - mean)),
+ * g = out * act'(bz*scale + shift), for accunet_bn_bwd_part. wgrad writes dW [C][1][3][3] and db [C].
  * ------------------------------------------------------------------------- */
 int accunet_dw3x3_rows(int B, int H, int W, int C);
 int accunet_dw3x3_fwd(const float* x, const float* wt, const float* bias, const float* sc,
                       const float* sh, int act, int flip, float* z, double* stats, int B, int H,
-                      int W, int C, void* stream);
+                      int W, int C, const float* bz, const float* bst, int bact, void* stream);
 size_t accunet_dw3x3_wgrad_ws(int B, int H, int W, int C);
 int accunet_dw3x3_wgrad(const float* x, const float* dz, const float* sc, const float* sh,
                         int act, float* dw, float* db, int B, int H, int W, int C, float* ws,

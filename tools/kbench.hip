@@ -127,10 +127,10 @@ int main(int argc, char** argv) {
            timeit([&] { hipLaunchKernelGGL(copy4_x4_nt, dim3((n4 + 1023) / 1024), dim3(256), 0, 0,
                                            (const float4*)x, (float4*)z, n4); }, iters), bytes);
     report("K1 dw3x3_fwd 16x256x256x96 pro+stats",
-           timeit([&] { CA(accunet_dw3x3_fwd(x, wt, bi, sc, sh, 1, 0, z, st, B, H, W, C, 0)); }, iters),
+           timeit([&] { CA(accunet_dw3x3_fwd(x, wt, bi, sc, sh, 1, 0, z, st, B, H, W, C, nullptr, nullptr, 0, 0)); }, iters),
            bytes);
     report("K1 dw3x3_fwd flip (dgrad) no pro/stats",
-           timeit([&] { CA(accunet_dw3x3_fwd(x, wt, nullptr, nullptr, nullptr, 0, 1, z, nullptr, B, H, W, C, 0)); }, iters),
+           timeit([&] { CA(accunet_dw3x3_fwd(x, wt, nullptr, nullptr, nullptr, 0, 1, z, nullptr, B, H, W, C, nullptr, nullptr, 0, 0)); }, iters),
            bytes);
     size_t wse = accunet_dw3x3_wgrad_ws(B, H, W, C);
     float* ws = dalloc(wse);
@@ -151,7 +151,7 @@ int main(int argc, char** argv) {
       CK(hipMalloc(&st, (size_t)rows * 2 * C * sizeof(double)));
       char name[96];
       snprintf(name, sizeof name, "K1 sweep 16x256x256x%d", C);
-      report(name, timeit([&] { CA(accunet_dw3x3_fwd(x, wt, bi, sc, sh, 1, 0, z, st, B, H, W, C, 0)); }, iters),
+      report(name, timeit([&] { CA(accunet_dw3x3_fwd(x, wt, bi, sc, sh, 1, 0, z, st, B, H, W, C, nullptr, nullptr, 0, 0)); }, iters),
              2.0 * 4 * n);
       CK(hipFree(x)); CK(hipFree(z)); CK(hipFree(st)); CK(hipFree(wt)); CK(hipFree(bi));
       CK(hipFree(sc)); CK(hipFree(sh));
