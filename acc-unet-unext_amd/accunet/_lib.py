@@ -58,7 +58,7 @@ IP = POINTER(c_int)
 # name -> argtypes (restype is always int status)
 _SIGS = {
     "accunet_gemm": [POINTER(AccGemmDesc), P, S, P],
-    "accunet_gemm_stats_rows": [I, I, I, I, I],
+    "accunet_gemm_stats_rows": [I, I, I, I, I, I],
     "accunet_stream_rows": [L, I],
     "accunet_bn_finalize": [P, I, I, D, P, P, P, P, P, F, F, I, P, P, P],
     "accunet_affine_act_fwd": [P, P, P, I, P, P, L, I, P, IP, P],

@@ -124,8 +124,9 @@ def gemm(M: int, N: int, K: int, *, a: Sequence[torch.Tensor], lda: Sequence[int
     return ws  # keep alive until the stream consumes it (caching allocator is stream-ordered)
 
 
-def gemm_stats_rows(M, N, amode=_lib.AMODE_ROW, bmode=_lib.BMODE_NT, cin=0) -> int:
-    return int(_lib.load().accunet_gemm_stats_rows(int(M), int(N), amode, bmode, int(cin)))
+def gemm_stats_rows(M, N, K, amode=_lib.AMODE_ROW, bmode=_lib.BMODE_NT, cin=0) -> int:
+    """partial-statistics rows accunet_gemm writes for an M x N x K GEMM."""
+    return int(_lib.load().accunet_gemm_stats_rows(int(M), int(N), int(K), amode, bmode, int(cin)))
 
 
 def stream_rows(P: int, C: int) -> int:

@@ -178,7 +178,7 @@ class _PWConvFn(torch.autograd.Function):
         stats = None
         rows = 0
         if cfg.want_stats:
-            rows = kern.gemm_stats_rows(P, N)
+            rows = kern.gemm_stats_rows(P, N, K)
             stats = _stats((rows, 2, N), weight)
         pro = cfg.pro
         kern.gemm(P, N, K, a=list(srcs), lda=cfg.src_ch, kbeg=kbeg, b=weight, ldb=cfg.w_ld,
@@ -220,7 +220,7 @@ class _PWConvFn(torch.autograd.Function):
             dA = _empty((B, H, W, C), dZ)
             if s == 0 and pro.active:
                 # the prologue BatchNorm's backward reduce rides in this GEMM's epilogue
-                R = kern.gemm_stats_rows(P, C)
+                R = kern.gemm_stats_rows(P, C, N)
                 part = _bnb_part(pro, P, C, dZ, R)
                 keep.append(kern.gemm(P, C, N, a=[dZ], lda=[N], b=weight, ldb=cfg.w_ld,
                                       bmode=BMODE_NN, b_offset=cfg.w_off + kbeg[s], c=dA, ldc=C,
@@ -285,7 +285,7 @@ def pw_conv(srcs: Sequence, weight, bias, *, w_off: int = 0, ups: Sequence = (),
     Z, stats = _PWConvFn.apply(cfg, w2, bias, pg, pb, *[s.z for s in srcs],
                                *[g for g, _, _ in ups])
     return Pending(Z, consumer_bn, ACT_LRELU, stats if want_stats else None,
-                   kern.gemm_stats_rows(B * H * W, N) if want_stats else 0)
+                   stats.shape[0] if want_stats else 0)
 
 
 # --------------------------------------------------------------------------
@@ -426,7 +426,7 @@ class _HancLayerFn(torch.autograd.Function):
         Z = _empty((B, H, W, N), z)
         stats = None
         if cfg.want_stats:
-            stats = _stats((kern.gemm_stats_rows(P, N), 2, N), z)
+            stats = _stats((kern.gemm_stats_rows(P, N, C), 2, N), z)
         with _prof.region(f"hanc_gemm P{P} N{N} K{C}", kernel="gemm_f32_kernel (HANC x-branch)",
                           shape=f"M{P} N{N} K{C}", flops=2.0 * P * N * C):
             kern.gemm(P, N, C, a=[z], lda=[C], b=Wp, ldb=J * C, c=Z, ldc=N, bias=bias,
@@ -488,7 +488,7 @@ class _HancLayerFn(torch.autograd.Function):
         dA = torch.empty_like(z)
         part = R = None
         if pro.active:  # norm2's backward reduce rides in this epilogue too
-            R = kern.gemm_stats_rows(P, C)
+            R = kern.gemm_stats_rows(P, C, N)
             part = _bnb_part(pro, P, C, z, R)
         keep.append(kern.gemm(P, C, N, a=[dZ], lda=[N], b=Wp, ldb=J * C, bmode=BMODE_NN, c=dA,
                               ldc=C, H=H, W=W,
@@ -522,7 +522,7 @@ def hanc_layer(x, weight, bias, k: int, *, consumer_bn=None):
     pg, pb = _bn_params(x)
     Z, stats = _HancLayerFn.apply(cfg, x.z, pg, pb, w2, bias)
     return Pending(Z, consumer_bn, ACT_LRELU, stats if want else None,
-                   kern.gemm_stats_rows(B * H * W, N) if want else 0)
+                   stats.shape[0] if want else 0)
 
 
 # --------------------------------------------------------------------------
@@ -695,7 +695,7 @@ class _Conv3x3Fn(torch.autograd.Function):
         Wr = _empty((Co, 9 * Ci), x)  # [co][tap][ci]
         kern.permute4(weight, Wr, (Co, 3, 3, Ci), (9 * Ci, 3, 1, 9))
         Z = _empty((B, H, W, Co), x)
-        stats = _stats((kern.gemm_stats_rows(P, Co), 2, Co), x) if cfg.want_stats else None
+        stats = _stats((kern.gemm_stats_rows(P, Co, 9 * Ci), 2, Co), x) if cfg.want_stats else None
         kern.gemm(P, Co, 9 * Ci, a=[x], lda=[Ci], amode=AMODE_SHIFT3, b=Wr, ldb=9 * Ci, c=Z,
                   ldc=Co, bias=bias, H=H, W=W, cin=Ci, stats=stats)
         ctx.cfg = cfg
@@ -741,7 +741,7 @@ def conv3x3(x: torch.Tensor, weight, bias, *, consumer_bn=None):
     cfg = _C3Cfg(B, H, W, Ci, Co, want)
     Z, stats = _Conv3x3Fn.apply(cfg, x, weight, bias)
     return Pending(Z, consumer_bn, ACT_LRELU, stats if want else None,
-                   kern.gemm_stats_rows(B * H * W, Co) if want else 0)
+                   stats.shape[0] if want else 0)
 
 
 # --------------------------------------------------------------------------

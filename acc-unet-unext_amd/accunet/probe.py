@@ -92,7 +92,7 @@ def hanc_gemm(P, N, K, iters=10, device="cuda"):
     w = (torch.randn(N, K, generator=g) * K ** -0.5).to(device)
     bias = torch.zeros(N, device=device)
     c = torch.empty(P, N, device=device)
-    st = torch.empty(kern.gemm_stats_rows(P, N), 2, N, dtype=torch.float64, device=device)
+    st = torch.empty(kern.gemm_stats_rows(P, N, K), 2, N, dtype=torch.float64, device=device)
 
     def run():
         kern.gemm(P, N, K, a=[a], lda=[K], b=w, ldb=K, c=c, ldc=N, bias=bias, stats=st)

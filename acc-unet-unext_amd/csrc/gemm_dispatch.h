@@ -36,9 +36,14 @@ typedef void (*gemm_kfn)(const GemmParams);
 GEMM_DECLARE_TABLE(g_gemm_row_nt_p0)
 GEMM_DECLARE_TABLE(g_gemm_row_nt_p1)
 GEMM_DECLARE_TABLE(g_gemm_row_nt_p2)
+GEMM_DECLARE_TABLE(g_gemm_row_nt_p0_ups)
+GEMM_DECLARE_TABLE(g_gemm_row_nt_p1_ups)
+GEMM_DECLARE_TABLE(g_gemm_row_nt_p2_ups)
 GEMM_DECLARE_TABLE(g_gemm_sh3_nt)
 GEMM_DECLARE_TABLE(g_gemm_row_nn)
 GEMM_DECLARE_TABLE(g_gemm_row_nn_bnb)
+GEMM_DECLARE_TABLE(g_gemm_row_nn_pyr)
+GEMM_DECLARE_TABLE(g_gemm_row_nn_bnb_pyr)
 GEMM_DECLARE_TABLE(g_gemm_col_nn_p0)
 GEMM_DECLARE_TABLE(g_gemm_col_nn_p1)
 GEMM_DECLARE_TABLE(g_gemm_col_nn_p2)

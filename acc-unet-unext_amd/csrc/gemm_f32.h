@@ -80,7 +80,12 @@ ACC_DEV float pro_apply(float v, float sc, float sh) {
   return y;
 }
 
-// EPI = 1: BatchNorm-backward statistics epilogue (GemmParams.bz; data gradients only)
+// EPI: compile-time epilogue features (bit set) so that GEMMs without them do not pay
+// their registers: EPI_BNB BatchNorm-backward statistics (GemmParams.bz; data
+// gradients), EPI_PYR fused HANCLayer pyramid backward (pd2/pd4), EPI_UPS
+// nearest-upsampled addends (up[]). A launch whose arguments need a feature must
+// use a table that has it (gemm_run checks).
+enum { EPI_BNB = 1, EPI_PYR = 2, EPI_UPS = 4 };
 template <int AMODE, int BMODE, int PRO_A, int PRO_B, bool VA, bool VB, int WM, int TM, int TN,
           int EPI = 0>
 __global__ void __launch_bounds__(GEMM_THREADS)
@@ -486,7 +491,7 @@ gemm_f32_kernel(const GemmParams p) {
   }
   double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
   // BatchNorm-backward statistics mode: this thread's column-quad state
-  const bool bnb = EPI == 1 && !split && p.stats && p.bz;
+  const bool bnb = (EPI & EPI_BNB) && !split && p.stats && p.bz;
   float bmu[4] = {0.f, 0.f, 0.f, 0.f}, bsc4[4] = {0.f, 0.f, 0.f, 0.f}, bsh4[4] = {0.f, 0.f, 0.f, 0.f};
   if (bnb) {
 #pragma unroll
@@ -497,7 +502,7 @@ gemm_f32_kernel(const GemmParams p) {
       bsh4[e] = p.bst[BN_SHIFT * N + n];
     }
   }
-  const bool need_pix = !split && (p.nup > 0 || p.pd2);
+  const bool need_pix = !split && (((EPI & EPI_UPS) && p.nup > 0) || ((EPI & EPI_PYR) && p.pd2));
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     __syncthreads();  // LDS free (main loop / previous pass)
@@ -542,7 +547,7 @@ gemm_f32_kernel(const GemmParams p) {
           for (int e = 0; e < 4; ++e) v[c][e] += bq[e];
         }
       }
-      if (need_pix && p.pd2) {
+      if ((EPI & EPI_PYR) && need_pix && p.pd2) {
         // fused HANCLayer pyramid backward: same accumulation order as the standalone
         // pyramid backward, g = (avg2/4 [+ max2]) + avg4/16 [+ max4]; C += g
         float4 av2[EC], mx2[EC], av4[EC], mx4[EC];
@@ -611,7 +616,7 @@ gemm_f32_kernel(const GemmParams p) {
             v[c][e] += g;
           }
         }
-      } else if (need_pix) {
+      } else if ((EPI & EPI_UPS) && need_pix) {
         // nearest-upsampled addends (HANCLayer coarse branches, MLFC coarse sources),
         // added in source order
         float4 up4[EC][3];
@@ -673,7 +678,7 @@ gemm_f32_kernel(const GemmParams p) {
         }
         float* dst = Cout + (size_t)mrow[c] * (split ? N : p.ldc) + nq;
         if (evec) {
-          st4(dst, make_float4(v[c][0], v[c][1], v[c][2], v[c][3]));
+          st4_nt(dst, make_float4(v[c][0], v[c][1], v[c][2], v[c][3]));  // streaming: C is not re-read by this kernel
         } else {
 #pragma unroll
           for (int e = 0; e < 4; ++e)

@@ -2,6 +2,7 @@
 // split-K reduction (fixed slab order, no float atomics).
 #include "gemm_dispatch.h"
 #include <string.h>
+#include <stdlib.h>
 
 // One block = 64 consecutive outputs x 16 slab groups (1024 threads): thread
 // (c, g) sums slabs g, g+16, ... in order, then the 16 group sums are added in
@@ -43,17 +44,23 @@ splitk_reduce_kernel(const float* __restrict__ ws, float* __restrict__ C, int M,
   }
 }
 
-static gemm_kfn* table_for(int amode, int bmode, int pro_a, int pro_b, bool bnb) {
-  if (bnb) {  // BatchNorm-backward statistics epilogue: data gradients only
-    if (amode == AM_ROW && bmode == BM_NN && pro_a == PRO_NONE && pro_b == PRO_NONE)
-      return g_gemm_row_nn_bnb[0];
-    return nullptr;
+// epi: the EPI_* features this launch needs
+static gemm_kfn* table_for(int amode, int bmode, int pro_a, int pro_b, int epi) {
+  if (epi & (EPI_BNB | EPI_PYR)) {  // data-gradient epilogues
+    if (amode != AM_ROW || bmode != BM_NN || pro_a != PRO_NONE || pro_b != PRO_NONE ||
+        (epi & EPI_UPS))
+      return nullptr;
+    if (epi == EPI_BNB) return g_gemm_row_nn_bnb[0];
+    if (epi == EPI_PYR) return g_gemm_row_nn_pyr[0];
+    return g_gemm_row_nn_bnb_pyr[0];
   }
   if (amode == AM_ROW && bmode == BM_NT && pro_b == PRO_NONE) {
-    if (pro_a == PRO_NONE) return g_gemm_row_nt_p0[0];
-    if (pro_a == PRO_AFFINE) return g_gemm_row_nt_p1[0];
-    if (pro_a == PRO_AFFINE_LRELU) return g_gemm_row_nt_p2[0];
+    const bool u = (epi & EPI_UPS) != 0;
+    if (pro_a == PRO_NONE) return u ? g_gemm_row_nt_p0_ups[0] : g_gemm_row_nt_p0[0];
+    if (pro_a == PRO_AFFINE) return u ? g_gemm_row_nt_p1_ups[0] : g_gemm_row_nt_p1[0];
+    if (pro_a == PRO_AFFINE_LRELU) return u ? g_gemm_row_nt_p2_ups[0] : g_gemm_row_nt_p2[0];
   }
+  if (epi & EPI_UPS) return nullptr;  // nearest-up addends: forward 1x1 GEMMs only
   if (amode == AM_SHIFT3 && bmode == BM_NT && pro_a == PRO_NONE && pro_b == PRO_NONE)
     return g_gemm_sh3_nt[0];
   if (amode == AM_ROW && bmode == BM_NN && pro_a == PRO_NONE && pro_b == PRO_NONE)
@@ -68,14 +75,27 @@ static gemm_kfn* table_for(int amode, int bmode, int pro_a, int pro_b, bool bnb)
   return nullptr;
 }
 
-static gemm_kfn* table_v(int amode, int bmode, int pro_a, int pro_b, bool bnb, int v) {
+static gemm_kfn* table_v(int amode, int bmode, int pro_a, int pro_b, int epi, int v) {
   // the tables are [2][TILE_COUNT]; table_for returns row 0
-  gemm_kfn* t0 = table_for(amode, bmode, pro_a, pro_b, bnb);
+  gemm_kfn* t0 = table_for(amode, bmode, pro_a, pro_b, epi);
   return t0 ? t0 + v * TILE_COUNT : nullptr;
 }
 
-static int pick_tile(int M, int N, int bmode, int cin) {
+static int smallk_tile() {
+  static int v = -2;
+  if (v == -2) {
+    const char* e = getenv("ACCUNET_SMALLK_TILE");  // tuning knob: -1 = off, else tile id
+    v = e ? atoi(e) : TILE_E;
+  }
+  return v;
+}
+
+static int pick_tile(int M, int N, int K, int bmode, int cin) {
   int t;
+  // short-K GEMMs over many pixels (1x1 data gradients, K = the forward's N <= 64):
+  // epilogue-dominated, so smaller tiles (more resident waves to hide its gathers)
+  const int sk = smallk_tile();
+  if (sk >= 0 && K <= 64 && M >= 65536 && N > 32) return sk;
   if (M <= 32) t = TILE_D;
   else if (M <= 64) t = TILE_E;
   else if (N <= 32) t = TILE_C;
@@ -110,9 +130,10 @@ int gemm_run(GemmParams p, int amode, int bmode, int pro_a, int pro_b, bool allo
     if (bmode == BM_NN_SHIFT3 && (p.cin & 3)) vec = false;
   }
   if (amode == AM_ROW && p.nsrc == 1) { p.kbeg[0] = 0; p.kbeg[1] = p.K; }
-  gemm_kfn* tab = table_v(amode, bmode, pro_a, pro_b, p.bz != nullptr, vec ? 1 : 0);
+  const int epi = (p.bz ? EPI_BNB : 0) | (p.pd2 ? EPI_PYR : 0) | (p.nup > 0 ? EPI_UPS : 0);
+  gemm_kfn* tab = table_v(amode, bmode, pro_a, pro_b, epi, vec ? 1 : 0);
   if (!tab) return ACC_EBADARG;
-  int t = pick_tile(p.M, p.N, bmode, p.cin);
+  int t = pick_tile(p.M, p.N, p.K, bmode, p.cin);
   int BM = tile_bm(t), BN = tile_bn(t);
   int gx = ceil_div(p.M, BM), gy = ceil_div(p.N, BN);
 
@@ -216,7 +237,7 @@ extern "C" int accunet_gemm(const AccGemmDesc* d, float* ws, size_t ws_elems, vo
                   (hipStream_t)stream);
 }
 
-extern "C" int accunet_gemm_stats_rows(int M, int N, int amode, int bmode, int cin) {
-  int t = pick_tile(M, N, bmode, cin);
+extern "C" int accunet_gemm_stats_rows(int M, int N, int K, int amode, int bmode, int cin) {
+  int t = pick_tile(M, N, K, bmode, cin);
   return ceil_div(M, tile_bm(t));
 }

@@ -85,7 +85,7 @@ typedef struct AccGemmDesc {
 
 int accunet_gemm(const AccGemmDesc* d, float* ws, size_t ws_elems, void* stream);
 /* number of partial-statistics rows accunet_gemm writes for this shape */
-int accunet_gemm_stats_rows(int M, int N, int amode, int bmode, int cin);
+int accunet_gemm_stats_rows(int M, int N, int K, int amode, int bmode, int cin);
 
 /* ------------------------------------------------------------------------- *
  * BatchNorm2d (training: batch statistics, running-stat update with momentum

@@ -23,7 +23,7 @@ def test_row_nt_bias_stats(M, N, K):
     Wt = torch.randn(N, K, device=DEV)
     b = torch.randn(N, device=DEV)
     C = torch.empty(M, N, device=DEV)
-    rows = kern.gemm_stats_rows(M, N)
+    rows = kern.gemm_stats_rows(M, N, K)
     st = torch.zeros(rows, 2, N, device=DEV, dtype=torch.float64)
     kern.gemm(M, N, K, a=[A], lda=[K], b=Wt, ldb=K, c=C, ldc=N, bias=b, stats=st)
     ref = A.double() @ Wt.double().t() + b.double()
