@@ -32,6 +32,8 @@ typedef void (*gemm_kfn)(const GemmParams);
        gemm_f32_kernel<AM, BMo, PA, PB, true, true, 1, 1, 1, EPI>,                        \
        gemm_f32_kernel<AM, BMo, PA, PB, true, true, 2, 1, 1, EPI>}};
 #define GEMM_DEFINE_TABLE(NAME, AM, BMo, PA, PB) GEMM_DEFINE_TABLE_E(NAME, AM, BMo, PA, PB, 0)
+// forward GEMMs: optional (sum, sumsq) statistics of C for the consumer BatchNorm
+#define GEMM_DEFINE_TABLE_S(NAME, AM, BMo, PA, PB) GEMM_DEFINE_TABLE_E(NAME, AM, BMo, PA, PB, EPI_STATS)
 
 GEMM_DECLARE_TABLE(g_gemm_row_nt_p0)
 GEMM_DECLARE_TABLE(g_gemm_row_nt_p1)

@@ -85,7 +85,7 @@ ACC_DEV float pro_apply(float v, float sc, float sh) {
 // gradients), EPI_PYR fused HANCLayer pyramid backward (pd2/pd4), EPI_UPS
 // nearest-upsampled addends (up[]). A launch whose arguments need a feature must
 // use a table that has it (gemm_run checks).
-enum { EPI_BNB = 1, EPI_PYR = 2, EPI_UPS = 4 };
+enum { EPI_BNB = 1, EPI_PYR = 2, EPI_UPS = 4, EPI_STATS = 8 };  // EPI_STATS: (sum, sumsq) of C
 template <int AMODE, int BMODE, int PRO_A, int PRO_B, bool VA, bool VB, int WM, int TM, int TN,
           int EPI = 0>
 __global__ void __launch_bounds__(GEMM_THREADS)
@@ -668,7 +668,7 @@ gemm_f32_kernel(const GemmParams p) {
               s1[e] += g;
               s2[e] += (double)g * ((double)z - bmu[e]);
             }
-        } else if (!split && p.stats) {
+        } else if ((EPI & EPI_STATS) && !split && p.stats) {
 #pragma unroll
           for (int e = 0; e < 4; ++e)
             if (nq + e < N) {
@@ -688,7 +688,7 @@ gemm_f32_kernel(const GemmParams p) {
     }
   }
 
-  if (!split && p.stats) {
+  if ((EPI & (EPI_STATS | EPI_BNB)) && !split && p.stats) {
     __syncthreads();  // LDS reused as the reduction buffer
     double vv[8] = {s1[0], s1[1], s1[2], s1[3], s2[0], s2[1], s2[2], s2[3]};
     if (block_slot_reduce<CQN, 8, double>(vv, reinterpret_cast<double*>(smem))) {

@@ -48,7 +48,7 @@ splitk_reduce_kernel(const float* __restrict__ ws, float* __restrict__ C, int M,
 static gemm_kfn* table_for(int amode, int bmode, int pro_a, int pro_b, int epi) {
   if (epi & (EPI_BNB | EPI_PYR)) {  // data-gradient epilogues
     if (amode != AM_ROW || bmode != BM_NN || pro_a != PRO_NONE || pro_b != PRO_NONE ||
-        (epi & EPI_UPS))
+        (epi & (EPI_UPS | EPI_STATS)))
       return nullptr;
     if (epi == EPI_BNB) return g_gemm_row_nn_bnb[0];
     if (epi == EPI_PYR) return g_gemm_row_nn_pyr[0];
@@ -63,6 +63,7 @@ static gemm_kfn* table_for(int amode, int bmode, int pro_a, int pro_b, int epi) 
   if (epi & EPI_UPS) return nullptr;  // nearest-up addends: forward 1x1 GEMMs only
   if (amode == AM_SHIFT3 && bmode == BM_NT && pro_a == PRO_NONE && pro_b == PRO_NONE)
     return g_gemm_sh3_nt[0];
+  if (epi & EPI_STATS) return nullptr;  // C statistics: forward tables only
   if (amode == AM_ROW && bmode == BM_NN && pro_a == PRO_NONE && pro_b == PRO_NONE)
     return g_gemm_row_nn[0];
   if (amode == AM_COL && bmode == BM_NN && pro_a == PRO_NONE) {
@@ -130,7 +131,8 @@ int gemm_run(GemmParams p, int amode, int bmode, int pro_a, int pro_b, bool allo
     if (bmode == BM_NN_SHIFT3 && (p.cin & 3)) vec = false;
   }
   if (amode == AM_ROW && p.nsrc == 1) { p.kbeg[0] = 0; p.kbeg[1] = p.K; }
-  const int epi = (p.bz ? EPI_BNB : 0) | (p.pd2 ? EPI_PYR : 0) | (p.nup > 0 ? EPI_UPS : 0);
+  const int epi = (p.bz ? EPI_BNB : 0) | (p.pd2 ? EPI_PYR : 0) | (p.nup > 0 ? EPI_UPS : 0) |
+                  ((p.stats && !p.bz) ? EPI_STATS : 0);
   gemm_kfn* tab = table_v(amode, bmode, pro_a, pro_b, epi, vec ? 1 : 0);
   if (!tab) return ACC_EBADARG;
   int t = pick_tile(p.M, p.N, p.K, bmode, p.cin);
