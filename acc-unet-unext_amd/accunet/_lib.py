@@ -63,13 +63,13 @@ _SIGS = {
     "accunet_bn_finalize": [P, I, I, D, P, P, P, P, P, F, F, I, P, P, P],
     "accunet_affine_act_fwd": [P, P, P, I, P, P, L, I, P, IP, P],
     "accunet_bn_bwd_ws_elems": [L, I],
-    "accunet_bn_bwd": [P, P, P, P, I, I, L, I, P, I, P, P, P, IP, P, S, P],
+    "accunet_bn_bwd": [P, P, P, P, I, I, L, I, P, I, P, P, P, P, S, P],
     "accunet_colsum": [P, L, I, P, P, S, P],
     "accunet_reduce_stats": [P, I, I, P, P, P],
     "accunet_dw3x3_rows": [I, I, I, I],
     "accunet_dw3x3_fwd": [P, P, P, P, P, I, I, P, P, I, I, I, I, P, P, I, P],
-    "accunet_bn_bwd_part_ws_elems": [I, I],
-    "accunet_bn_bwd_part": [P, P, P, P, I, I, L, I, P, I, P, P, P, P, S, P],
+    "accunet_bn_bwd_part_ws_elems": [L, I, I],
+    "accunet_bn_bwd_part": [P, P, P, P, I, I, L, I, P, I, P, P, P, P, P, S, P],
     "accunet_dw3x3_wgrad_ws": [I, I, I, I],
     "accunet_dw3x3_wgrad": [P, P, P, P, I, P, P, I, I, I, I, P, S, P],
     "accunet_hanc_pyramid_fwd": [P, P, P, I, I, I, I, I, I, P, P, P, P, P],
@@ -87,7 +87,7 @@ _SIGS = {
     "accunet_se_stats_rows": [I, I, I],
     "accunet_se_bwd": [P, P, P, P, I, I, I, I, I, P, P, P, I, P, P, P, P, P, P, P, P, P, S, P],
     "accunet_se_bwd_pro": [P, P, P, I, P, I, I, I, I, I, P, P, P, I, P, P, P, P, P, P, P, P, P, P,
-                           P, S, P],
+                           P, P, S, P],
     "accunet_head_fwd": [P, P, P, I, P, L, I, P],
     "accunet_head_ws_elems": [L, I],
     "accunet_head_bwd": [P, P, P, P, I, P, P, P, L, I, P, S, P],
@@ -101,7 +101,7 @@ _SIGS = {
     "accunet_wmerge_bwd": [P, P, P, P, L, P],
 }
 # entry points returning a size/count rather than a status
-_SIZE_FNS = {"accunet_bn_bwd_ws_elems", "accunet_bn_bwd_part_ws_elems","accunet_dw3x3_wgrad_ws", "accunet_se_save_elems", "accunet_se_ws_elems",
+_SIZE_FNS = {"accunet_bn_bwd_ws_elems", "accunet_bn_bwd_part_ws_elems", "accunet_dw3x3_wgrad_ws", "accunet_se_save_elems", "accunet_se_ws_elems",
              "accunet_head_ws_elems", "accunet_loss_ws_elems"}
 
 _lib = None

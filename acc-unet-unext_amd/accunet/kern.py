@@ -159,24 +159,25 @@ def affine_act(x: torch.Tensor, sc, sh, act: int, res, y: torch.Tensor, P: int, 
 
 
 def bn_bwd(x, dy, st, gamma, act: int, training: bool, P: int, C: int, dx, accumulate: bool,
-           dgamma, dbeta, colsum=None):
+           dgamma, dbeta, dsum=None):
+    """BatchNorm(+act) backward; dsum (optional [C]) receives sum_p dx."""
     ws_elems = int(_lib.load().accunet_bn_bwd_ws_elems(int(P), int(C)))
     ws = workspace(ws_elems, x.device)
-    rows = ctypes.c_int(0)
     call("accunet_bn_bwd", _p(x), _p(dy), _p(st), _p(gamma), int(act), 1 if training else 0,
-         int(P), int(C), _p(dx), 1 if accumulate else 0, _p(dgamma), _p(dbeta), _p(colsum),
-         ctypes.byref(rows), _p(ws), ws_elems, _stream())
+         int(P), int(C), _p(dx), 1 if accumulate else 0, _p(dgamma), _p(dbeta), _p(dsum),
+         _p(ws), ws_elems, _stream())
     return ws
 
 
 def bn_bwd_part(x, dy, st, gamma, act: int, training: bool, P: int, C: int, part, R: int, dx,
-                dgamma, dbeta):
-    """BatchNorm backward from producer-side partials part [R][2][C] (fp64)."""
-    ws_elems = int(_lib.load().accunet_bn_bwd_part_ws_elems(int(R), int(C)))
+                dgamma, dbeta, dsum=None):
+    """BatchNorm backward from producer-side partials part [R][2][C] (fp64); dsum
+    (optional [C]) receives sum_p dx."""
+    ws_elems = int(_lib.load().accunet_bn_bwd_part_ws_elems(int(P), int(R), int(C)))
     ws = workspace(ws_elems, x.device)
     call("accunet_bn_bwd_part", _p(x), _p(dy), _p(st), _p(gamma), int(act), 1 if training else 0,
-         int(P), int(C), _p(part), int(R), _p(dx), _p(dgamma), _p(dbeta), _p(ws), ws_elems,
-         _stream())
+         int(P), int(C), _p(part), int(R), _p(dx), _p(dgamma), _p(dbeta), _p(dsum), _p(ws),
+         ws_elems, _stream())
     return ws
 
 
@@ -302,14 +303,14 @@ def se_bwd(z, dout, sc, sh, act, B, HW, C, Cr, w1, w2, gamma, training, save, da
 
 
 def se_bwd_pro(z, dout, pst, act, pgamma, ptraining, B, HW, C, Cr, w1, w2, gamma, training, save,
-               dz, dpgamma, dpbeta, dw1, db1, dw2, db2, dgamma, dbeta):
+               dz, dpgamma, dpbeta, dw1, db1, dw2, db2, dgamma, dbeta, dsum=None):
     """SE backward fused with the backward of its BatchNorm(+act) prologue (pst = [4][C]
     mean, rstd, scale, shift of that BatchNorm): writes dz and the prologue's dgamma/dbeta."""
     n = se_ws_elems(B, HW, C, Cr)
     ws = workspace(n, z.device)
     call("accunet_se_bwd_pro", _p(z), _p(dout), _p(pst), int(act), _p(pgamma),
          1 if ptraining else 0, B, HW, C, Cr, _p(w1), _p(w2), _p(gamma), 1 if training else 0,
-         _p(save), _p(dz), _p(dpgamma), _p(dpbeta), _p(dw1), _p(db1), _p(dw2), _p(db2),
+         _p(save), _p(dz), _p(dpgamma), _p(dpbeta), _p(dsum), _p(dw1), _p(db1), _p(dw2), _p(db2),
          _p(dgamma), _p(dbeta), _p(ws), n, _stream())
     return ws
 

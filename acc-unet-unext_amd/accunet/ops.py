@@ -47,16 +47,44 @@ def _flat_off(t: torch.Tensor, off: int) -> torch.Tensor:
 # Pending BatchNorm(+act)
 # --------------------------------------------------------------------------
 class Pending:
-    """value = act(bn(z)); bn None -> value = z (already materialised)."""
+    """value = act(bn(z)); bn None -> value = z (already materialised).
 
-    __slots__ = ("z", "bn", "act", "part", "rows")
+    bslot: optional _BiasSlot of the convolution that produced z. The consumer's
+    BatchNorm backward fills it with sum_p dz, which is that convolution's bias
+    gradient (z feeds only this BatchNorm), so the producer's backward needs no
+    separate column-sum pass over dz."""
 
-    def __init__(self, z: torch.Tensor, bn=None, act: int = ACT_NONE, part=None, rows: int = 0):
+    __slots__ = ("z", "bn", "act", "part", "rows", "bslot")
+
+    def __init__(self, z: torch.Tensor, bn=None, act: int = ACT_NONE, part=None, rows: int = 0,
+                 bslot=None):
         self.z = z
         self.bn = bn
         self.act = act
         self.part = part
         self.rows = rows
+        self.bslot = bslot
+
+
+class _BiasSlot:
+    """Bias gradient of a producer convolution, written by its consumer's backward."""
+
+    __slots__ = ("t",)
+
+    def __init__(self):
+        self.t = None
+
+
+def _bias_slot(bias, consumer_bn):
+    return _BiasSlot() if (bias is not None and consumer_bn is not None) else None
+
+
+def _take_bias_grad(slot):
+    """the consumer-computed bias gradient, or None (then the producer sums dZ itself)"""
+    if slot is None or slot.t is None:
+        return None
+    t, slot.t = slot.t, None
+    return t
 
     @property
     def shape(self):
@@ -74,6 +102,7 @@ class _Pro:
     st: Optional[torch.Tensor] = None   # [4, C] mean, rstd, scale, shift
     act: int = ACT_NONE
     training: bool = False
+    bslot: object = None  # the producer's _BiasSlot (filled with sum_p dz in backward)
 
 
 def _finalize(p: Pending) -> _Pro:
@@ -93,7 +122,7 @@ def _finalize(p: Pending) -> _Pro:
                      bn.running_var if bn.track_running_stats else None,
                      bn.num_batches_tracked if (training and bn.track_running_stats) else None,
                      mom, bn.eps, training, st)
-    return _Pro(True, st, p.act, training)
+    return _Pro(True, st, p.act, training, p.bslot)
 
 
 def _pro_mode(pro: _Pro) -> int:
@@ -111,7 +140,10 @@ def _pro_bwd(pro: _Pro, z, gamma, dA, need_z=True, need_params=True):
     dz = torch.empty_like(z)
     dg = _empty((C,), z) if need_params else None
     db = _empty((C,), z) if need_params else None
-    kern.bn_bwd(z, dA, pro.st, gamma, pro.act, pro.training, P, C, dz, False, dg, db)
+    dsum = _empty((C,), z) if pro.bslot is not None else None
+    kern.bn_bwd(z, dA, pro.st, gamma, pro.act, pro.training, P, C, dz, False, dg, db, dsum)
+    if dsum is not None:
+        pro.bslot.t = dsum
     return dz, dg, db
 
 
@@ -123,7 +155,10 @@ def _pro_bwd_part(pro: _Pro, z, gamma, dA, part, R):
     dz = torch.empty_like(z)
     dg = _empty((C,), z)
     db = _empty((C,), z)
-    kern.bn_bwd_part(z, dA, pro.st, gamma, pro.act, pro.training, P, C, part, R, dz, dg, db)
+    dsum = _empty((C,), z) if pro.bslot is not None else None
+    kern.bn_bwd_part(z, dA, pro.st, gamma, pro.act, pro.training, P, C, part, R, dz, dg, db, dsum)
+    if dsum is not None:
+        pro.bslot.t = dsum
     return dz, dg, db
 
 
@@ -161,6 +196,7 @@ class _PWCfg:
     ups: List[tuple] = field(default_factory=list)  # (log2f, col_off, ld)
     want_stats: bool = False
     has_bias: bool = True
+    bslot: object = None
 
 
 class _PWConvFn(torch.autograd.Function):
@@ -244,8 +280,10 @@ class _PWConvFn(torch.autograd.Function):
                                       b_shift=pro.st[3] if use_pro else None, allow_split=True))
         dbias = None
         if cfg.has_bias and nig[2]:
-            dbias = _empty((N,), dZ)
-            keep.append(kern.colsum(dZ, P, N, dbias))
+            dbias = _take_bias_grad(cfg.bslot)
+            if dbias is None:
+                dbias = _empty((N,), dZ)
+                keep.append(kern.colsum(dZ, P, N, dbias))
         d_ups = []
         for i, ((lg, off, ld), shp) in enumerate(zip(cfg.ups, ctx.up_shapes)):
             if not nig[5 + cfg.nsrc + i]:
@@ -280,12 +318,12 @@ def pw_conv(srcs: Sequence, weight, bias, *, w_off: int = 0, ups: Sequence = (),
     cfg = _PWCfg(nsrc=len(srcs), src_ch=[s.z.shape[-1] for s in srcs], pro=pro, w_off=w_off,
                  w_ld=w_ld, N=N, B=B, H=H, W=W,
                  ups=[(lg, off, g.shape[-1]) for g, lg, off in ups], want_stats=want_stats,
-                 has_bias=bias is not None)
+                 has_bias=bias is not None, bslot=_bias_slot(bias, consumer_bn))
     pg, pb = _bn_params(srcs[0])
     Z, stats = _PWConvFn.apply(cfg, w2, bias, pg, pb, *[s.z for s in srcs],
                                *[g for g, _, _ in ups])
     return Pending(Z, consumer_bn, ACT_LRELU, stats if want_stats else None,
-                   stats.shape[0] if want_stats else 0)
+                   stats.shape[0] if want_stats else 0, bslot=cfg.bslot)
 
 
 # --------------------------------------------------------------------------
@@ -388,6 +426,7 @@ class _HancCfg:
     C: int
     N: int
     want_stats: bool
+    bslot: object = None
 
 
 class _HancLayerFn(torch.autograd.Function):
@@ -499,8 +538,10 @@ class _HancLayerFn(torch.autograd.Function):
                               pro_b=_pro_mode(pro), b_scale=sc, b_shift=sh, allow_split=True))
         dW = _empty((N, J * C), z)
         kern.group_relayout(dWp, dW, N, C, J, _HANC_ORDER[k], inverse=True)
-        db = _empty((N,), z)
-        keep.append(kern.colsum(dZ, P, N, db))
+        db = _take_bias_grad(cfg.bslot)
+        if db is None:
+            db = _empty((N,), z)
+            keep.append(kern.colsum(dZ, P, N, db))
         if pro.active:
             dz, dg, dbeta = _pro_bwd_part(pro, z, pro_g, dA, part, R)
         else:
@@ -518,11 +559,11 @@ def hanc_layer(x, weight, bias, k: int, *, consumer_bn=None):
     if k >= 2 and (H % (2 if k == 2 else 4) or W % (2 if k == 2 else 4)):
         raise ValueError("HANCLayer: spatial size must be divisible by the pooling factor")
     want = _want_stats(consumer_bn)
-    cfg = _HancCfg(pro, k, B, H, W, C, N, want)
+    cfg = _HancCfg(pro, k, B, H, W, C, N, want, _bias_slot(bias, consumer_bn))
     pg, pb = _bn_params(x)
     Z, stats = _HancLayerFn.apply(cfg, x.z, pg, pb, w2, bias)
     return Pending(Z, consumer_bn, ACT_LRELU, stats if want else None,
-                   stats.shape[0] if want else 0)
+                   stats.shape[0] if want else 0, bslot=cfg.bslot)
 
 
 # --------------------------------------------------------------------------
@@ -642,9 +683,12 @@ class _SEFn(torch.autograd.Function):
             dz = torch.empty_like(z)
             dpg = _empty((C,), z)
             dpb = _empty((C,), z)
+            dsum = _empty((C,), z) if pro.bslot is not None else None
             kern.se_bwd_pro(z, dout, pro.st, pro.act, pro_g, pro.training, B, HW, C, Cr, w1,
                             w2, g, cfg.training, save, dz, dpg, dpb, dw1, db1, dw2, db2, dg,
-                            dbeta)
+                            dbeta, dsum)
+            if dsum is not None:
+                pro.bslot.t = dsum
             return None, dz, dpg, dpb, dw1, db1, dw2, db2, dg, dbeta
         da = torch.empty_like(z)
         kern.se_bwd(z, dout, None, None, pro.act, B, HW, C, Cr, w1, w2, g, cfg.training, save,
@@ -685,6 +729,7 @@ class _C3Cfg:
     Cin: int
     Cout: int
     want_stats: bool
+    bslot: object = None
 
 
 class _Conv3x3Fn(torch.autograd.Function):
@@ -729,8 +774,10 @@ class _Conv3x3Fn(torch.autograd.Function):
                               allow_split=True))
         dW = torch.empty_like(weight)
         kern.permute4(dWr, dW, (Co, Ci, 3, 3), (9 * Ci, 1, 3 * Ci, Ci))
-        db = _empty((Co,), x)
-        keep.append(kern.colsum(dZ, P, Co, db))
+        db = _take_bias_grad(cfg.bslot)
+        if db is None:
+            db = _empty((Co,), x)
+            keep.append(kern.colsum(dZ, P, Co, db))
         return None, dx, dW, db
 
 
@@ -738,10 +785,10 @@ def conv3x3(x: torch.Tensor, weight, bias, *, consumer_bn=None):
     B, H, W, Ci = x.shape
     Co = weight.shape[0]
     want = _want_stats(consumer_bn)
-    cfg = _C3Cfg(B, H, W, Ci, Co, want)
+    cfg = _C3Cfg(B, H, W, Ci, Co, want, _bias_slot(bias, consumer_bn))
     Z, stats = _Conv3x3Fn.apply(cfg, x, weight, bias)
     return Pending(Z, consumer_bn, ACT_LRELU, stats if want else None,
-                   stats.shape[0] if want else 0)
+                   stats.shape[0] if want else 0, bslot=cfg.bslot)
 
 
 # --------------------------------------------------------------------------

@@ -89,6 +89,17 @@ const float* reduce_partials(const float* part, int R, int Wd, float* ws, int* R
   return reduce_partials_t<float>(part, R, Wd, ws, Rout, s);
 }
 
+const double* reduce_partials_d(const double* part, int R, int Wd, double* ws, int* Rout,
+                                hipStream_t s) {
+  return reduce_partials_t<double>(part, R, Wd, ws, Rout, s);
+}
+
+void sum_rows_d_to_f(const double* pr, int rows, int stride, int ncols, float* out,
+                     hipStream_t s) {
+  hipLaunchKernelGGL(sum_rows_d_kernel<float>, dim3(ceil_div(ncols, 64)), dim3(256), 0, s, pr,
+                     rows, stride, ncols, out);
+}
+
 size_t accunet_partials_ws_elems(int R, int Wd) {
   int r1 = ceil_div(R, 32);
   return (size_t)(r1 + ceil_div(r1, 32) + 2) * Wd;
@@ -346,13 +357,15 @@ __global__ void __launch_bounds__(256)
 bn_bwd_apply_kernel(const float* __restrict__ x, const float* __restrict__ dy,
                     const float* __restrict__ st, const float* __restrict__ coef, int act,
                     long P, int C, float* __restrict__ dx, int accumulate,
-                    float* __restrict__ colsum) {
+                    double* __restrict__ colsum) {
   ChanTile t = chan_tile<V>(C);
   long rows_per = (P + gridDim.x - 1) / gridDim.x;
   long r0 = blockIdx.x * rows_per, r1 = min(P, r0 + rows_per);
-  float a[V], b[V];
+  // optional fp64 column sums of the written d: sum_p dx = the bias gradient of the
+  // convolution that produced x (its output feeds only this BatchNorm)
+  double a[V], b[V];
 #pragma unroll
-  for (int j = 0; j < V; ++j) { a[j] = 0.f; b[j] = 0.f; }
+  for (int j = 0; j < V; ++j) { a[j] = 0.0; b[j] = 0.0; }
   if (t.active) {
     float s[V], h[V], k1[V], k2[V], k3[V], mu[V];
 #pragma unroll
@@ -385,7 +398,7 @@ bn_bwd_apply_kernel(const float* __restrict__ x, const float* __restrict__ dy,
             float g = dv[u][j];
             if (act == ACT_LRELU) g *= lrelu_d(xv[u][j] * s[j] + h[j]);
             float d = k1[j] * g + k2[j] * (xv[u][j] - mu[j]) + k3[j];
-            a[j] += d;
+            if (colsum) a[j] += d;
             o[u][j] = accumulate ? o[u][j] + d : d;
           }
           stv<V>(dx + r * C + t.c0, o[u]);
@@ -401,15 +414,23 @@ extern "C" size_t accunet_bn_bwd_ws_elems(long P, int C) {
   return (size_t)nb * 2 * C * 2 + accunet_partials_ws_elems(nb, 2 * C) * 2 + 3 * (size_t)C;
 }
 
+// dsum (optional, [C]): sum over pixels of dx (fp64 partials in the apply pass, reduced
+// after it into the stats workspace, which the finalize no longer needs by then)
+static void bn_dsum_finish(double* part, int nb, int C, double* scratch, float* dsum,
+                           hipStream_t s) {
+  int rows;
+  const double* pr = reduce_partials_t<double>(part, nb, 2 * C, scratch, &rows, s);
+  hipLaunchKernelGGL(sum_rows_d_kernel<float>, dim3(ceil_div(C, 64)), dim3(256), 0, s, pr, rows,
+                     2 * C, C, dsum);
+}
+
 extern "C" int accunet_bn_bwd(const float* x, const float* dy, const float* st,
                               const float* gamma, int act, int training, long P, int C,
                               float* dx, int accumulate, float* dgamma, float* dbeta,
-                              float* colsum, int* colsum_rows, float* ws, size_t ws_elems,
-                              void* stream_) {
+                              float* dsum, float* ws, size_t ws_elems, void* stream_) {
   hipStream_t s = (hipStream_t)stream_;
   int V = (C % 4 == 0) ? 4 : 1;
   int nb = stream_rowblocks(P, C);
-  if (colsum_rows) *colsum_rows = nb;
   dim3 grid(nb, ceil_div(C / V, 64));
   // ws layout (floats): fp64 partials [nb][2][C] | fp64 reduce scratch | coef [3][C]
   size_t part_f = (size_t)nb * 2 * C * 2;
@@ -427,44 +448,60 @@ extern "C" int accunet_bn_bwd(const float* x, const float* dy, const float* st,
   const double* pr = reduce_partials_t<double>(part, nb, 2 * C, scratch, &rows, s);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(C, 64)), dim3(256), 0, s, pr, rows, C,
                      (double)P, st, gamma, training, dgamma, dbeta, coef, 0);
+  double* cpart = dsum ? part : nullptr;  // the reduce partials are consumed by now
   if (V == 4)
     hipLaunchKernelGGL(bn_bwd_apply_kernel<4>, grid, dim3(256), 0, s, x, dy, st, coef, act, P, C,
-                       dx, accumulate, colsum);
+                       dx, accumulate, cpart);
   else
     hipLaunchKernelGGL(bn_bwd_apply_kernel<1>, grid, dim3(256), 0, s, x, dy, st, coef, act, P, C,
-                       dx, accumulate, colsum);
+                       dx, accumulate, cpart);
+  if (dsum) bn_dsum_finish(part, nb, C, scratch, dsum, s);
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 
 // BatchNorm backward whose reduce pass ran in the producer of dy (GEMM / depthwise
 // data-gradient epilogues): part = [R][2][C] (sum g, sum g*(x - mean)).
-extern "C" size_t accunet_bn_bwd_part_ws_elems(int R, int C) {
-  return accunet_partials_ws_elems(R, 2 * C) * 2 + 3 * (size_t)C + 2;
+// coef [3][C] floats, padded to an even count so what follows stays 8-byte aligned
+static size_t bn_coef_floats(int C) { return ((3 * (size_t)C + 1) / 2) * 2; }
+
+// ws (floats): fp64 reduce scratch (R rows) | coef [3][C] (even pad) | fp64 dsum partials
+// [nb][2][C] | fp64 dsum reduce scratch; nb = stream_rowblocks(P, C)
+static size_t bn_bwd_part_ws(long P, int R, int C) {
+  const int nb = stream_rowblocks(P, C);
+  return accunet_partials_ws_elems(R, 2 * C) * 2 + bn_coef_floats(C) + (size_t)nb * 2 * C * 2 +
+         accunet_partials_ws_elems(nb, 2 * C) * 2;
+}
+extern "C" size_t accunet_bn_bwd_part_ws_elems(long P, int R, int C) {
+  return bn_bwd_part_ws(P, R, C);
 }
 
 extern "C" int accunet_bn_bwd_part(const float* x, const float* dy, const float* st,
                                    const float* gamma, int act, int training, long P, int C,
                                    const double* part, int R, float* dx, float* dgamma,
-                                   float* dbeta, float* ws, size_t ws_elems, void* stream_) {
+                                   float* dbeta, float* dsum, float* ws, size_t ws_elems,
+                                   void* stream_) {
   hipStream_t s = (hipStream_t)stream_;
   if (C <= 0 || R <= 0) return ACC_EBADSHAPE;
-  if (ws_elems < accunet_bn_bwd_part_ws_elems(R, C) || ((uintptr_t)ws & 7)) return ACC_EBADARG;
+  if (ws_elems < bn_bwd_part_ws(P, R, C) || ((uintptr_t)ws & 7)) return ACC_EBADARG;
   const int V = (C % 4 == 0) ? 4 : 1;
   const int nb = stream_rowblocks(P, C);
   dim3 grid(nb, ceil_div(C / V, 64));
   const size_t scr_f = accunet_partials_ws_elems(R, 2 * C) * 2;
   double* scratch = reinterpret_cast<double*>(ws);
   float* coef = ws + scr_f;
+  double* cpart = reinterpret_cast<double*>(ws + scr_f + bn_coef_floats(C));
+  double* cscr = cpart + (size_t)nb * 2 * C;
   int rows;
   const double* pr = reduce_partials_t<double>(part, R, 2 * C, scratch, &rows, s);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(C, 64)), dim3(256), 0, s, pr, rows, C,
                      (double)P, st, gamma, training, dgamma, dbeta, coef, 1);
   if (V == 4)
     hipLaunchKernelGGL(bn_bwd_apply_kernel<4>, grid, dim3(256), 0, s, x, dy, st, coef, act, P, C,
-                       dx, 0, nullptr);
+                       dx, 0, dsum ? cpart : nullptr);
   else
     hipLaunchKernelGGL(bn_bwd_apply_kernel<1>, grid, dim3(256), 0, s, x, dy, st, coef, act, P, C,
-                       dx, 0, nullptr);
+                       dx, 0, dsum ? cpart : nullptr);
+  if (dsum) bn_dsum_finish(cpart, nb, C, cscr, dsum, s);
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 

@@ -585,9 +585,16 @@ se_bwd_apply_pro_kernel(const float* __restrict__ z, const float* __restrict__ d
                         const float* __restrict__ alpha, const float* __restrict__ betap,
                         const float* __restrict__ sgate, const float* __restrict__ mean,
                         const float* __restrict__ coef, const float* __restrict__ pcoef,
-                        float* __restrict__ dz) {
+                        float* __restrict__ dz, double* __restrict__ colsum) {
   ChanTile t = chan_tile<V>(g.C);
-  if (!t.active) return;
+  // optional fp64 column sums of dz (the bias gradient of z's producer convolution)
+  double cs[V], cz[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) { cs[j] = 0.0; cz[j] = 0.0; }
+  if (!t.active) {
+    if (colsum) block_chan_reduce2<V>(t, cs, cz, colsum, blockIdx.x, g.C);
+    return;
+  }
   const int C = g.C;
   const int b = blockIdx.x / g.NCH, ch = blockIdx.x % g.NCH;
   long r0 = (long)b * g.HW + ch * g.rows_per;
@@ -635,11 +642,13 @@ se_bwd_apply_pro_kernel(const float* __restrict__ z, const float* __restrict__ d
           float da = A[j] * g2 + Bc[j] * (x * sgv[j] - mu[j]) + Cc[j];
           if (act == ACT_LRELU) da *= lrelu_d(pre);
           d[u][j] = k1[j] * da + k2[j] * (v[u][j] - mu1[j]) + k3[j];
+          if (colsum) cs[j] += d[u][j];
         }
         stv<V>(dz + r * C + t.c0, d[u]);
       }
     }
   }
+  if (colsum) block_chan_reduce2<V>(t, cs, cz, colsum, blockIdx.x, g.C);
 }
 
 // ---------------------------------------------------------------------------
@@ -663,9 +672,15 @@ static size_t se_scratch_floats(int B, int C, int Cr) {
   return ((size_t)B * C * (1 + SE_PRO_NQ) + 2 * (size_t)C + (size_t)B * Cr) * 2;
 }
 
+// + fp64 reduce scratch for the optional dz column sums (accunet_se_bwd_pro dsum)
+static size_t se_dsum_scr_floats(const SeGeom& g) {
+  return accunet_partials_ws_elems(g.B * g.NCH, 2 * g.C) * 2;
+}
+
 extern "C" size_t accunet_se_ws_elems(int B, int HW, int C, int Cr) {
   SeGeom g = se_geom(B, HW, C);
-  return se_part_floats(g) + se_scratch_floats(B, C, Cr) + (size_t)B * C * 3 + 3 * (size_t)C + 4;
+  return se_part_floats(g) + se_scratch_floats(B, C, Cr) + (size_t)B * C * 3 + 3 * (size_t)C + 4 +
+         se_dsum_scr_floats(g);
 }
 
 extern "C" int accunet_se_fwd(const float* z, const float* sc, const float* sh, int act, int B,
@@ -767,7 +782,8 @@ extern "C" int accunet_se_bwd_pro(const float* z, const float* dout, const float
                                   const float* pgamma, int ptraining, int B, int HW, int C,
                                   int Cr, const float* w1, const float* w2, const float* gamma,
                                   int training, const float* save, float* dz, float* dpgamma,
-                                  float* dpbeta, float* dw1, float* db1, float* dw2, float* db2,
+                                  float* dpbeta, float* dsum, float* dw1, float* db1, float* dw2,
+                                  float* db2,
                                   float* dgamma, float* dbeta, float* ws, size_t ws_elems,
                                   void* stream) {
   hipStream_t s = (hipStream_t)stream;
@@ -781,6 +797,8 @@ extern "C" int accunet_se_bwd_pro(const float* z, const float* dout, const float
   double* scratch = reinterpret_cast<double*>(ws + se_part_floats(g));
   float* coef = ws + se_part_floats(g) + se_scratch_floats(B, C, Cr);
   float* pcoef = coef + (size_t)B * C * 3;
+  // dsum scratch after pcoef (3C floats + 4 pad), 8-byte aligned
+  double* dscr = reinterpret_cast<double*>(pcoef + ((3 * (size_t)C + 4 + 1) / 2) * 2);
   const float* alpha = save + se_alpha_offset(B, C, Cr);
   const float* betap = alpha + (size_t)B * C;
   const float* sgate = save + (size_t)B * C * 4 + (size_t)B * Cr;
@@ -797,11 +815,18 @@ extern "C" int accunet_se_bwd_pro(const float* z, const float* dout, const float
   const double* UW = scratch + 2 * (size_t)C + (size_t)B * C + (size_t)B * Cr + 2 * (size_t)B * C;
   hipLaunchKernelGGL(se_pro_coef_kernel, dim3(ceil_div(C, 256)), dim3(256), 0, s, g, Cr, save, UW,
                      coef, pst, pgamma, ptraining, dpgamma, dpbeta, pcoef);
+  // the reduce-pass partials are consumed by the mid kernels: reuse them for dz's column sums
+  double* cpart = dsum ? part : nullptr;
   if (V == 4)
     hipLaunchKernelGGL(se_bwd_apply_pro_kernel<4>, grid, dim3(256), 0, s, z, dout, pst, act, g,
-                       alpha, betap, sgate, mean, coef, pcoef, dz);
+                       alpha, betap, sgate, mean, coef, pcoef, dz, cpart);
   else
     hipLaunchKernelGGL(se_bwd_apply_pro_kernel<1>, grid, dim3(256), 0, s, z, dout, pst, act, g,
-                       alpha, betap, sgate, mean, coef, pcoef, dz);
+                       alpha, betap, sgate, mean, coef, pcoef, dz, cpart);
+  if (dsum) {
+    int rows;
+    const double* pr = reduce_partials_d(cpart, B * g.NCH, 2 * C, dscr, &rows, s);
+    sum_rows_d_to_f(pr, rows, 2 * C, C, dsum, s);
+  }
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }

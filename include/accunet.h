@@ -106,19 +106,20 @@ int accunet_affine_act_fwd(const float* x, const float* sc, const float* sh, int
                            const float* res, float* y, long P, int C, double* stats,
                            int* stats_rows, void* stream);
 size_t accunet_bn_bwd_ws_elems(long P, int C);
+/* dsum (optional, [C]) receives sum_p dx: the bias gradient of the convolution whose
+ * output x feeds only this BatchNorm, without a separate pass over dx. */
 int accunet_bn_bwd(const float* x, const float* dy, const float* st, const float* gamma, int act,
                    int training, long P, int C, float* dx, int accumulate, float* dgamma,
-                   float* dbeta, float* colsum, int* colsum_rows, float* ws, size_t ws_elems,
-                   void* stream);
+                   float* dbeta, float* dsum, float* ws, size_t ws_elems, void* stream);
 /* BatchNorm backward from producer-side partials: part = [R][2][C] (sum g,
  * sum g*(x - mean)) written by a data-gradient epilogue (AccGemmDesc.bz,
  * accunet_dw3x3_fwd bz) -> dgamma, dbeta, dx = k1*g + k2*(x - mean) + k3 in one
  * streaming pass (the reduce pass of accunet_bn_bwd is skipped). */
-size_t accunet_bn_bwd_part_ws_elems(int R, int C);
+size_t accunet_bn_bwd_part_ws_elems(long P, int R, int C);
 int accunet_bn_bwd_part(const float* x, const float* dy, const float* st, const float* gamma,
                         int act, int training, long P, int C, const double* part, int R,
-                        float* dx, float* dgamma, float* dbeta, float* ws, size_t ws_elems,
-                        void* stream);
+                        float* dx, float* dgamma, float* dbeta, float* dsum, float* ws,
+                        size_t ws_elems, void* stream);
 int accunet_colsum(const float* x, long P, int C, float* out, double* ws, size_t ws_elems,
                    void* stream);
 int accunet_reduce_stats(const double* part, int R, int C, double* out2C, double* ws,
@@ -208,11 +209,13 @@ int accunet_se_bwd(const float* z, const float* dout, const float* sc, const flo
  * :183-185, MLFC.bns_mrg :520): pst = that BatchNorm's [4][C] (mean, rstd, scale,
  * shift) block, pgamma its weight, ptraining its mode. Returns dz (gradient w.r.t.
  * the pre-BN input z) and the prologue's dgamma/dbeta directly: 2 read passes over
- * (z, dout) and one write, da is never materialised. */
+ * (z, dout) and one write, da is never materialised. dsum (optional) = sum_p dz, the
+ * bias gradient of z's producer convolution. */
 int accunet_se_bwd_pro(const float* z, const float* dout, const float* pst, int act,
                        const float* pgamma, int ptraining, int B, int HW, int C, int Cr,
                        const float* w1, const float* w2, const float* gamma, int training,
-                       const float* save, float* dz, float* dpgamma, float* dpbeta, float* dw1,
+                       const float* save, float* dz, float* dpgamma, float* dpbeta, float* dsum,
+                       float* dw1,
                        float* db1, float* dw2, float* db2, float* dgamma, float* dbeta, float* ws,
                        size_t ws_elems, void* stream);
 
