@@ -82,6 +82,15 @@ static gemm_kfn* table_v(int amode, int bmode, int pro_a, int pro_b, int epi, in
   return t0 ? t0 + v * TILE_COUNT : nullptr;
 }
 
+static long split_min_tiles() {
+  static long v = -1;
+  if (v < 0) {
+    const char* e = getenv("ACCUNET_SPLIT_MIN_TILES");  // tuning knob
+    v = e ? atol(e) : 256;
+  }
+  return v;
+}
+
 static int smallk_tile() {
   static int v = -2;
   if (v == -2) {
@@ -147,7 +156,7 @@ int gemm_run(GemmParams p, int amode, int bmode, int pro_a, int pro_b, bool allo
   if (allow_split && ws != nullptr && p.bias == nullptr && p.nup == 0 && p.stats == nullptr &&
       p.pd2 == nullptr) {
     long tiles = (long)gx * gy;
-    long target = 1024;
+    long target = tiles >= split_min_tiles() ? 1 : 1024;  // enough tiles: no split, no reduce
     long maxS = p.K / (GEMM_BK * 4);
     long want = (target + tiles - 1) / tiles;
     S = (int)(want < maxS ? want : maxS);

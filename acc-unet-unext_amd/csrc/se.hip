@@ -154,6 +154,7 @@ se_mid_gate_kernel(SeGeom g, int Cr,
     int j = o >> 2, part_i = o & 3;
     float acc = 0.f;
     const float* wr = w1 + (long)j * C;
+    #pragma unroll 8
     for (int c = part_i; c < C; c += 4) acc = fmaf(wr[c], m[c], acc);
     acc += __shfl_xor(acc, 1);
     acc += __shfl_xor(acc, 2);
@@ -167,6 +168,7 @@ se_mid_gate_kernel(SeGeom g, int Cr,
   for (int c = tid; c < C; c += 256) {
     float acc = b2[c];
     const float* wr = w2 + (long)c * Cr;
+    #pragma unroll 8
     for (int j = 0; j < Cr; ++j) acc = fmaf(wr[j], hp[j], acc);
     sv.sg[b * C + c] = 1.f / (1.f + expf(-acc));
   }
@@ -188,6 +190,7 @@ se_mid_bn_kernel(SeGeom g, int Cr, const float* __restrict__ gamma,
   float mu, var;
   if (training) {
     double m1 = 0.0, m2 = 0.0;
+    #pragma unroll 8
     for (int b = 0; b < B; ++b) {
       double s = sv.sg[b * C + c];
       m1 += s * sv.S[b * C + c];
@@ -209,6 +212,7 @@ se_mid_bn_kernel(SeGeom g, int Cr, const float* __restrict__ gamma,
   sv.mean[c] = mu;
   sv.rstd[c] = rs;
   sv.betap[c] = beta[c] - k * mu;
+  #pragma unroll 8
   for (int b = 0; b < B; ++b) sv.alpha[b * C + c] = k * sv.sg[b * C + c];
 }
 
@@ -315,7 +319,7 @@ se_bwd_chan_kernel(SeGeom g, int Cr,
   const double mean = sv.mean[c], rstd = sv.rstd[c];
   double gs = 0.0, gy = 0.0;
   // per-(b,c) T1 = sum g2, T2 = sum g2*a (se_part_sum_kernel)
-  for (int b = 0; b < B; ++b) {
+    for (int b = 0; b < B; ++b) {
     double t1 = T1[b * C + c];
     gs += t1;
     gy += (double)sv.sg[b * C + c] * T2[b * C + c] - mean * t1;
@@ -326,7 +330,7 @@ se_bwd_chan_kernel(SeGeom g, int Cr,
   if (dgamma) dgamma[c] = (float)gy;
   if (dbeta) dbeta[c] = (float)gs;
   const double k = (double)gamma[c] * rstd;
-  for (int b = 0; b < B; ++b) {
+    for (int b = 0; b < B; ++b) {
     double s = sv.sg[b * C + c];
     double t2 = T2[b * C + c];
     double ds;
@@ -356,6 +360,7 @@ se_bwd_sample_kernel(SeGeom g, int Cr, const float* __restrict__ w1,
   for (int o = tid; o < Cr * 4; o += 256) {
     int j = o >> 2, part_i = o & 3;
     double acc = 0.0;
+    #pragma unroll 8
     for (int c = part_i; c < C; c += 4) acc += (double)w2[(long)c * Cr + j] * du[b * C + c];
     acc += __shfl_xor(acc, 1);
     acc += __shfl_xor(acc, 2);
@@ -372,6 +377,7 @@ se_bwd_sample_kernel(SeGeom g, int Cr, const float* __restrict__ w1,
   float* Cc = Bc + (size_t)B * C;
   for (int c = tid; c < C; c += 256) {
     double dm = 0.0;
+    #pragma unroll 8
     for (int j = 0; j < Cr; ++j) dm += (double)w1[(long)j * C + c] * smd[j];
     double k = (double)gamma[c] * sv.rstd[c];
     double s = sv.sg[b * C + c];
@@ -401,22 +407,26 @@ se_bwd_param_kernel(SeGeom g, int Cr, float* __restrict__ save, const double* __
   if (i < nW) {  // dw2[c][j] = sum_b du[b,c] * lrelu(hpre[b,j])
     int c = (int)(i / Cr), j = (int)(i % Cr);
     double acc = 0.0;
+    #pragma unroll 8
     for (int b = 0; b < B; ++b) acc += du[b * C + c] * lrelu(sv.hpre[b * Cr + j]);
     dw2[i] = (float)acc;
   } else if (i < 2 * nW) {  // dw1[j][c] = sum_b dh[b,j] * m[b,c]
     long t = i - nW;
     int j = (int)(t / C), c = (int)(t % C);
     double acc = 0.0;
+    #pragma unroll 8
     for (int b = 0; b < B; ++b) acc += dh[b * Cr + j] * (sv.S[b * C + c] / g.HW);
     dw1[t] = (float)acc;
   } else if (i < 2 * nW + C) {
     int c = (int)(i - 2 * nW);
     double acc = 0.0;
+    #pragma unroll 8
     for (int b = 0; b < B; ++b) acc += du[b * C + c];
     db2[c] = (float)acc;
   } else if (i < 2 * nW + C + Cr) {
     int j = (int)(i - 2 * nW - C);
     double acc = 0.0;
+    #pragma unroll 8
     for (int b = 0; b < B; ++b) acc += dh[b * Cr + j];
     db1[j] = (float)acc;
   }
@@ -553,7 +563,7 @@ se_pro_coef_kernel(SeGeom g, int Cr, const float* __restrict__ save,
   const float* Cc = Bc + BC;
   const double mean = sv.mean[c];
   double sg = 0.0, sgx = 0.0;
-  for (int b = 0; b < B; ++b) {
+    for (int b = 0; b < B; ++b) {
     const long i = (long)b * C + c;
     const double a = A[i], bb = Bc[i], s = sv.sg[i];
     const double cst = (double)Cc[i] - bb * mean;
