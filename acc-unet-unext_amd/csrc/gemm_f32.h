@@ -475,7 +475,9 @@ gemm_f32_kernel(const GemmParams p) {
   constexpr int PR = WM * 32;               // tile rows staged per pass
   constexpr int SC = BN + 4;                // LDS row stride (floats)
   constexpr int NR = PR / RPP;              // rows per thread per pass
-  constexpr int EC = NR < 2 ? NR : 2;       // rows per load chunk
+  // rows per load chunk (more for the gather-heavy data-gradient epilogues)
+  constexpr int ECMAX = (EPI & (EPI_PYR | EPI_BNB)) ? 1 : 2;
+  constexpr int EC = NR < ECMAX ? NR : ECMAX;
   static_assert(PR % RPP == 0, "pass rows must split evenly over the sweeps");
   static_assert(PR * SC <= 2 * BK * SA + 2 * BK * SB, "epilogue staging exceeds the LDS tile");
   static_assert(GEMM_THREADS % CQN == 0, "BN/4 must divide the block");

@@ -187,7 +187,7 @@ int main(int argc, char** argv) {
       float* bw = dalloc(bws);
       report("bn_bwd 16x65536x32 (rd 2 + rd 2 + wr 1)",
              timeit([&] { CA(accunet_bn_bwd(z, dout, stb, g, 1, 1, (long)B * HW, C, da, 0, dg, dbe,
-                                            nullptr, nullptr, bw, bws, 0)); }, iters),
+                                            nullptr, bw, bws, 0)); }, iters),
              5.0 * 4 * n);
     }
     report("K3 se_fwd 16x65536x32 pro",
