@@ -301,14 +301,26 @@ se_bwd_reduce_kernel(const float* __restrict__ z, const float* __restrict__ dout
 //   da = A*g2 + Bc*(a*s - mean) + Cc
 // scratch (fp64): G[C] GY[C] du[B*C] dh[B*Cr] T1[B*C] T2[B*C]
 // part 1: one thread per channel — BN backward sums and du = ds * s * (1 - s)
+// SE_LANES lanes per channel: lane l handles samples b = l, l + SE_LANES, ...; the
+// per-channel sums are reduced with an xor butterfly inside the lane group and lane 0's
+// value is broadcast, so every lane uses identical totals (deterministic).
+#define SE_LANES 16
+ACC_DEV double se_lane_sum(double v) {
+#pragma unroll
+  for (int off = 1; off < SE_LANES; off <<= 1) v += __shfl_xor(v, off);
+  return __shfl(v, (threadIdx.x & 63) & ~(SE_LANES - 1));
+}
+
 __global__ void __launch_bounds__(256)
 se_bwd_chan_kernel(SeGeom g, int Cr,
                    const float* __restrict__ gamma, int training, float* __restrict__ save,
                    float* __restrict__ dgamma, float* __restrict__ dbeta,
                    double* __restrict__ scratch) {
   const int B = g.B, C = g.C;
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = gid / SE_LANES, lane = gid % SE_LANES;
+  const bool live = c < C;  // dead lanes still join the shuffles
+  const int cc = live ? c : 0;
   SeSave sv = se_save_view(save, B, C, Cr);
   double* G = scratch;
   double* GY = G + C;
@@ -316,21 +328,26 @@ se_bwd_chan_kernel(SeGeom g, int Cr,
   const double* T1 = du + (size_t)B * C + (size_t)B * Cr;
   const double* T2 = T1 + (size_t)B * C;
   const double n = (double)B * g.HW;
-  const double mean = sv.mean[c], rstd = sv.rstd[c];
+  const double mean = sv.mean[cc], rstd = sv.rstd[cc];
   double gs = 0.0, gy = 0.0;
   // per-(b,c) T1 = sum g2, T2 = sum g2*a (se_part_sum_kernel)
-    for (int b = 0; b < B; ++b) {
-    double t1 = T1[b * C + c];
-    gs += t1;
-    gy += (double)sv.sg[b * C + c] * T2[b * C + c] - mean * t1;
+  if (live)
+    for (int b = lane; b < B; b += SE_LANES) {
+      double t1 = T1[b * C + c];
+      gs += t1;
+      gy += (double)sv.sg[b * C + c] * T2[b * C + c] - mean * t1;
+    }
+  gs = se_lane_sum(gs);
+  gy = se_lane_sum(gy) * rstd;
+  if (!live) return;
+  if (lane == 0) {
+    G[c] = gs;
+    GY[c] = gy;
+    if (dgamma) dgamma[c] = (float)gy;
+    if (dbeta) dbeta[c] = (float)gs;
   }
-  gy *= rstd;
-  G[c] = gs;
-  GY[c] = gy;
-  if (dgamma) dgamma[c] = (float)gy;
-  if (dbeta) dbeta[c] = (float)gs;
   const double k = (double)gamma[c] * rstd;
-    for (int b = 0; b < B; ++b) {
+  for (int b = lane; b < B; b += SE_LANES) {
     double s = sv.sg[b * C + c];
     double t2 = T2[b * C + c];
     double ds;
@@ -554,22 +571,28 @@ se_pro_coef_kernel(SeGeom g, int Cr, const float* __restrict__ save,
                    int ptraining, float* __restrict__ dpg, float* __restrict__ dpb,
                    float* __restrict__ pcoef) {
   const int B = g.B, C = g.C;
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = gid / SE_LANES, lane = gid % SE_LANES;  // SE_LANES lanes per channel
+  const bool live = c < C;
   SeSave sv = se_save_view(const_cast<float*>(save), B, C, Cr);
   const long BC = (long)B * C;
   const float* A = coef;
   const float* Bc = A + BC;
   const float* Cc = Bc + BC;
-  const double mean = sv.mean[c];
   double sg = 0.0, sgx = 0.0;
-    for (int b = 0; b < B; ++b) {
-    const long i = (long)b * C + c;
-    const double a = A[i], bb = Bc[i], s = sv.sg[i];
-    const double cst = (double)Cc[i] - bb * mean;
-    sg += a * UW[0 * BC + i] + bb * s * UW[1 * BC + i] + cst * UW[2 * BC + i];
-    sgx += a * UW[3 * BC + i] + bb * s * UW[4 * BC + i] + cst * UW[5 * BC + i];
+  if (live) {
+    const double mean = sv.mean[c];
+    for (int b = lane; b < B; b += SE_LANES) {
+      const long i = (long)b * C + c;
+      const double a = A[i], bb = Bc[i], s = sv.sg[i];
+      const double cst = (double)Cc[i] - bb * mean;
+      sg += a * UW[0 * BC + i] + bb * s * UW[1 * BC + i] + cst * UW[2 * BC + i];
+      sgx += a * UW[3 * BC + i] + bb * s * UW[4 * BC + i] + cst * UW[5 * BC + i];
+    }
   }
+  sg = se_lane_sum(sg);
+  sgx = se_lane_sum(sgx);
+  if (!live || lane != 0) return;
   const float rstd1 = pst[BN_RSTD * C + c];
   sgx *= rstd1;  // sum g*xhat
   if (dpg) dpg[c] = (float)sgx;
@@ -742,7 +765,8 @@ static void se_bwd_mid(const SeGeom& g, int Cr, const double* part, int nq, cons
   else
     hipLaunchKernelGGL(se_part_sum_kernel<SE_PRO_NQ>, dim3(ceil_div(C, 64), B), dim3(256), 0, s,
                        part, g, T1);
-  hipLaunchKernelGGL(se_bwd_chan_kernel, dim3(ceil_div(C, 256)), dim3(256), 0, s, g, Cr, gamma,
+  hipLaunchKernelGGL(se_bwd_chan_kernel, dim3(ceil_div((long)C * SE_LANES, 256)), dim3(256), 0, s,
+                     g, Cr, gamma,
                      training, sv, dgamma, dbeta, scratch);
   hipLaunchKernelGGL(se_bwd_sample_kernel, dim3(B), dim3(256), (Cr > 0 ? Cr : 1) * sizeof(double),
                      s, g, Cr, w1, w2, gamma, training, sv, scratch, coef);
@@ -823,7 +847,8 @@ extern "C" int accunet_se_bwd_pro(const float* z, const float* dout, const float
   se_bwd_mid(g, Cr, part, SE_PRO_NQ, w1, w2, gamma, training, sv, scratch, coef, dw1, db1, dw2,
              db2, dgamma, dbeta, s);
   const double* UW = scratch + 2 * (size_t)C + (size_t)B * C + (size_t)B * Cr + 2 * (size_t)B * C;
-  hipLaunchKernelGGL(se_pro_coef_kernel, dim3(ceil_div(C, 256)), dim3(256), 0, s, g, Cr, save, UW,
+  hipLaunchKernelGGL(se_pro_coef_kernel, dim3(ceil_div((long)C * SE_LANES, 256)), dim3(256), 0, s,
+                     g, Cr, save, UW,
                      coef, pst, pgamma, ptraining, dpgamma, dpbeta, pcoef);
   // the reduce-pass partials are consumed by the mid kernels: reuse them for dz's column sums
   double* cpart = dsum ? part : nullptr;
