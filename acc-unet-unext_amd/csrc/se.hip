@@ -6,9 +6,10 @@
 //
 // Forward (K3 "SE gate"), z = pending input, a = act(z*sc1+sh1) (or a = z):
 //   pass 1 (se_reduce): per-(b,c) S = sum_hw a, Q = sum_hw a^2      [reads z once]
-//   mid   (se_mid):    m = S/HW, s = sigmoid(fc2(lrelu(fc1(m)))),
-//                      BN stats of y = a*s derived exactly from (S, Q, s):
-//                        mean = sum_b s*S / n,  E[y^2] = sum_b s^2*Q / n
+//   mid   (se_mid_sample, one block per sample): S, Q from the chunk partials,
+//                      m = S/HW, s = sigmoid(fc2(lrelu(fc1(m))))
+//   mid   (se_mid_bn, one thread per channel): BN stats of y = a*s derived exactly
+//                      from (S, Q, s): mean = sum_b s*S / n,  E[y^2] = sum_b s^2*Q / n
 //                      -> per-(b,c) alpha = gamma*rstd*s, per-c beta' = beta - gamma*rstd*mean
 //   pass 2 (se_apply): out = lrelu(alpha*a + beta')                [reads z, writes out]
 // so neither a nor y = a*s is ever materialised.
@@ -135,20 +136,45 @@ se_part_sum_kernel(const double* __restrict__ part, SeGeom g, double* __restrict
   }
 }
 
-// mid forward, part 1: one block per sample b — the channel means (from the
-// per-(b,c) sums S), fc1 (+LeakyReLU) and fc2 (+sigmoid) of that sample.
+// mid forward, fused per sample (one block per sample b): the chunk partials of b
+// -> S[b,c], Q[b,c] (same fixed summation order as se_part_sum_kernel: 4 chunk
+// groups k = grp mod 4, each in chunk order, then ((g0 + g1) + g2) + g3), then the
+// channel means, fc1 (+LeakyReLU) and fc2 (+sigmoid) of that sample (as
+// the reference gate, :41-45). One launch for the whole per-sample middle step.
 __global__ void __launch_bounds__(256)
-se_mid_gate_kernel(SeGeom g, int Cr,
-                   const float* __restrict__ w1, const float* __restrict__ b1,
-                   const float* __restrict__ w2, const float* __restrict__ b2,
-                   float* __restrict__ save) {
+se_mid_sample_kernel(const double* __restrict__ part, SeGeom g, int Cr,
+                     const float* __restrict__ w1, const float* __restrict__ b1,
+                     const float* __restrict__ w2, const float* __restrict__ b2,
+                     float* __restrict__ save) {
   extern __shared__ __attribute__((aligned(16))) float sm[];  // m[C] | h'[Cr]
+  __shared__ double r[2][4][64];
   const int B = g.B, C = g.C, b = blockIdx.x, tid = threadIdx.x;
   SeSave sv = se_save_view(save, B, C, Cr);
   float* m = sm;
   float* hp = sm + C;
-  for (int c = tid; c < C; c += 256) m[c] = (float)(sv.S[b * C + c] / g.HW);
-  __syncthreads();
+  const int cl = tid & 63, grp = tid >> 6;
+  for (int cb = 0; cb < C; cb += 64) {
+    const int c = cb + cl;
+    double s0 = 0.0, s1 = 0.0;
+    if (c < C) {
+      for (int k = grp; k < g.NCH; k += 4) {
+        const double* pr = part + ((long)(b * g.NCH + k) * 2) * C;
+        s0 += pr[c];
+        s1 += pr[(long)C + c];
+      }
+    }
+    r[0][grp][cl] = s0;
+    r[1][grp][cl] = s1;
+    __syncthreads();
+    if (grp == 0 && c < C) {
+      const double S = ((r[0][0][cl] + r[0][1][cl]) + r[0][2][cl]) + r[0][3][cl];
+      const double Q = ((r[1][0][cl] + r[1][1][cl]) + r[1][2][cl]) + r[1][3][cl];
+      sv.S[b * C + c] = S;
+      sv.Q[b * C + c] = Q;
+      m[c] = (float)(S / g.HW);
+    }
+    __syncthreads();
+  }
   // fc1: 4 threads per output, interleaved over the input channels
   for (int o = tid; o < Cr * 4; o += 256) {
     int j = o >> 2, part_i = o & 3;
@@ -733,11 +759,9 @@ extern "C" int accunet_se_fwd(const float* z, const float* sc, const float* sh, 
     hipLaunchKernelGGL(se_reduce_kernel<4>, grid, dim3(256), 0, s, z, sc, sh, act, g, part);
   else
     hipLaunchKernelGGL(se_reduce_kernel<1>, grid, dim3(256), 0, s, z, sc, sh, act, g, part);
-  // SeSave: S[B*C] then Q[B*C]
-  hipLaunchKernelGGL(se_part_sum_kernel<2>, dim3(ceil_div(C, 64), B), dim3(256), 0, s, part, g,
-                     reinterpret_cast<double*>(save));
-  hipLaunchKernelGGL(se_mid_gate_kernel, dim3(B), dim3(256), (C + Cr) * sizeof(float), s, g, Cr, w1,
-                     b1, w2, b2, save);
+  // S, Q and the gate per sample, then the BN-of-gated statistics per channel
+  hipLaunchKernelGGL(se_mid_sample_kernel, dim3(B), dim3(256), (C + Cr) * sizeof(float), s, part,
+                     g, Cr, w1, b1, w2, b2, save);
   hipLaunchKernelGGL(se_mid_bn_kernel, dim3(ceil_div(C, 256)), dim3(256), 0, s, g, Cr, gamma, beta,
                      rmean, rvar, momentum, eps, training, save, training ? nbt : nullptr);
   const float* alpha = save + se_alpha_offset(B, C, Cr);
