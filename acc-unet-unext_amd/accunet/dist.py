@@ -31,12 +31,31 @@ def init_from_env(backend: Optional[str] = None):
     if world == 1:
         return 0, 1
     if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        # ACCUNET_DIST_BACKEND=gloo runs the same path over gloo (e.g. several ranks
+        # sharing one GPU in tests, where RCCL refuses duplicate devices)
+        backend = os.environ.get("ACCUNET_DIST_BACKEND") or (
+            "nccl" if torch.cuda.is_available() else "gloo")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    if backend == "nccl":
-        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local_device())
     dist.init_process_group(backend=backend)
     return dist.get_rank(), dist.get_world_size()
+
+
+def local_device() -> int:
+    """GPU index of this rank: LOCAL_RANK (modulo the visible devices, so ranks can
+    share a GPU when there are fewer devices than ranks)."""
+    n = torch.cuda.device_count()
+    return int(os.environ.get("LOCAL_RANK", "0")) % max(n, 1)
+
+
+def all_reduce_mean(t: torch.Tensor, group=None):
+    """In-place mean over ranks: RCCL's AVG, or SUM / world on backends without AVG."""
+    if dist.get_backend(group) == "nccl":
+        dist.all_reduce(t, op=dist.ReduceOp.AVG, group=group)
+    else:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        t.div_(dist.get_world_size(group))
 
 
 class GradBucketReducer:

@@ -28,7 +28,9 @@ class FusedAdam(torch.optim.Optimizer):
         # The chunk map depends only on the parameter set; gradient pointers change
         # every step when autograd hands over fresh gradient tensors, so only the
         # pointer table is re-uploaded (pinned, async: no host sync).
-        key = (group_idx, tuple(p.data_ptr() for p in params))
+        # the moment buffers are part of the key: load_state_dict replaces them
+        key = (group_idx, tuple((p.data_ptr(), self.state[p]["exp_avg"].data_ptr(),
+                                 self.state[p]["exp_avg_sq"].data_ptr()) for p in params))
         gkey = tuple(p.grad.data_ptr() for p in params)
         t = self._tables.get(group_idx)
         if t is not None and t[0] == key:

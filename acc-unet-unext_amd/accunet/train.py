@@ -22,6 +22,7 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
+from .dist import all_reduce_mean
 from .loss import WeightedDiceBCE
 from .optim import FusedAdam
 
@@ -130,7 +131,7 @@ class TrainStep:
             self._m.copy_(masks)
         self._g.replay()
         if self.world > 1:
-            dist.all_reduce(self._flat, op=dist.ReduceOp.AVG, group=self.pg)
+            all_reduce_mean(self._flat, self.pg)
         self.opt.step()
         return self._loss
 

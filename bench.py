@@ -99,7 +99,7 @@ def main():
     from accunet.train import TrainStep
 
     rank, world = adist.init_from_env()
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = adist.local_device()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 

@@ -1,0 +1,82 @@
+"""Worker for tests/test_dist_gpu.py: one rank of a world-2 data-parallel run.
+
+Launched by torch.distributed.run with ACCUNET_DIST_BACKEND=gloo so that two ranks
+can share the single GPU of a test box (RCCL refuses two ranks on one device); the
+data-parallel code path is the one bench.py runs over RCCL on a node:
+  1. graph mode: TrainStep(graph=True) = HIP-graph replay + one flat gradient
+     all-reduce (mean) + fused Adam, 3 steps on rank-specific data;
+  2. eager mode: TrainStep with GradBucketReducer (bucketed all-reduce overlapped
+     with backward through post-accumulate-grad hooks), same start, same data.
+Checks: parameters identical on both ranks after each mode (bitwise), both modes
+agree with each other, and the parameters moved.
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "acc-unet-unext_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import accunet_oracle as O  # noqa: E402
+from accunet import dist as adist  # noqa: E402
+from accunet.model import ACC_UNet  # noqa: E402
+from accunet.train import TrainStep  # noqa: E402
+
+
+def flat_params(m):
+    return torch.cat([p.detach().reshape(-1) for p in m.parameters()])
+
+
+def run(mode, sd, data, dev):
+    m = ACC_UNet(3, 1, n_filts=8)
+    m.load_state_dict(sd)
+    m = m.to(dev).train()
+    if mode == "graph":
+        step = TrainStep(m, lr=1e-3, graph=True)
+    else:
+        step = TrainStep(m, lr=1e-3, reducer=adist.GradBucketReducer(m, bucket_mb=0.25))
+    losses = []
+    for x, y in data:
+        losses.append(float(step(x, y)))
+    torch.cuda.synchronize()
+    return flat_params(m), losses
+
+
+def main():
+    rank, world = adist.init_from_env()
+    assert world == 2, world
+    dev = torch.device("cuda", adist.local_device())
+    sd = O.det_state_dict(O.param_spec("canonical", 3, 1, 8), seed=0)
+    m0 = ACC_UNet(3, 1, n_filts=8)
+    m0.load_state_dict(sd)
+    p0 = flat_params(m0).to(dev)
+    g = torch.Generator().manual_seed(1000 + rank)
+    data = [(torch.randn(2, 3, 32, 32, generator=g).to(dev),
+             (torch.rand(2, 1, 32, 32, generator=g) < 0.3).float().to(dev)) for _ in range(3)]
+    out = {}
+    for mode in ("graph", "eager"):
+        p, losses = run(mode, sd, data, dev)
+        other = [torch.empty_like(p) for _ in range(world)]
+        dist.all_gather(other, p)
+        same = bool(torch.equal(other[0], other[1]))
+        moved = float((p - p0).abs().max())
+        out[mode] = (p, losses)
+        print(f"rank {rank} {mode}: losses {losses} ranks-identical {same} moved {moved:.3e}",
+              flush=True)
+        assert same, f"{mode}: parameters differ between ranks"
+        assert moved > 1e-5, f"{mode}: parameters did not move"
+    d = float((out["graph"][0] - out["eager"][0]).abs().max())
+    print(f"rank {rank} graph vs eager max|dp| {d:.3e}", flush=True)
+    assert d < 1e-5, d
+    assert all(abs(a - b) < 1e-5 for a, b in zip(out["graph"][1], out["eager"][1]))
+    dist.barrier()
+    dist.destroy_process_group()
+    if rank == 0:
+        print("DIST_OK", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,49 @@
+"""World-2 data-parallel runs on the GPU box: two ranks share the one
+GPU of a test box over gloo (ACCUNET_DIST_BACKEND=gloo; RCCL refuses two ranks on
+one device), exercising the same HIP-graph + flat all-reduce path and the bucketed
+eager reducer that bench.py drives over RCCL on an 8-GPU node."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(args, timeout=280):
+    env = dict(os.environ, ACCUNET_DIST_BACKEND="gloo", OMP_NUM_THREADS="4")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port())] + args
+    return subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+
+
+@pytest.mark.gpu
+def test_world2_graph_and_bucketed_reducer_agree():
+    r = _run([os.path.join(HERE, "dist_worker.py")])
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "DIST_OK" in r.stdout
+
+
+@pytest.mark.gpu
+def test_world2_bench_line():
+    r = _run(["bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1", "--batch", "2",
+              "--size", "64", "--no-probe"])
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith('{"metric"')]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 4 and d["value"] > 0
+    assert d["scaling"] == "weak" and "cpu_baseline" not in d

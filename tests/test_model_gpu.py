@@ -294,3 +294,42 @@ def test_hip_graph_train_step_equals_eager(variant):
     assert runs[False][0] == runs[True][0], (runs[False][0], runs[True][0])
     for k, v in runs[False][1].items():
         assert torch.equal(v, runs[True][1][k]), k
+
+
+@pytest.mark.parametrize("variant,B,S", [("canonical", 16, 256), ("w", 4, 512)])
+def test_full_size_configs_properties(variant, B, S):
+    """BASELINE configs[1] (canonical, 16x3x256x256) and configs[3] (ACC_UNet_W,
+    4x3x512x512) at full size, where the fp64 oracle is too slow to run: properties
+    that hold at any size. (1) determinism: two training steps from the same state
+    are bit-identical (no float atomics anywhere); (2) probabilities in [0, 1] and
+    every gradient finite; (3) the loss of the HIP forward equals WeightedDiceBCE
+    recomputed in fp64 from the HIP probabilities (loss kernel at full size);
+    (4) three Adam steps on one batch lower the loss."""
+    from accunet.train import TrainStep
+    torch.manual_seed(0)
+    m = M.VARIANTS[variant](3, 1, n_filts=32).to(DEV).train()
+    sd0 = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(B, 3, S, S, generator=g).to(DEV)
+    mask = (torch.rand(B, 1, S, S, generator=g) < 0.3).float().to(DEV)
+    crit = WeightedDiceBCE(0.5, 0.5)
+    grads = []
+    for _ in range(2):
+        m.load_state_dict(sd0)
+        m.zero_grad(set_to_none=True)
+        out = m(x)
+        loss = crit(out, mask)
+        loss.backward()
+        grads.append((out.detach().clone(), float(loss),
+                      [p.grad.detach().clone() for p in m.parameters() if p.grad is not None]))
+    (o1, l1, g1), (o2, l2, g2) = grads
+    assert torch.equal(o1, o2) and l1 == l2
+    assert all(torch.equal(a, b) for a, b in zip(g1, g2))
+    assert float(o1.min()) >= 0.0 and float(o1.max()) <= 1.0
+    assert all(torch.isfinite(a).all() for a in g1)
+    ref = O.dice_bce_loss(o1.double().cpu(), mask.double().cpu())
+    assert abs(l1 - float(ref)) < 1e-5 * max(1.0, abs(float(ref)))
+    m.load_state_dict(sd0)
+    step = TrainStep(m, lr=1e-3, graph=False)
+    losses = [float(step(x, mask)) for _ in range(4)]
+    assert losses[-1] < losses[0], losses
