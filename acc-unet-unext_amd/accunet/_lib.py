@@ -99,6 +99,8 @@ _SIGS = {
     "accunet_dotdiff": [P, P, P, L, P, I, P, P],
     "accunet_wmerge_fwd": [P, P, P, P, L, I, P, P],
     "accunet_wmerge_bwd": [P, P, P, P, L, P],
+    "accunet_image_prep": [P, I, I, I, I, P, P],
+    "accunet_mask_prep": [P, I, I, I, I, I, P, P],
 }
 # entry points returning a size/count rather than a status
 _SIZE_FNS = {"accunet_bn_bwd_ws_elems", "accunet_bn_bwd_part_ws_elems", "accunet_dw3x3_wgrad_ws", "accunet_se_save_elems", "accunet_se_ws_elems",

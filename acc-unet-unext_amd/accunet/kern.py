@@ -363,3 +363,23 @@ def wmerge_fwd(a, b, w, y, P, C, stats=None):
 
 def wmerge_bwd(g, w, da, db, n):
     call("accunet_wmerge_bwd", _p(g), _p(w), _p(da), _p(db), int(n), _stream())
+
+
+def image_prep(raw, N, Hin, Win, S, out):
+    """raw [N,Hin,Win] fp32 planes -> out [N,1,S,S]: INTER_LINEAR resize + z-score."""
+    _check(raw, "image_prep raw")
+    _check(out, "image_prep out")
+    if raw.numel() != N * Hin * Win or out.numel() != N * S * S:
+        raise _lib.AccError("image_prep: shape mismatch")
+    call("accunet_image_prep", _p(raw), N, Hin, Win, S, _p(out), _stream())
+
+
+def mask_prep(raw, dtype_code, N, Hin, Win, S, out):
+    """raw [N,Hin,Win] masks (uint8/bool 0, float32 1, int64 2) -> out fp32 {0,1}
+    [N,1,S,S] (INTER_NEAREST resize + binarise)."""
+    if not raw.is_cuda:
+        raise _lib.AccError("mask_prep: expected a device tensor")
+    _check(out, "mask_prep out")
+    if raw.numel() != N * Hin * Win or out.numel() != N * S * S:
+        raise _lib.AccError("mask_prep: shape mismatch")
+    call("accunet_mask_prep", _p(raw), int(dtype_code), N, Hin, Win, S, _p(out), _stream())

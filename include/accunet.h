@@ -261,6 +261,19 @@ int accunet_wmerge_bwd(const float* g, const float* w, float* da, float* db, lon
 int accunet_dotdiff(const float* g, const float* a, const float* b, long n, float* out,
                     int accumulate, float* ws, void* stream);
 
+/* ------------------------------------------------------------------------- *
+ * Input preparation (csrc/data.hip). Replaces the per-image host work of
+ * ImageToImage2D.__getitem__, Experiments/Load_Dataset.py:453-487, for a whole
+ * batch: image_prep takes N raw channel planes [N][Hin][Win] (fp32) and writes
+ * [N][1][S][S] = z-score((INTER_LINEAR resize to S x S if needed)) with
+ * torch's unbiased std and +1e-8 (:470-472); mask_prep takes N raw masks
+ * (dtype 0 = uint8/bool, 1 = float32, 2 = int64) and writes fp32 {0,1}
+ * (INTER_NEAREST resize, mask > 0, :478-481).
+ * ------------------------------------------------------------------------- */
+int accunet_image_prep(const float* raw, int N, int Hin, int Win, int S, float* out, void* stream);
+int accunet_mask_prep(const void* raw, int dtype, int N, int Hin, int Win, int S, float* out,
+                      void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -467,3 +467,54 @@ def cosine_warm_restarts_lr(base_lr, eta_min, T_0, epoch):
     """CosineAnnealingWarmRestarts.get_lr with T_mult=1, Experiments/utils.py:668-784."""
     t_cur = epoch % T_0
     return eta_min + (base_lr - eta_min) * (1 + math.cos(math.pi * t_cur / T_0)) / 2
+
+
+# --------------------------------------------------------------------------
+# Input pipeline: ImageToImage2D.__getitem__, Experiments/Load_Dataset.py:453-487.
+# cv2 is absent from this image (and the reference pins no fixture for the resize
+# branch): cv2.resize's float rules are restated directly (parity unpinned for
+# the resize branch; the no-resize branch is plain numpy/torch arithmetic).
+# --------------------------------------------------------------------------
+def cv_resize_linear(img: np.ndarray, S: int) -> np.ndarray:
+    """cv2.resize(img, (S, S)) default INTER_LINEAR on float data: source coordinate
+    (d + 0.5) * in / out - 0.5, clamped at 0; the upper neighbour clamped to the last
+    pixel (Load_Dataset.py:465-466)."""
+    H, W = img.shape
+
+    def axis(n_in):
+        f = (np.arange(S, dtype=np.float64) + 0.5) * (n_in / S) - 0.5
+        f = np.maximum(f, 0.0)
+        i0 = np.minimum(np.floor(f).astype(np.int64), n_in - 1)
+        a = np.where(i0 >= n_in - 1, 0.0, f - i0)
+        i1 = np.minimum(i0 + 1, n_in - 1)
+        return i0, i1, a
+
+    y0, y1, ay = axis(H)
+    x0, x1, ax = axis(W)
+    im = img.astype(np.float64)
+    top = im[y0][:, x0] * (1 - ax) + im[y0][:, x1] * ax
+    bot = im[y1][:, x0] * (1 - ax) + im[y1][:, x1] * ax
+    return (top * (1 - ay)[:, None] + bot * ay[:, None]).astype(np.float32)
+
+
+def cv_resize_nearest(m: np.ndarray, S: int) -> np.ndarray:
+    """cv2.resize(..., interpolation=INTER_NEAREST): source index floor(d * in / out)
+    (Load_Dataset.py:478-479)."""
+    H, W = m.shape
+    iy = np.minimum(np.floor(np.arange(S) * (H / S)).astype(np.int64), H - 1)
+    ix = np.minimum(np.floor(np.arange(S) * (W / S)).astype(np.int64), W - 1)
+    return m[iy][:, ix]
+
+
+def load_item(img_raw: np.ndarray, mask_raw: np.ndarray, S: int, channel_idx: int = 0):
+    """Load_Dataset.py:453-487: channel select, resize if needed, per-image z-score
+    (torch mean / unbiased std, + 1e-8), mask resize (nearest) and mask > 0 as int64."""
+    img = img_raw[channel_idx]
+    if img.shape[0] != S:
+        img = cv_resize_linear(img, S)
+    t = torch.from_numpy(np.ascontiguousarray(img[None])).float()
+    t = (t - t.mean()) / (t.std() + 1e-8)
+    m = mask_raw
+    if m.shape[0] != S:
+        m = cv_resize_nearest(m, S)
+    return t, torch.from_numpy((m > 0).astype(np.uint8)).long()
