@@ -80,7 +80,7 @@ def k3_se(B, H, W, C, se_mod, iters=20, device="cuda"):
                     p["fc2.bias"], p["bn.weight"], p["bn.bias"], rm, rv, None, 0.1, 1e-5, True,
                     out, save, None)
     us = _time(run, iters)
-    return _hbm_row("se_reduce+se_part_sum+se_mid+se_apply", f"{B}x{HW}x{C}",
+    return _hbm_row("se_reduce+se_mid_sample+se_mid_bn+se_apply", f"{B}x{HW}x{C}",
                     2.0 * 4 * B * HW * C, us, iters)
 
 
