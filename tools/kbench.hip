@@ -129,6 +129,16 @@ int main(int argc, char** argv) {
     report("K1 dw3x3_fwd 16x256x256x96 pro+stats",
            timeit([&] { CA(accunet_dw3x3_fwd(x, wt, bi, sc, sh, 1, 0, z, st, B, H, W, C, nullptr, nullptr, 0, 0)); }, iters),
            bytes);
+    {  // bit pattern checksum of z and the stats partials (compare kernel variants)
+      std::vector<unsigned> hz(n);
+      std::vector<unsigned long long> hs((size_t)rows * 2 * C);
+      CK(hipMemcpy(hz.data(), z, n * 4, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(hs.data(), st, hs.size() * 8, hipMemcpyDeviceToHost));
+      unsigned long long hh = 1469598103934665603ull;
+      for (unsigned v : hz) hh = (hh ^ v) * 1099511628211ull;
+      for (unsigned long long v : hs) hh = (hh ^ v) * 1099511628211ull;
+      printf("K1 checksum %016llx\n", hh);
+    }
     report("K1 dw3x3_fwd flip (dgrad) no pro/stats",
            timeit([&] { CA(accunet_dw3x3_fwd(x, wt, nullptr, nullptr, nullptr, 0, 1, z, nullptr, B, H, W, C, nullptr, nullptr, 0, 0)); }, iters),
            bytes);
