@@ -101,10 +101,17 @@ _SIGS = {
     "accunet_wmerge_bwd": [P, P, P, P, L, P],
     "accunet_image_prep": [P, I, I, I, I, P, P],
     "accunet_mask_prep": [P, I, I, I, I, I, P, P],
+    "accunet_dwconvk_out_hw": [I, I, I, I, I, I, IP, IP],
+    "accunet_dwconvk_fwd": [P, P, P, P, I, I, I, I, I, I, I, I, I, P],
+    "accunet_dwconvk_dgrad_ws": [I, I, I, I, I, I, I, I, I],
+    "accunet_dwconvk_dgrad": [P, P, P, I, I, I, I, I, I, I, I, I, P, S, P],
+    "accunet_dwconvk_wgrad_ws": [I, I, I, I, I, I, I, I],
+    "accunet_dwconvk_wgrad": [P, P, P, P, I, I, I, I, I, I, I, I, I, P, S, P],
 }
 # entry points returning a size/count rather than a status
 _SIZE_FNS = {"accunet_bn_bwd_ws_elems", "accunet_bn_bwd_part_ws_elems", "accunet_dw3x3_wgrad_ws", "accunet_se_save_elems", "accunet_se_ws_elems",
-             "accunet_head_ws_elems", "accunet_loss_ws_elems"}
+             "accunet_head_ws_elems", "accunet_loss_ws_elems", "accunet_dwconvk_wgrad_ws",
+             "accunet_dwconvk_dgrad_ws"}
 
 _lib = None
 

@@ -383,3 +383,30 @@ def mask_prep(raw, dtype_code, N, Hin, Win, S, out):
     if raw.numel() != N * Hin * Win or out.numel() != N * S * S:
         raise _lib.AccError("mask_prep: shape mismatch")
     call("accunet_mask_prep", _p(raw), int(dtype_code), N, Hin, Win, S, _p(out), _stream())
+
+
+def dwconvk_out_hw(H, W, kh, kw, ph, pw):
+    oh, ow = ctypes.c_int(0), ctypes.c_int(0)
+    call("accunet_dwconvk_out_hw", H, W, kh, kw, ph, pw, ctypes.byref(oh), ctypes.byref(ow))
+    return oh.value, ow.value
+
+
+def dwconvk_fwd(x, w, bias, out, N, C, H, W, kh, kw, ph, pw, replicate):
+    for t, n in ((x, "x"), (w, "weight"), (out, "out")):
+        _check(t, f"dwconvk_fwd {n}")
+    call("accunet_dwconvk_fwd", _p(x), _p(w), _p(bias), _p(out), N, C, H, W, kh, kw, ph, pw,
+         int(replicate), _stream())
+
+
+def dwconvk_dgrad(dy, w, dx, N, C, H, W, kh, kw, ph, pw, replicate):
+    n = _lib.load().accunet_dwconvk_dgrad_ws(N, C, H, W, kh, kw, ph, pw, int(replicate))
+    ws = workspace(n, dy.device)
+    call("accunet_dwconvk_dgrad", _p(dy), _p(w), _p(dx), N, C, H, W, kh, kw, ph, pw,
+         int(replicate), _p(ws), ctypes.c_size_t(ws.numel()), _stream())
+
+
+def dwconvk_wgrad(x, dy, dw, db, N, C, H, W, kh, kw, ph, pw, replicate):
+    n = _lib.load().accunet_dwconvk_wgrad_ws(N, C, H, W, kh, kw, ph, pw)
+    ws = workspace(n, x.device)
+    call("accunet_dwconvk_wgrad", _p(x), _p(dy), _p(dw), _p(db), N, C, H, W, kh, kw, ph, pw,
+         int(replicate), _p(ws), ctypes.c_size_t(ws.numel()), _stream())

@@ -274,6 +274,30 @@ int accunet_image_prep(const float* raw, int N, int Hin, int Win, int S, float* 
 int accunet_mask_prep(const void* raw, int dtype, int N, int Hin, int Win, int S, float* out,
                       void* stream);
 
+/* ------------------------------------------------------------------------- *
+ * Large-kernel depthwise convolution, NCHW fp32 (csrc/dwconvk.hip). Replaces the
+ * reference's native extension kernels/dwconv2d: dwconv2d_fp32 /
+ * dwconv2dbias_fp32 (dwconv2d.cpp:14-28 -> depthwise_fwd/launch.cu:12-80), and
+ * adds the data / weight / bias gradients whose bindings the reference leaves
+ * commented out (dwconv2d.cpp:30-52; Dwconv/dwconv_layer.py:20-31 calls them).
+ * replicate = 1: the reference kernel's clamped tile fill (kernel.cuh:104-115,
+ * window bounded by pad_h in both directions); 0: zero padding (its 3x3 routes).
+ * Output size oH = H - kh + 1 + 2 ph, oW = W - kw + 1 + 2 pw; kh, kw <= 31.
+ * ------------------------------------------------------------------------- */
+int accunet_dwconvk_out_hw(int H, int W, int kh, int kw, int ph, int pw, int* oH, int* oW);
+int accunet_dwconvk_fwd(const float* x, const float* w, const float* bias, float* out, int N,
+                        int C, int H, int W, int kh, int kw, int ph, int pw, int replicate,
+                        void* stream);
+size_t accunet_dwconvk_dgrad_ws(int N, int C, int H, int W, int kh, int kw, int ph, int pw,
+                                int replicate);
+int accunet_dwconvk_dgrad(const float* dy, const float* w, float* dx, int N, int C, int H, int W,
+                          int kh, int kw, int ph, int pw, int replicate, float* ws, size_t ws_elems,
+                          void* stream);
+size_t accunet_dwconvk_wgrad_ws(int N, int C, int H, int W, int kh, int kw, int ph, int pw);
+int accunet_dwconvk_wgrad(const float* x, const float* dy, float* dw, float* db, int N, int C,
+                          int H, int W, int kh, int kw, int ph, int pw, int replicate, float* ws,
+                          size_t ws_elems, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -518,3 +518,29 @@ def load_item(img_raw: np.ndarray, mask_raw: np.ndarray, S: int, channel_idx: in
     if m.shape[0] != S:
         m = cv_resize_nearest(m, S)
     return t, torch.from_numpy((m > 0).astype(np.uint8)).long()
+
+
+# --------------------------------------------------------------------------
+# kernels/dwconv2d (large-kernel depthwise conv, NCHW): depthwise_fwd/launch.cu:12-80
+# and the tile fill of depthwise_fwd/kernel.cuh:77-120 (clamped source indices,
+# window bounded by pad_h in both directions, zero beyond it). The 3x3 routes of
+# the launchers use zero padding (cudnn_convolution / at::conv2d).
+# --------------------------------------------------------------------------
+def dwconvk(x, w, b, ph, pw, replicate):
+    """out[n,c,oh,ow] = b[c] + sum_ij w[c,0,i,j] x[n,c,src(oh-ph+i),src(ow-pw+j)]."""
+    N, C, H, W = x.shape
+    kh, kw = w.shape[2], w.shape[3]
+    oH, oW = H - kh + 1 + 2 * ph, W - kw + 1 + 2 * pw
+    if replicate:
+        rows = torch.arange(-ph, H + ph)
+        cols = torch.arange(-pw, W - 1 + pw + 1)
+        xr = x[:, :, rows.clamp(0, H - 1)][:, :, :, cols.clamp(0, W - 1)]
+        # kernel.cuh:104: beyond pad_h (rows AND columns) the tile holds 0
+        xr = xr * (cols.abs() * 0 + ((cols >= -ph) & (cols <= W - 1 + ph)).to(x.dtype))
+    else:
+        xr = F.pad(x, (pw, pw, ph, ph))
+    out = F.conv2d(xr, w, None, groups=C)
+    assert out.shape[2:] == (oH, oW)
+    if b is not None:
+        out = out + b.view(1, C, 1, 1)
+    return out
