@@ -56,3 +56,9 @@ GEMM_DECLARE_TABLE(g_gemm_col_nnsh3)
 // falls back to no split. Returns ACC_OK or an error code.
 int gemm_run(GemmParams p, int amode, int bmode, int pro_a, int pro_b, bool allow_split,
              float* ws, size_t ws_elems, hipStream_t stream);
+
+// Skinny weight-gradient path (csrc/gemm_skinny.hip): returns the number of
+// [M][N] partial slabs written into ws (to be summed by the split-K reduction),
+// or 0 when the shape does not qualify.
+int gemm_skinny_try(const GemmParams& p, int amode, int bmode, int pro_a, int pro_b, float* ws,
+                    size_t ws_elems, hipStream_t stream);

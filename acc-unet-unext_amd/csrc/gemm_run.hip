@@ -140,6 +140,16 @@ int gemm_run(GemmParams p, int amode, int bmode, int pro_a, int pro_b, bool allo
     if (bmode == BM_NN_SHIFT3 && (p.cin & 3)) vec = false;
   }
   if (amode == AM_ROW && p.nsrc == 1) { p.kbeg[0] = 0; p.kbeg[1] = p.K; }
+  if (allow_split) {
+    const int S = gemm_skinny_try(p, amode, bmode, pro_a, pro_b, ws, ws_elems, stream);
+    if (S > 0) {
+      const long total = (long)p.M * p.N;
+      hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((total + SPLITK_COLS - 1) / SPLITK_COLS)),
+                         dim3(SPLITK_COLS * SPLITK_GROUPS), 0, stream, ws, p.C, p.M, p.N, p.ldc, S,
+                         (size_t)total);
+      return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+    }
+  }
   const int epi = (p.bz ? EPI_BNB : 0) | (p.pd2 ? EPI_PYR : 0) | (p.nup > 0 ? EPI_UPS : 0) |
                   ((p.stats && !p.bz) ? EPI_STATS : 0);
   gemm_kfn* tab = table_v(amode, bmode, pro_a, pro_b, epi, vec ? 1 : 0);

@@ -130,3 +130,36 @@ def test_conv3x3_fwd_dgrad_wgrad(B, H, W, Ci, Co):
               bmode=_lib.BMODE_NN_SHIFT3, c=dw, ldc=9 * Ci, H=H, W=W, cin=Ci, allow_split=True)
     refw = w.grad.permute(0, 2, 3, 1).reshape(Co, 9 * Ci)
     assert rel(dw, refw) < 1e-5
+
+
+@pytest.mark.parametrize("M,N,K,lda,pro_b", [(32, 32, 1 << 20, 32, 0), (32, 32, 100003, 48, 1),
+                                             (32, 96, 40000, 64, 2), (96, 32, 65536, 96, 0),
+                                             (64, 32, 20000, 80, 2), (32, 64, 16384, 32, 1),
+                                             (64, 192, 20000, 80, 2)])
+def test_skinny_weight_gradient_path(M, N, K, lda, pro_b):
+    """csrc/gemm_skinny.hip: AMODE_COL x BMODE_NN with small M, N (multiples of 32, at
+    most 3 tiles; the last case takes the tiled path) and K >= 16384 (the 1x1-conv weight gradients over a batch of
+    pixels), optional affine(+LeakyReLU) prologue on B's columns, ragged K, lda > M.
+    Also bit-reproducible run to run (fixed reduction order)."""
+    torch.manual_seed(3)
+    A = torch.randn(K, lda, device=DEV)
+    B = torch.randn(K, N, device=DEV)
+    sc = torch.rand(N, device=DEV) + 0.5
+    sh = torch.randn(N, device=DEV) * 0.2
+    C = torch.empty(M, N, device=DEV)
+    kw = {}
+    if pro_b:
+        kw = dict(pro_b=pro_b, b_scale=sc, b_shift=sh)
+    kern.gemm(M, N, K, a=[A], lda=[lda], amode=_lib.AMODE_COL, b=B, ldb=N, bmode=_lib.BMODE_NN,
+              c=C, ldc=N, allow_split=True, **kw)
+    Bd = B.double()
+    if pro_b:
+        Bd = Bd * sc.double() + sh.double()
+        if pro_b == 2:
+            Bd = torch.where(Bd > 0, Bd, 0.01 * Bd)
+    ref = A[:, :M].double().t() @ Bd
+    assert rel(C, ref) < 2e-5
+    C2 = torch.empty_like(C)
+    kern.gemm(M, N, K, a=[A], lda=[lda], amode=_lib.AMODE_COL, b=B, ldb=N, bmode=_lib.BMODE_NN,
+              c=C2, ldc=N, allow_split=True, **kw)
+    assert torch.equal(C, C2)
