@@ -102,6 +102,16 @@ _SIGS = {
     "accunet_image_prep": [P, I, I, I, I, P, P],
     "accunet_mask_prep": [P, I, I, I, I, I, P, P],
     "accunet_dwconvk_out_hw": [I, I, I, I, I, I, IP, IP],
+    "accunet_layernorm_rows": [L],
+    "accunet_layernorm_fwd": [P, P, P, P, P, L, I, F, P],
+    "accunet_layernorm_bwd": [P, P, P, P, P, P, P, P, L, I, P],
+    "accunet_gelu_fwd": [P, P, L, P],
+    "accunet_gelu_bwd": [P, P, P, L, P],
+    "accunet_token_shift": [P, P, I, I, I, I, I, I, I, P],
+    "accunet_up2_relu_add_fwd": [P, P, P, P, I, I, I, I, P],
+    "accunet_up2_relu_bwd": [P, P, P, I, I, I, I, P],
+    "accunet_relu": [P, P, P, L, P],
+    "accunet_subsample2": [P, P, I, I, I, I, I, P],
     "accunet_dwconvk_fwd": [P, P, P, P, I, I, I, I, I, I, I, I, I, P],
     "accunet_dwconvk_dgrad_ws": [I, I, I, I, I, I, I, I, I],
     "accunet_dwconvk_dgrad": [P, P, P, I, I, I, I, I, I, I, I, I, P, S, P],

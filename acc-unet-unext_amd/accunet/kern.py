@@ -410,3 +410,51 @@ def dwconvk_wgrad(x, dy, dw, db, N, C, H, W, kh, kw, ph, pw, replicate):
     ws = workspace(n, x.device)
     call("accunet_dwconvk_wgrad", _p(x), _p(dy), _p(dw), _p(db), N, C, H, W, kh, kw, ph, pw,
          int(replicate), _p(ws), ctypes.c_size_t(ws.numel()), _stream())
+
+
+# ----------------------------------------------------------------- UNeXt kernels
+def layernorm_fwd(x, g, b, y, mr, P, C, eps):
+    _check(x, "layernorm x")
+    call("accunet_layernorm_fwd", _p(x), _p(g), _p(b), _p(y), _p(mr), P, C, float(eps), _stream())
+
+
+def layernorm_bwd(x, g, mr, dy, dx, dgb, P, C):
+    """dgb: [2*C] buffer receiving dgamma | dbeta."""
+    R = int(_lib.load().accunet_layernorm_rows(P))
+    part = workspace(R * 2 * C, x.device)
+    call("accunet_layernorm_bwd", _p(x), _p(g), _p(mr), _p(dy), _p(dx), _p(dgb),
+         _p(_flat(dgb, C)), _p(part), P, C, _stream())
+    return part
+
+
+def _flat(t, off):
+    f = t.view(-1)
+    return f.narrow(0, off, f.numel() - off)
+
+
+def gelu_fwd(x, y):
+    call("accunet_gelu_fwd", _p(x), _p(y), x.numel(), _stream())
+
+
+def gelu_bwd(x, dy, dx):
+    call("accunet_gelu_bwd", _p(x), _p(dy), _p(dx), x.numel(), _stream())
+
+
+def token_shift(x, y, B, H, W, C, axis, direction, shift_size=5):
+    call("accunet_token_shift", _p(x), _p(y), B, H, W, C, axis, direction, shift_size, _stream())
+
+
+def up2_relu_add_fwd(x, skip, out, mask, B, H, W, C):
+    call("accunet_up2_relu_add_fwd", _p(x), _p(skip), _p(out), _p(mask), B, H, W, C, _stream())
+
+
+def up2_relu_bwd(dout, mask, dx, B, H, W, C):
+    call("accunet_up2_relu_bwd", _p(dout), _p(mask), _p(dx), B, H, W, C, _stream())
+
+
+def relu(x, dy, y):
+    call("accunet_relu", _p(x), _p(dy), _p(y), x.numel(), _stream())
+
+
+def subsample2(src, dst, B, H, W, C, bwd):
+    call("accunet_subsample2", _p(src), _p(dst), B, H, W, C, int(bwd), _stream())

@@ -298,6 +298,41 @@ int accunet_dwconvk_wgrad(const float* x, const float* dy, float* dw, float* db,
                           int H, int W, int kh, int kw, int ph, int pw, int replicate, float* ws,
                           size_t ws_elems, void* stream);
 
+/* ------------------------------------------------------------------------- *
+ * UNeXt tokenized-MLP model (Experiments/nets/UNext.py), NHWC fp32 = token rows
+ * [B*H*W][C] (csrc/unext.hip). Together with the GEMM (Linear fc1/fc2, 3x3 convs),
+ * the depthwise 3x3 (DWConv :150-161), BatchNorm, max-pool and head entry points
+ * above, these replace every ATen op of UNext.forward (:251-358):
+ *   layernorm   nn.LayerNorm (:181,221,244-248); mr = [P][2] mean, rstd saved;
+ *               backward writes dx and dgamma | dbeta (db must be dg + C);
+ *               part = [accunet_layernorm_rows(P)][2][C] scratch
+ *   gelu        nn.GELU() exact (:49)
+ *   token_shift shiftmlp's pad / chunk / roll / narrow (:86-111), axis 0 = H, 1 = W,
+ *               dir +1 forward, -1 its backward
+ *   up2_relu_*  relu(F.interpolate(x2, bilinear)) (+ skip add) (:313-333); mask = relu
+ *               mask bytes [B][2H][2W][C] for the backward
+ *   relu        F.relu (:257-265): dy == NULL -> y = relu(x); else y = dy * (x > 0)
+ *   subsample2  stride-2 pick of even pixels (OverlapPatchEmbed.proj stride 2, :219);
+ *               H, W = full resolution; bwd = 1 scatters the strided gradient back
+ * ------------------------------------------------------------------------- */
+int accunet_layernorm_rows(long P);
+int accunet_layernorm_fwd(const float* x, const float* g, const float* b, float* y, float* mr,
+                          long P, int C, float eps, void* stream);
+int accunet_layernorm_bwd(const float* x, const float* g, const float* mr, const float* dy,
+                          float* dx, float* dg, float* db, float* part, long P, int C,
+                          void* stream);
+int accunet_gelu_fwd(const float* x, float* y, long n, void* stream);
+int accunet_gelu_bwd(const float* x, const float* dy, float* dx, long n, void* stream);
+int accunet_token_shift(const float* x, float* y, int B, int H, int W, int C, int axis, int dir,
+                        int shift_size, void* stream);
+int accunet_up2_relu_add_fwd(const float* x, const float* skip, float* out, unsigned char* mask,
+                             int B, int H, int W, int C, void* stream);
+int accunet_up2_relu_bwd(const float* dout, const unsigned char* mask, float* dx, int B, int H,
+                         int W, int C, void* stream);
+int accunet_relu(const float* x, const float* dy, float* y, long n, void* stream);
+int accunet_subsample2(const float* src, float* dst, int B, int H, int W, int C, int bwd,
+                       void* stream);
+
 #ifdef __cplusplus
 }
 #endif

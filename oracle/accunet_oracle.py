@@ -221,6 +221,8 @@ def det_state_dict(spec, seed: int = 0) -> "OrderedDict[str, torch.Tensor]":
             v = (1.0 + 0.2 * u) if leaf == "weight" else 0.1 * u
         elif leaf == "W":  # ACC_UNet_W merge weight (zeros in the reference init)
             v = 0.3 + 0.2 * u
+        elif len(shapes[prefix + ".weight"]) == 1:  # LayerNorm affine (UNeXt)
+            v = (1.0 + 0.2 * u) if leaf == "weight" else 0.1 * u
         else:
             wshape = shapes[prefix + ".weight"]
             fi = fan_in(wshape)
@@ -543,4 +545,146 @@ def dwconvk(x, w, b, ph, pw, replicate):
     assert out.shape[2:] == (oH, oW)
     if b is not None:
         out = out + b.view(1, C, 1, 1)
+    return out
+
+
+# --------------------------------------------------------------------------
+# UNeXt (Experiments/nets/UNext.py:26-358), NCHW functional restatement. The
+# reference module imports timm / torchvision (absent here): parity unpinned by
+# reference fixtures; this restatement follows the source line by line.
+# --------------------------------------------------------------------------
+UNEXT_DIMS = (128, 160, 256)  # embed_dims (:231)
+
+
+def _ln_spec(prefix, c, out):
+    out += [(prefix + ".weight", (c,)), (prefix + ".bias", (c,))]
+
+
+def _lin_spec(prefix, cout, cin, out):
+    out += [(prefix + ".weight", (cout, cin)), (prefix + ".bias", (cout,))]
+
+
+def _shifted_block_spec(prefix, dim, out):
+    # shiftedBlock (:166-201): drop_path (Identity), norm2, mlp = shiftmlp(dim, dim)
+    _ln_spec(prefix + ".norm2", dim, out)
+    _lin_spec(prefix + ".mlp.fc1", dim, dim, out)          # shiftmlp.fc1 (:46)
+    _conv_spec(prefix + ".mlp.dwconv.dwconv", dim, dim, 3, 3, out, groups=dim)  # DWConv :150
+    _lin_spec(prefix + ".mlp.fc2", dim, dim, out)          # shiftmlp.fc2 (:50)
+
+
+def unext_param_spec(n_channels: int = 3, n_classes: int = 1):
+    """UNext.__init__ (:231-300) in registration order."""
+    d0, d1, d2 = UNEXT_DIMS
+    out: list = []
+    _conv_spec("encoder1", 16, n_channels, 3, 3, out)
+    _conv_spec("encoder2", 32, 16, 3, 3, out)
+    _conv_spec("encoder3", d0, 32, 3, 3, out)
+    _bn_spec("ebn1", 16, out)
+    _bn_spec("ebn2", 32, out)
+    _bn_spec("ebn3", d0, out)
+    _ln_spec("norm3", d1, out)
+    _ln_spec("norm4", d2, out)
+    _ln_spec("dnorm3", d1, out)
+    _ln_spec("dnorm4", d0, out)
+    _shifted_block_spec("block1.0", d1, out)
+    _shifted_block_spec("block2.0", d2, out)
+    _shifted_block_spec("dblock1.0", d1, out)
+    _shifted_block_spec("dblock2.0", d0, out)
+    _conv_spec("patch_embed3.proj", d1, d0, 3, 3, out)   # OverlapPatchEmbed :219-221
+    _ln_spec("patch_embed3.norm", d1, out)
+    _conv_spec("patch_embed4.proj", d2, d1, 3, 3, out)
+    _ln_spec("patch_embed4.norm", d2, out)
+    _conv_spec("decoder1", d1, d2, 3, 3, out)
+    _conv_spec("decoder2", d0, d1, 3, 3, out)
+    _conv_spec("decoder3", 32, d0, 3, 3, out)
+    _conv_spec("decoder4", 16, 32, 3, 3, out)
+    _conv_spec("decoder5", 16, 16, 3, 3, out)
+    _bn_spec("dbn1", d1, out)
+    _bn_spec("dbn2", d0, out)
+    _bn_spec("dbn3", 32, out)
+    _bn_spec("dbn4", 16, out)
+    _conv_spec("final", n_classes, 16, 1, 1, out)
+    return out
+
+
+def _shift(x, axis, shift_size=5):
+    """shiftmlp's pad / chunk / roll / narrow (:86-93, :104-111), NCHW, axis 2 or 3."""
+    B, C, H, W = x.shape
+    pad = shift_size // 2
+    xn = F.pad(x, (pad, pad, pad, pad), "constant", 0)
+    xs = torch.chunk(xn, shift_size, 1)
+    x_shift = [torch.roll(x_c, sh, axis) for x_c, sh in zip(xs, range(-pad, pad + 1))]
+    x_cat = torch.cat(x_shift, 1)
+    x_cat = torch.narrow(x_cat, 2, pad, H)
+    return torch.narrow(x_cat, 3, pad, W)
+
+
+def _shiftmlp(x, sd, p, H, W):
+    """shiftmlp.forward (:82-118) on tokens (B, N, C)."""
+    B, N, C = x.shape
+    xn = x.transpose(1, 2).reshape(B, C, H, W)
+    xs = _shift(xn, 2).reshape(B, C, H * W).transpose(1, 2)
+    x = F.linear(xs, sd[p + ".fc1.weight"], sd[p + ".fc1.bias"])
+    Ch = x.shape[-1]
+    xd = x.transpose(1, 2).reshape(B, Ch, H, W)
+    xd = F.conv2d(xd, sd[p + ".dwconv.dwconv.weight"], sd[p + ".dwconv.dwconv.bias"], padding=1,
+                  groups=Ch)
+    x = F.gelu(xd.flatten(2).transpose(1, 2))
+    xn = x.transpose(1, 2).reshape(B, Ch, H, W)
+    xs = _shift(xn, 3).reshape(B, Ch, H * W).transpose(1, 2)
+    return F.linear(xs, sd[p + ".fc2.weight"], sd[p + ".fc2.bias"])
+
+
+def _ln(x, sd, p):
+    return F.layer_norm(x, (x.shape[-1],), sd[p + ".weight"], sd[p + ".bias"], 1e-5)
+
+
+def _block(x, sd, p, H, W):
+    """shiftedBlock.forward (:198-201): x + mlp(norm2(x))."""
+    return x + _shiftmlp(_ln(x, sd, p + ".norm2"), sd, p + ".mlp", H, W)
+
+
+def _patch_embed(x, sd, p):
+    """OverlapPatchEmbed.forward (:223-229): conv 3x3 stride 2 pad 1, flatten, LN."""
+    x = F.conv2d(x, sd[p + ".proj.weight"], sd[p + ".proj.bias"], stride=2, padding=1)
+    _, _, H, W = x.shape
+    return _ln(x.flatten(2).transpose(1, 2), sd, p + ".norm"), H, W
+
+
+def unext_forward(sd, x, training=True):
+    """UNext.forward (:302-358); returns sigmoid probabilities for n_classes == 1."""
+    B = x.shape[0]
+    cv = lambda t, n: F.conv2d(t, sd[n + ".weight"], sd[n + ".bias"], padding=1)
+    up = lambda t: F.interpolate(t, scale_factor=(2, 2), mode="bilinear")
+    out = F.relu(F.max_pool2d(bn(cv(x, "encoder1"), sd, "ebn1", training), 2, 2))
+    t1 = out
+    out = F.relu(F.max_pool2d(bn(cv(out, "encoder2"), sd, "ebn2", training), 2, 2))
+    t2 = out
+    out = F.relu(F.max_pool2d(bn(cv(out, "encoder3"), sd, "ebn3", training), 2, 2))
+    t3 = out
+    out, H, W = _patch_embed(out, sd, "patch_embed3")
+    out = _block(out, sd, "block1.0", H, W)
+    out = _ln(out, sd, "norm3").reshape(B, H, W, -1).permute(0, 3, 1, 2)
+    t4 = out
+    out, H, W = _patch_embed(out, sd, "patch_embed4")
+    out = _block(out, sd, "block2.0", H, W)
+    out = _ln(out, sd, "norm4").reshape(B, H, W, -1).permute(0, 3, 1, 2)
+    out = F.relu(up(bn(cv(out, "decoder1"), sd, "dbn1", training)))
+    out = out + t4
+    _, _, H, W = out.shape
+    out = _block(out.flatten(2).transpose(1, 2), sd, "dblock1.0", H, W)
+    out = _ln(out, sd, "dnorm3").reshape(B, H, W, -1).permute(0, 3, 1, 2)
+    out = F.relu(up(bn(cv(out, "decoder2"), sd, "dbn2", training)))
+    out = out + t3
+    _, _, H, W = out.shape
+    out = _block(out.flatten(2).transpose(1, 2), sd, "dblock2.0", H, W)
+    out = _ln(out, sd, "dnorm4").reshape(B, H, W, -1).permute(0, 3, 1, 2)
+    out = F.relu(up(bn(cv(out, "decoder3"), sd, "dbn3", training)))
+    out = out + t2
+    out = F.relu(up(bn(cv(out, "decoder4"), sd, "dbn4", training)))
+    out = out + t1
+    out = F.relu(up(cv(out, "decoder5")))
+    out = F.conv2d(out, sd["final.weight"], sd["final.bias"])
+    if out.shape[1] == 1:
+        out = torch.sigmoid(out)
     return out
