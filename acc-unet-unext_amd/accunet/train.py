@@ -16,6 +16,10 @@ Two execution modes, same arithmetic:
       graph also packs the gradients into one flat buffer, which is all-reduced
       (AVG, RCCL) as ONE 67 MB collective between the replay and the optimizer
       (~0.3 ms on xGMI vs ~120 ms of compute); Adam is one launch.
+      Capture happens on the first call: no autograd graph of an earlier eager
+      step may still be alive then (drop references to its outputs / loss), since
+      PyTorch keeps the stream of every AccumulateGrad node such a graph holds and
+      accumulating through it on the default stream breaks the capture.
 """
 from __future__ import annotations
 

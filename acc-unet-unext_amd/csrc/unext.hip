@@ -20,7 +20,7 @@
 
 // ------------------------------------------------------------------ LayerNorm
 // One wave per token, lane = channel quad (C % 4 == 0, C <= 256).
-#define LN_TOK_PER_BLOCK 16  // 4 waves x 4 tokens
+#define LN_TOK_PER_BLOCK 64  // 4 waves x 16 tokens (fewer gamma/beta partial rows)
 
 ACC_DEV float wave_sum(float v) {
 #pragma unroll

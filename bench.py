@@ -15,6 +15,10 @@ Each step replays one HIP graph holding forward + loss + backward (captured on t
 first call, accunet/train.py), then the RCCL all-reduce (N > 1) and the fused Adam
 launch; --eager launches every kernel from Python instead.
 
+`--model unext` runs BASELINE configs[4] instead: UNeXt (Experiments/nets/UNext.py,
+1.47 M params) at 32 x 3 x 224 x 224 per GPU, same step and line format (no
+roofline probes; accunet/unext.py).
+
 Extra objects on the line:
   roofline     — the HANC depthwise stage (K1, `dw3x3_tile_fwd_kernel` of cnv12,
                  B x 256^2 x 96) re-launched back-to-back at its in-model shape after
@@ -40,6 +44,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 METRIC = "images/sec fwd+bwd, ACC-UNet 3×256×256 bs=16/GPU, 1→8 MI355X"
+METRIC_UNEXT = "images/sec fwd+bwd, UNeXt 3×224×224 bs=32/GPU"
 HBM_PEAK_GBS = 8000.0
 
 
@@ -48,31 +53,38 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=16)
-    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--model", default="acc_unet", choices=["acc_unet", "unext"],
+                    help="acc_unet: the headline (BASELINE configs[1]); unext: configs[4]")
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (16; unext 32)")
+    ap.add_argument("--size", type=int, default=None, help="image size (256; unext 224)")
     ap.add_argument("--variant", default="canonical")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true",
                     help="launch every kernel from Python (default: replay one HIP graph per step)")
     ap.add_argument("--no-probe", action="store_true", help="skip the roofline probes")
-    ap.add_argument("--cpu-sample", type=int, default=3, help="images in the CPU sample")
+    ap.add_argument("--cpu-sample", type=int, default=None,
+                    help="images in the CPU sample (3; unext 16)")
     return ap.parse_args()
 
 
-def cpu_baseline(variant, size, n_img):
+def cpu_baseline(variant, size, n_img, model="acc_unet"):
     """Time the CPU oracle (fwd + loss + bwd) on n_img images of the same workload."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import accunet_oracle as O
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
     torch.set_num_threads(threads)
-    spec = O.param_spec(variant, 3, 1, 32)
+    spec = O.unext_param_spec(3, 1) if model == "unext" else O.param_spec(variant, 3, 1, 32)
     sd = O.det_state_dict(spec, seed=0)
     params = [v.requires_grad_(True) for k, v in sd.items()
               if not k.endswith(("running_mean", "running_var", "num_batches_tracked"))]
     x = O.det_input((n_img, 3, size, size), "bench-cpu-x")
     m = O.det_mask((n_img, 1, size, size), "bench-cpu-mask", p=0.3)
     t0 = time.perf_counter()
-    out = O.forward(sd, x, variant, training=True)
+    if model == "unext":
+        out = O.unext_forward(sd, x, training=True)
+        variant = "UNeXt"
+    else:
+        out = O.forward(sd, x, variant, training=True)
     loss = O.dice_bce_loss(out, m)
     loss.backward()
     dt = time.perf_counter() - t0
@@ -103,8 +115,19 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
+    unext = args.model == "unext"
+    if args.batch is None:
+        args.batch = 32 if unext else 16
+    if args.size is None:
+        args.size = 224 if unext else 256
+    if args.cpu_sample is None:
+        args.cpu_sample = 16 if unext else 3
     torch.manual_seed(0)
-    model = M.VARIANTS[args.variant](3, 1, n_filts=32).to(dev).train()
+    if unext:
+        from accunet.unext import UNext
+        model = UNext(3, 1, img_size=args.size).to(dev).train()
+    else:
+        model = M.VARIANTS[args.variant](3, 1, n_filts=32).to(dev).train()
     if args.eager:
         reducer = adist.GradBucketReducer(model) if world > 1 else None
         step = TrainStep(model, lr=1e-3, reducer=reducer)
@@ -139,7 +162,7 @@ def main():
         dt = float(tt.item())
     imgs = B * world * args.steps
     line = {
-        "metric": METRIC,
+        "metric": METRIC_UNEXT if unext else METRIC,
         "value": imgs / dt,
         "unit": "images/s",
         "n_gpus": world,
@@ -152,9 +175,12 @@ def main():
         "dtype": "fp32",
         "data": "synthetic (x ~ N(0,1), mask ~ Bernoulli(0.3), per-rank seed 1000+rank); "
                 "torch.manual_seed(0) default init",
-        "config": {"workload": f"ACC_UNet {args.variant} fwd+WeightedDiceBCE+bwd+Adam, "
-                               f"{B}x3x{S}x{S} per GPU",
-                   "model": "ACC_UNet (16.77M)" if args.variant == "canonical" else args.variant,
+        "config": {"workload": (f"UNext fwd+WeightedDiceBCE+bwd+Adam, {B}x3x{S}x{S} per GPU"
+                                if unext else
+                                f"ACC_UNet {args.variant} fwd+WeightedDiceBCE+bwd+Adam, "
+                                f"{B}x3x{S}x{S} per GPU"),
+                   "model": ("UNext (1.47M)" if unext else
+                             "ACC_UNet (16.77M)" if args.variant == "canonical" else args.variant),
                    "global_batch": B * world, "per_gpu_batch": B, "image": [3, S, S],
                    "parallelism": f"dp{world}"},
         "final_loss": float(loss.item()),
@@ -163,7 +189,7 @@ def main():
     # dw3x3 over B x 256^2 x 96; cnv92 has the same shape), SURVEY.md 8(d), plus K3
     # (cnv12's SE) and the largest MFMA GEMM, each re-launched back-to-back at its
     # in-model shape right after the timed steps (accunet/probe.py)
-    if not args.no_probe:
+    if not args.no_probe and not unext:
         from accunet import probe
         blk = model.cnv12
         rl = [probe.k1_dw3x3(B, S, S, blk.conv2.weight.shape[0], blk.conv2.weight, blk.conv2.bias),
@@ -185,7 +211,7 @@ def main():
         line["rooflines_in_model"] = prof.rooflines(HBM_PEAK_GBS)
     line["mode"] = "eager" if args.eager else "hipgraph"
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(args.variant, S, args.cpu_sample)
+        line["cpu_baseline"] = cpu_baseline(args.variant, S, args.cpu_sample, args.model)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -184,3 +184,43 @@ def test_unext_train_step_matches_oracle():
     bad = [r for r in rows if not r[4]]
     assert not bad, bad[:8]
     assert abs(float(hip["loss"]) - float(r64["loss"])) < 1e-5
+
+
+@pytest.mark.gpu
+def test_unext_full_size_config_properties():
+    """BASELINE configs[4] at full size (32 x 3 x 224 x 224), where the fp64 oracle is
+    too slow: bit-identical repeated steps, finite gradients, probabilities in [0, 1],
+    the loss kernel equal to WeightedDiceBCE recomputed in fp64 from the HIP output,
+    and three Adam steps on one batch lower the loss."""
+    from accunet.loss import WeightedDiceBCE
+    from accunet.train import TrainStep
+    from accunet.unext import UNext
+    torch.manual_seed(0)
+    m = UNext(3, 1).cuda().train()
+    sd0 = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(32, 3, 224, 224, generator=g).cuda()
+    mask = (torch.rand(32, 1, 224, 224, generator=g) < 0.3).float().cuda()
+    crit = WeightedDiceBCE(0.5, 0.5)
+    runs = []
+    for _ in range(2):
+        m.load_state_dict(sd0)
+        m.zero_grad(set_to_none=True)
+        out = m(x)
+        loss = crit(out, mask)
+        loss.backward()
+        runs.append((out.detach().clone(), float(loss), [p.grad.clone() for p in m.parameters()]))
+    # drop the eager autograd graph before capturing: PyTorch keeps the stream of each
+    # AccumulateGrad node while a graph holding it is alive, and a capture whose
+    # backward accumulates through such a node on the default stream fails
+    del out, loss
+    (o1, l1, g1), (o2, l2, g2) = runs
+    assert torch.equal(o1, o2) and l1 == l2 and all(torch.equal(a, b) for a, b in zip(g1, g2))
+    assert float(o1.min()) >= 0 and float(o1.max()) <= 1
+    assert all(torch.isfinite(a).all() for a in g1)
+    ref = O.dice_bce_loss(o1.double().cpu(), mask.double().cpu())
+    assert abs(l1 - float(ref)) < 1e-5 * max(1.0, abs(float(ref)))
+    m.load_state_dict(sd0)
+    step = TrainStep(m, lr=1e-3, graph=True)
+    losses = [float(step(x, mask)) for _ in range(4)]
+    assert losses[-1] < losses[0], losses
