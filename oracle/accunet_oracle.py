@@ -688,3 +688,15 @@ def unext_forward(sd, x, training=True):
     if out.shape[1] == 1:
         out = torch.sigmoid(out)
     return out
+
+
+def test_image_dice_iou(output, labs):
+    """Experiments/test_model.py:30-38,41-48 (batch of 1): pred = output > 0.5,
+    dice = 2 sum(l p) / (sum l + sum p + 1e-5), iou = jaccard_score(l, p) (0 when both
+    masks are empty: sklearn's zero_division default)."""
+    p = (output.detach().cpu().double().numpy().reshape(-1) > 0.5).astype(np.float32)
+    lab = labs.detach().cpu().double().numpy().reshape(-1).astype(np.float32)
+    dice = 2 * np.sum(lab * p) / (np.sum(lab) + np.sum(p) + 1e-5)
+    inter = np.sum((lab > 0) & (p > 0))
+    union = np.sum((lab > 0) | (p > 0))
+    return float(dice), float(inter / union) if union > 0 else 0.0

@@ -140,3 +140,43 @@ def test_trainer_acc_unet_gpu(tmp_path):
         # the restored optimizer state drives the next HIP Adam step
         tr2.train_one_epoch(train, tr2.start_epoch, training=True)
         assert all(torch.isfinite(p).all() for p in m2.parameters())
+
+
+def test_eval_metrics_match_test_model_restatement():
+    from accunet.evaluate import image_dice_iou
+    g = torch.Generator().manual_seed(9)
+    out = torch.rand(4, 1, 10, 10, generator=g)
+    lab = (torch.rand(4, 10, 10, generator=g) < 0.4).long()
+    lab[0] = 0
+    out[0] = 0.2  # both empty: dice 0 (no numerator smoothing), IoU 0
+    d, i = image_dice_iou(out, lab)
+    for b in range(4):
+        rd, ri = O.test_image_dice_iou(out[b], lab[b])
+        assert abs(float(d[b]) - rd) < 1e-6 and abs(float(i[b]) - ri) < 1e-12
+
+
+@pytest.mark.gpu
+def test_evaluate_acc_unet_gpu(tmp_path):
+    from accunet.evaluate import evaluate, image_dice_iou, load_best
+    from accunet.model import ACC_UNet
+    sd = O.det_state_dict(O.param_spec("canonical", 3, 1, 8), seed=0)
+    m = ACC_UNet(3, 1, n_filts=8).cuda()
+    m.load_state_dict(sd)
+    torch.save({"epoch": 0, "best_model": True, "model": "ACC_UNet", "state_dict": m.state_dict(),
+                "val_loss": 0.0, "val_dice": 0.0, "optimizer": {}},
+               os.path.join(str(tmp_path), "best_model-ACC_UNet.pth.tar"))
+    m2 = load_best(ACC_UNet(3, 1, n_filts=8).cuda(),
+                   os.path.join(str(tmp_path), "best_model-ACC_UNet.pth.tar"))
+    batches = _loader(3, 2, 21, H=32, ch=3)
+    r = evaluate(m2, batches)
+    assert r["n"] == 6 and 0 <= r["dice"] <= 1 and 0 <= r["iou"] <= 1
+    # the same numbers from the oracle metric on the HIP outputs, one image at a time
+    ds, ios = [], []
+    with torch.no_grad():
+        for b, _ in batches:
+            out = m2.eval()(b["image"].cuda())
+            for j in range(out.shape[0]):
+                dd, ii = O.test_image_dice_iou(out[j], b["label"][j])
+                ds.append(dd)
+                ios.append(ii)
+    assert abs(r["dice"] - sum(ds) / 6) < 1e-6 and abs(r["iou"] - sum(ios) / 6) < 1e-9
