@@ -111,6 +111,12 @@ static int pick_tile(int M, int N, int K, int bmode, int cin) {
   else if (N <= 32) t = TILE_C;
   else if (N <= 64) t = TILE_B;
   else t = TILE_A;
+  // too few output tiles to occupy the 256 CUs (small-M layers: UNeXt's 14x14 / 28x28
+  // token stages, ACC-UNet's 16x16 level): 64x64 tiles give 2-4x the workgroups
+  if (t != TILE_D && t != TILE_E && M > 64) {
+    const long tiles = (long)ceil_div(M, tile_bm(t)) * ceil_div(N, tile_bn(t));
+    if (tiles < 128) t = TILE_E;
+  }
   (void)bmode;
   (void)cin;
   return t;

@@ -109,18 +109,33 @@ layernorm_bwd_kernel(const float* __restrict__ x, const float* __restrict__ g,
   }
 }
 
-// out[c] (c < 2C) = sum over R partial rows in order; dgamma = out[0:C], dbeta = out[C:2C]
-__global__ void __launch_bounds__(256)
+// out[c] (c < W) = sum over R partial rows, fixed order: 16 row groups x 64 columns
+// per 1024-thread block, each group with 4 independent accumulators (rows r, r+16,
+// r+32, r+48 of its stride-64 sweep) so the loads are not one dependent chain.
+__global__ void __launch_bounds__(1024)
 colsum_rows_kernel(const float* __restrict__ part, int R, int W, float* __restrict__ out) {
-  __shared__ double red[4][64];
+  __shared__ double red[16][64];
   const int cl = threadIdx.x & 63, gq = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
-  double s = 0.0;
-  if (c < W)
-    for (int r = gq; r < R; r += 4) s += part[(long)r * W + c];
-  red[gq][cl] = s;
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  if (c < W) {
+    int r = gq;
+    for (; r + 48 < R; r += 64) {
+      s0 += part[(long)r * W + c];
+      s1 += part[(long)(r + 16) * W + c];
+      s2 += part[(long)(r + 32) * W + c];
+      s3 += part[(long)(r + 48) * W + c];
+    }
+    for (; r < R; r += 16) s0 += part[(long)r * W + c];
+  }
+  red[gq][cl] = (s0 + s1) + (s2 + s3);
   __syncthreads();
-  if (gq == 0 && c < W) out[c] = (float)(((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl]);
+  if (gq == 0 && c < W) {
+    double t = 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += red[k][cl];
+    out[c] = (float)t;
+  }
 }
 
 // ------------------------------------------------------------------ GELU (exact)
@@ -319,7 +334,7 @@ extern "C" int accunet_layernorm_bwd(const float* x, const float* g, const float
   // columns [0, C) -> dgamma, [C, 2C) -> dbeta (contiguous when dg, db are the halves of
   // one buffer; otherwise two launches)
   if (db == dg + C) {
-    hipLaunchKernelGGL(colsum_rows_kernel, dim3(ceil_div(2 * C, 64)), dim3(256), 0, s, part, R,
+    hipLaunchKernelGGL(colsum_rows_kernel, dim3(ceil_div(2 * C, 64)), dim3(1024), 0, s, part, R,
                        2 * C, dg);
   } else {
     return ACC_EBADARG;
