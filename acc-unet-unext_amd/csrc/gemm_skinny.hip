@@ -1,6 +1,7 @@
 // Skinny weight-gradient GEMM: C[M][N] = sum_k A(m,k) B(k,n) with A column-mode
-// ([K][lda] rows of M values, AMODE_COL) and B row-major ([K][ldb], BMODE_NN), small
-// M and N (multiples of 32, at most 3 output tiles of 32x32) and a huge K (the
+// ([K][lda] rows of M values, AMODE_COL) and B row-major ([K][ldb], BMODE_NN) or the
+// 3x3 tap gather (BMODE_NN_SHIFT3), small M and N (at most 3 output tiles of 32x32,
+// edge tiles masked) and a huge K (the
 // pixels of a batch): the weight gradients of the 1x1 convolutions (dW = X^T dZ)
 // and of narrow layers. The tiled GEMM gives such a shape one output tile and
 // splits K 1024 ways, each split streaming 2 KB operand panels through LDS per
@@ -28,9 +29,13 @@ struct SkinnyParams {
   const float* b_shift;
   int rows_per_block;  // multiple of 8
   float* slabs;        // [gridDim.x][M][N]
+  // BMODE_NN_SHIFT3 (3x3 weight gradient): B(k = pixel, n = tap*cin + ci) =
+  // X[shift_tap(k)*ldb + ci], zero outside the H x W image
+  int H, W, cin;
+  FastDiv fW, fH;
 };
 
-template <int TI, int TJ, int PROB>
+template <int TI, int TJ, int PROB, bool SH3>
 __global__ void __launch_bounds__(256) gemm_skinny_kernel(const SkinnyParams p) {
   __shared__ float red[4][32 * 32];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -40,11 +45,26 @@ __global__ void __launch_bounds__(256) gemm_skinny_kernel(const SkinnyParams p) 
   const int q = p.rows_per_block / 4;  // rows per wave (even)
   const long k0 = kb + (long)wave * q, k1 = min(kend, k0 + q);
   float bs[TJ], bh[TJ];
+  bool nok[TJ];
+  int boff[TJ], bdh[TJ], bdw[TJ];  // SH3: per-lane tap offset (constant over k)
 #pragma unroll
   for (int j = 0; j < TJ; ++j) {
-    bs[j] = PROB != PRO_NONE ? p.b_scale[j * 32 + l31] : 1.f;
-    bh[j] = PROB != PRO_NONE ? p.b_shift[j * 32 + l31] : 0.f;
+    const int n = j * 32 + l31;
+    nok[j] = n < p.N;
+    bs[j] = (PROB != PRO_NONE && nok[j]) ? p.b_scale[n] : 1.f;
+    bh[j] = (PROB != PRO_NONE && nok[j]) ? p.b_shift[n] : 0.f;
+    boff[j] = n;
+    bdh[j] = bdw[j] = 0;
+    if (SH3) {
+      const int tap = nok[j] ? n / p.cin : 0, ci = nok[j] ? n - tap * p.cin : 0;
+      bdh[j] = tap / 3 - 1;
+      bdw[j] = tap - (tap / 3) * 3 - 1;
+      boff[j] = (bdh[j] * p.W + bdw[j]) * p.ldb + ci;
+    }
   }
+  bool mok[TI];
+#pragma unroll
+  for (int i = 0; i < TI; ++i) mok[i] = i * 32 + l31 < p.M;
   floatx16 acc[TI][TJ];
 #pragma unroll
   for (int i = 0; i < TI; ++i)
@@ -59,13 +79,23 @@ __global__ void __launch_bounds__(256) gemm_skinny_kernel(const SkinnyParams p) 
       const long kk = k + 2 * u + lh;
       const bool ok = kk < k1;
       const float* ar = p.A + kk * p.lda + l31;
-      const float* br = p.B + kk * p.ldb + l31;
 #pragma unroll
-      for (int i = 0; i < TI; ++i) a[u][i] = ok ? ar[i * 32] : 0.f;
+      for (int i = 0; i < TI; ++i) a[u][i] = (ok && mok[i]) ? ar[i * 32] : 0.f;
+      int hh = 0, ww = 0;
+      if (SH3 && ok) {
+        const uint32_t q = fdiv((uint32_t)kk, p.fW);
+        ww = (int)kk - (int)q * p.W;
+        hh = (int)(q - fdiv(q, p.fH) * p.H);
+      }
+      const float* br = p.B + kk * p.ldb;
 #pragma unroll
       for (int j = 0; j < TJ; ++j) {
-        float v = ok ? br[j * 32] : 0.f;
-        if (PROB != PRO_NONE && ok) v = pro_apply<PROB>(v, bs[j], bh[j]);
+        bool in = ok && nok[j];
+        if (SH3)
+          in = in && hh + bdh[j] >= 0 && hh + bdh[j] < p.H && ww + bdw[j] >= 0 &&
+               ww + bdw[j] < p.W;
+        float v = in ? br[boff[j]] : 0.f;
+        if (PROB != PRO_NONE && in) v = pro_apply<PROB>(v, bs[j], bh[j]);
         b[u][j] = v;
       }
     }
@@ -88,8 +118,9 @@ __global__ void __launch_bounds__(256) gemm_skinny_kernel(const SkinnyParams p) 
         red[wave][((r & 3) + 8 * (r >> 2) + 4 * lh) * 32 + l31] = acc[i][j][r];
       __syncthreads();
       for (int e = tid; e < 1024; e += 256) {
+        const int m = i * 32 + (e >> 5), n = j * 32 + (e & 31);
         const float s = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
-        slab[(size_t)(i * 32 + (e >> 5)) * p.N + j * 32 + (e & 31)] = s;
+        if (m < p.M && n < p.N) slab[(size_t)m * p.N + n] = s;
       }
       __syncthreads();
     }
@@ -97,10 +128,10 @@ __global__ void __launch_bounds__(256) gemm_skinny_kernel(const SkinnyParams p) 
 
 typedef void (*skinny_kfn)(const SkinnyParams);
 
-template <int PROB>
+template <int PROB, bool SH3>
 static skinny_kfn skinny_pick(int TI, int TJ) {
 #define SK_CASE(I, J) \
-  if (TI == I && TJ == J) return gemm_skinny_kernel<I, J, PROB>;
+  if (TI == I && TJ == J) return gemm_skinny_kernel<I, J, PROB, SH3>;
   SK_CASE(1, 1) SK_CASE(1, 2) SK_CASE(2, 1) SK_CASE(1, 3) SK_CASE(3, 1)
 #undef SK_CASE
   return nullptr;
@@ -115,17 +146,21 @@ int gemm_skinny_try(const GemmParams& p, int amode, int bmode, int pro_a, int pr
     const char* e = getenv("ACCUNET_NO_SKINNY");  // A/B knob
     off = (e && atoi(e)) ? 1 : 0;
   }
-  if (off || amode != AM_COL || bmode != BM_NN || pro_a != PRO_NONE || p.nsrc != 1) return 0;
+  const bool sh3 = bmode == BM_NN_SHIFT3;
+  if (off || amode != AM_COL || (bmode != BM_NN && !sh3) || pro_a != PRO_NONE || p.nsrc != 1)
+    return 0;
+  if (sh3 && pro_b != PRO_NONE) return 0;
   if (p.bias || p.nup || p.stats || p.pd2 || p.bz || !ws) return 0;
-  if ((p.M & 31) || (p.N & 31) || p.K < 16384) return 0;
-  const int TI = p.M / 32, TJ = p.N / 32;
+  if (p.K < 16384) return 0;
+  const int TI = (p.M + 31) / 32, TJ = (p.N + 31) / 32;  // edge tiles masked
   // measured (tools/gemm_census.py): a clear win while the stream dominates (up to 3
   // output tiles: 32x32 2.1x, 32x96 / 96x32 faster); from 4 tiles the MFMA work per
   // K pair makes the tiled kernel equal or better (64x64 at K 262144: 40 vs 36 us)
   if (TI * TJ > 3) return 0;
-  skinny_kfn fn = pro_b == PRO_NONE ? skinny_pick<PRO_NONE>(TI, TJ)
-                  : pro_b == PRO_AFFINE ? skinny_pick<PRO_AFFINE>(TI, TJ)
-                                        : skinny_pick<PRO_AFFINE_LRELU>(TI, TJ);
+  skinny_kfn fn = sh3 ? skinny_pick<PRO_NONE, true>(TI, TJ)
+                  : pro_b == PRO_NONE ? skinny_pick<PRO_NONE, false>(TI, TJ)
+                  : pro_b == PRO_AFFINE ? skinny_pick<PRO_AFFINE, false>(TI, TJ)
+                                        : skinny_pick<PRO_AFFINE_LRELU, false>(TI, TJ);
   if (!fn) return 0;
   // blocks: ~4 per CU for the stream, fewer if the slabs would not fit ws
   long nb = 1024;
@@ -142,6 +177,8 @@ int gemm_skinny_try(const GemmParams& p, int amode, int bmode, int pro_a, int pr
   s.b_scale = p.b_scale; s.b_shift = p.b_shift;
   s.rows_per_block = (int)rows;
   s.slabs = ws;
+  s.H = p.H; s.W = p.W; s.cin = p.cin;
+  s.fW = p.fW; s.fH = p.fH;
   hipLaunchKernelGGL(fn, dim3((unsigned)nb), dim3(256), 0, stream, s);
   return (int)nb;
 }

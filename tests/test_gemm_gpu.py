@@ -163,3 +163,34 @@ def test_skinny_weight_gradient_path(M, N, K, lda, pro_b):
     kern.gemm(M, N, K, a=[A], lda=[lda], amode=_lib.AMODE_COL, b=B, ldb=N, bmode=_lib.BMODE_NN,
               c=C2, ldc=N, allow_split=True, **kw)
     assert torch.equal(C, C2)
+
+
+@pytest.mark.parametrize("M,N,K", [(9, 3, 100000), (48, 40, 50000), (16, 27, 65536)])
+def test_skinny_masked_edges(M, N, K):
+    """Skinny path with M, N not multiples of 32 (edge tiles masked)."""
+    torch.manual_seed(4)
+    A = torch.randn(K, M, device=DEV)
+    B = torch.randn(K, N, device=DEV)
+    C = torch.empty(M, N, device=DEV)
+    kern.gemm(M, N, K, a=[A], lda=[M], amode=_lib.AMODE_COL, b=B, ldb=N, bmode=_lib.BMODE_NN,
+              c=C, ldc=N, allow_split=True)
+    assert rel(C, A.double().t() @ B.double()) < 2e-5
+
+
+@pytest.mark.parametrize("Bn,H,W,Co,Ci", [(8, 64, 64, 16, 3), (4, 48, 40, 32, 1), (2, 128, 96, 24, 2)])
+def test_skinny_shift3_weight_gradient(Bn, H, W, Co, Ci):
+    """Skinny path for the 3x3 weight gradient (BMODE_NN_SHIFT3, <= 3 output tiles):
+    dW[co][tap*Ci + ci] = sum_p dZ[p][co] * X[shift_tap(p)][ci] vs torch's conv2d
+    weight gradient."""
+    torch.manual_seed(5)
+    P = Bn * H * W
+    X = torch.randn(Bn, H, W, Ci, device=DEV)
+    dZ = torch.randn(Bn, H, W, Co, device=DEV)
+    C = torch.empty(Co, 9 * Ci, device=DEV)
+    kern.gemm(Co, 9 * Ci, P, a=[dZ], lda=[Co], amode=_lib.AMODE_COL, b=X, ldb=Ci,
+              bmode=_lib.BMODE_NN_SHIFT3, c=C, ldc=9 * Ci, H=H, W=W, cin=Ci, allow_split=True)
+    xd = X.double().permute(0, 3, 1, 2).cpu()
+    gd = dZ.double().permute(0, 3, 1, 2).cpu()
+    wref = torch.nn.grad.conv2d_weight(xd, (Co, Ci, 3, 3), gd, padding=1)  # [co][ci][kh][kw]
+    ref = wref.permute(0, 2, 3, 1).reshape(Co, 9 * Ci)  # [co][tap][ci]
+    assert rel(C.cpu(), ref) < 2e-5
