@@ -100,7 +100,7 @@ static int smallk_tile() {
   return v;
 }
 
-static int pick_tile(int M, int N, int K, int bmode, int cin) {
+static int pick_tile(int M, int N, int K, int bmode, int cin, bool can_split) {
   int t;
   // short-K GEMMs over many pixels (1x1 data gradients, K = the forward's N <= 64):
   // epilogue-dominated, so smaller tiles (more resident waves to hide its gathers)
@@ -112,8 +112,10 @@ static int pick_tile(int M, int N, int K, int bmode, int cin) {
   else if (N <= 64) t = TILE_B;
   else t = TILE_A;
   // too few output tiles to occupy the 256 CUs (small-M layers: UNeXt's 14x14 / 28x28
-  // token stages, ACC-UNet's 16x16 level): 64x64 tiles give 2-4x the workgroups
-  if (t != TILE_D && t != TILE_E && M > 64) {
+  // token stages, ACC-UNet's 16x16 level): 64x64 tiles give 2-4x the workgroups.
+  // Not for split-K GEMMs (weight gradients): their K split already fills the chip
+  // and the larger tile needs fewer operand loads per MFMA.
+  if (!can_split && t != TILE_D && t != TILE_E && M > 64) {
     const long tiles = (long)ceil_div(M, tile_bm(t)) * ceil_div(N, tile_bn(t));
     if (tiles < 128) t = TILE_E;
   }
@@ -160,7 +162,9 @@ int gemm_run(GemmParams p, int amode, int bmode, int pro_a, int pro_b, bool allo
                   ((p.stats && !p.bz) ? EPI_STATS : 0);
   gemm_kfn* tab = table_v(amode, bmode, pro_a, pro_b, epi, vec ? 1 : 0);
   if (!tab) return ACC_EBADARG;
-  int t = pick_tile(p.M, p.N, p.K, bmode, p.cin);
+  const bool can_split = allow_split && ws != nullptr && p.bias == nullptr && p.nup == 0 &&
+                         p.stats == nullptr && p.pd2 == nullptr;
+  int t = pick_tile(p.M, p.N, p.K, bmode, p.cin, can_split);
   int BM = tile_bm(t), BN = tile_bn(t);
   int gx = ceil_div(p.M, BM), gy = ceil_div(p.N, BN);
 
@@ -265,6 +269,6 @@ extern "C" int accunet_gemm(const AccGemmDesc* d, float* ws, size_t ws_elems, vo
 }
 
 extern "C" int accunet_gemm_stats_rows(int M, int N, int K, int amode, int bmode, int cin) {
-  int t = pick_tile(M, N, K, bmode, cin);
+  int t = pick_tile(M, N, K, bmode, cin, false);  // statistics GEMMs never split
   return ceil_div(M, tile_bm(t));
 }
