@@ -155,7 +155,8 @@ int gemm_skinny_try(const GemmParams& p, int amode, int bmode, int pro_a, int pr
   const int TI = (p.M + 31) / 32, TJ = (p.N + 31) / 32;  // edge tiles masked
   // measured (tools/gemm_census.py): a clear win while the stream dominates (up to 3
   // output tiles: 32x32 2.1x, 32x96 / 96x32 faster); from 4 tiles the MFMA work per
-  // K pair makes the tiled kernel equal or better (64x64 at K 262144: 40 vs 36 us)
+  // K pair makes the tiled kernel equal or better (64x64 at K 262144: 40 vs 36 us;
+  // the 32 x 288 3x3 weight gradient as 1 x 9 tiles: 539 vs 361 us)
   if (TI * TJ > 3) return 0;
   skinny_kfn fn = sh3 ? skinny_pick<PRO_NONE, true>(TI, TJ)
                   : pro_b == PRO_NONE ? skinny_pick<PRO_NONE, false>(TI, TJ)

@@ -177,7 +177,8 @@ def test_skinny_masked_edges(M, N, K):
     assert rel(C, A.double().t() @ B.double()) < 2e-5
 
 
-@pytest.mark.parametrize("Bn,H,W,Co,Ci", [(8, 64, 64, 16, 3), (4, 48, 40, 32, 1), (2, 128, 96, 24, 2)])
+@pytest.mark.parametrize("Bn,H,W,Co,Ci", [(8, 64, 64, 16, 3), (4, 48, 40, 32, 1), (2, 128, 96, 24, 2),
+                                           (4, 64, 96, 32, 32)])
 def test_skinny_shift3_weight_gradient(Bn, H, W, Co, Ci):
     """Skinny path for the 3x3 weight gradient (BMODE_NN_SHIFT3, <= 3 output tiles):
     dW[co][tap*Ci + ci] = sum_p dZ[p][co] * X[shift_tap(p)][ci] vs torch's conv2d
