@@ -476,7 +476,9 @@ gemm_f32_kernel(const GemmParams p) {
   constexpr int SC = BN + 4;                // LDS row stride (floats)
   constexpr int NR = PR / RPP;              // rows per thread per pass
   // rows per load chunk (more for the gather-heavy data-gradient epilogues)
-  constexpr int ECMAX = (EPI & (EPI_PYR | EPI_BNB)) ? 1 : 2;
+  // (2-row chunks pay for the pyramid gathers of the 128-row tiles; the 64x64 small-K
+  // tiles keep 1 for occupancy: tools/gemm_census.py)
+  constexpr int ECMAX = ((EPI & EPI_PYR) && TM == 2) ? 2 : (EPI & (EPI_PYR | EPI_BNB)) ? 1 : 2;
   constexpr int EC = NR < ECMAX ? NR : ECMAX;
   static_assert(PR % RPP == 0, "pass rows must split evenly over the sweeps");
   static_assert(PR * SC <= 2 * BK * SA + 2 * BK * SB, "epilogue staging exceeds the LDS tile");
