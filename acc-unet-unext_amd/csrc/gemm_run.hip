@@ -105,7 +105,9 @@ static int pick_tile(int M, int N, int K, int bmode, int cin, bool can_split) {
   // short-K GEMMs over many pixels (1x1 data gradients, K = the forward's N <= 64):
   // epilogue-dominated, so smaller tiles (more resident waves to hide its gathers)
   const int sk = smallk_tile();
-  if (sk >= 0 && K <= 64 && M >= 65536 && N > 32) return sk;
+  // (128x32 tiles for 64 < N <= 96: 1Mx96x32 pyramid dgrad 368 vs 447 us; N = 64 is
+  // slower with them: 262144x64x64 +10 us)
+  if (sk >= 0 && K <= 64 && M >= 65536 && N > 32) return (N > 64 && N <= 96) ? TILE_C : sk;
   if (M <= 32) t = TILE_D;
   else if (M <= 64) t = TILE_E;
   else if (N <= 32) t = TILE_C;
