@@ -293,6 +293,7 @@ struct DwTGeom {
   int rch;    // 8-row chunks per block (forward kernel: a vertical strip of 8*rch rows)
   int ntl;    // non-temporal input loads (tuning knob ACCUNET_DW_NTL)
   int remap;  // ntiles % 8 == 0: XCD-contiguous tile order
+  int cgf;    // forward: > 0 = 1-D grid, channel group fastest (cgf groups per tile)
 };
 
 ACC_DEV int dw_tile_id(const DwTGeom& g) {
@@ -429,9 +430,15 @@ dw3x3_tile_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
   const bool bnb = BNB && stats != nullptr && bz != nullptr;
   const int tid = threadIdx.x;
   const int q = tid % TCQ, p = tid / TCQ;
-  const int c0 = blockIdx.y * TCQ * 4;
-  const int c = c0 + 4 * q;
   int t = dw_tile_id(g);
+  int cg = blockIdx.y;
+  if (g.cgf) {  // the channel groups of one tile are neighbours in dispatch order
+    cg = t % g.cgf;
+    t /= g.cgf;
+  }
+  const int srow = g.cgf ? t : (int)blockIdx.x;  // statistics partial row of this tile
+  const int c0 = cg * TCQ * 4;
+  const int c = c0 + 4 * q;
   const int tw = t % g.tilesW;
   t /= g.tilesW;
   const int th = t % g.tilesH;
@@ -550,7 +557,7 @@ dw3x3_tile_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
     __syncthreads();  // the tile is reused as the reduction buffer
     double v[8] = {s1[0], s1[1], s1[2], s1[3], s2[0], s2[1], s2[2], s2[3]};
     if (block_slot_reduce<TCQ, 8, double>(v, reinterpret_cast<double*>(tile))) {
-      const long row = (long)(blockIdx.x) * 2 * g.C;
+      const long row = (long)srow * 2 * g.C;
       const int cc = c0 + 4 * threadIdx.x;  // slot = quad index q
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -652,11 +659,24 @@ static int dw_tile_tcq(int W, int C) {
   return 8;
 }
 
-static int dw_ntl() {
+// Non-temporal input loads: by default only for inputs larger than the 256 MB
+// Infinity Cache (streamed once, nothing to keep); ACCUNET_DW_NTL=0/1 forces it.
+static int dw_ntl(long bytes) {
+  static int v = -2;
+  if (v == -2) {
+    const char* e = getenv("ACCUNET_DW_NTL");
+    v = e ? atoi(e) : -1;
+  }
+  return v >= 0 ? v : (bytes > (256L << 20) ? 1 : 0);
+}
+
+static int dw_cgfast() {
   static int v = -1;
   if (v < 0) {
-    const char* e = getenv("ACCUNET_DW_NTL");
-    v = e ? atoi(e) : 0;
+    // default on: the channel groups of one tile run together, so each pixel's
+    // 384-byte row is fetched as a unit (tools/k1_sweep2.sh: 161 -> 157.5 us on K1)
+    const char* e = getenv("ACCUNET_DW_CGFAST");  // tuning knob (tools/kbench)
+    v = e ? atoi(e) : 1;
   }
   return v;
 }
@@ -699,11 +719,12 @@ static DwTGeom dw_tgeom(int B, int H, int W, int C, int tcq, dim3* grid, int rch
       }
   }
   g.rch = rch;
-  g.ntl = dw_ntl();
+  g.ntl = dw_ntl((long)B * H * W * C * 4);
   g.tilesH = ceil_div(H, DW_TR * rch);
   long nt = (long)B * g.tilesH * g.tilesW;
   static const char* noremap = getenv("ACCUNET_DW_NOREMAP");  // tuning knob (tools/kbench)
   g.remap = (nt % 8 == 0 && !noremap) ? 1 : 0;
+  g.cgf = 0;
   *grid = dim3((unsigned)nt, C / 4 / tcq);
   return g;
 }
@@ -740,6 +761,10 @@ extern "C" int accunet_dw3x3_fwd(const float* x, const float* wt, const float* b
   int tcq = dw_tile_tcq(W, C);
   if (tcq) {
     DwTGeom tg = dw_tgeom(B, H, W, C, tcq, &grid, dw_rch_max());
+    if (dw_cgfast() && grid.y > 1) {
+      tg.cgf = (int)grid.y;
+      grid = dim3(grid.x * grid.y, 1);
+    }
     if (bz) {
       if (tcq == 16)
         hipLaunchKernelGGL((dw3x3_tile_fwd_kernel<16, true>), grid, dim3(256), 0, s, x, wt, bias, sc,
