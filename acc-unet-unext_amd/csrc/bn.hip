@@ -20,10 +20,12 @@ sum_rows_kernel(const float* __restrict__ part, int R, int stride, int ncols,
   __shared__ double red[4][64];
   int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
   int c = blockIdx.x * 64 + cl;
-  double s1 = 0.0;
+  double s1[1] = {0.0};
   if (c < ncols)
-    for (int r = g; r < R; r += 4) s1 += (double)part[(long)r * stride + c];
-  red[g][cl] = s1;
+    ordered_strided_sum<8>(s1, g, R, 4, [&](int r, double (&v)[1]) {
+      v[0] = (double)part[(long)r * stride + c];
+    });
+  red[g][cl] = s1[0];
   __syncthreads();
   if (g == 0 && c < ncols) out[c] = (float)(red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl]);
 }
@@ -35,10 +37,12 @@ sum_rows_d_kernel(const double* __restrict__ part, int R, int stride, int ncols,
   __shared__ double red[4][64];
   int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
   int c = blockIdx.x * 64 + cl;
-  double s1 = 0.0;
+  double s1[1] = {0.0};
   if (c < ncols)
-    for (int r = g; r < R; r += 4) s1 += part[(long)r * stride + c];
-  red[g][cl] = s1;
+    ordered_strided_sum<8>(s1, g, R, 4, [&](int r, double (&v)[1]) {
+      v[0] = part[(long)r * stride + c];
+    });
+  red[g][cl] = s1[0];
   __syncthreads();
   if (g == 0 && c < ncols) out[c] = (TOUT)(red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl]);
 }
@@ -55,10 +59,10 @@ colreduce_kernel(const T* __restrict__ in, T* __restrict__ out, int R, int Wd, i
   int g = threadIdx.x >> 6;
   int r0 = blockIdx.x * RB;
   int r1 = min(R, r0 + RB);
-  T s = 0;
+  T s[1] = {0};
   if (c < Wd)
-    for (int r = r0 + g; r < r1; r += 4) s += in[(long)r * Wd + c];
-  red[g][threadIdx.x & 63] = s;
+    ordered_strided_sum<8>(s, r0 + g, r1, 4, [&](int r, T (&v)[1]) { v[0] = in[(long)r * Wd + c]; });
+  red[g][threadIdx.x & 63] = s[0];
   __syncthreads();
   if (g == 0 && c < Wd) out[(long)blockIdx.x * Wd + c] = red[0][threadIdx.x] + red[1][threadIdx.x] +
                                                      red[2][threadIdx.x] + red[3][threadIdx.x];
@@ -118,13 +122,13 @@ bn_finalize_kernel(const double* __restrict__ part, int R, int C, double count,
   int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
   int c = blockIdx.x * 64 + cl;
   if (nbt && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;  // num_batches_tracked
-  double s1 = 0.0, s2 = 0.0;
-  if (training && c < C) {
-    for (int r = g; r < R; r += 4) {
-      s1 += part[(long)r * 2 * C + c];
-      s2 += part[(long)r * 2 * C + C + c];
-    }
-  }
+  double s[2] = {0.0, 0.0};
+  if (training && c < C)
+    ordered_strided_sum<8>(s, g, R, 4, [&](int r, double (&v)[2]) {
+      v[0] = part[(long)r * 2 * C + c];
+      v[1] = part[(long)r * 2 * C + C + c];
+    });
+  double s1 = s[0], s2 = s[1];
   red[0][g][cl] = s1;
   red[1][g][cl] = s2;
   __syncthreads();
@@ -319,12 +323,13 @@ bn_bwd_finalize_kernel(const double* __restrict__ part, int R, int C, double cou
   __shared__ double red[2][4][64];
   int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
   int c = blockIdx.x * 64 + cl;
-  double s1 = 0.0, s2 = 0.0;
+  double s[2] = {0.0, 0.0};
   if (c < C)
-    for (int r = g; r < R; r += 4) {
-      s1 += part[(long)r * 2 * C + c];
-      s2 += part[(long)r * 2 * C + C + c];
-    }
+    ordered_strided_sum<8>(s, g, R, 4, [&](int r, double (&v)[2]) {
+      v[0] = part[(long)r * 2 * C + c];
+      v[1] = part[(long)r * 2 * C + C + c];
+    });
+  double s1 = s[0], s2 = s[1];
   red[0][g][cl] = s1;
   red[1][g][cl] = s2;
   __syncthreads();

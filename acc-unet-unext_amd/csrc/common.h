@@ -45,6 +45,28 @@ ACC_DEV uint32_t fdiv(uint32_t n, const FastDiv& f) {
   return (t + n) >> f.s;
 }
 
+// s[i] += v_r[i] for r = r, r+st, ... < r1 in that order (so the result is bit-identical
+// to the plain loop), with the loads of U consecutive terms issued before any add:
+// the small partial-row reductions are load-latency chains, not bandwidth bound.
+template <int U, int N, typename T, class L>
+ACC_DEV void ordered_strided_sum(T (&s)[N], int r, int r1, int st, L load) {
+  for (; r + (U - 1) * st < r1; r += U * st) {
+    T v[U][N];
+#pragma unroll
+    for (int u = 0; u < U; ++u) load(r + u * st, v[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int i = 0; i < N; ++i) s[i] += v[u][i];
+  }
+  for (; r < r1; r += st) {
+    T v[N];
+    load(r, v);
+#pragma unroll
+    for (int i = 0; i < N; ++i) s[i] += v[i];
+  }
+}
+
 ACC_DEV float lrelu(float x) { return x > 0.f ? x : x * LRELU_SLOPE; }
 // torch LeakyReLU backward: grad * (input > 0 ? 1 : slope)
 ACC_DEV float lrelu_d(float pre) { return pre > 0.f ? 1.f : LRELU_SLOPE; }

@@ -274,9 +274,11 @@ extern "C" int accunet_pool2_bwd(const float* x, const float* y, const float* dy
 // Nearest-upsample backward: out[b,hs,ws,c] (+)= sum over the f x f block of
 // in[b, hs*f+dy, ws*f+dx, in_off + c] (in has ld_in channels per pixel).
 // ---------------------------------------------------------------------------
+template <int F>  // F > 0: compile-time factor (the f*f loads unrolled); 0: runtime f
 __global__ void __launch_bounds__(256)
 blocksum_kernel(const float* __restrict__ in, int ld_in, int in_off, float* __restrict__ out,
-                int ld_out, int B, int H, int W, int C, int f, int accumulate) {
+                int ld_out, int B, int H, int W, int C, int f_rt, int accumulate) {
+  const int f = F > 0 ? F : f_rt;
   const int Hs = H / f, Ws = W / f;
   long total = (long)B * Hs * Ws * C;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
@@ -287,10 +289,20 @@ blocksum_kernel(const float* __restrict__ in, int ld_in, int in_off, float* __re
     long t = pix / Ws;
     int hs = (int)(t % Hs);
     int b = (int)(t / Hs);
+    const float* src = in + (((long)b * H + hs * f) * W + ws * f) * ld_in + in_off + c;
     float s = 0.f;
-    for (int dy = 0; dy < f; ++dy)
-      for (int dx = 0; dx < f; ++dx)
-        s += in[(((long)b * H + hs * f + dy) * W + ws * f + dx) * ld_in + in_off + c];
+    if (F > 0) {
+      float v[F > 0 ? F * F : 1];
+#pragma unroll
+      for (int dy = 0; dy < F; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < F; ++dx) v[dy * F + dx] = src[((long)dy * W + dx) * ld_in];
+#pragma unroll
+      for (int k = 0; k < F * F; ++k) s += v[k];  // same (dy, dx) order as below
+    } else {
+      for (int dy = 0; dy < f; ++dy)
+        for (int dx = 0; dx < f; ++dx) s += src[((long)dy * W + dx) * ld_in];
+    }
     float* o = out + pix * ld_out + c;
     *o = accumulate ? *o + s : s;
   }
@@ -301,8 +313,20 @@ extern "C" int accunet_upsample_bwd(const float* in, int ld_in, int in_off, floa
                                     void* stream) {
   if (H % f || W % f) return ACC_EBADSHAPE;
   long total = (long)B * (H / f) * (W / f) * C;
-  hipLaunchKernelGGL(blocksum_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, in,
-                     ld_in, in_off, out, ld_out, B, H, W, C, f, accumulate);
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid(grid_for(total));
+  if (f == 2)
+    hipLaunchKernelGGL(blocksum_kernel<2>, grid, dim3(256), 0, s, in, ld_in, in_off, out, ld_out, B,
+                       H, W, C, f, accumulate);
+  else if (f == 4)
+    hipLaunchKernelGGL(blocksum_kernel<4>, grid, dim3(256), 0, s, in, ld_in, in_off, out, ld_out, B,
+                       H, W, C, f, accumulate);
+  else if (f == 8)
+    hipLaunchKernelGGL(blocksum_kernel<8>, grid, dim3(256), 0, s, in, ld_in, in_off, out, ld_out, B,
+                       H, W, C, f, accumulate);
+  else
+    hipLaunchKernelGGL(blocksum_kernel<0>, grid, dim3(256), 0, s, in, ld_in, in_off, out, ld_out, B,
+                       H, W, C, f, accumulate);
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 

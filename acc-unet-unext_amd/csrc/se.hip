@@ -118,13 +118,12 @@ se_part_sum_kernel(const double* __restrict__ part, SeGeom g, double* __restrict
   double s[N];
 #pragma unroll
   for (int i = 0; i < N; ++i) s[i] = 0.0;
-  if (c < C) {
-    for (int k = grp; k < g.NCH; k += 4) {
+  if (c < C)
+    ordered_strided_sum<4>(s, grp, g.NCH, 4, [&](int k, double (&v)[N]) {
       const double* pr = part + ((long)(b * g.NCH + k) * N) * C;
 #pragma unroll
-      for (int i = 0; i < N; ++i) s[i] += pr[(long)i * C + c];
-    }
-  }
+      for (int i = 0; i < N; ++i) v[i] = pr[(long)i * C + c];
+    });
 #pragma unroll
   for (int i = 0; i < N; ++i) r[i][grp][t & 63] = s[i];
   __syncthreads();
@@ -155,16 +154,15 @@ se_mid_sample_kernel(const double* __restrict__ part, SeGeom g, int Cr,
   const int cl = tid & 63, grp = tid >> 6;
   for (int cb = 0; cb < C; cb += 64) {
     const int c = cb + cl;
-    double s0 = 0.0, s1 = 0.0;
-    if (c < C) {
-      for (int k = grp; k < g.NCH; k += 4) {
+    double s2[2] = {0.0, 0.0};
+    if (c < C)
+      ordered_strided_sum<8>(s2, grp, g.NCH, 4, [&](int k, double (&v)[2]) {
         const double* pr = part + ((long)(b * g.NCH + k) * 2) * C;
-        s0 += pr[c];
-        s1 += pr[(long)C + c];
-      }
-    }
-    r[0][grp][cl] = s0;
-    r[1][grp][cl] = s1;
+        v[0] = pr[c];
+        v[1] = pr[(long)C + c];
+      });
+    r[0][grp][cl] = s2[0];
+    r[1][grp][cl] = s2[1];
     __syncthreads();
     if (grp == 0 && c < C) {
       const double S = ((r[0][0][cl] + r[0][1][cl]) + r[0][2][cl]) + r[0][3][cl];
