@@ -12,10 +12,14 @@
 //    shuffle (:578-590), and generic 4-D permutes for weight / boundary layouts.
 #include "common.h"
 #include "kernels.h"
+#include "chan.h"
 
 // ---------------------------------------------------------------------------
-// pyramid forward: one thread per (low-res 4x4 cell or 2x2 cell, channel)
+// pyramid forward: one thread per (low-res 4x4 or 2x2 cell, V consecutive channels);
+// V = 4 moves channel quads (16-byte loads/stores, 4-byte mask stores). The
+// per-element arithmetic is the same for every V.
 // ---------------------------------------------------------------------------
+template <int V>
 __global__ void __launch_bounds__(256)
 hanc_pyramid_fwd_kernel(const float* __restrict__ x, const float* __restrict__ sc,
                         const float* __restrict__ sh, int act, int B, int H, int W, int C, int k,
@@ -23,64 +27,100 @@ hanc_pyramid_fwd_kernel(const float* __restrict__ x, const float* __restrict__ s
                         unsigned char* __restrict__ mk2, unsigned char* __restrict__ mk4) {
   // k == 3: cell = 4x4 (one P4 pixel, four P2 pixels); k == 2: cell = 2x2 (one P2 pixel)
   const int cs = (k == 3) ? 4 : 2;
-  const int Hc = H / cs, Wc = W / cs;
-  long total = (long)B * Hc * Wc * C;
+  const int Hc = H / cs, Wc = W / cs, CV = C / V;
+  const long total = (long)B * Hc * Wc * CV;
+  const bool pro = sc != nullptr;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
        i += (long)gridDim.x * blockDim.x) {
-    int c = (int)(i % C);
-    long cell = i / C;
-    int wc = (int)(cell % Wc);
-    long t = cell / Wc;
-    int hc = (int)(t % Hc);
-    int b = (int)(t / Hc);
-    float s = sc ? sc[c] : 1.f, h = sh ? sh[c] : 0.f;
-    const bool pro = sc != nullptr;
-    float v[4][4];
+    const int c = (int)(i % CV) * V;
+    const long cell = i / CV;
+    const int wc = (int)(cell % Wc);
+    const long t = cell / Wc;
+    const int hc = (int)(t % Hc);
+    const int b = (int)(t / Hc);
+    float s[V], h[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      s[j] = pro ? sc[c + j] : 1.f;
+      h[j] = pro ? sh[c + j] : 0.f;
+    }
+    float v[4][4][V];
+    const float* src = x + (((long)b * H + hc * cs) * W + wc * cs) * C + c;
 #pragma unroll
     for (int dy = 0; dy < 4; ++dy)
 #pragma unroll
       for (int dx = 0; dx < 4; ++dx) {
         if (dy < cs && dx < cs) {
-          float q = x[(((long)b * H + hc * cs + dy) * W + wc * cs + dx) * C + c];
-          v[dy][dx] = pro ? apply_act(q * s + h, act) : q;
+          float q[V];
+          ldv<V>(src + ((long)dy * W + dx) * C, q);
+#pragma unroll
+          for (int j = 0; j < V; ++j) v[dy][dx][j] = pro ? apply_act(q[j] * s[j] + h[j], act) : q[j];
         }
       }
     const int H2 = H / 2, W2 = W / 2;
-    float s4 = 0.f, m4 = -INFINITY;
     const int n2 = cs / 2;
     for (int qy = 0; qy < n2; ++qy)
       for (int qx = 0; qx < n2; ++qx) {
-        float a0 = v[2 * qy][2 * qx], a1 = v[2 * qy][2 * qx + 1];
-        float a2 = v[2 * qy + 1][2 * qx], a3 = v[2 * qy + 1][2 * qx + 1];
-        float sum = ((a0 + a1) + a2) + a3;  // torch CPU avg_pool2d summation order
-        float mx = fmaxf(fmaxf(a0, a1), fmaxf(a2, a3));
-        long q2 = ((long)b * H2 + hc * n2 + qy) * W2 + wc * n2 + qx;
-        long o = q2 * (2 * C);
-        p2[o + c] = sum * 0.25f;
-        p2[o + C + c] = mx;
-        if (mk2) {  // first maximum in window order (0,0) (0,1) (1,0) (1,1)
-          unsigned char code = a0 == mx ? 0 : a1 == mx ? 1 : a2 == mx ? 2 : a3 == mx ? 3 : 255;
-          mk2[q2 * C + c] = code;
+        float sum[V], mx[V];
+        unsigned char code[V];
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          float a0 = v[2 * qy][2 * qx][j], a1 = v[2 * qy][2 * qx + 1][j];
+          float a2 = v[2 * qy + 1][2 * qx][j], a3 = v[2 * qy + 1][2 * qx + 1][j];
+          sum[j] = (((a0 + a1) + a2) + a3) * 0.25f;  // torch CPU avg_pool2d summation order
+          mx[j] = fmaxf(fmaxf(a0, a1), fmaxf(a2, a3));
+          // first maximum in window order (0,0) (0,1) (1,0) (1,1)
+          code[j] = a0 == mx[j] ? 0 : a1 == mx[j] ? 1 : a2 == mx[j] ? 2 : a3 == mx[j] ? 3 : 255;
+        }
+        const long q2 = ((long)b * H2 + hc * n2 + qy) * W2 + wc * n2 + qx;
+        const long o = q2 * (2 * C);
+        stv<V>(p2 + o + c, sum);
+        stv<V>(p2 + o + C + c, mx);
+        if (mk2) {
+          if (V == 4) {
+            uchar4 cv = make_uchar4(code[0], code[V > 1 ? 1 : 0], code[V > 2 ? 2 : 0],
+                                    code[V > 3 ? 3 : 0]);
+            *reinterpret_cast<uchar4*>(mk2 + q2 * C + c) = cv;
+          } else {
+#pragma unroll
+            for (int j = 0; j < V; ++j) mk2[q2 * C + c + j] = code[j];
+          }
         }
       }
     if (k == 3) {
+      float s4[V], m4[V];
+      unsigned char code[V];
 #pragma unroll
-      for (int dy = 0; dy < 4; ++dy)
+      for (int j = 0; j < V; ++j) {
+        float a = 0.f, m = -INFINITY;
 #pragma unroll
-        for (int dx = 0; dx < 4; ++dx) {
-          s4 += v[dy][dx];
-          m4 = fmaxf(m4, v[dy][dx]);
-        }
-      long q4 = ((long)b * Hc + hc) * Wc + wc;
-      long o = q4 * (2 * C);
-      p4[o + c] = s4 * (1.f / 16.f);
-      p4[o + C + c] = m4;
-      if (mk4) {
-        unsigned char code = 255;
+        for (int dy = 0; dy < 4; ++dy)
+#pragma unroll
+          for (int dx = 0; dx < 4; ++dx) {
+            a += v[dy][dx][j];
+            m = fmaxf(m, v[dy][dx][j]);
+          }
+        s4[j] = a * (1.f / 16.f);
+        m4[j] = m;
+        unsigned char cd = 255;
 #pragma unroll
         for (int e = 15; e >= 0; --e)
-          if (v[e >> 2][e & 3] == m4) code = (unsigned char)e;
-        mk4[q4 * C + c] = code;
+          if (v[e >> 2][e & 3][j] == m) cd = (unsigned char)e;
+        code[j] = cd;
+      }
+      const long q4 = ((long)b * Hc + hc) * Wc + wc;
+      const long o = q4 * (2 * C);
+      stv<V>(p4 + o + c, s4);
+      stv<V>(p4 + o + C + c, m4);
+      if (mk4) {
+        if (V == 4) {
+          uchar4 cv = make_uchar4(code[0], code[V > 1 ? 1 : 0], code[V > 2 ? 2 : 0],
+                                  code[V > 3 ? 3 : 0]);
+          *reinterpret_cast<uchar4*>(mk4 + q4 * C + c) = cv;
+        } else {
+#pragma unroll
+          for (int j = 0; j < V; ++j) mk4[q4 * C + c + j] = code[j];
+        }
       }
     }
   }
@@ -175,9 +215,18 @@ extern "C" int accunet_hanc_pyramid_fwd(const float* x, const float* sc, const f
   int cs = (k == 3) ? 4 : 2;
   if (H % cs || W % cs) return ACC_EBADSHAPE;
   long total = (long)B * (H / cs) * (W / cs) * C;
-  hipLaunchKernelGGL(hanc_pyramid_fwd_kernel, dim3(grid_for(total)), dim3(256), 0,
-                     (hipStream_t)stream, x, sc, sh, act, B, H, W, C, k, p2, p4, mk2,
-                     k == 3 ? mk4 : nullptr);
+  // quads need 16-byte aligned rows: C % 4 == 0 and aligned base pointers
+  const bool q4 = C % 4 == 0 && !((uintptr_t)x & 15) && !((uintptr_t)p2 & 15) &&
+                  (k != 3 || !((uintptr_t)p4 & 15)) && !((uintptr_t)mk2 & 3) &&
+                  (k != 3 || !((uintptr_t)mk4 & 3));
+  if (q4)
+    hipLaunchKernelGGL(hanc_pyramid_fwd_kernel<4>, dim3(grid_for(total / 4)), dim3(256), 0,
+                       (hipStream_t)stream, x, sc, sh, act, B, H, W, C, k, p2, p4, mk2,
+                       k == 3 ? mk4 : nullptr);
+  else
+    hipLaunchKernelGGL(hanc_pyramid_fwd_kernel<1>, dim3(grid_for(total)), dim3(256), 0,
+                       (hipStream_t)stream, x, sc, sh, act, B, H, W, C, k, p2, p4, mk2,
+                       k == 3 ? mk4 : nullptr);
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 
