@@ -22,7 +22,10 @@ cv2 is not part of this image: resizing follows cv2's INTER_LINEAR / INTER_NEARE
 rules for float data (half-pixel centres, clamped; floor(dst * in / out)), which
 torch's F.interpolate(bilinear, align_corners=False) / (nearest) also implement;
 no reference fixture pins the resize (parity unpinned for that branch; the
-tests check the HIP kernels against F.interpolate).
+tests check the HIP kernels against F.interpolate). Integer-typed raw planes are
+interpolated as fp32 here, whereas cv2 interpolates in the native dtype and
+rounds (parity unpinned). Non-square raw inputs are refused: the reference
+resizes only when the height differs (Load_Dataset.py:467,481).
 """
 from __future__ import annotations
 
@@ -109,6 +112,12 @@ class DeviceBatches:
         if any(i.shape != (hin, win) for i in imgs):
             raise ValueError("DeviceBatches: images of one batch must share their raw size")
         mh, mw = masks[0].shape
+        # the reference resizes only when the HEIGHT differs from S (Load_Dataset.py:467,
+        # :481), so a non-square raw plane with H == S would stay non-square there; the
+        # device kernels write S x S, so such inputs are refused rather than resampled
+        if hin != win or mh != mw:
+            raise ValueError("DeviceBatches: raw images and masks must be square "
+                             f"(got {hin}x{win} / {mh}x{mw}); Load_Dataset.py resizes on height only")
         mdt = masks[0].dtype
         if any(m.shape != (mh, mw) or m.dtype != mdt for m in masks):
             raise ValueError("DeviceBatches: masks of one batch must share size and dtype")

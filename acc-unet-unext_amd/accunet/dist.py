@@ -94,12 +94,11 @@ class GradBucketReducer:
             self.bucket_range.append((lo, hi))
             for i in idxs:
                 self.bucket_of[i] = b
-        for i, p in enumerate(params):
-            p.grad = self.flat[offs[i]:offs[i] + p.numel()].view_as(p)
-        self._pending = [0] * len(self.buckets)
-        self._launched = [False] * len(self.buckets)
-        self._handles = []
-        self._callback_queued = False
+        self._views = [self.flat[offs[i]:offs[i] + p.numel()].view_as(p)
+                       for i, p in enumerate(params)]
+        for p, v in zip(params, self._views):
+            p.grad = v
+        self._reset()
         for i, p in enumerate(params):
             p.register_post_accumulate_grad_hook(self._make_hook(i))
         if broadcast_params and self.world > 1:
@@ -136,13 +135,21 @@ class GradBucketReducer:
             h.wait()
             if self.world > 1 and dist.get_backend(self.pg) != "nccl":
                 self.flat[lo:hi].div_(self.world)
-        self._handles = []
+        # ready for the next backward whether or not the caller runs prepare()
+        self._reset()
 
     def _make_hook(self, i):
         def hook(p):
             if not self._callback_queued:
                 self._callback_queued = True
                 torch.autograd.Variable._execution_engine.queue_callback(self._finish)
+            v = self._views[i]
+            if p.grad is not v and (p.grad is None or p.grad.data_ptr() != v.data_ptr()):
+                # the gradient was detached from the flat buffer (e.g.
+                # optimizer.zero_grad()'s set_to_none): move it back in, so the bucket
+                # reduces what backward produced instead of stale zeros
+                v.copy_(p.grad)
+                p.grad = v
             b = self.bucket_of[i]
             self._pending[b] -= 1
             if self._pending[b] == 0:
@@ -150,5 +157,5 @@ class GradBucketReducer:
         return hook
 
     def prepare(self):
-        """Call before each backward."""
+        """Optional before a backward (the state also resets after every flush)."""
         self._reset()

@@ -86,10 +86,6 @@ def _take_bias_grad(slot):
     t, slot.t = slot.t, None
     return t
 
-    @property
-    def shape(self):
-        return self.z.shape
-
 
 def as_pending(x) -> Pending:
     return x if isinstance(x, Pending) else Pending(x)

@@ -129,6 +129,13 @@ class TrainStep:
                     p.grad = torch.zeros_like(p)
 
     def _replay(self, images, masks):
+        if images.shape != self._x.shape or masks.shape != self._m.shape:
+            # copy_ would broadcast a smaller batch silently (e.g. a ragged last batch
+            # of size 1 replicated over every captured slot)
+            raise ValueError(f"TrainStep(graph=True) was captured for images "
+                             f"{tuple(self._x.shape)} / masks {tuple(self._m.shape)}, got "
+                             f"{tuple(images.shape)} / {tuple(masks.shape)}; use drop_last "
+                             f"batching or graph=False for ragged batches")
         if images.data_ptr() != self._x.data_ptr():
             self._x.copy_(images)
         if masks.data_ptr() != self._m.data_ptr():

@@ -169,6 +169,13 @@ class Trainer:
         ck = load_checkpoint(path, map_location=self.device)
         self.model.load_state_dict(ck["state_dict"])
         self.optimizer.load_state_dict(ck["optimizer"])
+        if isinstance(self.lr_scheduler, CosineAnnealingWarmRestarts):
+            # the reference builds its scheduler AFTER optimizer.load_state_dict
+            # (train_model.py:677 then :738): the fresh scheduler's first step puts every
+            # group back at its initial_lr, so the first resumed epoch runs at base LR
+            s = self.lr_scheduler
+            self.lr_scheduler = CosineAnnealingWarmRestarts(self.optimizer, T_0=s.T_0,
+                                                            T_mult=s.T_mult, eta_min=s.eta_min)
         self.start_epoch = ck["epoch"] + 1
         self.max_dice = float(ck.get("val_dice", 0.0))
         self.best_epoch = self.start_epoch

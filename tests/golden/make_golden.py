@@ -1,7 +1,8 @@
 """Generate the golden fixtures that pin the CPU oracle to the reference.
 
 Run in the build container only (needs /root/reference):
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py               # every fixture
+    python tests/golden/make_golden.py --fullwidth   # only the n_filts=32 ones (6)
 It imports the reference modules from /root/reference (read-only), fills them
 with the oracle's deterministic, version-independent parameters
 (oracle/accunet_oracle.py: det_state_dict), runs them on deterministic inputs
@@ -67,10 +68,53 @@ def grad_summary(model):
     return names, np.array(s1), np.array(s2), np.array(s3), np.stack(samp)
 
 
+def fullwidth(models, U):
+    """6) The full-width models at the bench resolution (pin n_filts=32 at
+    256^2): canonical ACC_UNet (16.77 M, ACC_UNet/ACC_UNet.py:535-659) eval output on
+    1x3x256x256, and train-mode fwd + WeightedDiceBCE + bwd on 2x3x256x256 for the
+    canonical and the script variant (logits, Experiments/nets/ACC_UNet.py:530-655):
+    outputs, loss, per-parameter gradient summaries and running-stat sums."""
+    x1 = O.det_input((1, 3, 256, 256), "fw-x1")
+    x2 = O.det_input((2, 3, 256, 256), "fw-x2")
+    m2 = O.det_mask((2, 1, 256, 256), "fw-mask", p=0.3)
+    for v in ("canonical", "script"):
+        torch.manual_seed(0)
+        m = models[v](3, 1)
+        spec = [(k, tuple(t.shape)) for k, t in m.state_dict().items()]
+        sd = O.det_state_dict(spec, seed=7)
+        res = {}
+        if v == "canonical":
+            m.load_state_dict(sd)
+            m.eval()
+            with torch.no_grad():
+                res["out_eval"] = m(x1).numpy()
+        m.load_state_dict(sd)
+        m.train()
+        out = m(x2)
+        crit = U.WeightedDiceBCE(dice_weight=0.5, BCE_weight=0.5)
+        loss = crit(out, m2.clone())
+        m.zero_grad()
+        loss.backward()
+        names, s1, s2, s3, samp = grad_summary(m)
+        bufs = {k: t.detach().numpy() for k, t in m.state_dict().items()
+                if k.endswith("running_mean") or k.endswith("running_var")}
+        rm_names = sorted(bufs)
+        np.savez_compressed(
+            os.path.join(HERE, f"fullwidth_{v}_nf32.npz"), out_train=out.detach().numpy(),
+            loss=np.array(loss.item()), grad_names=np.array(names), grad_sum=s1, grad_abs=s2,
+            grad_sq=s3, grad_samples=samp, buf_names=np.array(rm_names),
+            buf_sums=np.array([bufs[k].astype(np.float64).sum() for k in rm_names]),
+            show_dice=np.array(float(crit._show_dice(out.detach(), m2.clone()))), **res)
+        print("fullwidth", v, "loss", loss.item())
+
+
 def main():
     torch.set_num_threads(8)
     models = ref_models()
     U = ref_utils()
+    if "--fullwidth" in sys.argv:
+        fullwidth(models, U)
+        return
     meta = {}
 
     # 1) state_dict key/shape lists at the default size (n_filts=32, n_channels=3) and a
@@ -179,6 +223,8 @@ def main():
 
     with open(os.path.join(HERE, "meta.json"), "w") as f:
         json.dump(meta, f, indent=1)
+
+    fullwidth(models, U)
 
 
 if __name__ == "__main__":

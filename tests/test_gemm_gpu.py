@@ -195,3 +195,132 @@ def test_skinny_shift3_weight_gradient(Bn, H, W, Co, Ci):
     wref = torch.nn.grad.conv2d_weight(xd, (Co, Ci, 3, 3), gd, padding=1)  # [co][ci][kh][kw]
     ref = wref.permute(0, 2, 3, 1).reshape(Co, 9 * Ci)  # [co][tap][ci]
     assert rel(C.cpu(), ref) < 2e-5
+
+
+# ---------------------------------------------------------------------------
+# The shape-gated paths only the full-size model reaches:
+#   * K <= 64 && M >= 65536 small-K tiles (gemm_run.hip pick_tile) with the fused
+#     HANCLayer pyramid backward (EPI_PYR) and BatchNorm-backward statistics
+#     (EPI_BNB) epilogues, at the HANC x-branch data-gradient shapes of cnv12/cnv92
+#     (1x1 GEMM P x 96 x 32) and cnv22/cnv82 (P x 192 x 64);
+#   * the "< 128 output tiles -> 64x64 tiles" rule (16^2 / 32^2 levels);
+#   * the skinny split-K weight gradient at cnv12's real K = 16 * 256^2 pixels.
+# ---------------------------------------------------------------------------
+def _pyr_bnb_reference(dZ, Wp, C, B, H, W, dP2, dP4, mk2, mk4, z, st, act):
+    """fp64: dA = dZ @ Wp[:, :C] + pyramid backward; BN-backward partial sums."""
+    P = B * H * W
+    dA = dZ.double() @ Wp[:, :C].double()
+    h = torch.arange(H, device=dZ.device).view(1, H, 1, 1)
+    w = torch.arange(W, device=dZ.device).view(1, 1, W, 1)
+    pos2 = ((h & 1) * 2 + (w & 1)).expand(B, H, W, 1)
+    pos4 = ((h & 3) * 4 + (w & 3)).expand(B, H, W, 1)
+
+    def up(t, f):
+        return t.repeat_interleave(f, 1).repeat_interleave(f, 2)
+    d2 = dP2.double().view(B, H // 2, W // 2, 2 * C)
+    g = up(d2[..., :C], 2) * 0.25 + up(d2[..., C:], 2) * (up(mk2.view(B, H // 2, W // 2, C).long(), 2) == pos2)
+    if dP4 is not None:
+        d4 = dP4.double().view(B, H // 4, W // 4, 2 * C)
+        g = g + up(d4[..., :C], 4) / 16.0 + up(d4[..., C:], 4) * (
+            up(mk4.view(B, H // 4, W // 4, C).long(), 4) == pos4)
+    dA = dA + g.reshape(P, C)
+    zd = z.double()
+    pre = zd * st[2].double() + st[3].double()
+    gg = dA * torch.where(pre > 0, 1.0, 0.01) if act == _lib.ACT_LRELU else dA
+    t2 = gg * (zd - st[0].double())
+    return dA, gg.sum(0), t2.sum(0), gg.abs().sum(0), t2.abs().sum(0)
+
+
+@pytest.mark.parametrize("B,H,W,C,N,k", [(2, 256, 256, 96, 32, 3), (4, 128, 128, 192, 64, 3),
+                                         (4, 128, 128, 96, 32, 2)])
+def test_hanc_dgrad_pyramid_bnb_epilogue_full_size(B, H, W, C, N, k):
+    torch.manual_seed(6)
+    P = B * H * W
+    J = 2 * k - 1
+    dZ = torch.randn(P, N, device=DEV)
+    Wp = torch.randn(N, J * C, device=DEV) * 0.2
+    dP2 = torch.randn(P // 4, 2 * C, device=DEV)
+    mk2 = torch.randint(0, 4, (P // 4, C), device=DEV, dtype=torch.uint8)
+    mk2[::7] = 255  # windows without a maximum (NaN input): no max routing
+    dP4 = mk4 = None
+    if k == 3:
+        dP4 = torch.randn(P // 16, 2 * C, device=DEV)
+        mk4 = torch.randint(0, 16, (P // 16, C), device=DEV, dtype=torch.uint8)
+    z = torch.randn(P, C, device=DEV)
+    st = torch.stack([torch.randn(C), torch.rand(C) + 0.5, torch.rand(C) + 0.5,
+                      torch.randn(C) * 0.3]).float().to(DEV)
+    R = kern.gemm_stats_rows(P, C, N)
+    part = torch.empty(R, 2, C, device=DEV, dtype=torch.float64)
+    dA = torch.empty(P, C, device=DEV)
+    kern.gemm(P, C, N, a=[dZ], lda=[N], b=Wp, ldb=J * C, bmode=_lib.BMODE_NN, c=dA, ldc=C,
+              H=H, W=W, pyr=(dP2, dP4, mk2, mk4), stats=part, bnb=(z, st, _lib.ACT_LRELU))
+    ref, s1, s2, a1, a2 = _pyr_bnb_reference(dZ, Wp, C, B, H, W, dP2, dP4, mk2, mk4, z, st,
+                                             _lib.ACT_LRELU)
+    assert rel(dA, ref) < 1e-5
+    tot = part.sum(0)
+    # fp32 g per element (relative rounding ~6e-8), summed in fp64
+    assert bool(((tot[0] - s1).abs() <= 1e-6 * a1 + 1e-9).all())
+    assert bool(((tot[1] - s2).abs() <= 1e-6 * a2 + 1e-9).all())
+    # deterministic: same bits on a second launch
+    dA2 = torch.empty_like(dA)
+    part2 = torch.empty_like(part)
+    kern.gemm(P, C, N, a=[dZ], lda=[N], b=Wp, ldb=J * C, bmode=_lib.BMODE_NN, c=dA2, ldc=C,
+              H=H, W=W, pyr=(dP2, dP4, mk2, mk4), stats=part2, bnb=(z, st, _lib.ACT_LRELU))
+    assert torch.equal(dA, dA2) and torch.equal(part, part2)
+
+
+@pytest.mark.parametrize("P,N,K", [(131072, 96, 32), (65536, 64, 64), (262144, 32, 16)])
+def test_small_k_dgrad_full_size(P, N, K):
+    """K <= 64, M >= 65536: the small-K tile choice, plain data gradient."""
+    torch.manual_seed(7)
+    dZ = torch.randn(P, K, device=DEV)
+    Wt = torch.randn(K, N, device=DEV)
+    dX = torch.empty(P, N, device=DEV)
+    kern.gemm(P, N, K, a=[dZ], lda=[K], b=Wt, ldb=N, bmode=_lib.BMODE_NN, c=dX, ldc=N)
+    assert rel(dX, dZ.double() @ Wt.double()) < 1e-5
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 256, 512), (4096, 128, 1024), (1024, 512, 1536)])
+def test_few_tiles_rule_with_prologue_bias_stats(M, N, K):
+    """< 128 output tiles of the default size -> 64x64 tiles (16^2 / 32^2 levels), with
+    the affine+LeakyReLU prologue, bias and C statistics of the forward GEMMs."""
+    torch.manual_seed(8)
+    A = torch.randn(M, K, device=DEV)
+    Wt = torch.randn(N, K, device=DEV) * 0.1
+    b = torch.randn(N, device=DEV)
+    sc = torch.rand(K, device=DEV) + 0.5
+    sh = torch.randn(K, device=DEV)
+    C = torch.empty(M, N, device=DEV)
+    rows = kern.gemm_stats_rows(M, N, K)
+    st = torch.zeros(rows, 2, N, device=DEV, dtype=torch.float64)
+    kern.gemm(M, N, K, a=[A], lda=[K], b=Wt, ldb=K, c=C, ldc=N, bias=b,
+              pro_a=_lib.PRO_AFFINE_LRELU, a_scale=sc, a_shift=sh, stats=st)
+    X = F.leaky_relu(A.double() * sc.double() + sh.double(), 0.01)
+    ref = X @ Wt.double().t() + b.double()
+    assert rel(C, ref) < 1e-5
+    s = st.sum(0)
+    assert torch.allclose(s[0], ref.sum(0), rtol=1e-6, atol=1e-6 * ref.abs().sum().item())
+    assert torch.allclose(s[1], (ref * ref).sum(0), rtol=1e-6)
+
+
+@pytest.mark.parametrize("M,N,lda,pro_b", [(96, 32, 96, 0), (32, 96, 32, 2), (32, 32, 32, 1)])
+def test_skinny_weight_gradient_cnv12_shapes(M, N, lda, pro_b):
+    """cnv12's 1x1 weight gradients at the bench batch: K = 16 * 256 * 256 pixels
+    (conv1 96x32, hnc.cnv x-branch 32x96 with the norm2 prologue, conv3 32x32)."""
+    K = 16 * 256 * 256
+    torch.manual_seed(9)
+    A = torch.randn(K, lda, device=DEV)
+    B = torch.randn(K, N, device=DEV)
+    sc = torch.rand(N, device=DEV) + 0.5
+    sh = torch.randn(N, device=DEV) * 0.2
+    C = torch.empty(M, N, device=DEV)
+    kw = dict(pro_b=pro_b, b_scale=sc, b_shift=sh) if pro_b else {}
+    kern.gemm(M, N, K, a=[A], lda=[lda], amode=_lib.AMODE_COL, b=B, ldb=N, bmode=_lib.BMODE_NN,
+              c=C, ldc=N, allow_split=True, **kw)
+    Bd = B.double()
+    if pro_b:
+        Bd = Bd * sc.double() + sh.double()
+        if pro_b == 2:
+            Bd = torch.where(Bd > 0, Bd, 0.01 * Bd)
+    ref = A[:, :M].double().t() @ Bd
+    assert rel(C, ref) < 2e-5

@@ -103,21 +103,30 @@ def _reducer_worker(rank, world, port, q):
         "a": torch.nn.Linear(16, 32), "b": torch.nn.Linear(32, 8),
         "unused": torch.nn.Linear(8, 8)})  # never used: must still be flushed
     red = GradBucketReducer(net, bucket_mb=0.001)  # tiny buckets -> several collectives
-    for it in range(2):
-        red.zero_grad()
-        red.prepare()
+    last = 3
+    for it in range(last + 1):
+        if it % 2 == 0:
+            red.zero_grad()
+            if it == 0:
+                red.prepare()  # optional: the state also resets after every flush
+        else:
+            # optimizer.zero_grad() style (set_to_none) and no prepare(): the hooks must
+            # move the fresh gradients back into the flat buffer and still reduce them
+            net.zero_grad(set_to_none=True)
         g = torch.Generator().manual_seed(100 * it + rank)
         x = torch.randn(4, 16, generator=g)
         y = net["b"](torch.relu(net["a"](x))).square().mean()
         y.backward()
-    got = {k: p.grad.clone() for k, p in net.named_parameters()}
+    # (the unused layer's gradient is None after a set_to_none zero_grad, as in torch)
+    got = {k: p.grad.clone() if p.grad is not None else torch.zeros_like(p)
+           for k, p in net.named_parameters()}
     # expected: average over ranks of the per-rank gradients of the last iteration
     exp = {k: torch.zeros_like(p) for k, p in net.named_parameters()}
     for r in range(world):
         net.zero_grad(set_to_none=True)
         for p in net.parameters():
             p.grad = None
-        g = torch.Generator().manual_seed(100 * 1 + r)
+        g = torch.Generator().manual_seed(100 * last + r)
         x = torch.randn(4, 16, generator=g)
         y = net["b"](torch.relu(net["a"](x))).square().mean()
         gr = torch.autograd.grad(y, [net["a"].weight, net["a"].bias, net["b"].weight,

@@ -333,3 +333,102 @@ def test_full_size_configs_properties(variant, B, S):
     step = TrainStep(m, lr=1e-3, graph=False)
     losses = [float(step(x, mask)) for _ in range(4)]
     assert losses[-1] < losses[0], losses
+
+
+@pytest.mark.parametrize("variant", ["canonical", "script"])
+def test_fullwidth_nf32_at_256_matches_reference_and_oracle(variant):
+    """The bench-width models (n_filts 32; canonical = 16.77 M with cnv72 inv_fctr 34)
+    at 256^2, where every shape-gated kernel path of the bench runs (K <= 64 small-K
+    tiles over M >= 65536 pixels with the pyramid / BN-backward epilogues, the
+    skinny weight-gradient path, the < 128-tile rule at 16^2):
+      - train fwd + WeightedDiceBCE + bwd on 2x3x256x256 against the reference's own
+        fp32 run (tests/golden/fullwidth_*_nf32.npz, made by importing the
+        reference) and the fp64 oracle: output within 4x the reference's own fp32
+        distance to fp64 + 1e-4 of scale, loss within 1e-5 of the reference's;
+      - every gradient and running statistic within 4x the fp32 oracle's distance
+        to fp64 (+ the floors of test_whole_model_train_step_matches_oracle), and the
+        whole gradient vector within 3x;
+      - canonical eval output on 1x3x256x256 within 1e-4 of the reference's (the
+        north-star bound)."""
+    g = np.load(os.path.join(GOLD, f"fullwidth_{variant}_nf32.npz"))
+    spec = O.param_spec(variant, 3, 1, 32)
+    sd = O.det_state_dict(spec, seed=7)
+    torch.set_num_threads(16)
+    if variant == "canonical":
+        m = _hip_model(variant, sd, 32).eval()
+        with torch.no_grad():
+            oe = m(O.det_input((1, 3, 256, 256), "fw-x1").to(DEV)).double().cpu().numpy()
+        assert np.abs(oe - g["out_eval"]).max() < 1e-4
+        del m
+    x = O.det_input((2, 3, 256, 256), "fw-x2")
+    mask = O.det_mask((2, 1, 256, 256), "fw-mask", p=0.3)
+    m = _hip_model(variant, sd, 32).train()
+    out = m(x.to(DEV))
+    loss = WeightedDiceBCE(0.5, 0.5)(out, mask.to(DEV))
+    loss.backward()
+    torch.cuda.synchronize()
+    assert abs(loss.item() - float(g["loss"])) < 1e-5, (loss.item(), float(g["loss"]))
+    ref_out, ref_loss, ref_grads, ref_sd = PU.oracle_run(variant, sd, x, mask)
+    e_ref = float(np.abs(g["out_train"] - ref_out.numpy()).max())
+    e_hip = (out.detach().double().cpu() - ref_out).abs().max().item()
+    assert e_hip <= 4 * e_ref + 1e-4 * ref_out.abs().max().item(), (e_hip, e_ref)
+    r32_out, _, r32_grads, r32_sd = PU.oracle_run(variant, sd, x, mask, dtype=torch.float32)
+    hip, r64, r32 = {"out": out}, {"out": ref_out}, {"out": r32_out}
+    gkeys = []
+    for k, p in m.named_parameters():
+        hip["grad:" + k] = p.grad if p.grad is not None else torch.zeros_like(p)
+        r64["grad:" + k] = ref_grads[k]
+        r32["grad:" + k] = r32_grads[k]
+        gkeys.append("grad:" + k)
+    e_glob_h = PU.global_rel_err(hip, r64, gkeys)
+    e_glob_r = PU.global_rel_err(r32, r64, gkeys)
+    assert e_glob_h <= 3 * e_glob_r + 1e-6, (e_glob_h, e_glob_r)
+    med = PU.median_live_grad(ref_grads)
+    floor = {k: (0.5 if ".fc1." in k else 0.05) * med for k in gkeys}
+    msd = m.state_dict()
+    for k, v in ref_sd.items():
+        if k.endswith(("running_mean", "running_var")):
+            hip["buf:" + k] = msd[k]
+            r64["buf:" + k] = v
+            r32["buf:" + k] = r32_sd[k]
+    rows = PU.compare_vs_reference_fp32(hip, r64, r32, abs_floor=floor)
+    bad = [r for r in rows if not r[4]]
+    assert not bad, sorted(bad, key=lambda r: -r[1] / r[3])[:8]
+
+
+def test_multiclass_head_matches_oracle():
+    """n_classes > 1 (ACC_UNet/ACC_UNet.py:597-599): n_classes + 1 output channels from
+    the 1x1 head, no activation. Train-mode forward and the gradients of a fixed
+    linear functional of the output against the fp64 oracle (fp32-error yardstick)."""
+    nf, B, S, nc = 8, 2, 32, 2
+    spec = O.param_spec("canonical", 3, nc, nf)
+    sd = O.det_state_dict(spec, seed=3)
+    x = O.det_input((B, 3, S, S), "mc-x")
+    go = O.det_input((B, nc + 1, S, S), "mc-go")
+    m = M.ACC_UNet(3, nc, n_filts=nf)
+    m.load_state_dict(sd)
+    m = m.to(DEV).train()
+    out = m(x.to(DEV))
+    assert tuple(out.shape) == (B, nc + 1, S, S) and m.last_activation is None
+    (out * go.to(DEV)).sum().backward()
+    res = {}
+    for dt in (torch.float64, torch.float32):
+        sdo = {k: (v.clone().to(dt).requires_grad_(not k.endswith(PU.BUFFER_LEAVES))
+                   if v.is_floating_point() else v.clone()) for k, v in sd.items()}
+        o = O.forward(sdo, x.to(dt), "canonical", training=True, n_classes=nc)
+        (o * go.to(dt)).sum().backward()
+        res[dt] = (o.detach(), {k: v.grad for k, v in sdo.items() if v.is_floating_point()
+                                and not k.endswith(PU.BUFFER_LEAVES)})
+    (o64, g64), (o32, g32) = res[torch.float64], res[torch.float32]
+    e_h = (out.detach().double().cpu() - o64).abs().max().item()
+    e_r = (o32.double() - o64).abs().max().item()
+    assert e_h <= 4 * e_r + 1e-4 * o64.abs().max().item(), (e_h, e_r)
+    hip = {k: p.grad for k, p in m.named_parameters()}
+    for k in ("out.weight", "out.bias", "cnv92.conv3.weight", "cnv11.conv1.weight"):
+        eh = (hip[k].double().cpu() - g64[k]).abs().max().item()
+        er = (g32[k].double() - g64[k]).abs().max().item()
+        assert eh <= 4 * er + 1e-4 * g64[k].abs().max().item(), (k, eh, er)
+    gk = [k for k in g64 if hip.get(k) is not None]
+    num = sum(float((hip[k].double().cpu() - g64[k]).norm() ** 2) for k in gk)
+    num32 = sum(float((g32[k].double() - g64[k]).norm() ** 2) for k in gk)
+    assert num ** 0.5 <= 3 * num32 ** 0.5 + 1e-9, (num ** 0.5, num32 ** 0.5)

@@ -47,23 +47,11 @@ def test_state_dict_keys_match_reference(variant):
     assert n == ref["n_params"]
 
 
-@pytest.mark.parametrize("variant", O.VARIANTS)
-def test_whole_model_nf8_matches_reference(variant):
-    g = np.load(os.path.join(GOLD, f"model_{variant}_nf8.npz"))
-    spec = O.param_spec(variant, 3, 1, 8)
-    x = O.det_input((2, 3, 32, 32), "golden-x")
-    mask = O.det_mask((2, 1, 32, 32), "golden-mask", p=0.4)
-    sd = O.det_state_dict(spec, seed=0)
-    with torch.no_grad():
-        out_eval = O.forward({k: v.clone() for k, v in sd.items()}, x, variant, training=False)
-    np.testing.assert_allclose(out_eval.numpy(), g["out_eval"], rtol=0, atol=2e-5)
-
-    params = oracle_params(sd)
-    out = O.forward(sd, x, variant, training=True)
-    np.testing.assert_allclose(out.detach().numpy(), g["out_train"], rtol=0, atol=2e-5)
-    loss = O.dice_bce_loss(out, mask.clone())
-    assert abs(loss.item() - float(g["loss"])) < 1e-5
-    loss.backward()
+def check_grad_summary(params, g, rtol=2e-3, se_rtol=2e-2):
+    """The oracle's parameter gradients against the reference's per-tensor summaries
+    (sum |g|, 8 samples) written by make_golden.grad_summary. SE gate fc1 gradients
+    are sums of per-sample terms that the SE's own batch BatchNorm nearly cancels
+    (few samples), so their fp32 op-order noise is ~10x larger: se_rtol."""
     names = list(g["grad_names"])
     assert names == [k for k in params]
     # model-wide gradient scale: median per-element mean |g|; absolute floors are
@@ -85,11 +73,32 @@ def test_whole_model_nf8_matches_reference(variant):
             continue
         # sums of |g| and g^2 are robust; the plain sum can cancel to ~0
         # (rtol 2e-3 plus the absolute floor per element)
-        assert abs(gr.abs().sum().item() - ref_abs) <= 2e-3 * ref_abs + floor * gr.numel(), n
+        rt = se_rtol if ".fc1." in n else rtol
+        assert abs(gr.abs().sum().item() - ref_abs) <= rt * ref_abs + floor * gr.numel(), n
         idx = torch.linspace(0, gr.numel() - 1, 8).long()
         scale = gr.abs().max().item()
         np.testing.assert_allclose(gr[idx].numpy(), g["grad_samples"][i],
-                                   rtol=0, atol=2e-3 * scale + floor, err_msg=n)
+                                   rtol=0, atol=rt * scale + floor, err_msg=n)
+
+
+@pytest.mark.parametrize("variant", O.VARIANTS)
+def test_whole_model_nf8_matches_reference(variant):
+    g = np.load(os.path.join(GOLD, f"model_{variant}_nf8.npz"))
+    spec = O.param_spec(variant, 3, 1, 8)
+    x = O.det_input((2, 3, 32, 32), "golden-x")
+    mask = O.det_mask((2, 1, 32, 32), "golden-mask", p=0.4)
+    sd = O.det_state_dict(spec, seed=0)
+    with torch.no_grad():
+        out_eval = O.forward({k: v.clone() for k, v in sd.items()}, x, variant, training=False)
+    np.testing.assert_allclose(out_eval.numpy(), g["out_eval"], rtol=0, atol=2e-5)
+
+    params = oracle_params(sd)
+    out = O.forward(sd, x, variant, training=True)
+    np.testing.assert_allclose(out.detach().numpy(), g["out_train"], rtol=0, atol=2e-5)
+    loss = O.dice_bce_loss(out, mask.clone())
+    assert abs(loss.item() - float(g["loss"])) < 1e-5
+    loss.backward()
+    check_grad_summary(params, g)
     bnames = list(g["buf_names"])
     for i, n in enumerate(bnames):
         assert abs(sd[n].double().sum().item() - float(g["buf_sums"][i])) < 1e-4, n
@@ -142,3 +151,33 @@ def test_lr_schedule_matches_reference():
     g = np.load(os.path.join(GOLD, "lr_schedule.npz"))
     lrs = [O.cosine_warm_restarts_lr(1e-3, 1e-5, 10, e) for e in range(25)]
     np.testing.assert_allclose(lrs, g["lrs"], rtol=1e-9)
+
+
+@pytest.mark.parametrize("variant", ["canonical", "script"])
+def test_fullwidth_nf32_at_256_matches_reference(variant):
+    """The full-width models (n_filts 32; canonical 16.77 M with cnv72 inv_fctr 34,
+    ACC_UNet/ACC_UNet.py:584) at the bench resolution: train fwd + loss + bwd on
+    2x3x256x256 (and the canonical eval output on 1x3x256x256) against the reference's
+    own fp32 run (tests/golden/fullwidth_*_nf32.npz)."""
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    g = np.load(os.path.join(GOLD, f"fullwidth_{variant}_nf32.npz"))
+    spec = O.param_spec(variant, 3, 1, 32)
+    sd = O.det_state_dict(spec, seed=7)
+    if variant == "canonical":
+        with torch.no_grad():
+            oe = O.forward({k: v.clone() for k, v in sd.items()},
+                           O.det_input((1, 3, 256, 256), "fw-x1"), variant, training=False)
+        np.testing.assert_allclose(oe.numpy(), g["out_eval"], rtol=0, atol=2e-5)
+    x = O.det_input((2, 3, 256, 256), "fw-x2")
+    mask = O.det_mask((2, 1, 256, 256), "fw-mask", p=0.3)
+    params = oracle_params(sd)
+    out = O.forward(sd, x, variant, training=True)
+    scale = float(np.abs(g["out_train"]).max())
+    np.testing.assert_allclose(out.detach().numpy(), g["out_train"], rtol=0, atol=2e-5 * max(1.0, scale))
+    loss = O.dice_bce_loss(out, mask.clone())
+    assert abs(loss.item() - float(g["loss"])) < 1e-5
+    loss.backward()
+    check_grad_summary(params, g)
+    for i, n in enumerate(list(g["buf_names"])):
+        assert abs(sd[n].double().sum().item() - float(g["buf_sums"][i])) < 1e-4 * max(1.0, abs(float(g["buf_sums"][i]))), n
+    assert abs(O.show_dice(out.detach(), mask.clone()).item() - float(g["show_dice"])) < 1e-6

@@ -93,6 +93,30 @@ def test_loop_schedule_checkpoint_early_stop_resume(tmp_path):
     assert opt2.state_dict()["state"][0]["exp_avg"].shape == model2[0].weight.shape
 
 
+def test_resume_restarts_cosine_schedule_at_base_lr(tmp_path):
+    """train_model.py:677,738: the scheduler is built after optimizer.load_state_dict,
+    so a resumed run's first epoch uses initial_lr, not the checkpoint's mid-cycle LR."""
+    torch.manual_seed(0)
+    model = nn.Conv2d(1, 1, 3, padding=1)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    sched = CosineAnnealingWarmRestarts(opt, T_0=10, T_mult=1, eta_min=1e-5)
+    for _ in range(4):
+        sched.step()
+    assert opt.param_groups[0]["lr"] < 1e-3 * 0.9  # mid-cycle
+    T.save_checkpoint({"epoch": 3, "best_model": True, "model": "T",
+                       "state_dict": model.state_dict(), "val_loss": 0.0, "val_dice": 0.5,
+                       "optimizer": opt.state_dict()}, str(tmp_path))
+    model2 = nn.Conv2d(1, 1, 3, padding=1)
+    opt2 = torch.optim.Adam(model2.parameters(), lr=1e-3)
+    tr = T.Trainer(model2, "T", str(tmp_path), criterion=OracleLoss(), optimizer=opt2,
+                   device=torch.device("cpu"))
+    assert tr.resume()
+    assert opt2.param_groups[0]["lr"] == 1e-3
+    assert abs(opt2.param_groups[0]["lr"] - O.cosine_warm_restarts_lr(1e-3, 1e-5, 10, 0)) < 1e-15
+    tr.lr_scheduler.step()
+    assert abs(opt2.param_groups[0]["lr"] - O.cosine_warm_restarts_lr(1e-3, 1e-5, 10, 1)) < 1e-15
+
+
 def test_epoch_average_is_per_image(tmp_path):
     model = nn.Conv2d(1, 1, 1)
     crit = OracleLoss()
@@ -129,17 +153,20 @@ def test_trainer_acc_unet_gpu(tmp_path):
     assert len(tr.history) == 4
     assert all(h["loss"] == h["loss"] for h in tr.history)
     fn = os.path.join(str(tmp_path), "best_model-ACC_UNet.pth.tar")
-    if tr.max_dice > 0:
-        ck = T.load_checkpoint(fn)
-        assert set(ck) == CK_KEYS
-        m2 = ACC_UNet(3, 1, n_filts=8).to(dev)
-        tr2 = T.Trainer(m2, "ACC_UNet", str(tmp_path))
-        assert tr2.resume()
-        for k, v in ck["state_dict"].items():
-            assert torch.equal(m2.state_dict()[k].cpu(), v.cpu())
-        # the restored optimizer state drives the next HIP Adam step
-        tr2.train_one_epoch(train, tr2.start_epoch, training=True)
-        assert all(torch.isfinite(p).all() for p in m2.parameters())
+    # the canonical head outputs probabilities, so _show_dice's second sigmoid makes
+    # the hard mask all-ones: val Dice = 2|m|/(|m|+N) > 0 for any
+    # non-empty mask, the first validation pass always improves on 0 and saves
+    assert tr.max_dice > 0
+    ck = T.load_checkpoint(fn)
+    assert set(ck) == CK_KEYS
+    m2 = ACC_UNet(3, 1, n_filts=8).to(dev)
+    tr2 = T.Trainer(m2, "ACC_UNet", str(tmp_path))
+    assert tr2.resume()
+    for k, v in ck["state_dict"].items():
+        assert torch.equal(m2.state_dict()[k].cpu(), v.cpu())
+    # the restored optimizer state drives the next HIP Adam step
+    tr2.train_one_epoch(train, tr2.start_epoch, training=True)
+    assert all(torch.isfinite(p).all() for p in m2.parameters())
 
 
 def test_eval_metrics_match_test_model_restatement():
