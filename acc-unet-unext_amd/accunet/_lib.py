@@ -19,6 +19,7 @@ AMODE_ROW, AMODE_COL, AMODE_SHIFT3 = 0, 1, 2
 BMODE_NT, BMODE_NN, BMODE_NN_SHIFT3 = 0, 1, 2
 PRO_NONE, PRO_AFFINE, PRO_AFFINE_LRELU = 0, 1, 2
 ACT_NONE, ACT_LRELU = 0, 1
+ACC_F32, ACC_BF16 = 0, 1
 
 
 class AccGemmDesc(Structure):
@@ -44,6 +45,7 @@ class AccGemmDesc(Structure):
         ("pd2", c_void_p), ("pd4", c_void_p),  # fused pyramid backward (float*)
         ("mk2", c_void_p), ("mk4", c_void_p),  # first-max codes (uint8*)
         ("bz", c_void_p), ("bst", c_void_p), ("bact", c_int),  # BN-backward epilogue stats
+        ("adt", c_int), ("bdt", c_int), ("cdt", c_int),  # storage: ACC_F32 / ACC_BF16
     ]
 
 
@@ -61,44 +63,44 @@ _SIGS = {
     "accunet_gemm_stats_rows": [I, I, I, I, I, I],
     "accunet_stream_rows": [L, I],
     "accunet_bn_finalize": [P, I, I, D, P, P, P, P, P, F, F, I, P, P, P],
-    "accunet_affine_act_fwd": [P, P, P, I, P, P, L, I, P, IP, P],
+    "accunet_affine_act_fwd": [P, P, P, I, P, P, L, I, P, IP, I, P],
     "accunet_bn_bwd_ws_elems": [L, I],
-    "accunet_bn_bwd": [P, P, P, P, I, I, L, I, P, I, P, P, P, P, S, P],
-    "accunet_colsum": [P, L, I, P, P, S, P],
+    "accunet_bn_bwd": [P, P, P, P, I, I, L, I, P, I, P, P, P, P, S, I, P],
+    "accunet_colsum": [P, L, I, P, P, S, I, P],
     "accunet_reduce_stats": [P, I, I, P, P, P],
     "accunet_dw3x3_rows": [I, I, I, I],
-    "accunet_dw3x3_fwd": [P, P, P, P, P, I, I, P, P, I, I, I, I, P, P, I, P],
+    "accunet_dw3x3_fwd": [P, P, P, P, P, I, I, P, P, I, I, I, I, P, P, I, I, P],
     "accunet_bn_bwd_part_ws_elems": [L, I, I],
-    "accunet_bn_bwd_part": [P, P, P, P, I, I, L, I, P, I, P, P, P, P, P, S, P],
+    "accunet_bn_bwd_part": [P, P, P, P, I, I, L, I, P, I, P, P, P, P, P, S, I, P],
     "accunet_dw3x3_wgrad_ws": [I, I, I, I],
-    "accunet_dw3x3_wgrad": [P, P, P, P, I, P, P, I, I, I, I, P, S, P],
-    "accunet_hanc_pyramid_fwd": [P, P, P, I, I, I, I, I, I, P, P, P, P, P],
-    "accunet_hanc_pyramid_bwd": [P, P, P, I, I, I, I, I, I, P, P, P, P, P, P],
-    "accunet_pool2_fwd": [P, P, I, I, I, I, I, P],
-    "accunet_pool2_bwd": [P, P, P, P, I, I, I, I, I, I, P],
-    "accunet_upsample_bwd": [P, I, I, P, I, I, I, I, I, I, I, P],
-    "accunet_slice_copy": [P, I, I, P, I, I, L, I, I, P],
-    "accunet_pixel_shuffle2": [P, P, P, I, I, I, I, I, P],
-    "accunet_permute4": [P, P, IP, POINTER(c_longlong), IP, I, P],
+    "accunet_dw3x3_wgrad": [P, P, P, P, I, P, P, I, I, I, I, P, S, I, P],
+    "accunet_hanc_pyramid_fwd": [P, P, P, I, I, I, I, I, I, P, P, P, P, I, P],
+    "accunet_hanc_pyramid_bwd": [P, P, P, I, I, I, I, I, I, P, P, P, P, P, I, P],
+    "accunet_pool2_fwd": [P, P, I, I, I, I, I, I, P],
+    "accunet_pool2_bwd": [P, P, P, P, I, I, I, I, I, I, I, P],
+    "accunet_upsample_bwd": [P, I, I, P, I, I, I, I, I, I, I, I, P],
+    "accunet_slice_copy": [P, I, I, P, I, I, L, I, I, I, P],
+    "accunet_pixel_shuffle2": [P, P, P, I, I, I, I, I, I, P],
+    "accunet_permute4": [P, P, IP, POINTER(c_longlong), IP, I, I, I, P],
     "accunet_group_relayout": [P, P, I, I, I, IP, I, P],
     "accunet_se_save_elems": [I, I, I],
     "accunet_se_ws_elems": [I, I, I, I],
-    "accunet_se_fwd": [P, P, P, I, I, I, I, I, P, P, P, P, P, P, P, P, P, F, F, I, P, P, P, P, S, P],
+    "accunet_se_fwd": [P, P, P, I, I, I, I, I, P, P, P, P, P, P, P, P, P, F, F, I, P, P, P, P, S, I, P],
     "accunet_se_stats_rows": [I, I, I],
-    "accunet_se_bwd": [P, P, P, P, I, I, I, I, I, P, P, P, I, P, P, P, P, P, P, P, P, P, S, P],
+    "accunet_se_bwd": [P, P, P, P, I, I, I, I, I, P, P, P, I, P, P, P, P, P, P, P, P, P, S, I, P],
     "accunet_se_bwd_pro": [P, P, P, I, P, I, I, I, I, I, P, P, P, I, P, P, P, P, P, P, P, P, P, P,
-                           P, P, S, P],
-    "accunet_head_fwd": [P, P, P, I, P, L, I, P],
+                           P, P, S, I, P],
+    "accunet_head_fwd": [P, P, P, I, P, L, I, I, P],
     "accunet_head_ws_elems": [L, I],
-    "accunet_head_bwd": [P, P, P, P, I, P, P, P, L, I, P, S, P],
+    "accunet_head_bwd": [P, P, P, P, I, P, P, P, L, I, P, S, I, P],
     "accunet_loss_ws_elems": [I],
     "accunet_loss_fwd": [P, P, I, L, F, F, P, P, S, P],
     "accunet_loss_bwd": [P, P, I, L, F, F, P, P, P, P],
     "accunet_adam_chunk_elems": [],
     "accunet_adam_step": [P, P, P, I, F, F, F, F, F, I, P],
-    "accunet_dotdiff": [P, P, P, L, P, I, P, P],
-    "accunet_wmerge_fwd": [P, P, P, P, L, I, P, P],
-    "accunet_wmerge_bwd": [P, P, P, P, L, P],
+    "accunet_dotdiff": [P, P, P, L, P, I, P, I, P],
+    "accunet_wmerge_fwd": [P, P, P, P, L, I, P, I, P],
+    "accunet_wmerge_bwd": [P, P, P, P, L, I, P],
     "accunet_image_prep": [P, I, I, I, I, P, P],
     "accunet_mask_prep": [P, I, I, I, I, I, P, P],
     "accunet_dwconvk_out_hw": [I, I, I, I, I, I, IP, IP],

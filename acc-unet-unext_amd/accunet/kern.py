@@ -25,11 +25,31 @@ def _p(t: Optional[torch.Tensor]):
     return ctypes.c_void_p(t.data_ptr())
 
 
-def _check(t: torch.Tensor, name: str):
+_DT = {torch.float32: _lib.ACC_F32, torch.bfloat16: _lib.ACC_BF16}
+
+
+def _check(t: torch.Tensor, name: str, act: bool = False):
+    """Device tensor of fp32 (or, for activation operands, act=True, fp32 / bf16)."""
     if not t.is_cuda:
         raise _lib.AccError(f"{name}: expected a device tensor (HIP), got {t.device}")
-    if t.dtype != torch.float32:
-        raise _lib.AccError(f"{name}: expected float32, got {t.dtype}")
+    if t.dtype != torch.float32 and not (act and t.dtype == torch.bfloat16):
+        raise _lib.AccError(f"{name}: expected float32{' or bfloat16' if act else ''}, "
+                            f"got {t.dtype}")
+
+
+def _dt(t: torch.Tensor) -> int:
+    """ACC_F32 / ACC_BF16 storage code of an activation tensor (include/accunet.h)."""
+    try:
+        return _DT[t.dtype]
+    except KeyError:
+        raise _lib.AccError(f"activation storage must be float32 or bfloat16, got {t.dtype}")
+
+
+def _same_dt(ref: torch.Tensor, *ts):
+    for t in ts:
+        if t is not None and t.dtype != ref.dtype:
+            raise _lib.AccError(f"mixed activation storage: {t.dtype} vs {ref.dtype}")
+    return _dt(ref)
 
 
 def workspace(n_elems: int, device, dtype=torch.float32) -> torch.Tensor:
@@ -66,30 +86,34 @@ def gemm(M: int, N: int, K: int, *, a: Sequence[torch.Tensor], lda: Sequence[int
     d.nsrc = len(a)
     offs = a_offsets or [0] * len(a)
     for i, (t, ld) in enumerate(zip(a, lda)):
-        _check(t, "gemm.a")
-        d.a[i] = t.data_ptr() + 4 * int(offs[i])
+        _check(t, "gemm.a", act=True)
+        d.a[i] = t.data_ptr() + t.element_size() * int(offs[i])
         d.lda[i] = int(ld)
+    d.adt = _same_dt(a[0], *a[1:])
     if kbeg is None:
         kbeg = [0, K]
     for i, v in enumerate(kbeg):
         d.kbeg[i] = int(v)
     d.a_scale = a_scale.data_ptr() if a_scale is not None else None
     d.a_shift = a_shift.data_ptr() if a_shift is not None else None
-    _check(b, "gemm.b")
-    d.b = b.data_ptr() + 4 * int(b_offset)
+    _check(b, "gemm.b", act=True)
+    d.b = b.data_ptr() + b.element_size() * int(b_offset)
+    d.bdt = _dt(b)
     d.ldb = int(ldb)
     d.b_scale = b_scale.data_ptr() if b_scale is not None else None
     d.b_shift = b_shift.data_ptr() if b_shift is not None else None
     d.H, d.W, d.cin = int(H), int(W), int(cin)
-    _check(c, "gemm.c")
-    d.c = c.data_ptr() + 4 * int(c_offset)
+    _check(c, "gemm.c", act=True)
+    d.c = c.data_ptr() + c.element_size() * int(c_offset)
+    d.cdt = _dt(c)
     d.ldc = int(ldc)
     d.bias = bias.data_ptr() if bias is not None else None
     d.nup = len(ups)
     for i, u in enumerate(ups):
         t, ld, lg = u[0], u[1], u[2]
         off = u[3] if len(u) > 3 else 0
-        d.up[i] = t.data_ptr() + 4 * int(off)
+        _same_dt(c, t)
+        d.up[i] = t.data_ptr() + t.element_size() * int(off)
         d.upld[i] = int(ld)
         d.uplog[i] = int(lg)
     if stats is not None and stats.dtype != torch.float64:
@@ -98,7 +122,8 @@ def gemm(M: int, N: int, K: int, *, a: Sequence[torch.Tensor], lda: Sequence[int
     d.allow_split = 1 if allow_split else 0
     if pyr is not None:
         pd2, pd4, mk2, mk4 = pyr
-        _check(pd2, "gemm.pd2")
+        _check(pd2, "gemm.pd2", act=True)
+        _same_dt(c, pd2, pd4)
         if mk2.dtype != torch.uint8 or (mk4 is not None and mk4.dtype != torch.uint8):
             raise _lib.AccError("gemm.pyr: uint8 first-max codes expected")
         d.pd2 = pd2.data_ptr()
@@ -107,7 +132,8 @@ def gemm(M: int, N: int, K: int, *, a: Sequence[torch.Tensor], lda: Sequence[int
         d.mk4 = mk4.data_ptr() if mk4 is not None else None
     if bnb is not None:
         bz, bst, bact = bnb
-        _check(bz, "gemm.bz")
+        _check(bz, "gemm.bz", act=True)
+        _same_dt(c, bz)
         if stats is None:
             raise _lib.AccError("gemm.bnb needs a stats buffer")
         d.bz = bz.data_ptr()
@@ -154,7 +180,7 @@ def affine_act(x: torch.Tensor, sc, sh, act: int, res, y: torch.Tensor, P: int, 
                stats: Optional[torch.Tensor] = None) -> int:
     rows = ctypes.c_int(0)
     call("accunet_affine_act_fwd", _p(x), _p(sc), _p(sh), int(act), _p(res), _p(y), int(P),
-         int(C), _p(stats), ctypes.byref(rows), _stream())
+         int(C), _p(stats), ctypes.byref(rows), _same_dt(x, res, y), _stream())
     return rows.value
 
 
@@ -165,7 +191,7 @@ def bn_bwd(x, dy, st, gamma, act: int, training: bool, P: int, C: int, dx, accum
     ws = workspace(ws_elems, x.device)
     call("accunet_bn_bwd", _p(x), _p(dy), _p(st), _p(gamma), int(act), 1 if training else 0,
          int(P), int(C), _p(dx), 1 if accumulate else 0, _p(dgamma), _p(dbeta), _p(dsum),
-         _p(ws), ws_elems, _stream())
+         _p(ws), ws_elems, _same_dt(x, dy, dx), _stream())
     return ws
 
 
@@ -177,7 +203,7 @@ def bn_bwd_part(x, dy, st, gamma, act: int, training: bool, P: int, C: int, part
     ws = workspace(ws_elems, x.device)
     call("accunet_bn_bwd_part", _p(x), _p(dy), _p(st), _p(gamma), int(act), 1 if training else 0,
          int(P), int(C), _p(part), int(R), _p(dx), _p(dgamma), _p(dbeta), _p(dsum), _p(ws),
-         ws_elems, _stream())
+         ws_elems, _same_dt(x, dy, dx), _stream())
     return ws
 
 
@@ -185,7 +211,7 @@ def colsum(x, P: int, C: int, out):
     nb = stream_rows(P, C)
     ws_elems = nb * 2 * C + partial_ws_elems(nb, 2 * C)
     ws = workspace(ws_elems, x.device, torch.float64)
-    call("accunet_colsum", _p(x), int(P), int(C), _p(out), _p(ws), ws_elems, _stream())
+    call("accunet_colsum", _p(x), int(P), int(C), _p(out), _p(ws), ws_elems, _dt(x), _stream())
     return ws
 
 
@@ -208,60 +234,61 @@ def dw3x3_fwd(x, wt, bias, sc, sh, act, flip, z, stats, B, H, W, C, bnb=None):
     accunet_dw3x3_fwd in include/accunet.h)."""
     bz, bst, bact = bnb if bnb is not None else (None, None, 0)
     call("accunet_dw3x3_fwd", _p(x), _p(wt), _p(bias), _p(sc), _p(sh), int(act), int(flip), _p(z),
-         _p(stats), B, H, W, C, _p(bz), _p(bst), int(bact), _stream())
+         _p(stats), B, H, W, C, _p(bz), _p(bst), int(bact), _same_dt(x, z, bz), _stream())
 
 
 def dw3x3_wgrad(x, dz, sc, sh, act, dw, db, B, H, W, C):
     n = int(_lib_raw().accunet_dw3x3_wgrad_ws(B, H, W, C))
     ws = workspace(n, x.device)
     call("accunet_dw3x3_wgrad", _p(x), _p(dz), _p(sc), _p(sh), int(act), _p(dw), _p(db), B, H, W,
-         C, _p(ws), n, _stream())
+         C, _p(ws), n, _same_dt(x, dz), _stream())
     return ws
 
 
 def hanc_pyramid_fwd(x, sc, sh, act, B, H, W, C, k, p2, p4, mk2=None, mk4=None):
     call("accunet_hanc_pyramid_fwd", _p(x), _p(sc), _p(sh), int(act), B, H, W, C, k, _p(p2),
          _p(p4), None if mk2 is None else mk2.data_ptr(),
-         None if mk4 is None else mk4.data_ptr(), _stream())
+         None if mk4 is None else mk4.data_ptr(), _same_dt(x, p2, p4), _stream())
 
 
 def hanc_pyramid_bwd(x, sc, sh, act, B, H, W, C, k, p2, p4, dp2, dp4, da):
     call("accunet_hanc_pyramid_bwd", _p(x), _p(sc), _p(sh), int(act), B, H, W, C, k, _p(p2),
-         _p(p4), _p(dp2), _p(dp4), _p(da), _stream())
+         _p(p4), _p(dp2), _p(dp4), _p(da), _same_dt(x, p2, p4, dp2, dp4, da), _stream())
 
 
 POOL_MAX, POOL_AVG = 0, 1
 
 
 def pool2_fwd(x, y, B, H, W, C, mode):
-    call("accunet_pool2_fwd", _p(x), _p(y), B, H, W, C, mode, _stream())
+    call("accunet_pool2_fwd", _p(x), _p(y), B, H, W, C, mode, _same_dt(x, y), _stream())
 
 
 def pool2_bwd(x, y, dy, dx, B, H, W, C, mode, accumulate=False):
     call("accunet_pool2_bwd", _p(x), _p(y), _p(dy), _p(dx), B, H, W, C, mode,
-         1 if accumulate else 0, _stream())
+         1 if accumulate else 0, _same_dt(x, y, dy, dx), _stream())
 
 
 def upsample_bwd(inp, ld_in, in_off, out, ld_out, B, H, W, C, f, accumulate=False):
     call("accunet_upsample_bwd", _p(inp), int(ld_in), int(in_off), _p(out), int(ld_out), B, H, W,
-         C, int(f), 1 if accumulate else 0, _stream())
+         C, int(f), 1 if accumulate else 0, _same_dt(inp, out), _stream())
 
 
 def slice_copy(src, ld_src, src_off, dst, ld_dst, dst_off, P, C, accumulate=False):
     call("accunet_slice_copy", _p(src), int(ld_src), int(src_off), _p(dst), int(ld_dst),
-         int(dst_off), int(P), int(C), 1 if accumulate else 0, _stream())
+         int(dst_off), int(P), int(C), 1 if accumulate else 0, _same_dt(src, dst), _stream())
 
 
 def pixel_shuffle2(t, bias, y, B, Hi, Wi, Cout, inverse=False):
     call("accunet_pixel_shuffle2", _p(t), _p(bias), _p(y), B, Hi, Wi, Cout, 1 if inverse else 0,
-         _stream())
+         _same_dt(t, y), _stream())
 
 
 def permute4(inp, out, dims, strides, flips=None, accumulate=False):
     d = (ctypes.c_int * 4)(*[int(v) for v in dims])
     s = (ctypes.c_longlong * 4)(*[int(v) for v in strides])
     f = (ctypes.c_int * 4)(*[int(v) for v in (flips or (0, 0, 0, 0))])
-    call("accunet_permute4", _p(inp), _p(out), d, s, f, 1 if accumulate else 0, _stream())
+    call("accunet_permute4", _p(inp), _p(out), d, s, f, 1 if accumulate else 0, _dt(inp),
+         _dt(out), _stream())
 
 
 def group_relayout(inp, out, N, C, J, order, inverse=False):
@@ -288,7 +315,8 @@ def se_fwd(z, sc, sh, act, B, HW, C, Cr, w1, b1, w2, b2, gamma, beta, rmean, rva
     ws = workspace(n, z.device)
     call("accunet_se_fwd", _p(z), _p(sc), _p(sh), int(act), B, HW, C, Cr, _p(w1), _p(b1), _p(w2),
          _p(b2), _p(gamma), _p(beta), _p(rmean), _p(rvar), _p(nbt), float(momentum), float(eps),
-         1 if training else 0, _p(out), _p(save), _p(ostats), _p(ws), n, _stream())
+         1 if training else 0, _p(out), _p(save), _p(ostats), _p(ws), n, _same_dt(z, out),
+         _stream())
     return ws
 
 
@@ -298,7 +326,7 @@ def se_bwd(z, dout, sc, sh, act, B, HW, C, Cr, w1, w2, gamma, training, save, da
     ws = workspace(n, z.device)
     call("accunet_se_bwd", _p(z), _p(dout), _p(sc), _p(sh), int(act), B, HW, C, Cr, _p(w1),
          _p(w2), _p(gamma), 1 if training else 0, _p(save), _p(da), _p(dw1), _p(db1), _p(dw2),
-         _p(db2), _p(dgamma), _p(dbeta), _p(ws), n, _stream())
+         _p(db2), _p(dgamma), _p(dbeta), _p(ws), n, _same_dt(z, dout, da), _stream())
     return ws
 
 
@@ -311,20 +339,20 @@ def se_bwd_pro(z, dout, pst, act, pgamma, ptraining, B, HW, C, Cr, w1, w2, gamma
     call("accunet_se_bwd_pro", _p(z), _p(dout), _p(pst), int(act), _p(pgamma),
          1 if ptraining else 0, B, HW, C, Cr, _p(w1), _p(w2), _p(gamma), 1 if training else 0,
          _p(save), _p(dz), _p(dpgamma), _p(dpbeta), _p(dsum), _p(dw1), _p(db1), _p(dw2), _p(db2),
-         _p(dgamma), _p(dbeta), _p(ws), n, _stream())
+         _p(dgamma), _p(dbeta), _p(ws), n, _same_dt(z, dout, dz), _stream())
     return ws
 
 
 def head_fwd(x, w, b, sigm, y, P, C):
     call("accunet_head_fwd", _p(x), _p(w), _p(b), 1 if sigm else 0, _p(y), int(P), int(C),
-         _stream())
+         _dt(x), _stream())
 
 
 def head_bwd(x, w, y, dy, sigm, dx, dw, db, P, C):
     n = int(_lib_raw().accunet_head_ws_elems(int(P), int(C)))
     ws = workspace(n, x.device)
     call("accunet_head_bwd", _p(x), _p(w), _p(y), _p(dy), 1 if sigm else 0, _p(dx), _p(dw),
-         _p(db), int(P), int(C), _p(ws), n, _stream())
+         _p(db), int(P), int(C), _p(ws), n, _same_dt(x, dx), _stream())
     return ws
 
 
@@ -353,16 +381,18 @@ def adam_step(table, chunk_t, chunk_s, nchunks, lr, b1, b2, eps, wd, step):
 def dotdiff(g, a, b, n, out, accumulate=False):
     ws = workspace(1024, g.device)
     call("accunet_dotdiff", _p(g), _p(a), _p(b), int(n), _p(out), 1 if accumulate else 0, _p(ws),
-         _stream())
+         _same_dt(g, a, b), _stream())
     return ws
 
 
 def wmerge_fwd(a, b, w, y, P, C, stats=None):
-    call("accunet_wmerge_fwd", _p(a), _p(b), _p(w), _p(y), int(P), int(C), _p(stats), _stream())
+    call("accunet_wmerge_fwd", _p(a), _p(b), _p(w), _p(y), int(P), int(C), _p(stats),
+         _same_dt(a, b, y), _stream())
 
 
 def wmerge_bwd(g, w, da, db, n):
-    call("accunet_wmerge_bwd", _p(g), _p(w), _p(da), _p(db), int(n), _stream())
+    call("accunet_wmerge_bwd", _p(g), _p(w), _p(da), _p(db), int(n), _same_dt(g, da, db),
+         _stream())
 
 
 def image_prep(raw, N, Hin, Win, S, out):

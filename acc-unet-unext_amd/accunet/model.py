@@ -292,10 +292,11 @@ class ACC_UNet(nn.Module):
     _sigmoid_head = True
     _mlfc_cls = MLFC
 
-    def __init__(self, n_channels, n_classes, n_filts=32):
+    def __init__(self, n_channels, n_classes, n_filts=32, *, precision="fp32"):
         super().__init__()
         self.n_channels = n_channels
         self.n_classes = n_classes
+        self.set_precision(precision)
         f = n_filts
         self.pool = nn.MaxPool2d(2)
         self.cnv11 = HANCBlock(n_channels, f, k=3, inv_fctr=3)
@@ -335,13 +336,32 @@ class ACC_UNet(nn.Module):
             self.out = nn.Conv2d(f, n_classes + 1, kernel_size=(1, 1))
             self.last_activation = None
 
+    def set_precision(self, precision: str):
+        """Activation storage of the training / inference step.
+
+        "fp32" (default): the reference's arithmetic (it trains in fp32,
+            Experiments/train_model.py:647), fp32 activations and fp32 MFMA GEMMs.
+        "bf16": BASELINE configs[2] mixed precision. Activations and activation
+            gradients are stored bf16 in HBM and every convolution runs on the bf16
+            MFMA engine (v_mfma_f32_32x32x16_bf16, fp32 accumulation); parameters,
+            their gradients, the Adam state, the BatchNorm / SE statistics (fp64
+            partials, fp32 running stats) and the model output stay fp32.
+        Parameters and state_dict are unchanged, so checkpoints move freely between
+        the two modes."""
+        dt = {"fp32": torch.float32, "bf16": torch.bfloat16}.get(precision)
+        if dt is None:
+            raise ValueError(f"precision must be 'fp32' or 'bf16', got {precision!r}")
+        self.precision = precision
+        self.act_dtype = dt
+        return self
+
     def forward(self, x):
         B, C, H, W = x.shape
         if H % 16 or W % 16:
             raise ValueError(f"ACC_UNet: H and W must be divisible by 16, got {H}x{W}")
         if C != self.n_channels:
             raise ValueError(f"ACC_UNet: expected {self.n_channels} input channels, got {C}")
-        x1 = ops.to_nhwc(x)
+        x1 = ops.to_nhwc(x, self.act_dtype)
         x2 = self.cnv12.run(self.cnv11.run(x1))
         x3 = self.cnv22.run(self.cnv21.run(ops.pool2(x2)))
         x4 = self.cnv32.run(self.cnv31.run(ops.pool2(x3)))

@@ -1,6 +1,9 @@
 """Fused ACC-UNet operators as autograd Functions over the HIP C ABI.
 
-Activations are NHWC fp32 tensors [B, H, W, C]. A BatchNorm2d(+LeakyReLU) whose
+Activations are NHWC tensors [B, H, W, C], stored fp32 or bf16 (the model's
+activation dtype; every op keeps the dtype of its input, kern.* passes it to the
+kernels as ACC_F32 / ACC_BF16); parameters, their gradients and all BatchNorm / SE
+state stay fp32, statistics fp64. A BatchNorm2d(+LeakyReLU) whose
 statistics are known but which has not been applied yet travels as a `Pending`
 (tensor z + the BatchNorm module + the partial statistics its producer's epilogue
 wrote); the op that consumes it finalises the statistics (running-stat update
@@ -28,8 +31,14 @@ __all__ = ["Pending", "pw_conv", "dw_conv", "hanc_layer", "bn_act_add", "se", "c
            "to_nhwc", "weighted_dice_bce"]
 
 
-def _empty(shape, like):
+def _f32(shape, like):
+    """fp32 tensor (parameter-shaped / state / model output) on like's device."""
     return torch.empty(shape, dtype=torch.float32, device=like.device)
+
+
+def _act(shape, like):
+    """activation-shaped tensor with like's storage dtype (fp32 or bf16)."""
+    return torch.empty(shape, dtype=like.dtype, device=like.device)
 
 
 def _stats(shape, like):
@@ -109,7 +118,7 @@ def _finalize(p: Pending) -> _Pro:
     C = z.shape[-1]
     P = z.numel() // C
     training = bn.training or not bn.track_running_stats
-    st = _empty((4, C), z)
+    st = _f32((4, C), z)
     if training and p.part is None:
         raise RuntimeError("pending BatchNorm in training mode without producer statistics")
     mom = bn.momentum if bn.momentum is not None else 0.1
@@ -134,9 +143,9 @@ def _pro_bwd(pro: _Pro, z, gamma, dA, need_z=True, need_params=True):
     C = z.shape[-1]
     P = z.numel() // C
     dz = torch.empty_like(z)
-    dg = _empty((C,), z) if need_params else None
-    db = _empty((C,), z) if need_params else None
-    dsum = _empty((C,), z) if pro.bslot is not None else None
+    dg = _f32((C,), z) if need_params else None
+    db = _f32((C,), z) if need_params else None
+    dsum = _f32((C,), z) if pro.bslot is not None else None
     kern.bn_bwd(z, dA, pro.st, gamma, pro.act, pro.training, P, C, dz, False, dg, db, dsum)
     if dsum is not None:
         pro.bslot.t = dsum
@@ -149,9 +158,9 @@ def _pro_bwd_part(pro: _Pro, z, gamma, dA, part, R):
     C = z.shape[-1]
     P = z.numel() // C
     dz = torch.empty_like(z)
-    dg = _empty((C,), z)
-    db = _empty((C,), z)
-    dsum = _empty((C,), z) if pro.bslot is not None else None
+    dg = _f32((C,), z)
+    db = _f32((C,), z)
+    dsum = _f32((C,), z) if pro.bslot is not None else None
     kern.bn_bwd_part(z, dA, pro.st, gamma, pro.act, pro.training, P, C, part, R, dz, dg, db, dsum)
     if dsum is not None:
         pro.bslot.t = dsum
@@ -206,7 +215,7 @@ class _PWConvFn(torch.autograd.Function):
         for c in cfg.src_ch:
             kbeg.append(kbeg[-1] + c)
         K = kbeg[-1]
-        Z = _empty((B, H, W, N), weight)
+        Z = _act((B, H, W, N), srcs[0])
         stats = None
         rows = 0
         if cfg.want_stats:
@@ -223,7 +232,7 @@ class _PWConvFn(torch.autograd.Function):
         ctx.save_for_backward(weight, pro_g, *srcs)
         ctx.up_shapes = [u.shape for u in ups]
         if stats is None:
-            stats = _empty((0,), weight)
+            stats = _f32((0,), weight)
         ctx.mark_non_differentiable(stats)
         ctx.set_materialize_grads(False)
         ctx.rows = rows
@@ -249,7 +258,7 @@ class _PWConvFn(torch.autograd.Function):
             if not need:
                 d_srcs.append(None)
                 continue
-            dA = _empty((B, H, W, C), dZ)
+            dA = _act((B, H, W, C), dZ)
             if s == 0 and pro.active:
                 # the prologue BatchNorm's backward reduce rides in this GEMM's epilogue
                 R = kern.gemm_stats_rows(P, C, N)
@@ -278,15 +287,15 @@ class _PWConvFn(torch.autograd.Function):
         if cfg.has_bias and nig[2]:
             dbias = _take_bias_grad(cfg.bslot)
             if dbias is None:
-                dbias = _empty((N,), dZ)
+                dbias = _f32((N,), dZ)
                 keep.append(kern.colsum(dZ, P, N, dbias))
         d_ups = []
         for i, ((lg, off, ld), shp) in enumerate(zip(cfg.ups, ctx.up_shapes)):
             if not nig[5 + cfg.nsrc + i]:
                 d_ups.append(None)
                 continue
-            dG = torch.zeros(shp, dtype=torch.float32, device=dZ.device) if ld != N else \
-                torch.empty(shp, dtype=torch.float32, device=dZ.device)
+            dG = torch.zeros(shp, dtype=dZ.dtype, device=dZ.device) if ld != N else \
+                torch.empty(shp, dtype=dZ.dtype, device=dZ.device)
             kern.upsample_bwd(dZ, N, 0, _flat_off(dG, off), ld, B, H, W, N, 1 << lg)
             d_ups.append(dG)
         return (None, dW, dbias, dpro_g, dpro_b, *d_srcs, *d_ups)
@@ -339,7 +348,7 @@ class _DWConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, cfg: _DWCfg, z, pro_g, pro_b, weight, bias):
         B, H, W, C = cfg.B, cfg.H, cfg.W, cfg.C
-        Z = _empty((B, H, W, C), z)
+        Z = _act((B, H, W, C), z)
         stats = None
         if cfg.want_stats:
             stats = _stats((kern.dw3x3_rows(B, H, W, C), 2, C), z)
@@ -347,13 +356,14 @@ class _DWConvFn(torch.autograd.Function):
         # csrc/dwconv.hip picks the LDS-tiled kernel whenever C % 32 == 0
         kname = "dw3x3_tile_fwd_kernel" if C % 32 == 0 else "dw3x3_fwd_kernel"
         with _prof.region(f"dw3x3_fwd B{B} {H}x{W} C{C}", kernel=kname,
-                          shape=f"{B}x{H}x{W}x{C}", bytes_alg=2.0 * 4 * B * H * W * C):
+                          shape=f"{B}x{H}x{W}x{C}",
+                          bytes_alg=2.0 * z.element_size() * B * H * W * C):
             kern.dw3x3_fwd(z, weight, bias, pro.st[2] if pro.active else None,
                            pro.st[3] if pro.active else None, pro.act, 0, Z, stats, B, H, W, C)
         ctx.cfg = cfg
         ctx.save_for_backward(z, pro_g, weight)
         if stats is None:
-            stats = _empty((0,), z)
+            stats = _f32((0,), z)
         ctx.mark_non_differentiable(stats)
         ctx.set_materialize_grads(False)
         return Z, stats
@@ -378,7 +388,7 @@ class _DWConvFn(torch.autograd.Function):
         else:
             kern.dw3x3_fwd(dZ, weight, None, None, None, ACT_NONE, 1, dA, None, B, H, W, C)
         dW = torch.empty_like(weight)
-        db = _empty((C,), z)
+        db = _f32((C,), z)
         ws = kern.dw3x3_wgrad(z, dZ, pro.st[2] if pro.active else None,
                               pro.st[3] if pro.active else None, pro.act, dW, db, B, H, W, C)
         if pro.active:
@@ -434,31 +444,31 @@ class _HancLayerFn(torch.autograd.Function):
         pro = cfg.pro
         sc = pro.st[2] if pro.active else None
         sh = pro.st[3] if pro.active else None
-        Wp = _empty((N, J * C), z)
+        Wp = _f32((N, J * C), z)
         kern.group_relayout(weight, Wp, N, C, J, _HANC_ORDER[k])
         ups = []
         p2 = p4 = g2 = g4 = mk2 = mk4 = None
         if k >= 2:
-            p2 = _empty((B, H // 2, W // 2, 2 * C), z)
-            p4 = _empty((B, H // 4, W // 4, 2 * C), z) if k == 3 else None
+            p2 = _act((B, H // 2, W // 2, 2 * C), z)
+            p4 = _act((B, H // 4, W // 4, 2 * C), z) if k == 3 else None
             # first-max codes: the backward routes max-pool gradients with them inside
             # the x-branch data-gradient GEMM (no re-read of the activation)
             mk2 = torch.empty((B, H // 2, W // 2, C), dtype=torch.uint8, device=z.device)
             mk4 = (torch.empty((B, H // 4, W // 4, C), dtype=torch.uint8, device=z.device)
                    if k == 3 else None)
             kern.hanc_pyramid_fwd(z, sc, sh, pro.act, B, H, W, C, k, p2, p4, mk2, mk4)
-            g2 = _empty((B, H // 2, W // 2, N), z)
+            g2 = _act((B, H // 2, W // 2, N), z)
             # coarse branches: few output tiles, long K (2C) -> split-K
             keep_f = [kern.gemm(P // 4, N, 2 * C, a=[p2], lda=[2 * C], b=Wp, ldb=J * C,
                                 b_offset=C, c=g2, ldc=N, allow_split=True)]
             ups.append((g2, N, 1, 0))
             if k == 3:
-                g4 = _empty((B, H // 4, W // 4, N), z)
+                g4 = _act((B, H // 4, W // 4, N), z)
                 keep_f.append(kern.gemm(P // 16, N, 2 * C, a=[p4], lda=[2 * C], b=Wp,
                                         ldb=J * C, b_offset=3 * C, c=g4, ldc=N,
                                         allow_split=True))
                 ups.append((g4, N, 2, 0))
-        Z = _empty((B, H, W, N), z)
+        Z = _act((B, H, W, N), z)
         stats = None
         if cfg.want_stats:
             stats = _stats((kern.gemm_stats_rows(P, N, C), 2, N), z)
@@ -476,7 +486,7 @@ class _HancLayerFn(torch.autograd.Function):
                 saved += [p4, mk4]
         ctx.save_for_backward(*saved)
         if stats is None:
-            stats = _empty((0,), z)
+            stats = _f32((0,), z)
         ctx.mark_non_differentiable(stats)
         ctx.set_materialize_grads(False)
         return Z, stats
@@ -498,21 +508,21 @@ class _HancLayerFn(torch.autograd.Function):
         sc = pro.st[2] if pro.active else None
         sh = pro.st[3] if pro.active else None
         keep = []
-        dWp = _empty((N, J * C), z)
+        dWp = _f32((N, J * C), z)
         dP2 = dP4 = None
         if k >= 2:
-            dG2 = _empty((B, H // 2, W // 2, N), z)
+            dG2 = _act((B, H // 2, W // 2, N), dZ)
             kern.upsample_bwd(dZ, N, 0, dG2, N, B, H, W, N, 2)
-            dP2 = _empty(p2.shape, z)
+            dP2 = _act(p2.shape, dZ)
             keep.append(kern.gemm(P // 4, 2 * C, N, a=[dG2], lda=[N], b=Wp, ldb=J * C,
                                   bmode=BMODE_NN, b_offset=C, c=dP2, ldc=2 * C))
             keep.append(kern.gemm(N, 2 * C, P // 4, a=[dG2], lda=[N], amode=AMODE_COL, b=p2,
                                   ldb=2 * C, bmode=BMODE_NN, c=dWp, ldc=J * C, c_offset=C,
                                   allow_split=True))
             if k == 3:
-                dG4 = _empty((B, H // 4, W // 4, N), z)
+                dG4 = _act((B, H // 4, W // 4, N), dZ)
                 kern.upsample_bwd(dZ, N, 0, dG4, N, B, H, W, N, 4)
-                dP4 = _empty(p4.shape, z)
+                dP4 = _act(p4.shape, dZ)
                 keep.append(kern.gemm(P // 16, 2 * C, N, a=[dG4], lda=[N], b=Wp, ldb=J * C,
                                       bmode=BMODE_NN, b_offset=3 * C, c=dP4, ldc=2 * C))
                 keep.append(kern.gemm(N, 2 * C, P // 16, a=[dG4], lda=[N], amode=AMODE_COL,
@@ -532,11 +542,11 @@ class _HancLayerFn(torch.autograd.Function):
         keep.append(kern.gemm(N, C, P, a=[dZ], lda=[N], amode=AMODE_COL, b=z, ldb=C,
                               bmode=BMODE_NN, c=dWp, ldc=J * C, c_offset=0,
                               pro_b=_pro_mode(pro), b_scale=sc, b_shift=sh, allow_split=True))
-        dW = _empty((N, J * C), z)
+        dW = _f32((N, J * C), z)
         kern.group_relayout(dWp, dW, N, C, J, _HANC_ORDER[k], inverse=True)
         db = _take_bias_grad(cfg.bslot)
         if db is None:
-            db = _empty((N,), z)
+            db = _f32((N,), z)
             keep.append(kern.colsum(dZ, P, N, db))
         if pro.active:
             dz, dg, dbeta = _pro_bwd_part(pro, z, pro_g, dA, part, R)
@@ -586,7 +596,7 @@ class _BnActAddFn(torch.autograd.Function):
         ctx.cfg = cfg
         ctx.save_for_backward(z, pro_g)
         if stats is None:
-            stats = _empty((0,), z)
+            stats = _f32((0,), z)
         ctx.mark_non_differentiable(stats)
         ctx.set_materialize_grads(False)
         return y, stats
@@ -639,12 +649,12 @@ class _SEFn(torch.autograd.Function):
         pro = cfg.pro
         out = torch.empty_like(z)
         ostats = _stats((kern.se_stats_rows(B, HW, C), 2, C), z) if cfg.want_stats else None
-        save = _empty((kern.se_save_elems(B, C, Cr),), z)
+        save = _f32((kern.se_save_elems(B, C, Cr),), z)
         bn = cfg.bn
         mom = bn.momentum if bn.momentum is not None else 0.1
         tr = cfg.training
         with _prof.region(f"se_fwd B{B} HW{HW} C{C}", kernel="se_reduce+se_mid_sample+se_mid_bn+se_apply",
-                          shape=f"{B}x{HW}x{C}", bytes_alg=2.0 * 4 * B * HW * C):
+                          shape=f"{B}x{HW}x{C}", bytes_alg=2.0 * z.element_size() * B * HW * C):
             kern.se_fwd(z, pro.st[2] if pro.active else None,
                         pro.st[3] if pro.active else None, pro.act, B, HW, C, Cr, w1, b1, w2,
                         b2, g, b, bn.running_mean if bn.track_running_stats else None,
@@ -654,7 +664,7 @@ class _SEFn(torch.autograd.Function):
         ctx.cfg = cfg
         ctx.save_for_backward(z, pro_g, w1, w2, g, save)
         if ostats is None:
-            ostats = _empty((0,), z)
+            ostats = _f32((0,), z)
         ctx.mark_non_differentiable(ostats)
         ctx.set_materialize_grads(False)
         return out, ostats
@@ -669,17 +679,17 @@ class _SEFn(torch.autograd.Function):
         B, HW, C, Cr = cfg.B, cfg.HW, cfg.C, cfg.Cr
         pro = cfg.pro
         dw1 = torch.empty_like(w1)
-        db1 = _empty((Cr,), z)
+        db1 = _f32((Cr,), z)
         dw2 = torch.empty_like(w2)
-        db2 = _empty((C,), z)
-        dg = _empty((C,), z)
-        dbeta = _empty((C,), z)
+        db2 = _f32((C,), z)
+        dg = _f32((C,), z)
+        dbeta = _f32((C,), z)
         if pro.active:
             # the preceding BatchNorm(+act)'s backward rides on the SE's two passes
             dz = torch.empty_like(z)
-            dpg = _empty((C,), z)
-            dpb = _empty((C,), z)
-            dsum = _empty((C,), z) if pro.bslot is not None else None
+            dpg = _f32((C,), z)
+            dpb = _f32((C,), z)
+            dsum = _f32((C,), z) if pro.bslot is not None else None
             kern.se_bwd_pro(z, dout, pro.st, pro.act, pro_g, pro.training, B, HW, C, Cr, w1,
                             w2, g, cfg.training, save, dz, dpg, dpb, dw1, db1, dw2, db2, dg,
                             dbeta, dsum)
@@ -733,16 +743,16 @@ class _Conv3x3Fn(torch.autograd.Function):
     def forward(ctx, cfg: _C3Cfg, x, weight, bias):
         B, H, W, Ci, Co = cfg.B, cfg.H, cfg.W, cfg.Cin, cfg.Cout
         P = B * H * W
-        Wr = _empty((Co, 9 * Ci), x)  # [co][tap][ci]
+        Wr = _f32((Co, 9 * Ci), x)  # [co][tap][ci]
         kern.permute4(weight, Wr, (Co, 3, 3, Ci), (9 * Ci, 3, 1, 9))
-        Z = _empty((B, H, W, Co), x)
+        Z = _act((B, H, W, Co), x)
         stats = _stats((kern.gemm_stats_rows(P, Co, 9 * Ci), 2, Co), x) if cfg.want_stats else None
         kern.gemm(P, Co, 9 * Ci, a=[x], lda=[Ci], amode=AMODE_SHIFT3, b=Wr, ldb=9 * Ci, c=Z,
                   ldc=Co, bias=bias, H=H, W=W, cin=Ci, stats=stats)
         ctx.cfg = cfg
         ctx.save_for_backward(x, weight)
         if stats is None:
-            stats = _empty((0,), x)
+            stats = _f32((0,), x)
         ctx.mark_non_differentiable(stats)
         ctx.set_materialize_grads(False)
         return Z, stats
@@ -759,12 +769,12 @@ class _Conv3x3Fn(torch.autograd.Function):
         keep = []
         dx = None
         if ctx.needs_input_grad[1]:
-            Wf = _empty((Ci, 9 * Co), x)  # [ci][tap'][co] = W[co][ci][8-tap']
+            Wf = _f32((Ci, 9 * Co), x)  # [ci][tap'][co] = W[co][ci][8-tap']
             kern.permute4(weight, Wf, (Ci, 3, 3, Co), (9, 3, 1, 9 * Ci), flips=(0, 1, 1, 0))
             dx = torch.empty_like(x)
             keep.append(kern.gemm(P, Ci, 9 * Co, a=[dZ], lda=[Co], amode=AMODE_SHIFT3, b=Wf,
                                   ldb=9 * Co, c=dx, ldc=Ci, H=H, W=W, cin=Co))
-        dWr = _empty((Co, 9 * Ci), x)
+        dWr = _f32((Co, 9 * Ci), x)
         keep.append(kern.gemm(Co, 9 * Ci, P, a=[dZ], lda=[Co], amode=AMODE_COL, b=x, ldb=Ci,
                               bmode=BMODE_NN_SHIFT3, c=dWr, ldc=9 * Ci, H=H, W=W, cin=Ci,
                               allow_split=True))
@@ -772,7 +782,7 @@ class _Conv3x3Fn(torch.autograd.Function):
         kern.permute4(dWr, dW, (Co, Ci, 3, 3), (9 * Ci, 1, 3 * Ci, Ci))
         db = _take_bias_grad(cfg.bslot)
         if db is None:
-            db = _empty((Co,), x)
+            db = _f32((Co,), x)
             keep.append(kern.colsum(dZ, P, Co, db))
         return None, dx, dW, db
 
@@ -796,12 +806,12 @@ class _ConvT2Fn(torch.autograd.Function):
         B, H, W, Ci = x.shape
         Co = weight.shape[1]
         P = B * H * W
-        Wr = _empty((Ci, 4 * Co), x)  # [ci][d][co], d = di*2+dj
+        Wr = _f32((Ci, 4 * Co), x)  # [ci][d][co], d = di*2+dj
         kern.permute4(weight, Wr, (Ci, 2, 2, Co), (4 * Co, 2, 1, 4))
-        T = _empty((B, H, W, 4 * Co), x)
+        T = _act((B, H, W, 4 * Co), x)
         kern.gemm(P, 4 * Co, Ci, a=[x], lda=[Ci], b=Wr, ldb=4 * Co, bmode=BMODE_NN, c=T,
                   ldc=4 * Co)
-        Y = _empty((B, 2 * H, 2 * W, Co), x)
+        Y = _act((B, 2 * H, 2 * W, Co), x)
         kern.pixel_shuffle2(T, bias, Y, B, H, W, Co)
         ctx.save_for_backward(x, Wr)
         ctx.shape = (B, H, W, Ci, Co)
@@ -813,7 +823,7 @@ class _ConvT2Fn(torch.autograd.Function):
         B, H, W, Ci, Co = ctx.shape
         P = B * H * W
         dY = dY.contiguous()
-        dT = _empty((B, H, W, 4 * Co), x)
+        dT = _act((B, H, W, 4 * Co), dY)
         kern.pixel_shuffle2(dT, None, dY, B, H, W, Co, inverse=True)
         keep = []
         dx = None
@@ -821,12 +831,12 @@ class _ConvT2Fn(torch.autograd.Function):
             dx = torch.empty_like(x)
             keep.append(kern.gemm(P, Ci, 4 * Co, a=[dT], lda=[4 * Co], b=Wr, ldb=4 * Co, c=dx,
                                   ldc=Ci))
-        dWr = _empty((Ci, 4 * Co), x)
+        dWr = _f32((Ci, 4 * Co), x)
         keep.append(kern.gemm(Ci, 4 * Co, P, a=[x], lda=[Ci], amode=AMODE_COL, b=dT,
                               ldb=4 * Co, bmode=BMODE_NN, c=dWr, ldc=4 * Co, allow_split=True))
-        dW = _empty((Ci, Co, 2, 2), x)
+        dW = _f32((Ci, Co, 2, 2), x)
         kern.permute4(dWr, dW, (Ci, Co, 2, 2), (4 * Co, 1, 2 * Co, Co))
-        db = _empty((Co,), x)
+        db = _f32((Co,), x)
         keep.append(kern.colsum(dY, B * 4 * H * W, Co, db))
         return dx, dW, db
 
@@ -844,7 +854,7 @@ class _Pool2Fn(torch.autograd.Function):
         B, H, W, C = x.shape
         if H % 2 or W % 2:
             raise ValueError("pool2: spatial size must be even")
-        y = _empty((B, H // 2, W // 2, C), x)
+        y = _act((B, H // 2, W // 2, C), x)
         kern.pool2_fwd(x, y, B, H, W, C, mode)
         ctx.mode = mode
         if mode == kern.POOL_MAX:
@@ -877,7 +887,7 @@ class _CatFn(torch.autograd.Function):
         B, H, W, Ca = a.shape
         Cb = b.shape[-1]
         P = B * H * W
-        y = _empty((B, H, W, Ca + Cb), a)
+        y = _act((B, H, W, Ca + Cb), a)
         kern.slice_copy(a, Ca, 0, y, Ca + Cb, 0, P, Ca)
         kern.slice_copy(b, Cb, 0, y, Ca + Cb, Ca, P, Cb)
         ctx.dims = (P, Ca, Cb)
@@ -889,10 +899,10 @@ class _CatFn(torch.autograd.Function):
         dy = dy.contiguous()
         da = db = None
         if ctx.needs_input_grad[0]:
-            da = _empty(dy.shape[:-1] + (Ca,), dy)
+            da = _act(dy.shape[:-1] + (Ca,), dy)
             kern.slice_copy(dy, Ca + Cb, 0, da, Ca, 0, P, Ca)
         if ctx.needs_input_grad[1]:
-            db = _empty(dy.shape[:-1] + (Cb,), dy)
+            db = _act(dy.shape[:-1] + (Cb,), dy)
             kern.slice_copy(dy, Ca + Cb, Ca, db, Cb, 0, P, Cb)
         return da, db
 
@@ -908,7 +918,7 @@ class _HeadFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, sigm):
         B, H, W, C = x.shape
-        y = _empty((B, H, W, 1), x)
+        y = _f32((B, H, W, 1), x)  # the model output stays fp32 (it feeds the loss)
         kern.head_fwd(x, w, b, sigm, y, B * H * W, C)
         ctx.sigm = sigm
         ctx.save_for_backward(x, w, y)
@@ -920,7 +930,7 @@ class _HeadFn(torch.autograd.Function):
         B, H, W, C = x.shape
         dx = torch.empty_like(x)
         dw = torch.empty_like(w)
-        db = _empty((1,), x)
+        db = _f32((1,), x)
         ws = kern.head_bwd(x, w, y, dy.contiguous(), ctx.sigm, dx, dw, db, B * H * W, C)
         del ws
         return dx, dw, db, None
@@ -944,7 +954,7 @@ class _WMergeFn(torch.autograd.Function):
         kern.wmerge_fwd(a, b, w, y, P, C, stats)
         ctx.save_for_backward(a, b, w)
         if stats is None:
-            stats = _empty((0,), a)
+            stats = _f32((0,), a)
         ctx.mark_non_differentiable(stats)
         ctx.set_materialize_grads(False)
         return y, stats
@@ -958,7 +968,7 @@ class _WMergeFn(torch.autograd.Function):
         da = torch.empty_like(a)
         db = torch.empty_like(b)
         kern.wmerge_bwd(dy, w, da, db, a.numel())
-        dw = _empty((1,), a)
+        dw = _f32((1,), a)
         ws = kern.dotdiff(dy, a, b, a.numel(), dw)
         del ws
         return da, db, dw, None
@@ -980,7 +990,7 @@ class _GroupRelayoutFn(torch.autograd.Function):
     def forward(ctx, w2, J, order):
         N, K = w2.shape
         C = K // J
-        out = _empty((N, K), w2)
+        out = _f32((N, K), w2)
         kern.group_relayout(w2, out, N, C, J, order)
         ctx.meta = (N, C, J, list(order))
         return out
@@ -988,7 +998,7 @@ class _GroupRelayoutFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         N, C, J, order = ctx.meta
-        out = _empty((N, J * C), g)
+        out = _f32((N, J * C), g)
         kern.group_relayout(g.contiguous(), out, N, C, J, order, inverse=True)
         return out, None, None
 
@@ -1002,46 +1012,48 @@ def group_relayout(w2, J, order):
 # --------------------------------------------------------------------------
 class _ToNHWCFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x):
+    def forward(ctx, x, dtype):
         B, C, H, W = x.shape
-        y = _empty((B, H, W, C), x)
+        y = torch.empty((B, H, W, C), dtype=dtype, device=x.device)
         kern.permute4(x, y, (B, H, W, C), (C * H * W, W, 1, H * W))
         return y
 
     @staticmethod
     def backward(ctx, dy):
         B, H, W, C = dy.shape
-        dx = _empty((B, C, H, W), dy)
+        dx = _f32((B, C, H, W), dy)
         kern.permute4(dy.contiguous(), dx, (B, C, H, W), (H * W * C, 1, W * C, C))
-        return dx
+        return dx, None
 
 
-def to_nhwc(x):
+def to_nhwc(x, dtype=torch.float32):
+    """NCHW input -> NHWC activations stored as `dtype` (fp32 or bf16)."""
     x = x.contiguous()
     if x.dtype != torch.float32:
         x = x.float()
-    return _ToNHWCFn.apply(x)
+    return _ToNHWCFn.apply(x, dtype)
 
 
 class _ToNCHWFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, y):
         B, H, W, C = y.shape
-        x = _empty((B, C, H, W), y)
+        x = _f32((B, C, H, W), y)  # module outputs are fp32 NCHW
         kern.permute4(y, x, (B, C, H, W), (H * W * C, 1, W * C, C))
+        ctx.act_dtype = y.dtype
         return x
 
     @staticmethod
     def backward(ctx, dx):
         B, C, H, W = dx.shape
-        dy = _empty((B, H, W, C), dx)
+        dy = torch.empty((B, H, W, C), dtype=ctx.act_dtype, device=dx.device)
         kern.permute4(dx.contiguous(), dy, (B, H, W, C), (C * H * W, W, 1, H * W))
         return dy
 
 
 def nhwc_to_nchw(y):
     B, H, W, C = y.shape
-    if C == 1:
+    if C == 1 and y.dtype == torch.float32:
         return y.view(B, 1, H, W)
     return _ToNCHWFn.apply(y.contiguous())
 

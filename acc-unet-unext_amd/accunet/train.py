@@ -5,6 +5,7 @@ step, Train_one_epoch.py:134,167,185): metrics stay on the device and are read
 only when logged.
 
     step = TrainStep(model, lr=1e-3)            # Adam(lr 1e-3), WeightedDiceBCE(0.5, 0.5)
+    step = TrainStep(model, precision="bf16")   # BASELINE configs[2]: bf16 activations
     loss = step(images, masks)                  # fwd + loss + bwd (+ RCCL all-reduce) + Adam
 
 Two execution modes, same arithmetic:
@@ -33,9 +34,11 @@ from .optim import FusedAdam
 
 class TrainStep:
     def __init__(self, model, lr=1e-3, reducer=None, dice_weight=0.5, bce_weight=0.5,
-                 graph=False, process_group=None):
+                 graph=False, process_group=None, precision=None):
         if graph and reducer is not None:
             raise ValueError("graph mode does its own single-bucket all-reduce; pass no reducer")
+        if precision is not None:  # "fp32" / "bf16": see ACC_UNet.set_precision
+            model.set_precision(precision)
         self.model = model
         self.reducer = reducer
         self.graph = graph

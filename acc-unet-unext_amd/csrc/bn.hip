@@ -1,4 +1,4 @@
-// Training-mode BatchNorm2d (+LeakyReLU) on NHWC fp32, split into streaming
+// Training-mode BatchNorm2d (+LeakyReLU) on NHWC fp32 / bf16 activations, split into streaming
 // passes whose per-channel statistics are reduced deterministically
 // (per-block partials -> fixed-order reduction, fp64 final accumulation).
 //
@@ -180,11 +180,11 @@ extern "C" int accunet_bn_finalize(const double* part, int R, int C, double coun
 // ---------------------------------------------------------------------------
 // affine_act: y = act(x*scale[c] + shift[c]) (+ res), optional partial stats of y
 // ---------------------------------------------------------------------------
-template <int V>
+template <int V, typename T>
 __global__ void __launch_bounds__(256)
-affine_act_kernel(const float* __restrict__ x, const float* __restrict__ sc,
-                  const float* __restrict__ sh, int act, const float* __restrict__ res,
-                  float* __restrict__ y, long P, int C, double* __restrict__ stats) {
+affine_act_kernel(const T* __restrict__ x, const float* __restrict__ sc,
+                  const float* __restrict__ sh, int act, const T* __restrict__ res,
+                  T* __restrict__ y, long P, int C, double* __restrict__ stats) {
   ChanTile t = chan_tile<V>(C);
   long rows_per = (P + gridDim.x - 1) / gridDim.x;
   long r0 = blockIdx.x * rows_per, r1 = min(P, r0 + rows_per);
@@ -220,7 +220,7 @@ affine_act_kernel(const float* __restrict__ x, const float* __restrict__ sc,
             v[u][j] = apply_act(v[u][j] * s[j] + h[j], act);
             if (res) v[u][j] += q[u][j];
           }
-          if (y) stv<V>(y + r * C + t.c0, v[u]);  // y == nullptr: statistics only (accunet_colsum)
+          if (y) stv_r<V>(y + r * C + t.c0, v[u]);  // y == nullptr: statistics only (accunet_colsum)
 #pragma unroll
           for (int j = 0; j < V; ++j) { a[j] += v[u][j]; b[j] += (double)v[u][j] * v[u][j]; }
         }
@@ -239,21 +239,25 @@ int stream_rowblocks(long P, int C) {
   return (int)want;
 }
 
-extern "C" int accunet_affine_act_fwd(const float* x, const float* sc, const float* sh, int act,
-                                      const float* res, float* y, long P, int C, double* stats,
-                                      int* stats_rows, void* stream_) {
+extern "C" int accunet_affine_act_fwd(const void* x, const float* sc, const float* sh, int act,
+                                      const void* res, void* y, long P, int C, double* stats,
+                                      int* stats_rows, int dt, void* stream_) {
   hipStream_t s = (hipStream_t)stream_;
   int V = (C % 4 == 0) ? 4 : 1;
   int CQ = C / V;
   int nb = stream_rowblocks(P, C);
   if (stats_rows) *stats_rows = nb;
   dim3 grid(nb, ceil_div(CQ, 64));
-  if (V == 4)
-    hipLaunchKernelGGL(affine_act_kernel<4>, grid, dim3(256), 0, s, x, sc, sh, act, res, y, P, C,
-                       stats);
-  else
-    hipLaunchKernelGGL(affine_act_kernel<1>, grid, dim3(256), 0, s, x, sc, sh, act, res, y, P, C,
-                       stats);
+  if (with_dt(dt, [&](auto tag) {
+        using T = decltype(tag);
+        if (V == 4)
+          hipLaunchKernelGGL((affine_act_kernel<4, T>), grid, dim3(256), 0, s, (const T*)x, sc, sh,
+                             act, (const T*)res, (T*)y, P, C, stats);
+        else
+          hipLaunchKernelGGL((affine_act_kernel<1, T>), grid, dim3(256), 0, s, (const T*)x, sc, sh,
+                             act, (const T*)res, (T*)y, P, C, stats);
+      }))
+    return ACC_EBADARG;
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 
@@ -266,9 +270,9 @@ extern "C" int accunet_stream_rows(long P, int C) { return stream_rowblocks(P, C
 //   finalize: dgamma, dbeta, dx = k1*g + k2*x + k3
 //   apply:    dx (optionally accumulated), optional partial column sums of dx
 // ---------------------------------------------------------------------------
-template <int V>
+template <int V, typename T>
 __global__ void __launch_bounds__(256)
-bn_bwd_reduce_kernel(const float* __restrict__ x, const float* __restrict__ dy,
+bn_bwd_reduce_kernel(const T* __restrict__ x, const T* __restrict__ dy,
                      const float* __restrict__ st, int act, long P, int C,
                      double* __restrict__ part) {
   // fp64 accumulation, as ATen's CPU batch_norm backward (acc_type<float> = double)
@@ -357,11 +361,11 @@ bn_bwd_finalize_kernel(const double* __restrict__ part, int R, int C, double cou
   coef[2 * C + c] = k3;
 }
 
-template <int V>
+template <int V, typename T>
 __global__ void __launch_bounds__(256)
-bn_bwd_apply_kernel(const float* __restrict__ x, const float* __restrict__ dy,
+bn_bwd_apply_kernel(const T* __restrict__ x, const T* __restrict__ dy,
                     const float* __restrict__ st, const float* __restrict__ coef, int act,
-                    long P, int C, float* __restrict__ dx, int accumulate,
+                    long P, int C, T* __restrict__ dx, int accumulate,
                     double* __restrict__ colsum) {
   ChanTile t = chan_tile<V>(C);
   long rows_per = (P + gridDim.x - 1) / gridDim.x;
@@ -403,8 +407,10 @@ bn_bwd_apply_kernel(const float* __restrict__ x, const float* __restrict__ dy,
             float g = dv[u][j];
             if (act == ACT_LRELU) g *= lrelu_d(xv[u][j] * s[j] + h[j]);
             float d = k1[j] * g + k2[j] * (xv[u][j] - mu[j]) + k3[j];
-            if (colsum) a[j] += d;
-            o[u][j] = accumulate ? o[u][j] + d : d;
+            // statistics describe the stored tensor (bf16: the rounded value)
+            const float dd = rnd<T>(d);
+            if (colsum) a[j] += accumulate ? d : dd;
+            o[u][j] = accumulate ? rnd<T>(o[u][j] + d) : dd;
           }
           stv<V>(dx + r * C + t.c0, o[u]);
         }
@@ -429,10 +435,10 @@ static void bn_dsum_finish(double* part, int nb, int C, double* scratch, float* 
                      2 * C, C, dsum);
 }
 
-extern "C" int accunet_bn_bwd(const float* x, const float* dy, const float* st,
+extern "C" int accunet_bn_bwd(const void* x, const void* dy, const float* st,
                               const float* gamma, int act, int training, long P, int C,
-                              float* dx, int accumulate, float* dgamma, float* dbeta,
-                              float* dsum, float* ws, size_t ws_elems, void* stream_) {
+                              void* dx, int accumulate, float* dgamma, float* dbeta,
+                              float* dsum, float* ws, size_t ws_elems, int dt, void* stream_) {
   hipStream_t s = (hipStream_t)stream_;
   int V = (C % 4 == 0) ? 4 : 1;
   int nb = stream_rowblocks(P, C);
@@ -445,21 +451,30 @@ extern "C" int accunet_bn_bwd(const float* x, const float* dy, const float* st,
   double* part = reinterpret_cast<double*>(ws);
   double* scratch = reinterpret_cast<double*>(ws + part_f);
   float* coef = ws + part_f + scr_f;
-  if (V == 4)
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<4>, grid, dim3(256), 0, s, x, dy, st, act, P, C, part);
-  else
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<1>, grid, dim3(256), 0, s, x, dy, st, act, P, C, part);
+  if (dt != ACC_F32 && dt != ACC_BF16) return ACC_EBADARG;
+  with_dt(dt, [&](auto tag) {
+    using T = decltype(tag);
+    if (V == 4)
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<4, T>), grid, dim3(256), 0, s, (const T*)x,
+                         (const T*)dy, st, act, P, C, part);
+    else
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<1, T>), grid, dim3(256), 0, s, (const T*)x,
+                         (const T*)dy, st, act, P, C, part);
+  });
   int rows;
   const double* pr = reduce_partials_t<double>(part, nb, 2 * C, scratch, &rows, s);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(C, 64)), dim3(256), 0, s, pr, rows, C,
                      (double)P, st, gamma, training, dgamma, dbeta, coef, 0);
   double* cpart = dsum ? part : nullptr;  // the reduce partials are consumed by now
-  if (V == 4)
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<4>, grid, dim3(256), 0, s, x, dy, st, coef, act, P, C,
-                       dx, accumulate, cpart);
-  else
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<1>, grid, dim3(256), 0, s, x, dy, st, coef, act, P, C,
-                       dx, accumulate, cpart);
+  with_dt(dt, [&](auto tag) {
+    using T = decltype(tag);
+    if (V == 4)
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<4, T>), grid, dim3(256), 0, s, (const T*)x,
+                         (const T*)dy, st, coef, act, P, C, (T*)dx, accumulate, cpart);
+    else
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<1, T>), grid, dim3(256), 0, s, (const T*)x,
+                         (const T*)dy, st, coef, act, P, C, (T*)dx, accumulate, cpart);
+  });
   if (dsum) bn_dsum_finish(part, nb, C, scratch, dsum, s);
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
@@ -480,13 +495,14 @@ extern "C" size_t accunet_bn_bwd_part_ws_elems(long P, int R, int C) {
   return bn_bwd_part_ws(P, R, C);
 }
 
-extern "C" int accunet_bn_bwd_part(const float* x, const float* dy, const float* st,
+extern "C" int accunet_bn_bwd_part(const void* x, const void* dy, const float* st,
                                    const float* gamma, int act, int training, long P, int C,
-                                   const double* part, int R, float* dx, float* dgamma,
-                                   float* dbeta, float* dsum, float* ws, size_t ws_elems,
+                                   const double* part, int R, void* dx, float* dgamma,
+                                   float* dbeta, float* dsum, float* ws, size_t ws_elems, int dt,
                                    void* stream_) {
   hipStream_t s = (hipStream_t)stream_;
   if (C <= 0 || R <= 0) return ACC_EBADSHAPE;
+  if (dt != ACC_F32 && dt != ACC_BF16) return ACC_EBADARG;
   if (ws_elems < bn_bwd_part_ws(P, R, C) || ((uintptr_t)ws & 7)) return ACC_EBADARG;
   const int V = (C % 4 == 0) ? 4 : 1;
   const int nb = stream_rowblocks(P, C);
@@ -500,12 +516,15 @@ extern "C" int accunet_bn_bwd_part(const float* x, const float* dy, const float*
   const double* pr = reduce_partials_t<double>(part, R, 2 * C, scratch, &rows, s);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(C, 64)), dim3(256), 0, s, pr, rows, C,
                      (double)P, st, gamma, training, dgamma, dbeta, coef, 1);
-  if (V == 4)
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<4>, grid, dim3(256), 0, s, x, dy, st, coef, act, P, C,
-                       dx, 0, dsum ? cpart : nullptr);
-  else
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<1>, grid, dim3(256), 0, s, x, dy, st, coef, act, P, C,
-                       dx, 0, dsum ? cpart : nullptr);
+  with_dt(dt, [&](auto tag) {
+    using T = decltype(tag);
+    if (V == 4)
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<4, T>), grid, dim3(256), 0, s, (const T*)x,
+                         (const T*)dy, st, coef, act, P, C, (T*)dx, 0, dsum ? cpart : nullptr);
+    else
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<1, T>), grid, dim3(256), 0, s, (const T*)x,
+                         (const T*)dy, st, coef, act, P, C, (T*)dx, 0, dsum ? cpart : nullptr);
+  });
   if (dsum) bn_dsum_finish(cpart, nb, C, cscr, dsum, s);
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
@@ -513,8 +532,8 @@ extern "C" int accunet_bn_bwd_part(const float* x, const float* dy, const float*
 // ---------------------------------------------------------------------------
 // Column sums (conv bias gradients when no BN-backward pass precedes them).
 // ---------------------------------------------------------------------------
-extern "C" int accunet_colsum(const float* x, long P, int C, float* out, double* ws,
-                              size_t ws_elems, void* stream_) {
+extern "C" int accunet_colsum(const void* x, long P, int C, float* out, double* ws,
+                              size_t ws_elems, int dt, void* stream_) {
   hipStream_t s = (hipStream_t)stream_;
   int V = (C % 4 == 0) ? 4 : 1;
   int nb = stream_rowblocks(P, C);
@@ -522,12 +541,16 @@ extern "C" int accunet_colsum(const float* x, long P, int C, float* out, double*
   double* part = ws;
   double* scratch = ws + (size_t)nb * 2 * C;
   if ((size_t)nb * 2 * C + accunet_partials_ws_elems(nb, 2 * C) > ws_elems) return ACC_EBADARG;
-  if (V == 4)
-    hipLaunchKernelGGL(affine_act_kernel<4>, grid, dim3(256), 0, s, x, nullptr, nullptr, ACT_NONE,
-                       nullptr, nullptr, P, C, part);
-  else
-    hipLaunchKernelGGL(affine_act_kernel<1>, grid, dim3(256), 0, s, x, nullptr, nullptr, ACT_NONE,
-                       nullptr, nullptr, P, C, part);
+  if (with_dt(dt, [&](auto tag) {
+        using T = decltype(tag);
+        if (V == 4)
+          hipLaunchKernelGGL((affine_act_kernel<4, T>), grid, dim3(256), 0, s, (const T*)x, nullptr,
+                             nullptr, ACT_NONE, nullptr, nullptr, P, C, part);
+        else
+          hipLaunchKernelGGL((affine_act_kernel<1, T>), grid, dim3(256), 0, s, (const T*)x, nullptr,
+                             nullptr, ACT_NONE, nullptr, nullptr, P, C, part);
+      }))
+    return ACC_EBADARG;
   int rows;
   const double* pr = reduce_partials_t<double>(part, nb, 2 * C, scratch, &rows, s);
   hipLaunchKernelGGL(sum_rows_d_kernel<float>, dim3(ceil_div(C, 64)), dim3(256), 0, s, pr, rows,

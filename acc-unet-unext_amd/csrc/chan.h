@@ -26,22 +26,29 @@ ACC_DEV ChanTile chan_tile(int C) {
   return t;
 }
 
-template <int V>
-ACC_DEV void ldv(const float* p, float (&v)[V]) {
+template <int V, typename T>
+ACC_DEV void ldv(const T* p, float (&v)[V]) {
   if (V == 4) {
-    float4 q = ld4(p);
-    v[0] = q.x; v[1] = q.y; v[2 % V] = q.z; v[3 % V] = q.w;
+    float4 q = ldq(p);
+    v[0] = q.x; v[1 % V] = q.y; v[2 % V] = q.z; v[3 % V] = q.w;
   } else {
-    v[0] = p[0];
+    v[0] = ld1(p);
   }
 }
-template <int V>
-ACC_DEV void stv(float* p, const float (&v)[V]) {
+template <int V, typename T>
+ACC_DEV void stv(T* p, const float (&v)[V]) {
   if (V == 4) {
-    st4(p, make_float4(v[0], v[1 % V], v[2 % V], v[3 % V]));
+    stq(p, make_float4(v[0], v[1 % V], v[2 % V], v[3 % V]));
   } else {
-    p[0] = v[0];
+    st1(p, v[0]);
   }
+}
+// stv that also rounds v to what was stored (so statistics describe the tensor)
+template <int V, typename T>
+ACC_DEV void stv_r(T* p, float (&v)[V]) {
+#pragma unroll
+  for (int j = 0; j < V; ++j) v[j] = rnd<T>(v[j]);
+  stv<V>(p, v);
 }
 
 // Reduce per-thread (a[V], b[V]) across the RG row-groups of the block and write

@@ -1,10 +1,13 @@
 // Shared device helpers for the ACC-UNet gfx950 kernels.
 //
 // Layout convention for every activation tensor handed to this library:
-// NHWC (channels-last), fp32, contiguous, viewed as a row-major matrix
+// NHWC (channels-last), contiguous, viewed as a row-major matrix
 // [P = B*H*W pixels][C channels]. A "pixel row" is therefore C contiguous
-// floats, which makes 1x1 convolutions plain row-major GEMMs and keeps the
+// elements, which makes 1x1 convolutions plain row-major GEMMs and keeps the
 // per-channel BatchNorm / SE statistics coalesced along the fast axis.
+// Activations (and activation gradients) are stored as fp32 or bf16 (`dt` =
+// ACC_F32 / ACC_BF16 on the C ABI); arithmetic is always fp32 in registers,
+// statistics fp64, parameters and their gradients fp32.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -84,6 +87,65 @@ ACC_DEV float4 ld4_nt(const float* p) {
 ACC_DEV void st4_nt(float* p, float4 v) {
   accv4 w = {v.x, v.y, v.z, v.w};
   __builtin_nontemporal_store(w, reinterpret_cast<accv4*>(p));
+}
+
+// ---------------------------------------------------------------------------
+// bf16 activation storage (round-to-nearest-even via v_cvt_pk_bf16_f32)
+// ---------------------------------------------------------------------------
+typedef unsigned short bf16_t;
+typedef __bf16 bf16x2_v __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8_v __attribute__((ext_vector_type(8)));
+
+ACC_DEV float bf2f(bf16_t v) { return __uint_as_float((unsigned)v << 16); }
+ACC_DEV bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
+ACC_DEV unsigned pack_bf2(float a, float b) {
+  bf16x2_v v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(unsigned, v);
+}
+ACC_DEV float bflo(unsigned u) { return __uint_as_float(u << 16); }
+ACC_DEV float bfhi(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
+
+// Typed activation access: fp32 in registers whatever the storage type.
+ACC_DEV float ld1(const float* p) { return *p; }
+ACC_DEV float ld1(const bf16_t* p) { return bf2f(*p); }
+ACC_DEV void st1(float* p, float v) { *p = v; }
+ACC_DEV void st1(bf16_t* p, float v) { *p = f2bf(v); }
+// channel quads: 16 bytes (fp32) / 8 bytes (bf16)
+ACC_DEV float4 ldq(const float* p) { return ld4(p); }
+ACC_DEV float4 ldq(const bf16_t* p) {
+  const uint2 u = *reinterpret_cast<const uint2*>(p);
+  return make_float4(bflo(u.x), bfhi(u.x), bflo(u.y), bfhi(u.y));
+}
+ACC_DEV void stq(float* p, float4 v) { st4(p, v); }
+ACC_DEV void stq(bf16_t* p, float4 v) {
+  uint2 u;
+  u.x = pack_bf2(v.x, v.y);
+  u.y = pack_bf2(v.z, v.w);
+  *reinterpret_cast<uint2*>(p) = u;
+}
+typedef unsigned accu2 __attribute__((ext_vector_type(2)));
+ACC_DEV float4 ldq_nt(const float* p) { return ld4_nt(p); }
+ACC_DEV float4 ldq_nt(const bf16_t* p) {
+  const accu2 u = __builtin_nontemporal_load(reinterpret_cast<const accu2*>(p));
+  return make_float4(bflo(u.x), bfhi(u.x), bflo(u.y), bfhi(u.y));
+}
+ACC_DEV void stq_nt(float* p, float4 v) { st4_nt(p, v); }
+ACC_DEV void stq_nt(bf16_t* p, float4 v) {
+  accu2 u = {pack_bf2(v.x, v.y), pack_bf2(v.z, v.w)};
+  __builtin_nontemporal_store(u, reinterpret_cast<accu2*>(p));
+}
+// the value v takes once stored as T (statistics are taken of what is stored)
+ACC_DEV float rnd_as(float v, const float*) { return v; }
+ACC_DEV float rnd_as(float v, const bf16_t*) { return bf2f(f2bf(v)); }
+template <typename T>
+ACC_DEV float rnd(float v) { return rnd_as(v, (const T*)nullptr); }
+
+// Host: run f(T{}) with T = the storage type named by dt (ACC_F32 / ACC_BF16).
+template <typename F>
+static inline int with_dt(int dt, F f) {
+  if (dt == ACC_BF16) { f(bf16_t{}); return ACC_OK; }
+  if (dt == ACC_F32) { f(float{}); return ACC_OK; }
+  return ACC_EBADARG;
 }
 
 ACC_DEV float f4get(const float4& v, int i) {

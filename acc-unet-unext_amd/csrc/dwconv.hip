@@ -1,4 +1,4 @@
-// Depthwise 3x3 convolution (stride 1, zero padding 1, +bias) on NHWC fp32:
+// Depthwise 3x3 convolution (stride 1, zero padding 1, +bias) on NHWC fp32 / bf16:
 // HANCBlock.conv2 + norm2 statistics, reference ACC_UNet/ACC_UNet.py:240-247,273-275.
 //
 // K1 (forward): z[b,h,w,c] = bias[c] + sum_tap W[c][tap] * a[b,h+dh,w+dw,c] where the
@@ -29,19 +29,13 @@ struct VecT<1> {
   typedef float T;
 };
 
-template <int V>
-ACC_DEV void vload(const float* p, float (&v)[V]) {
-  if (V == 4) {
-    float4 q = ld4(p);
-    v[0] = q.x; v[1 % V] = q.y; v[2 % V] = q.z; v[3 % V] = q.w;
-  } else {
-    v[0] = p[0];
-  }
+template <int V, typename T>
+ACC_DEV void vload(const T* p, float (&v)[V]) {
+  ldv<V>(p, v);
 }
-template <int V>
-ACC_DEV void vstore(float* p, const float (&v)[V]) {
-  if (V == 4) st4(p, make_float4(v[0], v[1 % V], v[2 % V], v[3 % V]));
-  else p[0] = v[0];
+template <int V, typename T>
+ACC_DEV void vstore(T* p, const float (&v)[V]) {
+  stv<V>(p, v);
 }
 
 struct DwGeom {
@@ -52,12 +46,12 @@ struct DwGeom {
 };
 
 // flip != 0: use W[c][8-tap] (data gradient = correlation with the flipped kernel)
-template <int V>
+template <int V, typename T>
 __global__ void __launch_bounds__(256)
-dw3x3_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
+dw3x3_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
                  const float* __restrict__ bias, const float* __restrict__ sc,
-                 const float* __restrict__ sh, int act, int flip, float* __restrict__ z,
-                 double* __restrict__ stats, DwGeom g, const float* __restrict__ bz,
+                 const float* __restrict__ sh, int act, int flip, T* __restrict__ z,
+                 double* __restrict__ stats, DwGeom g, const T* __restrict__ bz,
                  const float* __restrict__ bst, int bact) {
   const bool bnb = stats != nullptr && bz != nullptr;  // see dw3x3_tile_fwd_kernel
   const int tid = threadIdx.x;
@@ -121,9 +115,10 @@ dw3x3_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
         for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
           for (int dx = 0; dx < 3; ++dx) acc = fmaf(k[dy * 3 + dx][j], win[dy][dx][j], acc);
+        acc = rnd<T>(acc);  // statistics of the stored value
         o[j] = acc;
         if (bnb) {
-          const float zz = bz[(((long)b * g.H + h) * g.W + w) * C + c0 + j];
+          const float zz = ld1(bz + (((long)b * g.H + h) * g.W + w) * C + c0 + j);
           float gg = acc;
           if (bact == ACT_LRELU)
             gg *= lrelu_d(zz * bst[BN_SCALE * C + c0 + j] + bst[BN_SHIFT * C + c0 + j]);
@@ -172,9 +167,9 @@ dw3x3_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
 // Weight + bias gradient: dW[c][tap] = sum_p dz[p,c] * a[shift_tap(p), c],
 // db[c] = sum_p dz[p,c]; a = act(x*scale+shift) recomputed. Output partials
 // [block][10][C] (taps 0..8, then bias).
-template <int V>
+template <int V, typename T>
 __global__ void __launch_bounds__(256)
-dw3x3_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dz,
+dw3x3_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dz,
                    const float* __restrict__ sc, const float* __restrict__ sh, int act,
                    float* __restrict__ part, DwGeom g) {
   const int tid = threadIdx.x;
@@ -321,21 +316,21 @@ struct DwT {
 // block's strip (which starts at output row hbeg) in slot (h - hbeg + 1) % 10.
 // Fetch `n` float4 elements of consecutive input rows starting at row hA into
 // registers (zero outside the image).
-template <int TCQ, int NKK>
-ACC_DEV void dw_fetch_rows(float4 (&v)[NKK], const float* __restrict__ x, const DwTGeom& g, int b,
+template <int TCQ, int NKK, typename TX>
+ACC_DEV void dw_fetch_rows(float4 (&v)[NKK], const TX* __restrict__ x, const DwTGeom& g, int b,
                            int hA, int n, int w0, int c0) {
-  typedef DwT<TCQ> T;
+  typedef DwT<TCQ> G;
   const int tid = threadIdx.x, q = tid % TCQ;
 #pragma unroll
   for (int k = 0; k < NKK; ++k) {
     const int i = tid + 256 * k;
     const int rp = i / TCQ;
-    const int p = rp % T::IP, r = rp / T::IP;
+    const int p = rp % G::IP, r = rp / G::IP;
     const int hh = hA + r, ww = w0 - 1 + p;
     v[k] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (i < n && hh >= 0 && hh < g.H && ww >= 0 && ww < g.W) {
-      const float* src = x + (((long)b * g.H + hh) * g.W + ww) * g.C + c0 + 4 * q;
-      v[k] = g.ntl ? ld4_nt(src) : ld4(src);
+      const TX* src = x + (((long)b * g.H + hh) * g.W + ww) * g.C + c0 + 4 * q;
+      v[k] = g.ntl ? ldq_nt(src) : ldq(src);
     }
   }
 }
@@ -345,14 +340,14 @@ template <int TCQ, int NKK>
 ACC_DEV void dw_park_rows(float4* __restrict__ ring, const float4 (&v)[NKK], const DwTGeom& g,
                           int hA, int n, int w0, int hbeg, bool pro, float4 ps, float4 pb,
                           int act) {
-  typedef DwT<TCQ> T;
+  typedef DwT<TCQ> G;
   const int tid = threadIdx.x, q = tid % TCQ;
 #pragma unroll
   for (int k = 0; k < NKK; ++k) {
     const int i = tid + 256 * k;
     if (i < n) {
       const int rp = i / TCQ;
-      const int p = rp % T::IP, r = rp / T::IP;
+      const int p = rp % G::IP, r = rp / G::IP;
       const int hh = hA + r, ww = w0 - 1 + p;
       float4 a = v[k];
       if (pro && hh >= 0 && hh < g.H && ww >= 0 && ww < g.W) {
@@ -361,18 +356,18 @@ ACC_DEV void dw_park_rows(float4* __restrict__ ring, const float4 (&v)[NKK], con
         a.z = apply_act(a.z * ps.z + pb.z, act);
         a.w = apply_act(a.w * ps.w + pb.w, act);
       }
-      const int slot = (hh - hbeg + 1) % T::IR;
-      ring[(slot * T::IP + p) * TCQ + q] = a;
+      const int slot = (hh - hbeg + 1) % G::IR;
+      ring[(slot * G::IP + p) * TCQ + q] = a;
     }
   }
 }
 
 // load the activated input tile a = act(x*sc+sh) (zero outside the image) into LDS
-template <int TCQ>
-ACC_DEV void dw_fill_tile(float4* __restrict__ tile, const float* __restrict__ x,
+template <int TCQ, typename TX>
+ACC_DEV void dw_fill_tile(float4* __restrict__ tile, const TX* __restrict__ x,
                           const float* __restrict__ sc, const float* __restrict__ sh, int act,
                           const DwTGeom& g, int b, int h0, int w0, int c0) {
-  typedef DwT<TCQ> T;
+  typedef DwT<TCQ> G;
   const int tid = threadIdx.x;
   const int q = tid % TCQ;  // 256 % TCQ == 0: a thread always loads the same quad
   float4 ps = make_float4(1.f, 1.f, 1.f, 1.f), pb = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -381,22 +376,22 @@ ACC_DEV void dw_fill_tile(float4* __restrict__ tile, const float* __restrict__ x
     ps = ld4(sc + c0 + 4 * q);
     pb = ld4(sh + c0 + 4 * q);
   }
-  float4 v[T::NK];
-  bool in[T::NK];
+  float4 v[G::NK];
+  bool in[G::NK];
 #pragma unroll
-  for (int k = 0; k < T::NK; ++k) {
+  for (int k = 0; k < G::NK; ++k) {
     const int i = tid + 256 * k;
     const int rp = i / TCQ;
-    const int p = rp % T::IP, r = rp / T::IP;
+    const int p = rp % G::IP, r = rp / G::IP;
     const int hh = h0 - 1 + r, ww = w0 - 1 + p;
-    in[k] = (i < T::N4) && hh >= 0 && hh < g.H && ww >= 0 && ww < g.W;
+    in[k] = (i < G::N4) && hh >= 0 && hh < g.H && ww >= 0 && ww < g.W;
     v[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (in[k]) v[k] = ld4(x + (((long)b * g.H + hh) * g.W + ww) * g.C + c0 + 4 * q);
+    if (in[k]) v[k] = ldq(x + (((long)b * g.H + hh) * g.W + ww) * g.C + c0 + 4 * q);
   }
 #pragma unroll
-  for (int k = 0; k < T::NK; ++k) {
+  for (int k = 0; k < G::NK; ++k) {
     const int i = tid + 256 * k;
-    if (i < T::N4) {
+    if (i < G::N4) {
       float4 a = v[k];
       if (pro && in[k]) {
         a.x = apply_act(a.x * ps.x + pb.x, act);
@@ -415,16 +410,16 @@ ACC_DEV void dw_fill_tile(float4* __restrict__ tile, const float* __restrict__ x
 // NEXT chunk adds (r0+9 .. r0+12) are fetched into registers before this chunk is
 // computed and parked afterwards in the slots of rows r0-1 .. r0+2 (dead by then),
 // so HBM reads stay in flight through the compute (software pipeline).
-template <int TCQ, bool BNB>
+template <int TCQ, bool BNB, typename T>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BNB ? 2 : 3)))
-dw3x3_tile_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
+dw3x3_tile_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
                       const float* __restrict__ bias, const float* __restrict__ sc,
-                      const float* __restrict__ sh, int act, int flip, float* __restrict__ z,
-                      double* __restrict__ stats, DwTGeom g, const float* __restrict__ bz,
+                      const float* __restrict__ sh, int act, int flip, T* __restrict__ z,
+                      double* __restrict__ stats, DwTGeom g, const T* __restrict__ bz,
                       const float* __restrict__ bst, int bact) {
-  typedef DwT<TCQ> T;
-  constexpr int CR = T::CR;
-  __shared__ float4 tile[T::N4 > 1024 ? T::N4 : 1024];
+  typedef DwT<TCQ> G;
+  constexpr int CR = G::CR;
+  __shared__ float4 tile[G::N4 > 1024 ? G::N4 : 1024];
   // bz != null (data gradient, flip = 1): stats receive the BatchNorm-backward partials
   // (sum g, sum g*(bz - mean)) of g = out * act'(bz*scale + shift) instead of (sum, sumsq)
   const bool bnb = BNB && stats != nullptr && bz != nullptr;
@@ -443,7 +438,7 @@ dw3x3_tile_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
   t /= g.tilesW;
   const int th = t % g.tilesH;
   const int b = t / g.tilesH;
-  const int hbeg = th * DW_TR * g.rch, w0 = tw * T::TP;
+  const int hbeg = th * DW_TR * g.rch, w0 = tw * G::TP;
   const int hend = min(g.H, hbeg + DW_TR * g.rch);
   const int nch = (hend - hbeg + CR - 1) / CR;
   const bool pro = sc != nullptr;
@@ -453,9 +448,9 @@ dw3x3_tile_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
     pb = ld4(sh + c);
   }
   {
-    float4 v[T::NK];
-    dw_fetch_rows<TCQ, T::NK>(v, x, g, b, hbeg - 1, T::N4, w0, c0);
-    dw_park_rows<TCQ, T::NK>(tile, v, g, hbeg - 1, T::N4, w0, hbeg, pro, ps, pb, act);
+    float4 v[G::NK];
+    dw_fetch_rows<TCQ, G::NK>(v, x, g, b, hbeg - 1, G::N4, w0, c0);
+    dw_park_rows<TCQ, G::NK>(tile, v, g, hbeg - 1, G::N4, w0, hbeg, pro, ps, pb, act);
   }
   float k[9][4], bi[4];
 #pragma unroll
@@ -482,7 +477,7 @@ dw3x3_tile_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
 #pragma unroll
     for (int r = 0; r < CR; ++r)
       zz[r] = (w < g.W && rbase + r < hend)
-                  ? ld4(bz + (((long)b * g.H + rbase + r) * g.W + w) * g.C + c)
+                  ? ldq(bz + (((long)b * g.H + rbase + r) * g.W + w) * g.C + c)
                   : make_float4(0.f, 0.f, 0.f, 0.f);
   };
   if (bnb) fetch_z(zcur, hbeg);
@@ -490,18 +485,18 @@ dw3x3_tile_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
     const int r0 = hbeg + CR * kc;
     // rows r0+9 .. are needed only if the strip's last input row (hend) lies there
     const bool more = kc + 1 < nch && r0 + 9 <= hend;
-    float4 nx[T::NK8];
-    if (more) dw_fetch_rows<TCQ, T::NK8>(nx, x, g, b, r0 + 9, T::N8, w0, c0);
+    float4 nx[G::NK8];
+    if (more) dw_fetch_rows<TCQ, G::NK8>(nx, x, g, b, r0 + 9, G::N8, w0, c0);
     if (bnb && kc + 1 < nch) fetch_z(znext, r0 + CR);
     if (w < g.W) {
-      const int base = (CR * kc) % T::IR;  // slot of input row r0 - 1
+      const int base = (CR * kc) % G::IR;  // slot of input row r0 - 1
       float win[3][3][4];
       auto rd = [&](int j, float (&row)[3][4]) {
         int sl = base + j;
-        sl = sl >= T::IR ? sl - T::IR : sl;
+        sl = sl >= G::IR ? sl - G::IR : sl;
 #pragma unroll
         for (int dx = 0; dx < 3; ++dx) {
-          float4 a = tile[(sl * T::IP + p + dx) * TCQ + q];
+          float4 a = tile[(sl * G::IP + p + dx) * TCQ + q];
           row[dx][0] = a.x; row[dx][1] = a.y; row[dx][2] = a.z; row[dx][3] = a.w;
         }
       };
@@ -520,6 +515,7 @@ dw3x3_tile_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
             for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
               for (int dx = 0; dx < 3; ++dx) acc = fmaf(k[dy * 3 + dx][j], win[dy][dx][j], acc);
+            acc = rnd<T>(acc);  // statistics of the stored value
             o[j] = acc;
             if (bnb) {
               const float zz = f4get(zcur[r], j);
@@ -532,7 +528,7 @@ dw3x3_tile_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
               s2[j] += (double)acc * acc;
             }
           }
-          st4_nt(z + (((long)b * g.H + r0 + r) * g.W + w) * g.C + c, make_float4(o[0], o[1], o[2], o[3]));
+          stq_nt(z + (((long)b * g.H + r0 + r) * g.W + w) * g.C + c, make_float4(o[0], o[1], o[2], o[3]));
 #pragma unroll
           for (int dx = 0; dx < 3; ++dx)
 #pragma unroll
@@ -545,7 +541,7 @@ dw3x3_tile_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
     }
     if (more) {
       __syncthreads();  // every thread is done with rows r0-1 .. r0+CR-2
-      dw_park_rows<TCQ, T::NK8>(tile, nx, g, r0 + 9, T::N8, w0, hbeg, pro, ps, pb, act);
+      dw_park_rows<TCQ, G::NK8>(tile, nx, g, r0 + 9, G::N8, w0, hbeg, pro, ps, pb, act);
       __syncthreads();
     }
     if (bnb) {
@@ -568,13 +564,13 @@ dw3x3_tile_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
   }
 }
 
-template <int TCQ>
+template <int TCQ, typename T>
 __global__ void __launch_bounds__(256)
-dw3x3_tile_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dz,
+dw3x3_tile_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dz,
                         const float* __restrict__ sc, const float* __restrict__ sh, int act,
                         float* __restrict__ part, DwTGeom g) {
-  typedef DwT<TCQ> T;
-  __shared__ float4 tile[T::N4 > 1024 ? T::N4 : 1024];
+  typedef DwT<TCQ> G;
+  __shared__ float4 tile[G::N4 > 1024 ? G::N4 : 1024];
   const int tid = threadIdx.x;
   const int q = tid % TCQ, p = tid / TCQ;
   const int c0 = blockIdx.y * TCQ * 4;
@@ -584,7 +580,7 @@ dw3x3_tile_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ d
   t /= g.tilesW;
   const int th = t % g.tilesH;
   const int b = t / g.tilesH;
-  const int h0 = th * DW_TR, w0 = tw * T::TP;
+  const int h0 = th * DW_TR, w0 = tw * G::TP;
   const int w = w0 + p;
   const int nr = min(DW_TR, g.H - h0);
   // this thread's dz column (independent loads issued before the tile fill completes)
@@ -592,7 +588,7 @@ dw3x3_tile_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ d
 #pragma unroll
   for (int r = 0; r < DW_TR; ++r) {
     d[r] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (w < g.W && r < nr) d[r] = ld4(dz + (((long)b * g.H + h0 + r) * g.W + w) * g.C + c);
+    if (w < g.W && r < nr) d[r] = ldq(dz + (((long)b * g.H + h0 + r) * g.W + w) * g.C + c);
   }
   dw_fill_tile<TCQ>(tile, x, sc, sh, act, g, b, h0, w0, c0);
   __syncthreads();
@@ -606,7 +602,7 @@ dw3x3_tile_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ d
     auto rd = [&](int r, float (&row)[3][4]) {
 #pragma unroll
       for (int dx = 0; dx < 3; ++dx) {
-        float4 a = tile[(r * T::IP + p + dx) * TCQ + q];
+        float4 a = tile[(r * G::IP + p + dx) * TCQ + q];
         row[dx][0] = a.x; row[dx][1] = a.y; row[dx][2] = a.z; row[dx][3] = a.w;
       }
     };
@@ -751,44 +747,57 @@ extern "C" int accunet_dw3x3_rows(int B, int H, int W, int C) {
   return (int)grid.x;
 }
 
-extern "C" int accunet_dw3x3_fwd(const float* x, const float* wt, const float* bias,
-                                 const float* sc, const float* sh, int act, int flip, float* z,
-                                 double* stats, int B, int H, int W, int C, const float* bz,
-                                 const float* bst, int bact, void* stream) {
+extern "C" int accunet_dw3x3_fwd(const void* x, const float* wt, const float* bias,
+                                 const float* sc, const float* sh, int act, int flip, void* z,
+                                 double* stats, int B, int H, int W, int C, const void* bz,
+                                 const float* bst, int bact, int dt, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (bz && (!bst || !stats)) return ACC_EBADARG;
   dim3 grid;
   int tcq = dw_tile_tcq(W, C);
   if (tcq) {
     DwTGeom tg = dw_tgeom(B, H, W, C, tcq, &grid, dw_rch_max());
+    // non-temporal loads only for inputs above the Infinity Cache (bytes as stored)
+    tg.ntl = dw_ntl((long)B * H * W * C * (dt == ACC_BF16 ? 2 : 4));
     if (dw_cgfast() && grid.y > 1) {
       tg.cgf = (int)grid.y;
       grid = dim3(grid.x * grid.y, 1);
     }
-    if (bz) {
-      if (tcq == 16)
-        hipLaunchKernelGGL((dw3x3_tile_fwd_kernel<16, true>), grid, dim3(256), 0, s, x, wt, bias, sc,
-                           sh, act, flip, z, stats, tg, bz, bst, bact);
-      else
-        hipLaunchKernelGGL((dw3x3_tile_fwd_kernel<8, true>), grid, dim3(256), 0, s, x, wt, bias, sc,
-                           sh, act, flip, z, stats, tg, bz, bst, bact);
-    } else if (tcq == 16) {
-      hipLaunchKernelGGL((dw3x3_tile_fwd_kernel<16, false>), grid, dim3(256), 0, s, x, wt, bias, sc,
-                         sh, act, flip, z, stats, tg, bz, bst, bact);
-    } else {
-      hipLaunchKernelGGL((dw3x3_tile_fwd_kernel<8, false>), grid, dim3(256), 0, s, x, wt, bias, sc,
-                         sh, act, flip, z, stats, tg, bz, bst, bact);
-    }
+    if (with_dt(dt, [&](auto tag) {
+          using T = decltype(tag);
+          const T* xx = (const T*)x;
+          const T* zb = (const T*)bz;
+          T* zz = (T*)z;
+          if (bz) {
+            if (tcq == 16)
+              hipLaunchKernelGGL((dw3x3_tile_fwd_kernel<16, true, T>), grid, dim3(256), 0, s, xx, wt,
+                                 bias, sc, sh, act, flip, zz, stats, tg, zb, bst, bact);
+            else
+              hipLaunchKernelGGL((dw3x3_tile_fwd_kernel<8, true, T>), grid, dim3(256), 0, s, xx, wt,
+                                 bias, sc, sh, act, flip, zz, stats, tg, zb, bst, bact);
+          } else if (tcq == 16) {
+            hipLaunchKernelGGL((dw3x3_tile_fwd_kernel<16, false, T>), grid, dim3(256), 0, s, xx, wt,
+                               bias, sc, sh, act, flip, zz, stats, tg, zb, bst, bact);
+          } else {
+            hipLaunchKernelGGL((dw3x3_tile_fwd_kernel<8, false, T>), grid, dim3(256), 0, s, xx, wt,
+                               bias, sc, sh, act, flip, zz, stats, tg, zb, bst, bact);
+          }
+        }))
+      return ACC_EBADARG;
     return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
   }
   int V = (C % 4 == 0) ? 4 : 1;
   DwGeom g = dw_geom(B, H, W, C, V, &grid);
-  if (V == 4)
-    hipLaunchKernelGGL(dw3x3_fwd_kernel<4>, grid, dim3(256), 0, s, x, wt, bias, sc, sh, act, flip,
-                       z, stats, g, bz, bst, bact);
-  else
-    hipLaunchKernelGGL(dw3x3_fwd_kernel<1>, grid, dim3(256), 0, s, x, wt, bias, sc, sh, act, flip,
-                       z, stats, g, bz, bst, bact);
+  if (with_dt(dt, [&](auto tag) {
+        using T = decltype(tag);
+        if (V == 4)
+          hipLaunchKernelGGL((dw3x3_fwd_kernel<4, T>), grid, dim3(256), 0, s, (const T*)x, wt, bias,
+                             sc, sh, act, flip, (T*)z, stats, g, (const T*)bz, bst, bact);
+        else
+          hipLaunchKernelGGL((dw3x3_fwd_kernel<1, T>), grid, dim3(256), 0, s, (const T*)x, wt, bias,
+                             sc, sh, act, flip, (T*)z, stats, g, (const T*)bz, bst, bact);
+      }))
+    return ACC_EBADARG;
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 
@@ -807,9 +816,9 @@ size_t dw_wgrad_ws(int B, int H, int W, int C) {
 
 extern "C" size_t accunet_dw3x3_wgrad_ws(int B, int H, int W, int C) { return dw_wgrad_ws(B, H, W, C); }
 
-extern "C" int accunet_dw3x3_wgrad(const float* x, const float* dz, const float* sc,
+extern "C" int accunet_dw3x3_wgrad(const void* x, const void* dz, const float* sc,
                                    const float* sh, int act, float* dw, float* db, int B, int H,
-                                   int W, int C, float* ws, size_t ws_elems, void* stream) {
+                                   int W, int C, float* ws, size_t ws_elems, int dt, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   int V = (C % 4 == 0) ? 4 : 1;
   dim3 grid;
@@ -823,14 +832,24 @@ extern "C" int accunet_dw3x3_wgrad(const float* x, const float* dz, const float*
   float* part = ws;
   float* scratch = ws + (size_t)R * 10 * C;
   float* sums = scratch + accunet_partials_ws_elems(R, 10 * C);
-  if (tcq == 16)
-    hipLaunchKernelGGL(dw3x3_tile_wgrad_kernel<16>, grid, dim3(256), 0, s, x, dz, sc, sh, act, part, tg);
-  else if (tcq == 8)
-    hipLaunchKernelGGL(dw3x3_tile_wgrad_kernel<8>, grid, dim3(256), 0, s, x, dz, sc, sh, act, part, tg);
-  else if (V == 4)
-    hipLaunchKernelGGL(dw3x3_wgrad_kernel<4>, grid, dim3(256), 0, s, x, dz, sc, sh, act, part, g);
-  else
-    hipLaunchKernelGGL(dw3x3_wgrad_kernel<1>, grid, dim3(256), 0, s, x, dz, sc, sh, act, part, g);
+  if (with_dt(dt, [&](auto tag) {
+        using T = decltype(tag);
+        const T* xx = (const T*)x;
+        const T* dd = (const T*)dz;
+        if (tcq == 16)
+          hipLaunchKernelGGL((dw3x3_tile_wgrad_kernel<16, T>), grid, dim3(256), 0, s, xx, dd, sc, sh,
+                             act, part, tg);
+        else if (tcq == 8)
+          hipLaunchKernelGGL((dw3x3_tile_wgrad_kernel<8, T>), grid, dim3(256), 0, s, xx, dd, sc, sh,
+                             act, part, tg);
+        else if (V == 4)
+          hipLaunchKernelGGL((dw3x3_wgrad_kernel<4, T>), grid, dim3(256), 0, s, xx, dd, sc, sh, act,
+                             part, g);
+        else
+          hipLaunchKernelGGL((dw3x3_wgrad_kernel<1, T>), grid, dim3(256), 0, s, xx, dd, sc, sh, act,
+                             part, g);
+      }))
+    return ACC_EBADARG;
   int rows;
   const float* pr = reduce_partials(part, R, 10 * C, scratch, &rows, s);
   hipLaunchKernelGGL(sum_rows_kernel, dim3(ceil_div(10 * C, 64)), dim3(256), 0, s, pr, rows, 10 * C,

@@ -1,6 +1,7 @@
-// Tile selection + template dispatch for gemm_f32_kernel.
+// Tile selection + template dispatch for gemm_f32_kernel / gemm_bf16_kernel.
 #pragma once
 #include "gemm_f32.h"
+#include "gemm_bf16.h"
 
 // Tile configurations (WM, TM, TN) -> (BM, BN):
 //   T_A 128x128 (2,2,2)  T_B 128x64 (2,2,1)  T_C 128x32 (4,1,1)
@@ -35,6 +36,27 @@ typedef void (*gemm_kfn)(const GemmParams);
 // forward GEMMs: optional (sum, sumsq) statistics of C for the consumer BatchNorm
 #define GEMM_DEFINE_TABLE_S(NAME, AM, BMo, PA, PB) GEMM_DEFINE_TABLE_E(NAME, AM, BMo, PA, PB, EPI_STATS)
 
+// bf16 engine tables (same tile order). Storage per table: forward / data-gradient
+// GEMMs read bf16 activations and fp32 weights and write bf16; weight gradients
+// read two bf16 activation operands and write fp32.
+#define GEMM_DEFINE_BTABLE_E(NAME, AM, BMo, PA, PB, EPI, TA, TB, TC)                        \
+  gemm_kfn NAME[2][TILE_COUNT] = {                                                        \
+      {gemm_bf16_kernel<AM, BMo, PA, PB, false, false, 2, 2, 2, EPI, TA, TB, TC>,         \
+       gemm_bf16_kernel<AM, BMo, PA, PB, false, false, 2, 2, 1, EPI, TA, TB, TC>,         \
+       gemm_bf16_kernel<AM, BMo, PA, PB, false, false, 4, 1, 1, EPI, TA, TB, TC>,         \
+       gemm_bf16_kernel<AM, BMo, PA, PB, false, false, 1, 1, 1, EPI, TA, TB, TC>,         \
+       gemm_bf16_kernel<AM, BMo, PA, PB, false, false, 2, 1, 1, EPI, TA, TB, TC>},        \
+      {gemm_bf16_kernel<AM, BMo, PA, PB, true, true, 2, 2, 2, EPI, TA, TB, TC>,           \
+       gemm_bf16_kernel<AM, BMo, PA, PB, true, true, 2, 2, 1, EPI, TA, TB, TC>,           \
+       gemm_bf16_kernel<AM, BMo, PA, PB, true, true, 4, 1, 1, EPI, TA, TB, TC>,           \
+       gemm_bf16_kernel<AM, BMo, PA, PB, true, true, 1, 1, 1, EPI, TA, TB, TC>,           \
+       gemm_bf16_kernel<AM, BMo, PA, PB, true, true, 2, 1, 1, EPI, TA, TB, TC>}};
+// forward / data gradient: bf16 x fp32-weight -> bf16; weight gradient: bf16 x bf16 -> fp32
+#define GEMM_DEFINE_BTABLE_FWD(NAME, AM, BMo, PA, PB, EPI) \
+  GEMM_DEFINE_BTABLE_E(NAME, AM, BMo, PA, PB, EPI, bf16_t, float, bf16_t)
+#define GEMM_DEFINE_BTABLE_WGRAD(NAME, AM, BMo, PA, PB) \
+  GEMM_DEFINE_BTABLE_E(NAME, AM, BMo, PA, PB, 0, bf16_t, bf16_t, float)
+
 GEMM_DECLARE_TABLE(g_gemm_row_nt_p0)
 GEMM_DECLARE_TABLE(g_gemm_row_nt_p1)
 GEMM_DECLARE_TABLE(g_gemm_row_nt_p2)
@@ -50,15 +72,33 @@ GEMM_DECLARE_TABLE(g_gemm_col_nn_p0)
 GEMM_DECLARE_TABLE(g_gemm_col_nn_p1)
 GEMM_DECLARE_TABLE(g_gemm_col_nn_p2)
 GEMM_DECLARE_TABLE(g_gemm_col_nnsh3)
+GEMM_DECLARE_TABLE(g_bgemm_row_nt_p0)
+GEMM_DECLARE_TABLE(g_bgemm_row_nt_p1)
+GEMM_DECLARE_TABLE(g_bgemm_row_nt_p2)
+GEMM_DECLARE_TABLE(g_bgemm_row_nt_p0_ups)
+GEMM_DECLARE_TABLE(g_bgemm_row_nt_p1_ups)
+GEMM_DECLARE_TABLE(g_bgemm_row_nt_p2_ups)
+GEMM_DECLARE_TABLE(g_bgemm_sh3_nt)
+GEMM_DECLARE_TABLE(g_bgemm_row_nn)
+GEMM_DECLARE_TABLE(g_bgemm_row_nn_bnb)
+GEMM_DECLARE_TABLE(g_bgemm_row_nn_pyr)
+GEMM_DECLARE_TABLE(g_bgemm_row_nn_bnb_pyr)
+GEMM_DECLARE_TABLE(g_bgemm_col_nn_p0)
+GEMM_DECLARE_TABLE(g_bgemm_col_nn_p1)
+GEMM_DECLARE_TABLE(g_bgemm_col_nn_p2)
+GEMM_DECLARE_TABLE(g_bgemm_col_nnsh3)
 
 // Host-side driver: picks a tile, split-K factor and launches. ws (workspace,
 // may be null) is used for split-K partial slabs; if the split would not fit it
 // falls back to no split. Returns ACC_OK or an error code.
+// adt / bdt / cdt: storage of A, B and C (+ activation-shaped epilogue operands):
+// all ACC_F32 -> fp32 engine; adt = ACC_BF16 -> bf16 engine (bdt fp32 weights or bf16
+// activations, cdt bf16 or fp32 as the tables above).
 int gemm_run(GemmParams p, int amode, int bmode, int pro_a, int pro_b, bool allow_split,
-             float* ws, size_t ws_elems, hipStream_t stream);
+             float* ws, size_t ws_elems, int adt, int bdt, int cdt, hipStream_t stream);
 
 // Skinny weight-gradient path (csrc/gemm_skinny.hip): returns the number of
 // [M][N] partial slabs written into ws (to be summed by the split-K reduction),
 // or 0 when the shape does not qualify.
 int gemm_skinny_try(const GemmParams& p, int amode, int bmode, int pro_a, int pro_b, float* ws,
-                    size_t ws_elems, hipStream_t stream);
+                    size_t ws_elems, int dt, hipStream_t stream);

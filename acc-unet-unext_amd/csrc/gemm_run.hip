@@ -1,5 +1,6 @@
-// Host driver for the fp32 MFMA GEMM: tile choice, split-K, deterministic
-// split-K reduction (fixed slab order, no float atomics).
+// Host driver for the MFMA GEMM engines (fp32: gemm_f32.h, bf16: gemm_bf16.h): engine
+// and tile choice, split-K, deterministic split-K reduction (fixed slab order, no
+// float atomics).
 #include "gemm_dispatch.h"
 #include <string.h>
 #include <stdlib.h>
@@ -45,40 +46,58 @@ splitk_reduce_kernel(const float* __restrict__ ws, float* __restrict__ C, int M,
 }
 
 // epi: the EPI_* features this launch needs
-static gemm_kfn* table_for(int amode, int bmode, int pro_a, int pro_b, int epi) {
-  if (epi & (EPI_BNB | EPI_PYR)) {  // data-gradient epilogues
-    if (amode != AM_ROW || bmode != BM_NN || pro_a != PRO_NONE || pro_b != PRO_NONE ||
-        (epi & (EPI_UPS | EPI_STATS)))
-      return nullptr;
-    if (epi == EPI_BNB) return g_gemm_row_nn_bnb[0];
-    if (epi == EPI_PYR) return g_gemm_row_nn_pyr[0];
-    return g_gemm_row_nn_bnb_pyr[0];
-  }
-  if (amode == AM_ROW && bmode == BM_NT && pro_b == PRO_NONE) {
-    const bool u = (epi & EPI_UPS) != 0;
-    if (pro_a == PRO_NONE) return u ? g_gemm_row_nt_p0_ups[0] : g_gemm_row_nt_p0[0];
-    if (pro_a == PRO_AFFINE) return u ? g_gemm_row_nt_p1_ups[0] : g_gemm_row_nt_p1[0];
-    if (pro_a == PRO_AFFINE_LRELU) return u ? g_gemm_row_nt_p2_ups[0] : g_gemm_row_nt_p2[0];
-  }
-  if (epi & EPI_UPS) return nullptr;  // nearest-up addends: forward 1x1 GEMMs only
-  if (amode == AM_SHIFT3 && bmode == BM_NT && pro_a == PRO_NONE && pro_b == PRO_NONE)
-    return g_gemm_sh3_nt[0];
-  if (epi & EPI_STATS) return nullptr;  // C statistics: forward tables only
-  if (amode == AM_ROW && bmode == BM_NN && pro_a == PRO_NONE && pro_b == PRO_NONE)
-    return g_gemm_row_nn[0];
-  if (amode == AM_COL && bmode == BM_NN && pro_a == PRO_NONE) {
-    if (pro_b == PRO_NONE) return g_gemm_col_nn_p0[0];
-    if (pro_b == PRO_AFFINE) return g_gemm_col_nn_p1[0];
-    if (pro_b == PRO_AFFINE_LRELU) return g_gemm_col_nn_p2[0];
-  }
-  if (amode == AM_COL && bmode == BM_NN_SHIFT3 && pro_a == PRO_NONE && pro_b == PRO_NONE)
-    return g_gemm_col_nnsh3[0];
+#define GEMM_TABLE_SELECT(P)                                                                    \
+  if (epi & (EPI_BNB | EPI_PYR)) { /* data-gradient epilogues */                               \
+    if (amode != AM_ROW || bmode != BM_NN || pro_a != PRO_NONE || pro_b != PRO_NONE ||          \
+        (epi & (EPI_UPS | EPI_STATS)))                                                          \
+      return nullptr;                                                                           \
+    if (epi == EPI_BNB) return P##row_nn_bnb[0];                                                \
+    if (epi == EPI_PYR) return P##row_nn_pyr[0];                                                \
+    return P##row_nn_bnb_pyr[0];                                                                \
+  }                                                                                             \
+  if (amode == AM_ROW && bmode == BM_NT && pro_b == PRO_NONE) {                                 \
+    const bool u = (epi & EPI_UPS) != 0;                                                        \
+    if (pro_a == PRO_NONE) return u ? P##row_nt_p0_ups[0] : P##row_nt_p0[0];                    \
+    if (pro_a == PRO_AFFINE) return u ? P##row_nt_p1_ups[0] : P##row_nt_p1[0];                  \
+    if (pro_a == PRO_AFFINE_LRELU) return u ? P##row_nt_p2_ups[0] : P##row_nt_p2[0];            \
+  }                                                                                             \
+  if (epi & EPI_UPS) return nullptr; /* nearest-up addends: forward 1x1 GEMMs only */           \
+  if (amode == AM_SHIFT3 && bmode == BM_NT && pro_a == PRO_NONE && pro_b == PRO_NONE)           \
+    return P##sh3_nt[0];                                                                        \
+  if (epi & EPI_STATS) return nullptr; /* C statistics: forward tables only */                  \
+  if (amode == AM_ROW && bmode == BM_NN && pro_a == PRO_NONE && pro_b == PRO_NONE)              \
+    return P##row_nn[0];                                                                        \
+  if (amode == AM_COL && bmode == BM_NN && pro_a == PRO_NONE) {                                 \
+    if (pro_b == PRO_NONE) return P##col_nn_p0[0];                                              \
+    if (pro_b == PRO_AFFINE) return P##col_nn_p1[0];                                            \
+    if (pro_b == PRO_AFFINE_LRELU) return P##col_nn_p2[0];                                      \
+  }                                                                                             \
+  if (amode == AM_COL && bmode == BM_NN_SHIFT3 && pro_a == PRO_NONE && pro_b == PRO_NONE)       \
+    return P##col_nnsh3[0];                                                                     \
   return nullptr;
+
+// bf16 engine: forward / data-gradient tables take (bf16, fp32 weights) -> bf16, the
+// weight-gradient (AM_COL) tables (bf16, bf16) -> fp32
+static gemm_kfn* table_for_bf16(int amode, int bmode, int pro_a, int pro_b, int epi, int bdt,
+                                int cdt) {
+  const bool wgrad = amode == AM_COL;
+  if (wgrad ? (bdt != ACC_BF16 || cdt != ACC_F32) : (bdt != ACC_F32 || cdt != ACC_BF16))
+    return nullptr;
+  GEMM_TABLE_SELECT(g_bgemm_)
 }
 
-static gemm_kfn* table_v(int amode, int bmode, int pro_a, int pro_b, int epi, int v) {
+static gemm_kfn* table_for(int amode, int bmode, int pro_a, int pro_b, int epi) {
+  GEMM_TABLE_SELECT(g_gemm_)
+}
+
+static gemm_kfn* table_v(int amode, int bmode, int pro_a, int pro_b, int epi, int v, int adt,
+                         int bdt, int cdt) {
   // the tables are [2][TILE_COUNT]; table_for returns row 0
-  gemm_kfn* t0 = table_for(amode, bmode, pro_a, pro_b, epi);
+  gemm_kfn* t0 = nullptr;
+  if (adt == ACC_F32 && bdt == ACC_F32 && cdt == ACC_F32)
+    t0 = table_for(amode, bmode, pro_a, pro_b, epi);
+  else if (adt == ACC_BF16)
+    t0 = table_for_bf16(amode, bmode, pro_a, pro_b, epi, bdt, cdt);
   return t0 ? t0 + v * TILE_COUNT : nullptr;
 }
 
@@ -127,45 +146,52 @@ static int pick_tile(int M, int N, int K, int bmode, int cin, bool can_split) {
 }
 
 int gemm_run(GemmParams p, int amode, int bmode, int pro_a, int pro_b, bool allow_split,
-             float* ws, size_t ws_elems, hipStream_t stream) {
+             float* ws, size_t ws_elems, int adt, int bdt, int cdt, hipStream_t stream) {
   if (p.M <= 0 || p.N <= 0) return ACC_OK;
   if ((amode == AM_SHIFT3 || bmode == BM_NN_SHIFT3) && p.cin <= 0) return ACC_EBADSHAPE;
-  // vectorised (float4) operand loads need every contiguous extent % 4 == 0
+  const bool bf = adt == ACC_BF16;
+  // vectorised operand loads need every contiguous extent to be a whole number of
+  // chunks: fp32 engine float4 (4 elements, 16 B), bf16 engine 8 elements (16 B bf16 /
+  // 32 B fp32 weights), with chunk-aligned base pointers
+  const int q = bf ? 7 : 3;
+  const uintptr_t aal = 15, bal = 15;
   bool vec = true;
   if (amode == AM_ROW) {
     for (int s = 0; s < p.nsrc; ++s) {
       int w = p.kbeg[s + 1] - p.kbeg[s];
-      if ((w & 3) || (p.lda[s] & 3) || ((uintptr_t)p.A[s] & 15)) vec = false;
+      if ((w & q) || (p.lda[s] & q) || ((uintptr_t)p.A[s] & aal)) vec = false;
     }
-    if (p.K & 3) vec = false;
+    if (p.K & q) vec = false;
   } else if (amode == AM_SHIFT3) {
-    if ((p.cin & 3) || (p.lda[0] & 3) || ((uintptr_t)p.A[0] & 15)) vec = false;
+    if ((p.cin & q) || (p.lda[0] & q) || ((uintptr_t)p.A[0] & aal)) vec = false;
   } else {  // AM_COL
-    if ((p.M & 3) || (p.lda[0] & 3) || ((uintptr_t)p.A[0] & 15)) vec = false;
+    if ((p.M & q) || (p.lda[0] & q) || ((uintptr_t)p.A[0] & aal)) vec = false;
   }
   if (bmode == BM_NT) {
-    if ((p.K & 3) || (p.ldb & 3) || ((uintptr_t)p.B & 15)) vec = false;
+    if ((p.K & q) || (p.ldb & q) || ((uintptr_t)p.B & bal)) vec = false;
   } else {
-    if ((p.N & 3) || (p.ldb & 3) || ((uintptr_t)p.B & 15)) vec = false;
-    if (bmode == BM_NN_SHIFT3 && (p.cin & 3)) vec = false;
+    if ((p.N & q) || (p.ldb & q) || ((uintptr_t)p.B & bal)) vec = false;
+    if (bmode == BM_NN_SHIFT3 && (p.cin & q)) vec = false;
   }
   if (amode == AM_ROW && p.nsrc == 1) { p.kbeg[0] = 0; p.kbeg[1] = p.K; }
-  if (allow_split) {
-    const int S = gemm_skinny_try(p, amode, bmode, pro_a, pro_b, ws, ws_elems, stream);
+  if (allow_split && cdt == ACC_F32 && adt == bdt) {
+    const int S = gemm_skinny_try(p, amode, bmode, pro_a, pro_b, ws, ws_elems, adt, stream);
     if (S > 0) {
       const long total = (long)p.M * p.N;
       hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((total + SPLITK_COLS - 1) / SPLITK_COLS)),
-                         dim3(SPLITK_COLS * SPLITK_GROUPS), 0, stream, ws, p.C, p.M, p.N, p.ldc, S,
+                         dim3(SPLITK_COLS * SPLITK_GROUPS), 0, stream, ws, (float*)p.C, p.M, p.N, p.ldc, S,
                          (size_t)total);
       return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
     }
   }
   const int epi = (p.bz ? EPI_BNB : 0) | (p.pd2 ? EPI_PYR : 0) | (p.nup > 0 ? EPI_UPS : 0) |
                   ((p.stats && !p.bz) ? EPI_STATS : 0);
-  gemm_kfn* tab = table_v(amode, bmode, pro_a, pro_b, epi, vec ? 1 : 0);
+  gemm_kfn* tab = table_v(amode, bmode, pro_a, pro_b, epi, vec ? 1 : 0, adt, bdt, cdt);
   if (!tab) return ACC_EBADARG;
+  // split-K slabs are fp32: only GEMMs whose C is fp32 (weight gradients) split
   const bool can_split = allow_split && ws != nullptr && p.bias == nullptr && p.nup == 0 &&
-                         p.stats == nullptr && p.pd2 == nullptr;
+                         p.stats == nullptr && p.pd2 == nullptr && cdt == ACC_F32;
+  const int BK = bf ? GB_BK : GEMM_BK;
   int t = pick_tile(p.M, p.N, p.K, bmode, p.cin, can_split);
   int BM = tile_bm(t), BN = tile_bn(t);
   int gx = ceil_div(p.M, BM), gy = ceil_div(p.N, BN);
@@ -173,20 +199,19 @@ int gemm_run(GemmParams p, int amode, int bmode, int pro_a, int pro_b, bool allo
   int S = 1;
   p.kchunk = p.K;
   p.zstride = 0;
-  float* Cfinal = p.C;
+  float* Cfinal = (float*)p.C;  // split-K runs only with cdt == ACC_F32
   int ldc_final = p.ldc;
-  if (allow_split && ws != nullptr && p.bias == nullptr && p.nup == 0 && p.stats == nullptr &&
-      p.pd2 == nullptr) {
+  if (can_split) {
     long tiles = (long)gx * gy;
     long target = tiles >= split_min_tiles() ? 1 : 1024;  // enough tiles: no split, no reduce
-    long maxS = p.K / (GEMM_BK * 4);
+    long maxS = p.K / (BK * 4);
     long want = (target + tiles - 1) / tiles;
     S = (int)(want < maxS ? want : maxS);
     if (S < 1) S = 1;
     while (S > 1 && (size_t)S * p.M * p.N > ws_elems) --S;
     if (S > 1) {
       int kt = ceil_div(p.K, S);
-      kt = ceil_div(kt, GEMM_BK) * GEMM_BK;
+      kt = ceil_div(kt, BK) * BK;
       S = ceil_div(p.K, kt);
       p.kchunk = kt;
       p.zstride = (size_t)p.M * p.N;
@@ -195,10 +220,12 @@ int gemm_run(GemmParams p, int amode, int bmode, int pro_a, int pro_b, bool allo
     }
   }
   {
-    // 16-byte epilogue accesses: C rows, up-add rows and pyramid rows all 4-float aligned
-    bool ev = (p.N % 4 == 0) && (p.ldc % 4 == 0) && (((uintptr_t)p.C & 15) == 0);
+    // quad (4-element) epilogue accesses: C rows, up-add rows and pyramid rows all
+    // 4-element aligned (16 B fp32 / 8 B bf16)
+    const uintptr_t cal = (cdt == ACC_BF16 && S == 1) ? 7 : 15;
+    bool ev = (p.N % 4 == 0) && (p.ldc % 4 == 0) && (((uintptr_t)p.C & cal) == 0);
     for (int u = 0; u < p.nup; ++u)
-      if ((p.upld[u] % 4) || ((uintptr_t)p.up[u] & 15)) ev = false;
+      if ((p.upld[u] % 4) || ((uintptr_t)p.up[u] & cal)) ev = false;
     p.evec = ev ? 1 : 0;
   }
   dim3 grid(gx, gy, S);
@@ -263,11 +290,14 @@ extern "C" int accunet_gemm(const AccGemmDesc* d, float* ws, size_t ws_elems, vo
   p.bst = d->bst;
   p.bact = d->bact;
   if (p.bz && (!p.bst || !p.stats)) return ACC_EBADARG;
+  if (d->adt < ACC_F32 || d->adt > ACC_BF16 || d->bdt < ACC_F32 || d->bdt > ACC_BF16 ||
+      d->cdt < ACC_F32 || d->cdt > ACC_BF16)
+    return ACC_EBADARG;
   if (p.pd2 && (!p.mk2 || (p.pd4 && !p.mk4) || (p.H & 1) || (p.W & 1) ||
                 (p.pd4 && ((p.H & 3) || (p.W & 3))) || p.ldc != p.N))
     return ACC_EBADARG;
   return gemm_run(p, d->amode, d->bmode, d->pro_a, d->pro_b, d->allow_split != 0, ws, ws_elems,
-                  (hipStream_t)stream);
+                  d->adt, d->bdt, d->cdt, (hipStream_t)stream);
 }
 
 extern "C" int accunet_gemm_stats_rows(int M, int N, int K, int amode, int bmode, int cin) {

@@ -21,9 +21,9 @@
 
 struct SkinnyParams {
   int M, N, K;
-  const float* A;
+  const void* A;  // fp32 or bf16 (kernel type T)
   int lda;
-  const float* B;
+  const void* B;
   int ldb;
   const float* b_scale;
   const float* b_shift;
@@ -35,7 +35,7 @@ struct SkinnyParams {
   FastDiv fW, fH;
 };
 
-template <int TI, int TJ, int PROB, bool SH3>
+template <int TI, int TJ, int PROB, bool SH3, typename T>
 __global__ void __launch_bounds__(256) gemm_skinny_kernel(const SkinnyParams p) {
   __shared__ float red[4][32 * 32];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -78,23 +78,23 @@ __global__ void __launch_bounds__(256) gemm_skinny_kernel(const SkinnyParams p) 
     for (int u = 0; u < SK_U; ++u) {
       const long kk = k + 2 * u + lh;
       const bool ok = kk < k1;
-      const float* ar = p.A + kk * p.lda + l31;
+      const T* ar = (const T*)p.A + kk * p.lda + l31;
 #pragma unroll
-      for (int i = 0; i < TI; ++i) a[u][i] = (ok && mok[i]) ? ar[i * 32] : 0.f;
+      for (int i = 0; i < TI; ++i) a[u][i] = (ok && mok[i]) ? ld1(ar + i * 32) : 0.f;
       int hh = 0, ww = 0;
       if (SH3 && ok) {
         const uint32_t q = fdiv((uint32_t)kk, p.fW);
         ww = (int)kk - (int)q * p.W;
         hh = (int)(q - fdiv(q, p.fH) * p.H);
       }
-      const float* br = p.B + kk * p.ldb;
+      const T* br = (const T*)p.B + kk * p.ldb;
 #pragma unroll
       for (int j = 0; j < TJ; ++j) {
         bool in = ok && nok[j];
         if (SH3)
           in = in && hh + bdh[j] >= 0 && hh + bdh[j] < p.H && ww + bdw[j] >= 0 &&
                ww + bdw[j] < p.W;
-        float v = in ? br[boff[j]] : 0.f;
+        float v = in ? ld1(br + boff[j]) : 0.f;
         if (PROB != PRO_NONE && in) v = pro_apply<PROB>(v, bs[j], bh[j]);
         b[u][j] = v;
       }
@@ -128,10 +128,10 @@ __global__ void __launch_bounds__(256) gemm_skinny_kernel(const SkinnyParams p) 
 
 typedef void (*skinny_kfn)(const SkinnyParams);
 
-template <int PROB, bool SH3>
+template <int PROB, bool SH3, typename T>
 static skinny_kfn skinny_pick(int TI, int TJ) {
 #define SK_CASE(I, J) \
-  if (TI == I && TJ == J) return gemm_skinny_kernel<I, J, PROB, SH3>;
+  if (TI == I && TJ == J) return gemm_skinny_kernel<I, J, PROB, SH3, T>;
   SK_CASE(1, 1) SK_CASE(1, 2) SK_CASE(2, 1) SK_CASE(1, 3) SK_CASE(3, 1)
 #undef SK_CASE
   return nullptr;
@@ -139,8 +139,17 @@ static skinny_kfn skinny_pick(int TI, int TJ) {
 
 // Launches the skinny path if the shape qualifies; returns the number of slabs it
 // wrote into ws (the caller reduces them), or 0 if the tiled GEMM should run.
+template <typename T>
+static skinny_kfn skinny_fn(bool sh3, int pro_b, int TI, int TJ) {
+  return sh3 ? skinny_pick<PRO_NONE, true, T>(TI, TJ)
+         : pro_b == PRO_NONE ? skinny_pick<PRO_NONE, false, T>(TI, TJ)
+         : pro_b == PRO_AFFINE ? skinny_pick<PRO_AFFINE, false, T>(TI, TJ)
+                               : skinny_pick<PRO_AFFINE_LRELU, false, T>(TI, TJ);
+}
+
+// dt: storage of both operands (A = dY, B = X); the slabs are fp32
 int gemm_skinny_try(const GemmParams& p, int amode, int bmode, int pro_a, int pro_b, float* ws,
-                    size_t ws_elems, hipStream_t stream) {
+                    size_t ws_elems, int dt, hipStream_t stream) {
   static int off = -1;
   if (off < 0) {
     const char* e = getenv("ACCUNET_NO_SKINNY");  // A/B knob
@@ -158,10 +167,8 @@ int gemm_skinny_try(const GemmParams& p, int amode, int bmode, int pro_a, int pr
   // K pair makes the tiled kernel equal or better (64x64 at K 262144: 40 vs 36 us;
   // the 32 x 288 3x3 weight gradient as 1 x 9 tiles: 539 vs 361 us)
   if (TI * TJ > 3) return 0;
-  skinny_kfn fn = sh3 ? skinny_pick<PRO_NONE, true>(TI, TJ)
-                  : pro_b == PRO_NONE ? skinny_pick<PRO_NONE, false>(TI, TJ)
-                  : pro_b == PRO_AFFINE ? skinny_pick<PRO_AFFINE, false>(TI, TJ)
-                                        : skinny_pick<PRO_AFFINE_LRELU, false>(TI, TJ);
+  skinny_kfn fn = dt == ACC_BF16 ? skinny_fn<bf16_t>(sh3, pro_b, TI, TJ)
+                                 : skinny_fn<float>(sh3, pro_b, TI, TJ);
   if (!fn) return 0;
   // blocks: ~4 per CU for the stream, fewer if the slabs would not fit ws
   long nb = 1024;

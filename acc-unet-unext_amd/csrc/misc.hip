@@ -16,15 +16,16 @@
 // ---------------------------------------------------------------------------
 // Forward: TQ = C/4 lanes per pixel (a power of two <= 64) each load one 16-byte
 // channel quad (coalesced rows), dot with w, xor-shuffle sum over the TQ lanes.
+template <typename T>
 __global__ void __launch_bounds__(256)
-head_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ b,
+head_fwd_kernel(const T* __restrict__ x, const float* __restrict__ w, const float* __restrict__ b,
                 int sigm, float* __restrict__ y, long P, int C, int TQ) {
   const int q = threadIdx.x % TQ;
   const int ppb = 256 / TQ;  // pixels per block sweep
   const float4 wq = ld4(w + 4 * q);
   const float bias = b[0];
   for (long p = (long)blockIdx.x * ppb + threadIdx.x / TQ; p < P; p += (long)gridDim.x * ppb) {
-    const float4 xv = ld4(x + p * C + 4 * q);
+    const float4 xv = ldq(x + p * C + 4 * q);
     float acc = xv.x * wq.x;
     acc = fmaf(xv.y, wq.y, acc);
     acc = fmaf(xv.z, wq.z, acc);
@@ -38,13 +39,14 @@ head_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w, const 
 }
 
 // generic fallback (C % 4 != 0 or C/4 not a power of two): one thread per pixel
+template <typename T>
 __global__ void __launch_bounds__(256)
-head_fwd_scalar_kernel(const float* __restrict__ x, const float* __restrict__ w,
+head_fwd_scalar_kernel(const T* __restrict__ x, const float* __restrict__ w,
                        const float* __restrict__ b, int sigm, float* __restrict__ y, long P, int C) {
   for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < P; p += (long)gridDim.x * blockDim.x) {
-    const float* xr = x + p * C;
+    const T* xr = x + p * C;
     float acc = 0.f;
-    for (int c = 0; c < C; ++c) acc = fmaf(xr[c], w[c], acc);
+    for (int c = 0; c < C; ++c) acc = fmaf(ld1(xr + c), w[c], acc);
     acc += b[0];
     y[p] = sigm ? 1.f / (1.f + expf(-acc)) : acc;
   }
@@ -53,9 +55,10 @@ head_fwd_scalar_kernel(const float* __restrict__ x, const float* __restrict__ w,
 // Backward (C % 4 == 0, C/4 a power of two <= 64): dx[p,c] = g[p]*w[c],
 // g = dy (* y(1-y) for the Sigmoid); per-block partials part[blk][2][C] of
 // (sum g*x[c], sum g) through the channel-tiled deterministic block reduction.
+template <typename T>
 __global__ void __launch_bounds__(256)
-head_bwd_kernel(const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ y,
-                const float* __restrict__ dy, int sigm, float* __restrict__ dx, long P, int C,
+head_bwd_kernel(const T* __restrict__ x, const float* __restrict__ w, const float* __restrict__ y,
+                const float* __restrict__ dy, int sigm, T* __restrict__ dx, long P, int C,
                 float* __restrict__ part) {
   ChanTile t = chan_tile<4>(C);
   float a[4] = {0.f, 0.f, 0.f, 0.f}, gs[4] = {0.f, 0.f, 0.f, 0.f};
@@ -69,8 +72,8 @@ head_bwd_kernel(const float* __restrict__ x, const float* __restrict__ w, const 
         const float yy = y[p];
         g *= yy * (1.f - yy);
       }
-      const float4 xv = ld4(x + p * C + t.c0);
-      st4(dx + p * C + t.c0, make_float4(g * wq.x, g * wq.y, g * wq.z, g * wq.w));
+      const float4 xv = ldq(x + p * C + t.c0);
+      stq(dx + p * C + t.c0, make_float4(g * wq.x, g * wq.y, g * wq.z, g * wq.w));
       a[0] = fmaf(g, xv.x, a[0]);
       a[1] = fmaf(g, xv.y, a[1]);
       a[2] = fmaf(g, xv.z, a[2]);
@@ -81,10 +84,11 @@ head_bwd_kernel(const float* __restrict__ x, const float* __restrict__ w, const 
   block_chan_reduce2<4>(t, a, gs, part, blockIdx.x, C);
 }
 
+template <typename T>
 __global__ void __launch_bounds__(256)
-head_bwd_scalar_kernel(const float* __restrict__ x, const float* __restrict__ w,
+head_bwd_scalar_kernel(const T* __restrict__ x, const float* __restrict__ w,
                        const float* __restrict__ y, const float* __restrict__ dy, int sigm,
-                       float* __restrict__ dx, long P, int C, float* __restrict__ part) {
+                       T* __restrict__ dx, long P, int C, float* __restrict__ part) {
   __shared__ float red[256][33];
   float acc[33];
   for (int c = 0; c <= C && c < 33; ++c) acc[c] = 0.f;
@@ -96,11 +100,11 @@ head_bwd_scalar_kernel(const float* __restrict__ x, const float* __restrict__ w,
       float yy = y[p];
       g *= yy * (1.f - yy);
     }
-    const float* xr = x + p * C;
-    float* dr = dx + p * C;
+    const T* xr = x + p * C;
+    T* dr = dx + p * C;
     for (int c = 0; c < C; ++c) {
-      dr[c] = g * w[c];
-      acc[c] = fmaf(g, xr[c], acc[c]);
+      st1(dr + c, g * w[c]);
+      acc[c] = fmaf(g, ld1(xr + c), acc[c]);
     }
     acc[C] += g;
   }
@@ -128,20 +132,24 @@ static int head_tq(int C) {
   return (q & (q - 1)) == 0 && q <= 64 ? q : 0;
 }
 
-extern "C" int accunet_head_fwd(const float* x, const float* w, const float* b, int sigm, float* y,
-                                long P, int C, void* stream) {
+extern "C" int accunet_head_fwd(const void* x, const float* w, const float* b, int sigm, float* y,
+                                long P, int C, int dt, void* stream) {
   const int tq = head_tq(C);
-  if (tq) {
-    long blocks = (P * tq + 255) / 256;
-    if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL(head_fwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, w, b,
-                       sigm, y, P, C, tq);
-  } else {
-    long blocks = (P + 255) / 256;
-    if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(head_fwd_scalar_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x,
-                       w, b, sigm, y, P, C);
-  }
+  if (with_dt(dt, [&](auto tag) {
+        using T = decltype(tag);
+        if (tq) {
+          long blocks = (P * tq + 255) / 256;
+          if (blocks > 8192) blocks = 8192;
+          hipLaunchKernelGGL((head_fwd_kernel<T>), dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                             (const T*)x, w, b, sigm, y, P, C, tq);
+        } else {
+          long blocks = (P + 255) / 256;
+          if (blocks > 4096) blocks = 4096;
+          hipLaunchKernelGGL((head_fwd_scalar_kernel<T>), dim3(blocks), dim3(256), 0,
+                             (hipStream_t)stream, (const T*)x, w, b, sigm, y, P, C);
+        }
+      }))
+    return ACC_EBADARG;
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 
@@ -150,9 +158,9 @@ extern "C" size_t accunet_head_ws_elems(long P, int C) {
   return (size_t)HEAD_NB * 2 * C + accunet_partials_ws_elems(HEAD_NB, 2 * C) + 2 * (size_t)C + 64;
 }
 
-extern "C" int accunet_head_bwd(const float* x, const float* w, const float* y, const float* dy,
-                                int sigm, float* dx, float* dw, float* db, long P, int C, float* ws,
-                                size_t ws_elems, void* stream) {
+extern "C" int accunet_head_bwd(const void* x, const float* w, const float* y, const float* dy,
+                                int sigm, void* dx, float* dw, float* db, long P, int C, float* ws,
+                                size_t ws_elems, int dt, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const int tq = head_tq(C);
   if (!tq && C > 32) return ACC_EBADSHAPE;
@@ -162,12 +170,16 @@ extern "C" int accunet_head_bwd(const float* x, const float* w, const float* y, 
   float* part = ws;
   float* scratch = ws + (size_t)HEAD_NB * 2 * C;
   float* sums = scratch + accunet_partials_ws_elems(HEAD_NB, 2 * C);
-  if (tq)
-    hipLaunchKernelGGL(head_bwd_kernel, dim3((unsigned)nb, ceil_div(C / 4, 64)), dim3(256), 0, s, x,
-                       w, y, dy, sigm, dx, P, C, part);
-  else
-    hipLaunchKernelGGL(head_bwd_scalar_kernel, dim3((unsigned)nb), dim3(256), 0, s, x, w, y, dy,
-                       sigm, dx, P, C, part);
+  if (with_dt(dt, [&](auto tag) {
+        using T = decltype(tag);
+        if (tq)
+          hipLaunchKernelGGL((head_bwd_kernel<T>), dim3((unsigned)nb, ceil_div(C / 4, 64)), dim3(256),
+                             0, s, (const T*)x, w, y, dy, sigm, (T*)dx, P, C, part);
+        else
+          hipLaunchKernelGGL((head_bwd_scalar_kernel<T>), dim3((unsigned)nb), dim3(256), 0, s,
+                             (const T*)x, w, y, dy, sigm, (T*)dx, P, C, part);
+      }))
+    return ACC_EBADARG;
   int rows;
   const float* pr = reduce_partials(part, (int)nb, 2 * C, scratch, &rows, s);
   hipLaunchKernelGGL(sum_rows_kernel, dim3(ceil_div(2 * C, 64)), dim3(256), 0, s, pr, rows, 2 * C,
@@ -411,13 +423,14 @@ extern "C" int accunet_adam_step(const void* table, const int* chunk_t, const lo
 // out[0] = sum_i g[i] * (a[i] - b[i])  (gradient of ACC_UNet_W's scalar merge weight,
 // ACC_UNet/ACC_UNet_w.py:497-522: y = m*W + x*(1-W)); deterministic two-level sum.
 // ---------------------------------------------------------------------------
+template <typename T>
 __global__ void __launch_bounds__(256)
-dotdiff_kernel(const float* __restrict__ g, const float* __restrict__ a, const float* __restrict__ b,
+dotdiff_kernel(const T* __restrict__ g, const T* __restrict__ a, const T* __restrict__ b,
                long n, float* __restrict__ part) {
   __shared__ float red[256];
   float s = 0.f;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
-    s += g[i] * (a[i] - b[i]);
+    s += ld1(g + i) * (ld1(a + i) - ld1(b + i));
   red[threadIdx.x] = s;
   __syncthreads();
   for (int k = 128; k > 0; k >>= 1) {
@@ -435,19 +448,24 @@ __global__ void finish_sum_kernel(const float* __restrict__ part, int n, float* 
   out[0] = accumulate ? out[0] + (float)s : (float)s;
 }
 
-extern "C" int accunet_dotdiff(const float* g, const float* a, const float* b, long n, float* out,
-                               int accumulate, float* ws, void* stream) {
+extern "C" int accunet_dotdiff(const void* g, const void* a, const void* b, long n, float* out,
+                               int accumulate, float* ws, int dt, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(dotdiff_kernel, dim3(1024), dim3(256), 0, s, g, a, b, n, ws);
+  if (with_dt(dt, [&](auto tag) {
+        using T = decltype(tag);
+        hipLaunchKernelGGL((dotdiff_kernel<T>), dim3(1024), dim3(256), 0, s, (const T*)g,
+                           (const T*)a, (const T*)b, n, ws);
+      }))
+    return ACC_EBADARG;
   hipLaunchKernelGGL(finish_sum_kernel, dim3(1), dim3(64), 0, s, ws, 1024, out, accumulate);
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 
 // y = a*w + b*(1-w) (w device scalar), with optional partial channel stats of y
-template <int V>
+template <int V, typename T>
 __global__ void __launch_bounds__(256)
-wmerge_kernel(const float* __restrict__ a, const float* __restrict__ b, const float* __restrict__ w,
-              float* __restrict__ y, long P, int C, double* __restrict__ stats) {
+wmerge_kernel(const T* __restrict__ a, const T* __restrict__ b, const float* __restrict__ w,
+              T* __restrict__ y, long P, int C, double* __restrict__ stats) {
   ChanTile t = chan_tile<V>(C);
   long rows_per = (P + gridDim.x - 1) / gridDim.x;
   long r0 = blockIdx.x * rows_per, r1 = min(P, r0 + rows_per);
@@ -462,7 +480,7 @@ wmerge_kernel(const float* __restrict__ a, const float* __restrict__ b, const fl
       ldv<V>(b + r * C + t.c0, vb);
 #pragma unroll
       for (int j = 0; j < V; ++j) {
-        va[j] = va[j] * wv + vb[j] * (1.f - wv);
+        va[j] = rnd<T>(va[j] * wv + vb[j] * (1.f - wv));  // statistics of the stored value
         s1[j] += va[j];
         s2[j] += (double)va[j] * va[j];
       }
@@ -472,34 +490,46 @@ wmerge_kernel(const float* __restrict__ a, const float* __restrict__ b, const fl
   if (stats) block_chan_reduce2<V>(t, s1, s2, stats, blockIdx.x, C);
 }
 
-extern "C" int accunet_wmerge_fwd(const float* a, const float* b, const float* w, float* y, long P,
-                                  int C, double* stats, void* stream) {
+extern "C" int accunet_wmerge_fwd(const void* a, const void* b, const float* w, void* y, long P,
+                                  int C, double* stats, int dt, void* stream) {
   int V = (C % 4 == 0) ? 4 : 1;
   int nb = stream_rowblocks(P, C);
   dim3 grid(nb, ceil_div(C / V, 64));
-  if (V == 4)
-    hipLaunchKernelGGL(wmerge_kernel<4>, grid, dim3(256), 0, (hipStream_t)stream, a, b, w, y, P, C, stats);
-  else
-    hipLaunchKernelGGL(wmerge_kernel<1>, grid, dim3(256), 0, (hipStream_t)stream, a, b, w, y, P, C, stats);
+  if (with_dt(dt, [&](auto tag) {
+        using T = decltype(tag);
+        if (V == 4)
+          hipLaunchKernelGGL((wmerge_kernel<4, T>), grid, dim3(256), 0, (hipStream_t)stream,
+                             (const T*)a, (const T*)b, w, (T*)y, P, C, stats);
+        else
+          hipLaunchKernelGGL((wmerge_kernel<1, T>), grid, dim3(256), 0, (hipStream_t)stream,
+                             (const T*)a, (const T*)b, w, (T*)y, P, C, stats);
+      }))
+    return ACC_EBADARG;
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 
 // dA = w*g, dB = (1-w)*g (B gradient optionally accumulated)
+template <typename T>
 __global__ void __launch_bounds__(256)
-wmerge_bwd_kernel(const float* __restrict__ g, const float* __restrict__ w, float* __restrict__ da,
-                  float* __restrict__ db, long n) {
+wmerge_bwd_kernel(const T* __restrict__ g, const float* __restrict__ w, T* __restrict__ da,
+                  T* __restrict__ db, long n) {
   const float wv = w[0];
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    float gv = g[i];
-    da[i] = wv * gv;
-    db[i] = (1.f - wv) * gv;
+    float gv = ld1(g + i);
+    st1(da + i, wv * gv);
+    st1(db + i, (1.f - wv) * gv);
   }
 }
 
-extern "C" int accunet_wmerge_bwd(const float* g, const float* w, float* da, float* db, long n,
+extern "C" int accunet_wmerge_bwd(const void* g, const float* w, void* da, void* db, long n, int dt,
                                   void* stream) {
   long blocks = (n + 255) / 256;
   if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(wmerge_bwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, g, w, da, db, n);
+  if (with_dt(dt, [&](auto tag) {
+        using T = decltype(tag);
+        hipLaunchKernelGGL((wmerge_bwd_kernel<T>), dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                           (const T*)g, w, (T*)da, (T*)db, n);
+      }))
+    return ACC_EBADARG;
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }

@@ -1,4 +1,4 @@
-// Pooling / resampling / layout kernels on NHWC fp32.
+// Pooling / resampling / layout kernels on NHWC fp32 / bf16 activations.
 //
 //  - HANC neighbourhood pyramid (HANCLayer, ACC_UNet/ACC_UNet.py:86-106): from the
 //    pending-BN input a = act(x*scale+shift) produce at 1/2 resolution
@@ -19,11 +19,11 @@
 // V = 4 moves channel quads (16-byte loads/stores, 4-byte mask stores). The
 // per-element arithmetic is the same for every V.
 // ---------------------------------------------------------------------------
-template <int V>
+template <int V, typename T>
 __global__ void __launch_bounds__(256)
-hanc_pyramid_fwd_kernel(const float* __restrict__ x, const float* __restrict__ sc,
+hanc_pyramid_fwd_kernel(const T* __restrict__ x, const float* __restrict__ sc,
                         const float* __restrict__ sh, int act, int B, int H, int W, int C, int k,
-                        float* __restrict__ p2, float* __restrict__ p4,
+                        T* __restrict__ p2, T* __restrict__ p4,
                         unsigned char* __restrict__ mk2, unsigned char* __restrict__ mk4) {
   // k == 3: cell = 4x4 (one P4 pixel, four P2 pixels); k == 2: cell = 2x2 (one P2 pixel)
   const int cs = (k == 3) ? 4 : 2;
@@ -45,7 +45,7 @@ hanc_pyramid_fwd_kernel(const float* __restrict__ x, const float* __restrict__ s
       h[j] = pro ? sh[c + j] : 0.f;
     }
     float v[4][4][V];
-    const float* src = x + (((long)b * H + hc * cs) * W + wc * cs) * C + c;
+    const T* src = x + (((long)b * H + hc * cs) * W + wc * cs) * C + c;
 #pragma unroll
     for (int dy = 0; dy < 4; ++dy)
 #pragma unroll
@@ -127,12 +127,13 @@ hanc_pyramid_fwd_kernel(const float* __restrict__ x, const float* __restrict__ s
 }
 
 // pyramid backward: da (+)= spread(dP2) + spread(dP4); accumulate into da
+template <typename T>
 __global__ void __launch_bounds__(256)
-hanc_pyramid_bwd_kernel(const float* __restrict__ x, const float* __restrict__ sc,
+hanc_pyramid_bwd_kernel(const T* __restrict__ x, const float* __restrict__ sc,
                         const float* __restrict__ sh, int act, int B, int H, int W, int C, int k,
-                        const float* __restrict__ p2, const float* __restrict__ p4,
-                        const float* __restrict__ dp2, const float* __restrict__ dp4,
-                        float* __restrict__ da) {
+                        const T* __restrict__ p2, const T* __restrict__ p4,
+                        const T* __restrict__ dp2, const T* __restrict__ dp4,
+                        T* __restrict__ da) {
   const int cs = (k == 3) ? 4 : 2;
   const int Hc = H / cs, Wc = W / cs;
   long total = (long)B * Hc * Wc * C;
@@ -153,7 +154,7 @@ hanc_pyramid_bwd_kernel(const float* __restrict__ x, const float* __restrict__ s
       for (int dx = 0; dx < 4; ++dx) {
         g[dy][dx] = 0.f;
         if (dy < cs && dx < cs) {
-          float q = x[(((long)b * H + hc * cs + dy) * W + wc * cs + dx) * C + c];
+          float q = ld1(x + (((long)b * H + hc * cs + dy) * W + wc * cs + dx) * C + c);
           v[dy][dx] = pro ? apply_act(q * s + h, act) : q;
         }
       }
@@ -162,9 +163,9 @@ hanc_pyramid_bwd_kernel(const float* __restrict__ x, const float* __restrict__ s
     for (int qy = 0; qy < n2; ++qy)
       for (int qx = 0; qx < n2; ++qx) {
         long o = (((long)b * H2 + hc * n2 + qy) * W2 + wc * n2 + qx) * (2 * C);
-        float gav = dp2[o + c] * 0.25f;
-        float gmx = dp2[o + C + c];
-        float mx = p2[o + C + c];
+        float gav = ld1(dp2 + o + c) * 0.25f;
+        float gmx = ld1(dp2 + o + C + c);
+        float mx = ld1(p2 + o + C + c);
         bool done = false;
         for (int dy = 0; dy < 2; ++dy)
           for (int dx = 0; dx < 2; ++dx) {
@@ -178,9 +179,9 @@ hanc_pyramid_bwd_kernel(const float* __restrict__ x, const float* __restrict__ s
       }
     if (k == 3) {
       long o = (((long)b * Hc + hc) * Wc + wc) * (2 * C);
-      float gav = dp4[o + c] * (1.f / 16.f);
-      float gmx = dp4[o + C + c];
-      float mx = p4[o + C + c];
+      float gav = ld1(dp4 + o + c) * (1.f / 16.f);
+      float gmx = ld1(dp4 + o + C + c);
+      float mx = ld1(p4 + o + C + c);
       bool done = false;
 #pragma unroll
       for (int dy = 0; dy < 4; ++dy)
@@ -197,7 +198,10 @@ hanc_pyramid_bwd_kernel(const float* __restrict__ x, const float* __restrict__ s
     for (int dy = 0; dy < 4; ++dy)
 #pragma unroll
       for (int dx = 0; dx < 4; ++dx)
-        if (dy < cs && dx < cs) da[(((long)b * H + hc * cs + dy) * W + wc * cs + dx) * C + c] += g[dy][dx];
+        if (dy < cs && dx < cs) {
+          T* d = da + (((long)b * H + hc * cs + dy) * W + wc * cs + dx) * C + c;
+          st1(d, ld1(d) + g[dy][dx]);
+        }
   }
 }
 
@@ -208,45 +212,57 @@ static int grid_for(long total) {
   return (int)b;
 }
 
-extern "C" int accunet_hanc_pyramid_fwd(const float* x, const float* sc, const float* sh, int act,
-                                        int B, int H, int W, int C, int k, float* p2, float* p4,
-                                        unsigned char* mk2, unsigned char* mk4, void* stream) {
+extern "C" int accunet_hanc_pyramid_fwd(const void* x, const float* sc, const float* sh, int act,
+                                        int B, int H, int W, int C, int k, void* p2, void* p4,
+                                        unsigned char* mk2, unsigned char* mk4, int dt,
+                                        void* stream) {
   if (k < 2 || k > 3) return ACC_EBADARG;
   int cs = (k == 3) ? 4 : 2;
   if (H % cs || W % cs) return ACC_EBADSHAPE;
   long total = (long)B * (H / cs) * (W / cs) * C;
-  // quads need 16-byte aligned rows: C % 4 == 0 and aligned base pointers
-  const bool q4 = C % 4 == 0 && !((uintptr_t)x & 15) && !((uintptr_t)p2 & 15) &&
-                  (k != 3 || !((uintptr_t)p4 & 15)) && !((uintptr_t)mk2 & 3) &&
+  // quads need aligned rows (16 B fp32 / 8 B bf16): C % 4 == 0 and aligned base pointers
+  const uintptr_t al = dt == ACC_BF16 ? 7 : 15;
+  const bool q4 = C % 4 == 0 && !((uintptr_t)x & al) && !((uintptr_t)p2 & al) &&
+                  (k != 3 || !((uintptr_t)p4 & al)) && !((uintptr_t)mk2 & 3) &&
                   (k != 3 || !((uintptr_t)mk4 & 3));
-  if (q4)
-    hipLaunchKernelGGL(hanc_pyramid_fwd_kernel<4>, dim3(grid_for(total / 4)), dim3(256), 0,
-                       (hipStream_t)stream, x, sc, sh, act, B, H, W, C, k, p2, p4, mk2,
-                       k == 3 ? mk4 : nullptr);
-  else
-    hipLaunchKernelGGL(hanc_pyramid_fwd_kernel<1>, dim3(grid_for(total)), dim3(256), 0,
-                       (hipStream_t)stream, x, sc, sh, act, B, H, W, C, k, p2, p4, mk2,
-                       k == 3 ? mk4 : nullptr);
+  if (with_dt(dt, [&](auto tag) {
+        using T = decltype(tag);
+        if (q4)
+          hipLaunchKernelGGL((hanc_pyramid_fwd_kernel<4, T>), dim3(grid_for(total / 4)), dim3(256), 0,
+                             (hipStream_t)stream, (const T*)x, sc, sh, act, B, H, W, C, k, (T*)p2,
+                             (T*)p4, mk2, k == 3 ? mk4 : nullptr);
+        else
+          hipLaunchKernelGGL((hanc_pyramid_fwd_kernel<1, T>), dim3(grid_for(total)), dim3(256), 0,
+                             (hipStream_t)stream, (const T*)x, sc, sh, act, B, H, W, C, k, (T*)p2,
+                             (T*)p4, mk2, k == 3 ? mk4 : nullptr);
+      }))
+    return ACC_EBADARG;
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 
-extern "C" int accunet_hanc_pyramid_bwd(const float* x, const float* sc, const float* sh, int act,
-                                        int B, int H, int W, int C, int k, const float* p2,
-                                        const float* p4, const float* dp2, const float* dp4,
-                                        float* da, void* stream) {
+extern "C" int accunet_hanc_pyramid_bwd(const void* x, const float* sc, const float* sh, int act,
+                                        int B, int H, int W, int C, int k, const void* p2,
+                                        const void* p4, const void* dp2, const void* dp4,
+                                        void* da, int dt, void* stream) {
   if (k < 2 || k > 3) return ACC_EBADARG;
   int cs = (k == 3) ? 4 : 2;
   long total = (long)B * (H / cs) * (W / cs) * C;
-  hipLaunchKernelGGL(hanc_pyramid_bwd_kernel, dim3(grid_for(total)), dim3(256), 0,
-                     (hipStream_t)stream, x, sc, sh, act, B, H, W, C, k, p2, p4, dp2, dp4, da);
+  if (with_dt(dt, [&](auto tag) {
+        using T = decltype(tag);
+        hipLaunchKernelGGL((hanc_pyramid_bwd_kernel<T>), dim3(grid_for(total)), dim3(256), 0,
+                           (hipStream_t)stream, (const T*)x, sc, sh, act, B, H, W, C, k,
+                           (const T*)p2, (const T*)p4, (const T*)dp2, (const T*)dp4, (T*)da);
+      }))
+    return ACC_EBADARG;
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 
 // ---------------------------------------------------------------------------
 // 2x2 pooling (stride 2): mode 0 = max, 1 = avg. Backward recomputes argmax.
 // ---------------------------------------------------------------------------
+template <typename T>
 __global__ void __launch_bounds__(256)
-pool2_fwd_kernel(const float* __restrict__ x, float* __restrict__ y, int B, int H, int W, int C,
+pool2_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int B, int H, int W, int C,
                  int mode) {
   const int Ho = H / 2, Wo = W / 2;
   long total = (long)B * Ho * Wo * C;
@@ -258,15 +274,16 @@ pool2_fwd_kernel(const float* __restrict__ x, float* __restrict__ y, int B, int 
     long t = pix / Wo;
     int ho = (int)(t % Ho);
     int b = (int)(t / Ho);
-    const float* p = x + (((long)b * H + 2 * ho) * W + 2 * wo) * C + c;
-    float a0 = p[0], a1 = p[C], a2 = p[(long)W * C], a3 = p[(long)W * C + C];
-    y[i] = mode == 0 ? fmaxf(fmaxf(a0, a1), fmaxf(a2, a3)) : (((a0 + a1) + a2) + a3) * 0.25f;
+    const T* p = x + (((long)b * H + 2 * ho) * W + 2 * wo) * C + c;
+    float a0 = ld1(p), a1 = ld1(p + C), a2 = ld1(p + (long)W * C), a3 = ld1(p + (long)W * C + C);
+    st1(y + i, mode == 0 ? fmaxf(fmaxf(a0, a1), fmaxf(a2, a3)) : (((a0 + a1) + a2) + a3) * 0.25f);
   }
 }
 
+template <typename T>
 __global__ void __launch_bounds__(256)
-pool2_bwd_kernel(const float* __restrict__ x, const float* __restrict__ y,
-                 const float* __restrict__ dy, float* __restrict__ dx, int B, int H, int W, int C,
+pool2_bwd_kernel(const T* __restrict__ x, const T* __restrict__ y,
+                 const T* __restrict__ dy, T* __restrict__ dx, int B, int H, int W, int C,
                  int mode, int accumulate) {
   const int Ho = H / 2, Wo = W / 2;
   long total = (long)B * Ho * Wo * C;
@@ -280,15 +297,15 @@ pool2_bwd_kernel(const float* __restrict__ x, const float* __restrict__ y,
     int b = (int)(t / Ho);
     long base = (((long)b * H + 2 * ho) * W + 2 * wo) * C + c;
     long off[4] = {base, base + C, base + (long)W * C, base + (long)W * C + C};
-    float g = dy[i];
+    float g = ld1(dy + i);
     float gv[4];
     if (mode == 0) {
-      float m = y[i];
+      float m = ld1(y + i);
       bool done = false;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         gv[j] = 0.f;
-        if (!done && x[off[j]] == m) {
+        if (!done && ld1(x + off[j]) == m) {
           gv[j] = g;
           done = true;
         }
@@ -298,24 +315,34 @@ pool2_bwd_kernel(const float* __restrict__ x, const float* __restrict__ y,
       for (int j = 0; j < 4; ++j) gv[j] = 0.25f * g;
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) dx[off[j]] = accumulate ? dx[off[j]] + gv[j] : gv[j];
+    for (int j = 0; j < 4; ++j) st1(dx + off[j], accumulate ? ld1(dx + off[j]) + gv[j] : gv[j]);
   }
 }
 
-extern "C" int accunet_pool2_fwd(const float* x, float* y, int B, int H, int W, int C, int mode,
-                                 void* stream) {
+extern "C" int accunet_pool2_fwd(const void* x, void* y, int B, int H, int W, int C, int mode,
+                                 int dt, void* stream) {
   if (H % 2 || W % 2) return ACC_EBADSHAPE;
   long total = (long)B * (H / 2) * (W / 2) * C;
-  hipLaunchKernelGGL(pool2_fwd_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, x,
-                     y, B, H, W, C, mode);
+  if (with_dt(dt, [&](auto tag) {
+        using T = decltype(tag);
+        hipLaunchKernelGGL((pool2_fwd_kernel<T>), dim3(grid_for(total)), dim3(256), 0,
+                           (hipStream_t)stream, (const T*)x, (T*)y, B, H, W, C, mode);
+      }))
+    return ACC_EBADARG;
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 
-extern "C" int accunet_pool2_bwd(const float* x, const float* y, const float* dy, float* dx, int B,
-                                 int H, int W, int C, int mode, int accumulate, void* stream) {
+extern "C" int accunet_pool2_bwd(const void* x, const void* y, const void* dy, void* dx, int B,
+                                 int H, int W, int C, int mode, int accumulate, int dt,
+                                 void* stream) {
   long total = (long)B * (H / 2) * (W / 2) * C;
-  hipLaunchKernelGGL(pool2_bwd_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, x,
-                     y, dy, dx, B, H, W, C, mode, accumulate);
+  if (with_dt(dt, [&](auto tag) {
+        using T = decltype(tag);
+        hipLaunchKernelGGL((pool2_bwd_kernel<T>), dim3(grid_for(total)), dim3(256), 0,
+                           (hipStream_t)stream, (const T*)x, (const T*)y, (const T*)dy, (T*)dx, B, H,
+                           W, C, mode, accumulate);
+      }))
+    return ACC_EBADARG;
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 
@@ -323,9 +350,9 @@ extern "C" int accunet_pool2_bwd(const float* x, const float* y, const float* dy
 // Nearest-upsample backward: out[b,hs,ws,c] (+)= sum over the f x f block of
 // in[b, hs*f+dy, ws*f+dx, in_off + c] (in has ld_in channels per pixel).
 // ---------------------------------------------------------------------------
-template <int F>  // F > 0: compile-time factor (the f*f loads unrolled); 0: runtime f
+template <int F, typename T>  // F > 0: compile-time factor (the f*f loads unrolled); 0: runtime f
 __global__ void __launch_bounds__(256)
-blocksum_kernel(const float* __restrict__ in, int ld_in, int in_off, float* __restrict__ out,
+blocksum_kernel(const T* __restrict__ in, int ld_in, int in_off, T* __restrict__ out,
                 int ld_out, int B, int H, int W, int C, int f_rt, int accumulate) {
   const int f = F > 0 ? F : f_rt;
   const int Hs = H / f, Ws = W / f;
@@ -338,69 +365,81 @@ blocksum_kernel(const float* __restrict__ in, int ld_in, int in_off, float* __re
     long t = pix / Ws;
     int hs = (int)(t % Hs);
     int b = (int)(t / Hs);
-    const float* src = in + (((long)b * H + hs * f) * W + ws * f) * ld_in + in_off + c;
+    const T* src = in + (((long)b * H + hs * f) * W + ws * f) * ld_in + in_off + c;
     float s = 0.f;
     if (F > 0) {
       float v[F > 0 ? F * F : 1];
 #pragma unroll
       for (int dy = 0; dy < F; ++dy)
 #pragma unroll
-        for (int dx = 0; dx < F; ++dx) v[dy * F + dx] = src[((long)dy * W + dx) * ld_in];
+        for (int dx = 0; dx < F; ++dx) v[dy * F + dx] = ld1(src + ((long)dy * W + dx) * ld_in);
 #pragma unroll
       for (int k = 0; k < F * F; ++k) s += v[k];  // same (dy, dx) order as below
     } else {
       for (int dy = 0; dy < f; ++dy)
-        for (int dx = 0; dx < f; ++dx) s += src[((long)dy * W + dx) * ld_in];
+        for (int dx = 0; dx < f; ++dx) s += ld1(src + ((long)dy * W + dx) * ld_in);
     }
-    float* o = out + pix * ld_out + c;
-    *o = accumulate ? *o + s : s;
+    T* o = out + pix * ld_out + c;
+    st1(o, accumulate ? ld1(o) + s : s);
   }
 }
 
-extern "C" int accunet_upsample_bwd(const float* in, int ld_in, int in_off, float* out, int ld_out,
-                                    int B, int H, int W, int C, int f, int accumulate,
+extern "C" int accunet_upsample_bwd(const void* in, int ld_in, int in_off, void* out, int ld_out,
+                                    int B, int H, int W, int C, int f, int accumulate, int dt,
                                     void* stream) {
   if (H % f || W % f) return ACC_EBADSHAPE;
   long total = (long)B * (H / f) * (W / f) * C;
   hipStream_t s = (hipStream_t)stream;
   dim3 grid(grid_for(total));
-  if (f == 2)
-    hipLaunchKernelGGL(blocksum_kernel<2>, grid, dim3(256), 0, s, in, ld_in, in_off, out, ld_out, B,
-                       H, W, C, f, accumulate);
-  else if (f == 4)
-    hipLaunchKernelGGL(blocksum_kernel<4>, grid, dim3(256), 0, s, in, ld_in, in_off, out, ld_out, B,
-                       H, W, C, f, accumulate);
-  else if (f == 8)
-    hipLaunchKernelGGL(blocksum_kernel<8>, grid, dim3(256), 0, s, in, ld_in, in_off, out, ld_out, B,
-                       H, W, C, f, accumulate);
-  else
-    hipLaunchKernelGGL(blocksum_kernel<0>, grid, dim3(256), 0, s, in, ld_in, in_off, out, ld_out, B,
-                       H, W, C, f, accumulate);
+  if (with_dt(dt, [&](auto tag) {
+        using T = decltype(tag);
+        const T* i = (const T*)in;
+        T* o = (T*)out;
+        if (f == 2)
+          hipLaunchKernelGGL((blocksum_kernel<2, T>), grid, dim3(256), 0, s, i, ld_in, in_off, o,
+                             ld_out, B, H, W, C, f, accumulate);
+        else if (f == 4)
+          hipLaunchKernelGGL((blocksum_kernel<4, T>), grid, dim3(256), 0, s, i, ld_in, in_off, o,
+                             ld_out, B, H, W, C, f, accumulate);
+        else if (f == 8)
+          hipLaunchKernelGGL((blocksum_kernel<8, T>), grid, dim3(256), 0, s, i, ld_in, in_off, o,
+                             ld_out, B, H, W, C, f, accumulate);
+        else
+          hipLaunchKernelGGL((blocksum_kernel<0, T>), grid, dim3(256), 0, s, i, ld_in, in_off, o,
+                             ld_out, B, H, W, C, f, accumulate);
+      }))
+    return ACC_EBADARG;
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 
 // ---------------------------------------------------------------------------
 // Strided channel-slice copy: dst[p, dst_off + c] (+)= src[p, src_off + c], c < C
 // ---------------------------------------------------------------------------
+template <typename T>
 __global__ void __launch_bounds__(256)
-slice_copy_kernel(const float* __restrict__ src, int ld_src, int src_off, float* __restrict__ dst,
+slice_copy_kernel(const T* __restrict__ src, int ld_src, int src_off, T* __restrict__ dst,
                   int ld_dst, int dst_off, long P, int C, int accumulate) {
   long total = P * C;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
        i += (long)gridDim.x * blockDim.x) {
     long p = i / C;
     int c = (int)(i - p * C);
-    float v = src[p * ld_src + src_off + c];
-    float* d = dst + p * ld_dst + dst_off + c;
-    *d = accumulate ? *d + v : v;
+    T* d = dst + p * ld_dst + dst_off + c;
+    if (accumulate) st1(d, ld1(d) + ld1(src + p * ld_src + src_off + c));
+    else *d = src[p * ld_src + src_off + c];  // exact copy in the storage type
   }
 }
 
-extern "C" int accunet_slice_copy(const float* src, int ld_src, int src_off, float* dst,
-                                  int ld_dst, int dst_off, long P, int C, int accumulate,
+extern "C" int accunet_slice_copy(const void* src, int ld_src, int src_off, void* dst,
+                                  int ld_dst, int dst_off, long P, int C, int accumulate, int dt,
                                   void* stream) {
-  hipLaunchKernelGGL(slice_copy_kernel, dim3(grid_for(P * C)), dim3(256), 0, (hipStream_t)stream,
-                     src, ld_src, src_off, dst, ld_dst, dst_off, P, C, accumulate);
+  if (with_dt(dt, [&](auto tag) {
+        using T = decltype(tag);
+        hipLaunchKernelGGL((slice_copy_kernel<T>), dim3(grid_for(P * C)), dim3(256), 0,
+                           (hipStream_t)stream, (const T*)src, ld_src, src_off, (T*)dst, ld_dst,
+                           dst_off, P, C, accumulate);
+      }))
+    return ACC_EBADARG;
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 
@@ -408,9 +447,10 @@ extern "C" int accunet_slice_copy(const float* src, int ld_src, int src_off, flo
 // ConvTranspose2d(k=2,s=2) pixel shuffle. GEMM output T[b,i,j,(d*Cout+co)],
 // d = di*2+dj  ->  Y[b,2i+di,2j+dj,co] (+bias). Inverse for the backward.
 // ---------------------------------------------------------------------------
+template <typename T>
 __global__ void __launch_bounds__(256)
-pixel_shuffle2_kernel(const float* __restrict__ t, const float* __restrict__ bias,
-                      float* __restrict__ y, int B, int Hi, int Wi, int Cout, int inverse) {
+pixel_shuffle2_kernel(const T* __restrict__ t, const float* __restrict__ bias,
+                      T* __restrict__ y, int B, int Hi, int Wi, int Cout, int inverse) {
   const int Ho = 2 * Hi, Wo = 2 * Wi;
   long total = (long)B * Ho * Wo * Cout;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
@@ -424,19 +464,23 @@ pixel_shuffle2_kernel(const float* __restrict__ t, const float* __restrict__ bia
     int d = (ho & 1) * 2 + (wo & 1);
     long ti = (((long)b * Hi + (ho >> 1)) * Wi + (wo >> 1)) * (4 * Cout) + d * Cout + co;
     if (!inverse) {
-      y[i] = t[ti] + (bias ? bias[co] : 0.f);
+      st1(y + i, ld1(t + ti) + (bias ? bias[co] : 0.f));
     } else {
       // here y is the gradient dY (input), t is dT (output)
-      const_cast<float*>(t)[ti] = y[i];
+      const_cast<T*>(t)[ti] = y[i];
     }
   }
 }
 
-extern "C" int accunet_pixel_shuffle2(const float* t, const float* bias, float* y, int B, int Hi,
-                                      int Wi, int Cout, int inverse, void* stream) {
+extern "C" int accunet_pixel_shuffle2(const void* t, const float* bias, void* y, int B, int Hi,
+                                      int Wi, int Cout, int inverse, int dt, void* stream) {
   long total = (long)B * 4 * Hi * Wi * Cout;
-  hipLaunchKernelGGL(pixel_shuffle2_kernel, dim3(grid_for(total)), dim3(256), 0,
-                     (hipStream_t)stream, t, bias, y, B, Hi, Wi, Cout, inverse);
+  if (with_dt(dt, [&](auto tag) {
+        using T = decltype(tag);
+        hipLaunchKernelGGL((pixel_shuffle2_kernel<T>), dim3(grid_for(total)), dim3(256), 0,
+                           (hipStream_t)stream, (const T*)t, bias, (T*)y, B, Hi, Wi, Cout, inverse);
+      }))
+    return ACC_EBADARG;
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 
@@ -451,8 +495,9 @@ struct Perm4 {
   int flip[4];
 };
 
+template <typename TI, typename TO>
 __global__ void __launch_bounds__(256)
-permute4_kernel(const float* __restrict__ in, float* __restrict__ out, Perm4 p, int accumulate) {
+permute4_kernel(const TI* __restrict__ in, TO* __restrict__ out, Perm4 p, int accumulate) {
   long total = (long)p.d[0] * p.d[1] * p.d[2] * p.d[3];
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
        i += (long)gridDim.x * blockDim.x) {
@@ -464,12 +509,13 @@ permute4_kernel(const float* __restrict__ in, float* __restrict__ out, Perm4 p, 
       if (p.flip[a]) ia = p.d[a] - 1 - ia;
       off += ia * p.s[a];
     }
-    out[i] = accumulate ? out[i] + in[off] : in[off];
+    st1(out + i, accumulate ? ld1(out + i) + ld1(in + off) : ld1(in + off));
   }
 }
 
-extern "C" int accunet_permute4(const float* in, float* out, const int* dims, const long long* strides,
-                                const int* flips, int accumulate, void* stream) {
+extern "C" int accunet_permute4(const void* in, void* out, const int* dims, const long long* strides,
+                                const int* flips, int accumulate, int in_dt, int out_dt,
+                                void* stream) {
   Perm4 p;
   for (int a = 0; a < 4; ++a) {
     p.d[a] = dims[a];
@@ -477,8 +523,16 @@ extern "C" int accunet_permute4(const float* in, float* out, const int* dims, co
     p.flip[a] = flips ? flips[a] : 0;
   }
   long total = (long)p.d[0] * p.d[1] * p.d[2] * p.d[3];
-  hipLaunchKernelGGL(permute4_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, in,
-                     out, p, accumulate);
+  if (with_dt(in_dt, [&](auto ti) {
+        using TI = decltype(ti);
+        if (with_dt(out_dt, [&](auto to) {
+              using TO = decltype(to);
+              hipLaunchKernelGGL((permute4_kernel<TI, TO>), dim3(grid_for(total)), dim3(256), 0,
+                                 (hipStream_t)stream, (const TI*)in, (TO*)out, p, accumulate);
+            }))
+          in_dt = -1;
+      }) || in_dt < 0)
+    return ACC_EBADARG;
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 

@@ -73,9 +73,9 @@ static SeGeom se_geom(int B, int HW, int C) {
 }
 
 // pass 1 forward: partials part[(b*NCH + chunk)][2][C] of (sum a, sum a^2)
-template <int V>
+template <int V, typename T>
 __global__ void __launch_bounds__(256)
-se_reduce_kernel(const float* __restrict__ z, const float* __restrict__ sc,
+se_reduce_kernel(const T* __restrict__ z, const float* __restrict__ sc,
                  const float* __restrict__ sh, int act, SeGeom g, double* __restrict__ part) {
   ChanTile t = chan_tile<V>(g.C);
   const int b = blockIdx.x / g.NCH, ch = blockIdx.x % g.NCH;
@@ -241,11 +241,11 @@ se_mid_bn_kernel(SeGeom g, int Cr, const float* __restrict__ gamma,
 }
 
 // pass 2 forward: out = lrelu(alpha[b,c]*a + betap[c])
-template <int V>
+template <int V, typename T>
 __global__ void __launch_bounds__(256)
-se_apply_kernel(const float* __restrict__ z, const float* __restrict__ sc,
+se_apply_kernel(const T* __restrict__ z, const float* __restrict__ sc,
                 const float* __restrict__ sh, int act, SeGeom g, const float* __restrict__ alpha,
-                const float* __restrict__ betap, float* __restrict__ out,
+                const float* __restrict__ betap, T* __restrict__ out,
                 double* __restrict__ ostats) {
   ChanTile t = chan_tile<V>(g.C);
   const int b = blockIdx.x / g.NCH, ch = blockIdx.x % g.NCH;
@@ -270,7 +270,7 @@ se_apply_kernel(const float* __restrict__ z, const float* __restrict__ sc,
 #pragma unroll
       for (int j = 0; j < V; ++j) {
         float x = pro ? apply_act(v[j] * s[j] + h[j], act) : v[j];
-        v[j] = lrelu(al[j] * x + be[j]);
+        v[j] = rnd<T>(lrelu(al[j] * x + be[j]));  // statistics of the stored value
         o1[j] += v[j];
         o2[j] += (double)v[j] * v[j];
       }
@@ -282,9 +282,9 @@ se_apply_kernel(const float* __restrict__ z, const float* __restrict__ sc,
 }
 
 // backward pass 1: partials of (T1 = sum g2, T2 = sum g2*a) per (b,c)
-template <int V>
+template <int V, typename T>
 __global__ void __launch_bounds__(256)
-se_bwd_reduce_kernel(const float* __restrict__ z, const float* __restrict__ dout,
+se_bwd_reduce_kernel(const T* __restrict__ z, const T* __restrict__ dout,
                      const float* __restrict__ sc, const float* __restrict__ sh, int act,
                      SeGeom g, const float* __restrict__ alpha, const float* __restrict__ betap,
                      double* __restrict__ part) {
@@ -473,13 +473,13 @@ se_bwd_param_kernel(SeGeom g, int Cr, float* __restrict__ save, const double* __
   }
 }
 
-template <int V>
+template <int V, typename T>
 __global__ void __launch_bounds__(256)
-se_bwd_apply_kernel(const float* __restrict__ z, const float* __restrict__ dout,
+se_bwd_apply_kernel(const T* __restrict__ z, const T* __restrict__ dout,
                     const float* __restrict__ sc, const float* __restrict__ sh, int act, SeGeom g,
                     const float* __restrict__ alpha, const float* __restrict__ betap,
                     const float* __restrict__ sgate, const float* __restrict__ mean,
-                    const float* __restrict__ coef, float* __restrict__ da) {
+                    const float* __restrict__ coef, T* __restrict__ da) {
   ChanTile t = chan_tile<V>(g.C);
   if (!t.active) return;
   const int b = blockIdx.x / g.NCH, ch = blockIdx.x % g.NCH;
@@ -532,9 +532,9 @@ se_bwd_apply_kernel(const float* __restrict__ z, const float* __restrict__ dout,
 // ---------------------------------------------------------------------------
 #define SE_PRO_NQ 8  // T1, T2, U1, U2, U3, W1, W2, W3
 
-template <int V>
+template <int V, typename T>
 __global__ void __launch_bounds__(256)
-se_bwd_reduce_pro_kernel(const float* __restrict__ z, const float* __restrict__ dout,
+se_bwd_reduce_pro_kernel(const T* __restrict__ z, const T* __restrict__ dout,
                          const float* __restrict__ pst, int act, SeGeom g,
                          const float* __restrict__ alpha, const float* __restrict__ betap,
                          double* __restrict__ part) {
@@ -635,14 +635,14 @@ se_pro_coef_kernel(SeGeom g, int Cr, const float* __restrict__ save,
   pcoef[2 * C + c] = k3;
 }
 
-template <int V>
+template <int V, typename T>
 __global__ void __launch_bounds__(256)
-se_bwd_apply_pro_kernel(const float* __restrict__ z, const float* __restrict__ dout,
+se_bwd_apply_pro_kernel(const T* __restrict__ z, const T* __restrict__ dout,
                         const float* __restrict__ pst, int act, SeGeom g,
                         const float* __restrict__ alpha, const float* __restrict__ betap,
                         const float* __restrict__ sgate, const float* __restrict__ mean,
                         const float* __restrict__ coef, const float* __restrict__ pcoef,
-                        float* __restrict__ dz, double* __restrict__ colsum) {
+                        T* __restrict__ dz, double* __restrict__ colsum) {
   ChanTile t = chan_tile<V>(g.C);
   // optional fp64 column sums of dz (the bias gradient of z's producer convolution)
   double cs[V], cz[V];
@@ -698,7 +698,7 @@ se_bwd_apply_pro_kernel(const float* __restrict__ z, const float* __restrict__ d
           const float g2 = d[u][j] * lrelu_d(al[j] * x + be[j]);
           float da = A[j] * g2 + Bc[j] * (x * sgv[j] - mu[j]) + Cc[j];
           if (act == ACT_LRELU) da *= lrelu_d(pre);
-          d[u][j] = k1[j] * da + k2[j] * (v[u][j] - mu1[j]) + k3[j];
+          d[u][j] = rnd<T>(k1[j] * da + k2[j] * (v[u][j] - mu1[j]) + k3[j]);
           if (colsum) cs[j] += d[u][j];
         }
         stv<V>(dz + r * C + t.c0, d[u]);
@@ -740,23 +740,29 @@ extern "C" size_t accunet_se_ws_elems(int B, int HW, int C, int Cr) {
          se_dsum_scr_floats(g);
 }
 
-extern "C" int accunet_se_fwd(const float* z, const float* sc, const float* sh, int act, int B,
+extern "C" int accunet_se_fwd(const void* z, const float* sc, const float* sh, int act, int B,
                               int HW, int C, int Cr, const float* w1, const float* b1,
                               const float* w2, const float* b2, const float* gamma,
                               const float* beta, float* rmean, float* rvar, long long* nbt,
-                              float momentum, float eps, int training, float* out, float* save,
-                              double* ostats, float* ws, size_t ws_elems, void* stream) {
+                              float momentum, float eps, int training, void* out, float* save,
+                              double* ostats, float* ws, size_t ws_elems, int dt, void* stream) {
   hipStream_t s = (hipStream_t)stream;
+  if (dt != ACC_F32 && dt != ACC_BF16) return ACC_EBADARG;
   if (ws_elems < accunet_se_ws_elems(B, HW, C, Cr)) return ACC_EBADARG;
   if (((uintptr_t)ws & 7) || ((uintptr_t)save & 7)) return ACC_EBADARG;
   SeGeom g = se_geom(B, HW, C);
   int V = (C % 4 == 0) ? 4 : 1;
   dim3 grid(B * g.NCH, ceil_div(C / V, 64));
   double* part = reinterpret_cast<double*>(ws);
-  if (V == 4)
-    hipLaunchKernelGGL(se_reduce_kernel<4>, grid, dim3(256), 0, s, z, sc, sh, act, g, part);
-  else
-    hipLaunchKernelGGL(se_reduce_kernel<1>, grid, dim3(256), 0, s, z, sc, sh, act, g, part);
+  with_dt(dt, [&](auto tag) {
+    using T = decltype(tag);
+    if (V == 4)
+      hipLaunchKernelGGL((se_reduce_kernel<4, T>), grid, dim3(256), 0, s, (const T*)z, sc, sh, act,
+                         g, part);
+    else
+      hipLaunchKernelGGL((se_reduce_kernel<1, T>), grid, dim3(256), 0, s, (const T*)z, sc, sh, act,
+                         g, part);
+  });
   // S, Q and the gate per sample, then the BN-of-gated statistics per channel
   hipLaunchKernelGGL(se_mid_sample_kernel, dim3(B), dim3(256), (C + Cr) * sizeof(float), s, part,
                      g, Cr, w1, b1, w2, b2, save);
@@ -764,12 +770,15 @@ extern "C" int accunet_se_fwd(const float* z, const float* sc, const float* sh, 
                      rmean, rvar, momentum, eps, training, save, training ? nbt : nullptr);
   const float* alpha = save + se_alpha_offset(B, C, Cr);
   const float* betap = alpha + (size_t)B * C;
-  if (V == 4)
-    hipLaunchKernelGGL(se_apply_kernel<4>, grid, dim3(256), 0, s, z, sc, sh, act, g, alpha, betap,
-                       out, ostats);
-  else
-    hipLaunchKernelGGL(se_apply_kernel<1>, grid, dim3(256), 0, s, z, sc, sh, act, g, alpha, betap,
-                       out, ostats);
+  with_dt(dt, [&](auto tag) {
+    using T = decltype(tag);
+    if (V == 4)
+      hipLaunchKernelGGL((se_apply_kernel<4, T>), grid, dim3(256), 0, s, (const T*)z, sc, sh, act, g,
+                         alpha, betap, (T*)out, ostats);
+    else
+      hipLaunchKernelGGL((se_apply_kernel<1, T>), grid, dim3(256), 0, s, (const T*)z, sc, sh, act, g,
+                         alpha, betap, (T*)out, ostats);
+  });
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 
@@ -797,13 +806,14 @@ static void se_bwd_mid(const SeGeom& g, int Cr, const double* part, int nq, cons
                      scratch, dw1, db1, dw2, db2);
 }
 
-extern "C" int accunet_se_bwd(const float* z, const float* dout, const float* sc, const float* sh,
+extern "C" int accunet_se_bwd(const void* z, const void* dout, const float* sc, const float* sh,
                               int act, int B, int HW, int C, int Cr, const float* w1,
                               const float* w2, const float* gamma, int training,
-                              const float* save, float* da, float* dw1, float* db1, float* dw2,
+                              const float* save, void* da, float* dw1, float* db1, float* dw2,
                               float* db2, float* dgamma, float* dbeta, float* ws, size_t ws_elems,
-                              void* stream) {
+                              int dt, void* stream) {
   hipStream_t s = (hipStream_t)stream;
+  if (dt != ACC_F32 && dt != ACC_BF16) return ACC_EBADARG;
   if (ws_elems < accunet_se_ws_elems(B, HW, C, Cr)) return ACC_EBADARG;
   if (((uintptr_t)ws & 7) || ((uintptr_t)save & 7)) return ACC_EBADARG;
   SeGeom g = se_geom(B, HW, C);
@@ -816,33 +826,40 @@ extern "C" int accunet_se_bwd(const float* z, const float* dout, const float* sc
   const float* betap = alpha + (size_t)B * C;
   const float* sgate = save + (size_t)B * C * 4 + (size_t)B * Cr;
   const float* mean = sgate + (size_t)B * C;
-  if (V == 4)
-    hipLaunchKernelGGL(se_bwd_reduce_kernel<4>, grid, dim3(256), 0, s, z, dout, sc, sh, act, g,
-                       alpha, betap, part);
-  else
-    hipLaunchKernelGGL(se_bwd_reduce_kernel<1>, grid, dim3(256), 0, s, z, dout, sc, sh, act, g,
-                       alpha, betap, part);
+  with_dt(dt, [&](auto tag) {
+    using T = decltype(tag);
+    if (V == 4)
+      hipLaunchKernelGGL((se_bwd_reduce_kernel<4, T>), grid, dim3(256), 0, s, (const T*)z,
+                         (const T*)dout, sc, sh, act, g, alpha, betap, part);
+    else
+      hipLaunchKernelGGL((se_bwd_reduce_kernel<1, T>), grid, dim3(256), 0, s, (const T*)z,
+                         (const T*)dout, sc, sh, act, g, alpha, betap, part);
+  });
   float* sv = const_cast<float*>(save);
   se_bwd_mid(g, Cr, part, 2, w1, w2, gamma, training, sv, scratch, coef, dw1, db1, dw2, db2,
              dgamma, dbeta, s);
-  if (V == 4)
-    hipLaunchKernelGGL(se_bwd_apply_kernel<4>, grid, dim3(256), 0, s, z, dout, sc, sh, act, g,
-                       alpha, betap, sgate, mean, coef, da);
-  else
-    hipLaunchKernelGGL(se_bwd_apply_kernel<1>, grid, dim3(256), 0, s, z, dout, sc, sh, act, g,
-                       alpha, betap, sgate, mean, coef, da);
+  with_dt(dt, [&](auto tag) {
+    using T = decltype(tag);
+    if (V == 4)
+      hipLaunchKernelGGL((se_bwd_apply_kernel<4, T>), grid, dim3(256), 0, s, (const T*)z,
+                         (const T*)dout, sc, sh, act, g, alpha, betap, sgate, mean, coef, (T*)da);
+    else
+      hipLaunchKernelGGL((se_bwd_apply_kernel<1, T>), grid, dim3(256), 0, s, (const T*)z,
+                         (const T*)dout, sc, sh, act, g, alpha, betap, sgate, mean, coef, (T*)da);
+  });
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 
-extern "C" int accunet_se_bwd_pro(const float* z, const float* dout, const float* pst, int act,
+extern "C" int accunet_se_bwd_pro(const void* z, const void* dout, const float* pst, int act,
                                   const float* pgamma, int ptraining, int B, int HW, int C,
                                   int Cr, const float* w1, const float* w2, const float* gamma,
-                                  int training, const float* save, float* dz, float* dpgamma,
+                                  int training, const float* save, void* dz, float* dpgamma,
                                   float* dpbeta, float* dsum, float* dw1, float* db1, float* dw2,
                                   float* db2,
-                                  float* dgamma, float* dbeta, float* ws, size_t ws_elems,
+                                  float* dgamma, float* dbeta, float* ws, size_t ws_elems, int dt,
                                   void* stream) {
   hipStream_t s = (hipStream_t)stream;
+  if (dt != ACC_F32 && dt != ACC_BF16) return ACC_EBADARG;
   if (ws_elems < accunet_se_ws_elems(B, HW, C, Cr)) return ACC_EBADARG;
   if (((uintptr_t)ws & 7) || ((uintptr_t)save & 7)) return ACC_EBADARG;
   if (!pst || !dz) return ACC_EBADARG;
@@ -859,12 +876,15 @@ extern "C" int accunet_se_bwd_pro(const float* z, const float* dout, const float
   const float* betap = alpha + (size_t)B * C;
   const float* sgate = save + (size_t)B * C * 4 + (size_t)B * Cr;
   const float* mean = sgate + (size_t)B * C;
-  if (V == 4)
-    hipLaunchKernelGGL(se_bwd_reduce_pro_kernel<4>, grid, dim3(256), 0, s, z, dout, pst, act, g,
-                       alpha, betap, part);
-  else
-    hipLaunchKernelGGL(se_bwd_reduce_pro_kernel<1>, grid, dim3(256), 0, s, z, dout, pst, act, g,
-                       alpha, betap, part);
+  with_dt(dt, [&](auto tag) {
+    using T = decltype(tag);
+    if (V == 4)
+      hipLaunchKernelGGL((se_bwd_reduce_pro_kernel<4, T>), grid, dim3(256), 0, s, (const T*)z,
+                         (const T*)dout, pst, act, g, alpha, betap, part);
+    else
+      hipLaunchKernelGGL((se_bwd_reduce_pro_kernel<1, T>), grid, dim3(256), 0, s, (const T*)z,
+                         (const T*)dout, pst, act, g, alpha, betap, part);
+  });
   float* sv = const_cast<float*>(save);
   se_bwd_mid(g, Cr, part, SE_PRO_NQ, w1, w2, gamma, training, sv, scratch, coef, dw1, db1, dw2,
              db2, dgamma, dbeta, s);
@@ -874,12 +894,17 @@ extern "C" int accunet_se_bwd_pro(const float* z, const float* dout, const float
                      coef, pst, pgamma, ptraining, dpgamma, dpbeta, pcoef);
   // the reduce-pass partials are consumed by the mid kernels: reuse them for dz's column sums
   double* cpart = dsum ? part : nullptr;
-  if (V == 4)
-    hipLaunchKernelGGL(se_bwd_apply_pro_kernel<4>, grid, dim3(256), 0, s, z, dout, pst, act, g,
-                       alpha, betap, sgate, mean, coef, pcoef, dz, cpart);
-  else
-    hipLaunchKernelGGL(se_bwd_apply_pro_kernel<1>, grid, dim3(256), 0, s, z, dout, pst, act, g,
-                       alpha, betap, sgate, mean, coef, pcoef, dz, cpart);
+  with_dt(dt, [&](auto tag) {
+    using T = decltype(tag);
+    if (V == 4)
+      hipLaunchKernelGGL((se_bwd_apply_pro_kernel<4, T>), grid, dim3(256), 0, s, (const T*)z,
+                         (const T*)dout, pst, act, g, alpha, betap, sgate, mean, coef, pcoef, (T*)dz,
+                         cpart);
+    else
+      hipLaunchKernelGGL((se_bwd_apply_pro_kernel<1, T>), grid, dim3(256), 0, s, (const T*)z,
+                         (const T*)dout, pst, act, g, alpha, betap, sgate, mean, coef, pcoef, (T*)dz,
+                         cpart);
+  });
   if (dsum) {
     int rows;
     const double* pr = reduce_partials_d(cpart, B * g.NCH, 2 * C, dscr, &rows, s);

@@ -26,7 +26,7 @@ extern "C" {
 #endif
 
 /* ------------------------------------------------------------------------- *
- * GEMM engine (fp32 MFMA 32x32x2).  Replaces every nn.Conv2d 1x1 / 3x3 forward
+ * GEMM engines (fp32 MFMA 32x32x2 / bf16 MFMA 32x32x16).  Replaces every nn.Conv2d 1x1 / 3x3 forward
  * and their autograd data/weight gradients:
  *   HANCBlock.conv1/conv3  ACC_UNet/ACC_UNet.py:233,259
  *   HANCLayer.cnv          ACC_UNet/ACC_UNet.py:72,140 (restructured)
@@ -35,6 +35,12 @@ extern "C" {
  *   ConvTranspose2d up6..9 ACC_UNet/ACC_UNet.py:578-590 (pixel-shuffled GEMM)
  * C[m,n] = sum_k A(m,k) B(k,n) (+bias[n]) (+ sum_u up_u[pixel(m)>>uplog_u][n])
  * ------------------------------------------------------------------------- */
+/* Activation storage types (`dt` arguments, AccGemmDesc.adt/bdt/cdt): the
+ * activation-shaped tensors of a call (inputs, outputs, activation gradients,
+ * pyramid / upsample operands) are fp32 or bf16; parameters, parameter gradients,
+ * BatchNorm / SE state are always fp32 and partial statistics fp64. */
+enum { ACC_F32 = 0, ACC_BF16 = 1 };
+
 enum { AMODE_ROW = 0, AMODE_COL = 1, AMODE_SHIFT3 = 2 };
 enum { BMODE_NT = 0, BMODE_NN = 1, BMODE_NN_SHIFT3 = 2 };
 enum { PRO_NONE = 0, PRO_AFFINE = 1, PRO_AFFINE_LRELU = 2 };
@@ -44,21 +50,21 @@ typedef struct AccGemmDesc {
   int M, N, K;
   int amode, bmode, pro_a, pro_b;
   int nsrc;                 /* AMODE_ROW: up to 4 channel-concatenated A sources */
-  const float* a[4];
+  const void* a[4];         /* storage adt */
   int lda[4];
   int kbeg[5];              /* source s covers k in [kbeg[s], kbeg[s+1]) */
   const float* a_scale;     /* prologue act(x*scale[k]+shift[k]) on A (AMODE_ROW) */
   const float* a_shift;
-  const float* b;
+  const void* b;            /* storage bdt */
   int ldb;
   const float* b_scale;     /* prologue on B's n axis (BMODE_NN) */
   const float* b_shift;
   int H, W, cin;            /* pixel grid (SHIFT3 modes, up-adds); channels per tap */
-  float* c;
+  void* c;                  /* storage cdt (also up[], pd2/pd4, bz) */
   int ldc;
   const float* bias;        /* [N] or NULL */
   int nup;                  /* 0..3 nearest-upsampled addends */
-  const float* up[3];
+  const void* up[3];
   int upld[3];
   int uplog[3];
   double* stats;            /* [rows][2][N] fp64 partial (sum,sumsq) of C, or NULL */
@@ -69,8 +75,8 @@ typedef struct AccGemmDesc {
    * with dP2 = pd2 [P/4][2N] ([avg | max] columns), dP4 = pd4 [P/16][2N] (or NULL),
    * mk2 [P/4][N], mk4 [P/16][N] the first-max codes written by
    * accunet_hanc_pyramid_fwd. pd2 == NULL disables it. */
-  const float* pd2;
-  const float* pd4;
+  const void* pd2;
+  const void* pd4;
   const unsigned char* mk2;
   const unsigned char* mk4;
   /* BatchNorm backward statistics in the epilogue (data gradients whose input went
@@ -78,9 +84,14 @@ typedef struct AccGemmDesc {
    * pre-BN input z [M][ldc] and bst its [4][N] state block, `stats` receives per-row-
    * block (sum g, sum g*(z - mean)) of g = C * act'(z*scale + shift) instead of
    * (sum C, sum C^2); accunet_bn_bwd_part finishes the BatchNorm backward. */
-  const float* bz;
+  const void* bz;
   const float* bst;
   int bact;
+  /* storage of A, B and C (ACC_F32 / ACC_BF16). All fp32: fp32 engine (fp32 MFMA).
+   * adt = ACC_BF16: bf16 engine (v_mfma_f32_32x32x16_bf16) with either bdt = ACC_F32
+   * (weights, rounded to bf16 on load) and cdt = ACC_BF16 (forward / data gradients),
+   * or bdt = ACC_BF16 and cdt = ACC_F32 (amode = AMODE_COL weight gradients). */
+  int adt, bdt, cdt;
 } AccGemmDesc;
 
 int accunet_gemm(const AccGemmDesc* d, float* ws, size_t ws_elems, void* stream);
@@ -102,26 +113,26 @@ int accunet_bn_finalize(const double* part, int R, int C, double count, const fl
                         const float* beta, float* rmean, float* rvar, long long* nbt,
                         float momentum, float eps, int training, float* st, double* ws,
                         void* stream);
-int accunet_affine_act_fwd(const float* x, const float* sc, const float* sh, int act,
-                           const float* res, float* y, long P, int C, double* stats,
-                           int* stats_rows, void* stream);
+int accunet_affine_act_fwd(const void* x, const float* sc, const float* sh, int act,
+                           const void* res, void* y, long P, int C, double* stats,
+                           int* stats_rows, int dt, void* stream);
 size_t accunet_bn_bwd_ws_elems(long P, int C);
 /* dsum (optional, [C]) receives sum_p dx: the bias gradient of the convolution whose
  * output x feeds only this BatchNorm, without a separate pass over dx. */
-int accunet_bn_bwd(const float* x, const float* dy, const float* st, const float* gamma, int act,
-                   int training, long P, int C, float* dx, int accumulate, float* dgamma,
-                   float* dbeta, float* dsum, float* ws, size_t ws_elems, void* stream);
+int accunet_bn_bwd(const void* x, const void* dy, const float* st, const float* gamma, int act,
+                   int training, long P, int C, void* dx, int accumulate, float* dgamma,
+                   float* dbeta, float* dsum, float* ws, size_t ws_elems, int dt, void* stream);
 /* BatchNorm backward from producer-side partials: part = [R][2][C] (sum g,
  * sum g*(x - mean)) written by a data-gradient epilogue (AccGemmDesc.bz,
  * accunet_dw3x3_fwd bz) -> dgamma, dbeta, dx = k1*g + k2*(x - mean) + k3 in one
  * streaming pass (the reduce pass of accunet_bn_bwd is skipped). */
 size_t accunet_bn_bwd_part_ws_elems(long P, int R, int C);
-int accunet_bn_bwd_part(const float* x, const float* dy, const float* st, const float* gamma,
+int accunet_bn_bwd_part(const void* x, const void* dy, const float* st, const float* gamma,
                         int act, int training, long P, int C, const double* part, int R,
-                        float* dx, float* dgamma, float* dbeta, float* dsum, float* ws,
-                        size_t ws_elems, void* stream);
-int accunet_colsum(const float* x, long P, int C, float* out, double* ws, size_t ws_elems,
-                   void* stream);
+                        void* dx, float* dgamma, float* dbeta, float* dsum, float* ws,
+                        size_t ws_elems, int dt, void* stream);
+int accunet_colsum(const void* x, long P, int C, float* out, double* ws, size_t ws_elems,
+                   int dt, void* stream);
 int accunet_reduce_stats(const double* part, int R, int C, double* out2C, double* ws,
                          void* stream);
 
@@ -135,13 +146,14 @@ int accunet_reduce_stats(const double* part, int R, int C, double* out2C, double
  * g = out * act'(bz*scale + shift), for accunet_bn_bwd_part. wgrad writes dW [C][1][3][3] and db [C].
  * ------------------------------------------------------------------------- */
 int accunet_dw3x3_rows(int B, int H, int W, int C);
-int accunet_dw3x3_fwd(const float* x, const float* wt, const float* bias, const float* sc,
-                      const float* sh, int act, int flip, float* z, double* stats, int B, int H,
-                      int W, int C, const float* bz, const float* bst, int bact, void* stream);
+int accunet_dw3x3_fwd(const void* x, const float* wt, const float* bias, const float* sc,
+                      const float* sh, int act, int flip, void* z, double* stats, int B, int H,
+                      int W, int C, const void* bz, const float* bst, int bact, int dt,
+                      void* stream);
 size_t accunet_dw3x3_wgrad_ws(int B, int H, int W, int C);
-int accunet_dw3x3_wgrad(const float* x, const float* dz, const float* sc, const float* sh,
+int accunet_dw3x3_wgrad(const void* x, const void* dz, const float* sc, const float* sh,
                         int act, float* dw, float* db, int B, int H, int W, int C, float* ws,
-                        size_t ws_elems, void* stream);
+                        size_t ws_elems, int dt, void* stream);
 
 /* ------------------------------------------------------------------------- *
  * HANCLayer neighbourhood pyramid (ACC_UNet/ACC_UNet.py:86-106): from
@@ -151,12 +163,12 @@ int accunet_dw3x3_wgrad(const float* x, const float* dz, const float* sc, const 
  * x-branch data-gradient GEMM uses to route the max-pool gradient (AccGemmDesc.pd2).
  * Backward (standalone form) accumulates into da (max: first max in window).
  * ------------------------------------------------------------------------- */
-int accunet_hanc_pyramid_fwd(const float* x, const float* sc, const float* sh, int act, int B,
-                             int H, int W, int C, int k, float* p2, float* p4,
-                             unsigned char* mk2, unsigned char* mk4, void* stream);
-int accunet_hanc_pyramid_bwd(const float* x, const float* sc, const float* sh, int act, int B,
-                             int H, int W, int C, int k, const float* p2, const float* p4,
-                             const float* dp2, const float* dp4, float* da, void* stream);
+int accunet_hanc_pyramid_fwd(const void* x, const float* sc, const float* sh, int act, int B,
+                             int H, int W, int C, int k, void* p2, void* p4,
+                             unsigned char* mk2, unsigned char* mk4, int dt, void* stream);
+int accunet_hanc_pyramid_bwd(const void* x, const float* sc, const float* sh, int act, int B,
+                             int H, int W, int C, int k, const void* p2, const void* p4,
+                             const void* dp2, const void* dp4, void* da, int dt, void* stream);
 /* HANCLayer / MLFC-merge channel interleave (ACC_UNet.py:138, :492):
  * out[n][jj][c] = W[n][c*J + order[jj]]  (inverse scatters back) */
 int accunet_group_relayout(const float* in, float* out, int N, int C, int J, const int* order,
@@ -169,18 +181,19 @@ int accunet_group_relayout(const float* in, float* out, int N, int C, int J, con
  * generic 4-D permute (weights, NCHW<->NHWC at the module boundary).
  * mode: 0 = max, 1 = avg.
  * ------------------------------------------------------------------------- */
-int accunet_pool2_fwd(const float* x, float* y, int B, int H, int W, int C, int mode,
+int accunet_pool2_fwd(const void* x, void* y, int B, int H, int W, int C, int mode, int dt,
                       void* stream);
-int accunet_pool2_bwd(const float* x, const float* y, const float* dy, float* dx, int B, int H,
-                      int W, int C, int mode, int accumulate, void* stream);
-int accunet_upsample_bwd(const float* in, int ld_in, int in_off, float* out, int ld_out, int B,
-                         int H, int W, int C, int f, int accumulate, void* stream);
-int accunet_slice_copy(const float* src, int ld_src, int src_off, float* dst, int ld_dst,
-                       int dst_off, long P, int C, int accumulate, void* stream);
-int accunet_pixel_shuffle2(const float* t, const float* bias, float* y, int B, int Hi, int Wi,
-                           int Cout, int inverse, void* stream);
-int accunet_permute4(const float* in, float* out, const int* dims, const long long* strides,
-                     const int* flips, int accumulate, void* stream);
+int accunet_pool2_bwd(const void* x, const void* y, const void* dy, void* dx, int B, int H,
+                      int W, int C, int mode, int accumulate, int dt, void* stream);
+int accunet_upsample_bwd(const void* in, int ld_in, int in_off, void* out, int ld_out, int B,
+                         int H, int W, int C, int f, int accumulate, int dt, void* stream);
+int accunet_slice_copy(const void* src, int ld_src, int src_off, void* dst, int ld_dst,
+                       int dst_off, long P, int C, int accumulate, int dt, void* stream);
+int accunet_pixel_shuffle2(const void* t, const float* bias, void* y, int B, int Hi, int Wi,
+                           int Cout, int inverse, int dt, void* stream);
+/* in_dt / out_dt: storage of in / out (e.g. NCHW fp32 input -> NHWC bf16 activations) */
+int accunet_permute4(const void* in, void* out, const int* dims, const long long* strides,
+                     const int* flips, int accumulate, int in_dt, int out_dt, void* stream);
 
 /* ------------------------------------------------------------------------- *
  * ChannelSELayer (ACC_UNet/ACC_UNet.py:9-49) fused with the BatchNorm(+LReLU)
@@ -193,17 +206,17 @@ int accunet_permute4(const float* in, float* out, const int* dims, const long lo
 size_t accunet_se_save_elems(int B, int C, int Cr);
 size_t accunet_se_ws_elems(int B, int HW, int C, int Cr);
 int accunet_se_stats_rows(int B, int HW, int C);
-int accunet_se_fwd(const float* z, const float* sc, const float* sh, int act, int B, int HW,
+int accunet_se_fwd(const void* z, const float* sc, const float* sh, int act, int B, int HW,
                    int C, int Cr, const float* w1, const float* b1, const float* w2,
                    const float* b2, const float* gamma, const float* beta, float* rmean,
                    float* rvar, long long* nbt, float momentum, float eps, int training,
-                   float* out, float* save, double* ostats, float* ws, size_t ws_elems,
+                   void* out, float* save, double* ostats, float* ws, size_t ws_elems, int dt,
                    void* stream);
-int accunet_se_bwd(const float* z, const float* dout, const float* sc, const float* sh, int act,
+int accunet_se_bwd(const void* z, const void* dout, const float* sc, const float* sh, int act,
                    int B, int HW, int C, int Cr, const float* w1, const float* w2,
-                   const float* gamma, int training, const float* save, float* da, float* dw1,
+                   const float* gamma, int training, const float* save, void* da, float* dw1,
                    float* db1, float* dw2, float* db2, float* dgamma, float* dbeta, float* ws,
-                   size_t ws_elems, void* stream);
+                   size_t ws_elems, int dt, void* stream);
 /* accunet_se_bwd fused with the backward of the BatchNorm(+act) prologue that feeds
  * the SE (HANCBlock.norm3 :281-283, ResPath.bns :326, Conv2d_batchnorm.batchnorm
  * :183-185, MLFC.bns_mrg :520): pst = that BatchNorm's [4][C] (mean, rstd, scale,
@@ -211,23 +224,24 @@ int accunet_se_bwd(const float* z, const float* dout, const float* sc, const flo
  * the pre-BN input z) and the prologue's dgamma/dbeta directly: 2 read passes over
  * (z, dout) and one write, da is never materialised. dsum (optional) = sum_p dz, the
  * bias gradient of z's producer convolution. */
-int accunet_se_bwd_pro(const float* z, const float* dout, const float* pst, int act,
+int accunet_se_bwd_pro(const void* z, const void* dout, const float* pst, int act,
                        const float* pgamma, int ptraining, int B, int HW, int C, int Cr,
                        const float* w1, const float* w2, const float* gamma, int training,
-                       const float* save, float* dz, float* dpgamma, float* dpbeta, float* dsum,
+                       const float* save, void* dz, float* dpgamma, float* dpbeta, float* dsum,
                        float* dw1,
                        float* db1, float* dw2, float* db2, float* dgamma, float* dbeta, float* ws,
-                       size_t ws_elems, void* stream);
+                       size_t ws_elems, int dt, void* stream);
 
 /* ------------------------------------------------------------------------- *
- * Head: out 1x1 conv n_filts -> 1 (+ Sigmoid when sigm) (ACC_UNet.py:594-599,653-659)
+ * Head: out 1x1 conv n_filts -> 1 (+ Sigmoid when sigm) (ACC_UNet.py:594-599,653-659);
+ * x / dx are activations (dt), y / dy (the model output, fed to the loss) fp32
  * ------------------------------------------------------------------------- */
-int accunet_head_fwd(const float* x, const float* w, const float* b, int sigm, float* y, long P,
-                     int C, void* stream);
+int accunet_head_fwd(const void* x, const float* w, const float* b, int sigm, float* y, long P,
+                     int C, int dt, void* stream);
 size_t accunet_head_ws_elems(long P, int C);
-int accunet_head_bwd(const float* x, const float* w, const float* y, const float* dy, int sigm,
-                     float* dx, float* dw, float* db, long P, int C, float* ws, size_t ws_elems,
-                     void* stream);
+int accunet_head_bwd(const void* x, const float* w, const float* y, const float* dy, int sigm,
+                     void* dx, float* dw, float* db, long P, int C, float* ws, size_t ws_elems,
+                     int dt, void* stream);
 
 /* ------------------------------------------------------------------------- *
  * WeightedDiceBCE (Experiments/utils.py:140-171; WeightedBCE :21-74 with the
@@ -254,12 +268,12 @@ int accunet_adam_step(const void* table, const int* chunk_t, const long long* ch
 /* ------------------------------------------------------------------------- *
  * ACC_UNet_W learnable merge y = a*w + b*(1-w) (ACC_UNet/ACC_UNet_w.py:497-522)
  * ------------------------------------------------------------------------- */
-int accunet_wmerge_fwd(const float* a, const float* b, const float* w, float* y, long P, int C,
-                       double* stats, void* stream);
-int accunet_wmerge_bwd(const float* g, const float* w, float* da, float* db, long n,
+int accunet_wmerge_fwd(const void* a, const void* b, const float* w, void* y, long P, int C,
+                       double* stats, int dt, void* stream);
+int accunet_wmerge_bwd(const void* g, const float* w, void* da, void* db, long n, int dt,
                        void* stream);
-int accunet_dotdiff(const float* g, const float* a, const float* b, long n, float* out,
-                    int accumulate, float* ws, void* stream);
+int accunet_dotdiff(const void* g, const void* a, const void* b, long n, float* out,
+                    int accumulate, float* ws, int dt, void* stream);
 
 /* ------------------------------------------------------------------------- *
  * Input preparation (csrc/data.hip). Replaces the per-image host work of

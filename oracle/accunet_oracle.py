@@ -254,6 +254,57 @@ def lrelu(x):
     return F.leaky_relu(x, SLOPE)
 
 
+# --------------------------------------------------------------------------
+# Storage-rounding emulation (tests of the build's bf16 mode only; the reference
+# itself is fp32 throughout). With storage_rounding(torch.bfloat16) active, the
+# tensors the build keeps in HBM as bf16 are rounded to bf16 where it stores them,
+# and so are their gradients in backward: convolution outputs, GEMM operands (the
+# activated input of every dense / 1x1 / transposed convolution and its weights),
+# pooled tensors, SE outputs and the residual sums. The depthwise 3x3, the SE gate
+# and the head read bf16 activations but compute with fp32 weights and do not round
+# their activated inputs. Everything else (BatchNorm / SE statistics, the loss) is
+# computed in the oracle's dtype. This measures the error bf16 storage alone causes.
+# --------------------------------------------------------------------------
+_STORE = None
+
+
+class _RoundStore(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, dt):
+        ctx.dt = dt
+        return x.to(dt).to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(ctx.dt).to(g.dtype), None
+
+
+def q(x):
+    """x as stored by the build (identity unless storage_rounding is active)."""
+    return x if _STORE is None else _RoundStore.apply(x, _STORE)
+
+
+def qw(w):
+    """a GEMM weight operand as the bf16 engine reads it (fp32 master, bf16 operand)."""
+    return w if _STORE is None else _RoundStore.apply(w, _STORE)
+
+
+class storage_rounding:
+    """with storage_rounding(torch.bfloat16): forward(...) emulates bf16 storage."""
+
+    def __init__(self, dt):
+        self.dt = dt
+
+    def __enter__(self):
+        global _STORE
+        self.prev, _STORE = _STORE, self.dt
+        return self
+
+    def __exit__(self, *exc):
+        global _STORE
+        _STORE = self.prev
+
+
 def bn(x, sd, p, training):
     # torch.nn.BatchNorm2d semantics (momentum 0.1, eps 1e-5, unbiased running var)
     if training:
@@ -263,7 +314,9 @@ def bn(x, sd, p, training):
 
 
 def conv(x, sd, p, padding=0, groups=1):
-    return F.conv2d(x, sd[p + ".weight"], sd[p + ".bias"], padding=padding, groups=groups)
+    if groups > 1:  # depthwise (HANCBlock.conv2): fp32 weights / activated input
+        return q(F.conv2d(x, sd[p + ".weight"], sd[p + ".bias"], padding=padding, groups=groups))
+    return q(F.conv2d(q(x), qw(sd[p + ".weight"]), sd[p + ".bias"], padding=padding))
 
 
 def se(x, sd, p, training):
@@ -273,7 +326,7 @@ def se(x, sd, p, training):
     s = lrelu(F.linear(s, sd[p + ".fc1.weight"], sd[p + ".fc1.bias"]))
     s = torch.sigmoid(F.linear(s, sd[p + ".fc2.weight"], sd[p + ".fc2.bias"]))
     y = x * s.view(b, c, 1, 1)
-    return lrelu(bn(y, sd, p + ".bn", training))
+    return q(lrelu(bn(y, sd, p + ".bn", training)))
 
 
 def _up(x, f):
@@ -286,13 +339,13 @@ def hanc_layer(x, sd, p, k, training):
     b, c, h, w = x.shape
     parts = [x]
     if k >= 2:
-        parts.append(_up(F.avg_pool2d(x, 2), 2))
+        parts.append(_up(q(F.avg_pool2d(x, 2)), 2))
     if k >= 3:
-        parts.append(_up(F.avg_pool2d(x, 4), 4))
+        parts.append(_up(q(F.avg_pool2d(x, 4)), 4))
     if k >= 2:
-        parts.append(_up(F.max_pool2d(x, 2), 2))
+        parts.append(_up(q(F.max_pool2d(x, 2)), 2))
     if k >= 3:
-        parts.append(_up(F.max_pool2d(x, 4), 4))
+        parts.append(_up(q(F.max_pool2d(x, 4)), 4))
     z = torch.cat(parts, dim=2).view(b, c * (2 * k - 1), h, w)
     return lrelu(bn(conv(z, sd, p + ".cnv"), sd, p + ".bn", training))
 
@@ -304,7 +357,7 @@ def hanc_block(x, sd, p, k, training):
     c = x.shape[1]
     x = lrelu(bn(conv(x, sd, p + ".conv2", padding=1, groups=c), sd, p + ".norm2", training))
     x = hanc_layer(x, sd, p + ".hnc", k, training)
-    x = bn(x + inp, sd, p + ".norm", training)
+    x = bn(q(x + inp), sd, p + ".norm", training)
     x = lrelu(bn(conv(x, sd, p + ".conv3"), sd, p + ".norm3", training))
     return se(x, sd, p + ".sqe", training)
 
@@ -313,8 +366,8 @@ def respath(x, sd, p, n_lvl, training):
     """ResPath.forward, ACC_UNet/ACC_UNet.py:323-328."""
     for i in range(n_lvl):
         y = lrelu(bn(conv(x, sd, f"{p}.convs.{i}", padding=1), sd, f"{p}.bns.{i}", training))
-        x = x + se(y, sd, f"{p}.sqes.{i}", training)
-    return bn(lrelu(bn(x, sd, p + ".bn", training)), sd, p + ".sqe", training)
+        x = q(x + se(y, sd, f"{p}.sqes.{i}", training))
+    return q(bn(q(lrelu(bn(x, sd, p + ".bn", training))), sd, p + ".sqe", training))
 
 
 def conv_bn_se(x, sd, p, training):
@@ -329,7 +382,7 @@ def mlfc(xs, sd, p, training, variant):
     x1, x2, x3, x4 = xs
     if variant == "lite":
         return tuple(se(x, sd, f"{p}.sqe{i}", training) for i, x in enumerate(xs, 1))
-    down = lambda t: F.avg_pool2d(t, 2)
+    down = lambda t: q(F.avg_pool2d(t, 2))
     up = lambda t: _up(t, 2)
     b = x1.shape[0]
     cats = [
@@ -341,7 +394,7 @@ def mlfc(xs, sd, p, training, variant):
     xc = []
     for lvl in range(4):
         z = conv_bn_se(torch.cat(cats[lvl], dim=1), sd, f"{p}.cnv_blks{lvl + 1}.0", training)
-        xc.append(lrelu(bn(z, sd, f"{p}.bns{lvl + 1}.0", training)))
+        xc.append(q(lrelu(bn(z, sd, f"{p}.bns{lvl + 1}.0", training))))
     outs = []
     for lvl, xl in enumerate(xs):
         c, h, w = xl.shape[1:]
@@ -349,21 +402,22 @@ def mlfc(xs, sd, p, training, variant):
         m = conv_bn_se(merged, sd, f"{p}.cnv_mrg{lvl + 1}.0", training)
         if variant == "w":
             wgt = sd[p + ".W"]
-            m = m * wgt + xl * (1 - wgt)
+            m = q(m * wgt + xl * (1 - wgt))
         else:
-            m = m + xl
+            m = q(m + xl)
         outs.append(lrelu(bn(m, sd, f"{p}.bns_mrg{lvl + 1}.0", training)))
     return tuple(se(o, sd, f"{p}.sqe{i}", training) for i, o in enumerate(outs, 1))
 
 
 def convT(x, sd, p):
-    return F.conv_transpose2d(x, sd[p + ".weight"], sd[p + ".bias"], stride=2)
+    return q(F.conv_transpose2d(q(x), qw(sd[p + ".weight"]), sd[p + ".bias"], stride=2))
 
 
 def forward(sd, x, variant="canonical", training=True, n_classes=1):
     """ACC_UNet.forward, ACC_UNet/ACC_UNet.py:601-659 (script variant returns logits,
     Experiments/nets/ACC_UNet.py:654-655)."""
     t = training
+    x = q(x)
     x2 = hanc_block(hanc_block(x, sd, "cnv11", 3, t), sd, "cnv12", 3, t)
     x3 = hanc_block(hanc_block(F.max_pool2d(x2, 2), sd, "cnv21", 3, t), sd, "cnv22", 3, t)
     x4 = hanc_block(hanc_block(F.max_pool2d(x3, 2), sd, "cnv31", 3, t), sd, "cnv32", 3, t)
@@ -385,7 +439,10 @@ def forward(sd, x, variant="canonical", training=True, n_classes=1):
     x9 = hanc_block(x9, sd, "cnv82", 3, t)
     x10 = hanc_block(torch.cat([convT(x9, sd, "up9"), x2], 1), sd, "cnv91", 3, t)
     x10 = hanc_block(x10, sd, "cnv92", 3, t)
-    logits = conv(x10, sd, "out")
+    if n_classes == 1:  # the head reads bf16 x10 with fp32 weights, fp32 output
+        logits = F.conv2d(x10, sd["out.weight"], sd["out.bias"])
+    else:
+        logits = conv(x10, sd, "out")
     if variant != "script" and n_classes == 1:
         return torch.sigmoid(logits)
     return logits
