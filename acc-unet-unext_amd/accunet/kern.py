@@ -52,6 +52,35 @@ def _same_dt(ref: torch.Tensor, *ts):
     return _dt(ref)
 
 
+class ExtEvent:
+    """A hipEvent_t that, recorded inside a stream capture, becomes an EXTERNAL
+    event-record node of the graph (accunet_event_record_external), re-recorded at
+    every replay; other streams can wait on it (torch disallows external events on
+    ROCm, so the HIP calls go through the C ABI)."""
+
+    def __init__(self):
+        h = ctypes.c_void_p()
+        call("accunet_event_create", ctypes.byref(h))
+        self.h = h
+
+    def record_external(self, stream=None):
+        s = (stream or torch.cuda.current_stream()).cuda_stream
+        call("accunet_event_record_external", self.h, ctypes.c_void_p(s))
+
+    def wait(self, stream):
+        call("accunet_stream_wait_event", ctypes.c_void_p(stream.cuda_stream), self.h)
+
+    def synchronize(self):
+        call("accunet_event_synchronize", self.h)
+
+    def __del__(self):
+        try:
+            if self.h:
+                _lib.load().accunet_event_destroy(self.h)
+        except Exception:
+            pass
+
+
 def workspace(n_elems: int, device, dtype=torch.float32) -> torch.Tensor:
     return torch.empty(max(int(n_elems), 1), dtype=dtype, device=device)
 

@@ -14,9 +14,16 @@ Two execution modes, same arithmetic:
   graph (graph=True): forward + loss + backward (~1.5k kernel launches) are
       captured once into a HIP graph and replayed, removing the host launch cost
       that otherwise leaves the GPU idle between short kernels. For world > 1 the
-      graph also packs the gradients into one flat buffer, which is all-reduced
-      (AVG, RCCL) as ONE 67 MB collective between the replay and the optimizer
-      (~0.3 ms on xGMI vs ~120 ms of compute); Adam is one launch.
+      gradients are bucketed (~16 MB, reverse registration order = the order
+      backward finishes them). Inside the graph, the moment a bucket's last
+      gradient is accumulated its gradients are packed into the flat all-reduce
+      buffer and an EXTERNAL event node is recorded (hipEventRecordWithFlags(...,
+      hipEventRecordExternal)). Each step the host replays the graph and, without
+      waiting, enqueues per bucket on a side stream: wait(bucket event) -> RCCL
+      all_reduce(AVG) of that slice. The collectives therefore run over xGMI while
+      the graph is still computing the rest of backward; only the last bucket's
+      reduce is exposed before the one-launch Adam. The collectives themselves are
+      not captured (they run on RCCL's own stream, outside the graph).
       Capture happens on the first call: no autograd graph of an earlier eager
       step may still be alive then (drop references to its outputs / loss), since
       PyTorch keeps the stream of every AccumulateGrad node such a graph holds and
@@ -27,14 +34,104 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
+from . import kern
 from .dist import all_reduce_mean
 from .loss import WeightedDiceBCE
 from .optim import FusedAdam
 
 
+class _GraphBuckets:
+    """Bucketed, event-gated gradient all-reduce for the captured backward (graph mode,
+    world > 1; see the module docstring). Built before capture; its hooks run only
+    while the backward is being captured."""
+
+    def __init__(self, params, bucket_mb, device):
+        self.params = params
+        total = sum(p.numel() for p in params)
+        self.flat = torch.zeros(total, dtype=torch.float32, device=device)
+        self.views, offs, o = [], [], 0
+        for p in params:
+            offs.append(o)
+            self.views.append(self.flat[o:o + p.numel()].view_as(p))
+            o += p.numel()
+        cap = max(1, int(bucket_mb * (1 << 20) / 4))
+        self.buckets, cur, n = [], [], 0
+        for i in reversed(range(len(params))):  # backward finishes the output layer first
+            cur.append(i)
+            n += params[i].numel()
+            if n >= cap:
+                self.buckets.append(cur)
+                cur, n = [], 0
+        if cur:
+            self.buckets.append(cur)
+        self.range = [(min(offs[i] for i in b), max(offs[i] + params[i].numel() for i in b))
+                      for b in self.buckets]
+        self.bucket_of = {i: k for k, b in enumerate(self.buckets) for i in b}
+        self.events = [kern.ExtEvent() for _ in self.buckets]
+        self._handles = []
+
+    # ------------------------------------------------------------ capture side
+    def _seal(self, k):
+        """pack bucket k's gradients into the flat buffer, then mark it ready"""
+        if self._sealed[k]:
+            return
+        self._sealed[k] = True
+        live = [i for i in self.buckets[k] if self.params[i].grad is not None]
+        if live:
+            torch._foreach_copy_([self.views[i] for i in live], [self.params[i].grad for i in live])
+        self.events[k].record_external()
+
+    def _hook(self, i):
+        def hook(p):
+            if not self._queued:  # buckets with unused parameters close at the end
+                self._queued = True
+                torch.autograd.Variable._execution_engine.queue_callback(self._flush)
+            k = self.bucket_of[i]
+            self._left[k] -= 1
+            if self._left[k] == 0:
+                self._seal(k)
+        return hook
+
+    def _flush(self):
+        for k in range(len(self.buckets)):
+            self._seal(k)
+
+    def arm(self):
+        self._left = [len(b) for b in self.buckets]
+        self._sealed = [False] * len(self.buckets)
+        self._queued = False
+        self._handles = [p.register_post_accumulate_grad_hook(self._hook(i))
+                         for i, p in enumerate(self.params)]
+
+    def disarm(self):
+        for h in self._handles:
+            h.remove()
+        self._handles = []
+
+    # -------------------------------------------------------------- step side
+    def reduce(self, pg):
+        """enqueue every bucket's all-reduce behind its event (no host wait for RCCL)"""
+        nccl = dist.get_backend(pg) == "nccl"
+        main = torch.cuda.current_stream()
+        if not nccl:  # gloo (tests): host-synchronous collectives on finished buckets
+            for k, (lo, hi) in enumerate(self.range):
+                self.events[k].synchronize()
+                all_reduce_mean(self.flat[lo:hi], pg)
+            return
+        works = []
+        with torch.cuda.stream(self.stream):
+            for k, (lo, hi) in enumerate(self.range):
+                self.events[k].wait(self.stream)
+                works.append(dist.all_reduce(self.flat[lo:hi], op=dist.ReduceOp.AVG, group=pg,
+                                             async_op=True))
+        for w in works:  # the main stream (Adam) waits on RCCL's stream
+            w.wait()
+        main.wait_stream(self.stream)
+
+
 class TrainStep:
     def __init__(self, model, lr=1e-3, reducer=None, dice_weight=0.5, bce_weight=0.5,
-                 graph=False, process_group=None, precision=None):
+                 graph=False, process_group=None, precision=None, bucket_mb=16.0):
         if graph and reducer is not None:
             raise ValueError("graph mode does its own single-bucket all-reduce; pass no reducer")
         if precision is not None:  # "fp32" / "bf16": see ACC_UNet.set_precision
@@ -52,6 +149,7 @@ class TrainStep:
         # are views of its flat all-reduce buffer.
         self.opt = FusedAdam(self.params, lr=lr)
         self._g = None
+        self.bucket_mb = bucket_mb
         if graph and self.world > 1:
             # identical replicas to start from (what DDP / GradBucketReducer do at wrap time)
             with torch.no_grad():
@@ -106,26 +204,26 @@ class TrainStep:
             p.grad = None
         torch.cuda.synchronize()
 
+        self._buckets = None
+        if self.world > 1:
+            self._buckets = _GraphBuckets(self.params, self.bucket_mb, self._x.device)
+            self._buckets.stream = torch.cuda.Stream()
+            self._buckets.arm()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            loss = self._fwd_bwd(self._x, self._m)
-            live = [p for p in self.params if p.grad is not None]
-            if self.world > 1:
-                total = sum(p.numel() for p in self.params)
-                self._flat = torch.zeros(total, dtype=torch.float32, device=self._x.device)
-                views, o = {}, 0
-                for p in self.params:
-                    views[p] = self._flat[o:o + p.numel()].view_as(p)
-                    o += p.numel()
-                torch._foreach_copy_([views[p] for p in live], [p.grad for p in live])
+        try:
+            with torch.cuda.graph(g):
+                loss = self._fwd_bwd(self._x, self._m)
+        finally:
+            if self._buckets is not None:
+                self._buckets.disarm()
         self._g = g
         self._loss = loss.detach()
         # keep the graph-pool gradient tensors alive; the optimizer reads either them
         # (world 1) or the flat all-reduced buffer (world > 1)
         self._graph_grads = [p.grad for p in self.params]
         if self.world > 1:
-            for p in self.params:
-                p.grad = views[p]
+            for p, v in zip(self.params, self._buckets.views):
+                p.grad = v
         else:
             for p in self.params:
                 if p.grad is None:  # never produced (e.g. Lite's idle MLFC): zero gradient
@@ -145,7 +243,7 @@ class TrainStep:
             self._m.copy_(masks)
         self._g.replay()
         if self.world > 1:
-            all_reduce_mean(self._flat, self.pg)
+            self._buckets.reduce(self.pg)
         self.opt.step()
         return self._loss
 

@@ -533,3 +533,38 @@ extern "C" int accunet_wmerge_bwd(const void* g, const float* w, void* da, void*
     return ACC_EBADARG;
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
+
+// ---------------------------------------------------------------------------
+// HIP events for the graph-mode gradient all-reduce (accunet/train.py): inside a
+// stream capture, accunet_event_record_external leaves an EXTERNAL event-record node
+// in the graph (hipEventRecordWithFlags(..., hipEventRecordExternal)), so each graph
+// launch re-records it; a side stream gated on it (accunet_stream_wait_event) starts
+// the bucket's collective while the graph is still running the rest of backward.
+// ---------------------------------------------------------------------------
+extern "C" int accunet_event_create(void** ev) {
+  if (!ev) return ACC_EBADARG;
+  hipEvent_t e;
+  if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return ACC_ELAUNCH;
+  *ev = (void*)e;
+  return ACC_OK;
+}
+
+extern "C" int accunet_event_destroy(void* ev) {
+  return hipEventDestroy((hipEvent_t)ev) == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+}
+
+extern "C" int accunet_event_record_external(void* ev, void* stream) {
+  return hipEventRecordWithFlags((hipEvent_t)ev, (hipStream_t)stream, hipEventRecordExternal) ==
+                 hipSuccess
+             ? ACC_OK
+             : ACC_ELAUNCH;
+}
+
+extern "C" int accunet_stream_wait_event(void* stream, void* ev) {
+  return hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)ev, 0) == hipSuccess ? ACC_OK
+                                                                                  : ACC_ELAUNCH;
+}
+
+extern "C" int accunet_event_synchronize(void* ev) {
+  return hipEventSynchronize((hipEvent_t)ev) == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+}

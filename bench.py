@@ -58,6 +58,10 @@ def parse():
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (16; unext 32)")
     ap.add_argument("--size", type=int, default=None, help="image size (256; unext 224)")
     ap.add_argument("--variant", default="canonical")
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="activation storage: fp32 (configs[1], the reference's precision) or "
+                         "bf16 (configs[2]: bf16 activations, fp32 master weights / Adam / "
+                         "BN statistics)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true",
                     help="launch every kernel from Python (default: replay one HIP graph per step)")
@@ -128,11 +132,14 @@ def main():
         model = UNext(3, 1, img_size=args.size).to(dev).train()
     else:
         model = M.VARIANTS[args.variant](3, 1, n_filts=32).to(dev).train()
+    prec = None if unext else args.dtype
+    if unext and args.dtype != "fp32":
+        raise SystemExit("--dtype bf16 is the ACC_UNet configs[2] mode")
     if args.eager:
         reducer = adist.GradBucketReducer(model) if world > 1 else None
-        step = TrainStep(model, lr=1e-3, reducer=reducer)
+        step = TrainStep(model, lr=1e-3, reducer=reducer, precision=prec)
     else:
-        step = TrainStep(model, lr=1e-3, graph=True)
+        step = TrainStep(model, lr=1e-3, graph=True, precision=prec)
 
     g = torch.Generator(device="cpu").manual_seed(1000 + rank)
     B, S = args.batch, args.size
@@ -172,13 +179,15 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32",
+        "dtype": args.dtype,
         "data": "synthetic (x ~ N(0,1), mask ~ Bernoulli(0.3), per-rank seed 1000+rank); "
                 "torch.manual_seed(0) default init",
         "config": {"workload": (f"UNext fwd+WeightedDiceBCE+bwd+Adam, {B}x3x{S}x{S} per GPU"
                                 if unext else
                                 f"ACC_UNet {args.variant} fwd+WeightedDiceBCE+bwd+Adam, "
-                                f"{B}x3x{S}x{S} per GPU"),
+                                f"{B}x3x{S}x{S} per GPU"
+                                + (", bf16 activations / fp32 master weights"
+                                   if args.dtype == "bf16" else "")),
                    "model": ("UNext (1.47M)" if unext else
                              "ACC_UNet (16.77M)" if args.variant == "canonical" else args.variant),
                    "global_batch": B * world, "per_gpu_batch": B, "image": [3, S, S],
@@ -192,17 +201,19 @@ def main():
     if not args.no_probe and not unext:
         from accunet import probe
         blk = model.cnv12
-        rl = [probe.k1_dw3x3(B, S, S, blk.conv2.weight.shape[0], blk.conv2.weight, blk.conv2.bias),
-              probe.k3_se(B, S, S, blk.sqe.fc2.weight.shape[0], blk.sqe),
+        adt = model.act_dtype
+        rl = [probe.k1_dw3x3(B, S, S, blk.conv2.weight.shape[0], blk.conv2.weight, blk.conv2.bias,
+                             dtype=adt),
+              probe.k3_se(B, S, S, blk.sqe.fc2.weight.shape[0], blk.sqe, dtype=adt),
               probe.hanc_gemm(B * (S // 4) ** 2, model.cnv72.hnc.cnv.weight.shape[0],
-                              model.cnv72.conv1.weight.shape[0])]
+                              model.cnv72.conv1.weight.shape[0], dtype=adt)]
         # HBM traffic of K1 from the committed PMC passes of this same bench command
         # (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate runs; tools/pmc_traffic.py)
         tf = os.path.join(ROOT, "profiles", "k1_traffic.json")
         if os.path.exists(tf):
             with open(tf) as f:
                 t = json.load(f)
-            if t.get("shape") == rl[0]["shape"]:
+            if t.get("shape") == rl[0]["shape"] and t.get("dtype", "fp32") == args.dtype:
                 rl[0]["traffic"] = t["traffic_bytes"]
                 rl[0]["traffic_source"] = t.get("source", tf)
         line["roofline"] = rl[0]

@@ -276,6 +276,19 @@ int accunet_dotdiff(const void* g, const void* a, const void* b, long n, float* 
                     int accumulate, float* ws, int dt, void* stream);
 
 /* ------------------------------------------------------------------------- *
+ * HIP events for the graph-mode data-parallel step (accunet/train.py; the
+ * reference has no data parallelism, Experiments/train_model.py:696-698): inside a
+ * stream capture, record_external leaves an external event-record node in the graph,
+ * re-recorded by every launch of it; a side stream waiting on it starts the RCCL
+ * all-reduce of a finished gradient bucket while the graph runs the rest of backward.
+ * ------------------------------------------------------------------------- */
+int accunet_event_create(void** ev);
+int accunet_event_destroy(void* ev);
+int accunet_event_record_external(void* ev, void* stream);
+int accunet_stream_wait_event(void* stream, void* ev);
+int accunet_event_synchronize(void* ev);
+
+/* ------------------------------------------------------------------------- *
  * Input preparation (csrc/data.hip). Replaces the per-image host work of
  * ImageToImage2D.__getitem__, Experiments/Load_Dataset.py:453-487, for a whole
  * batch: image_prep takes N raw channel planes [N][Hin][Win] (fp32) and writes

@@ -47,3 +47,48 @@ def test_world2_bench_line():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 4 and d["value"] > 0
     assert d["scaling"] == "weak" and "cpu_baseline" not in d
+
+
+@pytest.mark.gpu
+def test_external_event_node_gates_side_stream():
+    """The graph-mode all-reduce gating (accunet/train.py _GraphBuckets): an external
+    event recorded inside a captured graph is re-recorded by every replay, and a side
+    stream waiting on it after replay() starts only once the replay reached it, even
+    behind a long prefix of graph work. Checked with a copy on the side stream that
+    would read a stale value if the wait were not gated on the current replay."""
+    import torch
+    from accunet import kern
+    dev = torch.device("cuda")
+    a = torch.randn(2048, 2048, device=dev)
+    x = torch.zeros(1 << 20, device=dev)
+    y = torch.empty_like(x)
+    ev = kern.ExtEvent()
+    side = torch.cuda.Stream()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):  # warm-up outside capture
+        for _ in range(2):
+            a.copy_(torch.tanh(a @ a) * 0.1)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(30):  # ~ms of work ahead of the gated write
+            a.copy_(torch.tanh(a @ a) * 0.1)
+        x.add_(1.0)
+        ev.record_external()
+        for _ in range(30):  # and more after it
+            a.copy_(torch.tanh(a @ a) * 0.1)
+    for it in range(1, 4):
+        g.replay()
+        ev.wait(side)
+        with torch.cuda.stream(side):
+            y.copy_(x)
+        torch.cuda.synchronize()
+        assert float(y.min()) == float(it) and float(y.max()) == float(it), (it, float(y.min()))
+        g.replay()
+        ev.synchronize()  # host wait on the current replay's record
+        assert float(x[0]) == float(it + 1)
+        torch.cuda.synchronize()
+        x.sub_(1.0)
+        torch.cuda.synchronize()
