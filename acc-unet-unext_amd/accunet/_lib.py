@@ -101,9 +101,10 @@ _SIGS = {
     "accunet_dotdiff": [P, P, P, L, P, I, P, I, P],
     "accunet_wmerge_fwd": [P, P, P, P, L, I, P, I, P],
     "accunet_wmerge_bwd": [P, P, P, P, L, I, P],
+    "accunet_graph_marker": [I, P],
+    "accunet_graph_events_after_markers": [P, POINTER(c_void_p), I],
     "accunet_event_create": [POINTER(c_void_p)],
     "accunet_event_destroy": [P],
-    "accunet_event_record_external": [P, P],
     "accunet_stream_wait_event": [P, P],
     "accunet_event_synchronize": [P],
     "accunet_image_prep": [P, I, I, I, I, P, P],

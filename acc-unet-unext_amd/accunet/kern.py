@@ -52,20 +52,31 @@ def _same_dt(ref: torch.Tensor, *ts):
     return _dt(ref)
 
 
-class ExtEvent:
-    """A hipEvent_t that, recorded inside a stream capture, becomes an EXTERNAL
-    event-record node of the graph (accunet_event_record_external), re-recorded at
-    every replay; other streams can wait on it (torch disallows external events on
-    ROCm, so the HIP calls go through the C ABI)."""
+class GraphEvent:
+    """A hipEvent_t for the graph-mode all-reduce gating (see include/accunet.h,
+    accunet_graph_events_after_markers): `mark(id)` during capture leaves marker id
+    in the stream; `attach(graph, events)` after capture adds an event-record node
+    behind each marker; `wait(stream)` gates another stream on the event."""
 
     def __init__(self):
         h = ctypes.c_void_p()
         call("accunet_event_create", ctypes.byref(h))
         self.h = h
 
-    def record_external(self, stream=None):
+    @staticmethod
+    def mark(marker_id: int, stream=None):
         s = (stream or torch.cuda.current_stream()).cuda_stream
-        call("accunet_event_record_external", self.h, ctypes.c_void_p(s))
+        call("accunet_graph_marker", int(marker_id), ctypes.c_void_p(s))
+
+    @staticmethod
+    def attach(raw_graph: int, events) -> int:
+        """add an event-record node behind each marker of the captured graph"""
+        arr = (ctypes.c_void_p * len(events))(*[e.h.value for e in events])
+        n = _lib.load().accunet_graph_events_after_markers(ctypes.c_void_p(raw_graph), arr,
+                                                             len(events))
+        if n < 0:
+            raise _lib.AccError(f"accunet_graph_events_after_markers failed: {n}")
+        return n
 
     def wait(self, stream):
         call("accunet_stream_wait_event", ctypes.c_void_p(stream.cuda_stream), self.h)

@@ -17,13 +17,14 @@ Two execution modes, same arithmetic:
       gradients are bucketed (~16 MB, reverse registration order = the order
       backward finishes them). Inside the graph, the moment a bucket's last
       gradient is accumulated its gradients are packed into the flat all-reduce
-      buffer and an EXTERNAL event node is recorded (hipEventRecordWithFlags(...,
-      hipEventRecordExternal)). Each step the host replays the graph and, without
-      waiting, enqueues per bucket on a side stream: wait(bucket event) -> RCCL
-      all_reduce(AVG) of that slice. The collectives therefore run over xGMI while
-      the graph is still computing the rest of backward; only the last bucket's
-      reduce is exposed before the one-launch Adam. The collectives themselves are
-      not captured (they run on RCCL's own stream, outside the graph).
+      buffer and a marker kernel is left in the stream; after capture an
+      event-record node is added behind each marker (accunet_graph_events_after_
+      markers on the kept hipGraph_t, then instantiate). Each step the host replays
+      the graph and, without waiting, enqueues per bucket on a side stream:
+      wait(bucket event) -> RCCL all_reduce(AVG) of that slice. The collectives
+      therefore run over xGMI while the graph is still computing the rest of
+      backward; only the last bucket's reduce is exposed before the one-launch Adam.
+      The collectives themselves are not captured (they run on RCCL's own stream).
       Capture happens on the first call: no autograd graph of an earlier eager
       step may still be alive then (drop references to its outputs / loss), since
       PyTorch keeps the stream of every AccumulateGrad node such a graph holds and
@@ -67,7 +68,7 @@ class _GraphBuckets:
         self.range = [(min(offs[i] for i in b), max(offs[i] + params[i].numel() for i in b))
                       for b in self.buckets]
         self.bucket_of = {i: k for k, b in enumerate(self.buckets) for i in b}
-        self.events = [kern.ExtEvent() for _ in self.buckets]
+        self.events = [kern.GraphEvent() for _ in self.buckets]
         self._handles = []
 
     # ------------------------------------------------------------ capture side
@@ -79,7 +80,7 @@ class _GraphBuckets:
         live = [i for i in self.buckets[k] if self.params[i].grad is not None]
         if live:
             torch._foreach_copy_([self.views[i] for i in live], [self.params[i].grad for i in live])
-        self.events[k].record_external()
+        kern.GraphEvent.mark(k)
 
     def _hook(self, i):
         def hook(p):
@@ -209,13 +210,20 @@ class TrainStep:
             self._buckets = _GraphBuckets(self.params, self.bucket_mb, self._x.device)
             self._buckets.stream = torch.cuda.Stream()
             self._buckets.arm()
-        g = torch.cuda.CUDAGraph()
+        g = torch.cuda.CUDAGraph(keep_graph=self._buckets is not None)
         try:
             with torch.cuda.graph(g):
                 loss = self._fwd_bwd(self._x, self._m)
         finally:
             if self._buckets is not None:
                 self._buckets.disarm()
+        if self._buckets is not None:
+            # an event-record node behind every bucket's marker, then instantiate
+            n = kern.GraphEvent.attach(g.raw_cuda_graph(), self._buckets.events)
+            if n != len(self._buckets.buckets):
+                raise RuntimeError(f"graph bucket markers: found {n}, expected "
+                                   f"{len(self._buckets.buckets)}")
+            g.instantiate()
         self._g = g
         self._loss = loss.detach()
         # keep the graph-pool gradient tensors alive; the optimizer reads either them

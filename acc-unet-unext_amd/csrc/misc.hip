@@ -10,6 +10,7 @@
 #include "common.h"
 #include "chan.h"
 #include "kernels.h"
+#include <stdlib.h>
 
 // ---------------------------------------------------------------------------
 // head
@@ -535,12 +536,69 @@ extern "C" int accunet_wmerge_bwd(const void* g, const float* w, void* da, void*
 }
 
 // ---------------------------------------------------------------------------
-// HIP events for the graph-mode gradient all-reduce (accunet/train.py): inside a
-// stream capture, accunet_event_record_external leaves an EXTERNAL event-record node
-// in the graph (hipEventRecordWithFlags(..., hipEventRecordExternal)), so each graph
-// launch re-records it; a side stream gated on it (accunet_stream_wait_event) starts
-// the bucket's collective while the graph is still running the rest of backward.
+// HIP events for the graph-mode gradient all-reduce (accunet/train.py). While the
+// backward is captured, accunet_graph_marker(id) leaves a 1-thread marker kernel in
+// the stream at the point where gradient bucket `id` is complete. After capture (the
+// graph kept un-instantiated, torch CUDAGraph(keep_graph=True)),
+// accunet_graph_events_after_markers adds an event-record node behind every marker
+// (hipGraphAddEventRecordNode; recording events *during* capture needs external event
+// records, which the HIP runtime torch ships rejects). Each graph launch re-records
+// the events, so a side stream that waits on them (accunet_stream_wait_event) after
+// the launch starts that bucket's RCCL all-reduce while the graph still runs the rest
+// of backward.
 // ---------------------------------------------------------------------------
+#define ACC_MAX_MARKERS 32
+template <int ID>
+__global__ void graph_marker_kernel() {}
+
+template <int... I>
+struct MarkerTable {
+  static void* get(int i) {
+    static void* const t[] = {reinterpret_cast<void*>(&graph_marker_kernel<I>)...};
+    return t[i];
+  }
+};
+template <int N, int... I>
+struct MakeMarkers : MakeMarkers<N - 1, N - 1, I...> {};
+template <int... I>
+struct MakeMarkers<0, I...> {
+  typedef MarkerTable<I...> type;
+};
+typedef MakeMarkers<ACC_MAX_MARKERS>::type Markers;
+
+extern "C" int accunet_graph_marker(int id, void* stream) {
+  if (id < 0 || id >= ACC_MAX_MARKERS) return ACC_EBADARG;
+  hipLaunchKernel(Markers::get(id), dim3(1), dim3(1), nullptr, 0, (hipStream_t)stream);
+  return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+}
+
+// returns the number of event-record nodes added (one per marker found), or < 0
+extern "C" int accunet_graph_events_after_markers(void* graph, void* const* events, int n) {
+  if (!graph || !events || n < 0 || n > ACC_MAX_MARKERS) return ACC_EBADARG;
+  hipGraph_t g = (hipGraph_t)graph;
+  size_t nn = 0;
+  if (hipGraphGetNodes(g, nullptr, &nn) != hipSuccess) return ACC_ELAUNCH;
+  hipGraphNode_t* nodes = (hipGraphNode_t*)malloc(sizeof(hipGraphNode_t) * (nn ? nn : 1));
+  if (!nodes) return ACC_EBADARG;
+  int found = 0, status = ACC_OK;
+  if (hipGraphGetNodes(g, nodes, &nn) != hipSuccess) status = ACC_ELAUNCH;
+  for (size_t k = 0; k < nn && status == ACC_OK; ++k) {
+    hipGraphNodeType t;
+    if (hipGraphNodeGetType(nodes[k], &t) != hipSuccess || t != hipGraphNodeTypeKernel) continue;
+    hipKernelNodeParams kp;
+    if (hipGraphKernelNodeGetParams(nodes[k], &kp) != hipSuccess) continue;
+    for (int id = 0; id < n; ++id) {
+      if (kp.func != Markers::get(id)) continue;
+      hipGraphNode_t ev;
+      if (hipGraphAddEventRecordNode(&ev, g, &nodes[k], 1, (hipEvent_t)events[id]) != hipSuccess)
+        status = ACC_ELAUNCH;
+      ++found;
+    }
+  }
+  free(nodes);
+  return status == ACC_OK ? found : status;
+}
+
 extern "C" int accunet_event_create(void** ev) {
   if (!ev) return ACC_EBADARG;
   hipEvent_t e;
@@ -551,13 +609,6 @@ extern "C" int accunet_event_create(void** ev) {
 
 extern "C" int accunet_event_destroy(void* ev) {
   return hipEventDestroy((hipEvent_t)ev) == hipSuccess ? ACC_OK : ACC_ELAUNCH;
-}
-
-extern "C" int accunet_event_record_external(void* ev, void* stream) {
-  return hipEventRecordWithFlags((hipEvent_t)ev, (hipStream_t)stream, hipEventRecordExternal) ==
-                 hipSuccess
-             ? ACC_OK
-             : ACC_ELAUNCH;
 }
 
 extern "C" int accunet_stream_wait_event(void* stream, void* ev) {

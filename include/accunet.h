@@ -276,15 +276,19 @@ int accunet_dotdiff(const void* g, const void* a, const void* b, long n, float* 
                     int accumulate, float* ws, int dt, void* stream);
 
 /* ------------------------------------------------------------------------- *
- * HIP events for the graph-mode data-parallel step (accunet/train.py; the
- * reference has no data parallelism, Experiments/train_model.py:696-698): inside a
- * stream capture, record_external leaves an external event-record node in the graph,
- * re-recorded by every launch of it; a side stream waiting on it starts the RCCL
- * all-reduce of a finished gradient bucket while the graph runs the rest of backward.
+ * HIP graph / event plumbing for the graph-mode data-parallel step
+ * (accunet/train.py; the reference has no data parallelism,
+ * Experiments/train_model.py:696-698). graph_marker(id) launches an empty marker
+ * kernel; after capture, graph_events_after_markers(graph, events, n) adds an
+ * event-record node behind each marker id < n of the (un-instantiated) hipGraph_t
+ * and returns how many it added. Every launch of the graph re-records the events; a
+ * side stream waiting on one (stream_wait_event) starts the RCCL all-reduce of the
+ * gradient bucket that marker closed while the graph runs the rest of backward.
  * ------------------------------------------------------------------------- */
+int accunet_graph_marker(int id, void* stream);
+int accunet_graph_events_after_markers(void* graph, void* const* events, int n);
 int accunet_event_create(void** ev);
 int accunet_event_destroy(void* ev);
-int accunet_event_record_external(void* ev, void* stream);
 int accunet_stream_wait_event(void* stream, void* ev);
 int accunet_event_synchronize(void* ev);
 

@@ -50,19 +50,20 @@ def test_world2_bench_line():
 
 
 @pytest.mark.gpu
-def test_external_event_node_gates_side_stream():
-    """The graph-mode all-reduce gating (accunet/train.py _GraphBuckets): an external
-    event recorded inside a captured graph is re-recorded by every replay, and a side
-    stream waiting on it after replay() starts only once the replay reached it, even
-    behind a long prefix of graph work. Checked with a copy on the side stream that
-    would read a stale value if the wait were not gated on the current replay."""
+def test_graph_event_nodes_gate_side_stream():
+    """The graph-mode all-reduce gating (accunet/train.py _GraphBuckets): a marker left
+    in a captured graph gets an event-record node behind it (kern.GraphEvent.attach on
+    the kept graph), every replay re-records the event, and a side stream waiting on
+    it after replay() starts only once the replay has reached the marker, even behind
+    a long prefix of graph work. Checked with a copy on the side stream that would
+    read a stale value if the wait were not gated on the current replay."""
     import torch
     from accunet import kern
     dev = torch.device("cuda")
     a = torch.randn(2048, 2048, device=dev)
     x = torch.zeros(1 << 20, device=dev)
     y = torch.empty_like(x)
-    ev = kern.ExtEvent()
+    evs = [kern.GraphEvent(), kern.GraphEvent()]
     side = torch.cuda.Stream()
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
@@ -71,24 +72,24 @@ def test_external_event_node_gates_side_stream():
             a.copy_(torch.tanh(a @ a) * 0.1)
     torch.cuda.current_stream().wait_stream(s)
     torch.cuda.synchronize()
-    g = torch.cuda.CUDAGraph()
+    g = torch.cuda.CUDAGraph(keep_graph=True)
     with torch.cuda.graph(g):
         for _ in range(30):  # ~ms of work ahead of the gated write
             a.copy_(torch.tanh(a @ a) * 0.1)
         x.add_(1.0)
-        ev.record_external()
+        kern.GraphEvent.mark(1)
         for _ in range(30):  # and more after it
             a.copy_(torch.tanh(a @ a) * 0.1)
+        kern.GraphEvent.mark(0)
+    assert kern.GraphEvent.attach(g.raw_cuda_graph(), evs) == 2
+    g.instantiate()
     for it in range(1, 4):
         g.replay()
-        ev.wait(side)
+        evs[1].wait(side)
         with torch.cuda.stream(side):
             y.copy_(x)
         torch.cuda.synchronize()
         assert float(y.min()) == float(it) and float(y.max()) == float(it), (it, float(y.min()))
-        g.replay()
-        ev.synchronize()  # host wait on the current replay's record
-        assert float(x[0]) == float(it + 1)
-        torch.cuda.synchronize()
-        x.sub_(1.0)
-        torch.cuda.synchronize()
+    g.replay()
+    evs[0].synchronize()  # host wait on the current replay's record
+    assert float(x[0]) == 4.0
