@@ -134,6 +134,61 @@ ACC_DEV void stq_nt(bf16_t* p, float4 v) {
   accu2 u = {pack_bf2(v.x, v.y), pack_bf2(v.z, v.w)};
   __builtin_nontemporal_store(u, reinterpret_cast<accu2*>(p));
 }
+// A channel quad as loaded, before widening (float4 / 4 packed bf16). Prefetch
+// buffers hold this raw form: widening right after the load would make the
+// compiler wait for the load there, not where the data is consumed.
+template <typename T> struct QuadRaw;
+template <> struct QuadRaw<float> { typedef float4 type; };
+template <> struct QuadRaw<bf16_t> { typedef uint2 type; };
+ACC_DEV float4 ldq_raw(const float* p, bool nt) { return nt ? ld4_nt(p) : ld4(p); }
+ACC_DEV uint2 ldq_raw(const bf16_t* p, bool nt) {
+  if (nt) {
+    const accu2 u = __builtin_nontemporal_load(reinterpret_cast<const accu2*>(p));
+    return make_uint2(u.x, u.y);
+  }
+  return *reinterpret_cast<const uint2*>(p);
+}
+ACC_DEV float4 q2f(float4 v) { return v; }
+ACC_DEV float4 q2f(uint2 u) { return make_float4(bflo(u.x), bfhi(u.x), bflo(u.y), bfhi(u.y)); }
+ACC_DEV void qzero(float4& v) { v = make_float4(0.f, 0.f, 0.f, 0.f); }
+ACC_DEV void qzero(uint2& v) { v = make_uint2(0u, 0u); }
+
+// Raw buffer access through a 128-bit resource descriptor whose num_records range
+// check loads 0 / drops the store for any offset at or past it (ACC_OOB). Masking
+// a lane this way instead of branching around the access keeps the instruction
+// stream branch-free, so the compiler knows how many memory operations follow a
+// load and can wait for that load alone (s_waitcnt vmcnt(N)), not for vmcnt(0).
+// AUX: 0 = default cache policy, 2 = non-temporal. Descriptor bases and sizes
+// must be wave-uniform (kernel arguments / blockIdx-derived).
+#define ACC_OOB 0x80000000u
+typedef unsigned acc_u32x4 __attribute__((__vector_size__(16)));
+typedef unsigned acc_u32x2 __attribute__((__vector_size__(8)));
+ACC_DEV __amdgpu_buffer_rsrc_t acc_rsrc(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+template <int AUX>
+ACC_DEV float4 bufq_ld(__amdgpu_buffer_rsrc_t r, unsigned off, const float*) {
+  const acc_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AUX);
+  return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),
+                     __uint_as_float(v[3]));
+}
+template <int AUX>
+ACC_DEV uint2 bufq_ld(__amdgpu_buffer_rsrc_t r, unsigned off, const bf16_t*) {
+  const acc_u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, AUX);
+  return make_uint2(v[0], v[1]);
+}
+template <int AUX>
+ACC_DEV void bufq_st(__amdgpu_buffer_rsrc_t r, unsigned off, float4 v, float*) {
+  acc_u32x4 u = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z),
+                 __float_as_uint(v.w)};
+  __builtin_amdgcn_raw_buffer_store_b128(u, r, off, 0, AUX);
+}
+template <int AUX>
+ACC_DEV void bufq_st(__amdgpu_buffer_rsrc_t r, unsigned off, float4 v, bf16_t*) {
+  acc_u32x2 u = {pack_bf2(v.x, v.y), pack_bf2(v.z, v.w)};
+  __builtin_amdgcn_raw_buffer_store_b64(u, r, off, 0, AUX);
+}
+
 // the value v takes once stored as T (statistics are taken of what is stored)
 ACC_DEV float rnd_as(float v, const float*) { return v; }
 ACC_DEV float rnd_as(float v, const bf16_t*) { return bf2f(f2bf(v)); }

@@ -11,6 +11,7 @@
 // register window down its pixel column: per output row it issues 3 new 16-byte
 // loads (its own column + the two neighbours, which are L1/L2 hits shared with the
 // adjacent threads) and one 16-byte store, so HBM sees ~1 read + 1 write per element.
+#include <type_traits>
 #include "common.h"
 #include "kernels.h"
 #include "chan.h"
@@ -314,11 +315,11 @@ struct DwT {
 
 // Strip pipeline helpers: input rows live in a 10-slot LDS ring, row h of the
 // block's strip (which starts at output row hbeg) in slot (h - hbeg + 1) % 10.
-// Fetch `n` float4 elements of consecutive input rows starting at row hA into
-// registers (zero outside the image).
-template <int TCQ, int NKK, typename TX>
-ACC_DEV void dw_fetch_rows(float4 (&v)[NKK], const TX* __restrict__ x, const DwTGeom& g, int b,
-                           int hA, int n, int w0, int c0) {
+// Fetch `n` quads of consecutive input rows starting at row hA into registers, raw
+// (zero outside the image / past n: ACC_OOB offsets, no branches). rx covers one image.
+template <int TCQ, int NKK, int AUX, typename TX>
+ACC_DEV void dw_fetch_rows(typename QuadRaw<TX>::type (&v)[NKK], __amdgpu_buffer_rsrc_t rx,
+                           const DwTGeom& g, int hA, int n, int w0, int c0) {
   typedef DwT<TCQ> G;
   const int tid = threadIdx.x, q = tid % TCQ;
 #pragma unroll
@@ -327,17 +328,16 @@ ACC_DEV void dw_fetch_rows(float4 (&v)[NKK], const TX* __restrict__ x, const DwT
     const int rp = i / TCQ;
     const int p = rp % G::IP, r = rp / G::IP;
     const int hh = hA + r, ww = w0 - 1 + p;
-    v[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (i < n && hh >= 0 && hh < g.H && ww >= 0 && ww < g.W) {
-      const TX* src = x + (((long)b * g.H + hh) * g.W + ww) * g.C + c0 + 4 * q;
-      v[k] = g.ntl ? ldq_nt(src) : ldq(src);
-    }
+    const bool in = i < n && hh >= 0 && hh < g.H && ww >= 0 && ww < g.W;
+    const unsigned off = in ? (unsigned)(((hh * g.W + ww) * g.C + c0 + 4 * q) * (int)sizeof(TX))
+                            : ACC_OOB;
+    v[k] = bufq_ld<AUX>(rx, off, (const TX*)nullptr);
   }
 }
 
 // Activate (prologue BN+act, in-image elements only) and park fetched rows in the ring.
-template <int TCQ, int NKK>
-ACC_DEV void dw_park_rows(float4* __restrict__ ring, const float4 (&v)[NKK], const DwTGeom& g,
+template <int TCQ, int NKK, typename R>
+ACC_DEV void dw_park_rows(float4* __restrict__ ring, const R (&v)[NKK], const DwTGeom& g,
                           int hA, int n, int w0, int hbeg, bool pro, float4 ps, float4 pb,
                           int act) {
   typedef DwT<TCQ> G;
@@ -349,7 +349,7 @@ ACC_DEV void dw_park_rows(float4* __restrict__ ring, const float4 (&v)[NKK], con
       const int rp = i / TCQ;
       const int p = rp % G::IP, r = rp / G::IP;
       const int hh = hA + r, ww = w0 - 1 + p;
-      float4 a = v[k];
+      float4 a = q2f(v[k]);
       if (pro && hh >= 0 && hh < g.H && ww >= 0 && ww < g.W) {
         a.x = apply_act(a.x * ps.x + pb.x, act);
         a.y = apply_act(a.y * ps.y + pb.y, act);
@@ -410,7 +410,10 @@ ACC_DEV void dw_fill_tile(float4* __restrict__ tile, const TX* __restrict__ x,
 // NEXT chunk adds (r0+9 .. r0+12) are fetched into registers before this chunk is
 // computed and parked afterwards in the slots of rows r0-1 .. r0+2 (dead by then),
 // so HBM reads stay in flight through the compute (software pipeline).
-template <int TCQ, bool BNB, typename T>
+// The strip loop is branch-free in its memory operations (buffer loads / stores
+// with out-of-range offsets for the lanes and rows that are masked off), so the
+// park waits for the prefetched rows only (vmcnt(N)), not for the chunk's stores.
+template <int TCQ, bool BNB, int AUX, typename T>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BNB ? 2 : 3)))
 dw3x3_tile_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
                       const float* __restrict__ bias, const float* __restrict__ sc,
@@ -418,11 +421,11 @@ dw3x3_tile_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
                       double* __restrict__ stats, DwTGeom g, const T* __restrict__ bz,
                       const float* __restrict__ bst, int bact) {
   typedef DwT<TCQ> G;
+  typedef typename QuadRaw<T>::type RawQ;
   constexpr int CR = G::CR;
   __shared__ float4 tile[G::N4 > 1024 ? G::N4 : 1024];
-  // bz != null (data gradient, flip = 1): stats receive the BatchNorm-backward partials
+  // BNB (data gradient, flip = 1): stats receive the BatchNorm-backward partials
   // (sum g, sum g*(bz - mean)) of g = out * act'(bz*scale + shift) instead of (sum, sumsq)
-  const bool bnb = BNB && stats != nullptr && bz != nullptr;
   const int tid = threadIdx.x;
   const int q = tid % TCQ, p = tid / TCQ;
   int t = dw_tile_id(g);
@@ -441,6 +444,12 @@ dw3x3_tile_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
   const int hbeg = th * DW_TR * g.rch, w0 = tw * G::TP;
   const int hend = min(g.H, hbeg + DW_TR * g.rch);
   const int nch = (hend - hbeg + CR - 1) / CR;
+  // one image per descriptor (the host keeps H*W*C*4 < 2^31)
+  const long img = (long)b * g.H * g.W * g.C;
+  const unsigned ibytes = (unsigned)(g.H * g.W * g.C * (int)sizeof(T));
+  const __amdgpu_buffer_rsrc_t rx = acc_rsrc(x + img, ibytes);
+  const __amdgpu_buffer_rsrc_t rz = acc_rsrc(z + img, ibytes);
+  const __amdgpu_buffer_rsrc_t rb = acc_rsrc(BNB ? bz + img : x + img, BNB ? ibytes : 0u);
   const bool pro = sc != nullptr;
   float4 ps = make_float4(1.f, 1.f, 1.f, 1.f), pb = make_float4(0.f, 0.f, 0.f, 0.f);
   if (pro) {
@@ -448,8 +457,8 @@ dw3x3_tile_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
     pb = ld4(sh + c);
   }
   {
-    float4 v[G::NK];
-    dw_fetch_rows<TCQ, G::NK>(v, x, g, b, hbeg - 1, G::N4, w0, c0);
+    RawQ v[G::NK];
+    dw_fetch_rows<TCQ, G::NK, AUX, T>(v, rx, g, hbeg - 1, G::N4, w0, c0);
     dw_park_rows<TCQ, G::NK>(tile, v, g, hbeg - 1, G::N4, w0, hbeg, pro, ps, pb, act);
   }
   float k[9][4], bi[4];
@@ -460,7 +469,7 @@ dw3x3_tile_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
     bi[j] = bias ? bias[c + j] : 0.f;
   }
   float bmu[4] = {0.f, 0.f, 0.f, 0.f}, bsc[4] = {0.f, 0.f, 0.f, 0.f}, bsh[4] = {0.f, 0.f, 0.f, 0.f};
-  if (bnb) {
+  if (BNB) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       bmu[j] = bst[BN_MEAN * g.C + c + j];
@@ -468,83 +477,92 @@ dw3x3_tile_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
       bsh[j] = bst[BN_SHIFT * g.C + c + j];
     }
   }
+  // Retire every load issued so far (weights, bias, BN vectors) before the strip loop.
+  // Left pending, the waitcnt pass merges them into the loop's state and guards each
+  // row's first weight use with vmcnt(0), which then also drains the prefetched rows
+  // and the previous row's store -- one full HBM round trip per output row.
+  __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
   const int w = w0 + p;
+  const bool wv = w < g.W;
   // BNB: the bz rows of a chunk are fetched one chunk ahead (registers), like the input rows
-  float4 zcur[CR], znext[CR];
-  auto fetch_z = [&](float4 (&zz)[CR], int rbase) {
+  RawQ zcur[CR], znext[CR];
+  auto fetch_z = [&](RawQ (&zz)[CR], int rbase, bool on) {
 #pragma unroll
-    for (int r = 0; r < CR; ++r)
-      zz[r] = (w < g.W && rbase + r < hend)
-                  ? ldq(bz + (((long)b * g.H + rbase + r) * g.W + w) * g.C + c)
-                  : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int r = 0; r < CR; ++r) {
+      const bool in = on && wv && rbase + r < hend;
+      const unsigned off = in ? (unsigned)((((rbase + r) * g.W + w) * g.C + c) * (int)sizeof(T))
+                              : ACC_OOB;
+      zz[r] = bufq_ld<0>(rb, off, (const T*)nullptr);
+    }
   };
-  if (bnb) fetch_z(zcur, hbeg);
+  if (BNB) fetch_z(zcur, hbeg, true);
   for (int kc = 0; kc < nch; ++kc) {
     const int r0 = hbeg + CR * kc;
     // rows r0+9 .. are needed only if the strip's last input row (hend) lies there
     const bool more = kc + 1 < nch && r0 + 9 <= hend;
-    float4 nx[G::NK8];
-    if (more) dw_fetch_rows<TCQ, G::NK8>(nx, x, g, b, r0 + 9, G::N8, w0, c0);
-    if (bnb && kc + 1 < nch) fetch_z(znext, r0 + CR);
-    if (w < g.W) {
-      const int base = (CR * kc) % G::IR;  // slot of input row r0 - 1
-      float win[3][3][4];
-      auto rd = [&](int j, float (&row)[3][4]) {
-        int sl = base + j;
-        sl = sl >= G::IR ? sl - G::IR : sl;
+    RawQ nx[G::NK8];
+    dw_fetch_rows<TCQ, G::NK8, AUX, T>(nx, rx, g, r0 + 9, more ? G::N8 : 0, w0, c0);
+    if (BNB) fetch_z(znext, r0 + CR, kc + 1 < nch);
+    const int base = (CR * kc) % G::IR;  // slot of input row r0 - 1
+    float win[3][3][4];
+    auto rd = [&](int j, float (&row)[3][4]) {
+      int sl = base + j;
+      sl = sl >= G::IR ? sl - G::IR : sl;
 #pragma unroll
-        for (int dx = 0; dx < 3; ++dx) {
-          float4 a = tile[(sl * G::IP + p + dx) * TCQ + q];
-          row[dx][0] = a.x; row[dx][1] = a.y; row[dx][2] = a.z; row[dx][3] = a.w;
-        }
-      };
-      rd(0, win[0]);
-      rd(1, win[1]);
-      const int nr = min(CR, hend - r0);
+      for (int dx = 0; dx < 3; ++dx) {
+        float4 a = tile[(sl * G::IP + p + dx) * TCQ + q];
+        row[dx][0] = a.x; row[dx][1] = a.y; row[dx][2] = a.z; row[dx][3] = a.w;
+      }
+    };
+    rd(0, win[0]);
+    rd(1, win[1]);
+    const int nr = min(CR, hend - r0);
 #pragma unroll
-      for (int r = 0; r < CR; ++r) {
-        if (r < nr) {
-          rd(r + 2, win[2]);
-          float o[4];
+    for (int r = 0; r < CR; ++r) {
+      // rows past the strip end (r >= nr) read stale ring slots: computed, not kept
+      const bool on = wv && r < nr;
+      rd(r + 2, win[2]);
+      float o[4];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            float acc = bi[j];
+      for (int j = 0; j < 4; ++j) {
+        float acc = bi[j];
 #pragma unroll
-            for (int dy = 0; dy < 3; ++dy)
+        for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
-              for (int dx = 0; dx < 3; ++dx) acc = fmaf(k[dy * 3 + dx][j], win[dy][dx][j], acc);
-            acc = rnd<T>(acc);  // statistics of the stored value
-            o[j] = acc;
-            if (bnb) {
-              const float zz = f4get(zcur[r], j);
-              float gg = acc;
-              if (bact == ACT_LRELU) gg *= lrelu_d(zz * bsc[j] + bsh[j]);
-              s1[j] += gg;
-              s2[j] += (double)gg * ((double)zz - bmu[j]);
-            } else {
-              s1[j] += acc;
-              s2[j] += (double)acc * acc;
-            }
-          }
-          stq_nt(z + (((long)b * g.H + r0 + r) * g.W + w) * g.C + c, make_float4(o[0], o[1], o[2], o[3]));
-#pragma unroll
-          for (int dx = 0; dx < 3; ++dx)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              win[0][dx][j] = win[1][dx][j];
-              win[1][dx][j] = win[2][dx][j];
-            }
+          for (int dx = 0; dx < 3; ++dx) acc = fmaf(k[dy * 3 + dx][j], win[dy][dx][j], acc);
+        acc = rnd<T>(acc);  // statistics of the stored value
+        o[j] = acc;
+        const float am = on ? acc : 0.f;
+        if (BNB) {
+          const float zz = f4get(q2f(zcur[r]), j);
+          float gg = am;
+          if (bact == ACT_LRELU) gg *= lrelu_d(zz * bsc[j] + bsh[j]);
+          s1[j] += gg;
+          s2[j] += (double)gg * ((double)zz - bmu[j]);
+        } else {
+          s1[j] += am;
+          s2[j] += (double)am * am;
         }
       }
+      const unsigned off =
+          on ? (unsigned)((((r0 + r) * g.W + w) * g.C + c) * (int)sizeof(T)) : ACC_OOB;
+      bufq_st<2>(rz, off, make_float4(o[0], o[1], o[2], o[3]), (T*)nullptr);
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          win[0][dx][j] = win[1][dx][j];
+          win[1][dx][j] = win[2][dx][j];
+        }
     }
     if (more) {
       __syncthreads();  // every thread is done with rows r0-1 .. r0+CR-2
       dw_park_rows<TCQ, G::NK8>(tile, nx, g, r0 + 9, G::N8, w0, hbeg, pro, ps, pb, act);
       __syncthreads();
     }
-    if (bnb) {
+    if (BNB) {
 #pragma unroll
       for (int r = 0; r < CR; ++r) zcur[r] = znext[r];
     }
@@ -648,8 +666,9 @@ dw3x3_tile_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dz,
 }
 
 // tile-kernel selection: 0 = none (register-window kernel), else TCQ
-static int dw_tile_tcq(int W, int C) {
+static int dw_tile_tcq(int H, int W, int C) {
   if (C % 32) return 0;
+  if ((long)H * W * C * 4 >= (1L << 31)) return 0;  // one image per 32-bit buffer descriptor
   int CQ = C / 4;
   if (W <= 16 && CQ % 16 == 0) return 16;
   return 8;
@@ -741,7 +760,7 @@ static DwGeom dw_geom(int B, int H, int W, int C, int V, dim3* grid) {
 
 extern "C" int accunet_dw3x3_rows(int B, int H, int W, int C) {
   dim3 grid;
-  int tcq = dw_tile_tcq(W, C);
+  int tcq = dw_tile_tcq(H, W, C);
   if (tcq) dw_tgeom(B, H, W, C, tcq, &grid, dw_rch_max());
   else dw_geom(B, H, W, C, (C % 4 == 0) ? 4 : 1, &grid);
   return (int)grid.x;
@@ -754,7 +773,7 @@ extern "C" int accunet_dw3x3_fwd(const void* x, const float* wt, const float* bi
   hipStream_t s = (hipStream_t)stream;
   if (bz && (!bst || !stats)) return ACC_EBADARG;
   dim3 grid;
-  int tcq = dw_tile_tcq(W, C);
+  int tcq = dw_tile_tcq(H, W, C);
   if (tcq) {
     DwTGeom tg = dw_tgeom(B, H, W, C, tcq, &grid, dw_rch_max());
     // non-temporal loads only for inputs above the Infinity Cache (bytes as stored)
@@ -763,25 +782,31 @@ extern "C" int accunet_dw3x3_fwd(const void* x, const float* wt, const float* bi
       tg.cgf = (int)grid.y;
       grid = dim3(grid.x * grid.y, 1);
     }
+    // both fixed-function choices (channel-group width, nt loads) are template arguments
+    auto launch = [&](auto tag, auto tcqc, auto bnbc, auto auxc) {
+      using T = decltype(tag);
+      hipLaunchKernelGGL((dw3x3_tile_fwd_kernel<decltype(tcqc)::value, decltype(bnbc)::value,
+                                                decltype(auxc)::value, T>),
+                         grid, dim3(256), 0, s, (const T*)x, wt, bias, sc, sh, act, flip, (T*)z,
+                         stats, tg, (const T*)bz, bst, bact);
+    };
+    using I16 = std::integral_constant<int, 16>;
+    using I8 = std::integral_constant<int, 8>;
+    using BT = std::integral_constant<bool, true>;
+    using BF = std::integral_constant<bool, false>;
+    using A2 = std::integral_constant<int, 2>;
+    using A0 = std::integral_constant<int, 0>;
     if (with_dt(dt, [&](auto tag) {
-          using T = decltype(tag);
-          const T* xx = (const T*)x;
-          const T* zb = (const T*)bz;
-          T* zz = (T*)z;
-          if (bz) {
-            if (tcq == 16)
-              hipLaunchKernelGGL((dw3x3_tile_fwd_kernel<16, true, T>), grid, dim3(256), 0, s, xx, wt,
-                                 bias, sc, sh, act, flip, zz, stats, tg, zb, bst, bact);
-            else
-              hipLaunchKernelGGL((dw3x3_tile_fwd_kernel<8, true, T>), grid, dim3(256), 0, s, xx, wt,
-                                 bias, sc, sh, act, flip, zz, stats, tg, zb, bst, bact);
-          } else if (tcq == 16) {
-            hipLaunchKernelGGL((dw3x3_tile_fwd_kernel<16, false, T>), grid, dim3(256), 0, s, xx, wt,
-                               bias, sc, sh, act, flip, zz, stats, tg, zb, bst, bact);
-          } else {
-            hipLaunchKernelGGL((dw3x3_tile_fwd_kernel<8, false, T>), grid, dim3(256), 0, s, xx, wt,
-                               bias, sc, sh, act, flip, zz, stats, tg, zb, bst, bact);
-          }
+          auto by_aux = [&](auto tc, auto bn) {
+            if (tg.ntl) launch(tag, tc, bn, A2{});
+            else launch(tag, tc, bn, A0{});
+          };
+          auto by_bnb = [&](auto tc) {
+            if (bz) by_aux(tc, BT{});
+            else by_aux(tc, BF{});
+          };
+          if (tcq == 16) by_bnb(I16{});
+          else by_bnb(I8{});
         }))
       return ACC_EBADARG;
     return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
@@ -803,7 +828,7 @@ extern "C" int accunet_dw3x3_fwd(const void* x, const float* wt, const float* bi
 
 static int dw_wgrad_rows(int B, int H, int W, int C) {
   dim3 grid;
-  int tcq = dw_tile_tcq(W, C);
+  int tcq = dw_tile_tcq(H, W, C);
   if (tcq) dw_tgeom(B, H, W, C, tcq, &grid);
   else dw_geom(B, H, W, C, (C % 4 == 0) ? 4 : 1, &grid);
   return (int)grid.x;
@@ -822,7 +847,7 @@ extern "C" int accunet_dw3x3_wgrad(const void* x, const void* dz, const float* s
   hipStream_t s = (hipStream_t)stream;
   int V = (C % 4 == 0) ? 4 : 1;
   dim3 grid;
-  int tcq = dw_tile_tcq(W, C);
+  int tcq = dw_tile_tcq(H, W, C);
   DwTGeom tg;
   DwGeom g;
   if (tcq) tg = dw_tgeom(B, H, W, C, tcq, &grid);

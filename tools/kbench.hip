@@ -9,6 +9,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <vector>
+#include <algorithm>
 
 #include "../include/accunet.h"
 
@@ -77,19 +78,24 @@ static float* dalloc(size_t n, float s = 1.f) {
   return p;
 }
 
+// median per-launch time (an event pair around every launch): robust to the clock
+// ramp / power give-back that makes back-to-back means drift (MI355X DVFS)
 template <class F>
 static double timeit(F f, int iters) {
   f();
-  hipEvent_t a, b;
-  CK(hipEventCreate(&a));
-  CK(hipEventCreate(&b));
-  CK(hipEventRecord(a, 0));
-  for (int i = 0; i < iters; ++i) f();
-  CK(hipEventRecord(b, 0));
-  CK(hipEventSynchronize(b));
-  float ms;
-  CK(hipEventElapsedTime(&ms, a, b));
-  return 1000.0 * ms / iters;
+  std::vector<hipEvent_t> ev(2 * iters);
+  for (auto& e : ev) CK(hipEventCreate(&e));
+  for (int i = 0; i < iters; ++i) {
+    CK(hipEventRecord(ev[2 * i], 0));
+    f();
+    CK(hipEventRecord(ev[2 * i + 1], 0));
+  }
+  CK(hipEventSynchronize(ev.back()));
+  std::vector<float> t(iters);
+  for (int i = 0; i < iters; ++i) CK(hipEventElapsedTime(&t[i], ev[2 * i], ev[2 * i + 1]));
+  for (auto& e : ev) CK(hipEventDestroy(e));
+  std::sort(t.begin(), t.end());
+  return 1000.0 * t[iters / 2];
 }
 
 static void report(const char* name, double us, double bytes) {
@@ -127,7 +133,7 @@ int main(int argc, char** argv) {
            timeit([&] { hipLaunchKernelGGL(copy4_x4_nt, dim3((n4 + 1023) / 1024), dim3(256), 0, 0,
                                            (const float4*)x, (float4*)z, n4); }, iters), bytes);
     report("K1 dw3x3_fwd 16x256x256x96 pro+stats",
-           timeit([&] { CA(accunet_dw3x3_fwd(x, wt, bi, sc, sh, 1, 0, z, st, B, H, W, C, nullptr, nullptr, 0, 0)); }, iters),
+           timeit([&] { CA(accunet_dw3x3_fwd(x, wt, bi, sc, sh, 1, 0, z, st, B, H, W, C, nullptr, nullptr, 0, ACC_F32, 0)); }, iters),
            bytes);
     {  // bit pattern checksum of z and the stats partials (compare kernel variants)
       std::vector<unsigned> hz(n);
@@ -139,14 +145,20 @@ int main(int argc, char** argv) {
       for (unsigned long long v : hs) hh = (hh ^ v) * 1099511628211ull;
       printf("K1 checksum %016llx\n", hh);
     }
+    report("K1 bf16 dw3x3_fwd 16x256x256x96 pro+stats",
+           timeit([&] { CA(accunet_dw3x3_fwd(x, wt, bi, sc, sh, 1, 0, z, st, B, H, W, C, nullptr, nullptr, 0, ACC_BF16, 0)); }, iters),
+           bytes / 2);
+    report("copy float4 (same bytes as bf16 K1)",
+           timeit([&] { hipLaunchKernelGGL(copy4, dim3(8192), dim3(256), 0, 0, (const float4*)x,
+                                           (float4*)z, (long)(n / 8)); }, iters), bytes / 2);
     report("K1 dw3x3_fwd flip (dgrad) no pro/stats",
-           timeit([&] { CA(accunet_dw3x3_fwd(x, wt, nullptr, nullptr, nullptr, 0, 1, z, nullptr, B, H, W, C, nullptr, nullptr, 0, 0)); }, iters),
+           timeit([&] { CA(accunet_dw3x3_fwd(x, wt, nullptr, nullptr, nullptr, 0, 1, z, nullptr, B, H, W, C, nullptr, nullptr, 0, ACC_F32, 0)); }, iters),
            bytes);
     size_t wse = accunet_dw3x3_wgrad_ws(B, H, W, C);
     float* ws = dalloc(wse);
     float *dw = dalloc(9 * C), *db = dalloc(C);
     report("K1' dw3x3_wgrad 16x256x256x96 pro",
-           timeit([&] { CA(accunet_dw3x3_wgrad(x, z, sc, sh, 1, dw, db, B, H, W, C, ws, wse, 0)); }, iters),
+           timeit([&] { CA(accunet_dw3x3_wgrad(x, z, sc, sh, 1, dw, db, B, H, W, C, ws, wse, ACC_F32, 0)); }, iters),
            bytes);
     CK(hipFree(x)); CK(hipFree(z)); CK(hipFree(ws)); CK(hipFree(st));
   }
@@ -161,7 +173,7 @@ int main(int argc, char** argv) {
       CK(hipMalloc(&st, (size_t)rows * 2 * C * sizeof(double)));
       char name[96];
       snprintf(name, sizeof name, "K1 sweep 16x256x256x%d", C);
-      report(name, timeit([&] { CA(accunet_dw3x3_fwd(x, wt, bi, sc, sh, 1, 0, z, st, B, H, W, C, nullptr, nullptr, 0, 0)); }, iters),
+      report(name, timeit([&] { CA(accunet_dw3x3_fwd(x, wt, bi, sc, sh, 1, 0, z, st, B, H, W, C, nullptr, nullptr, 0, ACC_F32, 0)); }, iters),
              2.0 * 4 * n);
       CK(hipFree(x)); CK(hipFree(z)); CK(hipFree(st)); CK(hipFree(wt)); CK(hipFree(bi));
       CK(hipFree(sc)); CK(hipFree(sh));
@@ -191,22 +203,22 @@ int main(int argc, char** argv) {
       CK(hipMalloc(&st2, (size_t)rows * 2 * C * sizeof(double)));
       report("affine_act+stats 16x65536x32 (1 rd + 1 wr)",
              timeit([&] { CA(accunet_affine_act_fwd(z, sc, sh, 1, nullptr, out, (long)B * HW, C, st2,
-                                                    nullptr, 0)); }, iters), bytes);
+                                                    nullptr, ACC_F32, 0)); }, iters), bytes);
       float* stb = dalloc(4 * C, 1.f);
       size_t bws = accunet_bn_bwd_ws_elems((long)B * HW, C);
       float* bw = dalloc(bws);
       report("bn_bwd 16x65536x32 (rd 2 + rd 2 + wr 1)",
              timeit([&] { CA(accunet_bn_bwd(z, dout, stb, g, 1, 1, (long)B * HW, C, da, 0, dg, dbe,
-                                            nullptr, bw, bws, 0)); }, iters),
+                                            nullptr, bw, bws, ACC_F32, 0)); }, iters),
              5.0 * 4 * n);
     }
     report("K3 se_fwd 16x65536x32 pro",
            timeit([&] { CA(accunet_se_fwd(z, sc, sh, 1, B, HW, C, Cr, w1, b1, w2, b2, g, be, rm, rv,
-                                          nullptr, 0.1f, 1e-5f, 1, out, save, nullptr, ws, wse, 0)); }, iters),
+                                          nullptr, 0.1f, 1e-5f, 1, out, save, nullptr, ws, wse, ACC_F32, 0)); }, iters),
            bytes);
     report("K3' se_bwd 16x65536x32 pro (2 rd + 1 rd/wr)",
            timeit([&] { CA(accunet_se_bwd(z, dout, sc, sh, 1, B, HW, C, Cr, w1, w2, g, 1, save, da,
-                                          dw1, db1, dw2, db2, dg, dbe, ws, wse, 0)); }, iters),
+                                          dw1, db1, dw2, db2, dg, dbe, ws, wse, ACC_F32, 0)); }, iters),
            4.0 * 4 * n);
   }
   CK(hipDeviceSynchronize());
