@@ -12,7 +12,9 @@ import os
 from ctypes import POINTER, Structure, c_double, c_float, c_int, c_longlong, c_size_t, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libaccunet_hip.so")
+# ACCUNET_LIB_OVERRIDE: A/B experiments against another build of the same library
+# (tools/*_ab.sh); unset, the in-tree build is the only one ever loaded
+LIB_PATH = os.environ.get("ACCUNET_LIB_OVERRIDE") or os.path.join(_HERE, "libaccunet_hip.so")
 
 # mirrors include/accunet.h enums
 AMODE_ROW, AMODE_COL, AMODE_SHIFT3 = 0, 1, 2

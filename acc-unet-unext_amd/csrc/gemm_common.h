@@ -94,8 +94,8 @@ constexpr int gemm_epi_floats() {
 // same for v_mfma_f32_32x32x2_f32 and v_mfma_f32_32x32x16_bf16). smem: >=
 // gemm_epi_floats<WM,TM,TN>() floats, free when called.
 template <typename TC, int EPI, int WM, int TM, int TN>
-ACC_DEV void gemm_epilogue(const GemmParams& p, floatx16 (&acc)[TM][TN], float* smem, int m0,
-                           int n0) {
+ACC_DEV void gemm_epilogue_generic(const GemmParams& p, floatx16 (&acc)[TM][TN], float* smem,
+                                   int m0, int n0) {
   constexpr int WN = 4 / WM;
   constexpr int BN = WN * TN * 32;
   const int tid = threadIdx.x;
@@ -355,4 +355,257 @@ ACC_DEV void gemm_epilogue(const GemmParams& p, floatx16 (&acc)[TM][TN], float* 
       }
     }
   }
+}
+
+// pixel (b, h, w) of GEMM row m on the p.H x p.W grid
+ACC_DEV void gemm_pix(const GemmParams& p, int m, int& b, int& h, int& w) {
+  const uint32_t q = fdiv((uint32_t)m, p.fW);
+  w = m - (int)q * p.W;
+  const uint32_t bb = fdiv(q, p.fH);
+  h = (int)(q - bb * p.H);
+  b = (int)bb;
+}
+// index of the pixel that covers (b, h, w) on the grid downsampled by 2^lg
+ACC_DEV long gemm_pix_lg(const GemmParams& p, int b, int h, int w, int lg) {
+  return ((long)b * (p.H >> lg) + (h >> lg)) * (p.W >> lg) + (w >> lg);
+}
+
+// The epilogue operands of one C row quad, raw as loaded (unused members are dead)
+template <typename TC>
+struct EpiRow {
+  typedef typename QuadRaw<TC>::type R;
+  R zb;                  // EPI_BNB: pre-BN input
+  R av2, mx2, av4, mx4;  // EPI_PYR: pyramid gradients
+  unsigned k2, k4;       // EPI_PYR: argmax codes
+  R up[3];               // EPI_UPS: nearest-upsampled addends
+};
+
+// Vector epilogue (p.evec, no split-K): the same arithmetic as gemm_epilogue_generic,
+// with every global access a branch-free buffer load / store (lanes and rows that
+// are masked off use out-of-range offsets; absent operands get zero-size
+// descriptors). The exact instruction count lets the compiler wait for one chunk's
+// operand loads alone, and the loads of chunk t+1 are issued before chunk t is
+// stored, so neither the C stores nor the next chunk's gathers are ever drained
+// by a vmcnt(0) (the generic path pays about one L2/HBM round trip per chunk).
+// Descriptors cover one block's rows (wave-uniform bases from m0), so tensors of
+// any size stay within 32-bit offsets.
+template <typename TC, int EPI, int WM, int TM, int TN>
+ACC_DEV void gemm_epilogue_vec(const GemmParams& p, floatx16 (&acc)[TM][TN], float* smem, int m0,
+                               int n0) {
+  constexpr int WN = 4 / WM;
+  constexpr int BN = WN * TN * 32;
+  constexpr int BM = WM * TM * 32;
+  constexpr int CQN = BN / 4;
+  constexpr int RPP = GEMM_THREADS / CQN;
+  constexpr int PR = WM * 32;
+  constexpr int SC = BN + 4;
+  constexpr int NR = PR / RPP;
+  constexpr bool LOADS = (EPI & (EPI_BNB | EPI_PYR | EPI_UPS)) != 0;
+  constexpr int EC = LOADS ? 2 : NR;  // rows per chunk; two chunks of operands in flight
+  constexpr int NCH = NR / EC;
+  constexpr int NT = TM * NCH;        // chunks of the whole tile
+  constexpr int SZ = (int)sizeof(TC);
+  static_assert(NR % EC == 0, "chunks must split the pass rows");
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave % WM;
+  const int wn = wave / WM;
+  const int l31 = lane & 31;
+  const int lh = lane >> 5;
+  const int M = p.M, N = p.N, ldc = p.ldc;
+  const int cq = tid % CQN, rr0 = tid / CQN;
+  const int nq = n0 + 4 * cq;
+  const int mlast = min(M, m0 + BM) - 1;
+  const unsigned rows = (unsigned)(mlast - m0 + 1);
+  const __amdgpu_buffer_rsrc_t rC = acc_rsrc((const TC*)p.C + (size_t)m0 * ldc, rows * ldc * SZ);
+  float bq[4] = {0.f, 0.f, 0.f, 0.f};
+  if (p.bias) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bq[e] = (nq + e < N) ? p.bias[nq + e] : 0.f;
+  }
+  // ---- operand descriptors (block-local bases) -----------------------------
+  const bool bnb = (EPI & EPI_BNB) && p.stats && p.bz;
+  __amdgpu_buffer_rsrc_t rZ = rC, rP2 = rC, rK2 = rC, rP4 = rC, rK4 = rC, rU[3] = {rC, rC, rC};
+  long q2a = 0, q4a = 0, ua[3] = {0, 0, 0};
+  if (EPI & EPI_BNB)
+    rZ = acc_rsrc(bnb ? (const TC*)p.bz + (size_t)m0 * ldc : (const TC*)p.C,
+                  bnb ? rows * ldc * SZ : 0u);
+  if (EPI & (EPI_PYR | EPI_UPS)) {
+    int ba, ha, wa, bb, hb, wb;
+    gemm_pix(p, m0, ba, ha, wa);
+    gemm_pix(p, mlast, bb, hb, wb);
+    if (EPI & EPI_PYR) {
+      const bool on2 = p.pd2 != nullptr, on4 = on2 && p.pd4 != nullptr;
+      q2a = gemm_pix_lg(p, ba, ha, wa, 1);
+      q4a = gemm_pix_lg(p, ba, ha, wa, 2);
+      const unsigned n2 = (unsigned)(gemm_pix_lg(p, bb, hb, wb, 1) - q2a + 1);
+      const unsigned n4 = (unsigned)(gemm_pix_lg(p, bb, hb, wb, 2) - q4a + 1);
+      rP2 = acc_rsrc(on2 ? (const TC*)p.pd2 + q2a * 2 * N : (const TC*)p.C, on2 ? n2 * 2 * N * SZ : 0u);
+      rK2 = acc_rsrc(on2 ? p.mk2 + q2a * N : p.mk2, on2 ? n2 * N : 0u);
+      rP4 = acc_rsrc(on4 ? (const TC*)p.pd4 + q4a * 2 * N : (const TC*)p.C, on4 ? n4 * 2 * N * SZ : 0u);
+      rK4 = acc_rsrc(on4 ? p.mk4 + q4a * N : p.mk2, on4 ? n4 * N : 0u);
+    }
+    if (EPI & EPI_UPS) {
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {
+        const bool on = u < p.nup;
+        const int lg = on ? p.uplog[u] : 0;
+        ua[u] = gemm_pix_lg(p, ba, ha, wa, lg);
+        const unsigned nu = (unsigned)(gemm_pix_lg(p, bb, hb, wb, lg) - ua[u] + 1);
+        rU[u] = acc_rsrc(on ? (const TC*)p.up[u] + ua[u] * p.upld[u] : (const TC*)p.C,
+                         on ? nu * p.upld[u] * SZ : 0u);
+      }
+    }
+  }
+  float bmu[4] = {0.f, 0.f, 0.f, 0.f}, bsc4[4] = {0.f, 0.f, 0.f, 0.f}, bsh4[4] = {0.f, 0.f, 0.f, 0.f};
+  if (bnb) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int n = nq + e < N ? nq + e : N - 1;
+      bmu[e] = p.bst[BN_MEAN * N + n];
+      bsc4[e] = p.bst[BN_SCALE * N + n];
+      bsh4[e] = p.bst[BN_SHIFT * N + n];
+    }
+  }
+  // rows of chunk t (pass t / NCH): C row and in-range flag of its row c
+  auto row_of = [&](int t, int c, int& m) {
+    const int i = t / NCH, r = (t % NCH) * EC + c;
+    const int rr = rr0 + r * RPP;
+    m = m0 + (rr >> 5) * TM * 32 + i * 32 + (rr & 31);
+    return m < M && nq < N;
+  };
+  auto issue = [&](EpiRow<TC> (&L)[EC], int t) {
+#pragma unroll
+    for (int c = 0; c < EC; ++c) {
+      int m;
+      const bool ok = row_of(t, c, m);
+      if (EPI & EPI_BNB)
+        L[c].zb = bufq_ld<0>(rZ, ok ? (unsigned)(((m - m0) * ldc + nq) * SZ) : ACC_OOB, (const TC*)nullptr);
+      if (EPI & (EPI_PYR | EPI_UPS)) {
+        int b, h, w;
+        gemm_pix(p, ok ? m : m0, b, h, w);
+        if (EPI & EPI_PYR) {
+          const unsigned i2 = (unsigned)(gemm_pix_lg(p, b, h, w, 1) - q2a);
+          const unsigned i4 = (unsigned)(gemm_pix_lg(p, b, h, w, 2) - q4a);
+          const unsigned o2 = ok ? (i2 * 2 * N + nq) * SZ : ACC_OOB;
+          const unsigned o4 = ok ? (i4 * 2 * N + nq) * SZ : ACC_OOB;
+          L[c].av2 = bufq_ld<0>(rP2, o2, (const TC*)nullptr);
+          L[c].mx2 = bufq_ld<0>(rP2, o2 + N * SZ, (const TC*)nullptr);
+          L[c].k2 = __builtin_amdgcn_raw_buffer_load_b32(rK2, ok ? i2 * N + nq : ACC_OOB, 0, 0);
+          L[c].av4 = bufq_ld<0>(rP4, o4, (const TC*)nullptr);
+          L[c].mx4 = bufq_ld<0>(rP4, o4 + N * SZ, (const TC*)nullptr);
+          L[c].k4 = __builtin_amdgcn_raw_buffer_load_b32(rK4, ok ? i4 * N + nq : ACC_OOB, 0, 0);
+        }
+        if (EPI & EPI_UPS) {
+#pragma unroll
+          for (int u = 0; u < 3; ++u) {
+            const int lg = u < p.nup ? p.uplog[u] : 0;
+            const unsigned iu = (unsigned)(gemm_pix_lg(p, b, h, w, lg) - ua[u]);
+            L[c].up[u] = bufq_ld<0>(rU[u], ok ? (iu * p.upld[u] + nq) * SZ : ACC_OOB,
+                                    (const TC*)nullptr);
+          }
+        }
+      }
+    }
+  };
+  double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+  EpiRow<TC> L[2][EC];
+  if (LOADS) issue(L[0], 0);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int i = t / NCH;
+    if (t % NCH == 0) {
+      __syncthreads();  // LDS free (main loop / previous pass)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          smem[(wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * SC + wn * TN * 32 + j * 32 + l31] =
+              acc[i][j][r];
+      __syncthreads();
+    }
+    if (LOADS && t + 1 < NT) issue(L[(t + 1) & 1], t + 1);
+    EpiRow<TC>(&R)[EC] = L[t & 1];
+#pragma unroll
+    for (int c = 0; c < EC; ++c) {
+      int m;
+      const bool ok = row_of(t, c, m);
+      const int rr = rr0 + ((t % NCH) * EC + c) * RPP;
+      const float4 a4 = *reinterpret_cast<const float4*>(smem + rr * SC + 4 * cq);
+      float v[4] = {a4.x + bq[0], a4.y + bq[1], a4.z + bq[2], a4.w + bq[3]};
+      if ((EPI & EPI_PYR) && p.pd2) {
+        {
+          int b, h, w;
+          gemm_pix(p, ok ? m : m0, b, h, w);
+          const unsigned pos2 = (h & 1) * 2 + (w & 1), pos4 = (h & 3) * 4 + (w & 3);
+          const float4 av2 = q2f(R[c].av2), mx2 = q2f(R[c].mx2);
+          const float4 av4 = q2f(R[c].av4), mx4 = q2f(R[c].mx4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float g = f4get(av2, e) * 0.25f;
+            if (((R[c].k2 >> (8 * e)) & 255u) == pos2) g += f4get(mx2, e);
+            if (p.pd4) {
+              g += f4get(av4, e) * (1.f / 16.f);
+              if (((R[c].k4 >> (8 * e)) & 255u) == pos4) g += f4get(mx4, e);
+            }
+            v[e] += g;
+          }
+        }
+      } else if (EPI & EPI_UPS) {
+#pragma unroll
+        for (int u = 0; u < 3; ++u)
+          if (u < p.nup) {
+            const float4 a = q2f(R[c].up[u]);
+            v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
+          }
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = rnd<TC>(v[e]);  // statistics of the stored values
+      if (ok) {
+        if (bnb) {
+          const float4 z4 = q2f(R[c].zb);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float z = f4get(z4, e);
+            float g = v[e];
+            if (p.bact == ACT_LRELU) g *= lrelu_d(z * bsc4[e] + bsh4[e]);
+            s1[e] += g;
+            s2[e] += (double)g * ((double)z - bmu[e]);
+          }
+        } else if ((EPI & EPI_STATS) && p.stats) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            s1[e] += v[e];
+            s2[e] += (double)v[e] * v[e];
+          }
+        }
+      }
+      bufq_st<2>(rC, ok ? (unsigned)(((m - m0) * ldc + nq) * SZ) : ACC_OOB,
+                 make_float4(v[0], v[1], v[2], v[3]), (TC*)nullptr);
+    }
+  }
+  if ((EPI & (EPI_STATS | EPI_BNB)) && p.stats) {
+    __syncthreads();  // LDS reused as the reduction buffer
+    double vv[8] = {s1[0], s1[1], s1[2], s1[3], s2[0], s2[1], s2[2], s2[3]};
+    if (block_slot_reduce<CQN, 8, double>(vv, reinterpret_cast<double*>(smem))) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int n = n0 + 4 * tid + e;
+        if (n < N) {
+          p.stats[((size_t)blockIdx.x * 2 + 0) * N + n] = vv[e];
+          p.stats[((size_t)blockIdx.x * 2 + 1) * N + n] = vv[4 + e];
+        }
+      }
+    }
+  }
+}
+
+template <typename TC, int EPI, int WM, int TM, int TN>
+ACC_DEV void gemm_epilogue(const GemmParams& p, floatx16 (&acc)[TM][TN], float* smem, int m0,
+                           int n0) {
+  if (p.evec && gridDim.z == 1)
+    gemm_epilogue_vec<TC, EPI, WM, TM, TN>(p, acc, smem, m0, n0);
+  else
+    gemm_epilogue_generic<TC, EPI, WM, TM, TN>(p, acc, smem, m0, n0);
 }
