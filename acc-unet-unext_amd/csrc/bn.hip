@@ -110,6 +110,198 @@ size_t accunet_partials_ws_elems(int R, int Wd) {
 }
 
 // ---------------------------------------------------------------------------
+// reduce_finish: the whole partial-row reduction and its finish in ONE launch
+// (it replaces the colreduce stages + finish kernel: 2-4 launches of a few us each
+// per BatchNorm). Grid (nchunk, column blocks of 64). Block (k, y) sums rows
+// [k*rpc, (k+1)*rpc) of its 64 columns in a fixed order (fp64) into chunk row k;
+// the last block of column block y to arrive (ticket counter, agent-scope release /
+// acquire: MI355X guide section 6, Guideline 16) adds the nchunk chunk rows in index
+// order and runs the finish. The chunking depends on R only, so the result is
+// bitwise reproducible. Paired kinds (BatchNorm) map thread column cl < 32 to the
+// first moment of channel 32y+cl and cl >= 32 to its second moment (column C+ch).
+// The tickets live in a zero-initialised device array; every last arriver resets
+// its word, so consecutive launches on a stream (and graph replays) reuse it.
+// ---------------------------------------------------------------------------
+#define FIN_MAX_CB 16384  // column blocks (ncols <= 262144: dw wgrad of cnv72 has 10 x 4352)
+__device__ unsigned g_fin_tickets[FIN_MAX_CB];
+
+ACC_DEV void fin_column(const FinishArgs& fa, int col, double tot) {
+  switch (fa.kind) {
+    case FIN_SUM_F: fa.out_f[col] = (float)tot; break;
+    case FIN_SUM_D: fa.out_d[col] = tot; break;
+    case FIN_DW:  // [10][C] sums -> dW[c][tap] (torch layout [C][1][3][3]) and db[c]
+      if (col < 9 * fa.C) fa.out_f[(col % fa.C) * 9 + col / fa.C] = (float)tot;
+      else if (fa.out2) fa.out2[col - 9 * fa.C] = (float)tot;
+      break;
+    case FIN_HEAD:
+      if (col < fa.C) fa.out_f[col] = (float)tot;
+      else if (col == fa.C) fa.out2[0] = (float)tot;
+      break;
+    default: break;
+  }
+}
+
+// BatchNorm forward finish (training): see bn_finalize_kernel for the eval form
+ACC_DEV void fin_bn_fwd(const FinishArgs& fa, int c, double s1, double s2) {
+  const int C = fa.ncols;
+  const double m = s1 / fa.count;
+  double v = s2 / fa.count - m * m;
+  if (v < 0.0) v = 0.0;
+  const float mean = (float)m, var = (float)v;
+  if (fa.rmean) fa.rmean[c] = (1.f - fa.momentum) * fa.rmean[c] + fa.momentum * mean;
+  if (fa.rvar) {
+    const double unb = fa.count > 1.0 ? v * fa.count / (fa.count - 1.0) : v;
+    fa.rvar[c] = (1.f - fa.momentum) * fa.rvar[c] + fa.momentum * (float)unb;
+  }
+  const float rstd = 1.0f / sqrtf(var + fa.eps);
+  const float ga = fa.gamma ? fa.gamma[c] : 1.f;
+  const float be = fa.beta ? fa.beta[c] : 0.f;
+  const float sc = ga * rstd;
+  float* st = fa.out_f;
+  st[BN_MEAN * C + c] = mean;
+  st[BN_RSTD * C + c] = rstd;
+  st[BN_SCALE * C + c] = sc;
+  st[BN_SHIFT * C + c] = be - mean * sc;
+}
+
+// BatchNorm backward finish: (sum g, sum g*xhat | g*(x-mean)) -> dgamma, dbeta, coef
+ACC_DEV void fin_bn_bwd(const FinishArgs& fa, int c, double s1, double s2) {
+  const int C = fa.ncols;
+  const float* st = fa.st;
+  if (fa.xc_form) s2 *= (double)st[BN_RSTD * C + c];
+  if (fa.out2) fa.out2[c] = (float)s2;
+  if (fa.out3) fa.out3[c] = (float)s1;
+  const float ga = fa.gamma ? fa.gamma[c] : 1.f;
+  const float rstd = st[BN_RSTD * C + c];
+  const float k1 = ga * rstd;
+  float k2 = 0.f, k3 = 0.f;
+  if (fa.training) {
+    // dx = k1*(g - mean(g) - xhat*mean(g*xhat)) = k1*g + k2*(x - mean) + k3
+    const float mg = (float)(s1 / fa.count), mgx = (float)(s2 / fa.count);
+    k2 = -k1 * rstd * mgx;
+    k3 = -k1 * mg;
+  }
+  fa.out_f[c] = k1;
+  fa.out_f[C + c] = k2;
+  fa.out_f[2 * C + c] = k3;
+}
+
+// 256 threads = FIN_COLS columns x FIN_GROUPS row groups: with 8 loads in flight per
+// thread a block covers FIN_GROUPS*8 = 128 rows per memory round trip, which is
+// exactly one chunk, and the last arriver's pass over the chunk rows is one more.
+#define FIN_COLS 16
+#define FIN_GROUPS 16
+template <typename TP>
+__global__ void __launch_bounds__(256)
+reduce_finish_kernel(const TP* __restrict__ part, int R, int stride, int rpc, double* chunks,
+                     FinishArgs fa) {
+  __shared__ double red[FIN_GROUPS][FIN_COLS];
+  __shared__ int last;
+  const int cl = threadIdx.x % FIN_COLS, g = threadIdx.x / FIN_COLS;
+  const bool paired = fa.kind == FIN_BN_FWD || fa.kind == FIN_BN_BWD;
+  constexpr int HC = FIN_COLS / 2;
+  int col;
+  bool valid;
+  if (paired) {
+    const int ch = blockIdx.y * HC + (cl % HC);
+    valid = ch < fa.ncols;
+    col = cl < HC ? ch : fa.ncols + ch;
+  } else {
+    col = blockIdx.y * FIN_COLS + cl;
+    valid = col < fa.ncols;
+  }
+  auto combine = [&](double v) {  // fixed-order sum over the row groups
+    red[g][cl] = v;
+    __syncthreads();
+    double t = 0.0;
+#pragma unroll
+    for (int k = 0; k < FIN_GROUPS; ++k) t += red[k][cl];
+    __syncthreads();
+    return t;
+  };
+  const int nchunk = gridDim.x;
+  const int r0 = blockIdx.x * rpc, r1 = min(R, r0 + rpc);
+  double s[1] = {0.0};
+  if (valid)
+    ordered_strided_sum<8>(s, r0 + g, r1, FIN_GROUPS, [&](int r, double (&v)[1]) {
+      v[0] = (double)part[(long)r * stride + col];
+    });
+  double tot = combine(s[0]);
+  if (nchunk > 1) {
+    // hand-off without fences: the chunk totals are stored write-through (agent-scope
+    // atomic store = sc1) and drained before the ticket, and the last arriver reads
+    // them with sc1 loads (L1 bypass), so neither an L2 write-back (release) nor an L1
+    // invalidate (acquire) is needed (MI355X guide section 6, Guideline 16, R1/R2)
+    typedef __attribute__((address_space(1))) unsigned long long gu64;
+    if (g == 0 && valid)
+      __hip_atomic_store((gu64*)(chunks + (long)blockIdx.x * stride + col),
+                         (unsigned long long)__double_as_longlong(tot), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      auto* t = (__attribute__((address_space(1))) unsigned*)(g_fin_tickets + blockIdx.y);
+      const unsigned k = __hip_atomic_fetch_add(t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int me_last = k == (unsigned)(nchunk - 1);
+      if (me_last) __hip_atomic_store(t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = me_last;
+    }
+    __syncthreads();
+    if (!last) return;
+    double c1[1] = {0.0};
+    if (valid)
+      ordered_strided_sum<8>(c1, g, nchunk, FIN_GROUPS, [&](int k, double (&v)[1]) {
+        v[0] = __longlong_as_double((long long)__hip_atomic_load(
+            (gu64*)(chunks + (long)k * stride + col), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      });
+    tot = combine(c1[0]);
+  }
+  if (paired) {
+    if (g == 0) red[0][cl] = tot;
+    __syncthreads();
+    if (g == 0 && cl < HC && valid) {
+      const int ch = blockIdx.y * HC + cl;
+      if (fa.kind == FIN_BN_FWD) {
+        fin_bn_fwd(fa, ch, red[0][cl], red[0][cl + HC]);
+        if (fa.nbt && ch == 0) *fa.nbt += 1;  // num_batches_tracked
+      } else {
+        fin_bn_bwd(fa, ch, red[0][cl], red[0][cl + HC]);
+      }
+    }
+  } else if (g == 0 && valid) {
+    fin_column(fa, col, tot);
+  }
+}
+
+static int fin_rows_per_chunk(int) { return FIN_GROUPS * 8; }
+
+size_t reduce_finish_ws(int R, int stride) {
+  const int nchunk = ceil_div(R, fin_rows_per_chunk(R));
+  return nchunk > 1 ? (size_t)nchunk * stride : 0;
+}
+
+int reduce_finish(const void* part, bool part_f64, int R, int stride, double* chunks,
+                  const FinishArgs& fa, hipStream_t s) {
+  const bool paired = fa.kind == FIN_BN_FWD || fa.kind == FIN_BN_BWD;
+  const int rpc = fin_rows_per_chunk(R);
+  const int nchunk = max(1, ceil_div(R, rpc));
+  const int ncb = paired ? ceil_div(fa.ncols, FIN_COLS / 2) : ceil_div(fa.ncols, FIN_COLS);
+  // (float workspaces may hand over a 4-byte aligned scratch: the partials workspace
+  // sizes keep two spare rows, so rounding up to 8 bytes stays inside it)
+  chunks = reinterpret_cast<double*>(((uintptr_t)chunks + 7) & ~(uintptr_t)7);
+  if (ncb > FIN_MAX_CB || (nchunk > 1 && !chunks)) return ACC_EBADARG;
+  const int wd = paired ? 2 * fa.ncols : fa.ncols;
+  if (wd > stride) return ACC_EBADARG;
+  if (part_f64)
+    hipLaunchKernelGGL(reduce_finish_kernel<double>, dim3(nchunk, ncb), dim3(256), 0, s,
+                       (const double*)part, R, stride, rpc, chunks, fa);
+  else
+    hipLaunchKernelGGL(reduce_finish_kernel<float>, dim3(nchunk, ncb), dim3(256), 0, s,
+                       (const float*)part, R, stride, rpc, chunks, fa);
+  return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+}
+
+// ---------------------------------------------------------------------------
 // bn_finalize: partial (sum, sumsq) rows -> mean, rstd, scale, shift; running
 // statistics update (training) or running-stat normalisation (eval).
 // ---------------------------------------------------------------------------
@@ -167,12 +359,23 @@ extern "C" int accunet_bn_finalize(const double* part, int R, int C, double coun
                                    int training, float* st, double* ws, void* stream_) {
   hipStream_t s = (hipStream_t)stream_;
   if (C <= 0) return ACC_EBADSHAPE;
-  int rows = R;
-  const double* p = part;
-  if (training) p = reduce_partials_t<double>(part, R, 2 * C, ws, &rows, s);
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(C, 64)), dim3(256), 0, s, p, rows, C,
-                     count, gamma, beta, rmean, rvar, momentum, eps, training, st,
-                     training ? nbt : nullptr);
+  if (training) {
+    FinishArgs fa{};
+    fa.kind = FIN_BN_FWD;
+    fa.ncols = C;
+    fa.count = count;
+    fa.gamma = gamma;
+    fa.beta = beta;
+    fa.rmean = rmean;
+    fa.rvar = rvar;
+    fa.nbt = nbt;
+    fa.momentum = momentum;
+    fa.eps = eps;
+    fa.out_f = st;
+    return reduce_finish(part, true, R, 2 * C, ws, fa, s);
+  }
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(C, 64)), dim3(256), 0, s, part, 0, C,
+                     count, gamma, beta, rmean, rvar, momentum, eps, 0, st, nullptr);
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 
@@ -427,12 +630,30 @@ extern "C" size_t accunet_bn_bwd_ws_elems(long P, int C) {
 
 // dsum (optional, [C]): sum over pixels of dx (fp64 partials in the apply pass, reduced
 // after it into the stats workspace, which the finalize no longer needs by then)
-static void bn_dsum_finish(double* part, int nb, int C, double* scratch, float* dsum,
-                           hipStream_t s) {
-  int rows;
-  const double* pr = reduce_partials_t<double>(part, nb, 2 * C, scratch, &rows, s);
-  hipLaunchKernelGGL(sum_rows_d_kernel<float>, dim3(ceil_div(C, 64)), dim3(256), 0, s, pr, rows,
-                     2 * C, C, dsum);
+static int bn_dsum_finish(double* part, int nb, int C, double* scratch, float* dsum,
+                          hipStream_t s) {
+  FinishArgs fa{};
+  fa.kind = FIN_SUM_F;
+  fa.ncols = C;
+  fa.out_f = dsum;
+  return reduce_finish(part, true, nb, 2 * C, scratch, fa, s);
+}
+
+// BatchNorm backward finish arguments (see fin_bn_bwd)
+static FinishArgs bn_bwd_fin(int C, long P, const float* st, const float* gamma, int training,
+                             float* dgamma, float* dbeta, float* coef, int xc_form) {
+  FinishArgs fa{};
+  fa.kind = FIN_BN_BWD;
+  fa.ncols = C;
+  fa.count = (double)P;
+  fa.st = st;
+  fa.gamma = gamma;
+  fa.training = training;
+  fa.xc_form = xc_form;
+  fa.out_f = coef;
+  fa.out2 = dgamma;
+  fa.out3 = dbeta;
+  return fa;
 }
 
 extern "C" int accunet_bn_bwd(const void* x, const void* dy, const float* st,
@@ -461,10 +682,9 @@ extern "C" int accunet_bn_bwd(const void* x, const void* dy, const float* st,
       hipLaunchKernelGGL((bn_bwd_reduce_kernel<1, T>), grid, dim3(256), 0, s, (const T*)x,
                          (const T*)dy, st, act, P, C, part);
   });
-  int rows;
-  const double* pr = reduce_partials_t<double>(part, nb, 2 * C, scratch, &rows, s);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(C, 64)), dim3(256), 0, s, pr, rows, C,
-                     (double)P, st, gamma, training, dgamma, dbeta, coef, 0);
+  int rc = reduce_finish(part, true, nb, 2 * C, scratch,
+                         bn_bwd_fin(C, P, st, gamma, training, dgamma, dbeta, coef, 0), s);
+  if (rc != ACC_OK) return rc;
   double* cpart = dsum ? part : nullptr;  // the reduce partials are consumed by now
   with_dt(dt, [&](auto tag) {
     using T = decltype(tag);
@@ -475,7 +695,7 @@ extern "C" int accunet_bn_bwd(const void* x, const void* dy, const float* st,
       hipLaunchKernelGGL((bn_bwd_apply_kernel<1, T>), grid, dim3(256), 0, s, (const T*)x,
                          (const T*)dy, st, coef, act, P, C, (T*)dx, accumulate, cpart);
   });
-  if (dsum) bn_dsum_finish(part, nb, C, scratch, dsum, s);
+  if (dsum) return bn_dsum_finish(part, nb, C, scratch, dsum, s);
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 
@@ -512,10 +732,9 @@ extern "C" int accunet_bn_bwd_part(const void* x, const void* dy, const float* s
   float* coef = ws + scr_f;
   double* cpart = reinterpret_cast<double*>(ws + scr_f + bn_coef_floats(C));
   double* cscr = cpart + (size_t)nb * 2 * C;
-  int rows;
-  const double* pr = reduce_partials_t<double>(part, R, 2 * C, scratch, &rows, s);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(C, 64)), dim3(256), 0, s, pr, rows, C,
-                     (double)P, st, gamma, training, dgamma, dbeta, coef, 1);
+  int rc = reduce_finish(part, true, R, 2 * C, scratch,
+                         bn_bwd_fin(C, P, st, gamma, training, dgamma, dbeta, coef, 1), s);
+  if (rc != ACC_OK) return rc;
   with_dt(dt, [&](auto tag) {
     using T = decltype(tag);
     if (V == 4)
@@ -525,7 +744,7 @@ extern "C" int accunet_bn_bwd_part(const void* x, const void* dy, const float* s
       hipLaunchKernelGGL((bn_bwd_apply_kernel<1, T>), grid, dim3(256), 0, s, (const T*)x,
                          (const T*)dy, st, coef, act, P, C, (T*)dx, 0, dsum ? cpart : nullptr);
   });
-  if (dsum) bn_dsum_finish(cpart, nb, C, cscr, dsum, s);
+  if (dsum) return bn_dsum_finish(cpart, nb, C, cscr, dsum, s);
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 
@@ -551,20 +770,20 @@ extern "C" int accunet_colsum(const void* x, long P, int C, float* out, double* 
                              nullptr, ACT_NONE, nullptr, nullptr, P, C, part);
       }))
     return ACC_EBADARG;
-  int rows;
-  const double* pr = reduce_partials_t<double>(part, nb, 2 * C, scratch, &rows, s);
-  hipLaunchKernelGGL(sum_rows_d_kernel<float>, dim3(ceil_div(C, 64)), dim3(256), 0, s, pr, rows,
-                     2 * C, C, out);
-  return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+  FinishArgs fa{};
+  fa.kind = FIN_SUM_F;
+  fa.ncols = C;
+  fa.out_f = out;
+  return reduce_finish(part, true, nb, 2 * C, scratch, fa, s);
 }
 
 // Reduce a partial-stats block [R][2][C] to totals [2][C] (fp64).
 extern "C" int accunet_reduce_stats(const double* part, int R, int C, double* out2C, double* ws,
                                     void* stream_) {
   hipStream_t s = (hipStream_t)stream_;
-  int rows;
-  const double* pr = reduce_partials_t<double>(part, R, 2 * C, ws, &rows, s);
-  hipLaunchKernelGGL(sum_rows_d_kernel<double>, dim3(ceil_div(2 * C, 64)), dim3(256), 0, s, pr,
-                     rows, 2 * C, 2 * C, out2C);
-  return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+  FinishArgs fa{};
+  fa.kind = FIN_SUM_D;
+  fa.ncols = 2 * C;
+  fa.out_d = out2C;
+  return reduce_finish(part, true, R, 2 * C, ws, fa, s);
 }

@@ -875,10 +875,12 @@ extern "C" int accunet_dw3x3_wgrad(const void* x, const void* dz, const float* s
                              part, g);
       }))
     return ACC_EBADARG;
-  int rows;
-  const float* pr = reduce_partials(part, R, 10 * C, scratch, &rows, s);
-  hipLaunchKernelGGL(sum_rows_kernel, dim3(ceil_div(10 * C, 64)), dim3(256), 0, s, pr, rows, 10 * C,
-                     10 * C, sums);
-  hipLaunchKernelGGL(dw_wgrad_finish_kernel, dim3(ceil_div(C, 256)), dim3(256), 0, s, sums, C, dw, db);
-  return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+  (void)sums;
+  FinishArgs fa{};
+  fa.kind = FIN_DW;
+  fa.ncols = 10 * C;
+  fa.C = C;
+  fa.out_f = dw;
+  fa.out2 = db;
+  return reduce_finish(part, false, R, 10 * C, reinterpret_cast<double*>(scratch), fa, s);
 }

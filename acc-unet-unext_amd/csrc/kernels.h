@@ -22,3 +22,29 @@ __global__ void sum_rows_kernel(const float* __restrict__ part, int R, int strid
                                 float* __restrict__ out);
 
 __global__ void inc_i64_kernel(long long* p);
+
+// One-launch reduction of a partial block [R][stride] (fp32 or fp64 rows, fp64
+// accumulation) followed by a per-column finish (bn.hip: reduce_finish_kernel).
+enum { FIN_SUM_F = 0, FIN_SUM_D, FIN_DW, FIN_HEAD, FIN_BN_FWD, FIN_BN_BWD };
+struct FinishArgs {
+  int kind;
+  int ncols;         // columns reduced (paired BN kinds: channels C; columns C..2C-1 are the second moments)
+  int C;             // FIN_DW / FIN_HEAD: channels
+  double count;      // BN kinds: pixels per channel
+  const float* gamma;
+  const float* beta;
+  float* rmean;
+  float* rvar;
+  long long* nbt;
+  float momentum, eps;
+  const float* st;   // FIN_BN_BWD: the forward BatchNorm state block
+  int training, xc_form;
+  float* out_f;      // FIN_SUM_F totals / FIN_BN_FWD state block / FIN_BN_BWD coef / FIN_DW+HEAD dw
+  double* out_d;     // FIN_SUM_D totals
+  float* out2;       // FIN_DW / FIN_HEAD: db ; FIN_BN_BWD: dgamma
+  float* out3;       // FIN_BN_BWD: dbeta
+};
+// chunks: fp64 scratch of reduce_finish_ws(R, stride) doubles, 8-byte aligned
+size_t reduce_finish_ws(int R, int stride);
+int reduce_finish(const void* part, bool part_f64, int R, int stride, double* chunks,
+                  const FinishArgs& fa, hipStream_t s);

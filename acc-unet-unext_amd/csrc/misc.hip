@@ -181,12 +181,14 @@ extern "C" int accunet_head_bwd(const void* x, const float* w, const float* y, c
                              (const T*)x, w, y, dy, sigm, (T*)dx, P, C, part);
       }))
     return ACC_EBADARG;
-  int rows;
-  const float* pr = reduce_partials(part, (int)nb, 2 * C, scratch, &rows, s);
-  hipLaunchKernelGGL(sum_rows_kernel, dim3(ceil_div(2 * C, 64)), dim3(256), 0, s, pr, rows, 2 * C,
-                     2 * C, sums);
-  hipLaunchKernelGGL(head_bwd_finish_kernel, dim3(1), dim3(64), 0, s, sums, C, dw, db);
-  return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+  (void)sums;
+  FinishArgs fa{};
+  fa.kind = FIN_HEAD;
+  fa.ncols = C + 1;  // dw columns, then the bias column
+  fa.C = C;
+  fa.out_f = dw;
+  fa.out2 = db;
+  return reduce_finish(part, false, (int)nb, 2 * C, reinterpret_cast<double*>(scratch), fa, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -568,7 +570,9 @@ typedef MakeMarkers<ACC_MAX_MARKERS>::type Markers;
 
 extern "C" int accunet_graph_marker(int id, void* stream) {
   if (id < 0 || id >= ACC_MAX_MARKERS) return ACC_EBADARG;
-  hipLaunchKernel(Markers::get(id), dim3(1), dim3(1), nullptr, 0, (hipStream_t)stream);
+  if (hipLaunchKernel(Markers::get(id), dim3(1), dim3(1), nullptr, 0, (hipStream_t)stream) !=
+      hipSuccess)
+    return ACC_ELAUNCH;
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 

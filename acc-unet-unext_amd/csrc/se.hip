@@ -906,9 +906,11 @@ extern "C" int accunet_se_bwd_pro(const void* z, const void* dout, const float* 
                          cpart);
   });
   if (dsum) {
-    int rows;
-    const double* pr = reduce_partials_d(cpart, B * g.NCH, 2 * C, dscr, &rows, s);
-    sum_rows_d_to_f(pr, rows, 2 * C, C, dsum, s);
+    FinishArgs fa{};
+    fa.kind = FIN_SUM_F;
+    fa.ncols = C;
+    fa.out_f = dsum;
+    return reduce_finish(cpart, true, B * g.NCH, 2 * C, dscr, fa, s);
   }
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
