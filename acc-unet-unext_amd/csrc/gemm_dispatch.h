@@ -1,6 +1,7 @@
 // Tile selection + template dispatch for gemm_f32_kernel / gemm_bf16_kernel.
 #pragma once
 #include "gemm_f32.h"
+#include "gemm_f32g.h"
 #include "gemm_bf16.h"
 
 // Tile configurations (WM, TM, TN) -> (BM, BN):
@@ -57,6 +58,32 @@ typedef void (*gemm_kfn)(const GemmParams);
 #define GEMM_DEFINE_BTABLE_WGRAD(NAME, AM, BMo, PA, PB) \
   GEMM_DEFINE_BTABLE_E(NAME, AM, BMo, PA, PB, 0, bf16_t, bf16_t, float)
 
+// LDS-DMA fp32 engine (gemm_f32g.h): vector-aligned operands only, so both rows of
+// the [2][TILE_COUNT] table hold the same kernels (GEMM_TABLE_SELECT shape)
+#define GEMM_DEFINE_GTABLE(NAME, AM, BMo, PA, PB, EPI)                                      \
+  gemm_kfn NAME[2][TILE_COUNT] = {                                                         \
+      {gemm_f32g_kernel<AM, BMo, PA, PB, 2, 2, 2, EPI>, gemm_f32g_kernel<AM, BMo, PA, PB, 2, 2, 1, EPI>, \
+       gemm_f32g_kernel<AM, BMo, PA, PB, 4, 1, 1, EPI>, gemm_f32g_kernel<AM, BMo, PA, PB, 1, 1, 1, EPI>, \
+       gemm_f32g_kernel<AM, BMo, PA, PB, 2, 1, 1, EPI>},                                   \
+      {gemm_f32g_kernel<AM, BMo, PA, PB, 2, 2, 2, EPI>, gemm_f32g_kernel<AM, BMo, PA, PB, 2, 2, 1, EPI>, \
+       gemm_f32g_kernel<AM, BMo, PA, PB, 4, 1, 1, EPI>, gemm_f32g_kernel<AM, BMo, PA, PB, 1, 1, 1, EPI>, \
+       gemm_f32g_kernel<AM, BMo, PA, PB, 2, 1, 1, EPI>}};
+
+GEMM_DECLARE_TABLE(g_ggemm_col_nn_p0)
+GEMM_DECLARE_TABLE(g_ggemm_col_nn_p1)
+GEMM_DECLARE_TABLE(g_ggemm_col_nn_p2)
+GEMM_DECLARE_TABLE(g_ggemm_col_nnsh3)
+GEMM_DECLARE_TABLE(g_ggemm_row_nn)
+GEMM_DECLARE_TABLE(g_ggemm_row_nn_bnb)
+GEMM_DECLARE_TABLE(g_ggemm_row_nn_bnb_pyr)
+GEMM_DECLARE_TABLE(g_ggemm_row_nn_pyr)
+GEMM_DECLARE_TABLE(g_ggemm_row_nt_p0)
+GEMM_DECLARE_TABLE(g_ggemm_row_nt_p0_ups)
+GEMM_DECLARE_TABLE(g_ggemm_row_nt_p1)
+GEMM_DECLARE_TABLE(g_ggemm_row_nt_p1_ups)
+GEMM_DECLARE_TABLE(g_ggemm_row_nt_p2)
+GEMM_DECLARE_TABLE(g_ggemm_row_nt_p2_ups)
+GEMM_DECLARE_TABLE(g_ggemm_sh3_nt)
 GEMM_DECLARE_TABLE(g_gemm_row_nt_p0)
 GEMM_DECLARE_TABLE(g_gemm_row_nt_p1)
 GEMM_DECLARE_TABLE(g_gemm_row_nt_p2)

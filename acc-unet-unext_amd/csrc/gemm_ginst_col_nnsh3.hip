@@ -1,0 +1,3 @@
+// gemm_f32g_kernel<AM_COL, BM_NN_SHIFT3, PRO_NONE, PRO_NONE, ...>: LDS-DMA fp32 engine table.
+#include "gemm_dispatch.h"
+GEMM_DEFINE_GTABLE(g_ggemm_col_nnsh3, AM_COL, BM_NN_SHIFT3, PRO_NONE, PRO_NONE, 0)

@@ -1,0 +1,3 @@
+// gemm_f32g_kernel<AM_SHIFT3, BM_NT, PRO_NONE, PRO_NONE, ...>: LDS-DMA fp32 engine table.
+#include "gemm_dispatch.h"
+GEMM_DEFINE_GTABLE(g_ggemm_sh3_nt, AM_SHIFT3, BM_NT, PRO_NONE, PRO_NONE, EPI_STATS)

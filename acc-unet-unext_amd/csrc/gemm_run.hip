@@ -101,6 +101,21 @@ static gemm_kfn* table_v(int amode, int bmode, int pro_a, int pro_b, int epi, in
   return t0 ? t0 + v * TILE_COUNT : nullptr;
 }
 
+// LDS-DMA fp32 engine (gemm_f32g.h) for vector-aligned fp32 GEMMs (ACCUNET_GEMM_G=0: off)
+static gemm_kfn* gtable_for(int amode, int bmode, int pro_a, int pro_b, int epi) {
+  GEMM_TABLE_SELECT(g_ggemm_)
+}
+static gemm_kfn ggemm_for(int amode, int bmode, int pro_a, int pro_b, int epi, int tile) {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("ACCUNET_GEMM_G");
+    on = e ? atoi(e) : 1;
+  }
+  if (!on) return nullptr;
+  gemm_kfn* t = gtable_for(amode, bmode, pro_a, pro_b, epi);
+  return t ? t[tile] : nullptr;
+}
+
 static long split_min_tiles() {
   static long v = -1;
   if (v < 0) {
@@ -229,7 +244,14 @@ int gemm_run(GemmParams p, int amode, int bmode, int pro_a, int pro_b, bool allo
     p.evec = ev ? 1 : 0;
   }
   dim3 grid(gx, gy, S);
-  hipLaunchKernelGGL(tab[t], grid, dim3(GEMM_THREADS), 0, stream, p);
+  gemm_kfn kfn = tab[t];
+  // (weight gradients, AM_COL: both operands k-major, 4 ds_read_b32 per fragment and
+  // k-chunk; the register-staged kernel is as fast or faster there, tools/gg_ab.sh)
+  if (vec && adt == ACC_F32 && amode != AM_COL) {
+    gemm_kfn g = ggemm_for(amode, bmode, pro_a, pro_b, epi, t);
+    if (g) kfn = g;
+  }
+  hipLaunchKernelGGL(kfn, grid, dim3(GEMM_THREADS), 0, stream, p);
   if (S > 1) {
     long total = (long)p.M * p.N;
     long blocks = (total + SPLITK_COLS - 1) / SPLITK_COLS;

@@ -345,9 +345,13 @@ def test_fullwidth_nf32_at_256_matches_reference_and_oracle(variant):
         fp32 run (tests/golden/fullwidth_*_nf32.npz, made by importing the
         reference) and the fp64 oracle: output within 4x the reference's own fp32
         distance to fp64 + 1e-4 of scale, loss within 1e-5 of the reference's;
-      - every gradient and running statistic within 4x the fp32 oracle's distance
-        to fp64 (+ the floors of test_whole_model_train_step_matches_oracle), and the
-        whole gradient vector within 3x;
+      - every gradient and running statistic within 4x the fp32 distance to fp64,
+        taken as the max over the fp32 oracle run and an ensemble of fp32 runs on
+        2^-24-perturbed inputs (parity_util.oracle_run_fp32_ensemble: one fp32 run
+        under-states the sensitivity of cancellation-dominated tensors several x, e.g.
+        cnv11.norm1.weight 2.8e-4 single vs 9.3e-4 ensemble; tools/fw_diag.py), plus
+        the floors of test_whole_model_train_step_matches_oracle, and the whole
+        gradient vector within 3x of the single run;
       - canonical eval output on 1x3x256x256 within 1e-4 of the reference's (the
         north-star bound)."""
     g = np.load(os.path.join(GOLD, f"fullwidth_{variant}_nf32.npz"))
@@ -391,7 +395,8 @@ def test_fullwidth_nf32_at_256_matches_reference_and_oracle(variant):
             hip["buf:" + k] = msd[k]
             r64["buf:" + k] = v
             r32["buf:" + k] = r32_sd[k]
-    rows = PU.compare_vs_reference_fp32(hip, r64, r32, abs_floor=floor)
+    ens = PU.oracle_run_fp32_ensemble(variant, sd, x, mask)
+    rows = PU.compare_vs_reference_fp32(hip, r64, r32, abs_floor=floor, ref32_extra=ens)
     bad = [r for r in rows if not r[4]]
     assert not bad, sorted(bad, key=lambda r: -r[1] / r[3])[:8]
 

@@ -3,6 +3,8 @@ ACC_UNet at B16 256^2 timed in isolation (synchronise before/after), grouped by
 shape and mode, with achieved TFLOP/s against the 157.3 TFLOP/s fp32 MFMA peak.
 
     python tools/gemm_census.py [--batch 16] [--size 256] [--top 40]
+    python tools/gemm_census.py --replay I [--reps 20]   (PMC passes: re-launch the
+        I-th GEMM of the census, by total time, REPS times at the end of the run)
 """
 import argparse
 import collections
@@ -21,6 +23,10 @@ def main():
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--replay", type=int, default=-1)
+    ap.add_argument("--replay-key", default="",
+                    help="M,N,K,amode,bmode[,pro_a]: replay the GEMM with this key (largest total if several)")
+    ap.add_argument("--reps", type=int, default=20)
     a = ap.parse_args()
     from accunet import kern
     from accunet import model as M
@@ -36,6 +42,7 @@ def main():
     torch.cuda.synchronize()
 
     rec = collections.defaultdict(list)
+    first = {}
     orig = kern.gemm
 
     REP = 5
@@ -56,6 +63,7 @@ def main():
                bool(kw.get("allow_split")), kw.get("stats") is not None,
                kw.get("pyr") is not None)
         rec[key].append(dt)
+        first.setdefault(key, ((M_, N_, K_), kw))
         return r
 
     kern.gemm = timed
@@ -77,6 +85,20 @@ def main():
         # roofline: fp32 MFMA 155 TF/s measured, HBM 6.3 TB/s measured (A + B + C only)
         ideal = max(2.0 * M_ * N_ * K_ / 155e12, 4.0 * (M_ * K_ + K_ * N_ + M_ * N_) / 6.3e12)
         print(f"{tt * 1e3:8.3f} {n:3d} {t * 1e6:9.1f} {tf:7.1f} {t / ideal:5.1f}x  {k}")
+    if a.replay_key:
+        want = tuple(int(v) for v in a.replay_key.split(","))
+        cand = [r for r in rows if tuple(r[4][:len(want)]) == want]
+        if not cand:
+            raise SystemExit(f"no GEMM with key {want}")
+        a.replay = rows.index(cand[0])
+    if a.replay >= 0:
+        k = rows[a.replay][4]
+        (M_, N_, K_), kw = first[k]
+        torch.cuda.synchronize()
+        for _ in range(a.reps):
+            orig(M_, N_, K_, **kw)
+        torch.cuda.synchronize()
+        print(f"replayed #{a.replay} {k} x{a.reps}: {2.0 * M_ * N_ * K_:.6e} flop per call")
 
 
 if __name__ == "__main__":
