@@ -22,6 +22,7 @@ BMODE_NT, BMODE_NN, BMODE_NN_SHIFT3 = 0, 1, 2
 PRO_NONE, PRO_AFFINE, PRO_AFFINE_LRELU = 0, 1, 2
 ACT_NONE, ACT_LRELU = 0, 1
 ACC_F32, ACC_BF16 = 0, 1
+ACC_AUG_F32, ACC_AUG_U8 = 0, 1  # accunet_aug_geom element types
 
 
 class AccGemmDesc(Structure):
@@ -111,6 +112,7 @@ _SIGS = {
     "accunet_event_synchronize": [P],
     "accunet_image_prep": [P, I, I, I, I, P, P],
     "accunet_mask_prep": [P, I, I, I, I, I, P, P],
+    "accunet_aug_geom": [P, P, I, I, I, I, P, P],
     "accunet_dwconvk_out_hw": [I, I, I, I, I, I, IP, IP],
     "accunet_layernorm_rows": [L],
     "accunet_layernorm_fwd": [P, P, P, P, P, L, I, F, P],

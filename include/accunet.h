@@ -306,6 +306,27 @@ int accunet_mask_prep(const void* raw, int dtype, int N, int Hin, int Win, int S
                       void* stream);
 
 /* ------------------------------------------------------------------------- *
+ * Training augmentation (csrc/augment.hip): RandomGenerator's geometric
+ * transforms, Experiments/Load_Dataset.py:19-32 (random_rot_flip: np.rot90 k
+ * times + np.flip(axis); random_rotate: scipy.ndimage.rotate(order=0,
+ * reshape=False)), one parameter block per sample, applied to a batch
+ * [B][S][S][C] of uint8 or fp32 elements (out != in). The host draws the
+ * parameters in the reference's random-call order and computes r / o as scipy
+ * does (accunet/augment.py).
+ * ------------------------------------------------------------------------- */
+enum { ACC_AUG_F32 = 0, ACC_AUG_U8 = 1 };
+typedef struct AccAugParam {
+  double r00, r01, r10, r11; /* mode 2: source = r @ (row, col) + o */
+  double o0, o1;
+  int mode;                  /* 0 copy, 1 rot90 + flip, 2 rotate */
+  int k;                     /* mode 1: quarter turns (counter-clockwise) */
+  int axis;                  /* mode 1: np.flip axis (0 rows, 1 columns) */
+  int pad;
+} AccAugParam;
+int accunet_aug_geom(const void* in, void* out, int dtype, int B, int S, int C,
+                     const AccAugParam* params, void* stream);
+
+/* ------------------------------------------------------------------------- *
  * Large-kernel depthwise convolution, NCHW fp32 (csrc/dwconvk.hip). Replaces the
  * reference's native extension kernels/dwconv2d: dwconv2d_fp32 /
  * dwconv2dbias_fp32 (dwconv2d.cpp:14-28 -> depthwise_fwd/launch.cu:12-80), and
