@@ -13,9 +13,26 @@ the bf16 activation mode); weights and statistics are excluded.
 """
 from __future__ import annotations
 
+import hashlib
+import os
+import statistics
+
 import torch
 
 from . import kern
+
+_CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
+# sources that decide K1's instruction stream (profiles/k1_traffic.json is only
+# attached to a bench line whose tree has the same bytes here)
+K1_SOURCES = ("dwconv.hip", "common.h", "chan.h")
+
+
+def src_hash(files=K1_SOURCES) -> str:
+    h = hashlib.sha256()
+    for f in files:
+        with open(os.path.join(_CSRC, f), "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
+    return h.hexdigest()[:16]
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E (MI355X_MICROARCH.md)
 FP32_MFMA_TFLOPS = 157.3   # dense fp32 MFMA
@@ -23,22 +40,32 @@ BF16_MFMA_TFLOPS = 2500.0  # dense bf16 MFMA (~2.5 PF, MI355X_MICROARCH.md "Matr
 
 
 def _time(fn, iters):
+    """(mean us per launch over `iters` back-to-back launches, the per-launch times).
+    An event pair brackets every launch: consecutive launches still run back to back
+    (events are stream markers), and the per-launch list shows the clock's give-back
+    under sustained load (MI355X DVFS: the same kernel slows as the chip heats, so
+    the mean and the median are both reported)."""
     fn()  # first launch outside the timed window
-    s = torch.cuda.Event(enable_timing=True)
-    e = torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(iters):
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(iters + 1)]
+    ev[0].record()
+    for i in range(iters):
         fn()
-    e.record()
-    e.synchronize()
-    return 1000.0 * s.elapsed_time(e) / iters  # us per launch
+        ev[i + 1].record()
+    ev[-1].synchronize()
+    per = [1000.0 * ev[i].elapsed_time(ev[i + 1]) for i in range(iters)]
+    total = 1000.0 * ev[0].elapsed_time(ev[-1])
+    return total / iters, per
 
 
-def _hbm_row(kernel, shape, bytes_alg, avg_us, launches):
+def _hbm_row(kernel, shape, bytes_alg, timing, launches):
+    avg_us, per = timing
     ach = bytes_alg / (avg_us * 1e-6) / 1e9
+    med = statistics.median(per)
     return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel": kernel,
-            "shape": shape, "avg_us": round(avg_us, 2), "launches": launches,
+            "shape": shape, "avg_us": round(avg_us, 2), "median_us": round(med, 2),
+            "frac_median": round(bytes_alg / (med * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+            "launch_us": [round(v, 1) for v in per], "launches": launches,
             "bytes_alg_per_launch": bytes_alg}
 
 
@@ -56,9 +83,9 @@ def k1_dw3x3(B, H, W, C, weight, bias, iters=20, device="cuda", dtype=torch.floa
 
     def run():
         kern.dw3x3_fwd(x, w, b, sc, sh, 1, 0, z, st, B, H, W, C)
-    us = _time(run, iters)
+    t = _time(run, iters)
     name = "dw3x3_tile_fwd_kernel" if C % 32 == 0 else "dw3x3_fwd_kernel"
-    return _hbm_row(name, f"{B}x{H}x{W}x{C}", 2.0 * x.element_size() * B * H * W * C, us, iters)
+    return _hbm_row(name, f"{B}x{H}x{W}x{C}", 2.0 * x.element_size() * B * H * W * C, t, iters)
 
 
 def k3_se(B, H, W, C, se_mod, iters=20, device="cuda", dtype=torch.float32):
@@ -80,9 +107,9 @@ def k3_se(B, H, W, C, se_mod, iters=20, device="cuda", dtype=torch.float32):
         kern.se_fwd(z, sc, sh, 1, B, HW, C, Cr, p["fc1.weight"], p["fc1.bias"], p["fc2.weight"],
                     p["fc2.bias"], p["bn.weight"], p["bn.bias"], rm, rv, None, 0.1, 1e-5, True,
                     out, save, None)
-    us = _time(run, iters)
+    t = _time(run, iters)
     return _hbm_row("se_reduce+se_mid_sample+se_mid_bn+se_apply", f"{B}x{HW}x{C}",
-                    2.0 * z.element_size() * B * HW * C, us, iters)
+                    2.0 * z.element_size() * B * HW * C, t, iters)
 
 
 def hanc_gemm(P, N, K, iters=10, device="cuda", dtype=torch.float32):
@@ -98,13 +125,16 @@ def hanc_gemm(P, N, K, iters=10, device="cuda", dtype=torch.float32):
 
     def run():
         kern.gemm(P, N, K, a=[a], lda=[K], b=w, ldb=K, c=c, ldc=N, bias=bias, stats=st)
-    us = _time(run, iters)
+    us, per = _time(run, iters)
     fl = 2.0 * P * N * K
     ach = fl / (us * 1e-6) / 1e12
     bf = dtype == torch.bfloat16
     peak = BF16_MFMA_TFLOPS if bf else FP32_MFMA_TFLOPS
+    # fp32: the LDS-DMA engine (gemm_f32g.h) unless ACCUNET_GEMM_G=0
+    kname = ("gemm_bf16_kernel" if bf else
+             "gemm_f32_kernel" if os.environ.get("ACCUNET_GEMM_G", "1") == "0" else "gemm_f32g_kernel")
     return {"bound": "mfma", "achieved": round(ach, 2), "peak": peak,
             "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": None,
-            "kernel": "gemm_bf16_kernel" if bf else "gemm_f32_kernel",
-            "shape": f"M{P} N{N} K{K}", "avg_us": round(us, 2),
+            "kernel": kname, "shape": f"M{P} N{N} K{K}", "avg_us": round(us, 2),
+            "median_us": round(statistics.median(per), 2),
             "launches": iters, "flops_alg_per_launch": fl}

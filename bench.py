@@ -214,8 +214,13 @@ def main():
             with open(tf) as f:
                 t = json.load(f)
             if t.get("shape") == rl[0]["shape"] and t.get("dtype", "fp32") == args.dtype:
-                rl[0]["traffic"] = t["traffic_bytes"]
-                rl[0]["traffic_source"] = t.get("source", tf)
+                # only PMC passes taken on this tree's K1 sources count
+                if t.get("src_sha") == probe.src_hash():
+                    rl[0]["traffic"] = t["traffic_bytes"]
+                    rl[0]["traffic_source"] = t.get("source", tf)
+                else:
+                    rl[0]["traffic_stale"] = {"k1_traffic_src_sha": t.get("src_sha"),
+                                              "tree_src_sha": probe.src_hash()}
         line["roofline"] = rl[0]
         line["rooflines"] = rl
     if args.eager:

@@ -1,19 +1,25 @@
-"""Copy the judged summaries of one GPU round (tools/gpu_round.sh, results merged
-into gpurun_out/) into profiles/, named per round:
+"""Copy the judged summaries of one GPU round into profiles/, named per round, each
+stamped with the git commit and K1's source hash (accunet.probe.src_hash):
 
-    python tools/save_profiles.py r01
+    python tools/save_profiles.py r02          (after tools/gpu_round2.sh and
+                                                 tools/pmc_gemm.sh + census, merged
+                                                 into gpurun_out/)
+    python tools/save_profiles.py --shrink-pmc DIR...   (on the box: keep only the
+                                                 probe dispatches of PMC passes)
 
+  {r}_bench_line.json / {r}_bench_line_bf16.json   bench.py JSON lines
   {r}_bench_kernel_stats.csv  rocprofv3 --stats of bench.py --steps 5 --warmup 2
   {r}_bench_kstats.txt        per-kernel totals of that trace (tools/kstats.py)
-  {r}_step_breakdown.txt      one graph-replayed step of that trace: time by kernel
-                              family, launches, inter-kernel gaps
-  {r}_k1_trace.txt            K1 (cnv12 dw3x3, 16x256x256x96) dispatches: the 20-launch
-                              roofline probe (must agree with bench.py's roofline.avg_us)
-                              and the in-model launches
-  {r}_pmc_k1.csv              FETCH_SIZE / WRITE_SIZE rows of the probe's K1 dispatches
-  k1_traffic.json             tools/pmc_traffic.py on those passes (bench.py reads it)
+  {r}_step_breakdown.txt      one graph-replayed step: time by kernel family, launches,
+                              inter-kernel gaps
+  {r}_k1_trace.txt            K1 dispatches: the 20-launch roofline probe (agrees with
+                              the bench line's roofline.avg_us) and the in-model ones
+  {r}_pmc_k1.csv / {r}_pmc_k3.csv   FETCH_SIZE / WRITE_SIZE rows of the probes
+  k1_traffic.json / k3_traffic.json tools/pmc_traffic.py on those passes
+  {r}_pmc_gemm.txt            tools/pmc_gemm_report.py: MFMA busy, clock, wave states,
+                              FETCH / WRITE for the top-5 GEMMs
+  {r}_gemm_census.txt         tools/gemm_census.py (every GEMM of one step)
   {r}_kbench.txt              tools/kbench (kernels + float4 copy ceilings)
-  {r}_bench_line.json         the bench.py JSON line of the round
 """
 import collections
 import csv
@@ -27,12 +33,24 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "gpurun_out")
 PROF = os.path.join(ROOT, "profiles")
-K1 = "dw3x3_tile_fwd_kernel<8, false>"
+K1 = "dw3x3_tile_fwd_kernel<8, false,"
+K1_GRID = 196608  # 768 workgroups x 256 (16x256x256x96, channel groups fastest)
+K3 = ["se_reduce_kernel<4, float>", "se_mid_sample_kernel", "se_mid_bn_kernel", "se_apply_kernel<4, float>"]
 
-FAMILIES = ["gemm_f32", "splitk", "dw3x3", "dw_wgrad", "bn_bwd", "bn_fin", "affine_act",
-            "se_", "hanc_pyramid", "pool", "colreduce", "sum_rows", "CUDAFunctor_add",
-            "copyBuffer", "group_relayout", "permute", "blocksum", "adam", "loss", "head",
-            "slice_copy", "pixel_shuffle"]
+FAMILIES = ["gemm_f32g", "gemm_f32", "gemm_bf16", "splitk", "dw3x3", "reduce_finish", "bn_bwd",
+            "bn_fin", "affine_act", "se_", "hanc_pyramid", "pool", "colreduce", "sum_rows",
+            "CUDAFunctor_add", "copyBuffer", "group_relayout", "permute", "blocksum", "adam",
+            "loss", "head", "slice_copy", "pixel_shuffle", "gemm_skinny"]
+
+
+def stamp():
+    sha = subprocess.run(["git", "rev-parse", "--short=12", "HEAD"], cwd=ROOT, capture_output=True,
+                         text=True).stdout.strip()
+    dirty = subprocess.run(["git", "status", "--porcelain", "acc-unet-unext_amd", "include",
+                            "bench.py"], cwd=ROOT, capture_output=True, text=True).stdout.strip()
+    sys.path.insert(0, os.path.join(ROOT, "acc-unet-unext_amd"))
+    from accunet.probe import src_hash
+    return f"git {sha}{' (+uncommitted)' if dirty else ''}, K1 src {src_hash()}"
 
 
 def family(name):
@@ -55,7 +73,11 @@ def dur(r):
     return int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
 
 
-def step_breakdown(rows):
+def grid(r):
+    return int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
+
+
+def step_breakdown(rows, st):
     idx = [i for i, r in enumerate(rows) if "adam" in r["Kernel_Name"]]
     s, e = idx[-2] + 1, idx[-1] + 1  # the last full step (replay + Adam) before the probes
     seg = rows[s:e]
@@ -66,7 +88,7 @@ def step_breakdown(rows):
         cnt[k] += 1
     busy = sum(cat.values())
     wall = int(seg[-1]["End_Timestamp"]) - int(seg[0]["Start_Timestamp"])
-    lines = [f"one training step (HIP-graph replay + Adam) from the rocprofv3 kernel trace",
+    lines = [f"one training step (HIP-graph replay + Adam) from the rocprofv3 kernel trace ({st})",
              f"kernels {len(seg)}, wall {wall / 1e6:.2f} ms, busy {busy / 1e6:.2f} ms, "
              f"gaps {(wall - busy) / 1e6:.2f} ms", "", "     ms      %  launches  family"]
     for k, v in cat.most_common():
@@ -74,62 +96,130 @@ def step_breakdown(rows):
     return "\n".join(lines) + "\n"
 
 
-def k1_trace(rows):
-    k = [r for r in rows if K1 in r["Kernel_Name"] and r["Grid_Size_X"] == "65536"
-         and r["Grid_Size_Y"] == "3"]
+def k1_trace(rows, st):
+    k = [r for r in rows if K1 in r["Kernel_Name"] and "float>" in r["Kernel_Name"] and grid(r) == K1_GRID]
     probe = k[-20:]
     pavg = sum(dur(r) for r in probe) / len(probe)
-    # cnv21's depthwise (16x128x128x96) launches the same 256x3 grid in ~1/4 the time
     inm = [r for r in k[:-20] if dur(r) > 0.5 * pavg]
     other = [r for r in k[:-20] if dur(r) <= 0.5 * pavg]
     avg = lambda rs: sum(dur(r) for r in rs) / max(len(rs), 1) / 1e3
-    lines = ["rocprofv3 --kernel-trace of `python bench.py --steps 5 --warmup 2 --no-cpu-baseline`",
-             f"{K1}, grid 256x3 workgroups (16x256x256x96: cnv12 / cnv92 forward)",
-             f"  last 20 dispatches = bench.py roofline probe: avg {avg(probe):.2f} us "
-             f"({805306368 / (avg(probe) * 1e-6) / 1e9:.0f} GB/s)",
+    pd = sorted(dur(r) for r in probe)
+    lines = [f"rocprofv3 --kernel-trace of `python bench.py --steps 5 --warmup 2 --no-cpu-baseline` ({st})",
+             f"{K1} ..., {K1_GRID // 256} workgroups (16x256x256x96: cnv12 / cnv92 forward)",
+             f"  last 20 dispatches = bench.py roofline probe: avg {avg(probe):.2f} us, median "
+             f"{pd[len(pd) // 2] / 1e3:.2f} us ({805306368 / (avg(probe) * 1e-6) / 1e9:.0f} GB/s at the avg)",
              f"  in-model dispatches of the same shape (cnv12 / cnv92 forward inside the "
              f"graph-replayed steps): {len(inm)}, avg {avg(inm):.2f} us",
-             f"  same grid, other shape (cnv21 depthwise, 16x128x128x96): {len(other)}, "
-             f"avg {avg(other):.2f} us", "", "  dispatch durations (us):"]
-    lab = lambda r: "probe" if r in probe else ("in-model cnv12/92" if r in inm else "cnv21")
+             f"  same grid, other shape: {len(other)}, avg {avg(other):.2f} us", "",
+             "  dispatch durations (us):"]
+    lab = lambda r: "probe" if r in probe else ("in-model cnv12/92" if r in inm else "other shape")
     lines += [f"    {dur(r) / 1e3:8.2f}  {lab(r)}" for r in k]
     return "\n".join(lines) + "\n"
 
 
-def main():
-    r = sys.argv[1]
-    os.makedirs(PROF, exist_ok=True)
-    st = glob.glob(os.path.join(OUT, "prof_bench", "**", "*kernel_stats.csv"), recursive=True)[0]
-    shutil.copy(st, os.path.join(PROF, f"{r}_bench_kernel_stats.csv"))
-    ks = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "kstats.py"),
-                         os.path.join(OUT, "prof_bench"), "--top", "60"],
-                        capture_output=True, text=True, check=True).stdout
-    open(os.path.join(PROF, f"{r}_bench_kstats.txt"), "w").write(ks)
-    rows = trace_rows()
-    open(os.path.join(PROF, f"{r}_step_breakdown.txt"), "w").write(step_breakdown(rows))
-    open(os.path.join(PROF, f"{r}_k1_trace.txt"), "w").write(k1_trace(rows))
-    # PMC rows of the probe's K1 dispatches + the traffic summary bench.py reads
+def shrink_pmc(dirs):
+    """keep the rows of the last 300 dispatches (the probes run last)"""
+    for d in dirs:
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            with open(f) as fh:
+                rd = csv.DictReader(fh)
+                fields, rows = rd.fieldnames, list(rd)
+            ids = sorted({int(r["Dispatch_Id"]) for r in rows})
+            keep = set(ids[-300:])
+            with open(f, "w", newline="") as fo:
+                w = csv.DictWriter(fo, fieldnames=fields)
+                w.writeheader()
+                w.writerows(r for r in rows if int(r["Dispatch_Id"]) in keep)
+        for f in glob.glob(os.path.join(d, "**", "*agent_info.csv"), recursive=True):
+            os.remove(f)
+
+
+def pmc_rows(kname, last=20, grid_size=None):
     out = []
     for d in ("pmc_fetch", "pmc_write"):
         f = glob.glob(os.path.join(OUT, d, "**", "*counter_collection.csv"), recursive=True)[0]
-        rs = [x for x in csv.DictReader(open(f)) if K1 in x["Kernel_Name"]
-              and x["Grid_Size"] == "196608"]
+        rs = [x for x in csv.DictReader(open(f)) if kname in x["Kernel_Name"]
+              and (grid_size is None or x["Grid_Size"] == str(grid_size))]
         rs.sort(key=lambda x: int(x["Dispatch_Id"]))
-        out += rs[-20:]
-    with open(os.path.join(PROF, f"{r}_pmc_k1.csv"), "w", newline="") as fo:
-        w = csv.DictWriter(fo, fieldnames=list(out[0].keys()))
+        out += rs[-last:]
+    return out
+
+
+def write_csv(path, rows):
+    with open(path, "w", newline="") as fo:
+        w = csv.DictWriter(fo, fieldnames=list(rows[0].keys()))
         w.writeheader()
-        w.writerows(out)
-    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_traffic.py"),
-                    os.path.join(OUT, "pmc_fetch"), os.path.join(OUT, "pmc_write"), K1, "196608",
-                    "20", os.path.join(PROF, "k1_traffic.json"), "16x256x256x96"],
-                   check=True, capture_output=True)
-    if os.path.exists(os.path.join(OUT, "kbench.txt")):
-        shutil.copy(os.path.join(OUT, "kbench.txt"), os.path.join(PROF, f"{r}_kbench.txt"))
-    for line in open(os.path.join(OUT, "bench_full.log")):
-        if line.startswith('{"metric"'):
-            open(os.path.join(PROF, f"{r}_bench_line.json"), "w").write(line)
-    print("saved", r)
+        w.writerows(rows)
+
+
+def traffic(kname, grid_size, shape, dtype="fp32"):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_traffic.py"),
+                        os.path.join(OUT, "pmc_fetch"), os.path.join(OUT, "pmc_write"), kname,
+                        str(grid_size), "20", "/dev/stdout", shape, dtype],
+                       check=True, capture_output=True, text=True)
+    return json.loads(r.stdout[:r.stdout.index("}") + 1])
+
+
+def main():
+    if sys.argv[1] == "--shrink-pmc":
+        return shrink_pmc(sys.argv[2:])
+    r = sys.argv[1]
+    st = stamp()
+    os.makedirs(PROF, exist_ok=True)
+    # bench lines
+    for log, name in (("bench_full.log", f"{r}_bench_line.json"), ("bench_bf16.log", f"{r}_bench_line_bf16.json")):
+        p = os.path.join(OUT, log)
+        if os.path.exists(p):
+            for line in open(p):
+                if line.startswith('{"metric"'):
+                    d = json.loads(line)
+                    d["_stamp"] = st
+                    open(os.path.join(PROF, name), "w").write(json.dumps(d) + "\n")
+    # trace
+    stf = glob.glob(os.path.join(OUT, "prof_bench", "**", "*kernel_stats.csv"), recursive=True)
+    if stf:
+        shutil.copy(stf[0], os.path.join(PROF, f"{r}_bench_kernel_stats.csv"))
+        ks = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "kstats.py"),
+                             os.path.join(OUT, "prof_bench"), "--top", "60"],
+                            capture_output=True, text=True, check=True).stdout
+        open(os.path.join(PROF, f"{r}_bench_kstats.txt"), "w").write(f"# {st}\n" + ks)
+        rows = trace_rows()
+        open(os.path.join(PROF, f"{r}_step_breakdown.txt"), "w").write(step_breakdown(rows, st))
+        open(os.path.join(PROF, f"{r}_k1_trace.txt"), "w").write(k1_trace(rows, st))
+    # PMC: K1 and K3 traffic
+    if glob.glob(os.path.join(OUT, "pmc_fetch", "**", "*counter_collection.csv"), recursive=True):
+        k1rows = [x for x in pmc_rows(K1, grid_size=K1_GRID) if "float>" in x["Kernel_Name"]]
+        write_csv(os.path.join(PROF, f"{r}_pmc_k1.csv"), k1rows)
+        t1 = traffic(K1, K1_GRID, "16x256x256x96")
+        t1["source"] = f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE of bench.py --eager ({st}); {r}_pmc_k1.csv"
+        json.dump(t1, open(os.path.join(PROF, "k1_traffic.json"), "w"), indent=1)
+        k3 = {"kernels": {}, "shape": "16x65536x32", "stamp": st,
+              "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), KiB -> bytes"}
+        k3rows = []
+        for kn in K3:
+            rs = pmc_rows(kn)
+            k3rows += rs
+            f = [float(x["Counter_Value"]) for x in rs if x["Counter_Name"] == "FETCH_SIZE"]
+            w = [float(x["Counter_Value"]) for x in rs if x["Counter_Name"] == "WRITE_SIZE"]
+            k3["kernels"][kn] = {"fetch_bytes": 2048.0 * sum(f) / max(len(f), 1),
+                                 "write_bytes": 1024.0 * sum(w) / max(len(w), 1), "dispatches": [len(f), len(w)]}
+        k3["traffic_bytes"] = sum(v["fetch_bytes"] + v["write_bytes"] for v in k3["kernels"].values())
+        k3["bytes_alg"] = 2.0 * 4 * 16 * 65536 * 32
+        write_csv(os.path.join(PROF, f"{r}_pmc_k3.csv"), k3rows)
+        json.dump(k3, open(os.path.join(PROF, "k3_traffic.json"), "w"), indent=1)
+    # GEMM PMC + census
+    rep = os.path.join(OUT, "pmc_gemm", "report.txt")
+    if os.path.exists(rep):
+        open(os.path.join(PROF, f"{r}_pmc_gemm.txt"), "w").write(
+            f"# tools/pmc_gemm.sh + tools/pmc_gemm_report.py ({st})\n" + open(rep).read())
+    cen = os.path.join(OUT, "census_full.txt")
+    if os.path.exists(cen):
+        open(os.path.join(PROF, f"{r}_gemm_census.txt"), "w").write(
+            f"# python tools/gemm_census.py --top 200 ({st})\n" + open(cen).read())
+    kb = os.path.join(OUT, "kbench.txt")
+    if os.path.exists(kb):
+        open(os.path.join(PROF, f"{r}_kbench.txt"), "w").write(f"# tools/kbench 20 ({st})\n" + open(kb).read())
+    print("saved", r, st)
 
 
 if __name__ == "__main__":
