@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--replay", type=int, default=-1)
     ap.add_argument("--replay-key", default="",
                     help="M,N,K,amode,bmode[,pro_a]: replay the GEMM with this key (largest total if several)")
@@ -35,7 +36,7 @@ def main():
     torch.manual_seed(0)
     dev = torch.device("cuda", 0)
     model = M.VARIANTS["canonical"](3, 1, n_filts=32).to(dev).train()
-    step = TrainStep(model, lr=1e-3)
+    step = TrainStep(model, lr=1e-3, precision=a.dtype)
     x = torch.randn(a.batch, 3, a.size, a.size, device=dev)
     m = (torch.rand(a.batch, 1, a.size, a.size, device=dev) < 0.3).float()
     step(x, m)
@@ -82,8 +83,11 @@ def main():
     print(f"{'ms':>8} {'n':>3} {'us/call':>9} {'TF/s':>7} {'/ideal':>6}  M N K amode bmode proA proB nsrc nup split stats pyr")
     for tt, n, t, tf, k in rows[:a.top]:
         M_, N_, K_ = k[:3]
-        # roofline: fp32 MFMA 155 TF/s measured, HBM 6.3 TB/s measured (A + B + C only)
-        ideal = max(2.0 * M_ * N_ * K_ / 155e12, 4.0 * (M_ * K_ + K_ * N_ + M_ * N_) / 6.3e12)
+        # roofline: fp32 MFMA 155 TF/s measured (bf16 ~2.5 PF), HBM 6.3 TB/s measured
+        # (A + B + C only, at the activation storage width)
+        es = 2.0 if a.dtype == "bf16" else 4.0
+        pk = 2500e12 if a.dtype == "bf16" else 155e12
+        ideal = max(2.0 * M_ * N_ * K_ / pk, es * (M_ * K_ + K_ * N_ + M_ * N_) / 6.3e12)
         print(f"{tt * 1e3:8.3f} {n:3d} {t * 1e6:9.1f} {tf:7.1f} {t / ideal:5.1f}x  {k}")
     if a.replay_key:
         want = tuple(int(v) for v in a.replay_key.split(","))
