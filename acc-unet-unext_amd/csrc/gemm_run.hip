@@ -125,6 +125,17 @@ static long split_min_tiles() {
   return v;
 }
 
+// workgroups a split-K GEMM aims for (ACCUNET_SPLIT_TARGET, tuning knob): more slabs fill
+// the chip for longer K but write and re-read S*M*N fp32 partials
+static long split_target() {
+  static long v = -1;
+  if (v < 0) {
+    const char* e = getenv("ACCUNET_SPLIT_TARGET");
+    v = e ? atol(e) : 1024;
+  }
+  return v;
+}
+
 static int smallk_tile() {
   static int v = -2;
   if (v == -2) {
@@ -218,7 +229,7 @@ int gemm_run(GemmParams p, int amode, int bmode, int pro_a, int pro_b, bool allo
   int ldc_final = p.ldc;
   if (can_split) {
     long tiles = (long)gx * gy;
-    long target = tiles >= split_min_tiles() ? 1 : 1024;  // enough tiles: no split, no reduce
+    long target = tiles >= split_min_tiles() ? 1 : split_target();  // enough tiles: no split
     long maxS = p.K / (BK * 4);
     long want = (target + tiles - 1) / tiles;
     S = (int)(want < maxS ? want : maxS);

@@ -72,40 +72,62 @@ __global__ void __launch_bounds__(256) gemm_skinny_kernel(const SkinnyParams p) 
     for (int j = 0; j < TJ; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  // Loads are unconditional (masked elements read a valid dummy address, zeroed after
+  // the load) and kept raw until every load of the step is issued: a conditional or
+  // immediately widened bf16 load makes hipcc wait for it on the spot (vmcnt(0) per
+  // element), which serialised the bf16 kernel.
+  const T* A0 = (const T*)p.A;
+  const T* B0 = (const T*)p.B;
   for (long k = k0; k < k1; k += 2 * SK_U) {
-    float a[SK_U][TI], b[SK_U][TJ];
+    T ar[SK_U][TI], br[SK_U][TJ];
+    bool aok[SK_U][TI], bok[SK_U][TJ];
 #pragma unroll
     for (int u = 0; u < SK_U; ++u) {
       const long kk = k + 2 * u + lh;
       const bool ok = kk < k1;
-      const T* ar = (const T*)p.A + kk * p.lda + l31;
+      const T* arow = A0 + kk * p.lda + l31;
 #pragma unroll
-      for (int i = 0; i < TI; ++i) a[u][i] = (ok && mok[i]) ? ld1(ar + i * 32) : 0.f;
+      for (int i = 0; i < TI; ++i) {
+        aok[u][i] = ok && mok[i];
+        ar[u][i] = *(aok[u][i] ? arow + i * 32 : A0);
+      }
       int hh = 0, ww = 0;
-      if (SH3 && ok) {
+      if (SH3) {
         const uint32_t q = fdiv((uint32_t)kk, p.fW);
         ww = (int)kk - (int)q * p.W;
         hh = (int)(q - fdiv(q, p.fH) * p.H);
       }
-      const T* br = (const T*)p.B + kk * p.ldb;
+      const T* brow = B0 + kk * p.ldb;
 #pragma unroll
       for (int j = 0; j < TJ; ++j) {
         bool in = ok && nok[j];
         if (SH3)
           in = in && hh + bdh[j] >= 0 && hh + bdh[j] < p.H && ww + bdw[j] >= 0 &&
                ww + bdw[j] < p.W;
-        float v = in ? ld1(br + boff[j]) : 0.f;
-        if (PROB != PRO_NONE && in) v = pro_apply<PROB>(v, bs[j], bh[j]);
-        b[u][j] = v;
+        bok[u][j] = in;
+        br[u][j] = *(in ? brow + boff[j] : B0);
       }
     }
+    // keep every load of the step ahead of the first MFMA (the scheduler would
+    // otherwise interleave the 2-byte bf16 loads with the MFMAs and drain them early)
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int u = 0; u < SK_U; ++u)
+    for (int u = 0; u < SK_U; ++u) {
+      float a[TI], b[TJ];
+#pragma unroll
+      for (int i = 0; i < TI; ++i) a[i] = aok[u][i] ? ld1(&ar[u][i]) : 0.f;
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        float v = ld1(&br[u][j]);
+        if (PROB != PRO_NONE) v = pro_apply<PROB>(v, bs[j], bh[j]);
+        b[j] = bok[u][j] ? v : 0.f;
+      }
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll
         for (int j = 0; j < TJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][i], b[u][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
   }
   // block reduction per output tile: wave partials summed in wave order
   float* slab = p.slabs + (size_t)blockIdx.x * p.M * p.N;
