@@ -98,11 +98,11 @@ class Conv2d_batchnorm(nn.Module):
         if tuple(ks) != (1, 1) or tuple(self.conv1.stride) != (1, 1):
             raise NotImplementedError("Conv2d_batchnorm: only the 1x1 / stride-1 form ACC-UNet uses")
 
-    def run(self, srcs, *, w_off=0, ups=(), weight=None, consumer_bn=None):
+    def run(self, srcs, *, w_off=0, ups=(), weight=None, consumer_bn=None, slots=None):
         self._check()
         w = self.conv1.weight if weight is None else weight
         z = ops.pw_conv(srcs, w, self.conv1.bias, w_off=w_off, ups=ups,
-                        consumer_bn=self.batchnorm)
+                        consumer_bn=self.batchnorm, slots=slots)
         return self.sqe.run(z, consumer_bn=consumer_bn)
 
     def forward(self, x):
@@ -174,13 +174,17 @@ class ResPath(nn.Module):
             self.bns.append(nn.BatchNorm2d(in_chnls))
             self.sqes.append(ChannelSELayer(in_chnls))
 
-    def run(self, x: torch.Tensor) -> torch.Tensor:
+    def run(self, x: torch.Tensor, slot=None) -> torch.Tensor:
+        """slot: GradSlot for x's gradient (x also feeds the encoder's next pool)."""
         n = len(self.convs)
         for i in range(n):
-            z = ops.conv3x3(x, self.convs[i].weight, self.convs[i].bias, consumer_bn=self.bns[i])
+            # x feeds the 3x3 conv and the residual add: one shared gradient buffer
+            sl = slot if (i == 0 and slot is not None) else ops.GradSlot()
+            z = ops.conv3x3(x, self.convs[i].weight, self.convs[i].bias, consumer_bn=self.bns[i],
+                            slot=sl)
             v = self.sqes[i].run(z)
             nxt = self.bn if i == n - 1 else None
-            x = ops.bn_act_add(v, res=x, consumer_bn=nxt, act_after=ACT_LRELU)
+            x = ops.bn_act_add(v, res=x, consumer_bn=nxt, act_after=ACT_LRELU, res_slot=sl)
             if i < n - 1:
                 x = x.z
         if n == 0:
@@ -229,18 +233,21 @@ class MLFC(nn.Module):
         self.sqe3 = ChannelSELayer(in_filters3)
         self.sqe4 = ChannelSELayer(in_filters4)
 
-    def _merge(self, m, xl, bn):
-        return ops.bn_act_add(m, res=xl, consumer_bn=bn, act_after=ACT_LRELU)
+    def _merge(self, m, xl, bn, slot=None):
+        return ops.bn_act_add(m, res=xl, consumer_bn=bn, act_after=ACT_LRELU, res_slot=slot)
 
     def run(self, x1, x2, x3, x4):
         xs = (x1, x2, x3, x4)
         fs = [x.shape[-1] for x in xs]
         offs = [0, fs[0], fs[0] + fs[1], fs[0] + fs[1] + fs[2]]
+        # every x_m and every pooled copy has several consumers below: their gradient
+        # contributions meet in one GradSlot each instead of autograd's adds
+        sl = {(m, l): ops.GradSlot() for m in range(4) for l in range(m, 4)}
         # AvgPool2d(2) chains (:431-485): at[m][l] = x_m resampled down to level l >= m
         at = {(m, m): xs[m] for m in range(4)}
         for m in range(4):
             for l in range(m + 1, 4):
-                at[(m, l)] = ops.pool2(at[(m, l - 1)], mode=ops.kern.POOL_AVG)
+                at[(m, l)] = ops.pool2(at[(m, l - 1)], mode=ops.kern.POOL_AVG, slot=sl[(m, l - 1)])
         finals = [None] * 4
         for i in range(len(self.cnv_blks1)):
             xcs = []
@@ -250,18 +257,21 @@ class MLFC(nn.Module):
                 # levels coarser than l: 1x1 conv at their own resolution, nearest-up add
                 ups = []
                 for m in range(l + 1, 4):
-                    g = ops.pw_conv([xs[m]], w, None, w_off=offs[m], want_stats=False).z
+                    g = ops.pw_conv([xs[m]], w, None, w_off=offs[m], want_stats=False,
+                                    slots=[sl[(m, m)]]).z
                     ups.append((g, _log2(1 << (m - l)), 0))
                 srcs = [at[(m, l)] for m in range(l + 1)]
-                v1 = blk.run(srcs, ups=ups, consumer_bn=getattr(self, f"bns{l + 1}")[i])
+                v1 = blk.run(srcs, ups=ups, consumer_bn=getattr(self, f"bns{l + 1}")[i],
+                             slots=[sl[(m, l)] for m in range(l + 1)])
                 xcs.append(ops.bn_act_add(v1).z)  # act(bns_l(.)) materialised
             for l in range(4):
                 mrg = getattr(self, f"cnv_mrg{l + 1}")[i]
                 f = fs[l]
                 # interleaved merge channels: 2c = x_c[c], 2c+1 = x_l[c] (:492)
                 wm = ops.group_relayout(mrg.conv1.weight.reshape(f, 2 * f), 2, (0, 1))
-                v2 = mrg.run([xcs[l], xs[l]], weight=wm)
-                finals[l] = self._merge(v2, xs[l], getattr(self, f"bns_mrg{l + 1}")[i])
+                v2 = mrg.run([xcs[l], xs[l]], weight=wm, slots=[None, sl[(l, l)]])
+                finals[l] = self._merge(v2, xs[l], getattr(self, f"bns_mrg{l + 1}")[i],
+                                        sl[(l, l)])
         return tuple(getattr(self, f"sqe{l + 1}").run(finals[l]) for l in range(4))
 
     def forward(self, x1, x2, x3, x4):
@@ -274,8 +284,8 @@ class MLFC_W(MLFC):
 
     _weighted = True
 
-    def _merge(self, m, xl, bn):
-        return ops.wmerge(m, xl, self.W, consumer_bn=bn)
+    def _merge(self, m, xl, bn, slot=None):
+        return ops.wmerge(m, xl, self.W, consumer_bn=bn)  # x_l's gradient: autograd adds it
 
 
 class MLFC_Lite(MLFC):
@@ -362,15 +372,18 @@ class ACC_UNet(nn.Module):
         if C != self.n_channels:
             raise ValueError(f"ACC_UNet: expected {self.n_channels} input channels, got {C}")
         x1 = ops.to_nhwc(x, self.act_dtype)
+        # each encoder output feeds the next level's pool and its ResPath: one shared
+        # gradient buffer per level (see ops.GradSlot)
+        s2, s3, s4, s5 = (ops.GradSlot() for _ in range(4))
         x2 = self.cnv12.run(self.cnv11.run(x1))
-        x3 = self.cnv22.run(self.cnv21.run(ops.pool2(x2)))
-        x4 = self.cnv32.run(self.cnv31.run(ops.pool2(x3)))
-        x5 = self.cnv42.run(self.cnv41.run(ops.pool2(x4)))
-        x6 = self.cnv52.run(self.cnv51.run(ops.pool2(x5)))
-        x2 = self.rspth1.run(x2)
-        x3 = self.rspth2.run(x3)
-        x4 = self.rspth3.run(x4)
-        x5 = self.rspth4.run(x5)
+        x3 = self.cnv22.run(self.cnv21.run(ops.pool2(x2, slot=s2)))
+        x4 = self.cnv32.run(self.cnv31.run(ops.pool2(x3, slot=s3)))
+        x5 = self.cnv42.run(self.cnv41.run(ops.pool2(x4, slot=s4)))
+        x6 = self.cnv52.run(self.cnv51.run(ops.pool2(x5, slot=s5)))
+        x2 = self.rspth1.run(x2, s2)
+        x3 = self.rspth2.run(x3, s3)
+        x4 = self.rspth3.run(x4, s4)
+        x5 = self.rspth4.run(x5, s5)
         x2, x3, x4, x5 = self.mlfc1.run(x2, x3, x4, x5)
         x2, x3, x4, x5 = self.mlfc2.run(x2, x3, x4, x5)
         x2, x3, x4, x5 = self.mlfc3.run(x2, x3, x4, x5)

@@ -16,6 +16,7 @@ used for allocation, views and autograd bookkeeping.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
 
@@ -26,7 +27,7 @@ from . import profile as _prof
 from ._lib import (ACT_LRELU, ACT_NONE, AMODE_COL, AMODE_SHIFT3, BMODE_NN, BMODE_NN_SHIFT3,
                    PRO_AFFINE, PRO_AFFINE_LRELU, PRO_NONE)
 
-__all__ = ["Pending", "pw_conv", "dw_conv", "hanc_layer", "bn_act_add", "se", "conv3x3",
+__all__ = ["Pending", "GradSlot", "pw_conv", "dw_conv", "hanc_layer", "bn_act_add", "se", "conv3x3",
            "conv_transpose2x2", "pool2", "cat_channels", "head", "wmerge", "group_relayout",
            "to_nhwc", "weighted_dice_bce"]
 
@@ -94,6 +95,93 @@ def _take_bias_grad(slot):
         return None
     t, slot.t = slot.t, None
     return t
+
+
+class GradSlot:
+    """One shared gradient buffer for an activation that several ops consume (MLFC's
+    level inputs and their pooled copies, ACC_UNet.py:427-525; the ResPath chain and
+    the encoder skips, :290-328, :612-620). Each consumer registers in its forward.
+    In backward the consumers' contributions meet in one buffer: a GEMM data gradient
+    writes it and folds the contributions that arrived before it in as epilogue
+    addends (the buffer itself and any pass-through gradients, read, not copied),
+    pool2 accumulates with its kernel flag, a residual add hands its incoming
+    gradient over untouched (`give`). The last consumer to finish returns the buffer
+    to autograd and the others return None, so autograd never runs an elementwise
+    add to sum them. Contributions arrive in autograd's execution order, which a
+    captured graph fixes, so the sum is deterministic."""
+
+    __slots__ = ("n", "left", "buf", "pend", "live")
+
+    def __init__(self):
+        self.n = 0
+        self.left = 0
+        self.buf = None
+        self.pend = []
+        self.live = False
+
+    def register(self):
+        self.n += 1
+        return self
+
+    def _begin(self):
+        if not self.live:
+            self.live = True
+            self.left = self.n
+            self.buf = None
+            self.pend = []
+
+    def give(self, g):
+        """contribute g as it is (read later as an addend, never written)."""
+        self._begin()
+        self.pend.append(g)
+
+    def gemm_target(self, shape, like):
+        """(buffer, addends) for a GEMM epilogue: C = A*B + sum(addends), in place."""
+        self._begin()
+        adds = ([self.buf] if self.buf is not None else []) + self.pend
+        if self.buf is None:
+            self.buf = torch.empty(shape, dtype=like.dtype, device=like.device)
+        self.pend = []
+        if len(adds) > 3:  # the epilogue takes three addends; fold the rest first
+            for t in adds[3:]:
+                adds[0].add_(t)
+            adds = adds[:3]
+        return self.buf, adds
+
+    def acc_target(self, shape, like):
+        """(buffer, accumulate) for a kernel with an accumulate flag; call flush() after."""
+        self._begin()
+        if self.buf is None:
+            self.buf = torch.empty(shape, dtype=like.dtype, device=like.device)
+            return self.buf, False
+        return self.buf, True
+
+    def flush(self):
+        for t in self.pend:
+            self.buf.add_(t)
+        self.pend = []
+
+    def done(self):
+        """a consumer finished (contributed or not): the gradient for the last one."""
+        self._begin()
+        self.left -= 1
+        if self.left > 0:
+            return None
+        if self.buf is None and self.pend:
+            self.buf = self.pend.pop(0) if len(self.pend) == 1 else self.pend.pop(0).clone()
+        if self.pend:
+            self.flush()
+        b, self.buf, self.live = self.buf, None, False
+        return b
+
+
+_SLOTS_ON = os.environ.get("ACCUNET_GRADSLOT", "1") != "0"  # 0: autograd sums (A/B runs)
+
+
+def _slot_reg(slot):
+    if slot is None or not _SLOTS_ON or not torch.is_grad_enabled():
+        return None
+    return slot.register()
 
 
 def as_pending(x) -> Pending:
@@ -202,6 +290,7 @@ class _PWCfg:
     want_stats: bool = False
     has_bias: bool = True
     bslot: object = None
+    slots: Optional[List] = None  # per source: GradSlot or None
 
 
 class _PWConvFn(torch.autograd.Function):
@@ -240,8 +329,10 @@ class _PWConvFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dZ, _dstats):
+        slots = ctx.cfg.slots or [None] * ctx.cfg.nsrc
         if dZ is None:  # output unused: every input gradient is zero
-            return (None,) * (5 + ctx.cfg.nsrc + len(ctx.up_shapes))
+            d_srcs = [sl.done() if sl is not None else None for sl in slots]
+            return (None,) * 5 + tuple(d_srcs) + (None,) * len(ctx.up_shapes)
         cfg = ctx.cfg
         weight, pro_g, *srcs = ctx.saved_tensors
         dZ = dZ.contiguous()
@@ -256,9 +347,10 @@ class _PWConvFn(torch.autograd.Function):
         for s, (x, C) in enumerate(zip(srcs, cfg.src_ch)):
             need = nig[5 + s] or (s == 0 and pro.active and (nig[3] or nig[4]))
             if not need:
-                d_srcs.append(None)
+                d_srcs.append(slots[s].done() if slots[s] is not None else None)
                 continue
-            dA = _act((B, H, W, C), dZ)
+            if slots[s] is None:
+                dA = _act((B, H, W, C), dZ)
             if s == 0 and pro.active:
                 # the prologue BatchNorm's backward reduce rides in this GEMM's epilogue
                 R = kern.gemm_stats_rows(P, C, N)
@@ -267,6 +359,14 @@ class _PWConvFn(torch.autograd.Function):
                                       bmode=BMODE_NN, b_offset=cfg.w_off + kbeg[s], c=dA, ldc=C,
                                       stats=part, bnb=(x, pro.st, pro.act)))
                 dA, dpro_g, dpro_b = _pro_bwd_part(pro, x, pro_g, dA, part, R)
+            elif slots[s] is not None:
+                # shared gradient buffer: the first contribution writes it, later ones
+                # add in the epilogue (addend = the buffer itself, read before written)
+                dA, adds = slots[s].gemm_target((B, H, W, C), dZ)
+                keep.append(kern.gemm(P, C, N, a=[dZ], lda=[N], b=weight, ldb=cfg.w_ld,
+                                      bmode=BMODE_NN, b_offset=cfg.w_off + kbeg[s], c=dA, ldc=C,
+                                      H=H, W=W, ups=[(t, C, 0, 0) for t in adds]))
+                dA = slots[s].done()
             else:
                 keep.append(kern.gemm(P, C, N, a=[dZ], lda=[N], b=weight, ldb=cfg.w_ld,
                                       bmode=BMODE_NN, b_offset=cfg.w_off + kbeg[s], c=dA, ldc=C))
@@ -302,17 +402,27 @@ class _PWConvFn(torch.autograd.Function):
 
 
 def pw_conv(srcs: Sequence, weight, bias, *, w_off: int = 0, ups: Sequence = (),
-            consumer_bn=None, want_stats: Optional[bool] = None):
+            consumer_bn=None, want_stats: Optional[bool] = None,
+            slots: Optional[Sequence] = None):
     """Z = sum_s src_s @ W[:, w_off + kbeg_s : ...]^T (+bias) (+ nearest-up adds).
 
     srcs[0] may be a Pending (its BatchNorm(+act) is applied in the GEMM prologue).
     ups: sequence of (G tensor [B, H>>lg, W>>lg, ld], log2 factor, column offset).
+    slots: per source, a GradSlot collecting that source's gradient (or None).
     Returns Pending(Z, consumer_bn, ...) carrying Z's partial statistics.
     """
     srcs = [as_pending(s) for s in srcs]
     for s in srcs[1:]:
         if s.bn is not None:
             raise ValueError("only the first source may carry a pending BatchNorm")
+    if slots is not None:
+        if len(slots) != len(srcs):
+            raise ValueError("pw_conv: one slot (or None) per source")
+        if slots[0] is not None and srcs[0].bn is not None:
+            raise ValueError("pw_conv: a pending-BatchNorm source cannot share a GradSlot")
+        slots = [_slot_reg(sl) for sl in slots]
+        if all(sl is None for sl in slots):
+            slots = None
     pro = _finalize(srcs[0])
     z0 = srcs[0].z
     B, H, W = z0.shape[:3]
@@ -323,7 +433,7 @@ def pw_conv(srcs: Sequence, weight, bias, *, w_off: int = 0, ups: Sequence = (),
     cfg = _PWCfg(nsrc=len(srcs), src_ch=[s.z.shape[-1] for s in srcs], pro=pro, w_off=w_off,
                  w_ld=w_ld, N=N, B=B, H=H, W=W,
                  ups=[(lg, off, g.shape[-1]) for g, lg, off in ups], want_stats=want_stats,
-                 has_bias=bias is not None, bslot=_bias_slot(bias, consumer_bn))
+                 has_bias=bias is not None, bslot=_bias_slot(bias, consumer_bn), slots=slots)
     pg, pb = _bn_params(srcs[0])
     Z, stats = _PWConvFn.apply(cfg, w2, bias, pg, pb, *[s.z for s in srcs],
                                *[g for g, _, _ in ups])
@@ -580,6 +690,7 @@ class _BAACfg:
     pro: _Pro
     has_res: bool
     want_stats: bool
+    res_slot: object = None  # GradSlot collecting res's gradient
 
 
 class _BnActAddFn(torch.autograd.Function):
@@ -604,22 +715,29 @@ class _BnActAddFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy, _ds):
         if dy is None:  # output unused: every input gradient is zero
-            return (None,) * 5
+            sl = ctx.cfg.res_slot
+            return (None,) * 4 + (sl.done() if sl is not None else None,)
         cfg = ctx.cfg
         z, pro_g = ctx.saved_tensors
         dy = dy.contiguous()
         dz, dg, db = _pro_bwd(cfg.pro, z, pro_g, dy)
         dres = dy if cfg.has_res else None
+        if cfg.res_slot is not None:  # dy joins the shared buffer as a read-only addend
+            cfg.res_slot.give(dy)
+            dres = cfg.res_slot.done()
         return None, dz, dg, db, dres
 
 
-def bn_act_add(x, res=None, *, consumer_bn=None, act_after=ACT_LRELU, want_stats=None):
-    """Materialise act(bn(x)) (+res); returns Pending(y, consumer_bn) with y's stats."""
+def bn_act_add(x, res=None, *, consumer_bn=None, act_after=ACT_LRELU, want_stats=None,
+               res_slot=None):
+    """Materialise act(bn(x)) (+res); returns Pending(y, consumer_bn) with y's stats.
+    res_slot: GradSlot collecting res's gradient (shared with res's other consumers)."""
     x = as_pending(x)
     pro = _finalize(x)
     if want_stats is None:
         want_stats = _want_stats(consumer_bn)
-    cfg = _BAACfg(pro, res is not None, want_stats)
+    cfg = _BAACfg(pro, res is not None, want_stats,
+                  _slot_reg(res_slot) if res is not None else None)
     pg, pb = _bn_params(x)
     y, stats = _BnActAddFn.apply(cfg, x.z, pg, pb, res)
     C = y.shape[-1]
@@ -736,6 +854,7 @@ class _C3Cfg:
     Cout: int
     want_stats: bool
     bslot: object = None
+    slot: object = None  # GradSlot collecting x's gradient
 
 
 class _Conv3x3Fn(torch.autograd.Function):
@@ -760,7 +879,7 @@ class _Conv3x3Fn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dZ, _ds):
         if dZ is None:  # output unused: every input gradient is zero
-            return (None,) * 4
+            return None, ctx.cfg.slot.done() if ctx.cfg.slot is not None else None, None, None
         cfg = ctx.cfg
         x, weight = ctx.saved_tensors
         dZ = dZ.contiguous()
@@ -771,9 +890,15 @@ class _Conv3x3Fn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             Wf = _f32((Ci, 9 * Co), x)  # [ci][tap'][co] = W[co][ci][8-tap']
             kern.permute4(weight, Wf, (Ci, 3, 3, Co), (9, 3, 1, 9 * Ci), flips=(0, 1, 1, 0))
-            dx = torch.empty_like(x)
+            if cfg.slot is None:
+                dx, adds = torch.empty_like(x), []
+            else:  # shared gradient buffer: earlier contributions are epilogue addends
+                dx, adds = cfg.slot.gemm_target(x.shape, x)
             keep.append(kern.gemm(P, Ci, 9 * Co, a=[dZ], lda=[Co], amode=AMODE_SHIFT3, b=Wf,
-                                  ldb=9 * Co, c=dx, ldc=Ci, H=H, W=W, cin=Co))
+                                  ldb=9 * Co, c=dx, ldc=Ci, H=H, W=W, cin=Co,
+                                  ups=[(t, Ci, 0, 0) for t in adds]))
+        if cfg.slot is not None:
+            dx = cfg.slot.done()
         dWr = _f32((Co, 9 * Ci), x)
         keep.append(kern.gemm(Co, 9 * Ci, P, a=[dZ], lda=[Co], amode=AMODE_COL, b=x, ldb=Ci,
                               bmode=BMODE_NN_SHIFT3, c=dWr, ldc=9 * Ci, H=H, W=W, cin=Ci,
@@ -787,11 +912,12 @@ class _Conv3x3Fn(torch.autograd.Function):
         return None, dx, dW, db
 
 
-def conv3x3(x: torch.Tensor, weight, bias, *, consumer_bn=None):
+def conv3x3(x: torch.Tensor, weight, bias, *, consumer_bn=None, slot=None):
+    """slot: GradSlot collecting x's gradient (shared with x's other consumers)."""
     B, H, W, Ci = x.shape
     Co = weight.shape[0]
     want = _want_stats(consumer_bn)
-    cfg = _C3Cfg(B, H, W, Ci, Co, want, _bias_slot(bias, consumer_bn))
+    cfg = _C3Cfg(B, H, W, Ci, Co, want, _bias_slot(bias, consumer_bn), _slot_reg(slot))
     Z, stats = _Conv3x3Fn.apply(cfg, x, weight, bias)
     return Pending(Z, consumer_bn, ACT_LRELU, stats if want else None,
                    stats.shape[0] if want else 0, bslot=cfg.bslot)
@@ -850,13 +976,14 @@ def conv_transpose2x2(x, weight, bias):
 # --------------------------------------------------------------------------
 class _Pool2Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, mode):
+    def forward(ctx, x, mode, slot=None):
         B, H, W, C = x.shape
         if H % 2 or W % 2:
             raise ValueError("pool2: spatial size must be even")
         y = _act((B, H // 2, W // 2, C), x)
         kern.pool2_fwd(x, y, B, H, W, C, mode)
         ctx.mode = mode
+        ctx.slot = slot
         if mode == kern.POOL_MAX:
             ctx.save_for_backward(x, y)
         else:
@@ -869,13 +996,21 @@ class _Pool2Fn(torch.autograd.Function):
         x = saved[0]
         y = saved[1] if ctx.mode == kern.POOL_MAX else x
         B, H, W, C = x.shape
-        dx = torch.empty_like(x)
-        kern.pool2_bwd(x, y, dy.contiguous(), dx, B, H, W, C, ctx.mode)
-        return dx, None
+        if ctx.slot is None:
+            dx = torch.empty_like(x)
+            kern.pool2_bwd(x, y, dy.contiguous(), dx, B, H, W, C, ctx.mode)
+            return dx, None, None
+        if dy is None:
+            return ctx.slot.done(), None, None
+        dx, acc = ctx.slot.acc_target(x.shape, x)
+        kern.pool2_bwd(x, y, dy.contiguous(), dx, B, H, W, C, ctx.mode, accumulate=acc)
+        ctx.slot.flush()
+        return ctx.slot.done(), None, None
 
 
-def pool2(x, mode=kern.POOL_MAX):
-    return _Pool2Fn.apply(x, mode)
+def pool2(x, mode=kern.POOL_MAX, slot=None):
+    """slot: GradSlot collecting x's gradient (shared with x's other consumers)."""
+    return _Pool2Fn.apply(x, mode, _slot_reg(slot))
 
 
 # --------------------------------------------------------------------------

@@ -196,7 +196,6 @@ __global__ void __launch_bounds__(256)
 reduce_finish_kernel(const TP* __restrict__ part, int R, int stride, int rpc, double* chunks,
                      FinishArgs fa) {
   __shared__ double red[FIN_GROUPS][FIN_COLS];
-  __shared__ int last;
   const int cl = threadIdx.x % FIN_COLS, g = threadIdx.x / FIN_COLS;
   const bool paired = fa.kind == FIN_BN_FWD || fa.kind == FIN_BN_BWD;
   constexpr int HC = FIN_COLS / 2;
@@ -232,27 +231,12 @@ reduce_finish_kernel(const TP* __restrict__ part, int R, int stride, int rpc, do
     // atomic store = sc1) and drained before the ticket, and the last arriver reads
     // them with sc1 loads (L1 bypass), so neither an L2 write-back (release) nor an L1
     // invalidate (acquire) is needed (MI355X guide section 6, Guideline 16, R1/R2)
-    typedef __attribute__((address_space(1))) unsigned long long gu64;
-    if (g == 0 && valid)
-      __hip_atomic_store((gu64*)(chunks + (long)blockIdx.x * stride + col),
-                         (unsigned long long)__double_as_longlong(tot), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      auto* t = (__attribute__((address_space(1))) unsigned*)(g_fin_tickets + blockIdx.y);
-      const unsigned k = __hip_atomic_fetch_add(t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int me_last = k == (unsigned)(nchunk - 1);
-      if (me_last) __hip_atomic_store(t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      last = me_last;
-    }
-    __syncthreads();
-    if (!last) return;
+    if (g == 0 && valid) st_wt(chunks + (long)blockIdx.x * stride + col, tot);
+    if (!handoff_last(g_fin_tickets + blockIdx.y, nchunk)) return;
     double c1[1] = {0.0};
     if (valid)
       ordered_strided_sum<8>(c1, g, nchunk, FIN_GROUPS, [&](int k, double (&v)[1]) {
-        v[0] = __longlong_as_double((long long)__hip_atomic_load(
-            (gu64*)(chunks + (long)k * stride + col), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        v[0] = ld_wt(chunks + (long)k * stride + col);
       });
     tot = combine(c1[0]);
   }

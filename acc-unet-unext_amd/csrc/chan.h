@@ -51,6 +51,56 @@ ACC_DEV void stv_r(T* p, float (&v)[V]) {
   stv<V>(p, v);
 }
 
+// Streaming visit of one thread's rows of a row chunk: local rows lr = rg, rg + RG, ...
+// < nrows of a chunk whose base pointers are block-uniform, channel quad c0 of C.
+// U rows (per input) are loaded raw before any is used, branch-free: rows past the
+// chunk read as 0 through the buffer range check (ACC_OOB), so the compiler waits for
+// each load alone instead of draining every outstanding access per row. f(ok, x...,
+// off) runs in row order (sums stay bit-identical to the plain row loop); off is the
+// row's byte offset or ACC_OOB, usable for a masked bufq_st of an output chunk.
+// Chunks must stay below 2^31 bytes (callers check).
+template <int U, typename T, typename F>
+ACC_DEV void quad_rows1(const T* base, long nrows, int rg, int RG, int C, int c0, F f) {
+  typedef typename QuadRaw<T>::type QR;
+  const __amdgpu_buffer_rsrc_t rs = acc_rsrc(base, (unsigned)(nrows * C * sizeof(T)));
+  const long nit = (nrows + RG - 1) / RG;
+  __builtin_amdgcn_s_waitcnt(0);  // no pre-loop load left pending across the loop
+  for (long i0 = 0; i0 < nit; i0 += U) {
+    QR raw[U];
+    unsigned off[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long lr = rg + (i0 + u) * RG;
+      off[u] = lr < nrows ? (unsigned)((lr * C + c0) * sizeof(T)) : ACC_OOB;
+      raw[u] = bufq_ld<0>(rs, off[u], (const T*)nullptr);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) f(off[u] != ACC_OOB, q2f(raw[u]), off[u]);
+  }
+}
+template <int U, typename T, typename F>
+ACC_DEV void quad_rows2(const T* base1, const T* base2, long nrows, int rg, int RG, int C, int c0,
+                        F f) {
+  typedef typename QuadRaw<T>::type QR;
+  const unsigned bytes = (unsigned)(nrows * C * sizeof(T));
+  const __amdgpu_buffer_rsrc_t r1 = acc_rsrc(base1, bytes), r2 = acc_rsrc(base2, bytes);
+  const long nit = (nrows + RG - 1) / RG;
+  __builtin_amdgcn_s_waitcnt(0);
+  for (long i0 = 0; i0 < nit; i0 += U) {
+    QR x1[U], x2[U];
+    unsigned off[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long lr = rg + (i0 + u) * RG;
+      off[u] = lr < nrows ? (unsigned)((lr * C + c0) * sizeof(T)) : ACC_OOB;
+      x1[u] = bufq_ld<0>(r1, off[u], (const T*)nullptr);
+      x2[u] = bufq_ld<0>(r2, off[u], (const T*)nullptr);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) f(off[u] != ACC_OOB, q2f(x1[u]), q2f(x2[u]), off[u]);
+  }
+}
+
 // Reduce per-thread (a[V], b[V]) across the RG row-groups of the block and write
 // the block's partial row out[(row)*2*C + {0,C} + c].
 template <int V, typename T>

@@ -74,6 +74,7 @@ GEMM_DECLARE_TABLE(g_ggemm_col_nn_p1)
 GEMM_DECLARE_TABLE(g_ggemm_col_nn_p2)
 GEMM_DECLARE_TABLE(g_ggemm_col_nnsh3)
 GEMM_DECLARE_TABLE(g_ggemm_row_nn)
+GEMM_DECLARE_TABLE(g_ggemm_row_nn_ups)
 GEMM_DECLARE_TABLE(g_ggemm_row_nn_bnb)
 GEMM_DECLARE_TABLE(g_ggemm_row_nn_bnb_pyr)
 GEMM_DECLARE_TABLE(g_ggemm_row_nn_pyr)
@@ -84,6 +85,7 @@ GEMM_DECLARE_TABLE(g_ggemm_row_nt_p1_ups)
 GEMM_DECLARE_TABLE(g_ggemm_row_nt_p2)
 GEMM_DECLARE_TABLE(g_ggemm_row_nt_p2_ups)
 GEMM_DECLARE_TABLE(g_ggemm_sh3_nt)
+GEMM_DECLARE_TABLE(g_ggemm_sh3_nt_ups)
 GEMM_DECLARE_TABLE(g_gemm_row_nt_p0)
 GEMM_DECLARE_TABLE(g_gemm_row_nt_p1)
 GEMM_DECLARE_TABLE(g_gemm_row_nt_p2)
@@ -91,7 +93,9 @@ GEMM_DECLARE_TABLE(g_gemm_row_nt_p0_ups)
 GEMM_DECLARE_TABLE(g_gemm_row_nt_p1_ups)
 GEMM_DECLARE_TABLE(g_gemm_row_nt_p2_ups)
 GEMM_DECLARE_TABLE(g_gemm_sh3_nt)
+GEMM_DECLARE_TABLE(g_gemm_sh3_nt_ups)
 GEMM_DECLARE_TABLE(g_gemm_row_nn)
+GEMM_DECLARE_TABLE(g_gemm_row_nn_ups)
 GEMM_DECLARE_TABLE(g_gemm_row_nn_bnb)
 GEMM_DECLARE_TABLE(g_gemm_row_nn_pyr)
 GEMM_DECLARE_TABLE(g_gemm_row_nn_bnb_pyr)
@@ -106,7 +110,9 @@ GEMM_DECLARE_TABLE(g_bgemm_row_nt_p0_ups)
 GEMM_DECLARE_TABLE(g_bgemm_row_nt_p1_ups)
 GEMM_DECLARE_TABLE(g_bgemm_row_nt_p2_ups)
 GEMM_DECLARE_TABLE(g_bgemm_sh3_nt)
+GEMM_DECLARE_TABLE(g_bgemm_sh3_nt_ups)
 GEMM_DECLARE_TABLE(g_bgemm_row_nn)
+GEMM_DECLARE_TABLE(g_bgemm_row_nn_ups)
 GEMM_DECLARE_TABLE(g_bgemm_row_nn_bnb)
 GEMM_DECLARE_TABLE(g_bgemm_row_nn_pyr)
 GEMM_DECLARE_TABLE(g_bgemm_row_nn_bnb_pyr)

@@ -61,7 +61,13 @@ splitk_reduce_kernel(const float* __restrict__ ws, float* __restrict__ C, int M,
     if (pro_a == PRO_AFFINE) return u ? P##row_nt_p1_ups[0] : P##row_nt_p1[0];                  \
     if (pro_a == PRO_AFFINE_LRELU) return u ? P##row_nt_p2_ups[0] : P##row_nt_p2[0];            \
   }                                                                                             \
-  if (epi & EPI_UPS) return nullptr; /* nearest-up addends: forward 1x1 GEMMs only */           \
+  if (epi == EPI_UPS && amode == AM_ROW && bmode == BM_NN && pro_a == PRO_NONE &&               \
+      pro_b == PRO_NONE)                                                                        \
+    return P##row_nn_ups[0]; /* data gradient accumulated in place (addend = C) */              \
+  if (epi == EPI_UPS && amode == AM_SHIFT3 && bmode == BM_NT && pro_a == PRO_NONE &&            \
+      pro_b == PRO_NONE)                                                                        \
+    return P##sh3_nt_ups[0]; /* 3x3 data gradient accumulated in place */                      \
+  if (epi & EPI_UPS) return nullptr;                                                            \
   if (amode == AM_SHIFT3 && bmode == BM_NT && pro_a == PRO_NONE && pro_b == PRO_NONE)           \
     return P##sh3_nt[0];                                                                        \
   if (epi & EPI_STATS) return nullptr; /* C statistics: forward tables only */                  \

@@ -22,6 +22,8 @@
 #include "common.h"
 #include "chan.h"
 #include "kernels.h"
+#include <cstdlib>
+#include <type_traits>
 
 struct SeGeom {
   int B, HW, C, NCH;
@@ -72,8 +74,157 @@ static SeGeom se_geom(int B, int HW, int C) {
   return g;
 }
 
-// pass 1 forward: partials part[(b*NCH + chunk)][2][C] of (sum a, sum a^2)
-template <int V, typename T>
+// Forward middle-step arguments (the gate MLP and the BatchNorm of the gated tensor)
+struct SeMid {
+  int Cr;
+  const float *w1, *b1, *w2, *b2, *gamma, *beta;
+  float *rmean, *rvar;
+  long long* nbt;
+  float momentum, eps;
+  int training;
+  float* save;
+};
+
+// Per-thread fp64 sums of a = act(z*sc + sh) and a^2 over the thread's rows of the
+// block's row chunk [r0, r1) (row order, so bit-identical to the plain loop).
+template <int V, typename T, bool PRO>
+ACC_DEV void se_fwd_sums(const T* __restrict__ z, const float* __restrict__ sc,
+                         const float* __restrict__ sh, int act, const SeGeom& g,
+                         const ChanTile& t, long r0, long r1, double (&a)[V], double (&q)[V]) {
+  if (!t.active) return;
+  float s[V], h[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    s[j] = PRO ? sc[t.c0 + j] : 1.f;
+    h[j] = PRO ? sh[t.c0 + j] : 0.f;
+  }
+  if constexpr (V == 4) {
+    quad_rows1<8>(z + r0 * g.C, r1 > r0 ? r1 - r0 : 0, t.rg, t.RG, g.C, t.c0,
+                  [&](bool ok, float4 x4, unsigned) {
+                    const float v[4] = {x4.x, x4.y, x4.z, x4.w};
+#pragma unroll
+                    for (int j = 0; j < V; ++j) {
+                      double x = PRO ? apply_act(v[j] * s[j] + h[j], act) : v[j];
+                      x = ok ? x : 0.0;
+                      a[j] += x;
+                      q[j] += x * x;
+                    }
+                  });
+    return;
+  }
+  for (long r = r0 + t.rg; r < r1; r += t.RG) {
+    float v[V];
+    ldv<V>(z + r * g.C + t.c0, v);
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      double x = PRO ? apply_act(v[j] * s[j] + h[j], act) : v[j];
+      a[j] += x;
+      q[j] += x * x;
+    }
+  }
+}
+
+// middle step of one sample b: the chunk partials of b -> S[b,c], Q[b,c] (fixed
+// summation order: 4 chunk groups k = grp mod 4, each in chunk order, then
+// ((g0 + g1) + g2) + g3), the channel means, fc1 (+LeakyReLU) and fc2 (+sigmoid) of
+// that sample (the reference gate, :41-45). sm: LDS m[C] | h'[Cr].
+ACC_DEV void se_mid_sample_body(const double* __restrict__ part, const SeGeom& g, const SeMid& m,
+                                int b, float* sm) {
+  __shared__ double r[2][4][64];
+  const int B = g.B, C = g.C, Cr = m.Cr, tid = threadIdx.x;
+  SeSave sv = se_save_view(m.save, B, C, Cr);
+  float* mm = sm;
+  float* hp = sm + C;
+  const int cl = tid & 63, grp = tid >> 6;
+  for (int cb = 0; cb < C; cb += 64) {
+    const int c = cb + cl;
+    double s2[2] = {0.0, 0.0};
+    if (c < C)
+      ordered_strided_sum<8>(s2, grp, g.NCH, 4, [&](int k, double (&v)[2]) {
+        const double* pr = part + ((long)(b * g.NCH + k) * 2) * C;
+        v[0] = *(pr + c);
+        v[1] = *(pr + C + c);
+      });
+    r[0][grp][cl] = s2[0];
+    r[1][grp][cl] = s2[1];
+    __syncthreads();
+    if (grp == 0 && c < C) {
+      const double S = ((r[0][0][cl] + r[0][1][cl]) + r[0][2][cl]) + r[0][3][cl];
+      const double Q = ((r[1][0][cl] + r[1][1][cl]) + r[1][2][cl]) + r[1][3][cl];
+      sv.S[b * C + c] = S;
+      sv.Q[b * C + c] = Q;
+      mm[c] = (float)(S / g.HW);
+    }
+    __syncthreads();
+  }
+  // fc1: 4 threads per output, interleaved over the input channels
+  for (int o = tid; o < Cr * 4; o += 256) {
+    int j = o >> 2, part_i = o & 3;
+    float acc = 0.f;
+    const float* wr = m.w1 + (long)j * C;
+#pragma unroll 8
+    for (int c = part_i; c < C; c += 4) acc = fmaf(wr[c], mm[c], acc);
+    acc += __shfl_xor(acc, 1);
+    acc += __shfl_xor(acc, 2);
+    if (part_i == 0) {
+      acc += m.b1[j];
+      sv.hpre[b * Cr + j] = acc;
+      hp[j] = lrelu(acc);
+    }
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += 256) {
+    float acc = m.b2[c];
+    const float* wr = m.w2 + (long)c * Cr;
+#pragma unroll 8
+    for (int j = 0; j < Cr; ++j) acc = fmaf(wr[j], hp[j], acc);
+    sv.sg[b * C + c] = 1.f / (1.f + expf(-acc));
+  }
+}
+
+// middle step, part 2, channel c: BatchNorm statistics of y = a*s derived from
+// (S, Q, s), running-stat update, per-(b,c) coefficients.
+ACC_DEV void se_mid_bn_body(const SeGeom& g, const SeMid& m, int c) {
+  const int B = g.B, C = g.C;
+  if (m.nbt && c == 0) *m.nbt += 1;  // num_batches_tracked (training only; null otherwise)
+  if (c >= C) return;
+  SeSave sv = se_save_view(m.save, B, C, m.Cr);
+  const double n = (double)B * g.HW;
+  float mu, var;
+  if (m.training) {
+    double m1 = 0.0, m2 = 0.0;
+#pragma unroll 8
+    for (int b = 0; b < B; ++b) {
+      double s = *(sv.sg + b * C + c);
+      m1 += s * *(sv.S + b * C + c);
+      m2 += s * s * *(sv.Q + b * C + c);
+    }
+    m1 /= n;
+    m2 = m2 / n - m1 * m1;
+    if (m2 < 0.0) m2 = 0.0;
+    mu = (float)m1;
+    var = (float)m2;
+    if (m.rmean) m.rmean[c] = (1.f - m.momentum) * m.rmean[c] + m.momentum * mu;
+    if (m.rvar)
+      m.rvar[c] = (1.f - m.momentum) * m.rvar[c] + m.momentum * (float)(m2 * n / (n - 1.0));
+  } else {
+    mu = m.rmean[c];
+    var = m.rvar[c];
+  }
+  float rs = 1.f / sqrtf(var + m.eps);
+  float k = m.gamma[c] * rs;
+  sv.mean[c] = mu;
+  sv.rstd[c] = rs;
+  sv.betap[c] = m.beta[c] - k * mu;
+#pragma unroll 8
+  for (int b = 0; b < B; ++b) sv.alpha[b * C + c] = k * *(sv.sg + b * C + c);
+}
+
+// pass 1 forward: partials part[(b*NCH + chunk)][2][C] of (sum a, sum a^2).
+// (The middle step stays two launches: folding it into this launch's last blocks with
+// ticketed hand-offs measured slower, as its cost is the chain of dependent memory
+// round trips, not the launches.)
+template <int V, typename T, bool PRO>
 __global__ void __launch_bounds__(256)
 se_reduce_kernel(const T* __restrict__ z, const float* __restrict__ sc,
                  const float* __restrict__ sh, int act, SeGeom g, double* __restrict__ part) {
@@ -84,164 +235,22 @@ se_reduce_kernel(const T* __restrict__ z, const float* __restrict__ sc,
   double a[V], q[V];
 #pragma unroll
   for (int j = 0; j < V; ++j) { a[j] = 0.0; q[j] = 0.0; }
-  if (t.active) {
-    float s[V], h[V];
-#pragma unroll
-    for (int j = 0; j < V; ++j) {
-      s[j] = sc ? sc[t.c0 + j] : 1.f;
-      h[j] = sh ? sh[t.c0 + j] : 0.f;
-    }
-    const bool pro = sc != nullptr;
-    for (long r = r0 + t.rg; r < r1; r += t.RG) {
-      float v[V];
-      ldv<V>(z + r * g.C + t.c0, v);
-#pragma unroll
-      for (int j = 0; j < V; ++j) {
-        double x = pro ? apply_act(v[j] * s[j] + h[j], act) : v[j];
-        a[j] += x;
-        q[j] += x * x;
-      }
-    }
-  }
+  se_fwd_sums<V, T, PRO>(z, sc, sh, act, g, t, r0, r1, a, q);
   block_chan_reduce2<V>(t, a, q, part, blockIdx.x, g.C);
 }
 
-// chunk partials [B*NCH][N][C] -> per-(b,c) sums out[i][B*C] (i < N): block = 64
-// channels x 4 chunk groups of one sample; each group sums its chunks in order, the 4
-// group sums are added in order.
-template <int N>
+// middle step: per sample, then per channel
 __global__ void __launch_bounds__(256)
-se_part_sum_kernel(const double* __restrict__ part, SeGeom g, double* __restrict__ out) {
-  __shared__ double r[N][4][64];
-  const int C = g.C, b = blockIdx.y, t = threadIdx.x;
-  const int c = blockIdx.x * 64 + (t & 63), grp = t >> 6;
-  double s[N];
-#pragma unroll
-  for (int i = 0; i < N; ++i) s[i] = 0.0;
-  if (c < C)
-    ordered_strided_sum<4>(s, grp, g.NCH, 4, [&](int k, double (&v)[N]) {
-      const double* pr = part + ((long)(b * g.NCH + k) * N) * C;
-#pragma unroll
-      for (int i = 0; i < N; ++i) v[i] = pr[(long)i * C + c];
-    });
-#pragma unroll
-  for (int i = 0; i < N; ++i) r[i][grp][t & 63] = s[i];
-  __syncthreads();
-  if (grp == 0 && c < C) {
-    const long BC = (long)g.B * C;
-#pragma unroll
-    for (int i = 0; i < N; ++i)
-      out[i * BC + b * C + c] = ((r[i][0][t] + r[i][1][t]) + r[i][2][t]) + r[i][3][t];
-  }
+se_mid_sample_kernel(const double* __restrict__ part, SeGeom g, SeMid m) {
+  extern __shared__ __attribute__((aligned(16))) float se_dyn[];
+  se_mid_sample_body(part, g, m, blockIdx.x, se_dyn);
 }
-
-// mid forward, fused per sample (one block per sample b): the chunk partials of b
-// -> S[b,c], Q[b,c] (same fixed summation order as se_part_sum_kernel: 4 chunk
-// groups k = grp mod 4, each in chunk order, then ((g0 + g1) + g2) + g3), then the
-// channel means, fc1 (+LeakyReLU) and fc2 (+sigmoid) of that sample (as
-// the reference gate, :41-45). One launch for the whole per-sample middle step.
-__global__ void __launch_bounds__(256)
-se_mid_sample_kernel(const double* __restrict__ part, SeGeom g, int Cr,
-                     const float* __restrict__ w1, const float* __restrict__ b1,
-                     const float* __restrict__ w2, const float* __restrict__ b2,
-                     float* __restrict__ save) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];  // m[C] | h'[Cr]
-  __shared__ double r[2][4][64];
-  const int B = g.B, C = g.C, b = blockIdx.x, tid = threadIdx.x;
-  SeSave sv = se_save_view(save, B, C, Cr);
-  float* m = sm;
-  float* hp = sm + C;
-  const int cl = tid & 63, grp = tid >> 6;
-  for (int cb = 0; cb < C; cb += 64) {
-    const int c = cb + cl;
-    double s2[2] = {0.0, 0.0};
-    if (c < C)
-      ordered_strided_sum<8>(s2, grp, g.NCH, 4, [&](int k, double (&v)[2]) {
-        const double* pr = part + ((long)(b * g.NCH + k) * 2) * C;
-        v[0] = pr[c];
-        v[1] = pr[(long)C + c];
-      });
-    r[0][grp][cl] = s2[0];
-    r[1][grp][cl] = s2[1];
-    __syncthreads();
-    if (grp == 0 && c < C) {
-      const double S = ((r[0][0][cl] + r[0][1][cl]) + r[0][2][cl]) + r[0][3][cl];
-      const double Q = ((r[1][0][cl] + r[1][1][cl]) + r[1][2][cl]) + r[1][3][cl];
-      sv.S[b * C + c] = S;
-      sv.Q[b * C + c] = Q;
-      m[c] = (float)(S / g.HW);
-    }
-    __syncthreads();
-  }
-  // fc1: 4 threads per output, interleaved over the input channels
-  for (int o = tid; o < Cr * 4; o += 256) {
-    int j = o >> 2, part_i = o & 3;
-    float acc = 0.f;
-    const float* wr = w1 + (long)j * C;
-    #pragma unroll 8
-    for (int c = part_i; c < C; c += 4) acc = fmaf(wr[c], m[c], acc);
-    acc += __shfl_xor(acc, 1);
-    acc += __shfl_xor(acc, 2);
-    if (part_i == 0) {
-      acc += b1[j];
-      sv.hpre[b * Cr + j] = acc;
-      hp[j] = lrelu(acc);
-    }
-  }
-  __syncthreads();
-  for (int c = tid; c < C; c += 256) {
-    float acc = b2[c];
-    const float* wr = w2 + (long)c * Cr;
-    #pragma unroll 8
-    for (int j = 0; j < Cr; ++j) acc = fmaf(wr[j], hp[j], acc);
-    sv.sg[b * C + c] = 1.f / (1.f + expf(-acc));
-  }
-}
-
-// mid forward, part 2: one thread per channel — BatchNorm statistics of y = a*s
-// derived from (S, Q, s), running-stat update, per-(b,c) coefficients.
-__global__ void __launch_bounds__(256)
-se_mid_bn_kernel(SeGeom g, int Cr, const float* __restrict__ gamma,
-                 const float* __restrict__ beta, float* __restrict__ rmean,
-                 float* __restrict__ rvar, float momentum, float eps, int training,
-                 float* __restrict__ save, long long* __restrict__ nbt) {
-  const int B = g.B, C = g.C;
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (nbt && c == 0) *nbt += 1;  // num_batches_tracked (training only; null otherwise)
-  if (c >= C) return;
-  SeSave sv = se_save_view(save, B, C, Cr);
-  const double n = (double)B * g.HW;
-  float mu, var;
-  if (training) {
-    double m1 = 0.0, m2 = 0.0;
-    #pragma unroll 8
-    for (int b = 0; b < B; ++b) {
-      double s = sv.sg[b * C + c];
-      m1 += s * sv.S[b * C + c];
-      m2 += s * s * sv.Q[b * C + c];
-    }
-    m1 /= n;
-    m2 = m2 / n - m1 * m1;
-    if (m2 < 0.0) m2 = 0.0;
-    mu = (float)m1;
-    var = (float)m2;
-    if (rmean) rmean[c] = (1.f - momentum) * rmean[c] + momentum * mu;
-    if (rvar) rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)(m2 * n / (n - 1.0));
-  } else {
-    mu = rmean[c];
-    var = rvar[c];
-  }
-  float rs = 1.f / sqrtf(var + eps);
-  float k = gamma[c] * rs;
-  sv.mean[c] = mu;
-  sv.rstd[c] = rs;
-  sv.betap[c] = beta[c] - k * mu;
-  #pragma unroll 8
-  for (int b = 0; b < B; ++b) sv.alpha[b * C + c] = k * sv.sg[b * C + c];
+__global__ void __launch_bounds__(256) se_mid_bn_kernel(SeGeom g, SeMid m) {
+  se_mid_bn_body(g, m, blockIdx.x * blockDim.x + threadIdx.x);
 }
 
 // pass 2 forward: out = lrelu(alpha[b,c]*a + betap[c])
-template <int V, typename T>
+template <int V, typename T, bool PRO>
 __global__ void __launch_bounds__(256)
 se_apply_kernel(const T* __restrict__ z, const float* __restrict__ sc,
                 const float* __restrict__ sh, int act, SeGeom g, const float* __restrict__ alpha,
@@ -258,23 +267,40 @@ se_apply_kernel(const T* __restrict__ z, const float* __restrict__ sc,
     float s[V], h[V], al[V], be[V];
 #pragma unroll
     for (int j = 0; j < V; ++j) {
-      s[j] = sc ? sc[t.c0 + j] : 1.f;
-      h[j] = sh ? sh[t.c0 + j] : 0.f;
+      s[j] = PRO ? sc[t.c0 + j] : 1.f;
+      h[j] = PRO ? sh[t.c0 + j] : 0.f;
       al[j] = alpha[b * g.C + t.c0 + j];
       be[j] = betap[t.c0 + j];
     }
-    const bool pro = sc != nullptr;
-    for (long r = r0 + t.rg; r < r1; r += t.RG) {
-      float v[V];
-      ldv<V>(z + r * g.C + t.c0, v);
+    if constexpr (V == 4) {
+      const long nr = r1 > r0 ? r1 - r0 : 0;
+      const __amdgpu_buffer_rsrc_t ro = acc_rsrc(out + r0 * g.C, (unsigned)(nr * g.C * sizeof(T)));
+      const bool st = ostats != nullptr;
+      quad_rows1<8>(z + r0 * g.C, nr, t.rg, t.RG, g.C, t.c0, [&](bool ok, float4 x4, unsigned off) {
+        float v[4] = {x4.x, x4.y, x4.z, x4.w};
 #pragma unroll
-      for (int j = 0; j < V; ++j) {
-        float x = pro ? apply_act(v[j] * s[j] + h[j], act) : v[j];
-        v[j] = rnd<T>(lrelu(al[j] * x + be[j]));  // statistics of the stored value
-        o1[j] += v[j];
-        o2[j] += (double)v[j] * v[j];
+        for (int j = 0; j < V; ++j) {
+          float x = PRO ? apply_act(v[j] * s[j] + h[j], act) : v[j];
+          v[j] = rnd<T>(lrelu(al[j] * x + be[j]));  // statistics of the stored value
+          const double y = (st && ok) ? (double)v[j] : 0.0;
+          o1[j] += y;
+          o2[j] += y * y;
+        }
+        bufq_st<0>(ro, off, make_float4(v[0], v[1], v[2], v[3]), (T*)nullptr);
+      });
+    } else {
+      for (long r = r0 + t.rg; r < r1; r += t.RG) {
+        float v[V];
+        ldv<V>(z + r * g.C + t.c0, v);
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          float x = PRO ? apply_act(v[j] * s[j] + h[j], act) : v[j];
+          v[j] = rnd<T>(lrelu(al[j] * x + be[j]));
+          o1[j] += v[j];
+          o2[j] += (double)v[j] * v[j];
+        }
+        stv<V>(out + r * g.C + t.c0, v);
       }
-      stv<V>(out + r * g.C + t.c0, v);
     }
   }
   // optional statistics of the SE output (MLFC feeds it straight into bns_l, :427-487)
@@ -321,13 +347,69 @@ se_bwd_reduce_kernel(const T* __restrict__ z, const T* __restrict__ dout,
   block_chan_reduce2<V>(t, t1, t2, part, blockIdx.x, g.C);
 }
 
-// backward mid (three small launches). coef (fp32): A[B*C] Bc[B*C] Cc[B*C] with
+// backward middle step. coef (fp32): A[B*C] Bc[B*C] Cc[B*C] with
 //   da = A*g2 + Bc*(a*s - mean) + Cc
-// scratch (fp64): G[C] GY[C] du[B*C] dh[B*Cr] T1[B*C] T2[B*C]
-// part 1: one thread per channel — BN backward sums and du = ds * s * (1 - s)
+// scratch (fp64): G[C] GY[C] du[B*C] dh[B*Cr] T1[B*C] T2[B*C] (+ U1..W3 with a prologue)
+// Four small launches (part sums, channel, sample, parameter step); the prologue
+// variant adds a fifth (coefficient step).
+struct SeBwdMid {
+  int Cr;
+  const float *w1, *w2, *gamma;
+  int training;
+  float* save;
+  double* scratch;
+  float* coef;
+  float *dw1, *db1, *dw2, *db2, *dgamma, *dbeta;
+  // prologue BatchNorm (accunet_se_bwd_pro)
+  const float *pst, *pgamma;
+  int ptraining;
+  float *dpg, *dpb, *pcoef;
+};
+
+ACC_DEV double* se_T1(const SeGeom& g, const SeBwdMid& m) {
+  return m.scratch + 2 * (size_t)g.C + (size_t)g.B * g.C + (size_t)g.B * m.Cr;
+}
+
+// chunk partials [B*NCH][N][C] of sample b -> per-(b,c) sums out[i][B*C] (i < N): 64
+// channels x 4 chunk groups per pass; each group sums its chunks in order, the 4
+// group sums are added in order.
+template <int N>
+ACC_DEV void se_part_sum_body(const double* __restrict__ part, const SeGeom& g, int b, int cb,
+                              double* __restrict__ out) {
+  __shared__ double r[N][4][64];
+  const int C = g.C, t = threadIdx.x;
+  const int c = cb + (t & 63), grp = t >> 6;
+  double s[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) s[i] = 0.0;
+  if (c < C)
+    ordered_strided_sum<4>(s, grp, g.NCH, 4, [&](int k, double (&v)[N]) {
+      const double* pr = part + ((long)(b * g.NCH + k) * N) * C;
+#pragma unroll
+      for (int i = 0; i < N; ++i) v[i] = *(pr + (long)i * C + c);
+    });
+#pragma unroll
+  for (int i = 0; i < N; ++i) r[i][grp][t & 63] = s[i];
+  __syncthreads();
+  if (grp == 0 && c < C) {
+    const long BC = (long)g.B * C;
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      out[i * BC + b * C + c] = ((r[i][0][t] + r[i][1][t]) + r[i][2][t]) + r[i][3][t];
+  }
+  __syncthreads();
+}
+
+template <int N>
+__global__ void __launch_bounds__(256)
+se_part_sum_kernel(const double* __restrict__ part, SeGeom g, double* __restrict__ out) {
+  se_part_sum_body<N>(part, g, blockIdx.y, blockIdx.x * 64, out);
+}
+
 // SE_LANES lanes per channel: lane l handles samples b = l, l + SE_LANES, ...; the
 // per-channel sums are reduced with an xor butterfly inside the lane group and lane 0's
-// value is broadcast, so every lane uses identical totals (deterministic).
+// value is broadcast, so every lane uses identical totals (deterministic). All lanes of
+// the wave take part (dead channels too).
 #define SE_LANES 16
 ACC_DEV double se_lane_sum(double v) {
 #pragma unroll
@@ -335,31 +417,26 @@ ACC_DEV double se_lane_sum(double v) {
   return __shfl(v, (threadIdx.x & 63) & ~(SE_LANES - 1));
 }
 
-__global__ void __launch_bounds__(256)
-se_bwd_chan_kernel(SeGeom g, int Cr,
-                   const float* __restrict__ gamma, int training, float* __restrict__ save,
-                   float* __restrict__ dgamma, float* __restrict__ dbeta,
-                   double* __restrict__ scratch) {
+// channel step, channel c (lane `lane` of its group): BN backward sums and
+// du = ds * s * (1 - s).
+ACC_DEV void se_bwd_chan_body(const SeGeom& g, const SeBwdMid& m, int c, int lane) {
   const int B = g.B, C = g.C;
-  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  const int c = gid / SE_LANES, lane = gid % SE_LANES;
-  const bool live = c < C;  // dead lanes still join the shuffles
+  const bool live = c < C;
   const int cc = live ? c : 0;
-  SeSave sv = se_save_view(save, B, C, Cr);
-  double* G = scratch;
+  SeSave sv = se_save_view(m.save, B, C, m.Cr);
+  double* G = m.scratch;
   double* GY = G + C;
   double* du = GY + C;
-  const double* T1 = du + (size_t)B * C + (size_t)B * Cr;
+  const double* T1 = se_T1(g, m);
   const double* T2 = T1 + (size_t)B * C;
   const double n = (double)B * g.HW;
   const double mean = sv.mean[cc], rstd = sv.rstd[cc];
   double gs = 0.0, gy = 0.0;
-  // per-(b,c) T1 = sum g2, T2 = sum g2*a (se_part_sum_kernel)
   if (live)
     for (int b = lane; b < B; b += SE_LANES) {
-      double t1 = T1[b * C + c];
+      double t1 = *(T1 + b * C + c);
       gs += t1;
-      gy += (double)sv.sg[b * C + c] * T2[b * C + c] - mean * t1;
+      gy += (double)sv.sg[b * C + c] * *(T2 + b * C + c) - mean * t1;
     }
   gs = se_lane_sum(gs);
   gy = se_lane_sum(gy) * rstd;
@@ -367,15 +444,15 @@ se_bwd_chan_kernel(SeGeom g, int Cr,
   if (lane == 0) {
     G[c] = gs;
     GY[c] = gy;
-    if (dgamma) dgamma[c] = (float)gy;
-    if (dbeta) dbeta[c] = (float)gs;
+    if (m.dgamma) m.dgamma[c] = (float)gy;
+    if (m.dbeta) m.dbeta[c] = (float)gs;
   }
-  const double k = (double)gamma[c] * rstd;
+  const double k = (double)m.gamma[c] * rstd;
   for (int b = lane; b < B; b += SE_LANES) {
     double s = sv.sg[b * C + c];
-    double t2 = T2[b * C + c];
+    double t2 = *(T2 + b * C + c);
     double ds;
-    if (training) {
+    if (m.training) {
       double yha = rstd * (s * sv.Q[b * C + c] - mean * sv.S[b * C + c]);
       ds = k * (t2 - (gs / n) * sv.S[b * C + c] - (gy / n) * yha);
     } else {
@@ -385,24 +462,25 @@ se_bwd_chan_kernel(SeGeom g, int Cr,
   }
 }
 
-// part 2: one block per sample — dh = lrelu'(hpre) * W2^T du, dm = W1^T dh, coefficients
-__global__ void __launch_bounds__(256)
-se_bwd_sample_kernel(SeGeom g, int Cr, const float* __restrict__ w1,
-                     const float* __restrict__ w2, const float* __restrict__ gamma, int training,
-                     float* __restrict__ save, double* __restrict__ scratch,
-                     float* __restrict__ coef) {
-  extern __shared__ __attribute__((aligned(16))) double smd[];  // dh[Cr]
-  const int B = g.B, C = g.C, b = blockIdx.x, tid = threadIdx.x;
-  SeSave sv = se_save_view(save, B, C, Cr);
-  double* G = scratch;
-  double* GY = G + C;
-  double* du = GY + C;
-  double* dh = du + (size_t)B * C;
+__global__ void __launch_bounds__(256) se_bwd_chan_kernel(SeGeom g, SeBwdMid m) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  se_bwd_chan_body(g, m, gid / SE_LANES, gid % SE_LANES);
+}
+
+// sample step, sample b: dh = lrelu'(hpre) * W2^T du, dm = W1^T dh, coefficients.
+// smd: LDS dh[Cr]. Ends with a barrier (smd reusable).
+ACC_DEV void se_bwd_sample_body(const SeGeom& g, const SeBwdMid& m, int b, double* smd) {
+  const int B = g.B, C = g.C, Cr = m.Cr, tid = threadIdx.x;
+  SeSave sv = se_save_view(m.save, B, C, Cr);
+  const double* G = m.scratch;
+  const double* GY = G + C;
+  const double* du = GY + C;
+  double* dh = const_cast<double*>(du) + (size_t)B * C;
   for (int o = tid; o < Cr * 4; o += 256) {
     int j = o >> 2, part_i = o & 3;
     double acc = 0.0;
-    #pragma unroll 8
-    for (int c = part_i; c < C; c += 4) acc += (double)w2[(long)c * Cr + j] * du[b * C + c];
+#pragma unroll 8
+    for (int c = part_i; c < C; c += 4) acc += (double)m.w2[(long)c * Cr + j] * du[b * C + c];
     acc += __shfl_xor(acc, 1);
     acc += __shfl_xor(acc, 2);
     if (part_i == 0) {
@@ -413,18 +491,18 @@ se_bwd_sample_kernel(SeGeom g, int Cr, const float* __restrict__ w1,
   }
   __syncthreads();
   const double n = (double)B * g.HW;
-  float* A = coef;
+  float* A = m.coef;
   float* Bc = A + (size_t)B * C;
   float* Cc = Bc + (size_t)B * C;
   for (int c = tid; c < C; c += 256) {
     double dm = 0.0;
-    #pragma unroll 8
-    for (int j = 0; j < Cr; ++j) dm += (double)w1[(long)j * C + c] * smd[j];
-    double k = (double)gamma[c] * sv.rstd[c];
+#pragma unroll 8
+    for (int j = 0; j < Cr; ++j) dm += (double)m.w1[(long)j * C + c] * smd[j];
+    double k = (double)m.gamma[c] * sv.rstd[c];
     double s = sv.sg[b * C + c];
     int i = b * C + c;
     A[i] = (float)(s * k);
-    if (training) {
+    if (m.training) {
       Bc[i] = (float)(-s * k * sv.rstd[c] * (GY[c] / n));
       Cc[i] = (float)(-s * k * (G[c] / n) + dm / g.HW);
     } else {
@@ -432,45 +510,51 @@ se_bwd_sample_kernel(SeGeom g, int Cr, const float* __restrict__ w1,
       Cc[i] = (float)(dm / g.HW);
     }
   }
+  __syncthreads();
 }
 
-// part 3: parameter gradients of fc1 / fc2 (sums over the batch)
-__global__ void __launch_bounds__(256)
-se_bwd_param_kernel(SeGeom g, int Cr, float* __restrict__ save, const double* __restrict__ scratch,
-                    float* __restrict__ dw1, float* __restrict__ db1, float* __restrict__ dw2,
-                    float* __restrict__ db2) {
-  const int B = g.B, C = g.C;
-  SeSave sv = se_save_view(save, B, C, Cr);
-  const double* du = scratch + 2 * (size_t)C;
+__global__ void __launch_bounds__(256) se_bwd_sample_kernel(SeGeom g, SeBwdMid m) {
+  extern __shared__ __attribute__((aligned(16))) double smd[];  // dh[Cr]
+  se_bwd_sample_body(g, m, blockIdx.x, smd);
+}
+
+// parameter step, output i of [dw2 | dw1 | db2 | db1] (sums over the batch)
+ACC_DEV void se_bwd_param_body(const SeGeom& g, const SeBwdMid& m, long i) {
+  const int B = g.B, C = g.C, Cr = m.Cr;
+  SeSave sv = se_save_view(m.save, B, C, Cr);
+  const double* du = m.scratch + 2 * (size_t)C;
   const double* dh = du + (size_t)B * C;
   const long nW = (long)C * Cr;
-  const long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
   if (i < nW) {  // dw2[c][j] = sum_b du[b,c] * lrelu(hpre[b,j])
     int c = (int)(i / Cr), j = (int)(i % Cr);
     double acc = 0.0;
-    #pragma unroll 8
+#pragma unroll 8
     for (int b = 0; b < B; ++b) acc += du[b * C + c] * lrelu(sv.hpre[b * Cr + j]);
-    dw2[i] = (float)acc;
+    m.dw2[i] = (float)acc;
   } else if (i < 2 * nW) {  // dw1[j][c] = sum_b dh[b,j] * m[b,c]
     long t = i - nW;
     int j = (int)(t / C), c = (int)(t % C);
     double acc = 0.0;
-    #pragma unroll 8
+#pragma unroll 8
     for (int b = 0; b < B; ++b) acc += dh[b * Cr + j] * (sv.S[b * C + c] / g.HW);
-    dw1[t] = (float)acc;
+    m.dw1[t] = (float)acc;
   } else if (i < 2 * nW + C) {
     int c = (int)(i - 2 * nW);
     double acc = 0.0;
-    #pragma unroll 8
+#pragma unroll 8
     for (int b = 0; b < B; ++b) acc += du[b * C + c];
-    db2[c] = (float)acc;
+    m.db2[c] = (float)acc;
   } else if (i < 2 * nW + C + Cr) {
     int j = (int)(i - 2 * nW - C);
     double acc = 0.0;
-    #pragma unroll 8
+#pragma unroll 8
     for (int b = 0; b < B; ++b) acc += dh[b * Cr + j];
-    db1[j] = (float)acc;
+    m.db1[j] = (float)acc;
   }
+}
+
+__global__ void __launch_bounds__(256) se_bwd_param_kernel(SeGeom g, SeBwdMid m) {
+  se_bwd_param_body(g, m, blockIdx.x * (long)blockDim.x + threadIdx.x);
 }
 
 template <int V, typename T>
@@ -515,6 +599,60 @@ se_bwd_apply_kernel(const T* __restrict__ z, const T* __restrict__ dout,
   }
 }
 
+#define SE_PRO_NQ 8  // T1, T2, U1, U2, U3, W1, W2, W3
+
+// prologue coefficient step, channel c (lane `lane` of its group): the prologue BN's
+// backward coefficients dz = k1*g + k2*(z - mean1) + k3, dgamma1 = sum g*xhat,
+// dbeta1 = sum g, from the per-(b,c) sums UW[i][B*C] (i = 0..5 -> U1 U2 U3 W1 W2 W3)
+// and the SE coefficients A, Bc, Cc.
+ACC_DEV void se_pro_coef_body(const SeGeom& g, const SeBwdMid& m, int c, int lane) {
+  const int B = g.B, C = g.C;
+  const bool live = c < C;
+  SeSave sv = se_save_view(m.save, B, C, m.Cr);
+  const long BC = (long)B * C;
+  const double* UW = se_T1(g, m) + 2 * BC;
+  const float* A = m.coef;
+  const float* Bc = A + BC;
+  const float* Cc = Bc + BC;
+  double sg = 0.0, sgx = 0.0;
+  if (live) {
+    const double mean = sv.mean[c];
+    for (int b = lane; b < B; b += SE_LANES) {
+      const long i = (long)b * C + c;
+      const double a = A[i], bb = Bc[i], s = sv.sg[i];
+      const double cst = (double)Cc[i] - bb * mean;
+      sg += a * *(UW + 0 * BC + i) + bb * s * *(UW + 1 * BC + i) +
+            cst * *(UW + 2 * BC + i);
+      sgx += a * *(UW + 3 * BC + i) + bb * s * *(UW + 4 * BC + i) +
+             cst * *(UW + 5 * BC + i);
+    }
+  }
+  sg = se_lane_sum(sg);
+  sgx = se_lane_sum(sgx);
+  if (!live || lane != 0) return;
+  const float rstd1 = m.pst[BN_RSTD * C + c];
+  sgx *= rstd1;  // sum g*xhat
+  if (m.dpg) m.dpg[c] = (float)sgx;
+  if (m.dpb) m.dpb[c] = (float)sg;
+  const double n = (double)B * g.HW;
+  const float ga = m.pgamma ? m.pgamma[c] : 1.f;
+  const float k1 = ga * rstd1;
+  float k2 = 0.f, k3 = 0.f;
+  if (m.ptraining) {  // same coefficients as bn_bwd_finalize_kernel (csrc/bn.hip)
+    const float mg = (float)(sg / n), mgx = (float)(sgx / n);
+    k2 = -k1 * rstd1 * mgx;
+    k3 = -k1 * mg;
+  }
+  m.pcoef[c] = k1;
+  m.pcoef[C + c] = k2;
+  m.pcoef[2 * C + c] = k3;
+}
+
+__global__ void __launch_bounds__(256) se_pro_coef_kernel(SeGeom g, SeBwdMid m) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  se_pro_coef_body(g, m, gid / SE_LANES, gid % SE_LANES);
+}
+
 // ---------------------------------------------------------------------------
 // SE backward fused with the backward of the BatchNorm(+act) prologue that feeds it
 // (the preceding layer's BN: HANCBlock.norm3 :281-283, ResPath.bns[i] :326,
@@ -530,8 +668,6 @@ se_bwd_apply_kernel(const T* __restrict__ z, const T* __restrict__ dout,
 // the pair costs 2 read passes of (z, dout) + 1 write of dz, instead of 4 read
 // passes + 2 writes (da is never materialised).
 // ---------------------------------------------------------------------------
-#define SE_PRO_NQ 8  // T1, T2, U1, U2, U3, W1, W2, W3
-
 template <int V, typename T>
 __global__ void __launch_bounds__(256)
 se_bwd_reduce_pro_kernel(const T* __restrict__ z, const T* __restrict__ dout,
@@ -558,10 +694,7 @@ se_bwd_reduce_pro_kernel(const T* __restrict__ z, const T* __restrict__ dout,
       al[j] = alpha[b * C + t.c0 + j];
       be[j] = betap[t.c0 + j];
     }
-    for (long r = r0 + t.rg; r < r1; r += t.RG) {
-      float v[V], d[V];
-      ldv<V>(z + r * C + t.c0, v);
-      ldv<V>(dout + r * C + t.c0, d);
+    auto row = [&](const float (&v)[V], const float (&d)[V]) {
 #pragma unroll
       for (int j = 0; j < V; ++j) {
         const float pre = v[j] * s[j] + h[j];
@@ -579,60 +712,17 @@ se_bwd_reduce_pro_kernel(const T* __restrict__ z, const T* __restrict__ dout,
         acc[6][j] += la * xc;
         acc[7][j] += lp * xc;
       }
+    };
+    // plain row loop: the 8 fp64 accumulators per channel already hold 64 VGPRs, and
+    // the unrolled buffer-load form (quad_rows2) costs a wave of occupancy (measured)
+    for (long r = r0 + t.rg; r < r1; r += t.RG) {
+      float v[V], d[V];
+      ldv<V>(z + r * C + t.c0, v);
+      ldv<V>(dout + r * C + t.c0, d);
+      row(v, d);
     }
   }
   block_chan_reduceN<V, SE_PRO_NQ>(t, acc, part, blockIdx.x, C);
-}
-
-// one thread per channel: the prologue BN's backward coefficients
-//   dz = k1*g + k2*(z - mean1) + k3, dgamma1 = sum g*xhat, dbeta1 = sum g
-// from the per-(b,c) sums (UW[i][B*C], i = 0..5 -> U1 U2 U3 W1 W2 W3) and the SE
-// coefficients A, Bc, Cc.
-__global__ void __launch_bounds__(256)
-se_pro_coef_kernel(SeGeom g, int Cr, const float* __restrict__ save,
-                   const double* __restrict__ UW, const float* __restrict__ coef,
-                   const float* __restrict__ pst, const float* __restrict__ pgamma,
-                   int ptraining, float* __restrict__ dpg, float* __restrict__ dpb,
-                   float* __restrict__ pcoef) {
-  const int B = g.B, C = g.C;
-  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  const int c = gid / SE_LANES, lane = gid % SE_LANES;  // SE_LANES lanes per channel
-  const bool live = c < C;
-  SeSave sv = se_save_view(const_cast<float*>(save), B, C, Cr);
-  const long BC = (long)B * C;
-  const float* A = coef;
-  const float* Bc = A + BC;
-  const float* Cc = Bc + BC;
-  double sg = 0.0, sgx = 0.0;
-  if (live) {
-    const double mean = sv.mean[c];
-    for (int b = lane; b < B; b += SE_LANES) {
-      const long i = (long)b * C + c;
-      const double a = A[i], bb = Bc[i], s = sv.sg[i];
-      const double cst = (double)Cc[i] - bb * mean;
-      sg += a * UW[0 * BC + i] + bb * s * UW[1 * BC + i] + cst * UW[2 * BC + i];
-      sgx += a * UW[3 * BC + i] + bb * s * UW[4 * BC + i] + cst * UW[5 * BC + i];
-    }
-  }
-  sg = se_lane_sum(sg);
-  sgx = se_lane_sum(sgx);
-  if (!live || lane != 0) return;
-  const float rstd1 = pst[BN_RSTD * C + c];
-  sgx *= rstd1;  // sum g*xhat
-  if (dpg) dpg[c] = (float)sgx;
-  if (dpb) dpb[c] = (float)sg;
-  const double n = (double)B * g.HW;
-  const float ga = pgamma ? pgamma[c] : 1.f;
-  const float k1 = ga * rstd1;
-  float k2 = 0.f, k3 = 0.f;
-  if (ptraining) {  // same coefficients as bn_bwd_finalize_kernel (csrc/bn.hip)
-    const float mg = (float)(sg / n), mgx = (float)(sgx / n);
-    k2 = -k1 * rstd1 * mgx;
-    k3 = -k1 * mg;
-  }
-  pcoef[c] = k1;
-  pcoef[C + c] = k2;
-  pcoef[2 * C + c] = k3;
 }
 
 template <int V, typename T>
@@ -676,33 +766,36 @@ se_bwd_apply_pro_kernel(const T* __restrict__ z, const T* __restrict__ dout,
     k2[j] = pcoef[C + c];
     k3[j] = pcoef[2 * C + c];
   }
-  constexpr int U = 2;  // rows per iteration with all loads issued first
-  for (long rb = r0 + t.rg; rb < r1; rb += U * t.RG) {
-    float v[U][V], d[U][V];
+  const bool want_cs = colsum != nullptr;
+  auto row = [&](bool ok, float (&v)[V], float (&d)[V]) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const long r = rb + (long)u * t.RG;
-      if (r < r1) {
-        ldv<V>(z + r * C + t.c0, v[u]);
-        ldv<V>(dout + r * C + t.c0, d[u]);
-      }
+    for (int j = 0; j < V; ++j) {
+      const float pre = v[j] * s[j] + h[j];
+      const float x = apply_act(pre, act);
+      const float g2 = d[j] * lrelu_d(al[j] * x + be[j]);
+      float da = A[j] * g2 + Bc[j] * (x * sgv[j] - mu[j]) + Cc[j];
+      if (act == ACT_LRELU) da *= lrelu_d(pre);
+      d[j] = rnd<T>(k1[j] * da + k2[j] * (v[j] - mu1[j]) + k3[j]);
+      cs[j] += (want_cs && ok) ? (double)d[j] : 0.0;
     }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const long r = rb + (long)u * t.RG;
-      if (r < r1) {
-#pragma unroll
-        for (int j = 0; j < V; ++j) {
-          const float pre = v[u][j] * s[j] + h[j];
-          const float x = apply_act(pre, act);
-          const float g2 = d[u][j] * lrelu_d(al[j] * x + be[j]);
-          float da = A[j] * g2 + Bc[j] * (x * sgv[j] - mu[j]) + Cc[j];
-          if (act == ACT_LRELU) da *= lrelu_d(pre);
-          d[u][j] = rnd<T>(k1[j] * da + k2[j] * (v[u][j] - mu1[j]) + k3[j]);
-          if (colsum) cs[j] += d[u][j];
-        }
-        stv<V>(dz + r * C + t.c0, d[u]);
-      }
+  };
+  if constexpr (V == 4) {
+    const long nr = r1 > r0 ? r1 - r0 : 0;
+    const __amdgpu_buffer_rsrc_t ro = acc_rsrc(dz + r0 * C, (unsigned)(nr * C * sizeof(T)));
+    quad_rows2<4>(z + r0 * C, dout + r0 * C, nr, t.rg, t.RG, C, t.c0,
+                  [&](bool ok, float4 z4, float4 d4, unsigned off) {
+                    float v[V] = {z4.x, z4.y, z4.z, z4.w};  // V == 4 here
+                    float d[V] = {d4.x, d4.y, d4.z, d4.w};
+                    row(ok, v, d);
+                    bufq_st<0>(ro, off, make_float4(d[0], d[1 % V], d[2 % V], d[3 % V]), (T*)nullptr);
+                  });
+  } else {
+    for (long r = r0 + t.rg; r < r1; r += t.RG) {
+      float v[V], d[V];
+      ldv<V>(z + r * C + t.c0, v);
+      ldv<V>(dout + r * C + t.c0, d);
+      row(true, v, d);
+      stv<V>(dz + r * C + t.c0, d);
     }
   }
   if (colsum) block_chan_reduce2<V>(t, cs, cz, colsum, blockIdx.x, g.C);
@@ -740,6 +833,11 @@ extern "C" size_t accunet_se_ws_elems(int B, int HW, int C, int Cr) {
          se_dsum_scr_floats(g);
 }
 
+// the streaming loops address a row chunk through one buffer descriptor (< 2^31 bytes)
+static bool se_chunk_ok(const SeGeom& g, int dt) {
+  return g.rows_per * (long)g.C * (dt == ACC_BF16 ? 2 : 4) < (1L << 31);
+}
+
 extern "C" int accunet_se_fwd(const void* z, const float* sc, const float* sh, int act, int B,
                               int HW, int C, int Cr, const float* w1, const float* b1,
                               const float* w2, const float* b2, const float* gamma,
@@ -751,45 +849,60 @@ extern "C" int accunet_se_fwd(const void* z, const float* sc, const float* sh, i
   if (ws_elems < accunet_se_ws_elems(B, HW, C, Cr)) return ACC_EBADARG;
   if (((uintptr_t)ws & 7) || ((uintptr_t)save & 7)) return ACC_EBADARG;
   SeGeom g = se_geom(B, HW, C);
+  if (!se_chunk_ok(g, dt)) return ACC_EBADSHAPE;
   int V = (C % 4 == 0) ? 4 : 1;
   dim3 grid(B * g.NCH, ceil_div(C / V, 64));
   double* part = reinterpret_cast<double*>(ws);
+  SeMid m{Cr, w1, b1, w2, b2, gamma, beta, rmean, rvar, training ? nbt : nullptr,
+          momentum, eps, training, save};
+  const bool pro = sc != nullptr;
   with_dt(dt, [&](auto tag) {
     using T = decltype(tag);
-    if (V == 4)
-      hipLaunchKernelGGL((se_reduce_kernel<4, T>), grid, dim3(256), 0, s, (const T*)z, sc, sh, act,
-                         g, part);
-    else
-      hipLaunchKernelGGL((se_reduce_kernel<1, T>), grid, dim3(256), 0, s, (const T*)z, sc, sh, act,
-                         g, part);
+    auto go = [&](auto kv, auto kp) {
+      constexpr int KV = decltype(kv)::value;
+      constexpr bool KP = decltype(kp)::value;
+      hipLaunchKernelGGL((se_reduce_kernel<KV, T, KP>), grid, dim3(256), 0, s, (const T*)z, sc, sh,
+                         act, g, part);
+    };
+    using I4 = std::integral_constant<int, 4>;
+    using I1 = std::integral_constant<int, 1>;
+    if (V == 4) pro ? go(I4{}, std::true_type{}) : go(I4{}, std::false_type{});
+    else pro ? go(I1{}, std::true_type{}) : go(I1{}, std::false_type{});
   });
   // S, Q and the gate per sample, then the BN-of-gated statistics per channel
   hipLaunchKernelGGL(se_mid_sample_kernel, dim3(B), dim3(256), (C + Cr) * sizeof(float), s, part,
-                     g, Cr, w1, b1, w2, b2, save);
-  hipLaunchKernelGGL(se_mid_bn_kernel, dim3(ceil_div(C, 256)), dim3(256), 0, s, g, Cr, gamma, beta,
-                     rmean, rvar, momentum, eps, training, save, training ? nbt : nullptr);
+                     g, m);
+  hipLaunchKernelGGL(se_mid_bn_kernel, dim3(ceil_div(C, 256)), dim3(256), 0, s, g, m);
   const float* alpha = save + se_alpha_offset(B, C, Cr);
   const float* betap = alpha + (size_t)B * C;
   with_dt(dt, [&](auto tag) {
     using T = decltype(tag);
-    if (V == 4)
-      hipLaunchKernelGGL((se_apply_kernel<4, T>), grid, dim3(256), 0, s, (const T*)z, sc, sh, act, g,
-                         alpha, betap, (T*)out, ostats);
-    else
-      hipLaunchKernelGGL((se_apply_kernel<1, T>), grid, dim3(256), 0, s, (const T*)z, sc, sh, act, g,
-                         alpha, betap, (T*)out, ostats);
+    if (V == 4) {
+      if (pro)
+        hipLaunchKernelGGL((se_apply_kernel<4, T, true>), grid, dim3(256), 0, s, (const T*)z, sc,
+                           sh, act, g, alpha, betap, (T*)out, ostats);
+      else
+        hipLaunchKernelGGL((se_apply_kernel<4, T, false>), grid, dim3(256), 0, s, (const T*)z, sc,
+                           sh, act, g, alpha, betap, (T*)out, ostats);
+    } else {
+      if (pro)
+        hipLaunchKernelGGL((se_apply_kernel<1, T, true>), grid, dim3(256), 0, s, (const T*)z, sc,
+                           sh, act, g, alpha, betap, (T*)out, ostats);
+      else
+        hipLaunchKernelGGL((se_apply_kernel<1, T, false>), grid, dim3(256), 0, s, (const T*)z, sc,
+                           sh, act, g, alpha, betap, (T*)out, ostats);
+    }
   });
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 
-// shared by accunet_se_bwd / accunet_se_bwd_pro: the per-(b,c) sums in scratch (from
-// part) -> BN / gate / fc backward, coef (A, Bc, Cc), fc parameter gradients
-static void se_bwd_mid(const SeGeom& g, int Cr, const double* part, int nq, const float* w1,
-                       const float* w2, const float* gamma, int training, float* sv,
-                       double* scratch, float* coef, float* dw1, float* db1, float* dw2,
-                       float* db2, float* dgamma, float* dbeta, hipStream_t s) {
-  const int B = g.B, C = g.C;
-  double* T1 = scratch + 2 * (size_t)C + (size_t)B * C + (size_t)B * Cr;
+// the unfused backward middle step: per-(b,c) sums in scratch (from part) -> BN /
+// gate / fc backward, coef (A, Bc, Cc), fc parameter gradients (+ the prologue
+// coefficient step when m.pcoef is set)
+static void se_bwd_mid(const SeGeom& g, const SeBwdMid& m, const double* part, int nq,
+                       hipStream_t s) {
+  const int B = g.B, C = g.C, Cr = m.Cr;
+  double* T1 = m.scratch + 2 * (size_t)C + (size_t)B * C + (size_t)B * Cr;
   if (nq == 2)
     hipLaunchKernelGGL(se_part_sum_kernel<2>, dim3(ceil_div(C, 64), B), dim3(256), 0, s, part, g,
                        T1);
@@ -797,13 +910,14 @@ static void se_bwd_mid(const SeGeom& g, int Cr, const double* part, int nq, cons
     hipLaunchKernelGGL(se_part_sum_kernel<SE_PRO_NQ>, dim3(ceil_div(C, 64), B), dim3(256), 0, s,
                        part, g, T1);
   hipLaunchKernelGGL(se_bwd_chan_kernel, dim3(ceil_div((long)C * SE_LANES, 256)), dim3(256), 0, s,
-                     g, Cr, gamma,
-                     training, sv, dgamma, dbeta, scratch);
+                     g, m);
   hipLaunchKernelGGL(se_bwd_sample_kernel, dim3(B), dim3(256), (Cr > 0 ? Cr : 1) * sizeof(double),
-                     s, g, Cr, w1, w2, gamma, training, sv, scratch, coef);
+                     s, g, m);
   long nparam = 2L * C * Cr + C + Cr;
-  hipLaunchKernelGGL(se_bwd_param_kernel, dim3(ceil_div(nparam, 256)), dim3(256), 0, s, g, Cr, sv,
-                     scratch, dw1, db1, dw2, db2);
+  hipLaunchKernelGGL(se_bwd_param_kernel, dim3(ceil_div(nparam, 256)), dim3(256), 0, s, g, m);
+  if (m.pcoef)
+    hipLaunchKernelGGL(se_pro_coef_kernel, dim3(ceil_div((long)C * SE_LANES, 256)), dim3(256), 0,
+                       s, g, m);
 }
 
 extern "C" int accunet_se_bwd(const void* z, const void* dout, const float* sc, const float* sh,
@@ -835,9 +949,9 @@ extern "C" int accunet_se_bwd(const void* z, const void* dout, const float* sc, 
       hipLaunchKernelGGL((se_bwd_reduce_kernel<1, T>), grid, dim3(256), 0, s, (const T*)z,
                          (const T*)dout, sc, sh, act, g, alpha, betap, part);
   });
-  float* sv = const_cast<float*>(save);
-  se_bwd_mid(g, Cr, part, 2, w1, w2, gamma, training, sv, scratch, coef, dw1, db1, dw2, db2,
-             dgamma, dbeta, s);
+  SeBwdMid m{Cr, w1, w2, gamma, training, const_cast<float*>(save), scratch, coef,
+             dw1, db1, dw2, db2, dgamma, dbeta, nullptr, nullptr, 0, nullptr, nullptr, nullptr};
+  se_bwd_mid(g, m, part, 2, s);
   with_dt(dt, [&](auto tag) {
     using T = decltype(tag);
     if (V == 4)
@@ -864,6 +978,7 @@ extern "C" int accunet_se_bwd_pro(const void* z, const void* dout, const float* 
   if (((uintptr_t)ws & 7) || ((uintptr_t)save & 7)) return ACC_EBADARG;
   if (!pst || !dz) return ACC_EBADARG;
   SeGeom g = se_geom(B, HW, C);
+  if (!se_chunk_ok(g, dt)) return ACC_EBADSHAPE;
   int V = (C % 4 == 0) ? 4 : 1;
   dim3 grid(B * g.NCH, ceil_div(C / V, 64));
   double* part = reinterpret_cast<double*>(ws);
@@ -876,6 +991,8 @@ extern "C" int accunet_se_bwd_pro(const void* z, const void* dout, const float* 
   const float* betap = alpha + (size_t)B * C;
   const float* sgate = save + (size_t)B * C * 4 + (size_t)B * Cr;
   const float* mean = sgate + (size_t)B * C;
+  SeBwdMid m{Cr, w1, w2, gamma, training, const_cast<float*>(save), scratch, coef,
+             dw1, db1, dw2, db2, dgamma, dbeta, pst, pgamma, ptraining, dpgamma, dpbeta, pcoef};
   with_dt(dt, [&](auto tag) {
     using T = decltype(tag);
     if (V == 4)
@@ -885,14 +1002,8 @@ extern "C" int accunet_se_bwd_pro(const void* z, const void* dout, const float* 
       hipLaunchKernelGGL((se_bwd_reduce_pro_kernel<1, T>), grid, dim3(256), 0, s, (const T*)z,
                          (const T*)dout, pst, act, g, alpha, betap, part);
   });
-  float* sv = const_cast<float*>(save);
-  se_bwd_mid(g, Cr, part, SE_PRO_NQ, w1, w2, gamma, training, sv, scratch, coef, dw1, db1, dw2,
-             db2, dgamma, dbeta, s);
-  const double* UW = scratch + 2 * (size_t)C + (size_t)B * C + (size_t)B * Cr + 2 * (size_t)B * C;
-  hipLaunchKernelGGL(se_pro_coef_kernel, dim3(ceil_div((long)C * SE_LANES, 256)), dim3(256), 0, s,
-                     g, Cr, save, UW,
-                     coef, pst, pgamma, ptraining, dpgamma, dpbeta, pcoef);
-  // the reduce-pass partials are consumed by the mid kernels: reuse them for dz's column sums
+  se_bwd_mid(g, m, part, SE_PRO_NQ, s);
+  // the reduce-pass partials are consumed by the middle step: reuse them for dz's column sums
   double* cpart = dsum ? part : nullptr;
   with_dt(dt, [&](auto tag) {
     using T = decltype(tag);
