@@ -98,11 +98,12 @@ class Conv2d_batchnorm(nn.Module):
         if tuple(ks) != (1, 1) or tuple(self.conv1.stride) != (1, 1):
             raise NotImplementedError("Conv2d_batchnorm: only the 1x1 / stride-1 form ACC-UNet uses")
 
-    def run(self, srcs, *, w_off=0, ups=(), weight=None, consumer_bn=None, slots=None):
+    def run(self, srcs, *, w_off=0, ups=(), weight=None, consumer_bn=None, slots=None,
+            wslot=None):
         self._check()
         w = self.conv1.weight if weight is None else weight
         z = ops.pw_conv(srcs, w, self.conv1.bias, w_off=w_off, ups=ups,
-                        consumer_bn=self.batchnorm, slots=slots)
+                        consumer_bn=self.batchnorm, slots=slots, wslot=wslot)
         return self.sqe.run(z, consumer_bn=consumer_bn)
 
     def forward(self, x):
@@ -254,15 +255,16 @@ class MLFC(nn.Module):
             for l in range(4):
                 blk = getattr(self, f"cnv_blks{l + 1}")[i]
                 w = blk.conv1.weight
+                ws = ops.GradSlot()  # the calls below write disjoint column slices of w
                 # levels coarser than l: 1x1 conv at their own resolution, nearest-up add
                 ups = []
                 for m in range(l + 1, 4):
                     g = ops.pw_conv([xs[m]], w, None, w_off=offs[m], want_stats=False,
-                                    slots=[sl[(m, m)]]).z
+                                    slots=[sl[(m, m)]], wslot=ws).z
                     ups.append((g, _log2(1 << (m - l)), 0))
                 srcs = [at[(m, l)] for m in range(l + 1)]
                 v1 = blk.run(srcs, ups=ups, consumer_bn=getattr(self, f"bns{l + 1}")[i],
-                             slots=[sl[(m, l)] for m in range(l + 1)])
+                             slots=[sl[(m, l)] for m in range(l + 1)], wslot=ws)
                 xcs.append(ops.bn_act_add(v1).z)  # act(bns_l(.)) materialised
             for l in range(4):
                 mrg = getattr(self, f"cnv_mrg{l + 1}")[i]

@@ -291,6 +291,7 @@ class _PWCfg:
     has_bias: bool = True
     bslot: object = None
     slots: Optional[List] = None  # per source: GradSlot or None
+    wslot: object = None  # GradSlot shared by the calls that write column slices of one weight
 
 
 class _PWConvFn(torch.autograd.Function):
@@ -332,6 +333,8 @@ class _PWConvFn(torch.autograd.Function):
         slots = ctx.cfg.slots or [None] * ctx.cfg.nsrc
         if dZ is None:  # output unused: every input gradient is zero
             d_srcs = [sl.done() if sl is not None else None for sl in slots]
+            if ctx.cfg.wslot is not None:
+                raise RuntimeError("pw_conv: a weight-slice GradSlot call must reach the loss")
             return (None,) * 5 + tuple(d_srcs) + (None,) * len(ctx.up_shapes)
         cfg = ctx.cfg
         weight, pro_g, *srcs = ctx.saved_tensors
@@ -374,7 +377,10 @@ class _PWConvFn(torch.autograd.Function):
         dW = None
         if nig[1]:
             full = (cfg.w_off == 0 and kbeg[-1] == cfg.w_ld)
-            dW = torch.zeros_like(weight) if not full else torch.empty_like(weight)
+            if cfg.wslot is not None:  # the sharing calls write disjoint slices covering W
+                dW, _ = cfg.wslot.acc_target(weight.shape, weight)
+            else:
+                dW = torch.zeros_like(weight) if not full else torch.empty_like(weight)
             for s, (x, C) in enumerate(zip(srcs, cfg.src_ch)):
                 use_pro = (s == 0 and pro.active)
                 keep.append(kern.gemm(N, C, P, a=[dZ], lda=[N], amode=AMODE_COL, b=x, ldb=C,
@@ -398,17 +404,21 @@ class _PWConvFn(torch.autograd.Function):
                 torch.empty(shp, dtype=dZ.dtype, device=dZ.device)
             kern.upsample_bwd(dZ, N, 0, _flat_off(dG, off), ld, B, H, W, N, 1 << lg)
             d_ups.append(dG)
+        if cfg.wslot is not None:
+            dW = cfg.wslot.done()
         return (None, dW, dbias, dpro_g, dpro_b, *d_srcs, *d_ups)
 
 
 def pw_conv(srcs: Sequence, weight, bias, *, w_off: int = 0, ups: Sequence = (),
             consumer_bn=None, want_stats: Optional[bool] = None,
-            slots: Optional[Sequence] = None):
+            slots: Optional[Sequence] = None, wslot=None):
     """Z = sum_s src_s @ W[:, w_off + kbeg_s : ...]^T (+bias) (+ nearest-up adds).
 
     srcs[0] may be a Pending (its BatchNorm(+act) is applied in the GEMM prologue).
     ups: sequence of (G tensor [B, H>>lg, W>>lg, ld], log2 factor, column offset).
     slots: per source, a GradSlot collecting that source's gradient (or None).
+    wslot: GradSlot shared by every call that uses a column slice of `weight`, when
+        those slices cover it: one dW buffer, no zero fill, no autograd adds.
     Returns Pending(Z, consumer_bn, ...) carrying Z's partial statistics.
     """
     srcs = [as_pending(s) for s in srcs]
@@ -433,7 +443,8 @@ def pw_conv(srcs: Sequence, weight, bias, *, w_off: int = 0, ups: Sequence = (),
     cfg = _PWCfg(nsrc=len(srcs), src_ch=[s.z.shape[-1] for s in srcs], pro=pro, w_off=w_off,
                  w_ld=w_ld, N=N, B=B, H=H, W=W,
                  ups=[(lg, off, g.shape[-1]) for g, lg, off in ups], want_stats=want_stats,
-                 has_bias=bias is not None, bslot=_bias_slot(bias, consumer_bn), slots=slots)
+                 has_bias=bias is not None, bslot=_bias_slot(bias, consumer_bn), slots=slots,
+                 wslot=_slot_reg(wslot) if weight.requires_grad else None)
     pg, pb = _bn_params(srcs[0])
     Z, stats = _PWConvFn.apply(cfg, w2, bias, pg, pb, *[s.z for s in srcs],
                                *[g for g, _, _ in ups])
