@@ -114,43 +114,53 @@ gemm_bf16_kernel(const GemmParams p) {
 
   const TA* A0 = (const TA*)p.A[0];
   const TB* Bp = (const TB*)p.B;
+  // Staged operands stay raw until store_tiles: the vector paths (VA / VB) load
+  // unconditionally (masked chunks read a valid address and are zeroed at the store)
+  // and convert / apply the prologue only when parking in LDS, so the compiler waits
+  // for the loads there, after this k-tile's MFMAs, not right after issuing them.
+  // The scalar fallback paths (!VA / !VB) finish their chunk at load time.
+  constexpr bool BF = sizeof(TB) == 4;  // fp32 B operand (weights): rounded at the store
   uint4 ra[NPA], rb[NPB];
+  float4 rbl[BF ? NPB : 1], rbh[BF ? NPB : 1];
+  float4 asl[PRO_A != PRO_NONE ? NPA : 1], ash[PRO_A != PRO_NONE ? NPA : 1];
+  float4 asl2[PRO_A != PRO_NONE ? NPA : 1], ash2[PRO_A != PRO_NONE ? NPA : 1];
+  bool aok[NPA], apro[NPA], bok[NPB];
 
   auto load_tiles = [&](int k0) {
     // ------------------------------ A ---------------------------------------
 #pragma unroll
     for (int i = 0; i < NPA; ++i) {
       const int c = tid + i * GEMM_THREADS;
-      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      aok[i] = false;
+      apro[i] = false;
       if (AMODE == AM_ROW) {
         const int r = c / (BK / 8), q = c % (BK / 8);
         const int g = m0 + r, k = k0 + 8 * q;
-        if (c < NCA && g < M) {
-          if (VA) {
-            if (k < K) {
-              // source of this chunk (widths % 8 == 0: a chunk never straddles a seam);
-              // explicit selects keep base / ld / kbeg scalar (see gemm_f32.h)
-              const TA* base = A0;
-              int ld = p.lda[0], kb = 0;
-              if (p.nsrc > 1) {
-                if (k >= p.kbeg[1]) { base = (const TA*)p.A[1]; ld = p.lda[1]; kb = p.kbeg[1]; }
-                if (p.nsrc > 2 && k >= p.kbeg[2]) { base = (const TA*)p.A[2]; ld = p.lda[2]; kb = p.kbeg[2]; }
-                if (p.nsrc > 3 && k >= p.kbeg[3]) { base = (const TA*)p.A[3]; ld = p.lda[3]; kb = p.kbeg[3]; }
-              }
-              const TA* src = base + (long)g * ld + (k - kb);
-              if (PRO_A != PRO_NONE && kb == 0) {  // the pending BatchNorm sits on source 0
-                float f[8], sc[8], sh[8];
-                ld8f(src, f);
-                ld8f(p.a_scale + k, sc);
-                ld8f(p.a_shift + k, sh);
-#pragma unroll
-                for (int j = 0; j < 8; ++j) f[j] = pro_apply<PRO_A>(f[j], sc[j], sh[j]);
-                v = pack8(f);
-              } else {
-                v = ld8_bf(src);
-              }
-            }
-          } else {
+        if (VA) {
+          const bool ok = c < NCA && g < M && k < K;
+          // source of this chunk (widths % 8 == 0: a chunk never straddles a seam);
+          // explicit selects keep base / ld / kbeg scalar (see gemm_f32.h)
+          const TA* base = A0;
+          int ld = p.lda[0], kb = 0;
+          if (p.nsrc > 1) {
+            if (k >= p.kbeg[1]) { base = (const TA*)p.A[1]; ld = p.lda[1]; kb = p.kbeg[1]; }
+            if (p.nsrc > 2 && k >= p.kbeg[2]) { base = (const TA*)p.A[2]; ld = p.lda[2]; kb = p.kbeg[2]; }
+            if (p.nsrc > 3 && k >= p.kbeg[3]) { base = (const TA*)p.A[3]; ld = p.lda[3]; kb = p.kbeg[3]; }
+          }
+          const TA* src = ok ? base + (long)g * ld + (k - kb) : A0;
+          ra[i] = ld8_bf(src);
+          aok[i] = ok;
+          if (PRO_A != PRO_NONE) {  // the pending BatchNorm sits on source 0
+            apro[i] = kb == 0;
+            const int kk = ok ? k : 0;
+            asl[i] = ld4(p.a_scale + kk);
+            asl2[i] = ld4(p.a_scale + kk + 4);
+            ash[i] = ld4(p.a_shift + kk);
+            ash2[i] = ld4(p.a_shift + kk + 4);
+          }
+        } else {
+          uint4 v = make_uint4(0u, 0u, 0u, 0u);
+          if (c < NCA && g < M) {
             float f[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
@@ -168,22 +178,23 @@ gemm_bf16_kernel(const GemmParams p) {
             }
             v = pack8(f);
           }
+          ra[i] = v;
         }
       } else if (AMODE == AM_SHIFT3) {
         const int r = c / (BK / 8), q = c % (BK / 8);
         const int g = m0 + r, k = k0 + 8 * q;
         const int lda = p.lda[0];
-        if (c < NCA && g < M) {
-          if (VA) {  // cin % 8 == 0: the chunk shares one tap
-            if (k < K) {
-              const int tap = (int)fdiv((uint32_t)k, p.fC);
-              const int ci = k - tap * p.cin;
-              const int dh = tap / 3 - 1, dw = tap - (tap / 3) * 3 - 1;
-              const int hh = a_h[i] + dh, ww = a_w[i] + dw;
-              if (hh >= 0 && hh < p.H && ww >= 0 && ww < p.W)
-                v = ld8_bf(A0 + ((long)g + dh * p.W + dw) * lda + ci);
-            }
-          } else {
+        if (VA) {  // cin % 8 == 0: the chunk shares one tap
+          const int tap = (int)fdiv((uint32_t)k, p.fC);
+          const int ci = k - tap * p.cin;
+          const int dh = tap / 3 - 1, dw = tap - (tap / 3) * 3 - 1;
+          const int hh = a_h[i] + dh, ww = a_w[i] + dw;
+          const bool ok = c < NCA && g < M && k < K && hh >= 0 && hh < p.H && ww >= 0 && ww < p.W;
+          ra[i] = ld8_bf(ok ? A0 + ((long)g + dh * p.W + dw) * lda + ci : A0);
+          aok[i] = ok;
+        } else {
+          uint4 v = make_uint4(0u, 0u, 0u, 0u);
+          if (c < NCA && g < M) {
             float f[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
@@ -200,106 +211,148 @@ gemm_bf16_kernel(const GemmParams p) {
             }
             v = pack8(f);
           }
+          ra[i] = v;
         }
       } else {  // AM_COL (transposed): A(m,k) = A[k*lda + m], 8 consecutive m at one k
         const int kr = c % BK, cq = c / BK;
         const int k = k0 + kr, m = m0 + 8 * cq;
-        if (c < NCA && k < kend) {
-          const TA* src = A0 + (long)k * p.lda[0] + m;
-          if (VA) {
-            if (m < M) v = ld8_bf(src);
-          } else {
+        const TA* src = A0 + (long)k * p.lda[0] + m;
+        if (VA) {
+          const bool ok = c < NCA && k < kend && m < M;
+          ra[i] = ld8_bf(ok ? src : A0);
+          aok[i] = ok;
+        } else {
+          uint4 v = make_uint4(0u, 0u, 0u, 0u);
+          if (c < NCA && k < kend) {
             float f[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) f[j] = (m + j < M) ? ld1(src + j) : 0.f;
             v = pack8(f);
           }
+          ra[i] = v;
         }
       }
-      ra[i] = v;
     }
     // ------------------------------ B ---------------------------------------
 #pragma unroll
     for (int i = 0; i < NPB; ++i) {
       const int c = tid + i * GEMM_THREADS;
+      bok[i] = false;
+      const TB* src = Bp;
+      bool vec = false;  // this chunk goes through the raw (store-time) path
       uint4 v = make_uint4(0u, 0u, 0u, 0u);
       if (BMODE == BM_NT) {  // B(k,n) = B[n*ldb + k]: 8 consecutive k of row n
         const int r = c / (BK / 8), q = c % (BK / 8);
         const int n = n0 + r, k = k0 + 8 * q;
-        if (c < NCB && n < N) {
-          const TB* src = Bp + (long)n * p.ldb + k;
-          if (VB) {
-            if (k < kend) v = ld8_bf(src);
-          } else {
-            float f[8];
+        if (VB) {
+          bok[i] = c < NCB && n < N && k < kend;
+          src = bok[i] ? Bp + (long)n * p.ldb + k : Bp;
+          vec = true;
+        } else if (c < NCB && n < N) {
+          const TB* s0 = Bp + (long)n * p.ldb + k;
+          float f[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) f[j] = (k + j < kend) ? ld1(src + j) : 0.f;
-            v = pack8(f);
-          }
+          for (int j = 0; j < 8; ++j) f[j] = (k + j < kend) ? ld1(s0 + j) : 0.f;
+          v = pack8(f);
         }
       } else if (BMODE == BM_NN) {  // B(k,n) = B[k*ldb + n]: 8 consecutive n at one k
         const int kr = c % BK, cq = c / BK;
         const int k = k0 + kr, n = n0 + 8 * cq;
-        if (c < NCB && k < kend) {
-          const TB* src = Bp + (long)k * p.ldb + n;
+        if (VB) {
+          bok[i] = c < NCB && k < kend && n < N;
+          src = bok[i] ? Bp + (long)k * p.ldb + n : Bp;
+          vec = true;
+        } else if (c < NCB && k < kend) {
+          const TB* s0 = Bp + (long)k * p.ldb + n;
           float f[8];
-          if (VB) {
-            if (n < N) {
-              if (PRO_B == PRO_NONE) {
-                v = ld8_bf(src);
-              } else {
-                ld8f(src, f);
 #pragma unroll
-                for (int j = 0; j < 8; ++j) f[j] = pro_apply<PRO_B>(f[j], bsc[i][j], bsh[i][j]);
-                v = pack8(f);
-              }
+          for (int j = 0; j < 8; ++j) {
+            f[j] = 0.f;
+            if (n + j < N) {
+              f[j] = ld1(s0 + j);
+              if (PRO_B != PRO_NONE) f[j] = pro_apply<PRO_B>(f[j], bsc[i][j], bsh[i][j]);
             }
-          } else {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              f[j] = 0.f;
-              if (n + j < N) {
-                f[j] = ld1(src + j);
-                if (PRO_B != PRO_NONE) f[j] = pro_apply<PRO_B>(f[j], bsc[i][j], bsh[i][j]);
-              }
-            }
-            v = pack8(f);
           }
+          v = pack8(f);
         }
       } else {  // BM_NN_SHIFT3: B(k = pixel, n = tap*cin + ci) = X[shift_tap(k)*ldb + ci]
         const int kr = c % BK, cq = c / BK;
         const int k = k0 + kr, n = n0 + 8 * cq;
-        if (c < NCB && k < kend) {
-          const uint32_t qq = fdiv((uint32_t)k, p.fW);
-          const int ww0 = k - (int)qq * p.W;
-          const int hh0 = (int)(qq - fdiv(qq, p.fH) * p.H);
-          if (VB) {  // cin % 8 == 0: the chunk shares one tap
-            if (n < N) {
-              const int tap = (int)fdiv((uint32_t)n, p.fC);
-              const int ci = n - tap * p.cin;
+        const uint32_t qq = fdiv((uint32_t)k, p.fW);
+        const int ww0 = k - (int)qq * p.W;
+        const int hh0 = (int)(qq - fdiv(qq, p.fH) * p.H);
+        if (VB) {  // cin % 8 == 0: the chunk shares one tap
+          const int tap = (int)fdiv((uint32_t)n, p.fC);
+          const int ci = n - tap * p.cin;
+          const int dh = tap / 3 - 1, dw = tap - (tap / 3) * 3 - 1;
+          bok[i] = c < NCB && k < kend && n < N && hh0 + dh >= 0 && hh0 + dh < p.H &&
+                   ww0 + dw >= 0 && ww0 + dw < p.W;
+          src = bok[i] ? Bp + ((long)k + dh * p.W + dw) * p.ldb + ci : Bp;
+          vec = true;
+        } else if (c < NCB && k < kend) {
+          float f[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            f[j] = 0.f;
+            const int nn = n + j;
+            if (nn < N) {
+              const int tap = (int)fdiv((uint32_t)nn, p.fC);
+              const int ci = nn - tap * p.cin;
               const int dh = tap / 3 - 1, dw = tap - (tap / 3) * 3 - 1;
               if (hh0 + dh >= 0 && hh0 + dh < p.H && ww0 + dw >= 0 && ww0 + dw < p.W)
-                v = ld8_bf(Bp + ((long)k + dh * p.W + dw) * p.ldb + ci);
+                f[j] = ld1(Bp + ((long)k + dh * p.W + dw) * p.ldb + ci);
             }
-          } else {
-            float f[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              f[j] = 0.f;
-              const int nn = n + j;
-              if (nn < N) {
-                const int tap = (int)fdiv((uint32_t)nn, p.fC);
-                const int ci = nn - tap * p.cin;
-                const int dh = tap / 3 - 1, dw = tap - (tap / 3) * 3 - 1;
-                if (hh0 + dh >= 0 && hh0 + dh < p.H && ww0 + dw >= 0 && ww0 + dw < p.W)
-                  f[j] = ld1(Bp + ((long)k + dh * p.W + dw) * p.ldb + ci);
-              }
-            }
-            v = pack8(f);
           }
+          v = pack8(f);
         }
       }
-      rb[i] = v;
+      if (vec) {
+        if constexpr (BF) {
+          rbl[i] = ld4((const float*)src);
+          rbh[i] = ld4((const float*)src + 4);
+        } else {
+          rb[i] = *reinterpret_cast<const uint4*>(src);
+        }
+      } else {
+        rb[i] = v;
+      }
+    }
+  };
+
+  // the LDS image of A / B chunk i, finished from its raw staging registers
+  auto a_chunk = [&](int i) -> uint4 {
+    if (!VA) return ra[i];
+    const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+    if (PRO_A != PRO_NONE && AMODE == AM_ROW) {
+      float f[8];
+      unpack8(ra[i], f);
+      const float sc[8] = {asl[i].x, asl[i].y, asl[i].z, asl[i].w, asl2[i].x, asl2[i].y, asl2[i].z, asl2[i].w};
+      const float sh[8] = {ash[i].x, ash[i].y, ash[i].z, ash[i].w, ash2[i].x, ash2[i].y, ash2[i].z, ash2[i].w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = apro[i] ? pro_apply<PRO_A>(f[j], sc[j], sh[j]) : f[j];
+      return aok[i] ? pack8(f) : z;
+    }
+    return aok[i] ? ra[i] : z;
+  };
+  auto b_chunk = [&](int i) -> uint4 {
+    if (!VB) return rb[i];
+    const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+    if constexpr (BF) {
+      float f[8] = {rbl[i].x, rbl[i].y, rbl[i].z, rbl[i].w, rbh[i].x, rbh[i].y, rbh[i].z, rbh[i].w};
+      if (BMODE == BM_NN && PRO_B != PRO_NONE) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = pro_apply<PRO_B>(f[j], bsc[i][j], bsh[i][j]);
+      }
+      return bok[i] ? pack8(f) : z;
+    } else {
+      if (BMODE == BM_NN && PRO_B != PRO_NONE) {
+        float f[8];
+        unpack8(rb[i], f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = pro_apply<PRO_B>(f[j], bsc[i][j], bsh[i][j]);
+        return bok[i] ? pack8(f) : z;
+      }
+      return bok[i] ? rb[i] : z;
     }
   };
 
@@ -310,12 +363,13 @@ gemm_bf16_kernel(const GemmParams p) {
     for (int i = 0; i < NPA; ++i) {
       const int c = tid + i * GEMM_THREADS;
       if (c < NCA) {
+        const uint4 v = a_chunk(i);
         if (!TRA) {
-          *reinterpret_cast<uint4*>(as + (c / (BK / 8)) * SK + 8 * (c % (BK / 8))) = ra[i];
+          *reinterpret_cast<uint4*>(as + (c / (BK / 8)) * SK + 8 * (c % (BK / 8))) = v;
         } else {
           const int kr = c % BK, cq = c / BK;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) as[(8 * cq + j) * SK + kr] = u4get(ra[i], j);
+          for (int j = 0; j < 8; ++j) as[(8 * cq + j) * SK + kr] = u4get(v, j);
         }
       }
     }
@@ -323,12 +377,13 @@ gemm_bf16_kernel(const GemmParams p) {
     for (int i = 0; i < NPB; ++i) {
       const int c = tid + i * GEMM_THREADS;
       if (c < NCB) {
+        const uint4 v = b_chunk(i);
         if (!TRB) {
-          *reinterpret_cast<uint4*>(bs + (c / (BK / 8)) * SK + 8 * (c % (BK / 8))) = rb[i];
+          *reinterpret_cast<uint4*>(bs + (c / (BK / 8)) * SK + 8 * (c % (BK / 8))) = v;
         } else {
           const int kr = c % BK, cq = c / BK;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) bs[(8 * cq + j) * SK + kr] = u4get(rb[i], j);
+          for (int j = 0; j < 8; ++j) bs[(8 * cq + j) * SK + kr] = u4get(v, j);
         }
       }
     }
@@ -351,7 +406,12 @@ gemm_bf16_kernel(const GemmParams p) {
     __syncthreads();
     for (int kt = 0; kt < nkt; ++kt) {
       const int buf = kt & 1;
-      if (kt + 1 < nkt) load_tiles(kstart + (kt + 1) * BK);
+      // unconditional (the last iteration reloads its own tile, unused): no branch
+      // around the loads, so their waits are counted at the store below
+      load_tiles(kstart + min(kt + 1, nkt - 1) * BK);
+      // keep the loads ahead of this tile's MFMAs (the scheduler would otherwise sink
+      // them next to their LDS stores and expose their latency)
+      __builtin_amdgcn_sched_barrier(0);
       const bf16_t* as = As + buf * BM * SK;
       const bf16_t* bs = Bs + buf * BN * SK;
 #pragma unroll
@@ -369,6 +429,7 @@ gemm_bf16_kernel(const GemmParams p) {
           for (int j = 0; j < TN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
       }
+      __builtin_amdgcn_sched_barrier(0);
       if (kt + 1 < nkt) store_tiles(buf ^ 1);
       __syncthreads();
     }
