@@ -385,32 +385,48 @@ affine_act_kernel(const T* __restrict__ x, const float* __restrict__ sc,
       s[j] = sc ? sc[t.c0 + j] : 1.f;
       h[j] = sh ? sh[t.c0 + j] : 0.f;
     }
-    // rows are processed U at a time with all their loads issued first, so each
-    // thread keeps 2U-4U 16-byte loads in flight (latency hiding at 4 blocks/CU)
-    constexpr int U = 4;
-    for (long rb = r0 + t.rg; rb < r1; rb += U * t.RG) {
-      float v[U][V], q[U][V];
+    auto row = [&](bool ok, float (&v)[V], const float (&q)[V]) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        long r = rb + (long)u * t.RG;
-        if (r < r1) {
-          ldv<V>(x + r * C + t.c0, v[u]);
-          if (res) ldv<V>(res + r * C + t.c0, q[u]);
-        }
+      for (int j = 0; j < V; ++j) {
+        v[j] = apply_act(v[j] * s[j] + h[j], act);
+        if (res) v[j] += q[j];
+        if (y) v[j] = rnd<T>(v[j]);  // statistics of the stored value
+        const double e = ok ? (double)v[j] : 0.0;
+        a[j] += e;
+        b[j] += e * e;
       }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        long r = rb + (long)u * t.RG;
-        if (r < r1) {
-#pragma unroll
-          for (int j = 0; j < V; ++j) {
-            v[u][j] = apply_act(v[u][j] * s[j] + h[j], act);
-            if (res) v[u][j] += q[u][j];
-          }
-          if (y) stv_r<V>(y + r * C + t.c0, v[u]);  // y == nullptr: statistics only (accunet_colsum)
-#pragma unroll
-          for (int j = 0; j < V; ++j) { a[j] += v[u][j]; b[j] += (double)v[u][j] * v[u][j]; }
-        }
+    };
+    if constexpr (V == 4) {
+      // branch-free streaming (chan.h quad_rows*): rows past the chunk are masked
+      const long nr = r1 > r0 ? r1 - r0 : 0;
+      const __amdgpu_buffer_rsrc_t ry =
+          acc_rsrc(y ? y + r0 * C : x, y ? (unsigned)(nr * C * sizeof(T)) : 0u);
+      auto put = [&](const float (&v)[V], unsigned off) {
+        bufq_st<0>(ry, off, make_float4(v[0], v[1 % V], v[2 % V], v[3 % V]), (T*)nullptr);
+      };
+      if (res) {
+        quad_rows2<4>(x + r0 * C, res + r0 * C, nr, t.rg, t.RG, C, t.c0,
+                      [&](bool ok, float4 x4, float4 q4, unsigned off) {
+                        float v[V] = {x4.x, x4.y, x4.z, x4.w};
+                        const float q[V] = {q4.x, q4.y, q4.z, q4.w};
+                        row(ok, v, q);
+                        put(v, off);
+                      });
+      } else {
+        quad_rows1<8>(x + r0 * C, nr, t.rg, t.RG, C, t.c0, [&](bool ok, float4 x4, unsigned off) {
+          float v[V] = {x4.x, x4.y, x4.z, x4.w};
+          const float q[V] = {0.f, 0.f, 0.f, 0.f};
+          row(ok, v, q);
+          put(v, off);
+        });
+      }
+    } else {
+      for (long r = r0 + t.rg; r < r1; r += t.RG) {
+        float v[V], q[V];
+        ldv<V>(x + r * C + t.c0, v);
+        if (res) ldv<V>(res + r * C + t.c0, q);
+        row(true, v, q);
+        if (y) stv<V>(y + r * C + t.c0, v);  // y == nullptr: statistics only (accunet_colsum)
       }
     }
   }
@@ -478,28 +494,28 @@ bn_bwd_reduce_kernel(const T* __restrict__ x, const T* __restrict__ dy,
       s[j] = st[BN_SCALE * C + t.c0 + j];
       h[j] = st[BN_SHIFT * C + t.c0 + j];
     }
-    constexpr int U = 4;  // see affine_act_kernel
-    for (long rb = r0 + t.rg; rb < r1; rb += U * t.RG) {
-      float xv[U][V], dv[U][V];
+    auto row = [&](bool ok, const float (&xv)[V], const float (&dv)[V]) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        long r = rb + (long)u * t.RG;
-        if (r < r1) {
-          ldv<V>(x + r * C + t.c0, xv[u]);
-          ldv<V>(dy + r * C + t.c0, dv[u]);
-        }
+      for (int j = 0; j < V; ++j) {
+        float g = ok ? dv[j] : 0.f;
+        if (act == ACT_LRELU) g *= lrelu_d(xv[j] * s[j] + h[j]);
+        a[j] += g;
+        b[j] += (double)g * ((double)xv[j] - mu[j]) * rs[j];
       }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (rb + (long)u * t.RG < r1) {
-#pragma unroll
-          for (int j = 0; j < V; ++j) {
-            float g = dv[u][j];
-            if (act == ACT_LRELU) g *= lrelu_d(xv[u][j] * s[j] + h[j]);
-            a[j] += g;
-            b[j] += (double)g * ((double)xv[u][j] - mu[j]) * rs[j];
-          }
-        }
+    };
+    if constexpr (V == 4) {
+      quad_rows2<4>(x + r0 * C, dy + r0 * C, r1 > r0 ? r1 - r0 : 0, t.rg, t.RG, C, t.c0,
+                    [&](bool ok, float4 x4, float4 d4, unsigned) {
+                      const float xv[V] = {x4.x, x4.y, x4.z, x4.w};
+                      const float dv[V] = {d4.x, d4.y, d4.z, d4.w};
+                      row(ok, xv, dv);
+                    });
+    } else {
+      for (long r = r0 + t.rg; r < r1; r += t.RG) {
+        float xv[V], dv[V];
+        ldv<V>(x + r * C + t.c0, xv);
+        ldv<V>(dy + r * C + t.c0, dv);
+        row(true, xv, dv);
       }
     }
   }
@@ -573,35 +589,46 @@ bn_bwd_apply_kernel(const T* __restrict__ x, const T* __restrict__ dy,
       k2[j] = coef[C + t.c0 + j];
       k3[j] = coef[2 * C + t.c0 + j];
     }
-    constexpr int U = 4;  // see affine_act_kernel
-    for (long rb = r0 + t.rg; rb < r1; rb += U * t.RG) {
-      float xv[U][V], dv[U][V], o[U][V];
+    // d = k1*g + k2*(x - mean) + k3; o (accumulate) = the value already in dx
+    auto row = [&](bool ok, const float (&xv)[V], const float (&dv)[V], float (&o)[V]) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        long r = rb + (long)u * t.RG;
-        if (r < r1) {
-          ldv<V>(x + r * C + t.c0, xv[u]);
-          ldv<V>(dy + r * C + t.c0, dv[u]);
-          if (accumulate) ldv<V>(dx + r * C + t.c0, o[u]);
-        }
+      for (int j = 0; j < V; ++j) {
+        float g = dv[j];
+        if (act == ACT_LRELU) g *= lrelu_d(xv[j] * s[j] + h[j]);
+        float d = k1[j] * g + k2[j] * (xv[j] - mu[j]) + k3[j];
+        // statistics describe the stored tensor (bf16: the rounded value)
+        const float dd = rnd<T>(d);
+        if (colsum && ok) a[j] += accumulate ? d : dd;
+        o[j] = accumulate ? rnd<T>(o[j] + d) : dd;
       }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        long r = rb + (long)u * t.RG;
-        if (r < r1) {
-#pragma unroll
-          for (int j = 0; j < V; ++j) {
-            float g = dv[u][j];
-            if (act == ACT_LRELU) g *= lrelu_d(xv[u][j] * s[j] + h[j]);
-            float d = k1[j] * g + k2[j] * (xv[u][j] - mu[j]) + k3[j];
-            // statistics describe the stored tensor (bf16: the rounded value)
-            const float dd = rnd<T>(d);
-            if (colsum) a[j] += accumulate ? d : dd;
-            o[u][j] = accumulate ? rnd<T>(o[u][j] + d) : dd;
-          }
-          stv<V>(dx + r * C + t.c0, o[u]);
-        }
+    };
+    auto plain = [&]() {
+      for (long r = r0 + t.rg; r < r1; r += t.RG) {
+        float xv[V], dv[V], o[V];
+        ldv<V>(x + r * C + t.c0, xv);
+        ldv<V>(dy + r * C + t.c0, dv);
+        if (accumulate) ldv<V>(dx + r * C + t.c0, o);
+        row(true, xv, dv, o);
+        stv<V>(dx + r * C + t.c0, o);
       }
+    };
+    if constexpr (V == 4) {
+      if (!accumulate) {
+        const long nr = r1 > r0 ? r1 - r0 : 0;
+        const __amdgpu_buffer_rsrc_t rd = acc_rsrc(dx + r0 * C, (unsigned)(nr * C * sizeof(T)));
+        quad_rows2<4>(x + r0 * C, dy + r0 * C, nr, t.rg, t.RG, C, t.c0,
+                      [&](bool ok, float4 x4, float4 d4, unsigned off) {
+                        const float xv[V] = {x4.x, x4.y, x4.z, x4.w};
+                        const float dv[V] = {d4.x, d4.y, d4.z, d4.w};
+                        float o[V];
+                        row(ok, xv, dv, o);
+                        bufq_st<0>(rd, off, make_float4(o[0], o[1], o[2], o[3]), (T*)nullptr);
+                      });
+      } else {
+        plain();
+      }
+    } else {
+      plain();
     }
   }
   if (colsum) block_chan_reduce2<V>(t, a, b, colsum, blockIdx.x, C);

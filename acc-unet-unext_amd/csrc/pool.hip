@@ -13,23 +13,26 @@
 #include "common.h"
 #include "kernels.h"
 #include "chan.h"
+#include <type_traits>
 
 // ---------------------------------------------------------------------------
 // pyramid forward: one thread per (low-res 4x4 or 2x2 cell, V consecutive channels);
 // V = 4 moves channel quads (16-byte loads/stores, 4-byte mask stores). The
 // per-element arithmetic is the same for every V.
 // ---------------------------------------------------------------------------
-template <int V, typename T>
+template <int V, typename T, int CS, bool PRO>
 __global__ void __launch_bounds__(256)
 hanc_pyramid_fwd_kernel(const T* __restrict__ x, const float* __restrict__ sc,
-                        const float* __restrict__ sh, int act, int B, int H, int W, int C, int k,
+                        const float* __restrict__ sh, int act, int B, int H, int W, int C,
                         T* __restrict__ p2, T* __restrict__ p4,
                         unsigned char* __restrict__ mk2, unsigned char* __restrict__ mk4) {
-  // k == 3: cell = 4x4 (one P4 pixel, four P2 pixels); k == 2: cell = 2x2 (one P2 pixel)
-  const int cs = (k == 3) ? 4 : 2;
-  const int Hc = H / cs, Wc = W / cs, CV = C / V;
+  // CS = 4 (k == 3): cell = 4x4 (one P4 pixel, four P2 pixels); CS = 2 (k == 2): one P2
+  // pixel. The CS*CS quads of a cell are loaded raw and unconditionally before any is
+  // used (compile-time cell size, prologue flag as a template argument), so they are
+  // in flight together instead of one dependent round trip each.
+  typedef typename QuadRaw<T>::type RawQ;
+  const int Hc = H / CS, Wc = W / CS, CV = C / V;
   const long total = (long)B * Hc * Wc * CV;
-  const bool pro = sc != nullptr;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
        i += (long)gridDim.x * blockDim.x) {
     const int c = (int)(i % CV) * V;
@@ -38,28 +41,47 @@ hanc_pyramid_fwd_kernel(const T* __restrict__ x, const float* __restrict__ sc,
     const long t = cell / Wc;
     const int hc = (int)(t % Hc);
     const int b = (int)(t / Hc);
-    float s[V], h[V];
+    float v[CS][CS][V];
+    const T* src = x + (((long)b * H + hc * CS) * W + wc * CS) * C + c;
+    if (V == 4) {
+      RawQ r[CS][CS];
 #pragma unroll
-    for (int j = 0; j < V; ++j) {
-      s[j] = pro ? sc[c + j] : 1.f;
-      h[j] = pro ? sh[c + j] : 0.f;
-    }
-    float v[4][4][V];
-    const T* src = x + (((long)b * H + hc * cs) * W + wc * cs) * C + c;
+      for (int dy = 0; dy < CS; ++dy)
 #pragma unroll
-    for (int dy = 0; dy < 4; ++dy)
+        for (int dx = 0; dx < CS; ++dx) r[dy][dx] = ldq_raw(src + ((long)dy * W + dx) * C, false);
+      float4 s4 = make_float4(1.f, 1.f, 1.f, 1.f), h4 = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (PRO) {
+        s4 = ld4(sc + c);
+        h4 = ld4(sh + c);
+      }
+      const float s[4] = {s4.x, s4.y, s4.z, s4.w}, h[4] = {h4.x, h4.y, h4.z, h4.w};
 #pragma unroll
-      for (int dx = 0; dx < 4; ++dx) {
-        if (dy < cs && dx < cs) {
+      for (int dy = 0; dy < CS; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < CS; ++dx) {
+          const float4 q4 = q2f(r[dy][dx]);
+          const float q[4] = {q4.x, q4.y, q4.z, q4.w};
+#pragma unroll
+          for (int j = 0; j < V; ++j)
+            v[dy][dx][j] = PRO ? apply_act(q[j] * s[j % 4] + h[j % 4], act) : q[j % 4];
+        }
+    } else {
+#pragma unroll
+      for (int dy = 0; dy < CS; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < CS; ++dx) {
           float q[V];
           ldv<V>(src + ((long)dy * W + dx) * C, q);
 #pragma unroll
-          for (int j = 0; j < V; ++j) v[dy][dx][j] = pro ? apply_act(q[j] * s[j] + h[j], act) : q[j];
+          for (int j = 0; j < V; ++j)
+            v[dy][dx][j] = PRO ? apply_act(q[j] * sc[c + j] + sh[c + j], act) : q[j];
         }
-      }
+    }
     const int H2 = H / 2, W2 = W / 2;
-    const int n2 = cs / 2;
+    constexpr int n2 = CS / 2;
+#pragma unroll
     for (int qy = 0; qy < n2; ++qy)
+#pragma unroll
       for (int qx = 0; qx < n2; ++qx) {
         float sum[V], mx[V];
         unsigned char code[V];
@@ -87,16 +109,16 @@ hanc_pyramid_fwd_kernel(const T* __restrict__ x, const float* __restrict__ sc,
           }
         }
       }
-    if (k == 3) {
+    if (CS == 4) {
       float s4[V], m4[V];
       unsigned char code[V];
 #pragma unroll
       for (int j = 0; j < V; ++j) {
         float a = 0.f, m = -INFINITY;
 #pragma unroll
-        for (int dy = 0; dy < 4; ++dy)
+        for (int dy = 0; dy < CS; ++dy)
 #pragma unroll
-          for (int dx = 0; dx < 4; ++dx) {
+          for (int dx = 0; dx < CS; ++dx) {
             a += v[dy][dx][j];
             m = fmaxf(m, v[dy][dx][j]);
           }
@@ -104,8 +126,8 @@ hanc_pyramid_fwd_kernel(const T* __restrict__ x, const float* __restrict__ sc,
         m4[j] = m;
         unsigned char cd = 255;
 #pragma unroll
-        for (int e = 15; e >= 0; --e)
-          if (v[e >> 2][e & 3][j] == m) cd = (unsigned char)e;
+        for (int e = CS * CS - 1; e >= 0; --e)
+          if (v[e / CS][e % CS][j] == m) cd = (unsigned char)e;
         code[j] = cd;
       }
       const long q4 = ((long)b * Hc + hc) * Wc + wc;
@@ -227,14 +249,23 @@ extern "C" int accunet_hanc_pyramid_fwd(const void* x, const float* sc, const fl
                   (k != 3 || !((uintptr_t)mk4 & 3));
   if (with_dt(dt, [&](auto tag) {
         using T = decltype(tag);
-        if (q4)
-          hipLaunchKernelGGL((hanc_pyramid_fwd_kernel<4, T>), dim3(grid_for(total / 4)), dim3(256), 0,
-                             (hipStream_t)stream, (const T*)x, sc, sh, act, B, H, W, C, k, (T*)p2,
-                             (T*)p4, mk2, k == 3 ? mk4 : nullptr);
-        else
-          hipLaunchKernelGGL((hanc_pyramid_fwd_kernel<1, T>), dim3(grid_for(total)), dim3(256), 0,
-                             (hipStream_t)stream, (const T*)x, sc, sh, act, B, H, W, C, k, (T*)p2,
-                             (T*)p4, mk2, k == 3 ? mk4 : nullptr);
+        auto go = [&](auto vc, auto csc, auto proc) {
+          constexpr int KV = decltype(vc)::value, KCS = decltype(csc)::value;
+          constexpr bool KP = decltype(proc)::value;
+          hipLaunchKernelGGL((hanc_pyramid_fwd_kernel<KV, T, KCS, KP>),
+                             dim3(grid_for(total / KV)), dim3(256), 0, (hipStream_t)stream,
+                             (const T*)x, sc, sh, act, B, H, W, C, (T*)p2, (T*)p4, mk2,
+                             k == 3 ? mk4 : nullptr);
+        };
+        auto by_pro = [&](auto vc, auto csc) {
+          if (sc) go(vc, csc, std::true_type{});
+          else go(vc, csc, std::false_type{});
+        };
+        using I4 = std::integral_constant<int, 4>;
+        using I2 = std::integral_constant<int, 2>;
+        using I1 = std::integral_constant<int, 1>;
+        if (q4) k == 3 ? by_pro(I4{}, I4{}) : by_pro(I4{}, I2{});
+        else k == 3 ? by_pro(I1{}, I4{}) : by_pro(I1{}, I2{});
       }))
     return ACC_EBADARG;
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
