@@ -376,7 +376,10 @@ ACC_DEV void dw_fill_tile(float4* __restrict__ tile, const TX* __restrict__ x,
     ps = ld4(sc + c0 + 4 * q);
     pb = ld4(sh + c0 + 4 * q);
   }
-  float4 v[G::NK];
+  // raw, unconditional loads (out-of-image quads read the image origin and are zeroed
+  // at the LDS write): all NK in flight together, bf16 widened only when parked
+  typedef typename QuadRaw<TX>::type RawQ;
+  RawQ v[G::NK];
   bool in[G::NK];
 #pragma unroll
   for (int k = 0; k < G::NK; ++k) {
@@ -385,21 +388,20 @@ ACC_DEV void dw_fill_tile(float4* __restrict__ tile, const TX* __restrict__ x,
     const int p = rp % G::IP, r = rp / G::IP;
     const int hh = h0 - 1 + r, ww = w0 - 1 + p;
     in[k] = (i < G::N4) && hh >= 0 && hh < g.H && ww >= 0 && ww < g.W;
-    v[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (in[k]) v[k] = ldq(x + (((long)b * g.H + hh) * g.W + ww) * g.C + c0 + 4 * q);
+    v[k] = ldq_raw(in[k] ? x + (((long)b * g.H + hh) * g.W + ww) * g.C + c0 + 4 * q : x, false);
   }
 #pragma unroll
   for (int k = 0; k < G::NK; ++k) {
     const int i = tid + 256 * k;
     if (i < G::N4) {
-      float4 a = v[k];
-      if (pro && in[k]) {
+      float4 a = q2f(v[k]);
+      if (pro) {
         a.x = apply_act(a.x * ps.x + pb.x, act);
         a.y = apply_act(a.y * ps.y + pb.y, act);
         a.z = apply_act(a.z * ps.z + pb.z, act);
         a.w = apply_act(a.w * ps.w + pb.w, act);
       }
-      tile[i] = a;
+      tile[i] = in[k] ? a : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
 }
@@ -601,15 +603,20 @@ dw3x3_tile_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dz,
   const int h0 = th * DW_TR, w0 = tw * G::TP;
   const int w = w0 + p;
   const int nr = min(DW_TR, g.H - h0);
-  // this thread's dz column (independent loads issued before the tile fill completes)
-  float4 d[DW_TR];
+  // this thread's dz column (independent raw loads issued before the tile fill; rows
+  // outside the image read dz's origin and are zeroed when widened)
+  typename QuadRaw<T>::type dr[DW_TR];
 #pragma unroll
   for (int r = 0; r < DW_TR; ++r) {
-    d[r] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (w < g.W && r < nr) d[r] = ldq(dz + (((long)b * g.H + h0 + r) * g.W + w) * g.C + c);
+    const bool ok = w < g.W && r < nr;
+    dr[r] = ldq_raw(ok ? dz + (((long)b * g.H + h0 + r) * g.W + w) * g.C + c : dz, false);
   }
   dw_fill_tile<TCQ>(tile, x, sc, sh, act, g, b, h0, w0, c0);
   __syncthreads();
+  float4 d[DW_TR];
+#pragma unroll
+  for (int r = 0; r < DW_TR; ++r)
+    d[r] = (w < g.W && r < nr) ? q2f(dr[r]) : make_float4(0.f, 0.f, 0.f, 0.f);
   float acc[10][4];
 #pragma unroll
   for (int i = 0; i < 10; ++i)
