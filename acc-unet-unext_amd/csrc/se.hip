@@ -350,8 +350,8 @@ se_bwd_reduce_kernel(const T* __restrict__ z, const T* __restrict__ dout,
 // backward middle step. coef (fp32): A[B*C] Bc[B*C] Cc[B*C] with
 //   da = A*g2 + Bc*(a*s - mean) + Cc
 // scratch (fp64): G[C] GY[C] du[B*C] dh[B*Cr] T1[B*C] T2[B*C] (+ U1..W3 with a prologue)
-// Four small launches (part sums, channel, sample, parameter step); the prologue
-// variant adds a fifth (coefficient step).
+// Three launches: part sums + channel step (se_bwd_chan_sum_kernel), sample step,
+// parameter + prologue-coefficient step (se_bwd_tail_kernel).
 struct SeBwdMid {
   int Cr;
   const float *w1, *w2, *gamma;
@@ -368,42 +368,6 @@ struct SeBwdMid {
 
 ACC_DEV double* se_T1(const SeGeom& g, const SeBwdMid& m) {
   return m.scratch + 2 * (size_t)g.C + (size_t)g.B * g.C + (size_t)g.B * m.Cr;
-}
-
-// chunk partials [B*NCH][N][C] of sample b -> per-(b,c) sums out[i][B*C] (i < N): 64
-// channels x 4 chunk groups per pass; each group sums its chunks in order, the 4
-// group sums are added in order.
-template <int N>
-ACC_DEV void se_part_sum_body(const double* __restrict__ part, const SeGeom& g, int b, int cb,
-                              double* __restrict__ out) {
-  __shared__ double r[N][4][64];
-  const int C = g.C, t = threadIdx.x;
-  const int c = cb + (t & 63), grp = t >> 6;
-  double s[N];
-#pragma unroll
-  for (int i = 0; i < N; ++i) s[i] = 0.0;
-  if (c < C)
-    ordered_strided_sum<4>(s, grp, g.NCH, 4, [&](int k, double (&v)[N]) {
-      const double* pr = part + ((long)(b * g.NCH + k) * N) * C;
-#pragma unroll
-      for (int i = 0; i < N; ++i) v[i] = *(pr + (long)i * C + c);
-    });
-#pragma unroll
-  for (int i = 0; i < N; ++i) r[i][grp][t & 63] = s[i];
-  __syncthreads();
-  if (grp == 0 && c < C) {
-    const long BC = (long)g.B * C;
-#pragma unroll
-    for (int i = 0; i < N; ++i)
-      out[i * BC + b * C + c] = ((r[i][0][t] + r[i][1][t]) + r[i][2][t]) + r[i][3][t];
-  }
-  __syncthreads();
-}
-
-template <int N>
-__global__ void __launch_bounds__(256)
-se_part_sum_kernel(const double* __restrict__ part, SeGeom g, double* __restrict__ out) {
-  se_part_sum_body<N>(part, g, blockIdx.y, blockIdx.x * 64, out);
 }
 
 // SE_LANES lanes per channel: lane l handles samples b = l, l + SE_LANES, ...; the
@@ -462,9 +426,43 @@ ACC_DEV void se_bwd_chan_body(const SeGeom& g, const SeBwdMid& m, int c, int lan
   }
 }
 
-__global__ void __launch_bounds__(256) se_bwd_chan_kernel(SeGeom g, SeBwdMid m) {
-  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  se_bwd_chan_body(g, m, gid / SE_LANES, gid % SE_LANES);
+
+// Part sums + channel step in one launch, one block per channel c: 16 lanes per
+// sample b sum the chunk partials k = lane, lane + 16, ... (every quantity's loads in
+// flight together), an xor butterfly inside the 16-lane group adds the lane sums in a
+// fixed order, lane 0 stores T[q][b, c] (fp64 scratch, read by the prologue step
+// too); then the first wave runs the channel step of c (se_bwd_chan_body). One
+// launch and two memory round trips instead of two launches.
+template <int NQ>
+__global__ void __launch_bounds__(256)
+se_bwd_chan_sum_kernel(const double* __restrict__ part, SeGeom g, SeBwdMid m) {
+  const int C = g.C, c = blockIdx.x, tid = threadIdx.x;
+  const int lane = tid % 16;
+  double* T = se_T1(g, m);
+  const long BC = (long)g.B * C;
+  for (int b0 = 0; b0 < g.B; b0 += 16) {
+    const int b = b0 + tid / 16;
+    double s[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) s[q] = 0.0;
+    if (b < g.B)
+      ordered_strided_sum<4>(s, lane, g.NCH, 16, [&](int k, double (&v)[NQ]) {
+        const double* pr = part + ((long)(b * g.NCH + k) * NQ) * C + c;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) v[q] = pr[(long)q * C];
+      });
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) s[q] += __shfl_xor(s[q], off);
+    }
+    if (b < g.B && lane == 0) {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) T[q * BC + (long)b * C + c] = s[q];
+    }
+  }
+  __syncthreads();  // T of channel c complete (same-block global stores)
+  if (tid < 64) se_bwd_chan_body(g, m, tid < SE_LANES ? c : C, tid % SE_LANES);
 }
 
 // sample step, sample b: dh = lrelu'(hpre) * W2^T du, dm = W1^T dh, coefficients.
@@ -553,9 +551,6 @@ ACC_DEV void se_bwd_param_body(const SeGeom& g, const SeBwdMid& m, long i) {
   }
 }
 
-__global__ void __launch_bounds__(256) se_bwd_param_kernel(SeGeom g, SeBwdMid m) {
-  se_bwd_param_body(g, m, blockIdx.x * (long)blockDim.x + threadIdx.x);
-}
 
 template <int V, typename T>
 __global__ void __launch_bounds__(256)
@@ -648,9 +643,16 @@ ACC_DEV void se_pro_coef_body(const SeGeom& g, const SeBwdMid& m, int c, int lan
   m.pcoef[2 * C + c] = k3;
 }
 
-__global__ void __launch_bounds__(256) se_pro_coef_kernel(SeGeom g, SeBwdMid m) {
-  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  se_pro_coef_body(g, m, gid / SE_LANES, gid % SE_LANES);
+
+// parameter step and (prologue) coefficient step in one launch: they depend on the
+// sample step only, not on each other. Blocks [0, npb) run the parameter step.
+__global__ void __launch_bounds__(256) se_bwd_tail_kernel(SeGeom g, SeBwdMid m, int npb) {
+  if ((int)blockIdx.x < npb) {
+    se_bwd_param_body(g, m, blockIdx.x * (long)blockDim.x + threadIdx.x);
+  } else {
+    const int gid = (blockIdx.x - npb) * blockDim.x + threadIdx.x;
+    se_pro_coef_body(g, m, gid / SE_LANES, gid % SE_LANES);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -902,22 +904,16 @@ extern "C" int accunet_se_fwd(const void* z, const float* sc, const float* sh, i
 static void se_bwd_mid(const SeGeom& g, const SeBwdMid& m, const double* part, int nq,
                        hipStream_t s) {
   const int B = g.B, C = g.C, Cr = m.Cr;
-  double* T1 = m.scratch + 2 * (size_t)C + (size_t)B * C + (size_t)B * Cr;
   if (nq == 2)
-    hipLaunchKernelGGL(se_part_sum_kernel<2>, dim3(ceil_div(C, 64), B), dim3(256), 0, s, part, g,
-                       T1);
+    hipLaunchKernelGGL(se_bwd_chan_sum_kernel<2>, dim3(C), dim3(256), 0, s, part, g, m);
   else
-    hipLaunchKernelGGL(se_part_sum_kernel<SE_PRO_NQ>, dim3(ceil_div(C, 64), B), dim3(256), 0, s,
-                       part, g, T1);
-  hipLaunchKernelGGL(se_bwd_chan_kernel, dim3(ceil_div((long)C * SE_LANES, 256)), dim3(256), 0, s,
-                     g, m);
+    hipLaunchKernelGGL(se_bwd_chan_sum_kernel<SE_PRO_NQ>, dim3(C), dim3(256), 0, s, part, g, m);
   hipLaunchKernelGGL(se_bwd_sample_kernel, dim3(B), dim3(256), (Cr > 0 ? Cr : 1) * sizeof(double),
                      s, g, m);
-  long nparam = 2L * C * Cr + C + Cr;
-  hipLaunchKernelGGL(se_bwd_param_kernel, dim3(ceil_div(nparam, 256)), dim3(256), 0, s, g, m);
-  if (m.pcoef)
-    hipLaunchKernelGGL(se_pro_coef_kernel, dim3(ceil_div((long)C * SE_LANES, 256)), dim3(256), 0,
-                       s, g, m);
+  const long nparam = 2L * C * Cr + C + Cr;
+  const int npb = ceil_div(nparam, 256);
+  const int ncb = m.pcoef ? ceil_div((long)C * SE_LANES, 256) : 0;
+  hipLaunchKernelGGL(se_bwd_tail_kernel, dim3(npb + ncb), dim3(256), 0, s, g, m, npb);
 }
 
 extern "C" int accunet_se_bwd(const void* z, const void* dout, const float* sc, const float* sh,
