@@ -35,7 +35,8 @@ OUT = os.path.join(ROOT, "gpurun_out")
 PROF = os.path.join(ROOT, "profiles")
 K1 = "dw3x3_tile_fwd_kernel<8, false,"
 K1_GRID = 196608  # 768 workgroups x 256 (16x256x256x96, channel groups fastest)
-K3 = ["se_reduce_kernel<4, float>", "se_mid_sample_kernel", "se_mid_bn_kernel", "se_apply_kernel<4, float>"]
+K3 = ["se_reduce_kernel<4, float, true>", "se_mid_sample_kernel", "se_mid_bn_kernel",
+      "se_apply_kernel<4, float, true>"]
 
 FAMILIES = ["gemm_f32g", "gemm_f32", "gemm_bf16", "splitk", "dw3x3", "reduce_finish", "bn_bwd",
             "bn_fin", "affine_act", "se_", "hanc_pyramid", "pool", "colreduce", "sum_rows",
