@@ -115,7 +115,11 @@ def k3_se(B, H, W, C, se_mod, iters=20, device="cuda", dtype=torch.float32):
 def hanc_gemm(P, N, K, iters=10, device="cuda", dtype=torch.float32):
     """The largest MFMA GEMM of the step: HANCLayer x-branch 1x1 conv of cnv72
     (P = B*64*64 pixels, K = 128*34 inputs, N = 128 outputs) with fp64 output stats.
-    dtype = activation storage (fp32 engine / bf16 engine; fp32 weights either way)."""
+    dtype = activation storage (fp32 engine / bf16 engine; fp32 weights either way).
+
+    The row reports the roofline that binds this shape: MFMA time 2PNK / peak vs HBM
+    time (A + B + C bytes) / 8 TB/s. fp32: 465 us vs 147 us -> "mfma"; bf16 (2.5 PF
+    dense, half the A bytes): 29 us vs 74 us -> "hbm". Both fractions are kept."""
     g = torch.Generator(device="cpu").manual_seed(9)
     a = torch.randn(P, K, generator=g).to(device=device, dtype=dtype)
     w = (torch.randn(N, K, generator=g) * K ** -0.5).to(device)
@@ -127,14 +131,24 @@ def hanc_gemm(P, N, K, iters=10, device="cuda", dtype=torch.float32):
         kern.gemm(P, N, K, a=[a], lda=[K], b=w, ldb=K, c=c, ldc=N, bias=bias, stats=st)
     us, per = _time(run, iters)
     fl = 2.0 * P * N * K
-    ach = fl / (us * 1e-6) / 1e12
+    by = float(a.element_size() * P * K + w.element_size() * N * K + c.element_size() * P * N)
     bf = dtype == torch.bfloat16
     peak = BF16_MFMA_TFLOPS if bf else FP32_MFMA_TFLOPS
+    t_mfma = fl / (peak * 1e12)
+    t_hbm = by / (HBM_PEAK_GBS * 1e9)
+    tflops = fl / (us * 1e-6) / 1e12
+    gbs = by / (us * 1e-6) / 1e9
     # fp32: the LDS-DMA engine (gemm_f32g.h) unless ACCUNET_GEMM_G=0
     kname = ("gemm_bf16_kernel" if bf else
              "gemm_f32_kernel" if os.environ.get("ACCUNET_GEMM_G", "1") == "0" else "gemm_f32g_kernel")
-    return {"bound": "mfma", "achieved": round(ach, 2), "peak": peak,
-            "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": None,
-            "kernel": kname, "shape": f"M{P} N{N} K{K}", "avg_us": round(us, 2),
-            "median_us": round(statistics.median(per), 2),
-            "launches": iters, "flops_alg_per_launch": fl}
+    row = {"kernel": kname, "shape": f"M{P} N{N} K{K}", "avg_us": round(us, 2),
+           "median_us": round(statistics.median(per), 2), "launches": iters,
+           "flops_alg_per_launch": fl, "bytes_alg_per_launch": by, "traffic": None,
+           "frac_mfma": round(tflops / peak, 4), "frac_hbm": round(gbs / HBM_PEAK_GBS, 4)}
+    if t_mfma >= t_hbm:
+        row.update({"bound": "mfma", "achieved": round(tflops, 2), "peak": peak,
+                    "unit": "TFLOP/s", "frac": row["frac_mfma"]})
+    else:
+        row.update({"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": row["frac_hbm"]})
+    return row

@@ -313,51 +313,91 @@ struct DwT {
   static constexpr int NK8 = (N8 + 255) / 256;
 };
 
+// 16-byte raw loads of the staging paths: QL quads per load (fp32: 1 float4; bf16: 2
+// quads = 8 channels, so a bf16 tile moves in half the load instructions of fp32)
+template <typename T> struct Raw16 { typedef float4 type; static constexpr int QL = 1; };
+template <> struct Raw16<bf16_t> { typedef uint4 type; static constexpr int QL = 2; };
+template <int AUX>
+ACC_DEV float4 buf16_ld(__amdgpu_buffer_rsrc_t r, unsigned off, const float*) {
+  return bufq_ld<AUX>(r, off, (const float*)nullptr);
+}
+template <int AUX>
+ACC_DEV uint4 buf16_ld(__amdgpu_buffer_rsrc_t r, unsigned off, const bf16_t*) {
+  const acc_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AUX);
+  return make_uint4(v[0], v[1], v[2], v[3]);
+}
+ACC_DEV float4 r16q(float4 v, int) { return v; }
+ACC_DEV float4 r16q(uint4 u, int j) {
+  return j == 0 ? make_float4(bflo(u.x), bfhi(u.x), bflo(u.y), bfhi(u.y))
+                : make_float4(bflo(u.z), bfhi(u.z), bflo(u.w), bfhi(u.w));
+}
+ACC_DEV uint4 ld16_raw(const bf16_t* p) { return *reinterpret_cast<const uint4*>(p); }
+ACC_DEV float4 ld16_raw(const float* p) { return ld4(p); }
+
+// prologue (BN scale/shift) of the QL quads a thread always stages: quads q0 .. q0+QL-1,
+// q0 = (tid * QL) % TCQ (256 * QL % TCQ == 0, so the same quads for every load)
+template <int TCQ, int QL>
+ACC_DEV void dw_stage_pro(const float* sc, const float* sh, int c0, float4 (&ps)[QL],
+                          float4 (&pb)[QL]) {
+  const int q0 = (threadIdx.x * QL) % TCQ;
+#pragma unroll
+  for (int j = 0; j < QL; ++j) {
+    ps[j] = sc ? ld4(sc + c0 + 4 * (q0 + j)) : make_float4(1.f, 1.f, 1.f, 1.f);
+    pb[j] = sc ? ld4(sh + c0 + 4 * (q0 + j)) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
 // Strip pipeline helpers: input rows live in a 10-slot LDS ring, row h of the
 // block's strip (which starts at output row hbeg) in slot (h - hbeg + 1) % 10.
 // Fetch `n` quads of consecutive input rows starting at row hA into registers, raw
-// (zero outside the image / past n: ACC_OOB offsets, no branches). rx covers one image.
+// (zero outside the image / past n: ACC_OOB offsets, no branches), QL quads per
+// 16-byte load. rx covers one image.
 template <int TCQ, int NKK, int AUX, typename TX>
-ACC_DEV void dw_fetch_rows(typename QuadRaw<TX>::type (&v)[NKK], __amdgpu_buffer_rsrc_t rx,
+ACC_DEV void dw_fetch_rows(typename Raw16<TX>::type (&v)[NKK], __amdgpu_buffer_rsrc_t rx,
                            const DwTGeom& g, int hA, int n, int w0, int c0) {
   typedef DwT<TCQ> G;
-  const int tid = threadIdx.x, q = tid % TCQ;
+  constexpr int QL = Raw16<TX>::QL;
+  const int tid = threadIdx.x;
 #pragma unroll
   for (int k = 0; k < NKK; ++k) {
-    const int i = tid + 256 * k;
-    const int rp = i / TCQ;
+    const int i = (tid + 256 * k) * QL;  // first quad of this load
+    const int rp = i / TCQ, q = i % TCQ;
     const int p = rp % G::IP, r = rp / G::IP;
     const int hh = hA + r, ww = w0 - 1 + p;
     const bool in = i < n && hh >= 0 && hh < g.H && ww >= 0 && ww < g.W;
     const unsigned off = in ? (unsigned)(((hh * g.W + ww) * g.C + c0 + 4 * q) * (int)sizeof(TX))
                             : ACC_OOB;
-    v[k] = bufq_ld<AUX>(rx, off, (const TX*)nullptr);
+    v[k] = buf16_ld<AUX>(rx, off, (const TX*)nullptr);
   }
 }
 
 // Activate (prologue BN+act, in-image elements only) and park fetched rows in the ring.
-template <int TCQ, int NKK, typename R>
+template <int TCQ, int NKK, int QL, typename R>
 ACC_DEV void dw_park_rows(float4* __restrict__ ring, const R (&v)[NKK], const DwTGeom& g,
-                          int hA, int n, int w0, int hbeg, bool pro, float4 ps, float4 pb,
-                          int act) {
+                          int hA, int n, int w0, int hbeg, bool pro, const float4 (&ps)[QL],
+                          const float4 (&pb)[QL], int act) {
   typedef DwT<TCQ> G;
-  const int tid = threadIdx.x, q = tid % TCQ;
+  const int tid = threadIdx.x;
 #pragma unroll
   for (int k = 0; k < NKK; ++k) {
-    const int i = tid + 256 * k;
+    const int i = (tid + 256 * k) * QL;
     if (i < n) {
-      const int rp = i / TCQ;
+      const int rp = i / TCQ, q = i % TCQ;
       const int p = rp % G::IP, r = rp / G::IP;
       const int hh = hA + r, ww = w0 - 1 + p;
-      float4 a = q2f(v[k]);
-      if (pro && hh >= 0 && hh < g.H && ww >= 0 && ww < g.W) {
-        a.x = apply_act(a.x * ps.x + pb.x, act);
-        a.y = apply_act(a.y * ps.y + pb.y, act);
-        a.z = apply_act(a.z * ps.z + pb.z, act);
-        a.w = apply_act(a.w * ps.w + pb.w, act);
-      }
+      const bool in = hh >= 0 && hh < g.H && ww >= 0 && ww < g.W;
       const int slot = (hh - hbeg + 1) % G::IR;
-      ring[(slot * G::IP + p) * TCQ + q] = a;
+#pragma unroll
+      for (int j = 0; j < QL; ++j) {
+        float4 a = r16q(v[k], j);
+        if (pro && in) {
+          a.x = apply_act(a.x * ps[j].x + pb[j].x, act);
+          a.y = apply_act(a.y * ps[j].y + pb[j].y, act);
+          a.z = apply_act(a.z * ps[j].z + pb[j].z, act);
+          a.w = apply_act(a.w * ps[j].w + pb[j].w, act);
+        }
+        ring[(slot * G::IP + p) * TCQ + q + j] = a;
+      }
     }
   }
 }
@@ -368,40 +408,41 @@ ACC_DEV void dw_fill_tile(float4* __restrict__ tile, const TX* __restrict__ x,
                           const float* __restrict__ sc, const float* __restrict__ sh, int act,
                           const DwTGeom& g, int b, int h0, int w0, int c0) {
   typedef DwT<TCQ> G;
+  constexpr int QL = Raw16<TX>::QL;
+  constexpr int NL = (G::N4 / QL + 255) / 256;  // 16-byte loads per thread
   const int tid = threadIdx.x;
-  const int q = tid % TCQ;  // 256 % TCQ == 0: a thread always loads the same quad
-  float4 ps = make_float4(1.f, 1.f, 1.f, 1.f), pb = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 ps[QL], pb[QL];
   const bool pro = sc != nullptr;
-  if (pro) {
-    ps = ld4(sc + c0 + 4 * q);
-    pb = ld4(sh + c0 + 4 * q);
-  }
+  dw_stage_pro<TCQ, QL>(sc, sh, c0, ps, pb);
   // raw, unconditional loads (out-of-image quads read the image origin and are zeroed
-  // at the LDS write): all NK in flight together, bf16 widened only when parked
-  typedef typename QuadRaw<TX>::type RawQ;
-  RawQ v[G::NK];
-  bool in[G::NK];
+  // at the LDS write): all NL in flight together, bf16 widened only when parked
+  typedef typename Raw16<TX>::type RawL;
+  RawL v[NL];
+  bool in[NL];
 #pragma unroll
-  for (int k = 0; k < G::NK; ++k) {
-    const int i = tid + 256 * k;
-    const int rp = i / TCQ;
+  for (int k = 0; k < NL; ++k) {
+    const int i = (tid + 256 * k) * QL;
+    const int rp = i / TCQ, q = i % TCQ;
     const int p = rp % G::IP, r = rp / G::IP;
     const int hh = h0 - 1 + r, ww = w0 - 1 + p;
     in[k] = (i < G::N4) && hh >= 0 && hh < g.H && ww >= 0 && ww < g.W;
-    v[k] = ldq_raw(in[k] ? x + (((long)b * g.H + hh) * g.W + ww) * g.C + c0 + 4 * q : x, false);
+    v[k] = ld16_raw(in[k] ? x + (((long)b * g.H + hh) * g.W + ww) * g.C + c0 + 4 * q : x);
   }
 #pragma unroll
-  for (int k = 0; k < G::NK; ++k) {
-    const int i = tid + 256 * k;
+  for (int k = 0; k < NL; ++k) {
+    const int i = (tid + 256 * k) * QL;
     if (i < G::N4) {
-      float4 a = q2f(v[k]);
-      if (pro) {
-        a.x = apply_act(a.x * ps.x + pb.x, act);
-        a.y = apply_act(a.y * ps.y + pb.y, act);
-        a.z = apply_act(a.z * ps.z + pb.z, act);
-        a.w = apply_act(a.w * ps.w + pb.w, act);
+#pragma unroll
+      for (int j = 0; j < QL; ++j) {
+        float4 a = r16q(v[k], j);
+        if (pro) {
+          a.x = apply_act(a.x * ps[j].x + pb[j].x, act);
+          a.y = apply_act(a.y * ps[j].y + pb[j].y, act);
+          a.z = apply_act(a.z * ps[j].z + pb[j].z, act);
+          a.w = apply_act(a.w * ps[j].w + pb[j].w, act);
+        }
+        tile[i + j] = in[k] ? a : make_float4(0.f, 0.f, 0.f, 0.f);
       }
-      tile[i] = in[k] ? a : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
 }
@@ -424,7 +465,11 @@ dw3x3_tile_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
                       const float* __restrict__ bst, int bact) {
   typedef DwT<TCQ> G;
   typedef typename QuadRaw<T>::type RawQ;
+  typedef typename Raw16<T>::type RawL;
   constexpr int CR = G::CR;
+  constexpr int QL = Raw16<T>::QL;
+  constexpr int NL = (G::N4 / QL + 255) / 256;   // 16-byte loads: whole tile
+  constexpr int NL8 = (G::N8 / QL + 255) / 256;  // 16-byte loads: CR new rows
   __shared__ float4 tile[G::N4 > 1024 ? G::N4 : 1024];
   // BNB (data gradient, flip = 1): stats receive the BatchNorm-backward partials
   // (sum g, sum g*(bz - mean)) of g = out * act'(bz*scale + shift) instead of (sum, sumsq)
@@ -453,15 +498,12 @@ dw3x3_tile_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
   const __amdgpu_buffer_rsrc_t rz = acc_rsrc(z + img, ibytes);
   const __amdgpu_buffer_rsrc_t rb = acc_rsrc(BNB ? bz + img : x + img, BNB ? ibytes : 0u);
   const bool pro = sc != nullptr;
-  float4 ps = make_float4(1.f, 1.f, 1.f, 1.f), pb = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (pro) {
-    ps = ld4(sc + c);
-    pb = ld4(sh + c);
-  }
+  float4 ps[QL], pb[QL];
+  dw_stage_pro<TCQ, QL>(sc, sh, c0, ps, pb);
   {
-    RawQ v[G::NK];
-    dw_fetch_rows<TCQ, G::NK, AUX, T>(v, rx, g, hbeg - 1, G::N4, w0, c0);
-    dw_park_rows<TCQ, G::NK>(tile, v, g, hbeg - 1, G::N4, w0, hbeg, pro, ps, pb, act);
+    RawL v[NL];
+    dw_fetch_rows<TCQ, NL, AUX, T>(v, rx, g, hbeg - 1, G::N4, w0, c0);
+    dw_park_rows<TCQ, NL, QL>(tile, v, g, hbeg - 1, G::N4, w0, hbeg, pro, ps, pb, act);
   }
   float k[9][4], bi[4];
 #pragma unroll
@@ -504,8 +546,8 @@ dw3x3_tile_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
     const int r0 = hbeg + CR * kc;
     // rows r0+9 .. are needed only if the strip's last input row (hend) lies there
     const bool more = kc + 1 < nch && r0 + 9 <= hend;
-    RawQ nx[G::NK8];
-    dw_fetch_rows<TCQ, G::NK8, AUX, T>(nx, rx, g, r0 + 9, more ? G::N8 : 0, w0, c0);
+    RawL nx[NL8];
+    dw_fetch_rows<TCQ, NL8, AUX, T>(nx, rx, g, r0 + 9, more ? G::N8 : 0, w0, c0);
     if (BNB) fetch_z(znext, r0 + CR, kc + 1 < nch);
     const int base = (CR * kc) % G::IR;  // slot of input row r0 - 1
     float win[3][3][4];
@@ -561,7 +603,7 @@ dw3x3_tile_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
     }
     if (more) {
       __syncthreads();  // every thread is done with rows r0-1 .. r0+CR-2
-      dw_park_rows<TCQ, G::NK8>(tile, nx, g, r0 + 9, G::N8, w0, hbeg, pro, ps, pb, act);
+      dw_park_rows<TCQ, NL8, QL>(tile, nx, g, r0 + 9, G::N8, w0, hbeg, pro, ps, pb, act);
       __syncthreads();
     }
     if (BNB) {
@@ -784,7 +826,11 @@ extern "C" int accunet_dw3x3_fwd(const void* x, const float* wt, const float* bi
   if (tcq) {
     DwTGeom tg = dw_tgeom(B, H, W, C, tcq, &grid, dw_rch_max());
     // non-temporal loads only for inputs above the Infinity Cache (bytes as stored)
-    tg.ntl = dw_ntl((long)B * H * W * C * (dt == ACC_BF16 ? 2 : 4));
+    // and only when a block's pixel segment is whole 128-B lines: bf16 TCQ-8 blocks read
+    // 64 B of each line, and a streamed line is fetched again for the neighbouring
+    // channel group (16x256x256x192 bf16 forward 304 us in-model with them)
+    const int seg = tcq * 4 * (dt == ACC_BF16 ? 2 : 4);
+    tg.ntl = seg % 128 == 0 ? dw_ntl((long)B * H * W * C * (dt == ACC_BF16 ? 2 : 4)) : 0;
     if (dw_cgfast() && grid.y > 1) {
       tg.cgf = (int)grid.y;
       grid = dim3(grid.x * grid.y, 1);

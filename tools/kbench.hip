@@ -148,6 +148,18 @@ int main(int argc, char** argv) {
     report("K1 bf16 dw3x3_fwd 16x256x256x96 pro+stats",
            timeit([&] { CA(accunet_dw3x3_fwd(x, wt, bi, sc, sh, 1, 0, z, st, B, H, W, C, nullptr, nullptr, 0, ACC_BF16, 0)); }, iters),
            bytes / 2);
+    {  // cnv91 forward in the bf16 mode: 16x256x256x192 bf16 = the same buffers' bytes
+      const int C2 = 2 * C;
+      int rows2 = accunet_dw3x3_rows(B, H, W, C2);
+      double* st2;
+      CK(hipMalloc(&st2, (size_t)rows2 * 2 * C2 * sizeof(double)));
+      float *wt2 = dalloc(9 * C2, 0.3f), *bi2 = dalloc(C2, 0.1f), *sc2 = dalloc(C2, 1.f),
+            *sh2 = dalloc(C2, 0.1f);
+      report("K1 bf16 dw3x3_fwd 16x256x256x192 pro+stats",
+             timeit([&] { CA(accunet_dw3x3_fwd(x, wt2, bi2, sc2, sh2, 1, 0, z, st2, B, H, W, C2, nullptr, nullptr, 0, ACC_BF16, 0)); }, iters),
+             bytes);
+      CK(hipFree(st2)); CK(hipFree(wt2)); CK(hipFree(bi2)); CK(hipFree(sc2)); CK(hipFree(sh2));
+    }
     report("copy float4 (same bytes as bf16 K1)",
            timeit([&] { hipLaunchKernelGGL(copy4, dim3(8192), dim3(256), 0, 0, (const float4*)x,
                                            (float4*)z, (long)(n / 8)); }, iters), bytes / 2);

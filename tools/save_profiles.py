@@ -7,7 +7,8 @@ stamped with the git commit and K1's source hash (accunet.probe.src_hash):
     python tools/save_profiles.py --shrink-pmc DIR...   (on the box: keep only the
                                                  probe dispatches of PMC passes)
 
-  {r}_bench_line.json / {r}_bench_line_bf16.json   bench.py JSON lines
+  {r}_bench_line.json / {r}_bench_line_bf16.json / {r}_unext_bench_line.json
+                              bench.py JSON lines (fp32, bf16, --model unext)
   {r}_bench_kernel_stats.csv  rocprofv3 --stats of bench.py --steps 5 --warmup 2
   {r}_bench_kstats.txt        per-kernel totals of that trace (tools/kstats.py)
   {r}_step_breakdown.txt      one graph-replayed step: time by kernel family, launches,
@@ -168,7 +169,8 @@ def main():
     st = stamp()
     os.makedirs(PROF, exist_ok=True)
     # bench lines
-    for log, name in (("bench_full.log", f"{r}_bench_line.json"), ("bench_bf16.log", f"{r}_bench_line_bf16.json")):
+    for log, name in (("bench_full.log", f"{r}_bench_line.json"), ("bench_bf16.log", f"{r}_bench_line_bf16.json"),
+                      ("bench_unext.log", f"{r}_unext_bench_line.json")):
         p = os.path.join(OUT, log)
         if os.path.exists(p):
             for line in open(p):
