@@ -54,6 +54,64 @@ def _flat_off(t: torch.Tensor, off: int) -> torch.Tensor:
 
 
 # --------------------------------------------------------------------------
+# Weight gradients on a side stream
+# --------------------------------------------------------------------------
+# ACCUNET_WGRAD_STREAM=0 keeps every backward kernel on one stream (A/B runs).
+_WGRAD_STREAM = os.environ.get("ACCUNET_WGRAD_STREAM", "1") != "0"
+_SIDE_STREAMS = {}
+
+
+def set_wgrad_stream(on: bool) -> bool:
+    """Enable / disable the side-stream weight gradients; returns the previous setting."""
+    global _WGRAD_STREAM
+    prev = _WGRAD_STREAM
+    _WGRAD_STREAM = bool(on)
+    return prev
+
+
+class _WgradFork:
+    """Runs a backward's weight-gradient GEMMs on a side stream, concurrently with its
+    data-gradient chain (data-gradient GEMM, BatchNorm backward, column sums): both
+    only read dZ and the saved inputs, and write disjoint buffers. Under graph
+    capture the fork / join become graph edges, so the replayed backward has two
+    branches per layer.
+
+    Memory safety: the side stream first waits for the main stream; `join()` (main
+    waits for side) runs before the backward returns, so every tensor the side stream
+    read or wrote is freed -- or handed to autograd -- after the join in main-stream
+    order, and the caching allocator never hands out a block the side stream still
+    uses. Only MFMA GEMMs (and their split-K reduce) run on the side stream: the
+    one-launch statistics reduction (reduce_finish) shares a device ticket array
+    between launches and must stay on one stream."""
+
+    def __init__(self, like: torch.Tensor):
+        self.on = _WGRAD_STREAM and like.is_cuda
+        if not self.on:
+            return
+        self.main = torch.cuda.current_stream(like.device)
+        side = _SIDE_STREAMS.get(like.device.index)
+        if side is None:
+            side = _SIDE_STREAMS[like.device.index] = torch.cuda.Stream(device=like.device)
+        self.side = side
+        side.wait_stream(self.main)
+
+    def __enter__(self):
+        if self.on:
+            self._ctx = torch.cuda.stream(self.side)
+            self._ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        if self.on:
+            self._ctx.__exit__(*exc)
+        return False
+
+    def join(self):
+        if self.on:
+            self.main.wait_stream(self.side)
+
+
+# --------------------------------------------------------------------------
 # Pending BatchNorm(+act)
 # --------------------------------------------------------------------------
 class Pending:
@@ -347,6 +405,27 @@ class _PWConvFn(torch.autograd.Function):
         keep = []
         d_srcs = []
         dpro_g = dpro_b = None
+        # weight gradient first, on the side stream (overlaps the data gradients below)
+        dW = None
+        fork = _WgradFork(dZ)
+        if nig[1]:
+            full = (cfg.w_off == 0 and kbeg[-1] == cfg.w_ld)
+            if cfg.wslot is not None:  # the sharing calls write disjoint slices covering W
+                dW, _ = cfg.wslot.acc_target(weight.shape, weight)
+            else:
+                dW = torch.empty_like(weight)
+            with fork:
+                if cfg.wslot is None and not full:
+                    dW.zero_()
+                for s, (x, C) in enumerate(zip(srcs, cfg.src_ch)):
+                    use_pro = (s == 0 and pro.active)
+                    keep.append(kern.gemm(N, C, P, a=[dZ], lda=[N], amode=AMODE_COL, b=x, ldb=C,
+                                          bmode=BMODE_NN, c=dW, ldc=cfg.w_ld,
+                                          c_offset=cfg.w_off + kbeg[s],
+                                          pro_b=_pro_mode(pro) if use_pro else PRO_NONE,
+                                          b_scale=pro.st[2] if use_pro else None,
+                                          b_shift=pro.st[3] if use_pro else None,
+                                          allow_split=True))
         for s, (x, C) in enumerate(zip(srcs, cfg.src_ch)):
             need = nig[5 + s] or (s == 0 and pro.active and (nig[3] or nig[4]))
             if not need:
@@ -374,21 +453,6 @@ class _PWConvFn(torch.autograd.Function):
                 keep.append(kern.gemm(P, C, N, a=[dZ], lda=[N], b=weight, ldb=cfg.w_ld,
                                       bmode=BMODE_NN, b_offset=cfg.w_off + kbeg[s], c=dA, ldc=C))
             d_srcs.append(dA)
-        dW = None
-        if nig[1]:
-            full = (cfg.w_off == 0 and kbeg[-1] == cfg.w_ld)
-            if cfg.wslot is not None:  # the sharing calls write disjoint slices covering W
-                dW, _ = cfg.wslot.acc_target(weight.shape, weight)
-            else:
-                dW = torch.zeros_like(weight) if not full else torch.empty_like(weight)
-            for s, (x, C) in enumerate(zip(srcs, cfg.src_ch)):
-                use_pro = (s == 0 and pro.active)
-                keep.append(kern.gemm(N, C, P, a=[dZ], lda=[N], amode=AMODE_COL, b=x, ldb=C,
-                                      bmode=BMODE_NN, c=dW, ldc=cfg.w_ld,
-                                      c_offset=cfg.w_off + kbeg[s],
-                                      pro_b=_pro_mode(pro) if use_pro else PRO_NONE,
-                                      b_scale=pro.st[2] if use_pro else None,
-                                      b_shift=pro.st[3] if use_pro else None, allow_split=True))
         dbias = None
         if cfg.has_bias and nig[2]:
             dbias = _take_bias_grad(cfg.bslot)
@@ -404,6 +468,7 @@ class _PWConvFn(torch.autograd.Function):
                 torch.empty(shp, dtype=dZ.dtype, device=dZ.device)
             kern.upsample_bwd(dZ, N, 0, _flat_off(dG, off), ld, B, H, W, N, 1 << lg)
             d_ups.append(dG)
+        fork.join()
         if cfg.wslot is not None:
             dW = cfg.wslot.done()
         return (None, dW, dbias, dpro_g, dpro_b, *d_srcs, *d_ups)
@@ -630,25 +695,37 @@ class _HancLayerFn(torch.autograd.Function):
         sh = pro.st[3] if pro.active else None
         keep = []
         dWp = _f32((N, J * C), z)
-        dP2 = dP4 = None
+        dW = _f32((N, J * C), z)
+        dP2 = dP4 = dG2 = dG4 = None
         if k >= 2:
             dG2 = _act((B, H // 2, W // 2, N), dZ)
             kern.upsample_bwd(dZ, N, 0, dG2, N, B, H, W, N, 2)
-            dP2 = _act(p2.shape, dZ)
-            keep.append(kern.gemm(P // 4, 2 * C, N, a=[dG2], lda=[N], b=Wp, ldb=J * C,
-                                  bmode=BMODE_NN, b_offset=C, c=dP2, ldc=2 * C))
-            keep.append(kern.gemm(N, 2 * C, P // 4, a=[dG2], lda=[N], amode=AMODE_COL, b=p2,
-                                  ldb=2 * C, bmode=BMODE_NN, c=dWp, ldc=J * C, c_offset=C,
-                                  allow_split=True))
             if k == 3:
                 dG4 = _act((B, H // 4, W // 4, N), dZ)
                 kern.upsample_bwd(dZ, N, 0, dG4, N, B, H, W, N, 4)
-                dP4 = _act(p4.shape, dZ)
-                keep.append(kern.gemm(P // 16, 2 * C, N, a=[dG4], lda=[N], b=Wp, ldb=J * C,
-                                      bmode=BMODE_NN, b_offset=3 * C, c=dP4, ldc=2 * C))
+        # the three weight-gradient GEMMs on the side stream (overlap the data gradients)
+        fork = _WgradFork(dZ)
+        with fork:
+            if k >= 2:
+                keep.append(kern.gemm(N, 2 * C, P // 4, a=[dG2], lda=[N], amode=AMODE_COL, b=p2,
+                                      ldb=2 * C, bmode=BMODE_NN, c=dWp, ldc=J * C, c_offset=C,
+                                      allow_split=True))
+            if k == 3:
                 keep.append(kern.gemm(N, 2 * C, P // 16, a=[dG4], lda=[N], amode=AMODE_COL,
                                       b=p4, ldb=2 * C, bmode=BMODE_NN, c=dWp, ldc=J * C,
                                       c_offset=3 * C, allow_split=True))
+            keep.append(kern.gemm(N, C, P, a=[dZ], lda=[N], amode=AMODE_COL, b=z, ldb=C,
+                                  bmode=BMODE_NN, c=dWp, ldc=J * C, c_offset=0,
+                                  pro_b=_pro_mode(pro), b_scale=sc, b_shift=sh, allow_split=True))
+            kern.group_relayout(dWp, dW, N, C, J, _HANC_ORDER[k], inverse=True)
+        if k >= 2:
+            dP2 = _act(p2.shape, dZ)
+            keep.append(kern.gemm(P // 4, 2 * C, N, a=[dG2], lda=[N], b=Wp, ldb=J * C,
+                                  bmode=BMODE_NN, b_offset=C, c=dP2, ldc=2 * C))
+            if k == 3:
+                dP4 = _act(p4.shape, dZ)
+                keep.append(kern.gemm(P // 16, 2 * C, N, a=[dG4], lda=[N], b=Wp, ldb=J * C,
+                                      bmode=BMODE_NN, b_offset=3 * C, c=dP4, ldc=2 * C))
         # x branch data gradient; for k >= 2 its epilogue adds the pyramid's backward
         # (avg spread + first-max routing), so dA is written exactly once
         dA = torch.empty_like(z)
@@ -660,11 +737,6 @@ class _HancLayerFn(torch.autograd.Function):
                               ldc=C, H=H, W=W,
                               pyr=(dP2, dP4, mk2, mk4) if k >= 2 else None, stats=part,
                               bnb=(z, pro.st, pro.act) if pro.active else None))
-        keep.append(kern.gemm(N, C, P, a=[dZ], lda=[N], amode=AMODE_COL, b=z, ldb=C,
-                              bmode=BMODE_NN, c=dWp, ldc=J * C, c_offset=0,
-                              pro_b=_pro_mode(pro), b_scale=sc, b_shift=sh, allow_split=True))
-        dW = _f32((N, J * C), z)
-        kern.group_relayout(dWp, dW, N, C, J, _HANC_ORDER[k], inverse=True)
         db = _take_bias_grad(cfg.bslot)
         if db is None:
             db = _f32((N,), z)
@@ -673,6 +745,7 @@ class _HancLayerFn(torch.autograd.Function):
             dz, dg, dbeta = _pro_bwd_part(pro, z, pro_g, dA, part, R)
         else:
             dz, dg, dbeta = dA, None, None
+        fork.join()
         return None, dz, dg, dbeta, dW, db
 
 
@@ -898,6 +971,14 @@ class _Conv3x3Fn(torch.autograd.Function):
         P = B * H * W
         keep = []
         dx = None
+        dWr = _f32((Co, 9 * Ci), x)
+        dW = torch.empty_like(weight)
+        fork = _WgradFork(dZ)
+        with fork:  # weight gradient on the side stream (overlaps the data gradient)
+            keep.append(kern.gemm(Co, 9 * Ci, P, a=[dZ], lda=[Co], amode=AMODE_COL, b=x, ldb=Ci,
+                                  bmode=BMODE_NN_SHIFT3, c=dWr, ldc=9 * Ci, H=H, W=W, cin=Ci,
+                                  allow_split=True))
+            kern.permute4(dWr, dW, (Co, Ci, 3, 3), (9 * Ci, 1, 3 * Ci, Ci))
         if ctx.needs_input_grad[1]:
             Wf = _f32((Ci, 9 * Co), x)  # [ci][tap'][co] = W[co][ci][8-tap']
             kern.permute4(weight, Wf, (Ci, 3, 3, Co), (9, 3, 1, 9 * Ci), flips=(0, 1, 1, 0))
@@ -910,16 +991,11 @@ class _Conv3x3Fn(torch.autograd.Function):
                                   ups=[(t, Ci, 0, 0) for t in adds]))
         if cfg.slot is not None:
             dx = cfg.slot.done()
-        dWr = _f32((Co, 9 * Ci), x)
-        keep.append(kern.gemm(Co, 9 * Ci, P, a=[dZ], lda=[Co], amode=AMODE_COL, b=x, ldb=Ci,
-                              bmode=BMODE_NN_SHIFT3, c=dWr, ldc=9 * Ci, H=H, W=W, cin=Ci,
-                              allow_split=True))
-        dW = torch.empty_like(weight)
-        kern.permute4(dWr, dW, (Co, Ci, 3, 3), (9 * Ci, 1, 3 * Ci, Ci))
         db = _take_bias_grad(cfg.bslot)
         if db is None:
             db = _f32((Co,), x)
             keep.append(kern.colsum(dZ, P, Co, db))
+        fork.join()
         return None, dx, dW, db
 
 
@@ -964,17 +1040,20 @@ class _ConvT2Fn(torch.autograd.Function):
         kern.pixel_shuffle2(dT, None, dY, B, H, W, Co, inverse=True)
         keep = []
         dx = None
+        dWr = _f32((Ci, 4 * Co), x)
+        dW = _f32((Ci, Co, 2, 2), x)
+        fork = _WgradFork(dT)
+        with fork:  # weight gradient on the side stream (overlaps the data gradient)
+            keep.append(kern.gemm(Ci, 4 * Co, P, a=[x], lda=[Ci], amode=AMODE_COL, b=dT,
+                                  ldb=4 * Co, bmode=BMODE_NN, c=dWr, ldc=4 * Co, allow_split=True))
+            kern.permute4(dWr, dW, (Ci, Co, 2, 2), (4 * Co, 1, 2 * Co, Co))
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
             keep.append(kern.gemm(P, Ci, 4 * Co, a=[dT], lda=[4 * Co], b=Wr, ldb=4 * Co, c=dx,
                                   ldc=Ci))
-        dWr = _f32((Ci, 4 * Co), x)
-        keep.append(kern.gemm(Ci, 4 * Co, P, a=[x], lda=[Ci], amode=AMODE_COL, b=dT,
-                              ldb=4 * Co, bmode=BMODE_NN, c=dWr, ldc=4 * Co, allow_split=True))
-        dW = _f32((Ci, Co, 2, 2), x)
-        kern.permute4(dWr, dW, (Ci, Co, 2, 2), (4 * Co, 1, 2 * Co, Co))
         db = _f32((Co,), x)
         keep.append(kern.colsum(dY, B * 4 * H * W, Co, db))
+        fork.join()
         return dx, dW, db
 
 

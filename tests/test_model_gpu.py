@@ -296,6 +296,34 @@ def test_hip_graph_train_step_equals_eager(variant):
         assert torch.equal(v, runs[True][1][k]), k
 
 
+@pytest.mark.parametrize("graph,precision", [(False, "fp32"), (True, "fp32"), (True, "bf16")])
+def test_side_stream_weight_gradients_bit_identical(graph, precision):
+    """The weight-gradient GEMMs run on a side stream, concurrently with the data
+    gradients (ops._WgradFork; fork / join become graph edges under capture). Two
+    training steps with and without the side stream: identical losses, parameters
+    and BatchNorm state bit for bit (eager and HIP-graph, fp32 and bf16)."""
+    from accunet import ops
+    from accunet.train import TrainStep
+    nf, B, S = 8, 2, 64
+    sd = O.det_state_dict(O.param_spec("canonical", 3, 1, nf), seed=0)
+    x = O.det_input((B, 3, S, S), "golden-x").to(DEV)
+    mask = O.det_mask((B, 1, S, S), "golden-mask", p=0.4).to(DEV)
+    runs = {}
+    prev = ops.set_wgrad_stream(True)
+    try:
+        for side in (False, True):
+            ops.set_wgrad_stream(side)
+            m = _hip_model("canonical", sd, nf).train()
+            step = TrainStep(m, lr=1e-3, graph=graph, precision=precision)
+            losses = [float(step(x, mask).item()) for _ in range(2)]
+            runs[side] = (losses, {k: v.detach().clone() for k, v in m.state_dict().items()})
+    finally:
+        ops.set_wgrad_stream(prev)
+    assert runs[False][0] == runs[True][0], (runs[False][0], runs[True][0])
+    for k, v in runs[False][1].items():
+        assert torch.equal(v, runs[True][1][k]), k
+
+
 @pytest.mark.parametrize("variant,B,S", [("canonical", 16, 256), ("w", 4, 512)])
 def test_full_size_configs_properties(variant, B, S):
     """BASELINE configs[1] (canonical, 16x3x256x256) and configs[3] (ACC_UNet_W,
