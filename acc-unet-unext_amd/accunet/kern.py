@@ -265,6 +265,12 @@ def _lib_raw():
     return _lib.load()
 
 
+def ticket_bank(bank: int) -> int:
+    """Ticket bank of the statistics reductions enqueued from now on (accunet_ticket_bank);
+    returns the previous one."""
+    return int(_lib_raw().accunet_ticket_bank(int(bank)))
+
+
 def dw3x3_rows(B, H, W, C) -> int:
     return int(_lib_raw().accunet_dw3x3_rows(B, H, W, C))
 

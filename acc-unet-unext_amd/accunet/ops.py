@@ -80,9 +80,9 @@ class _WgradFork:
     waits for side) runs before the backward returns, so every tensor the side stream
     read or wrote is freed -- or handed to autograd -- after the join in main-stream
     order, and the caching allocator never hands out a block the side stream still
-    uses. Only MFMA GEMMs (and their split-K reduce) run on the side stream: the
-    one-launch statistics reduction (reduce_finish) shares a device ticket array
-    between launches and must stay on one stream."""
+    uses. The one-launch statistics reductions (reduce_finish) enqueued inside the
+    fork use ticket bank 1, the main stream's bank 0, so concurrent reductions never
+    share a ticket counter."""
 
     def __init__(self, like: torch.Tensor):
         self.on = _WGRAD_STREAM and like.is_cuda
@@ -99,10 +99,12 @@ class _WgradFork:
         if self.on:
             self._ctx = torch.cuda.stream(self.side)
             self._ctx.__enter__()
+            self._bank = kern.ticket_bank(1)
         return self
 
     def __exit__(self, *exc):
         if self.on:
+            kern.ticket_bank(self._bank)
             self._ctx.__exit__(*exc)
         return False
 
@@ -564,6 +566,12 @@ class _DWConvFn(torch.autograd.Function):
         B, H, W, C = cfg.B, cfg.H, cfg.W, cfg.C
         pro = cfg.pro
         dA = torch.empty_like(z)
+        dW = torch.empty_like(weight)
+        db = _f32((C,), z)
+        fork = _WgradFork(dZ)
+        with fork:  # weight / bias gradient on the side stream (overlaps the data gradient)
+            ws = kern.dw3x3_wgrad(z, dZ, pro.st[2] if pro.active else None,
+                                  pro.st[3] if pro.active else None, pro.act, dW, db, B, H, W, C)
         part = R = None
         if pro.active:
             # norm1's backward reduce rides in the data-gradient kernel's epilogue
@@ -573,14 +581,11 @@ class _DWConvFn(torch.autograd.Function):
                            bnb=(z, pro.st, pro.act))
         else:
             kern.dw3x3_fwd(dZ, weight, None, None, None, ACT_NONE, 1, dA, None, B, H, W, C)
-        dW = torch.empty_like(weight)
-        db = _f32((C,), z)
-        ws = kern.dw3x3_wgrad(z, dZ, pro.st[2] if pro.active else None,
-                              pro.st[3] if pro.active else None, pro.act, dW, db, B, H, W, C)
         if pro.active:
             dz, dg, dbeta = _pro_bwd_part(pro, z, pro_g, dA, part, R)
         else:
             dz, dg, dbeta = dA, None, None
+        fork.join()
         del ws
         return None, dz, dg, dbeta, dW, db
 

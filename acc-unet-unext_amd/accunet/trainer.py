@@ -97,8 +97,14 @@ class Trainer:
     def __init__(self, model: torch.nn.Module, model_type: str = "ACC_UNet",
                  save_path: str = "./models", lr: float = 1e-3, epochs: int = 1000,
                  early_stopping_patience: int = 100, criterion=None, optimizer=None,
-                 lr_scheduler="cosine", device: Optional[torch.device] = None, logger=None):
+                 lr_scheduler="cosine", device: Optional[torch.device] = None, logger=None,
+                 reducer=None):
+        """reducer: an accunet.dist.GradBucketReducer over `model` for data-parallel
+        training (one process per GPU; its hooks all-reduce the gradients during each
+        backward). The loop then zeroes gradients through it, keeping them views of
+        its flat all-reduce buffer; without one the loop is single-process."""
         self.model = model
+        self.reducer = reducer
         self.model_type = model_type
         self.save_path = save_path
         self.epochs = epochs
@@ -143,7 +149,10 @@ class Trainer:
                     preds = preds[0]
                 loss = crit(preds, masks.float())
                 if training:
-                    self.optimizer.zero_grad()
+                    if self.reducer is not None:
+                        self.reducer.zero_grad()
+                    else:
+                        self.optimizer.zero_grad()
                     loss.backward()
                     self.optimizer.step()
                 b = images.shape[0]

@@ -123,7 +123,17 @@ size_t accunet_partials_ws_elems(int R, int Wd) {
 // its word, so consecutive launches on a stream (and graph replays) reuse it.
 // ---------------------------------------------------------------------------
 #define FIN_MAX_CB 16384  // column blocks (ncols <= 262144: dw wgrad of cnv72 has 10 x 4352)
-__device__ unsigned g_fin_tickets[FIN_MAX_CB];
+// One ticket array per bank: launches that may run concurrently (the backward's side
+// stream, accunet_ticket_bank) must not share tickets.
+#define FIN_BANKS 2
+__device__ unsigned g_fin_tickets[FIN_BANKS * FIN_MAX_CB];
+static int g_ticket_bank = 0;
+
+extern "C" int accunet_ticket_bank(int bank) {
+  const int prev = g_ticket_bank;
+  if (bank >= 0 && bank < FIN_BANKS) g_ticket_bank = bank;
+  return prev;
+}
 
 ACC_DEV void fin_column(const FinishArgs& fa, int col, double tot) {
   switch (fa.kind) {
@@ -232,7 +242,7 @@ reduce_finish_kernel(const TP* __restrict__ part, int R, int stride, int rpc, do
     // them with sc1 loads (L1 bypass), so neither an L2 write-back (release) nor an L1
     // invalidate (acquire) is needed (MI355X guide section 6, Guideline 16, R1/R2)
     if (g == 0 && valid) st_wt(chunks + (long)blockIdx.x * stride + col, tot);
-    if (!handoff_last(g_fin_tickets + blockIdx.y, nchunk)) return;
+    if (!handoff_last(g_fin_tickets + fa.bank * FIN_MAX_CB + blockIdx.y, nchunk)) return;
     double c1[1] = {0.0};
     if (valid)
       ordered_strided_sum<8>(c1, g, nchunk, FIN_GROUPS, [&](int k, double (&v)[1]) {
@@ -265,7 +275,9 @@ size_t reduce_finish_ws(int R, int stride) {
 }
 
 int reduce_finish(const void* part, bool part_f64, int R, int stride, double* chunks,
-                  const FinishArgs& fa, hipStream_t s) {
+                  const FinishArgs& fa_in, hipStream_t s) {
+  FinishArgs fa = fa_in;
+  fa.bank = g_ticket_bank;
   const bool paired = fa.kind == FIN_BN_FWD || fa.kind == FIN_BN_BWD;
   const int rpc = fin_rows_per_chunk(R);
   const int nchunk = max(1, ceil_div(R, rpc));

@@ -7,6 +7,7 @@ data-parallel code path is the one bench.py runs over RCCL on a node:
      all-reduce (mean) + fused Adam, 3 steps on rank-specific data;
   2. eager mode: TrainStep with GradBucketReducer (bucketed all-reduce overlapped
      with backward through post-accumulate-grad hooks), same start, same data.
+  3. the epoch loop: Trainer(reducer=GradBucketReducer) over the same batches.
 Checks: parameters identical on both ranks after each mode (bitwise), both modes
 agree with each other, and the parameters moved.
 """
@@ -34,6 +35,13 @@ def run(mode, sd, data, dev):
     m = ACC_UNet(3, 1, n_filts=8)
     m.load_state_dict(sd)
     m = m.to(dev).train()
+    if mode == "trainer":  # the epoch loop with the bucketed reducer (Trainer(reducer=))
+        from accunet.trainer import Trainer
+        tr = Trainer(m, lr=1e-3, lr_scheduler=None, device=dev,
+                     reducer=adist.GradBucketReducer(m, bucket_mb=0.25))
+        tr.train_one_epoch([({"image": x, "label": y}, None) for x, y in data], 0, True)
+        torch.cuda.synchronize()
+        return flat_params(m), [h["loss"] for h in tr.history]
     if mode == "graph":
         step = TrainStep(m, lr=1e-3, graph=True)
     else:
@@ -57,7 +65,7 @@ def main():
     data = [(torch.randn(2, 3, 32, 32, generator=g).to(dev),
              (torch.rand(2, 1, 32, 32, generator=g) < 0.3).float().to(dev)) for _ in range(3)]
     out = {}
-    for mode in ("graph", "eager"):
+    for mode in ("graph", "eager", "trainer"):
         p, losses = run(mode, sd, data, dev)
         other = [torch.empty_like(p) for _ in range(world)]
         dist.all_gather(other, p)
@@ -72,6 +80,10 @@ def main():
     print(f"rank {rank} graph vs eager max|dp| {d:.3e}", flush=True)
     assert d < 1e-5, d
     assert all(abs(a - b) < 1e-5 for a, b in zip(out["graph"][1], out["eager"][1]))
+    # the epoch loop runs the same steps (its loss is the epoch average)
+    d = float((out["trainer"][0] - out["eager"][0]).abs().max())
+    print(f"rank {rank} trainer vs eager max|dp| {d:.3e}", flush=True)
+    assert d < 1e-5, d
     dist.barrier()
     dist.destroy_process_group()
     if rank == 0:
