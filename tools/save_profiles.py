@@ -89,10 +89,25 @@ def step_breakdown(rows, st):
         cat[k] += dur(r)
         cnt[k] += 1
     busy = sum(cat.values())
-    wall = int(seg[-1]["End_Timestamp"]) - int(seg[0]["Start_Timestamp"])
+    t0 = min(int(r["Start_Timestamp"]) for r in seg)
+    t1 = max(int(r["End_Timestamp"]) for r in seg)
+    wall = t1 - t0
+    # time with at least one kernel running (the backward's weight gradients run on a
+    # second stream, so kernel durations overlap and their sum exceeds the wall time)
+    iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in seg)
+    union, cs, ce = 0, iv[0][0], iv[0][1]
+    for a, b in iv[1:]:
+        if a > ce:
+            union += ce - cs
+            cs, ce = a, b
+        else:
+            ce = max(ce, b)
+    union += ce - cs
     lines = [f"one training step (HIP-graph replay + Adam) from the rocprofv3 kernel trace ({st})",
-             f"kernels {len(seg)}, wall {wall / 1e6:.2f} ms, busy {busy / 1e6:.2f} ms, "
-             f"gaps {(wall - busy) / 1e6:.2f} ms", "", "     ms      %  launches  family"]
+             f"kernels {len(seg)}, wall {wall / 1e6:.2f} ms, GPU busy (any kernel running) "
+             f"{union / 1e6:.2f} ms, idle gaps {(wall - union) / 1e6:.2f} ms; sum of kernel "
+             f"durations {busy / 1e6:.2f} ms (two streams overlap: per-kernel times include "
+             f"sharing the GPU with the other stream)", "", "     ms      %  launches  family"]
     for k, v in cat.most_common():
         lines.append(f"{v / 1e6:7.2f} {100 * v / busy:6.1f} {cnt[k]:9d}  {k}")
     return "\n".join(lines) + "\n"
