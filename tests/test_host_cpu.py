@@ -153,3 +153,77 @@ def test_grad_bucket_reducer_gloo_world2():
     for rank, err, nb in res:
         assert nb > 1
         assert err < 1e-6, (rank, err)
+
+
+class _BceDice(torch.nn.Module):
+    """Trainer-compatible criterion on CPU (loss + the _show_dice hook it logs)."""
+
+    def forward(self, pred, mask):
+        return torch.nn.functional.binary_cross_entropy_with_logits(pred, mask)
+
+    def _show_dice(self, pred, mask):
+        p = (torch.sigmoid(pred) >= 0.5).float()
+        return float((2 * (p * mask).sum() + 1e-5) / (p.sum() + mask.sum() + 1e-5))
+
+
+def _trainer_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from accunet.dist import GradBucketReducer
+    from accunet.trainer import Trainer
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Conv2d(3, 4, 1), torch.nn.ReLU(), torch.nn.Conv2d(4, 1, 1))
+    init = [p.detach().clone() for p in net.parameters()]
+
+    def batches(r):
+        g = torch.Generator().manual_seed(7 + r)
+        return [({"image": torch.randn(2, 3, 8, 8, generator=g),
+                  "label": (torch.rand(2, 1, 8, 8, generator=g) < 0.4).float()}, None)
+                for _ in range(2)]
+
+    red = GradBucketReducer(net, bucket_mb=0.00001)  # ~2-element buckets: several collectives
+    tr = Trainer(net, criterion=_BceDice(), optimizer=torch.optim.SGD(net.parameters(), lr=0.1),
+                 lr_scheduler=None, device=torch.device("cpu"), reducer=red)
+    tr.train_one_epoch(batches(rank), 0, True)
+    got = torch.cat([p.detach().reshape(-1) for p in net.parameters()])
+    # expected: SGD on the rank-averaged gradient of each step, replayed in-process
+    ref = torch.nn.Sequential(torch.nn.Conv2d(3, 4, 1), torch.nn.ReLU(), torch.nn.Conv2d(4, 1, 1))
+    with torch.no_grad():
+        for p, v in zip(ref.parameters(), init):
+            p.copy_(v)
+    data = [batches(r) for r in range(world)]
+    for step in range(2):
+        gs = [torch.zeros_like(p) for p in ref.parameters()]
+        for r in range(world):
+            b = data[r][step][0]
+            loss = _BceDice()(ref(b["image"]), b["label"])
+            for acc, t in zip(gs, torch.autograd.grad(loss, list(ref.parameters()))):
+                acc += t / world
+        with torch.no_grad():
+            for p, gg in zip(ref.parameters(), gs):
+                p -= 0.1 * gg
+    exp = torch.cat([p.detach().reshape(-1) for p in ref.parameters()])
+    q.put((rank, float((got - exp).abs().max()), len(red.buckets)))
+    dist.destroy_process_group()
+
+
+def test_trainer_with_bucket_reducer_gloo_world2():
+    """Trainer(reducer=GradBucketReducer): the epoch loop zeroes through the reducer,
+    whose hooks all-reduce (mean) each bucket during backward, so every rank applies
+    the rank-averaged gradient (accunet/trainer.py, accunet/dist.py)."""
+    import random
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = random.randint(20000, 40000)
+    procs = [ctx.Process(target=_trainer_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, err, nb in res:
+        assert nb > 1
+        assert err < 1e-6, (rank, err)
