@@ -25,6 +25,7 @@ _CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # sources that decide K1's instruction stream (profiles/k1_traffic.json is only
 # attached to a bench line whose tree has the same bytes here)
 K1_SOURCES = ("dwconv.hip", "common.h", "chan.h")
+K3_SOURCES = ("se.hip", "common.h", "chan.h")  # the same rule for K3's traffic
 
 
 def src_hash(files=K1_SOURCES) -> str:
@@ -33,6 +34,28 @@ def src_hash(files=K1_SOURCES) -> str:
         with open(os.path.join(_CSRC, f), "rb") as fh:
             h.update(f.encode() + b"\0" + fh.read())
     return h.hexdigest()[:16]
+
+def attach_traffic(row: dict, path: str, dtype: str, sources=K1_SOURCES) -> dict:
+    """Set row["traffic"] from a committed PMC summary (profiles/k1_traffic.json,
+    k3_traffic.json: FETCH_SIZE / WRITE_SIZE passes of the bench command, per launch)
+    when it describes this row: same shape, same storage dtype, and taken on the same
+    kernel sources as this tree (src_sha == src_hash(sources)). A summary of other
+    sources is reported as traffic_stale instead; a missing one leaves traffic None."""
+    if not os.path.exists(path):
+        return row
+    import json
+    with open(path) as f:
+        t = json.load(f)
+    if t.get("shape") != row.get("shape") or t.get("dtype", "fp32") != dtype:
+        return row
+    here = src_hash(sources)
+    if t.get("src_sha") == here:
+        row["traffic"] = t["traffic_bytes"]
+        row["traffic_source"] = t.get("source", t.get("stamp", path))
+    else:
+        row["traffic_stale"] = {"pmc_src_sha": t.get("src_sha"), "tree_src_sha": here}
+    return row
+
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E (MI355X_MICROARCH.md)
 FP32_MFMA_TFLOPS = 157.3   # dense fp32 MFMA

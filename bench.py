@@ -207,20 +207,13 @@ def main():
               probe.k3_se(B, S, S, blk.sqe.fc2.weight.shape[0], blk.sqe, dtype=adt),
               probe.hanc_gemm(B * (S // 4) ** 2, model.cnv72.hnc.cnv.weight.shape[0],
                               model.cnv72.conv1.weight.shape[0], dtype=adt)]
-        # HBM traffic of K1 from the committed PMC passes of this same bench command
-        # (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate runs; tools/pmc_traffic.py)
-        tf = os.path.join(ROOT, "profiles", "k1_traffic.json")
-        if os.path.exists(tf):
-            with open(tf) as f:
-                t = json.load(f)
-            if t.get("shape") == rl[0]["shape"] and t.get("dtype", "fp32") == args.dtype:
-                # only PMC passes taken on this tree's K1 sources count
-                if t.get("src_sha") == probe.src_hash():
-                    rl[0]["traffic"] = t["traffic_bytes"]
-                    rl[0]["traffic_source"] = t.get("source", tf)
-                else:
-                    rl[0]["traffic_stale"] = {"k1_traffic_src_sha": t.get("src_sha"),
-                                              "tree_src_sha": probe.src_hash()}
+        # HBM traffic of K1 / K3 from the committed PMC passes of this same bench command
+        # (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate runs; tools/pmc_traffic.py),
+        # only when taken on this tree's kernel sources
+        probe.attach_traffic(rl[0], os.path.join(ROOT, "profiles", "k1_traffic.json"),
+                             args.dtype, probe.K1_SOURCES)
+        probe.attach_traffic(rl[1], os.path.join(ROOT, "profiles", "k3_traffic.json"),
+                             args.dtype, probe.K3_SOURCES)
         line["roofline"] = rl[0]
         line["rooflines"] = rl
     if args.eager:

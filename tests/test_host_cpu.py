@@ -227,3 +227,29 @@ def test_trainer_with_bucket_reducer_gloo_world2():
     for rank, err, nb in res:
         assert nb > 1
         assert err < 1e-6, (rank, err)
+
+
+def test_bench_attaches_pmc_traffic_only_for_the_same_kernel_sources(tmp_path):
+    """bench.py's roofline rows take `traffic` from the committed PMC summaries only when
+    shape, dtype and the kernel-source hash match the tree (accunet.probe.attach_traffic);
+    the committed K1 / K3 summaries describe this tree's sources."""
+    import json
+    from accunet import probe
+    row = {"shape": "16x65536x32", "traffic": None}
+    f = tmp_path / "t.json"
+    base = {"shape": "16x65536x32", "dtype": "fp32", "traffic_bytes": 404.0}
+    f.write_text(json.dumps(dict(base, src_sha=probe.src_hash(probe.K3_SOURCES))))
+    assert probe.attach_traffic(dict(row), str(f), "fp32", probe.K3_SOURCES)["traffic"] == 404.0
+    assert probe.attach_traffic(dict(row), str(f), "bf16", probe.K3_SOURCES)["traffic"] is None
+    other = probe.attach_traffic(dict(row, shape="1x2x3"), str(f), "fp32", probe.K3_SOURCES)
+    assert other["traffic"] is None
+    f.write_text(json.dumps(dict(base, src_sha="0" * 16)))
+    stale = probe.attach_traffic(dict(row), str(f), "fp32", probe.K3_SOURCES)
+    assert stale["traffic"] is None and "traffic_stale" in stale
+    assert probe.attach_traffic(dict(row), str(tmp_path / "none.json"), "fp32")["traffic"] is None
+    prof = os.path.join(os.path.dirname(HERE), "profiles")
+    for name, src, shape in (("k1_traffic.json", probe.K1_SOURCES, "16x256x256x96"),
+                             ("k3_traffic.json", probe.K3_SOURCES, "16x65536x32")):
+        got = probe.attach_traffic({"shape": shape, "traffic": None}, os.path.join(prof, name),
+                                   "fp32", src)
+        assert got["traffic"] is not None, (name, got)

@@ -211,7 +211,9 @@ def main():
         t1 = traffic(K1, K1_GRID, "16x256x256x96")
         t1["source"] = f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE of bench.py --eager ({st}); {r}_pmc_k1.csv"
         json.dump(t1, open(os.path.join(PROF, "k1_traffic.json"), "w"), indent=1)
-        k3 = {"kernels": {}, "shape": "16x65536x32", "stamp": st,
+        from accunet.probe import K3_SOURCES, src_hash
+        k3 = {"kernels": {}, "shape": "16x65536x32", "stamp": st, "dtype": "fp32",
+              "src_sha": src_hash(K3_SOURCES),
               "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), KiB -> bytes"}
         k3rows = []
         for kn in K3:
