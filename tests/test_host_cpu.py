@@ -2,6 +2,7 @@
 symbol include/accunet.h declares, the drop-in module tree matches the
 reference's state_dict / seeded init, the LR schedule, the loud-failure policy
 (no CPU fallback), and the data-parallel gradient reducer on gloo."""
+import ctypes
 import hashlib
 import json
 import os
@@ -253,3 +254,22 @@ def test_bench_attaches_pmc_traffic_only_for_the_same_kernel_sources(tmp_path):
         got = probe.attach_traffic({"shape": shape, "traffic": None}, os.path.join(prof, name),
                                    "fp32", src)
         assert got["traffic"] is not None, (name, got)
+
+
+def test_abi_host_side_contract_without_a_device():
+    """C-ABI entry points that validate their arguments (or only compute host-side
+    geometry) answer without touching the device: bad arguments come back as -2
+    (include/accunet.h), the ticket-bank switch returns the previous bank and ignores
+    out-of-range banks, and the statistics row count of K1 follows its strip tiling."""
+    lib = _lib.load()
+    assert lib.accunet_ticket_bank(1) == 0
+    assert lib.accunet_ticket_bank(7) == 1   # out of range: unchanged
+    assert lib.accunet_ticket_bank(0) == 1
+    assert lib.accunet_ticket_bank(-1) == 0  # query
+    # bz without its BatchNorm state / statistics buffer: rejected before any launch
+    one = ctypes.c_void_p(16)
+    assert lib.accunet_dw3x3_fwd(one, one, None, None, None, 0, 1, one, None, 1, 8, 8, 32,
+                                 one, None, 0, 0, None) == -2
+    assert lib.accunet_gemm(None, None, 0, None) == -2
+    # 16x256x256x96: 8 tiles of 32 pixels per row, 128-row strips -> 16 * 2 * 8 = 256 rows
+    assert lib.accunet_dw3x3_rows(16, 256, 256, 96) == 256
