@@ -30,12 +30,23 @@ def main():
     n = len(marks) - 1
     rows = collections.defaultdict(list)
     busy = 0
+    union = 0  # time with any kernel running (two streams: durations overlap)
     for s, e in zip(marks[:-1], marks[1:]):
+        cs = ce = None
         for t0, t1, k in ev[s:e]:
             rows[k].append(t1 - t0)
             busy += t1 - t0
+            if ce is None or t0 > ce:
+                if ce is not None:
+                    union += ce - cs
+                cs, ce = t0, t1
+            else:
+                ce = max(ce, t1)
+        if ce is not None:
+            union += ce - cs
     wall = (ev[marks[-1]][0] - ev[marks[0]][0]) / n
-    print(f"{n} steps: wall {wall / 1e6:.2f} ms/step, kernel busy {busy / n / 1e6:.2f} ms/step, "
+    print(f"{n} steps: wall {wall / 1e6:.2f} ms/step, GPU busy {union / n / 1e6:.2f} ms/step, "
+          f"kernel time sum {busy / n / 1e6:.2f} ms/step, "
           f"launches {sum(len(v) for v in rows.values()) / n:.0f}/step")
     out = sorted(((sum(v) / n, len(v) / n, sum(v) / len(v), k) for k, v in rows.items()), reverse=True)
     for t, c, avg, k in out[:a.top]:
