@@ -58,6 +58,9 @@ def _flat_off(t: torch.Tensor, off: int) -> torch.Tensor:
 # --------------------------------------------------------------------------
 # ACCUNET_WGRAD_STREAM=0 keeps every backward kernel on one stream (A/B runs).
 _WGRAD_STREAM = os.environ.get("ACCUNET_WGRAD_STREAM", "1") != "0"
+# fork only weight gradients estimated to take at least this many microseconds (each
+# fork / join is a cross-queue graph edge with its own latency; 0 = fork every one)
+_FORK_MIN_US = float(os.environ.get("ACCUNET_WGRAD_FORK_MIN_US", "0"))
 _SIDE_STREAMS = {}
 
 
@@ -84,8 +87,11 @@ class _WgradFork:
     fork use ticket bank 1, the main stream's bank 0, so concurrent reductions never
     share a ticket counter."""
 
-    def __init__(self, like: torch.Tensor):
-        self.on = _WGRAD_STREAM and like.is_cuda
+    def __init__(self, like: torch.Tensor, flops: float = 0.0, nbytes: float = 0.0):
+        # (flops, nbytes): the side branch's work, for the ACCUNET_WGRAD_FORK_MIN_US cut
+        # (estimated at 100 TFLOP/s and 5 TB/s)
+        est_us = max(flops / 1e8, nbytes / 5e6)
+        self.on = _WGRAD_STREAM and like.is_cuda and est_us >= _FORK_MIN_US
         if not self.on:
             return
         self.main = torch.cuda.current_stream(like.device)
@@ -409,7 +415,8 @@ class _PWConvFn(torch.autograd.Function):
         dpro_g = dpro_b = None
         # weight gradient first, on the side stream (overlaps the data gradients below)
         dW = None
-        fork = _WgradFork(dZ)
+        cin = sum(cfg.src_ch)
+        fork = _WgradFork(dZ, 2.0 * N * P * cin, float(P * (N + cin) * dZ.element_size()))
         if nig[1]:
             full = (cfg.w_off == 0 and kbeg[-1] == cfg.w_ld)
             if cfg.wslot is not None:  # the sharing calls write disjoint slices covering W
@@ -568,7 +575,7 @@ class _DWConvFn(torch.autograd.Function):
         dA = torch.empty_like(z)
         dW = torch.empty_like(weight)
         db = _f32((C,), z)
-        fork = _WgradFork(dZ)
+        fork = _WgradFork(dZ, 18.0 * B * H * W * C, 2.0 * B * H * W * C * dZ.element_size())
         with fork:  # weight / bias gradient on the side stream (overlaps the data gradient)
             ws = kern.dw3x3_wgrad(z, dZ, pro.st[2] if pro.active else None,
                                   pro.st[3] if pro.active else None, pro.act, dW, db, B, H, W, C)
@@ -709,7 +716,8 @@ class _HancLayerFn(torch.autograd.Function):
                 dG4 = _act((B, H // 4, W // 4, N), dZ)
                 kern.upsample_bwd(dZ, N, 0, dG4, N, B, H, W, N, 4)
         # the three weight-gradient GEMMs on the side stream (overlap the data gradients)
-        fork = _WgradFork(dZ)
+        fork = _WgradFork(dZ, 2.0 * N * C * P * (1 + (1 if k >= 2 else 0) / 2 +
+                                                 (1 if k == 3 else 0) / 8))
         with fork:
             if k >= 2:
                 keep.append(kern.gemm(N, 2 * C, P // 4, a=[dG2], lda=[N], amode=AMODE_COL, b=p2,
@@ -978,7 +986,7 @@ class _Conv3x3Fn(torch.autograd.Function):
         dx = None
         dWr = _f32((Co, 9 * Ci), x)
         dW = torch.empty_like(weight)
-        fork = _WgradFork(dZ)
+        fork = _WgradFork(dZ, 2.0 * Co * 9 * Ci * P)
         with fork:  # weight gradient on the side stream (overlaps the data gradient)
             keep.append(kern.gemm(Co, 9 * Ci, P, a=[dZ], lda=[Co], amode=AMODE_COL, b=x, ldb=Ci,
                                   bmode=BMODE_NN_SHIFT3, c=dWr, ldc=9 * Ci, H=H, W=W, cin=Ci,
@@ -1047,7 +1055,7 @@ class _ConvT2Fn(torch.autograd.Function):
         dx = None
         dWr = _f32((Ci, 4 * Co), x)
         dW = _f32((Ci, Co, 2, 2), x)
-        fork = _WgradFork(dT)
+        fork = _WgradFork(dT, 2.0 * Ci * 4 * Co * P)
         with fork:  # weight gradient on the side stream (overlaps the data gradient)
             keep.append(kern.gemm(Ci, 4 * Co, P, a=[x], lda=[Ci], amode=AMODE_COL, b=dT,
                                   ldb=4 * Co, bmode=BMODE_NN, c=dWr, ldc=4 * Co, allow_split=True))
