@@ -15,7 +15,3 @@ for dt in fp32 bf16; do
 done
 timeout -k 10 120 tools/kbench 20 > gpurun_out/kbench.txt 2>&1
 cat gpurun_out/kbench.txt
-ACCUNET_DW_DMA=1 timeout -k 10 120 tools/kbench 20 > gpurun_out/kbench_dma.txt 2>&1
-grep -E "K1" gpurun_out/kbench_dma.txt
-ACCUNET_DW_DMA=1 timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/bench_dma.log 2>&1
-grep '^{"metric' gpurun_out/bench_dma.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('DMA', d['dtype'], d['value'], d['ms_per_step'], [(r['kernel'][:30], r['avg_us'], r.get('median_us'), r['frac']) for r in d['rooflines']])"
