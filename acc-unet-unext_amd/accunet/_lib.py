@@ -65,7 +65,7 @@ _SIGS = {
     "accunet_gemm": [POINTER(AccGemmDesc), P, S, P],
     "accunet_gemm_stats_rows": [I, I, I, I, I, I],
     "accunet_stream_rows": [L, I],
-    "accunet_ticket_bank": [I],
+    "accunet_stream_ticket_bank": [P, I],
     "accunet_bn_finalize": [P, I, I, D, P, P, P, P, P, F, F, I, P, P, P],
     "accunet_affine_act_fwd": [P, P, P, I, P, P, L, I, P, IP, I, P],
     "accunet_bn_bwd_ws_elems": [L, I],

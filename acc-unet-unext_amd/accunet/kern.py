@@ -52,6 +52,10 @@ def _same_dt(ref: torch.Tensor, *ts):
     return _dt(ref)
 
 
+# marker ids accunet_graph_marker accepts (ACC_MAX_MARKERS in csrc/misc.hip)
+MAX_GRAPH_MARKERS = 32
+
+
 class GraphEvent:
     """A hipEvent_t for the graph-mode all-reduce gating (see include/accunet.h,
     accunet_graph_events_after_markers): `mark(id)` during capture leaves marker id
@@ -79,7 +83,7 @@ class GraphEvent:
         return n
 
     def wait(self, stream):
-        call("accunet_stream_wait_event", ctypes.c_void_p(stream.cuda_stream), self.h)
+        call("accunet_stream_wait_event", ctypes.ctypes.c_void_p(stream.cuda_stream), self.h)
 
     def synchronize(self):
         call("accunet_event_synchronize", self.h)
@@ -265,10 +269,10 @@ def _lib_raw():
     return _lib.load()
 
 
-def ticket_bank(bank: int) -> int:
-    """Ticket bank of the statistics reductions enqueued from now on (accunet_ticket_bank);
-    returns the previous one."""
-    return int(_lib_raw().accunet_ticket_bank(int(bank)))
+def stream_ticket_bank(stream, bank: int) -> None:
+    """Register the ticket bank of the statistics reductions enqueued on `stream`
+    (a torch.cuda.Stream; accunet_stream_ticket_bank). Unregistered streams use bank 0."""
+    call("accunet_stream_ticket_bank", ctypes.c_void_p(stream.cuda_stream), int(bank))
 
 
 def dw3x3_rows(B, H, W, C) -> int:

@@ -62,6 +62,7 @@ _WGRAD_STREAM = os.environ.get("ACCUNET_WGRAD_STREAM", "1") != "0"
 # fork / join is a cross-queue graph edge with its own latency; 0 = fork every one)
 _FORK_MIN_US = float(os.environ.get("ACCUNET_WGRAD_FORK_MIN_US", "0"))
 _SIDE_STREAMS = {}
+FORK_COUNTS = [0, 0]  # weight gradients kept on the main stream / forked (diagnostics)
 
 
 def set_wgrad_stream(on: bool) -> bool:
@@ -69,6 +70,15 @@ def set_wgrad_stream(on: bool) -> bool:
     global _WGRAD_STREAM
     prev = _WGRAD_STREAM
     _WGRAD_STREAM = bool(on)
+    return prev
+
+
+def set_wgrad_fork_min_us(us: float) -> float:
+    """Fork only weight gradients estimated at >= `us` microseconds (0 = fork every one;
+    the default comes from ACCUNET_WGRAD_FORK_MIN_US); returns the previous cut."""
+    global _FORK_MIN_US
+    prev = _FORK_MIN_US
+    _FORK_MIN_US = float(us)
     return prev
 
 
@@ -83,21 +93,25 @@ class _WgradFork:
     waits for side) runs before the backward returns, so every tensor the side stream
     read or wrote is freed -- or handed to autograd -- after the join in main-stream
     order, and the caching allocator never hands out a block the side stream still
-    uses. The one-launch statistics reductions (reduce_finish) enqueued inside the
-    fork use ticket bank 1, the main stream's bank 0, so concurrent reductions never
-    share a ticket counter."""
+    uses. The one-launch statistics reductions (reduce_finish) enqueued on the side
+    stream use ticket bank 1 (registered per stream in the library when the stream is
+    created), every other stream bank 0, so concurrent reductions never share a ticket
+    counter, whichever thread enqueues them."""
 
     def __init__(self, like: torch.Tensor, flops: float = 0.0, nbytes: float = 0.0):
         # (flops, nbytes): the side branch's work, for the ACCUNET_WGRAD_FORK_MIN_US cut
         # (estimated at 100 TFLOP/s and 5 TB/s)
         est_us = max(flops / 1e8, nbytes / 5e6)
         self.on = _WGRAD_STREAM and like.is_cuda and est_us >= _FORK_MIN_US
+        if _WGRAD_STREAM and like.is_cuda:
+            FORK_COUNTS[int(self.on)] += 1
         if not self.on:
             return
         self.main = torch.cuda.current_stream(like.device)
         side = _SIDE_STREAMS.get(like.device.index)
         if side is None:
             side = _SIDE_STREAMS[like.device.index] = torch.cuda.Stream(device=like.device)
+            kern.stream_ticket_bank(side, 1)
         self.side = side
         side.wait_stream(self.main)
 
@@ -105,12 +119,10 @@ class _WgradFork:
         if self.on:
             self._ctx = torch.cuda.stream(self.side)
             self._ctx.__enter__()
-            self._bank = kern.ticket_bank(1)
         return self
 
     def __exit__(self, *exc):
         if self.on:
-            kern.ticket_bank(self._bank)
             self._ctx.__exit__(*exc)
         return False
 
@@ -209,9 +221,12 @@ class GradSlot:
             self.buf = torch.empty(shape, dtype=like.dtype, device=like.device)
         self.pend = []
         if len(adds) > 3:  # the epilogue takes three addends; fold the rest first
+            # into a tensor this slot owns: the shared buffer when it already holds a
+            # contribution, else a copy -- give() tensors are read, never written
+            acc = adds[0] if adds[0] is self.buf else adds[0].clone()
             for t in adds[3:]:
-                adds[0].add_(t)
-            adds = adds[:3]
+                acc.add_(t)
+            adds = [acc] + adds[1:3]
         return self.buf, adds
 
     def acc_target(self, shape, like):

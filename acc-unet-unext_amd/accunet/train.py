@@ -41,6 +41,25 @@ from .loss import WeightedDiceBCE
 from .optim import FusedAdam
 
 
+def cut_buckets(numels, bucket_mb):
+    """Parameter indices per bucket, in reverse registration order (backward finishes
+    the output layer first); each bucket but the last holds >= bucket_mb of fp32. One
+    graph marker per bucket, and accunet_graph_marker takes MAX_GRAPH_MARKERS ids, so
+    a smaller bucket_mb is raised until the greedy cut yields at most that many."""
+    total = sum(numels)
+    cap = max(1, int(bucket_mb * (1 << 20) / 4), -(-total // kern.MAX_GRAPH_MARKERS))
+    buckets, cur, n = [], [], 0
+    for i in reversed(range(len(numels))):
+        cur.append(i)
+        n += numels[i]
+        if n >= cap:
+            buckets.append(cur)
+            cur, n = [], 0
+    if cur:
+        buckets.append(cur)
+    return buckets
+
+
 class _GraphBuckets:
     """Bucketed, event-gated gradient all-reduce for the captured backward (graph mode,
     world > 1; see the module docstring). Built before capture; its hooks run only
@@ -55,16 +74,7 @@ class _GraphBuckets:
             offs.append(o)
             self.views.append(self.flat[o:o + p.numel()].view_as(p))
             o += p.numel()
-        cap = max(1, int(bucket_mb * (1 << 20) / 4))
-        self.buckets, cur, n = [], [], 0
-        for i in reversed(range(len(params))):  # backward finishes the output layer first
-            cur.append(i)
-            n += params[i].numel()
-            if n >= cap:
-                self.buckets.append(cur)
-                cur, n = [], 0
-        if cur:
-            self.buckets.append(cur)
+        self.buckets = cut_buckets([p.numel() for p in params], bucket_mb)
         self.range = [(min(offs[i] for i in b), max(offs[i] + params[i].numel() for i in b))
                       for b in self.buckets]
         self.bucket_of = {i: k for k, b in enumerate(self.buckets) for i in b}
@@ -143,6 +153,9 @@ class TrainStep:
         self.pg = process_group
         self.world = (dist.get_world_size(process_group)
                       if dist.is_available() and dist.is_initialized() else 1)
+        # data-parallel path: world > 1, or an explicitly passed process group (also at
+        # world 1, where the all-reduce is an identity: tests run the RCCL branch so)
+        self.dp = self.world > 1 or process_group is not None
         self.criterion = WeightedDiceBCE(dice_weight, bce_weight)
         self.params = [p for p in model.parameters() if p.requires_grad]
         # eager single GPU: gradients are the tensors the backward kernels produce
@@ -151,7 +164,7 @@ class TrainStep:
         self.opt = FusedAdam(self.params, lr=lr)
         self._g = None
         self.bucket_mb = bucket_mb
-        if graph and self.world > 1:
+        if graph and self.dp:
             # identical replicas to start from (what DDP / GradBucketReducer do at wrap time)
             with torch.no_grad():
                 for t in list(self.params) + [b for b in model.buffers()]:
@@ -206,7 +219,7 @@ class TrainStep:
         torch.cuda.synchronize()
 
         self._buckets = None
-        if self.world > 1:
+        if self.dp:
             self._buckets = _GraphBuckets(self.params, self.bucket_mb, self._x.device)
             self._buckets.stream = torch.cuda.Stream()
             self._buckets.arm()
@@ -229,7 +242,7 @@ class TrainStep:
         # keep the graph-pool gradient tensors alive; the optimizer reads either them
         # (world 1) or the flat all-reduced buffer (world > 1)
         self._graph_grads = [p.grad for p in self.params]
-        if self.world > 1:
+        if self.dp:
             for p, v in zip(self.params, self._buckets.views):
                 p.grad = v
         else:
@@ -250,7 +263,7 @@ class TrainStep:
         if masks.data_ptr() != self._m.data_ptr():
             self._m.copy_(masks)
         self._g.replay()
-        if self.world > 1:
+        if self.dp:
             self._buckets.reduce(self.pg)
         self.opt.step()
         return self._loss

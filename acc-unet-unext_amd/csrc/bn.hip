@@ -6,6 +6,7 @@
 // ACC_UNet/ACC_UNet.py, e.g. :235-262): normalise with the biased batch
 // variance, update running_mean / running_var with momentum 0.1 using the
 // UNBIASED variance, eps = 1e-5; eval mode uses the running statistics.
+#include <mutex>
 #include "common.h"
 #include "kernels.h"
 
@@ -114,25 +115,49 @@ size_t accunet_partials_ws_elems(int R, int Wd) {
 // (it replaces the colreduce stages + finish kernel: 2-4 launches of a few us each
 // per BatchNorm). Grid (nchunk, column blocks of 64). Block (k, y) sums rows
 // [k*rpc, (k+1)*rpc) of its 64 columns in a fixed order (fp64) into chunk row k;
-// the last block of column block y to arrive (ticket counter, agent-scope release /
-// acquire: MI355X guide section 6, Guideline 16) adds the nchunk chunk rows in index
-// order and runs the finish. The chunking depends on R only, so the result is
+// the last block of column block y to arrive (ticket counter; the chunk totals are
+// handed over with write-through stores and sc1 loads, no fences -- see handoff_last
+// in common.h) adds the nchunk chunk rows in index order and runs the finish. The chunking depends on R only, so the result is
 // bitwise reproducible. Paired kinds (BatchNorm) map thread column cl < 32 to the
 // first moment of channel 32y+cl and cl >= 32 to its second moment (column C+ch).
 // The tickets live in a zero-initialised device array; every last arriver resets
 // its word, so consecutive launches on a stream (and graph replays) reuse it.
 // ---------------------------------------------------------------------------
 #define FIN_MAX_CB 16384  // column blocks (ncols <= 262144: dw wgrad of cnv72 has 10 x 4352)
-// One ticket array per bank: launches that may run concurrently (the backward's side
-// stream, accunet_ticket_bank) must not share tickets.
+// One ticket array per bank: launches that may run concurrently must not share
+// tickets. The bank is a property of the STREAM a reduction is enqueued on: the host
+// registers its side streams (accunet_stream_ticket_bank, e.g. the backward's
+// weight-gradient stream -> bank 1) and every other stream uses bank 0. Keying by
+// stream (not by a "current bank" switch) keeps the choice correct whatever thread
+// enqueues the launch; the ticket array itself is per device (a __device__ symbol).
 #define FIN_BANKS 2
 __device__ unsigned g_fin_tickets[FIN_BANKS * FIN_MAX_CB];
-static int g_ticket_bank = 0;
+#define FIN_MAX_STREAMS 64
+static std::mutex g_bank_mu;
+static hipStream_t g_bank_stream[FIN_MAX_STREAMS];
+static int g_bank_of[FIN_MAX_STREAMS];
+static int g_bank_n = 0;
 
-extern "C" int accunet_ticket_bank(int bank) {
-  const int prev = g_ticket_bank;
-  if (bank >= 0 && bank < FIN_BANKS) g_ticket_bank = bank;
-  return prev;
+extern "C" int accunet_stream_ticket_bank(void* stream, int bank) {
+  if (bank < 0 || bank >= FIN_BANKS || !stream) return ACC_EBADARG;
+  std::lock_guard<std::mutex> lk(g_bank_mu);
+  for (int i = 0; i < g_bank_n; ++i)
+    if (g_bank_stream[i] == (hipStream_t)stream) {
+      g_bank_of[i] = bank;
+      return ACC_OK;
+    }
+  if (g_bank_n == FIN_MAX_STREAMS) return ACC_EBADARG;
+  g_bank_stream[g_bank_n] = (hipStream_t)stream;
+  g_bank_of[g_bank_n++] = bank;
+  return ACC_OK;
+}
+
+static int stream_bank(hipStream_t s) {
+  if (!s) return 0;
+  std::lock_guard<std::mutex> lk(g_bank_mu);
+  for (int i = 0; i < g_bank_n; ++i)
+    if (g_bank_stream[i] == s) return g_bank_of[i];
+  return 0;
 }
 
 ACC_DEV void fin_column(const FinishArgs& fa, int col, double tot) {
@@ -277,7 +302,7 @@ size_t reduce_finish_ws(int R, int stride) {
 int reduce_finish(const void* part, bool part_f64, int R, int stride, double* chunks,
                   const FinishArgs& fa_in, hipStream_t s) {
   FinishArgs fa = fa_in;
-  fa.bank = g_ticket_bank;
+  fa.bank = stream_bank(s);
   const bool paired = fa.kind == FIN_BN_FWD || fa.kind == FIN_BN_BWD;
   const int rpc = fin_rows_per_chunk(R);
   const int nchunk = max(1, ceil_div(R, rpc));

@@ -109,11 +109,14 @@ int accunet_gemm_stats_rows(int M, int N, int K, int amode, int bmode, int cin);
  * fp64 everywhere (ATen's CPU BatchNorm also accumulates in double).
  * ------------------------------------------------------------------------- */
 int accunet_stream_rows(long P, int C);
-/* Ticket bank (0 or 1) of the one-launch statistics reductions enqueued from now on
- * (their last-arriver hand-off counts arrivals in a device ticket array): launches
- * that may run concurrently on two streams must use different banks. No reference
- * counterpart (the reference's reductions are ATen's). Returns the previous bank. */
-int accunet_ticket_bank(int bank);
+/* Ticket bank (0 or 1) of the one-launch statistics reductions enqueued on `stream`
+ * (their last-arriver hand-off counts arrivals in a per-device ticket array): streams
+ * that may run reductions concurrently must use different banks. Unregistered streams
+ * (and the null stream) use bank 0; the registration is keyed by the stream, so it
+ * holds whatever host thread enqueues the launch. Returns 0, or -2 for a bank outside
+ * 0..1, a null stream or a full table (64 streams). No reference counterpart (the
+ * reference's reductions are ATen's). */
+int accunet_stream_ticket_bank(void* stream, int bank);
 int accunet_bn_finalize(const double* part, int R, int C, double count, const float* gamma,
                         const float* beta, float* rmean, float* rvar, long long* nbt,
                         float momentum, float eps, int training, float* st, double* ws,

@@ -3,13 +3,18 @@
 Launched by torch.distributed.run with ACCUNET_DIST_BACKEND=gloo so that two ranks
 can share the single GPU of a test box (RCCL refuses two ranks on one device); the
 data-parallel code path is the one bench.py runs over RCCL on a node:
-  1. graph mode: TrainStep(graph=True) = HIP-graph replay + one flat gradient
-     all-reduce (mean) + fused Adam, 3 steps on rank-specific data;
+  1. graph mode: TrainStep(graph=True, bucket_mb=0.25) = HIP-graph replay + the
+     event-gated bucketed all-reduce (mean; ~16 buckets of the n_filts=8 model, so
+     the multi-bucket marker/event path runs) + fused Adam, 3 steps on rank-specific
+     data;
   2. eager mode: TrainStep with GradBucketReducer (bucketed all-reduce overlapped
      with backward through post-accumulate-grad hooks), same start, same data.
   3. the epoch loop: Trainer(reducer=GradBucketReducer) over the same batches.
-Checks: parameters identical on both ranks after each mode (bitwise), both modes
-agree with each other, and the parameters moved.
+  4./5. graph and eager again in bf16 storage (BASELINE configs[2]'s precision).
+Checks: parameters identical on both ranks after each mode (bitwise), graph and eager
+identical to each other (bitwise, fp32 and bf16: the same kernels in the same order,
+and a world-2 sum is order-free), the epoch loop equal to eager, and the parameters
+moved.
 """
 import os
 import sys
@@ -35,6 +40,9 @@ def run(mode, sd, data, dev):
     m = ACC_UNet(3, 1, n_filts=8)
     m.load_state_dict(sd)
     m = m.to(dev).train()
+    prec = None
+    if mode.endswith("_bf16"):
+        mode, prec = mode[:-5], "bf16"
     if mode == "trainer":  # the epoch loop with the bucketed reducer (Trainer(reducer=))
         from accunet.trainer import Trainer
         tr = Trainer(m, lr=1e-3, lr_scheduler=None, device=dev,
@@ -43,13 +51,18 @@ def run(mode, sd, data, dev):
         torch.cuda.synchronize()
         return flat_params(m), [h["loss"] for h in tr.history]
     if mode == "graph":
-        step = TrainStep(m, lr=1e-3, graph=True)
+        step = TrainStep(m, lr=1e-3, graph=True, bucket_mb=0.25, precision=prec)
     else:
-        step = TrainStep(m, lr=1e-3, reducer=adist.GradBucketReducer(m, bucket_mb=0.25))
+        step = TrainStep(m, lr=1e-3, reducer=adist.GradBucketReducer(m, bucket_mb=0.25),
+                         precision=prec)
     losses = []
     for x, y in data:
         losses.append(float(step(x, y)))
     torch.cuda.synchronize()
+    if mode == "graph":
+        nb = len(step._buckets.buckets)
+        assert nb >= 3, f"graph mode ran {nb} bucket(s); the multi-bucket path needs >= 3"
+        print(f"graph{'_' + prec if prec else ''}: {nb} buckets", flush=True)
     return flat_params(m), losses
 
 
@@ -65,7 +78,7 @@ def main():
     data = [(torch.randn(2, 3, 32, 32, generator=g).to(dev),
              (torch.rand(2, 1, 32, 32, generator=g) < 0.3).float().to(dev)) for _ in range(3)]
     out = {}
-    for mode in ("graph", "eager", "trainer"):
+    for mode in ("graph", "eager", "trainer", "graph_bf16", "eager_bf16"):
         p, losses = run(mode, sd, data, dev)
         other = [torch.empty_like(p) for _ in range(world)]
         dist.all_gather(other, p)
@@ -76,10 +89,11 @@ def main():
               flush=True)
         assert same, f"{mode}: parameters differ between ranks"
         assert moved > 1e-5, f"{mode}: parameters did not move"
-    d = float((out["graph"][0] - out["eager"][0]).abs().max())
-    print(f"rank {rank} graph vs eager max|dp| {d:.3e}", flush=True)
-    assert d < 1e-5, d
-    assert all(abs(a - b) < 1e-5 for a, b in zip(out["graph"][1], out["eager"][1]))
+    for sfx in ("", "_bf16"):
+        d = float((out["graph" + sfx][0] - out["eager" + sfx][0]).abs().max())
+        print(f"rank {rank} graph{sfx} vs eager{sfx} max|dp| {d:.3e}", flush=True)
+        assert torch.equal(out["graph" + sfx][0], out["eager" + sfx][0]), d
+        assert out["graph" + sfx][1] == out["eager" + sfx][1]
     # the epoch loop runs the same steps (its loss is the epoch average)
     d = float((out["trainer"][0] - out["eager"][0]).abs().max())
     print(f"rank {rank} trainer vs eager max|dp| {d:.3e}", flush=True)

@@ -22,10 +22,10 @@ def _port():
     return p
 
 
-def _run(args, timeout=280):
-    env = dict(os.environ, ACCUNET_DIST_BACKEND="gloo", OMP_NUM_THREADS="4")
+def _run(args, timeout=280, nproc=2, backend="gloo"):
+    env = dict(os.environ, ACCUNET_DIST_BACKEND=backend, OMP_NUM_THREADS="4")
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
            "--master-addr", "127.0.0.1", "--master-port", str(_port())] + args
     return subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
 
@@ -35,6 +35,16 @@ def test_world2_graph_and_bucketed_reducer_agree():
     r = _run([os.path.join(HERE, "dist_worker.py")])
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "DIST_OK" in r.stdout
+
+
+@pytest.mark.gpu
+def test_rccl_world1_graph_buckets():
+    """The RCCL (nccl backend) branch of the graph-mode bucketed all-reduce
+    (_GraphBuckets.reduce) on the box's one GPU: >= 3 buckets, fp32 and bf16, bit-equal
+    to the plain world-1 graph step (tests/nccl_worker.py)."""
+    r = _run([os.path.join(HERE, "nccl_worker.py")], nproc=1, backend="nccl")
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "RCCL_OK" in r.stdout, r.stdout[-2000:]
 
 
 @pytest.mark.gpu

@@ -105,3 +105,26 @@ def test_gradslot_folds_extra_addends():
     assert len(adds) <= 3
     buf.copy_(parts[4] + sum(adds))
     torch.testing.assert_close(slot.done(), sum(parts), rtol=1e-12, atol=1e-12)
+
+
+def test_gradslot_fold_never_writes_given_tensors():
+    """give() promises its tensors are only read: with more than three contributions
+    the fold goes into a tensor the slot owns, never into a given (autograd-owned)
+    gradient such as a residual add's incoming dy. The tensors are passed without
+    cloning, and must be unchanged afterwards."""
+    torch.manual_seed(3)
+    shape = (3, 3)
+    slot = ops.GradSlot()
+    parts = [torch.randn(shape, dtype=torch.float64) for _ in range(5)]
+    keep = [p.clone() for p in parts]
+    for _ in parts:
+        slot.register()
+    for p in parts[:4]:
+        slot.give(p)
+        assert slot.done() is None
+    buf, adds = slot.gemm_target(shape, parts[0])
+    assert len(adds) <= 3
+    buf.copy_(parts[4] + sum(adds))
+    torch.testing.assert_close(slot.done(), sum(keep), rtol=1e-12, atol=1e-12)
+    for p, k in zip(parts, keep):
+        assert torch.equal(p, k)

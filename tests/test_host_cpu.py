@@ -256,16 +256,35 @@ def test_bench_attaches_pmc_traffic_only_for_the_same_kernel_sources(tmp_path):
         assert got["traffic"] is not None, (name, got)
 
 
+def test_graph_buckets_respect_the_marker_table():
+    """Graph-mode DP cuts one marker per bucket; the library's marker table holds 32.
+    A tiny bucket_mb on ACC_UNet's 918 gradients (16.77 M elements) still gives <= 32
+    buckets, covering every parameter exactly once in reverse registration order, and
+    a 16 MB cut gives the 4-5 buckets bench.py runs with."""
+    from accunet import kern
+    from accunet.model import ACC_UNet
+    from accunet.train import cut_buckets
+    numels = [p.numel() for p in ACC_UNet(3, 1).parameters()]
+    for mb, lo, hi in ((0.001, 2, kern.MAX_GRAPH_MARKERS), (16.0, 4, 5)):
+        b = cut_buckets(numels, mb)
+        assert lo <= len(b) <= hi, (mb, len(b))
+        flat = [i for k in b for i in k]
+        assert flat == list(reversed(range(len(numels))))
+
+
 def test_abi_host_side_contract_without_a_device():
     """C-ABI entry points that validate their arguments (or only compute host-side
     geometry) answer without touching the device: bad arguments come back as -2
-    (include/accunet.h), the ticket-bank switch returns the previous bank and ignores
-    out-of-range banks, and the statistics row count of K1 follows its strip tiling."""
+    (include/accunet.h), the per-stream ticket-bank registration rejects out-of-range
+    banks and the null stream (a host-side table, no device call), and the statistics
+    row count of K1 follows its strip tiling."""
     lib = _lib.load()
-    assert lib.accunet_ticket_bank(1) == 0
-    assert lib.accunet_ticket_bank(7) == 1   # out of range: unchanged
-    assert lib.accunet_ticket_bank(0) == 1
-    assert lib.accunet_ticket_bank(-1) == 0  # query
+    fake = ctypes.c_void_p(0x1234)  # only used as a table key, never dereferenced
+    assert lib.accunet_stream_ticket_bank(fake, 1) == 0
+    assert lib.accunet_stream_ticket_bank(fake, 0) == 0   # re-registration overwrites
+    assert lib.accunet_stream_ticket_bank(fake, 2) == -2  # out of range
+    assert lib.accunet_stream_ticket_bank(fake, -1) == -2
+    assert lib.accunet_stream_ticket_bank(None, 1) == -2  # null stream is always bank 0
     # bz without its BatchNorm state / statistics buffer: rejected before any launch
     one = ctypes.c_void_p(16)
     assert lib.accunet_dw3x3_fwd(one, one, None, None, None, 0, 1, one, None, 1, 8, 8, 32,

@@ -324,6 +324,42 @@ def test_side_stream_weight_gradients_bit_identical(graph, precision):
         assert torch.equal(v, runs[True][1][k]), k
 
 
+@pytest.mark.parametrize("graph", [False, True])
+def test_selective_fork_bit_identical(graph):
+    """ACCUNET_WGRAD_FORK_MIN_US > 0 (ops.set_wgrad_fork_min_us): some layers' weight
+    gradients run on the side stream and the others on the main stream in the same
+    backward. Two training steps at cuts 0 (fork every layer), 30 us (a mix at this
+    size: the estimate spans ~1-100 us) and 1e9 (never fork): identical losses,
+    parameters and BatchNorm state bit for bit."""
+    from accunet import ops
+    from accunet.train import TrainStep
+    nf, B, S = 32, 4, 64
+    sd = O.det_state_dict(O.param_spec("canonical", 3, 1, nf), seed=0)
+    x = O.det_input((B, 3, S, S), "golden-x").to(DEV)
+    mask = O.det_mask((B, 1, S, S), "golden-mask", p=0.4).to(DEV)
+    runs = {}
+    prev_s = ops.set_wgrad_stream(True)
+    prev_c = ops.set_wgrad_fork_min_us(0.0)
+    try:
+        for cut in (0.0, 30.0, 1e9):
+            ops.set_wgrad_fork_min_us(cut)
+            m = _hip_model("canonical", sd, nf).train()
+            step = TrainStep(m, lr=1e-3, graph=graph)
+            c0 = list(ops.FORK_COUNTS)
+            losses = [float(step(x, mask).item()) for _ in range(2)]
+            kept, forked = (ops.FORK_COUNTS[0] - c0[0], ops.FORK_COUNTS[1] - c0[1])
+            if cut == 30.0:  # the mixed configuration really mixes
+                assert kept > 0 and forked > 0, (kept, forked)
+            runs[cut] = (losses, {k: v.detach().clone() for k, v in m.state_dict().items()})
+    finally:
+        ops.set_wgrad_stream(prev_s)
+        ops.set_wgrad_fork_min_us(prev_c)
+    for cut in (30.0, 1e9):
+        assert runs[0.0][0] == runs[cut][0], (cut, runs[0.0][0], runs[cut][0])
+        for k, v in runs[0.0][1].items():
+            assert torch.equal(v, runs[cut][1][k]), (cut, k)
+
+
 @pytest.mark.parametrize("variant,B,S", [("canonical", 16, 256), ("w", 4, 512)])
 def test_full_size_configs_properties(variant, B, S):
     """BASELINE configs[1] (canonical, 16x3x256x256) and configs[3] (ACC_UNet_W,
