@@ -83,7 +83,7 @@ class GraphEvent:
         return n
 
     def wait(self, stream):
-        call("accunet_stream_wait_event", ctypes.ctypes.c_void_p(stream.cuda_stream), self.h)
+        call("accunet_stream_wait_event", ctypes.c_void_p(stream.cuda_stream), self.h)
 
     def synchronize(self):
         call("accunet_event_synchronize", self.h)
