@@ -14,7 +14,8 @@ from ctypes import POINTER, Structure, c_double, c_float, c_int, c_longlong, c_s
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # ACCUNET_LIB_OVERRIDE: A/B experiments against another build of the same library
 # (tools/*_ab.sh); unset, the in-tree build is the only one ever loaded
-LIB_PATH = os.environ.get("ACCUNET_LIB_OVERRIDE") or os.path.join(_HERE, "libaccunet_hip.so")
+_DEFAULT_LIB = os.path.join(_HERE, "libaccunet_hip.so")
+LIB_PATH = os.environ.get("ACCUNET_LIB_OVERRIDE") or _DEFAULT_LIB
 
 # mirrors include/accunet.h enums
 AMODE_ROW, AMODE_COL, AMODE_SHIFT3 = 0, 1, 2
@@ -73,6 +74,7 @@ _SIGS = {
     "accunet_colsum": [P, L, I, P, P, S, I, P],
     "accunet_reduce_stats": [P, I, I, P, P, P],
     "accunet_dw3x3_rows": [I, I, I, I],
+    "accunet_dw3x3_variant": [I, I, I, I],
     "accunet_dw3x3_fwd": [P, P, P, P, P, I, I, P, P, I, I, I, I, P, P, I, I, P],
     "accunet_bn_bwd_part_ws_elems": [L, I, I],
     "accunet_bn_bwd_part": [P, P, P, P, I, I, L, I, P, I, P, P, P, P, P, S, I, P],
@@ -153,6 +155,8 @@ def load():
             "`make -C acc-unet-unext_amd -j8` (or __graft_entry__.build())")
     lib = ctypes.CDLL(LIB_PATH)
     for name, args in _SIGS.items():
+        if LIB_PATH != _DEFAULT_LIB and not hasattr(lib, name):
+            continue  # A/B against an older build: entry points it predates stay unbound
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = c_size_t if name in _SIZE_FNS else c_int

@@ -279,6 +279,17 @@ def dw3x3_rows(B, H, W, C) -> int:
     return int(_lib_raw().accunet_dw3x3_rows(B, H, W, C))
 
 
+_DW_NAMES = {2: "dw3x3_span_fwd_kernel", 1: "dw3x3_tile_fwd_kernel", 0: "dw3x3_fwd_kernel"}
+
+
+def dw3x3_kernel_name(B, H, W, C) -> str:
+    """the forward depthwise kernel accunet_dw3x3_fwd launches for this shape"""
+    lib = _lib_raw()
+    if not hasattr(lib, "accunet_dw3x3_variant"):  # an older build (A/B runs)
+        return _DW_NAMES[1 if C % 32 == 0 else 0]
+    return _DW_NAMES[int(lib.accunet_dw3x3_variant(B, H, W, C))]
+
+
 def dw3x3_fwd(x, wt, bias, sc, sh, act, flip, z, stats, B, H, W, C, bnb=None):
     """bnb = (bz, bst, bact): `stats` receives BatchNorm-backward partials (see
     accunet_dw3x3_fwd in include/accunet.h)."""

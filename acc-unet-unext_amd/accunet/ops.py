@@ -63,6 +63,7 @@ _WGRAD_STREAM = os.environ.get("ACCUNET_WGRAD_STREAM", "1") != "0"
 _FORK_MIN_US = float(os.environ.get("ACCUNET_WGRAD_FORK_MIN_US", "0"))
 _SIDE_STREAMS = {}
 FORK_COUNTS = [0, 0]  # weight gradients kept on the main stream / forked (diagnostics)
+FORK_LOG = None  # a list: the estimated side-branch microseconds of every fork decision
 
 
 def set_wgrad_stream(on: bool) -> bool:
@@ -105,6 +106,8 @@ class _WgradFork:
         self.on = _WGRAD_STREAM and like.is_cuda and est_us >= _FORK_MIN_US
         if _WGRAD_STREAM and like.is_cuda:
             FORK_COUNTS[int(self.on)] += 1
+            if FORK_LOG is not None:
+                FORK_LOG.append(est_us)
         if not self.on:
             return
         self.main = torch.cuda.current_stream(like.device)
@@ -564,7 +567,7 @@ class _DWConvFn(torch.autograd.Function):
             stats = _stats((kern.dw3x3_rows(B, H, W, C), 2, C), z)
         pro = cfg.pro
         # csrc/dwconv.hip picks the LDS-tiled kernel whenever C % 32 == 0
-        kname = "dw3x3_tile_fwd_kernel" if C % 32 == 0 else "dw3x3_fwd_kernel"
+        kname = kern.dw3x3_kernel_name(B, H, W, C)
         with _prof.region(f"dw3x3_fwd B{B} {H}x{W} C{C}", kernel=kname,
                           shape=f"{B}x{H}x{W}x{C}",
                           bytes_alg=2.0 * z.element_size() * B * H * W * C):

@@ -714,6 +714,422 @@ dw3x3_tile_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dz,
   }
 }
 
+// ----------------------------------------------------------------------------
+// Span kernel (CQ = C/4 quads per pixel, CQ even and <= 64: every HANC width up to
+// 256 channels). A block owns R output rows x PX = NT/CQ whole pixels of one image, so
+// each row of its input tile -- pixels w0-1 .. w0+PX, every channel -- is ONE
+// contiguous (PX+2)*C-element segment of the NHWC row. Non-persistent: the whole
+// (R+2)-row halo tile is fetched with every load in flight (branch-free buffer loads,
+// out-of-image quads masked by the descriptor range), activated (prologue BN+act) into
+// LDS, and each of the PX*CQ compute lanes slides its 3x3 window down its pixel-quad
+// column. tools/k1lab (16x256x256x96 fp32, copies of K1's bytes without arithmetic):
+// whole-pixel spans stream at 78 % of HBM peak, the 32-pixel x 32-channel tiles of
+// the kernel above at 73 % (70 % through an LDS halo tile) and its persistent strip
+// pipeline at 66 %.
+// ----------------------------------------------------------------------------
+struct DwSGeom {
+  int B, H, W, C;
+  int CQ, PX;      // quads per pixel, output pixels per span (NT / CQ)
+  int NS, tilesH;  // spans per image row, row tiles per image
+  int remap;       // XCD-contiguous block order (tuning knob ACCUNET_DW_SPAN_REMAP)
+};
+
+#define DWS_R 8  // output rows per span block
+
+template <int NT>
+struct DwS {
+  static constexpr int R = DWS_R;
+  static constexpr int RWMAX = NT + 2 * (NT == 256 ? 32 : 64);  // (PX+2)*CQ, CQ <= NT/8
+  static constexpr int TILE = (R + 2) * RWMAX;                   // float4 slots
+  // 16-byte fill loads per lane: (R+2)*(PX+2)*CQ quads over PX*CQ lanes, PX >= 8
+  static constexpr int NLMAX = ((R + 2) * 10 + 7) / 8;
+};
+
+// Span-tile fill, split in two so independent work can sit between the loads and
+// their use: dws_issue fetches the (R+2)-row halo tile of rows h0-1 .. h0+R, pixels
+// w0-1 .. w0+PX (units of QL quads, fill lane f < NA/QL taking units f, f + NA/QL, ...:
+// a stride that is a multiple of CQ/QL, so a lane always stages the same QL quads),
+// out-of-image units masked by the descriptor range; dws_park activates them
+// (prologue BN+act, in-image only) into the LDS tile [R+2][RW] and zero-fills the rest.
+template <int NT, int AUX, typename T>
+struct DwsFill {
+  static constexpr int QL = Raw16<T>::QL;
+  typedef typename Raw16<T>::type RawL;
+  RawL v[DwS<NT>::NLMAX];
+  unsigned inb;
+  float4 ps[QL], pb[QL];
+  ACC_DEV void issue(__amdgpu_buffer_rsrc_t rx, const DwSGeom& g, int h0, int s0,
+                     const float* sc, const float* sh) {
+    constexpr int R = DwS<NT>::R;
+    // (tid laundered through an empty asm: inside a caller's loop the per-unit index
+    // math is then recomputed per call instead of hoisted and kept live in registers)
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const int CQ = g.CQ, RW = (g.PX + 2) * CQ, NF = g.PX * CQ / QL;
+    const int nunits = (R + 2) * RW / QL, L = g.W * CQ;
+    const int qf = (tid * QL) % CQ;
+#pragma unroll
+    for (int j = 0; j < QL; ++j) {
+      ps[j] = sc ? ld4(sc + 4 * (qf + j)) : make_float4(1.f, 1.f, 1.f, 1.f);
+      pb[j] = sc ? ld4(sh + 4 * (qf + j)) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    inb = 0;
+    // unit k sits at tile quad i = (tid + NF k) QL = row r, column jq; NF QL = PX CQ < RW, so
+    // each step advances jq by PX CQ and wraps into the next row at most once
+    int r = (tid * QL) / RW, jq = tid * QL - r * RW;
+#pragma unroll
+    for (int k = 0; k < DwS<NT>::NLMAX; ++k) {
+      const int u = tid + NF * k;
+      const int hh = h0 - 1 + r, pos = s0 - CQ + jq;
+      const bool in = tid < NF && u < nunits && hh >= 0 && hh < g.H && pos >= 0 && pos < L;
+      inb |= (in ? 1u : 0u) << k;
+      v[k] = buf16_ld<AUX>(rx, in ? (unsigned)((hh * L + pos) * 4 * (int)sizeof(T)) : ACC_OOB,
+                           (const T*)nullptr);
+      jq += NF * QL;
+      const bool wrap = jq >= RW;
+      jq -= wrap ? RW : 0;
+      r += wrap ? 1 : 0;
+    }
+  }
+  ACC_DEV void park(float4* __restrict__ tile, const DwSGeom& g, bool pro, int act) const {
+    constexpr int R = DwS<NT>::R;
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const int RW = (g.PX + 2) * g.CQ, NF = g.PX * g.CQ / QL;
+    const int nunits = (R + 2) * RW / QL;
+#pragma unroll
+    for (int k = 0; k < DwS<NT>::NLMAX; ++k) {
+      const int u = tid + NF * k;
+      if (tid < NF && u < nunits) {
+        const bool in = (inb >> k) & 1u;
+#pragma unroll
+        for (int j = 0; j < QL; ++j) {
+          float4 a = r16q(v[k], j);
+          if (pro) {
+            a.x = apply_act(a.x * ps[j].x + pb[j].x, act);
+            a.y = apply_act(a.y * ps[j].y + pb[j].y, act);
+            a.z = apply_act(a.z * ps[j].z + pb[j].z, act);
+            a.w = apply_act(a.w * ps[j].w + pb[j].w, act);
+          }
+          tile[u * QL + j] = in ? a : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+    }
+  }
+};
+
+template <int NT, bool BNB, int AUX, typename T>
+__global__ void __launch_bounds__(NT)
+dw3x3_span_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
+                      const float* __restrict__ bias, const float* __restrict__ sc,
+                      const float* __restrict__ sh, int act, int flip, T* __restrict__ z,
+                      double* __restrict__ stats, DwSGeom g, const T* __restrict__ bz,
+                      const float* __restrict__ bst, int bact) {
+  typedef DwS<NT> G;
+  constexpr int R = G::R;
+  typedef typename QuadRaw<T>::type RawQ;
+  __shared__ float4 tile[G::TILE];
+  const int tid = threadIdx.x;
+  const int CQ = g.CQ, PX = g.PX;
+  const int RW = (PX + 2) * CQ, NA = PX * CQ;
+  int bid = blockIdx.x;
+  if (g.remap) {
+    const int per = gridDim.x >> 3;
+    bid = (bid & 7) * per + (bid >> 3);
+  }
+  const int sp = bid % g.NS;
+  int t = bid / g.NS;
+  const int th = t % g.tilesH;
+  const int b = t / g.tilesH;
+  const int h0 = th * R, w0 = sp * PX;
+  const int L = g.W * CQ;  // quads per image row
+  const int s0 = w0 * CQ;  // first output quad of the span in its row
+  const long img = (long)b * g.H * g.W * g.C;
+  const unsigned ibytes = (unsigned)(g.H * g.W * g.C * (int)sizeof(T));
+  const __amdgpu_buffer_rsrc_t rx = acc_rsrc(x + img, ibytes);
+  const __amdgpu_buffer_rsrc_t rz = acc_rsrc(z + img, ibytes);
+  const __amdgpu_buffer_rsrc_t rb = acc_rsrc(BNB ? bz + img : x + img, BNB ? ibytes : 0u);
+  constexpr unsigned QB = 4 * sizeof(T);  // bytes per quad
+
+  // compute lane: pixel p of the span, quad q
+  const int p = tid / CQ, q = tid - (tid / CQ) * CQ;
+  const bool lane_on = tid < NA && w0 + p < g.W;
+  const int c = 4 * q;
+
+  // BNB: this lane's R rows of bz, in flight with the tile fill
+  RawQ zr[R];
+  if (BNB) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const bool in = lane_on && h0 + r < g.H;
+      zr[r] = bufq_ld<0>(rb, in ? (unsigned)(((h0 + r) * L + s0 + tid) * QB) : ACC_OOB,
+                         (const T*)nullptr);
+    }
+  }
+  DwsFill<NT, AUX, T> fill;
+  const bool pro = sc != nullptr;
+  fill.issue(rx, g, h0, s0, sc, sh);
+  // the lane's 4 channels x 9 taps are 36 contiguous floats of wt ([C][9], 16-B aligned
+  // since c % 4 == 0): 9 float4 loads instead of 36 scalar ones (every block reloads them)
+  float k9[9][4], bi[4];
+  float bmu[4] = {0.f, 0.f, 0.f, 0.f}, bsc[4] = {0.f, 0.f, 0.f, 0.f}, bsh[4] = {0.f, 0.f, 0.f, 0.f};
+  const int cc = tid < NA ? c : 0;
+  {
+    float wv[36];
+#pragma unroll
+    for (int e = 0; e < 9; ++e) {
+      const float4 w4 = ld4(wt + cc * 9 + 4 * e);
+      wv[4 * e] = w4.x; wv[4 * e + 1] = w4.y; wv[4 * e + 2] = w4.z; wv[4 * e + 3] = w4.w;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int tp = 0; tp < 9; ++tp) k9[tp][j] = wv[j * 9 + (flip ? 8 - tp : tp)];
+    const float4 b4 = bias ? ld4(bias + cc) : make_float4(0.f, 0.f, 0.f, 0.f);
+    bi[0] = b4.x; bi[1] = b4.y; bi[2] = b4.z; bi[3] = b4.w;
+    if (BNB) {
+      const float4 m4 = ld4(bst + BN_MEAN * g.C + cc), s4 = ld4(bst + BN_SCALE * g.C + cc),
+                   h4 = ld4(bst + BN_SHIFT * g.C + cc);
+      bmu[0] = m4.x; bmu[1] = m4.y; bmu[2] = m4.z; bmu[3] = m4.w;
+      bsc[0] = s4.x; bsc[1] = s4.y; bsc[2] = s4.z; bsc[3] = s4.w;
+      bsh[0] = h4.x; bsh[1] = h4.y; bsh[2] = h4.z; bsh[3] = h4.w;
+    }
+  }
+  fill.park(tile, g, pro, act);
+  __syncthreads();
+  double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+  if (tid < NA) {
+    float win[3][3][4];
+    auto rd = [&](int r, float (&row)[3][4]) {
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) {
+        const float4 a = tile[r * RW + (p + dx) * CQ + q];
+        row[dx][0] = a.x; row[dx][1] = a.y; row[dx][2] = a.z; row[dx][3] = a.w;
+      }
+    };
+    rd(0, win[0]);
+    rd(1, win[1]);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const bool on = lane_on && h0 + r < g.H;
+      rd(r + 2, win[2]);
+      float o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float acc = bi[j];
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+          for (int dx = 0; dx < 3; ++dx) acc = fmaf(k9[dy * 3 + dx][j], win[dy][dx][j], acc);
+        acc = rnd<T>(acc);  // statistics of the stored value
+        o[j] = acc;
+        const float am = on ? acc : 0.f;
+        if (BNB) {
+          const float zz = f4get(q2f(zr[r]), j);
+          float gg = am;
+          if (bact == ACT_LRELU) gg *= lrelu_d(zz * bsc[j] + bsh[j]);
+          s1[j] += gg;
+          s2[j] += (double)gg * ((double)zz - bmu[j]);
+        } else {
+          s1[j] += am;
+          s2[j] += (double)am * am;
+        }
+      }
+      bufq_st<2>(rz, on ? (unsigned)(((h0 + r) * L + s0 + tid) * QB) : ACC_OOB,
+                 make_float4(o[0], o[1], o[2], o[3]), (T*)nullptr);
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          win[0][dx][j] = win[1][dx][j];
+          win[1][dx][j] = win[2][dx][j];
+        }
+    }
+  }
+  if (stats) {
+    // per-channel sums over the span's PX pixels, in pixel order (deterministic)
+    __syncthreads();  // the tile is reused as the reduction buffer
+    double* red = reinterpret_cast<double*>(tile);
+    if (tid < NA) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        red[tid * 8 + j] = s1[j];
+        red[tid * 8 + 4 + j] = s2[j];
+      }
+    }
+    __syncthreads();
+    if (tid < CQ) {
+      double a[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+      for (int pp = 0; pp < PX; ++pp)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) a[e] += red[(pp * CQ + tid) * 8 + e];
+      const long row = (long)bid * 2 * g.C;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        stats[row + 4 * tid + j] = a[j];
+        stats[row + g.C + 4 * tid + j] = a[4 + j];
+      }
+    }
+  }
+}
+
+static int dw_span_on() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ACCUNET_DW_SPAN");  // tuning knob: 0 = the tile kernel
+    v = e ? atoi(e) : 1;
+  }
+  return v;
+}
+
+// span-kernel threads per block for C, or 0 when the span kernel does not apply
+static int dw_span_nt(int H, int W, int C) {
+  if (!dw_span_on() || C % 8) return 0;  // CQ even (bf16 fill units are quad pairs)
+  if ((long)H * W * C * 4 >= (1L << 31)) return 0;
+  const int CQ = C / 4;
+  return CQ <= 32 ? 256 : (CQ <= 64 ? 512 : 0);
+}
+
+static DwSGeom dw_sgeom(int B, int H, int W, int C, int nt, dim3* grid) {
+  DwSGeom g;
+  g.B = B; g.H = H; g.W = W; g.C = C;
+  g.CQ = C / 4;
+  g.PX = nt / g.CQ;
+  g.NS = ceil_div(W, g.PX);
+  g.tilesH = ceil_div(H, DWS_R);
+  static const char* rm = getenv("ACCUNET_DW_SPAN_REMAP");  // tuning knob
+  const long nb = (long)B * g.tilesH * g.NS;
+  g.remap = (rm && atoi(rm) && nb % 8 == 0) ? 1 : 0;
+  *grid = dim3((unsigned)nb);
+  return g;
+}
+
+
+// Weight + bias gradient in span geometry: dW[c][tap] = sum_p dz[p,c] * a[shift_tap(p), c],
+// db[c] = sum_p dz[p,c]. A block walks `nrt` consecutive R-row tiles of one span (fill,
+// then the R dz rows of its lanes, window sums in registers), then reduces its lanes'
+// 10 x 4 sums over the span's pixels (pixel order, deterministic) into partial row bid
+// of part[rows][10][C].
+template <int NT, int AUX, typename T>
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 ? 3 : 2)))
+dw3x3_span_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dz,
+                        const float* __restrict__ sc, const float* __restrict__ sh, int act,
+                        float* __restrict__ part, DwSGeom g, int nrt) {
+  typedef DwS<NT> G;
+  constexpr int R = G::R;
+  typedef typename QuadRaw<T>::type RawQ;
+  __shared__ float4 tile[G::TILE];
+  const int tid = threadIdx.x;
+  const int CQ = g.CQ, PX = g.PX;
+  const int RW = (PX + 2) * CQ, NA = PX * CQ;
+  const int bid = blockIdx.x;
+  const int sp = bid % g.NS;
+  int t = bid / g.NS;
+  const int tb = t % g.tilesH;  // tile band: row tiles tb*nrt .. tb*nrt + nrt - 1
+  const int b = t / g.tilesH;
+  const int w0 = sp * PX;
+  const int L = g.W * CQ;
+  const int s0 = w0 * CQ;
+  const long img = (long)b * g.H * g.W * g.C;
+  const unsigned ibytes = (unsigned)(g.H * g.W * g.C * (int)sizeof(T));
+  const __amdgpu_buffer_rsrc_t rx = acc_rsrc(x + img, ibytes);
+  const __amdgpu_buffer_rsrc_t rd_ = acc_rsrc(dz + img, ibytes);
+  constexpr unsigned QB = 4 * sizeof(T);
+  const int p = tid / CQ, q = tid - (tid / CQ) * CQ;
+  const bool lane_on = tid < NA && w0 + p < g.W;
+  const bool pro = sc != nullptr;
+  float acc[10][4];
+#pragma unroll
+  for (int i = 0; i < 10; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+  for (int it = 0; it < nrt; ++it) {
+    const int h0 = (tb * nrt + it) * R;
+    if (h0 >= g.H) break;  // block-uniform
+    {
+      DwsFill<NT, AUX, T> fill;
+      fill.issue(rx, g, h0, s0, sc, sh);
+      if (it > 0) __syncthreads();  // every lane is done with the previous tile
+      fill.park(tile, g, pro, act);
+    }
+    __builtin_amdgcn_sched_barrier(0);  // keep the dz loads behind the park (registers)
+    // this lane's dz rows, issued once the fill registers are free (in flight across
+    // the barrier)
+    RawQ dr[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const bool in = lane_on && h0 + r < g.H;
+      dr[r] = bufq_ld<0>(rd_, in ? (unsigned)(((h0 + r) * L + s0 + tid) * QB) : ACC_OOB,
+                         (const T*)nullptr);
+    }
+    __syncthreads();
+    if (tid < NA) {
+      float win[3][3][4];
+      auto rd = [&](int r, float (&row)[3][4]) {
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) {
+          const float4 a = tile[r * RW + (p + dx) * CQ + q];
+          row[dx][0] = a.x; row[dx][1] = a.y; row[dx][2] = a.z; row[dx][3] = a.w;
+        }
+      };
+      rd(0, win[0]);
+      rd(1, win[1]);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        rd(r + 2, win[2]);
+        const float4 d4 = q2f(dr[r]);  // zero outside the image (descriptor range)
+        const float dv[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+#pragma unroll
+          for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx)
+              acc[dy * 3 + dx][j] = fmaf(dv[j], win[dy][dx][j], acc[dy * 3 + dx][j]);
+          acc[9][j] += dv[j];
+        }
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            win[0][dx][j] = win[1][dx][j];
+            win[1][dx][j] = win[2][dx][j];
+          }
+      }
+    }
+  }
+  // lanes' sums -> per-channel partials: one thread per (tap i, quad qq) adds the span's
+  // pixels in order
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(tile);  // [NA][10][4]
+  if (tid < NA) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i)
+      *reinterpret_cast<float4*>(red + (tid * 10 + i) * 4) =
+          make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
+  }
+  __syncthreads();
+  for (int e = tid; e < 10 * CQ; e += NT) {
+    const int i = e / CQ, qq = e - (e / CQ) * CQ;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int pp = 0; pp < PX; ++pp) {
+      const float4 v = *reinterpret_cast<const float4*>(red + ((pp * CQ + qq) * 10 + i) * 4);
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+    st4(part + ((long)bid * 10 + i) * g.C + 4 * qq, a);
+  }
+}
+
+// span wgrad geometry: row-tile bands of nrt tiles (fewer partial rows)
+#define DWS_WG_NRT 4
+static DwSGeom dw_sgeom_wgrad(int B, int H, int W, int C, int nt, dim3* grid) {
+  DwSGeom g = dw_sgeom(B, H, W, C, nt, grid);
+  g.remap = 0;
+  g.tilesH = ceil_div(ceil_div(H, DWS_R), DWS_WG_NRT);  // bands
+  *grid = dim3((unsigned)((long)B * g.tilesH * g.NS));
+  return g;
+}
+
 // tile-kernel selection: 0 = none (register-window kernel), else TCQ
 static int dw_tile_tcq(int H, int W, int C) {
   if (C % 32) return 0;
@@ -807,8 +1223,20 @@ static DwGeom dw_geom(int B, int H, int W, int C, int V, dim3* grid) {
   return g;
 }
 
+// which forward kernel accunet_dw3x3_fwd runs for this shape: 2 = span, 1 = tile,
+// 0 = register window (profiling names / the bench probe)
+extern "C" int accunet_dw3x3_variant(int B, int H, int W, int C) {
+  (void)B;
+  if (dw_span_nt(H, W, C)) return 2;
+  return dw_tile_tcq(H, W, C) ? 1 : 0;
+}
+
 extern "C" int accunet_dw3x3_rows(int B, int H, int W, int C) {
   dim3 grid;
+  if (const int nt = dw_span_nt(H, W, C)) {
+    dw_sgeom(B, H, W, C, nt, &grid);
+    return (int)grid.x;
+  }
   int tcq = dw_tile_tcq(H, W, C);
   if (tcq) dw_tgeom(B, H, W, C, tcq, &grid, dw_rch_max());
   else dw_geom(B, H, W, C, (C % 4 == 0) ? 4 : 1, &grid);
@@ -822,6 +1250,38 @@ extern "C" int accunet_dw3x3_fwd(const void* x, const float* wt, const float* bi
   hipStream_t s = (hipStream_t)stream;
   if (bz && (!bst || !stats)) return ACC_EBADARG;
   dim3 grid;
+  if (const int nt = dw_span_nt(H, W, C)) {
+    const DwSGeom sg = dw_sgeom(B, H, W, C, nt, &grid);
+    // non-temporal input loads above the Infinity Cache (bytes as stored)
+    const bool ntl = dw_ntl((long)B * H * W * C * (dt == ACC_BF16 ? 2 : 4)) != 0;
+    auto launch = [&](auto tag, auto ntc, auto bnbc, auto auxc) {
+      using T = decltype(tag);
+      hipLaunchKernelGGL((dw3x3_span_fwd_kernel<decltype(ntc)::value, decltype(bnbc)::value,
+                                                decltype(auxc)::value, T>),
+                         grid, dim3(decltype(ntc)::value), 0, s, (const T*)x, wt, bias, sc, sh, act,
+                         flip, (T*)z, stats, sg, (const T*)bz, bst, bact);
+    };
+    using N256 = std::integral_constant<int, 256>;
+    using N512 = std::integral_constant<int, 512>;
+    using BT = std::integral_constant<bool, true>;
+    using BF = std::integral_constant<bool, false>;
+    using A2 = std::integral_constant<int, 2>;
+    using A0 = std::integral_constant<int, 0>;
+    if (with_dt(dt, [&](auto tag) {
+          auto by_aux = [&](auto n, auto bn) {
+            if (ntl) launch(tag, n, bn, A2{});
+            else launch(tag, n, bn, A0{});
+          };
+          auto by_bnb = [&](auto n) {
+            if (bz) by_aux(n, BT{});
+            else by_aux(n, BF{});
+          };
+          if (nt == 256) by_bnb(N256{});
+          else by_bnb(N512{});
+        }))
+      return ACC_EBADARG;
+    return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+  }
   int tcq = dw_tile_tcq(H, W, C);
   if (tcq) {
     DwTGeom tg = dw_tgeom(B, H, W, C, tcq, &grid, dw_rch_max());
@@ -881,6 +1341,10 @@ extern "C" int accunet_dw3x3_fwd(const void* x, const float* wt, const float* bi
 
 static int dw_wgrad_rows(int B, int H, int W, int C) {
   dim3 grid;
+  if (const int nt = dw_span_nt(H, W, C)) {
+    dw_sgeom_wgrad(B, H, W, C, nt, &grid);
+    return (int)grid.x;
+  }
   int tcq = dw_tile_tcq(H, W, C);
   if (tcq) dw_tgeom(B, H, W, C, tcq, &grid);
   else dw_geom(B, H, W, C, (C % 4 == 0) ? 4 : 1, &grid);
@@ -910,7 +1374,24 @@ extern "C" int accunet_dw3x3_wgrad(const void* x, const void* dz, const float* s
   float* part = ws;
   float* scratch = ws + (size_t)R * 10 * C;
   float* sums = scratch + accunet_partials_ws_elems(R, 10 * C);
-  if (with_dt(dt, [&](auto tag) {
+  if (const int nt = dw_span_nt(H, W, C)) {
+    dim3 sgrid;
+    const DwSGeom sg = dw_sgeom_wgrad(B, H, W, C, nt, &sgrid);
+    R = (int)sgrid.x;
+    if (ws_elems < dw_wgrad_ws(B, H, W, C)) return ACC_EBADARG;
+    part = ws;
+    scratch = ws + (size_t)R * 10 * C;
+    if (with_dt(dt, [&](auto tag) {
+          using T = decltype(tag);
+          if (nt == 256)
+            hipLaunchKernelGGL((dw3x3_span_wgrad_kernel<256, 0, T>), sgrid, dim3(256), 0, s,
+                               (const T*)x, (const T*)dz, sc, sh, act, part, sg, DWS_WG_NRT);
+          else
+            hipLaunchKernelGGL((dw3x3_span_wgrad_kernel<512, 0, T>), sgrid, dim3(512), 0, s,
+                               (const T*)x, (const T*)dz, sc, sh, act, part, sg, DWS_WG_NRT);
+        }))
+      return ACC_EBADARG;
+  } else if (with_dt(dt, [&](auto tag) {
         using T = decltype(tag);
         const T* xx = (const T*)x;
         const T* dd = (const T*)dz;

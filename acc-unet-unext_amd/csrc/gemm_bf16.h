@@ -73,8 +73,10 @@ gemm_bf16_kernel(const GemmParams p) {
   const int l31 = lane & 31;
   const int lh = lane >> 5;
 
-  const int m0 = blockIdx.x * BM;
-  const int n0 = blockIdx.y * BN;
+  int mt, nt;
+  gemm_tile(mt, nt);
+  const int m0 = mt * BM;
+  const int n0 = nt * BN;
   const int M = p.M, N = p.N, K = p.K;
 
   int kstart = 0, kend = K;

@@ -89,6 +89,26 @@ constexpr int gemm_epi_floats() {
   return WM * 32 * ((4 / WM) * TN * 32 + 4);
 }
 
+// Output tile (mt, nt) of this workgroup. Split-K grids and single-column grids keep
+// (blockIdx.x, blockIdx.y). Otherwise tiles run N-fastest: the N tiles of one M row
+// panel are consecutive, so they share that panel of A (the pixel-sized operand; B is
+// a weight panel) while it is hot. Workgroups are dealt round-robin to the 8 XCDs, so
+// when the tile count is a multiple of 8 each XCD takes a contiguous run of tiles and
+// an A panel is fetched into one XCD's L2 once, not once per N tile.
+ACC_DEV void gemm_tile(int& mt, int& nt) {
+  const int gy = gridDim.y;
+  if (gridDim.z > 1 || gy == 1) {
+    mt = blockIdx.x;
+    nt = blockIdx.y;
+    return;
+  }
+  const int T = gridDim.x * gy;
+  int bid = blockIdx.x + gridDim.x * blockIdx.y;  // dispatch order
+  if ((T & 7) == 0) bid = (bid & 7) * (T >> 3) + (bid >> 3);
+  nt = bid % gy;
+  mt = bid / gy;
+}
+
 // The epilogue shared by both engines. acc[i][j] holds this wave's 32x32 tile (i, j)
 // in the MFMA C/D layout (row = (r&3) + 8*(r>>2) + 4*(lane>>5), col = lane&31; the
 // same for v_mfma_f32_32x32x2_f32 and v_mfma_f32_32x32x16_bf16). smem: >=
@@ -349,8 +369,8 @@ ACC_DEV void gemm_epilogue_generic(const GemmParams& p, floatx16 (&acc)[TM][TN],
       for (int e = 0; e < 4; ++e) {
         const int n = n0 + 4 * tid + e;
         if (n < N) {
-          p.stats[((size_t)blockIdx.x * 2 + 0) * N + n] = vv[e];
-          p.stats[((size_t)blockIdx.x * 2 + 1) * N + n] = vv[4 + e];
+          p.stats[((size_t)(m0 / (WM * TM * 32)) * 2 + 0) * N + n] = vv[e];
+          p.stats[((size_t)(m0 / (WM * TM * 32)) * 2 + 1) * N + n] = vv[4 + e];
         }
       }
     }
@@ -593,8 +613,8 @@ ACC_DEV void gemm_epilogue_vec(const GemmParams& p, floatx16 (&acc)[TM][TN], flo
       for (int e = 0; e < 4; ++e) {
         const int n = n0 + 4 * tid + e;
         if (n < N) {
-          p.stats[((size_t)blockIdx.x * 2 + 0) * N + n] = vv[e];
-          p.stats[((size_t)blockIdx.x * 2 + 1) * N + n] = vv[4 + e];
+          p.stats[((size_t)(m0 / (WM * TM * 32)) * 2 + 0) * N + n] = vv[e];
+          p.stats[((size_t)(m0 / (WM * TM * 32)) * 2 + 1) * N + n] = vv[4 + e];
         }
       }
     }

@@ -3,8 +3,8 @@
 // register-staged kernel runs at about half MFMA occupancy.
 //
 //   * operand tiles go global -> LDS by global_load_lds_dwordx4 (no VGPR staging,
-//     no transposing ds_writes), into a 3-stage ring: tile kt+2 is in flight while
-//     tile kt is computed; each wave waits for its own DMA of tile kt with a counted
+//     no transposing ds_writes), into a GG_STAGES-deep ring: tiles kt+1 .. kt+3 are in
+//     flight while tile kt is computed; each wave waits for its own DMA of tile kt with a counted
 //     s_waitcnt vmcnt(N) and one raw s_barrier per k-tile publishes it (no
 //     __syncthreads in the loop: its implied vmcnt(0) would drain the ring);
 //   * LDS image = the global tile, lane-linear per DMA instruction, [row][16 k] with
@@ -23,7 +23,12 @@
 #include "gemm_common.h"
 
 #define GG_BK 16
-#define GG_STAGES 3
+// ring depth: GG_STAGES - 1 k-tiles (16 k each) in flight ahead of the one computed.
+// A k-tile of a 128x128 tile is ~2k cycles of MFMA work, so 3 tiles ahead cover an HBM
+// round trip under load; 4 stages of 16.5 KB keep 2 workgroups per CU in LDS.
+#ifndef GG_STAGES
+#define GG_STAGES 4
+#endif
 
 static __device__ __attribute__((aligned(16))) float g_gemm_zero16[4];
 
@@ -78,6 +83,8 @@ gemm_f32g_kernel(const GemmParams p) {
   constexpr int IA = (PWA + 63) / 64, IB = (PWB + 63) / 64, IC = CF ? 1 : 0;
   constexpr int GPW = IA + IB + IC;  // DMA instructions per wave and stage
   static_assert(BK == 16, "the chunk swizzle assumes 4 chunks per row");
+  static_assert(GG_STAGES >= 2 && GG_STAGES <= 4, "the vmcnt ladder covers up to 3 tiles ahead");
+  static_assert(3 * GPW < 64, "vmcnt range");
   static_assert(PWA % 64 == 0 || PWA < 64, "A pieces per wave");
   static_assert(PWB % 64 == 0 || PWB < 64, "B pieces per wave");
   static_assert(PRO_A == PRO_NONE || AMODE == AM_ROW, "A prologue: row-major A only");
@@ -93,8 +100,10 @@ gemm_f32g_kernel(const GemmParams p) {
   const int l31 = lane & 31;
   const int lh = lane >> 5;
 
-  const int m0 = blockIdx.x * BM;
-  const int n0 = blockIdx.y * BN;
+  int mt, nt;
+  gemm_tile(mt, nt);
+  const int m0 = mt * BM;
+  const int n0 = nt * BN;
   const int M = p.M, N = p.N, K = p.K;
   int kstart = 0, kend = K;
   if (gridDim.z > 1) {
@@ -289,17 +298,23 @@ gemm_f32g_kernel(const GemmParams p) {
     }
   };
 
+  constexpr int D = GG_STAGES - 1;  // k-tiles in flight ahead of the computed one
   if (nkt > 0) {
-    stage(0, 0);
-    if (nkt > 1) stage(1, 1);
+#pragma unroll
+    for (int s = 0; s < D; ++s)
+      if (s < nkt) stage(s, s);
     for (int kt = 0; kt < nkt; ++kt) {
-      // this wave's DMA of tile kt has landed (tile kt+1's may still be in flight) ...
-      if (kt + 1 < nkt) gg_wait_vm<GPW>();
+      // this wave's DMA of tile kt has landed (the up to D-1 later tiles may still be
+      // in flight: their GPW instructions each are the newest in the counter) ...
+      const int ahead = min(D - 1, nkt - 1 - kt);
+      if (ahead >= 3) gg_wait_vm<3 * GPW>();
+      else if (ahead == 2) gg_wait_vm<2 * GPW>();
+      else if (ahead == 1) gg_wait_vm<GPW>();
       else gg_wait_vm<0>();
       // ... and so has every wave's once all pass the barrier; the barrier also
-      // retires every read of the buffer that tile kt+2 overwrites (computed at kt-1)
+      // retires every read of the buffer that tile kt+D overwrites (computed at kt-1)
       __builtin_amdgcn_s_barrier();
-      if (kt + 2 < nkt) stage(kt + 2, (kt + 2) % GG_STAGES);
+      if (kt + D < nkt) stage(kt + D, (kt + D) % GG_STAGES);
       compute(kt, kt % GG_STAGES);
     }
   }

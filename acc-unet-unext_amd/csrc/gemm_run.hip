@@ -5,43 +5,56 @@
 #include <string.h>
 #include <stdlib.h>
 
-// One block = 64 consecutive outputs x 16 slab groups (1024 threads): thread
-// (c, g) sums slabs g, g+16, ... in order, then the 16 group sums are added in
-// fixed order -> deterministic, and S-way parallel enough that a 32x32 weight
-// gradient split 1024 ways does not serialise on one thread per output.
-#define SPLITK_COLS 64
-#define SPLITK_GROUPS 16
+// One block = COLS consecutive outputs x (1024 / COLS) slab groups: thread (c, g) sums
+// slabs g, g + G, ... in order, then the G group sums are added in fixed order ->
+// deterministic. Deep splits (a 32x288 weight gradient over 1M pixels splits ~340
+// ways) take 16 columns x 64 groups, so no thread walks more than a few slabs
+// (the reduction is latency-bound: each thread's slab reads are a dependent chain).
+template <int COLS>
 __global__ void __launch_bounds__(1024)
 splitk_reduce_kernel(const float* __restrict__ ws, float* __restrict__ C, int M, int N, int ldc,
                      int S, size_t zstride) {
-  __shared__ float part[SPLITK_GROUPS][SPLITK_COLS];
-  const int c = threadIdx.x & (SPLITK_COLS - 1), g = threadIdx.x / SPLITK_COLS;
+  constexpr int G = 1024 / COLS;
+  __shared__ float part[G][COLS];
+  const int c = threadIdx.x % COLS, g = threadIdx.x / COLS;
   const long total = (long)M * N;
-  const long i = (long)blockIdx.x * SPLITK_COLS + c;
+  const long i = (long)blockIdx.x * COLS + c;
   float acc = 0.f;
   if (i < total) {
     const float* src = ws + i;
     int z = g;
-    for (; z + 3 * SPLITK_GROUPS < S; z += 4 * SPLITK_GROUPS) {
+    for (; z + 3 * G < S; z += 4 * G) {
       float a0 = src[(size_t)z * zstride];
-      float a1 = src[(size_t)(z + SPLITK_GROUPS) * zstride];
-      float a2 = src[(size_t)(z + 2 * SPLITK_GROUPS) * zstride];
-      float a3 = src[(size_t)(z + 3 * SPLITK_GROUPS) * zstride];
+      float a1 = src[(size_t)(z + G) * zstride];
+      float a2 = src[(size_t)(z + 2 * G) * zstride];
+      float a3 = src[(size_t)(z + 3 * G) * zstride];
       acc += a0;
       acc += a1;
       acc += a2;
       acc += a3;
     }
-    for (; z < S; z += SPLITK_GROUPS) acc += src[(size_t)z * zstride];
+    for (; z < S; z += G) acc += src[(size_t)z * zstride];
   }
   part[g][c] = acc;
   __syncthreads();
   if (g == 0 && i < total) {
     float s = part[0][c];
-#pragma unroll
-    for (int k = 1; k < SPLITK_GROUPS; ++k) s += part[k][c];
+#pragma unroll 8
+    for (int k = 1; k < G; ++k) s += part[k][c];
     int m = (int)(i / N), n = (int)(i - (long)m * N);
     C[(size_t)m * ldc + n] = s;
+  }
+}
+
+static void splitk_reduce(const float* ws, float* C, int M, int N, int ldc, int S, size_t zstride,
+                          hipStream_t stream) {
+  const long total = (long)M * N;
+  if (S > 64) {
+    hipLaunchKernelGGL(splitk_reduce_kernel<16>, dim3((unsigned)((total + 15) / 16)), dim3(1024), 0,
+                       stream, ws, C, M, N, ldc, S, zstride);
+  } else {
+    hipLaunchKernelGGL(splitk_reduce_kernel<64>, dim3((unsigned)((total + 63) / 64)), dim3(1024), 0,
+                       stream, ws, C, M, N, ldc, S, zstride);
   }
 }
 
@@ -209,10 +222,7 @@ int gemm_run(GemmParams p, int amode, int bmode, int pro_a, int pro_b, bool allo
   if (allow_split && cdt == ACC_F32 && adt == bdt) {
     const int S = gemm_skinny_try(p, amode, bmode, pro_a, pro_b, ws, ws_elems, adt, stream);
     if (S > 0) {
-      const long total = (long)p.M * p.N;
-      hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((total + SPLITK_COLS - 1) / SPLITK_COLS)),
-                         dim3(SPLITK_COLS * SPLITK_GROUPS), 0, stream, ws, (float*)p.C, p.M, p.N, p.ldc, S,
-                         (size_t)total);
+      splitk_reduce(ws, (float*)p.C, p.M, p.N, p.ldc, S, (size_t)p.M * p.N, stream);
       return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
     }
   }
@@ -264,18 +274,17 @@ int gemm_run(GemmParams p, int amode, int bmode, int pro_a, int pro_b, bool allo
   gemm_kfn kfn = tab[t];
   // (weight gradients, AM_COL: both operands k-major, 4 ds_read_b32 per fragment and
   // k-chunk; the register-staged kernel is as fast or faster there, tools/gg_ab.sh)
-  if (vec && adt == ACC_F32 && amode != AM_COL) {
+  static int gwg = -1;
+  if (gwg < 0) {
+    const char* e = getenv("ACCUNET_GEMM_G_WGRAD");  // tuning knob: weight gradients on the DMA engine
+    gwg = e ? atoi(e) : 0;
+  }
+  if (vec && adt == ACC_F32 && (amode != AM_COL || gwg)) {
     gemm_kfn g = ggemm_for(amode, bmode, pro_a, pro_b, epi, t);
     if (g) kfn = g;
   }
   hipLaunchKernelGGL(kfn, grid, dim3(GEMM_THREADS), 0, stream, p);
-  if (S > 1) {
-    long total = (long)p.M * p.N;
-    long blocks = (total + SPLITK_COLS - 1) / SPLITK_COLS;
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)blocks), dim3(SPLITK_COLS * SPLITK_GROUPS),
-                       0, stream, ws, Cfinal, p.M,
-                       p.N, ldc_final, S, p.zstride);
-  }
+  if (S > 1) splitk_reduce(ws, Cfinal, p.M, p.N, ldc_final, S, p.zstride, stream);
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 

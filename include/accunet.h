@@ -154,6 +154,9 @@ int accunet_reduce_stats(const double* part, int R, int C, double* out2C, double
  * g = out * act'(bz*scale + shift), for accunet_bn_bwd_part. wgrad writes dW [C][1][3][3] and db [C].
  * ------------------------------------------------------------------------- */
 int accunet_dw3x3_rows(int B, int H, int W, int C);
+/* Which forward kernel runs for the shape: 2 = whole-pixel span kernel (C % 8 == 0,
+ * C <= 256), 1 = LDS tile kernel (other C % 32 == 0), 0 = register-window kernel. */
+int accunet_dw3x3_variant(int B, int H, int W, int C);
 int accunet_dw3x3_fwd(const void* x, const float* wt, const float* bias, const float* sc,
                       const float* sh, int act, int flip, void* z, double* stats, int B, int H,
                       int W, int C, const void* bz, const float* bst, int bact, int dt,

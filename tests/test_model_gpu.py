@@ -328,8 +328,8 @@ def test_side_stream_weight_gradients_bit_identical(graph, precision):
 def test_selective_fork_bit_identical(graph):
     """ACCUNET_WGRAD_FORK_MIN_US > 0 (ops.set_wgrad_fork_min_us): some layers' weight
     gradients run on the side stream and the others on the main stream in the same
-    backward. Two training steps at cuts 0 (fork every layer), 30 us (a mix at this
-    size: the estimate spans ~1-100 us) and 1e9 (never fork): identical losses,
+    backward. Two training steps at cuts 0 (fork every layer), the median of the
+    estimates the first run logged (a mix) and 1e9 (never fork): identical losses,
     parameters and BatchNorm state bit for bit."""
     from accunet import ops
     from accunet.train import TrainStep
@@ -341,20 +341,26 @@ def test_selective_fork_bit_identical(graph):
     prev_s = ops.set_wgrad_stream(True)
     prev_c = ops.set_wgrad_fork_min_us(0.0)
     try:
-        for cut in (0.0, 30.0, 1e9):
+        ops.FORK_LOG = []
+        cuts = [0.0, None, 1e9]
+        for i, cut in enumerate(cuts):
+            if cut is None:  # the median estimate of the first run splits the layers
+                est = sorted(ops.FORK_LOG)
+                cut = cuts[i] = est[len(est) // 2] + 1e-9
             ops.set_wgrad_fork_min_us(cut)
             m = _hip_model("canonical", sd, nf).train()
             step = TrainStep(m, lr=1e-3, graph=graph)
             c0 = list(ops.FORK_COUNTS)
             losses = [float(step(x, mask).item()) for _ in range(2)]
             kept, forked = (ops.FORK_COUNTS[0] - c0[0], ops.FORK_COUNTS[1] - c0[1])
-            if cut == 30.0:  # the mixed configuration really mixes
-                assert kept > 0 and forked > 0, (kept, forked)
+            if i == 1:  # the mixed configuration really mixes
+                assert kept > 0 and forked > 0, (cut, kept, forked)
             runs[cut] = (losses, {k: v.detach().clone() for k, v in m.state_dict().items()})
     finally:
+        ops.FORK_LOG = None
         ops.set_wgrad_stream(prev_s)
         ops.set_wgrad_fork_min_us(prev_c)
-    for cut in (30.0, 1e9):
+    for cut in cuts[1:]:
         assert runs[0.0][0] == runs[cut][0], (cut, runs[0.0][0], runs[cut][0])
         for k, v in runs[0.0][1].items():
             assert torch.equal(v, runs[cut][1][k]), (cut, k)

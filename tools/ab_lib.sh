@@ -1,11 +1,11 @@
 #!/bin/bash
-# Same-box A/B: current tree vs the library in $1 (default _exp/head, tools/build_alt.sh),
+# Same-box A/B: current tree vs the library in $1 (default _ab/head, tools/build_alt.sh),
 # bench.py --dtype $DT (default bf16) with the roofline probes, alternating, twice each.
 set -e -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-ALT=${1:-_exp/head}
+ALT=${1:-_ab/head}
 if [ -n "${PYTEST_K:-}" ]; then
   timeout -k 10 600 python -u -m pytest tests -q -m gpu --timeout 240 --timeout-method thread -k "$PYTEST_K" > gpurun_out/ab_tests.log 2>&1 || { tail -30 gpurun_out/ab_tests.log; exit 1; }
   tail -1 gpurun_out/ab_tests.log
