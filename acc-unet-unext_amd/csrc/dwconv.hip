@@ -730,11 +730,19 @@ dw3x3_tile_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dz,
 struct DwSGeom {
   int B, H, W, C;
   int CQ, PX;      // quads per pixel, output pixels per span (NT / CQ)
-  int NS, tilesH;  // spans per image row, row tiles per image
+  int NS, tilesH;  // spans per image row, row bands (of nrt R-row tiles) per image
+  int nrt;         // R-row tiles per block, walked in order
   int remap;       // XCD-contiguous block order (tuning knob ACCUNET_DW_SPAN_REMAP)
 };
 
 #define DWS_R 8  // output rows per span block
+
+// workgroup barrier for LDS reuse only: drains this wave's LDS operations
+// (lgkmcnt(0)), leaves its global loads / stores in flight (no fence)
+ACC_DEV void lds_barrier() {
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // gfx9: vmcnt 63, expcnt 7, lgkmcnt 0
+  __builtin_amdgcn_s_barrier();
+}
 
 template <int NT>
 struct DwS {
@@ -819,7 +827,7 @@ struct DwsFill {
 };
 
 template <int NT, bool BNB, int AUX, typename T>
-__global__ void __launch_bounds__(NT)
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(BNB ? 2 : 3)))
 dw3x3_span_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
                       const float* __restrict__ bias, const float* __restrict__ sc,
                       const float* __restrict__ sh, int act, int flip, T* __restrict__ z,
@@ -839,9 +847,9 @@ dw3x3_span_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
   }
   const int sp = bid % g.NS;
   int t = bid / g.NS;
-  const int th = t % g.tilesH;
+  const int tb = t % g.tilesH;  // row band: tiles tb*nrt .. tb*nrt + nrt - 1 of R rows
   const int b = t / g.tilesH;
-  const int h0 = th * R, w0 = sp * PX;
+  const int w0 = sp * PX;
   const int L = g.W * CQ;  // quads per image row
   const int s0 = w0 * CQ;  // first output quad of the span in its row
   const long img = (long)b * g.H * g.W * g.C;
@@ -856,21 +864,9 @@ dw3x3_span_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
   const bool lane_on = tid < NA && w0 + p < g.W;
   const int c = 4 * q;
 
-  // BNB: this lane's R rows of bz, in flight with the tile fill
-  RawQ zr[R];
-  if (BNB) {
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const bool in = lane_on && h0 + r < g.H;
-      zr[r] = bufq_ld<0>(rb, in ? (unsigned)(((h0 + r) * L + s0 + tid) * QB) : ACC_OOB,
-                         (const T*)nullptr);
-    }
-  }
-  DwsFill<NT, AUX, T> fill;
   const bool pro = sc != nullptr;
-  fill.issue(rx, g, h0, s0, sc, sh);
   // the lane's 4 channels x 9 taps are 36 contiguous floats of wt ([C][9], 16-B aligned
-  // since c % 4 == 0): 9 float4 loads instead of 36 scalar ones (every block reloads them)
+  // since c % 4 == 0): 9 float4 loads instead of 36 scalar ones
   float k9[9][4], bi[4];
   float bmu[4] = {0.f, 0.f, 0.f, 0.f}, bsc[4] = {0.f, 0.f, 0.f, 0.f}, bsh[4] = {0.f, 0.f, 0.f, 0.f};
   const int cc = tid < NA ? c : 0;
@@ -895,74 +891,99 @@ dw3x3_span_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
       bsh[0] = h4.x; bsh[1] = h4.y; bsh[2] = h4.z; bsh[3] = h4.w;
     }
   }
-  fill.park(tile, g, pro, act);
-  __syncthreads();
   double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
-  if (tid < NA) {
-    float win[3][3][4];
-    auto rd = [&](int r, float (&row)[3][4]) {
+  for (int it = 0; it < g.nrt; ++it) {
+    const int h0 = (tb * g.nrt + it) * R;
+    if (h0 >= g.H) break;  // block-uniform
+    // BNB: this lane's R rows of bz, in flight with the tile fill
+    RawQ zr[R];
+    if (BNB) {
 #pragma unroll
-      for (int dx = 0; dx < 3; ++dx) {
-        const float4 a = tile[r * RW + (p + dx) * CQ + q];
-        row[dx][0] = a.x; row[dx][1] = a.y; row[dx][2] = a.z; row[dx][3] = a.w;
+      for (int r = 0; r < R; ++r) {
+        const bool in = lane_on && h0 + r < g.H;
+        zr[r] = bufq_ld<0>(rb, in ? (unsigned)(((h0 + r) * L + s0 + tid) * QB) : ACC_OOB,
+                           (const T*)nullptr);
       }
-    };
-    rd(0, win[0]);
-    rd(1, win[1]);
+    }
+    {
+      DwsFill<NT, AUX, T> fill;
+      fill.issue(rx, g, h0, s0, sc, sh);
+      if (it > 0) lds_barrier();  // every lane is done with the previous tile
+      fill.park(tile, g, pro, act);
+    }
+    lds_barrier();
+    if (tid < NA) {
+      // (the lane's tile base laundered per tile: the 30 window addresses are then
+      // recomputed per tile instead of hoisted out of the tile loop into registers)
+      int base = p * CQ + q;
+      asm volatile("" : "+v"(base));
+      float win[3][3][4];
+      auto rd = [&](int r, float (&row)[3][4]) {
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const bool on = lane_on && h0 + r < g.H;
-      rd(r + 2, win[2]);
-      float o[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float acc = bi[j];
-#pragma unroll
-        for (int dy = 0; dy < 3; ++dy)
-#pragma unroll
-          for (int dx = 0; dx < 3; ++dx) acc = fmaf(k9[dy * 3 + dx][j], win[dy][dx][j], acc);
-        acc = rnd<T>(acc);  // statistics of the stored value
-        o[j] = acc;
-        const float am = on ? acc : 0.f;
-        if (BNB) {
-          const float zz = f4get(q2f(zr[r]), j);
-          float gg = am;
-          if (bact == ACT_LRELU) gg *= lrelu_d(zz * bsc[j] + bsh[j]);
-          s1[j] += gg;
-          s2[j] += (double)gg * ((double)zz - bmu[j]);
-        } else {
-          s1[j] += am;
-          s2[j] += (double)am * am;
+        for (int dx = 0; dx < 3; ++dx) {
+          const float4 a = tile[r * RW + base + dx * CQ];
+          row[dx][0] = a.x; row[dx][1] = a.y; row[dx][2] = a.z; row[dx][3] = a.w;
         }
-      }
-      bufq_st<2>(rz, on ? (unsigned)(((h0 + r) * L + s0 + tid) * QB) : ACC_OOB,
-                 make_float4(o[0], o[1], o[2], o[3]), (T*)nullptr);
+      };
+      rd(0, win[0]);
+      rd(1, win[1]);
 #pragma unroll
-      for (int dx = 0; dx < 3; ++dx)
+      for (int r = 0; r < R; ++r) {
+        const bool on = lane_on && h0 + r < g.H;
+        rd(r + 2, win[2]);
+        float o[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          win[0][dx][j] = win[1][dx][j];
-          win[1][dx][j] = win[2][dx][j];
+          float acc = bi[j];
+#pragma unroll
+          for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx) acc = fmaf(k9[dy * 3 + dx][j], win[dy][dx][j], acc);
+          acc = rnd<T>(acc);  // statistics of the stored value
+          o[j] = acc;
+          const float am = on ? acc : 0.f;
+          if (BNB) {
+            const float zz = f4get(q2f(zr[r]), j);
+            float gg = am;
+            if (bact == ACT_LRELU) gg *= lrelu_d(zz * bsc[j] + bsh[j]);
+            s1[j] += gg;
+            s2[j] += (double)gg * ((double)zz - bmu[j]);
+          } else {
+            s1[j] += am;
+            s2[j] += (double)am * am;
+          }
         }
+        bufq_st<2>(rz, on ? (unsigned)(((h0 + r) * L + s0 + tid) * QB) : ACC_OOB,
+                   make_float4(o[0], o[1], o[2], o[3]), (T*)nullptr);
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            win[0][dx][j] = win[1][dx][j];
+            win[1][dx][j] = win[2][dx][j];
+          }
+      }
     }
   }
   if (stats) {
-    // per-channel sums over the span's PX pixels, in pixel order (deterministic)
-    __syncthreads();  // the tile is reused as the reduction buffer
-    double* red = reinterpret_cast<double*>(tile);
+    // per-channel sums over the span's PX pixels, in pixel order (deterministic). LDS-only
+    // barriers: __syncthreads' release fence would make every wave wait for its z stores
+    // to complete (vmcnt(0)) before the reduction, once per 8-row block
+    lds_barrier();  // the tile is reused as the reduction buffer
+    double* red = reinterpret_cast<double*>(tile);  // [8][NA]: lane-contiguous, no conflicts
     if (tid < NA) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        red[tid * 8 + j] = s1[j];
-        red[tid * 8 + 4 + j] = s2[j];
+        red[j * NA + tid] = s1[j];
+        red[(4 + j) * NA + tid] = s2[j];
       }
     }
-    __syncthreads();
+    lds_barrier();
     if (tid < CQ) {
       double a[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
       for (int pp = 0; pp < PX; ++pp)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) a[e] += red[(pp * CQ + tid) * 8 + e];
+        for (int e = 0; e < 8; ++e) a[e] += red[e * NA + pp * CQ + tid];
       const long row = (long)bid * 2 * g.C;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -973,20 +994,29 @@ dw3x3_span_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
   }
 }
 
+// ACCUNET_DW_SPAN (tuning knob): which depthwise passes run the span kernels.
+// bit 0: weight gradient (default on: 16x256x256x96 fp32 169-171 us against the tile
+// kernel's 180 us), bit 1: forward / data gradient (default off: with the statistics
+// epilogue 178-198 us against 161 us; its halo tile re-reads neighbours' pixels from
+// other XCDs, tools/k1lab span_lds 65-68 % vs tile_lds 70 %)
 static int dw_span_on() {
   static int v = -1;
   if (v < 0) {
-    const char* e = getenv("ACCUNET_DW_SPAN");  // tuning knob: 0 = the tile kernel
+    const char* e = getenv("ACCUNET_DW_SPAN");
     v = e ? atoi(e) : 1;
   }
   return v;
 }
 
-// span-kernel threads per block for C, or 0 when the span kernel does not apply
-static int dw_span_nt(int H, int W, int C) {
-  if (!dw_span_on() || C % 8) return 0;  // CQ even (bf16 fill units are quad pairs)
+// span-kernel threads per block for C, or 0 when the span kernel does not apply to
+// pass `bit` (1 = weight gradient, 2 = forward)
+static int dw_span_nt(int H, int W, int C, int bit = 2) {
+  if (!(dw_span_on() & bit) || C % 8) return 0;  // CQ even (bf16 fill units are quad pairs)
   if ((long)H * W * C * 4 >= (1L << 31)) return 0;
   const int CQ = C / 4;
+  // (512-thread blocks, CQ 33..64, hold 102 KB of LDS, one block per CU: in the model
+  // the tile kernel is as fast there, so they run only for the forward knob)
+  if (bit == 1) return CQ <= 32 ? 256 : 0;
   return CQ <= 32 ? 256 : (CQ <= 64 ? 512 : 0);
 }
 
@@ -996,7 +1026,9 @@ static DwSGeom dw_sgeom(int B, int H, int W, int C, int nt, dim3* grid) {
   g.CQ = C / 4;
   g.PX = nt / g.CQ;
   g.NS = ceil_div(W, g.PX);
-  g.tilesH = ceil_div(H, DWS_R);
+  static const char* nr = getenv("ACCUNET_DW_SPAN_NRT");  // tuning knob: tiles per block
+  g.nrt = nr && atoi(nr) > 0 ? atoi(nr) : 1;
+  g.tilesH = ceil_div(ceil_div(H, DWS_R), g.nrt);
   static const char* rm = getenv("ACCUNET_DW_SPAN_REMAP");  // tuning knob
   const long nb = (long)B * g.tilesH * g.NS;
   g.remap = (rm && atoi(rm) && nb % 8 == 0) ? 1 : 0;
@@ -1014,7 +1046,8 @@ template <int NT, int AUX, typename T>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 ? 3 : 2)))
 dw3x3_span_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dz,
                         const float* __restrict__ sc, const float* __restrict__ sh, int act,
-                        float* __restrict__ part, DwSGeom g, int nrt) {
+                        float* __restrict__ part, DwSGeom g) {
+  const int nrt = g.nrt;
   typedef DwS<NT> G;
   constexpr int R = G::R;
   typedef typename QuadRaw<T>::type RawQ;
@@ -1101,19 +1134,17 @@ dw3x3_span_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dz,
   // lanes' sums -> per-channel partials: one thread per (tap i, quad qq) adds the span's
   // pixels in order
   __syncthreads();
-  float* red = reinterpret_cast<float*>(tile);  // [NA][10][4]
+  float4* red = reinterpret_cast<float4*>(tile);  // [10][NA] float4: lane-contiguous
   if (tid < NA) {
 #pragma unroll
-    for (int i = 0; i < 10; ++i)
-      *reinterpret_cast<float4*>(red + (tid * 10 + i) * 4) =
-          make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
+    for (int i = 0; i < 10; ++i) red[i * NA + tid] = make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
   }
   __syncthreads();
   for (int e = tid; e < 10 * CQ; e += NT) {
     const int i = e / CQ, qq = e - (e / CQ) * CQ;
     float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int pp = 0; pp < PX; ++pp) {
-      const float4 v = *reinterpret_cast<const float4*>(red + ((pp * CQ + qq) * 10 + i) * 4);
+      const float4 v = red[i * NA + pp * CQ + qq];
       a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
     }
     st4(part + ((long)bid * 10 + i) * g.C + 4 * qq, a);
@@ -1125,6 +1156,7 @@ dw3x3_span_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dz,
 static DwSGeom dw_sgeom_wgrad(int B, int H, int W, int C, int nt, dim3* grid) {
   DwSGeom g = dw_sgeom(B, H, W, C, nt, grid);
   g.remap = 0;
+  g.nrt = DWS_WG_NRT;
   g.tilesH = ceil_div(ceil_div(H, DWS_R), DWS_WG_NRT);  // bands
   *grid = dim3((unsigned)((long)B * g.tilesH * g.NS));
   return g;
@@ -1341,7 +1373,7 @@ extern "C" int accunet_dw3x3_fwd(const void* x, const float* wt, const float* bi
 
 static int dw_wgrad_rows(int B, int H, int W, int C) {
   dim3 grid;
-  if (const int nt = dw_span_nt(H, W, C)) {
+  if (const int nt = dw_span_nt(H, W, C, 1)) {
     dw_sgeom_wgrad(B, H, W, C, nt, &grid);
     return (int)grid.x;
   }
@@ -1374,7 +1406,7 @@ extern "C" int accunet_dw3x3_wgrad(const void* x, const void* dz, const float* s
   float* part = ws;
   float* scratch = ws + (size_t)R * 10 * C;
   float* sums = scratch + accunet_partials_ws_elems(R, 10 * C);
-  if (const int nt = dw_span_nt(H, W, C)) {
+  if (const int nt = dw_span_nt(H, W, C, 1)) {
     dim3 sgrid;
     const DwSGeom sg = dw_sgeom_wgrad(B, H, W, C, nt, &sgrid);
     R = (int)sgrid.x;
@@ -1385,10 +1417,10 @@ extern "C" int accunet_dw3x3_wgrad(const void* x, const void* dz, const float* s
           using T = decltype(tag);
           if (nt == 256)
             hipLaunchKernelGGL((dw3x3_span_wgrad_kernel<256, 0, T>), sgrid, dim3(256), 0, s,
-                               (const T*)x, (const T*)dz, sc, sh, act, part, sg, DWS_WG_NRT);
+                               (const T*)x, (const T*)dz, sc, sh, act, part, sg);
           else
             hipLaunchKernelGGL((dw3x3_span_wgrad_kernel<512, 0, T>), sgrid, dim3(512), 0, s,
-                               (const T*)x, (const T*)dz, sc, sh, act, part, sg, DWS_WG_NRT);
+                               (const T*)x, (const T*)dz, sc, sh, act, part, sg);
         }))
       return ACC_EBADARG;
   } else if (with_dt(dt, [&](auto tag) {

@@ -24,10 +24,11 @@
 
 #define GG_BK 16
 // ring depth: GG_STAGES - 1 k-tiles (16 k each) in flight ahead of the one computed.
-// A k-tile of a 128x128 tile is ~2k cycles of MFMA work, so 3 tiles ahead cover an HBM
-// round trip under load; 4 stages of 16.5 KB keep 2 workgroups per CU in LDS.
+// 3 stages of 16.5 KB (128x128 tiles) keep 3 workgroups per CU in LDS; 4 stages keep 2,
+// the same k-tiles in flight per CU, and measured 1-3 % slower per GEMM family
+// (profiles/r03_step_ab.txt), so 3 is the default.
 #ifndef GG_STAGES
-#define GG_STAGES 4
+#define GG_STAGES 3
 #endif
 
 static __device__ __attribute__((aligned(16))) float g_gemm_zero16[4];

@@ -19,6 +19,7 @@
 //   mid:    BN backward reduced to per-(b,c) terms, SE fc backward, and coefficients of
 //           da = A*g2 + Bc*a + Cc
 //   pass 2: da (then the caller runs the preceding BatchNorm's backward on it)
+#include <stdlib.h>
 #include "common.h"
 #include "chan.h"
 #include "kernels.h"
@@ -249,8 +250,8 @@ __global__ void __launch_bounds__(256) se_mid_bn_kernel(SeGeom g, SeMid m) {
   se_mid_bn_body(g, m, blockIdx.x * blockDim.x + threadIdx.x);
 }
 
-// pass 2 forward: out = lrelu(alpha[b,c]*a + betap[c])
-template <int V, typename T, bool PRO>
+// pass 2 forward: out = lrelu(alpha[b,c]*a + betap[c]); SAUX: store cache policy
+template <int V, typename T, bool PRO, int SAUX = 0>
 __global__ void __launch_bounds__(256)
 se_apply_kernel(const T* __restrict__ z, const float* __restrict__ sc,
                 const float* __restrict__ sh, int act, SeGeom g, const float* __restrict__ alpha,
@@ -286,7 +287,7 @@ se_apply_kernel(const T* __restrict__ z, const float* __restrict__ sc,
           o1[j] += y;
           o2[j] += y * y;
         }
-        bufq_st<0>(ro, off, make_float4(v[0], v[1], v[2], v[3]), (T*)nullptr);
+        bufq_st<SAUX>(ro, off, make_float4(v[0], v[1], v[2], v[3]), (T*)nullptr);
       });
     } else {
       for (long r = r0 + t.rg; r < r1; r += t.RG) {
@@ -879,9 +880,20 @@ extern "C" int accunet_se_fwd(const void* z, const float* sc, const float* sh, i
   const float* betap = alpha + (size_t)B * C;
   with_dt(dt, [&](auto tag) {
     using T = decltype(tag);
+    static int nts = -1;
+    if (nts < 0) {
+      const char* e = getenv("ACCUNET_SE_NT");  // tuning knob: non-temporal SE output stores
+      nts = e ? atoi(e) : 0;
+    }
     if (V == 4) {
-      if (pro)
+      if (pro && nts)
+        hipLaunchKernelGGL((se_apply_kernel<4, T, true, 2>), grid, dim3(256), 0, s, (const T*)z, sc,
+                           sh, act, g, alpha, betap, (T*)out, ostats);
+      else if (pro)
         hipLaunchKernelGGL((se_apply_kernel<4, T, true>), grid, dim3(256), 0, s, (const T*)z, sc,
+                           sh, act, g, alpha, betap, (T*)out, ostats);
+      else if (nts)
+        hipLaunchKernelGGL((se_apply_kernel<4, T, false, 2>), grid, dim3(256), 0, s, (const T*)z, sc,
                            sh, act, g, alpha, betap, (T*)out, ostats);
       else
         hipLaunchKernelGGL((se_apply_kernel<4, T, false>), grid, dim3(256), 0, s, (const T*)z, sc,

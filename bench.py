@@ -20,7 +20,7 @@ launch; --eager launches every kernel from Python instead.
 roofline probes; accunet/unext.py).
 
 Extra objects on the line:
-  roofline     — the HANC depthwise stage (K1, `dw3x3_span_fwd_kernel` of cnv12,
+  roofline     — the HANC depthwise stage (K1, `dw3x3_tile_fwd_kernel` of cnv12,
                  B x 256^2 x 96) re-launched back-to-back at its in-model shape after
                  the timed steps, timed with HIP events on its launch stream;
                  algorithmic bytes (2 x B*H*W*C*4) / average launch time vs the 8 TB/s

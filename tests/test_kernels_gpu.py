@@ -2,9 +2,10 @@
 of the reference ops (the depthwise conv + norm2 statistics of HANCBlock,
 ACC_UNet/ACC_UNet.py:240-247,273-275, and ChannelSELayer :37-49), called through
 the C ABI (accunet.kern) so every tile variant / fallback path is exercised:
-    dw3x3: whole-pixel span kernel (C % 8 == 0, C <= 256; 256- and 512-thread
-           blocks, ragged spans and row tiles), LDS-tiled TCQ=8 / TCQ=16 (wider
-           C % 32 == 0), register-window fallback (C % 8 != 0, incl. cnv11's C = 9)."""
+    dw3x3: forward / data gradient on the LDS-tiled TCQ=8 / TCQ=16 kernels
+           (C % 32 == 0) or the register-window fallback (incl. cnv11's C = 9); the
+           weight gradient on the whole-pixel span kernel (C % 8 == 0, C <= 256; 256-
+           and 512-thread blocks, ragged spans and row bands) or the tile kernels."""
 import os
 import sys
 
@@ -29,15 +30,15 @@ def _lrelu(t):
 
 
 DW_SHAPES = [
-    (2, 16, 16, 96),     # span, 256 threads, 10-pixel spans (last one 6 pixels)
-    (2, 24, 40, 64),     # span, 16-pixel spans, ragged W (40 = 2 x 16 + 8)
-    (1, 13, 35, 32),     # span, ragged everything
-    (3, 8, 8, 128),      # span, W < PX
-    (1, 13, 35, 96),     # span, ragged H (13) and W (35 = 3 x 10 + 5)
-    (2, 9, 21, 192),     # span, 512 threads (PX 10)
-    (1, 8, 17, 256),     # span, 512 threads (PX 8)
-    (2, 6, 300, 8),      # span, 2 quads per pixel (PX 128)
-    (2, 16, 24, 384),    # TCQ 8 tile (C > 256)
+    (2, 16, 16, 96),     # TCQ 16 tile, W = TP; wgrad span, 10-pixel spans (last 6)
+    (2, 24, 40, 64),     # TCQ 8 tile, ragged H and W; wgrad 16-pixel spans
+    (1, 13, 35, 32),     # ragged everything
+    (3, 8, 8, 128),      # W < TP / PX
+    (1, 13, 35, 96),     # wgrad span, ragged H (13) and W (35 = 3 x 10 + 5)
+    (2, 9, 21, 192),     # wgrad span, 512 threads (PX 10)
+    (1, 8, 17, 256),     # wgrad span, 512 threads (PX 8)
+    (2, 6, 300, 8),      # register kernel; wgrad span with 2 quads per pixel (PX 128)
+    (2, 16, 24, 384),    # TCQ 8 tile (C > 256, wgrad too)
     (2, 16, 16, 320),    # TCQ 16 tile (W <= 16)
     (2, 17, 19, 36),     # fallback register-window kernel, V = 4
     (2, 12, 12, 9),      # fallback, V = 1 (cnv11's hidden width)

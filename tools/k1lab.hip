@@ -159,13 +159,17 @@ __global__ void __launch_bounds__(256) row_reg(const float* x, float* z) {
 // span geometry with the LDS halo tile (the span K1 without arithmetic): R+2 rows of
 // 12 whole pixels into LDS (240 fill lanes, stride 240), each of 240 lanes stores its
 // R interior quads read back from LDS
-template <int R, int AUX>
+template <int R, int AUX, bool REMAP = false>
 __global__ void __launch_bounds__(256) span_lds(const float* x, float* z) {
   constexpr int PX = 10, NA = PX * CQ, RW = (PX + 2) * CQ, NU = (R + 2) * RW;
   constexpr int NL = (NU + NA - 1) / NA;
   __shared__ u32x4 tile[NU];
   const int nsp = (W + PX - 1) / PX;
-  const int bid = blockIdx.x;
+  int bid = blockIdx.x;
+  if (REMAP) {  // XCD-contiguous: the spans of one row (and the next rows) share an L2
+    const int per = gridDim.x >> 3;
+    bid = (bid & 7) * per + (bid >> 3);
+  }
   const int sp = bid % nsp;
   int t = bid / nsp;
   const int th = t % (H / R);
@@ -324,6 +328,7 @@ int main(int argc, char** argv) {
   rep("strip_lds default policy", [&] { hipLaunchKernelGGL((strip_lds<0>), dim3(B * 2 * 8 * 3), dim3(256), 0, 0, x, z); });
   rep("span_reg R8 nt", [&] { hipLaunchKernelGGL((span_reg<8, 2>), dim3(B * 32 * 26), dim3(256), 0, 0, x, z); });
   rep("span_lds R8 nt (span K1 shape)", [&] { hipLaunchKernelGGL((span_lds<8, 2>), dim3(B * 32 * 26), dim3(256), 0, 0, x, z); });
+  rep("span_lds R8 nt remap", [&] { hipLaunchKernelGGL((span_lds<8, 2, true>), dim3(B * 32 * 26), dim3(256), 0, 0, x, z); });
   rep("span_lds R16 nt", [&] { hipLaunchKernelGGL((span_lds<16, 2>), dim3(B * 16 * 26), dim3(256), 0, 0, x, z); });
   rep("span_reg R4 nt", [&] { hipLaunchKernelGGL((span_reg<4, 2>), dim3(B * 64 * 26), dim3(256), 0, 0, x, z); });
   rep("row_reg R1 nt", [&] { hipLaunchKernelGGL((row_reg<1, 2>), dim3(B * H), dim3(256), 0, 0, x, z); });

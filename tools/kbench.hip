@@ -172,6 +172,9 @@ int main(int argc, char** argv) {
     report("K1' dw3x3_wgrad 16x256x256x96 pro",
            timeit([&] { CA(accunet_dw3x3_wgrad(x, z, sc, sh, 1, dw, db, B, H, W, C, ws, wse, ACC_F32, 0)); }, iters),
            bytes);
+    report("K1' bf16 dw3x3_wgrad 16x256x256x96 pro",
+           timeit([&] { CA(accunet_dw3x3_wgrad(x, z, sc, sh, 1, dw, db, B, H, W, C, ws, wse, ACC_BF16, 0)); }, iters),
+           bytes / 2);
     CK(hipFree(x)); CK(hipFree(z)); CK(hipFree(ws)); CK(hipFree(st));
   }
   // ---- K1 channel-width sweep (1..6 channel groups of 32) ----

@@ -34,8 +34,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "gpurun_out")
 PROF = os.path.join(ROOT, "profiles")
-K1 = "dw3x3_span_fwd_kernel<256, false,"
-K1_GRID = 13312 * 256  # span kernel: 16 images x 32 row tiles x 26 spans of 10 pixels, 256 threads
+K1 = "dw3x3_tile_fwd_kernel<8, false,"
+K1_GRID = 196608  # 768 workgroups x 256 (16x256x256x96, channel groups fastest)
 K3 = ["se_reduce_kernel<4, float, true>", "se_mid_sample_kernel", "se_mid_bn_kernel",
       "se_apply_kernel<4, float, true>"]
 
