@@ -505,21 +505,30 @@ dw3x3_tile_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
     dw_fetch_rows<TCQ, NL, AUX, T>(v, rx, g, hbeg - 1, G::N4, w0, c0);
     dw_park_rows<TCQ, NL, QL>(tile, v, g, hbeg - 1, G::N4, w0, hbeg, pro, ps, pb, act);
   }
+  // the quad's 4 channels x 9 taps are 36 contiguous floats of wt ([C][9], 16-B aligned
+  // since c % 4 == 0): 9 float4 loads instead of 36 scalar ones
   float k[9][4], bi[4];
+  {
+    float wv[36];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+    for (int e = 0; e < 9; ++e) {
+      const float4 w4 = ld4(wt + c * 9 + 4 * e);
+      wv[4 * e] = w4.x; wv[4 * e + 1] = w4.y; wv[4 * e + 2] = w4.z; wv[4 * e + 3] = w4.w;
+    }
 #pragma unroll
-    for (int tp = 0; tp < 9; ++tp) k[tp][j] = wt[(c + j) * 9 + (flip ? 8 - tp : tp)];
-    bi[j] = bias ? bias[c + j] : 0.f;
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int tp = 0; tp < 9; ++tp) k[tp][j] = wv[j * 9 + (flip ? 8 - tp : tp)];
+    const float4 b4 = bias ? ld4(bias + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    bi[0] = b4.x; bi[1] = b4.y; bi[2] = b4.z; bi[3] = b4.w;
   }
   float bmu[4] = {0.f, 0.f, 0.f, 0.f}, bsc[4] = {0.f, 0.f, 0.f, 0.f}, bsh[4] = {0.f, 0.f, 0.f, 0.f};
   if (BNB) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      bmu[j] = bst[BN_MEAN * g.C + c + j];
-      bsc[j] = bst[BN_SCALE * g.C + c + j];
-      bsh[j] = bst[BN_SHIFT * g.C + c + j];
-    }
+    const float4 m4 = ld4(bst + BN_MEAN * g.C + c), s4 = ld4(bst + BN_SCALE * g.C + c),
+                 h4 = ld4(bst + BN_SHIFT * g.C + c);
+    bmu[0] = m4.x; bmu[1] = m4.y; bmu[2] = m4.z; bmu[3] = m4.w;
+    bsc[0] = s4.x; bsc[1] = s4.y; bsc[2] = s4.z; bsc[3] = s4.w;
+    bsh[0] = h4.x; bsh[1] = h4.y; bsh[2] = h4.z; bsh[3] = h4.w;
   }
   // Retire every load issued so far (weights, bias, BN vectors) before the strip loop.
   // Left pending, the waitcnt pass merges them into the loop's state and guards each
@@ -1215,19 +1224,13 @@ static DwTGeom dw_tgeom(int B, int H, int W, int C, int tcq, dim3* grid, int rch
   if (force && rch_max > 1) {
     rch = atoi(force) > 0 ? atoi(force) : 1;
   } else {
-      // pick the strip length by a wave-quantised cost model: a block costs its rows
-      // plus ~3 rows of unoverlapped prologue, and the grid runs in waves of
-      // 256 CUs x 3 resident blocks (measured on 16x256x256xC, tools/kbench)
-      long best = -1;
+      // the longest strips (powers of two) that still give >= 4 rounds of 3 resident
+      // blocks per CU (3072 blocks): 16x256x256x96 fp32 rch 1/2/4/8/16 = 180/159/154/155/
+      // 160 us, 32-row strips (3072 blocks) best (profiles/r03_k1lab.txt)
       for (int r = 1; r <= rch_max; r *= 2) {
-        long nb = cols * ceil_div(H, DW_TR * r);
-        long waves = (nb + 767) / 768;
-        long cost = waves * (min(DW_TR * r, H) + 3);
-        if (best < 0 || cost < best) {
-          best = cost;
-          rch = r;
-        }
+        rch = r;
         if (DW_TR * r >= H) break;
+        if (cols * ceil_div(H, DW_TR * 2 * r) < 3072) break;
       }
   }
   g.rch = rch;
