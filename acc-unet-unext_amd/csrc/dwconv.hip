@@ -836,7 +836,7 @@ struct DwsFill {
 };
 
 template <int NT, bool BNB, int AUX, typename T>
-__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(BNB ? 2 : 3)))
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(BNB || NT == 512 ? 2 : 3)))
 dw3x3_span_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
                       const float* __restrict__ bias, const float* __restrict__ sc,
                       const float* __restrict__ sh, int act, int flip, T* __restrict__ z,

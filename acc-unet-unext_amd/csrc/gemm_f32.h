@@ -11,6 +11,12 @@
 #include "gemm_common.h"
 
 #define GEMM_BK 16
+// k-tiles of register-staged prefetch in flight. 2 gives each tile two iterations of
+// MFMA work to land, but measured slower on every weight-gradient family (AM_COL 128x128
+// 73 -> 86 us per call, profiles/r03_step_ab.txt), so the default stays 1.
+#ifndef GEMM_PF
+#define GEMM_PF 1
+#endif
 
 template <int AMODE, int BMODE, int PRO_A, int PRO_B, bool VA, bool VB, int WM, int TM, int TN,
           int EPI = 0>
@@ -66,7 +72,11 @@ gemm_f32_kernel(const GemmParams p) {
     }
   }
 
-  float4 ra[NPA], rb[NPB];
+  // register staging: PF k-tiles in flight (tile kt+PF is loaded while kt is computed;
+  // tile kt+1 is written to the other LDS buffer at the end of iteration kt)
+  constexpr int PF = GEMM_PF;
+  static_assert(PF == 1 || PF == 2, "register prefetch depth 1 or 2");
+  float4 ra[PF][NPA], rb[PF][NPB];
   // BM_NN prologue coefficients: thread i-slot always loads the same column quad
   float4 bsc[NPB], bsh[NPB];
   if (BMODE == BM_NN && PRO_B != PRO_NONE) {
@@ -85,7 +95,7 @@ gemm_f32_kernel(const GemmParams p) {
   }
 
   const float* Bp = (const float*)p.B;
-  auto load_tiles = [&](int k0) {
+  auto load_tiles = [&](int k0, int sl) {
     // ------------------------------ A ---------------------------------------
     if (AMODE == AM_ROW) {
       // up to 4 channel-concatenated sources; source seams may fall anywhere (a
@@ -139,7 +149,7 @@ gemm_f32_kernel(const GemmParams p) {
             v = make_float4(e[0], e[1], e[2], e[3]);
           }
         }
-        ra[i] = v;
+        ra[sl][i] = v;
       }
     } else if (AMODE == AM_SHIFT3) {
       // implicit 3x3: k = tap*cin + ci; zero padding outside the image
@@ -180,7 +190,7 @@ gemm_f32_kernel(const GemmParams p) {
             v = make_float4(e[0], e[1], e[2], e[3]);
           }
         }
-        ra[i] = v;
+        ra[sl][i] = v;
       }
     } else {  // AM_COL: A(m,k) = A[k*lda + m]
       const float* Ab = (const float*)p.A[0];
@@ -203,7 +213,7 @@ gemm_f32_kernel(const GemmParams p) {
             if (m + 3 < M) v.w = ptr[3];
           }
         }
-        ra[i] = v;
+        ra[sl][i] = v;
       }
     }
     // ------------------------------ B ---------------------------------------
@@ -226,7 +236,7 @@ gemm_f32_kernel(const GemmParams p) {
             if (k + 3 < kend) v.w = ptr[3];
           }
         }
-        rb[i] = v;
+        rb[sl][i] = v;
       }
     } else if (BMODE == BM_NN) {  // B(k,n) = B[k*ldb + n]
 #pragma unroll
@@ -253,7 +263,7 @@ gemm_f32_kernel(const GemmParams p) {
             if (n + 3 < N) v.w = pro_apply<PRO_B>(v.w, bsc[i].w, bsh[i].w);
           }
         }
-        rb[i] = v;
+        rb[sl][i] = v;
       }
     } else {  // BM_NN_SHIFT3: B(k = pixel p, n = tap*cin + ci) = X[shift_tap(p)*ldb + ci]
 #pragma unroll
@@ -292,12 +302,12 @@ gemm_f32_kernel(const GemmParams p) {
             v = make_float4(e[0], e[1], e[2], e[3]);
           }
         }
-        rb[i] = v;
+        rb[sl][i] = v;
       }
     }
   };
 
-  auto store_tiles = [&](int buf) {
+  auto store_tiles = [&](int buf, int sl) {
     float* as = As + buf * BK * SA;
     float* bs = Bs + buf * BK * SB;
     if (AMODE == AM_COL) {
@@ -306,7 +316,7 @@ gemm_f32_kernel(const GemmParams p) {
         int idx = tid + i * GEMM_THREADS;
         if (idx < NA4) {
           int kr = idx / (BM / 4), q = idx % (BM / 4);
-          st4(as + kr * SA + 4 * q, ra[i]);
+          st4(as + kr * SA + 4 * q, ra[sl][i]);
         }
       }
     } else {
@@ -315,10 +325,10 @@ gemm_f32_kernel(const GemmParams p) {
         int idx = tid + i * GEMM_THREADS;
         if (idx < NA4) {
           int r = idx / QPR, q = idx % QPR;
-          as[(4 * q + 0) * SA + r] = ra[i].x;
-          as[(4 * q + 1) * SA + r] = ra[i].y;
-          as[(4 * q + 2) * SA + r] = ra[i].z;
-          as[(4 * q + 3) * SA + r] = ra[i].w;
+          as[(4 * q + 0) * SA + r] = ra[sl][i].x;
+          as[(4 * q + 1) * SA + r] = ra[sl][i].y;
+          as[(4 * q + 2) * SA + r] = ra[sl][i].z;
+          as[(4 * q + 3) * SA + r] = ra[sl][i].w;
         }
       }
     }
@@ -328,10 +338,10 @@ gemm_f32_kernel(const GemmParams p) {
         int idx = tid + i * GEMM_THREADS;
         if (idx < NB4) {
           int r = idx / QPR, q = idx % QPR;
-          bs[(4 * q + 0) * SB + r] = rb[i].x;
-          bs[(4 * q + 1) * SB + r] = rb[i].y;
-          bs[(4 * q + 2) * SB + r] = rb[i].z;
-          bs[(4 * q + 3) * SB + r] = rb[i].w;
+          bs[(4 * q + 0) * SB + r] = rb[sl][i].x;
+          bs[(4 * q + 1) * SB + r] = rb[sl][i].y;
+          bs[(4 * q + 2) * SB + r] = rb[sl][i].z;
+          bs[(4 * q + 3) * SB + r] = rb[sl][i].w;
         }
       }
     } else {
@@ -340,7 +350,7 @@ gemm_f32_kernel(const GemmParams p) {
         int idx = tid + i * GEMM_THREADS;
         if (idx < NB4) {
           int kr = idx / (BN / 4), q = idx % (BN / 4);
-          st4(bs + kr * SB + 4 * q, rb[i]);
+          st4(bs + kr * SB + 4 * q, rb[sl][i]);
         }
       }
     }
@@ -358,12 +368,21 @@ gemm_f32_kernel(const GemmParams p) {
   const int bn_off = wn * TN * 32 + l31;
 
   if (nkt > 0) {
-    load_tiles(kstart);
-    store_tiles(0);
+#pragma unroll
+    for (int sl = 0; sl < PF; ++sl) load_tiles(kstart + sl * BK, sl);
+    store_tiles(0, 0);
     __syncthreads();
     for (int kt = 0; kt < nkt; ++kt) {
       const int buf = kt & 1;
-      if (kt + 1 < nkt) load_tiles(kstart + (kt + 1) * BK);
+      // unconditional (tiles past kend load zeros under the lane masks), so the
+      // compiler's vmcnt counting stays exact across iterations
+      // (tile t lives in register slot t % PF; the slot of tile kt is free: kt is in LDS)
+      if (PF == 2) {
+        if ((kt & 1) == 0) load_tiles(kstart + (kt + 2) * BK, 0);
+        else load_tiles(kstart + (kt + 2) * BK, 1);
+      } else if (kt + 1 < nkt) {
+        load_tiles(kstart + (kt + 1) * BK, 0);
+      }
       const float* as = As + buf * BK * SA;
       const float* bs = Bs + buf * BK * SB;
       // fragments for step kk+1 are read from LDS before the MFMAs of step kk issue
@@ -387,7 +406,10 @@ gemm_f32_kernel(const GemmParams p) {
           for (int j = 0; j < TN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[cur][i], b[cur][j], acc[i][j], 0, 0, 0);
       }
-      if (kt + 1 < nkt) store_tiles(buf ^ 1);
+      if (kt + 1 < nkt) {  // tile kt+1 (slot (kt+1) % PF) -> the other LDS buffer
+        if (PF == 2 && (kt & 1) == 0) store_tiles(buf ^ 1, 1);
+        else store_tiles(buf ^ 1, 0);
+      }
       __syncthreads();
     }
   }

@@ -127,3 +127,11 @@ def median_live_grad(ref_grads: dict) -> float:
            if g.numel() and not structurally_zero(k)]
     per = [v for v in per if v > 0]
     return float(np.median(per)) if per else 0.0
+
+
+def grad_cosine(a: dict, b: dict, keys) -> float:
+    """cosine of the angle between two whole gradient vectors (the direction test)"""
+    num = sum(float((a[k].double().cpu() * b[k].double().cpu()).sum()) for k in keys)
+    na = sum(float((a[k].double().cpu() ** 2).sum()) for k in keys)
+    nb = sum(float((b[k].double().cpu() ** 2).sum()) for k in keys)
+    return num / max((na * nb) ** 0.5, 1e-300)

@@ -324,6 +324,37 @@ def test_side_stream_weight_gradients_bit_identical(graph, precision):
         assert torch.equal(v, runs[True][1][k]), k
 
 
+@pytest.mark.parametrize("variant", ["canonical", "script", "lite", "w"])
+def test_eval_mode_backward_matches_oracle(variant):
+    """Backward with the BatchNorms on their running statistics (model.eval(), as when a
+    caller fine-tunes or probes gradients of the reference module in eval mode): every
+    parameter gradient of the fp32 HIP path within 4x the fp32 oracle's own error of
+    the fp64 oracle, the whole gradient within 3x its relative error, same direction."""
+    nf, B, S = 8, 2, 32
+    sd = O.det_state_dict(O.param_spec(variant, 3, 1, nf), seed=0)
+    x = O.det_input((B, 3, S, S), "golden-x")
+    mask = O.det_mask((B, 1, S, S), "golden-mask", p=0.4)
+    o64, l64, g64, _ = PU.oracle_run(variant, sd, x, mask, training=False)
+    o32, l32, g32, _ = PU.oracle_run(variant, sd, x, mask, dtype=torch.float32, training=False)
+    m = _hip_model(variant, sd, nf).eval()
+    out = m(x.to(DEV))
+    loss = WeightedDiceBCE(0.5, 0.5)(out, mask.to(DEV))
+    loss.backward()
+    keys = [k for k, _ in m.named_parameters()]
+    hip = {k: (p.grad if p.grad is not None else torch.zeros_like(p)) for k, p in m.named_parameters()}
+    for k in keys:
+        ref = g64[k]
+        e32 = (g32[k].double() - ref).abs().max().item()
+        eh = (hip[k].double().cpu() - ref).abs().max().item()
+        assert eh <= 4 * e32 + 1e-4 * ref.abs().max().item() + 1e-9, (k, eh, e32)
+    eg_h = PU.global_rel_err(hip, g64, keys)
+    eg_32 = PU.global_rel_err(g32, g64, keys)
+    assert eg_h <= 3 * eg_32 + 1e-6, (eg_h, eg_32)
+    assert PU.grad_cosine(hip, g64, keys) >= 1 - 1e-9
+    assert abs(loss.item() - l64.item()) <= 4 * abs(l32.item() - l64.item()) + 1e-6
+    assert (out.double().cpu() - o64).abs().max().item() < 1e-4
+
+
 @pytest.mark.parametrize("graph", [False, True])
 def test_selective_fork_bit_identical(graph):
     """ACCUNET_WGRAD_FORK_MIN_US > 0 (ops.set_wgrad_fork_min_us): some layers' weight
