@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-2 profile pass, part A: parity tests, the bench lines (fp32 headline + bf16),
+# Round-3 profile pass, part A: parity tests, the bench lines (fp32 headline + bf16),
 # a rocprofv3 kernel trace (+ stats) of the bench, the FETCH_SIZE / WRITE_SIZE passes
 # (separate runs) that give K1's and K3's HBM traffic, and tools/kbench.
 # Part B (tools/pmc_gemm.sh + the GEMM census) runs as its own call.

@@ -1,7 +1,7 @@
 """Copy the judged summaries of one GPU round into profiles/, named per round, each
 stamped with the git commit and K1's source hash (accunet.probe.src_hash):
 
-    python tools/save_profiles.py r02          (after tools/gpu_round2.sh and
+    python tools/save_profiles.py r02          (after tools/gpu_round3.sh and
                                                  tools/pmc_gemm.sh + census, merged
                                                  into gpurun_out/)
     python tools/save_profiles.py --shrink-pmc DIR...   (on the box: keep only the
@@ -35,9 +35,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "gpurun_out")
 PROF = os.path.join(ROOT, "profiles")
 K1 = "dw3x3_tile_fwd_kernel<8, false,"
-K1_GRID = 196608  # 768 workgroups x 256 (16x256x256x96, channel groups fastest)
+K1_GRID = 3072 * 256  # 1024 tiles (32-row strips) x 3 channel groups, 256 threads (16x256x256x96)
 K3 = ["se_reduce_kernel<4, float, true>", "se_mid_sample_kernel", "se_mid_bn_kernel",
-      "se_apply_kernel<4, float, true>"]
+      "se_apply_kernel<4, float, true,"]
 
 FAMILIES = ["gemm_f32g", "gemm_f32", "gemm_bf16", "splitk", "dw3x3", "reduce_finish", "bn_bwd",
             "bn_fin", "affine_act", "se_", "hanc_pyramid", "pool", "colreduce", "sum_rows",
