@@ -290,9 +290,10 @@ def test_abi_host_side_contract_without_a_device():
     assert lib.accunet_dw3x3_fwd(one, one, None, None, None, 0, 1, one, None, 1, 8, 8, 32,
                                  one, None, 0, 0, None) == -2
     assert lib.accunet_gemm(None, None, 0, None) == -2
-    # 16x256x256x96: the tile kernel, 8 tiles of 32 pixels per row, 128-row strips
-    # -> 16 * 2 * 8 = 256 statistics rows; cnv11's 9 channels the register kernel
+    # 16x256x256x96: the tile kernel, 8 tiles of 32 pixels per row, 32-row strips (the
+    # longest with >= 3072 blocks) -> 16 * 8 * 8 = 1024 statistics rows; cnv11's 9
+    # channels the register kernel
     assert lib.accunet_dw3x3_variant(16, 256, 256, 96) == 1
-    assert lib.accunet_dw3x3_rows(16, 256, 256, 96) == 256
+    assert lib.accunet_dw3x3_rows(16, 256, 256, 96) == 1024
     assert lib.accunet_dw3x3_variant(16, 64, 64, 4352) == 1
     assert lib.accunet_dw3x3_variant(16, 256, 256, 9) == 0
