@@ -439,7 +439,7 @@ affine_act_kernel(const T* __restrict__ x, const float* __restrict__ sc,
       const __amdgpu_buffer_rsrc_t ry =
           acc_rsrc(y ? y + r0 * C : x, y ? (unsigned)(nr * C * sizeof(T)) : 0u);
       auto put = [&](const float (&v)[V], unsigned off) {
-        bufq_st<0>(ry, off, make_float4(v[0], v[1 % V], v[2 % V], v[3 % V]), (T*)nullptr);
+        bufq_st<ACC_STREAM_STORE_AUX>(ry, off, make_float4(v[0], v[1 % V], v[2 % V], v[3 % V]), (T*)nullptr);
       };
       if (res) {
         quad_rows2<4>(x + r0 * C, res + r0 * C, nr, t.rg, t.RG, C, t.c0,
@@ -659,7 +659,7 @@ bn_bwd_apply_kernel(const T* __restrict__ x, const T* __restrict__ dy,
                         const float dv[V] = {d4.x, d4.y, d4.z, d4.w};
                         float o[V];
                         row(ok, xv, dv, o);
-                        bufq_st<0>(rd, off, make_float4(o[0], o[1], o[2], o[3]), (T*)nullptr);
+                        bufq_st<ACC_STREAM_STORE_AUX>(rd, off, make_float4(o[0], o[1], o[2], o[3]), (T*)nullptr);
                       });
       } else {
         plain();

@@ -161,6 +161,11 @@ ACC_DEV void qzero(uint2& v) { v = make_uint2(0u, 0u); }
 // AUX: 0 = default cache policy, 2 = non-temporal. Descriptor bases and sizes
 // must be wave-uniform (kernel arguments / blockIdx-derived).
 #define ACC_OOB 0x80000000u
+// cache policy of the streaming kernels' output stores (BatchNorm apply / backward
+// apply, SE apply, SE backward apply): 0 = default, 2 = non-temporal
+#ifndef ACC_STREAM_STORE_AUX
+#define ACC_STREAM_STORE_AUX 0
+#endif
 typedef unsigned acc_u32x4 __attribute__((__vector_size__(16)));
 typedef unsigned acc_u32x2 __attribute__((__vector_size__(8)));
 ACC_DEV __amdgpu_buffer_rsrc_t acc_rsrc(const void* base, unsigned bytes) {

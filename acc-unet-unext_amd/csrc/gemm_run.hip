@@ -160,6 +160,12 @@ static int smallk_tile() {
 }
 
 static int pick_tile(int M, int N, int K, int bmode, int cin, bool can_split) {
+  static int force = -2;
+  if (force == -2) {
+    const char* e = getenv("ACCUNET_GEMM_TILE");  // tuning knob (tools/gbench): force a tile
+    force = e ? atoi(e) : -1;
+  }
+  if (force >= 0 && force < TILE_COUNT) return force;
   int t;
   // short-K GEMMs over many pixels (1x1 data gradients, K = the forward's N <= 64):
   // epilogue-dominated, so smaller tiles (more resident waves to hide its gathers)

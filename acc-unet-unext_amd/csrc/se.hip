@@ -251,7 +251,7 @@ __global__ void __launch_bounds__(256) se_mid_bn_kernel(SeGeom g, SeMid m) {
 }
 
 // pass 2 forward: out = lrelu(alpha[b,c]*a + betap[c]); SAUX: store cache policy
-template <int V, typename T, bool PRO, int SAUX = 0>
+template <int V, typename T, bool PRO, int SAUX = ACC_STREAM_STORE_AUX>
 __global__ void __launch_bounds__(256)
 se_apply_kernel(const T* __restrict__ z, const float* __restrict__ sc,
                 const float* __restrict__ sh, int act, SeGeom g, const float* __restrict__ alpha,
@@ -790,7 +790,7 @@ se_bwd_apply_pro_kernel(const T* __restrict__ z, const T* __restrict__ dout,
                     float v[V] = {z4.x, z4.y, z4.z, z4.w};  // V == 4 here
                     float d[V] = {d4.x, d4.y, d4.z, d4.w};
                     row(ok, v, d);
-                    bufq_st<0>(ro, off, make_float4(d[0], d[1 % V], d[2 % V], d[3 % V]), (T*)nullptr);
+                    bufq_st<ACC_STREAM_STORE_AUX>(ro, off, make_float4(d[0], d[1 % V], d[2 % V], d[3 % V]), (T*)nullptr);
                   });
   } else {
     for (long r = r0 + t.rg; r < r1; r += t.RG) {

@@ -1,0 +1,108 @@
+// Standalone fp32 GEMM microbenchmark through the C ABI (accunet_gemm): representative
+// ACC-UNet training-step shapes, median of per-launch HIP-event times, TFLOP/s against
+// the 157.3 TF fp32 MFMA peak. Links the in-tree libaccunet_hip.so:
+//   make -C tools gbench && tools/gbench [iters]
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <vector>
+#include <algorithm>
+
+#include "../include/accunet.h"
+
+#define CK(x)                                                                   \
+  do {                                                                          \
+    hipError_t e_ = (x);                                                        \
+    if (e_ != hipSuccess) {                                                     \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(1);                                                                  \
+    }                                                                           \
+  } while (0)
+
+__global__ void fill(float* p, long n, float s) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    p[i] = s * (float)((i * 2654435761u) % 1000) / 1000.f - 0.5f * s;
+}
+static float* dalloc(size_t n, float s = 1.f) {
+  float* p;
+  CK(hipMalloc(&p, n * sizeof(float)));
+  hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, p, (long)n, s);
+  return p;
+}
+
+template <class F>
+static double timeit(F f, int iters) {
+  f();
+  std::vector<hipEvent_t> ev(2 * iters);
+  for (auto& e : ev) CK(hipEventCreate(&e));
+  for (int i = 0; i < iters; ++i) {
+    CK(hipEventRecord(ev[2 * i], 0));
+    f();
+    CK(hipEventRecord(ev[2 * i + 1], 0));
+  }
+  CK(hipEventSynchronize(ev.back()));
+  std::vector<float> t(iters);
+  for (int i = 0; i < iters; ++i) CK(hipEventElapsedTime(&t[i], ev[2 * i], ev[2 * i + 1]));
+  for (auto& e : ev) CK(hipEventDestroy(e));
+  std::sort(t.begin(), t.end());
+  return 1000.0 * t[iters / 2];
+}
+
+struct Shape {
+  const char* name;
+  int M, N, K, amode, bmode, pro_a, stats, split, H, W, cin;
+};
+
+int main(int argc, char** argv) {
+  const int iters = argc > 1 ? atoi(argv[1]) : 20;
+  const Shape shapes[] = {
+      {"cnv72 x-branch fwd  65536x128x4352 NT proA stats", 65536, 128, 4352, AMODE_ROW, BMODE_NT, PRO_AFFINE_LRELU, 1, 0, 0, 0, 0},
+      {"cnv72 conv1 fwd     65536x4352x128 NT stats", 65536, 4352, 128, AMODE_ROW, BMODE_NT, PRO_NONE, 1, 0, 0, 0, 0},
+      {"cnv12 conv1 fwd   1048576x96x32 NT stats", 1048576, 96, 32, AMODE_ROW, BMODE_NT, PRO_NONE, 1, 0, 0, 0, 0},
+      {"cnv32 hnc fwd      262144x128x384 NT proA stats", 262144, 128, 384, AMODE_ROW, BMODE_NT, PRO_AFFINE_LRELU, 1, 0, 0, 0, 0},
+      {"cnv72 x dgrad       65536x4352x128 NN", 65536, 4352, 128, AMODE_ROW, BMODE_NN, PRO_NONE, 0, 0, 0, 0, 0},
+      {"cnv72 x wgrad       4352x128x65536 COL NN split", 4352, 128, 65536, AMODE_COL, BMODE_NN, PRO_NONE, 0, 1, 0, 0, 0},
+      {"rspth1 3x3 fwd   1048576x32x288 SHIFT3 stats", 1048576, 32, 288, AMODE_SHIFT3, BMODE_NT, PRO_NONE, 1, 0, 256, 256, 32},
+      {"rspth1 3x3 wgrad    32x288x1048576 COL SHIFT3 split", 32, 288, 1048576, AMODE_COL, BMODE_NN_SHIFT3, PRO_NONE, 0, 1, 256, 256, 32},
+  };
+  // operand buffers sized for the largest shape (65536 x 4352 activations, 1M x 32 for B
+  // of the 3x3 weight gradient)
+  const size_t nA = (size_t)300 << 20, nB = (size_t)40 << 20, nC = (size_t)300 << 20;
+  float *A = dalloc(nA), *B = dalloc(nB, 0.1f), *C = dalloc(nC);
+  float *sc = dalloc(8192, 1.f), *sh = dalloc(8192, 0.1f);
+  const size_t wse = (size_t)1 << 26;
+  float* ws = dalloc(wse);
+  // statistics partials: [ceil(M / BM)][2][N] doubles; BM >= 32 for every tile, so
+  // 65536/32 x 2 x 4352 x 8 B (142 MB) bounds any tile choice (ACCUNET_GEMM_TILE)
+  double* st;
+  CK(hipMalloc(&st, (size_t)160 << 20));
+  for (const Shape& s : shapes) {
+    AccGemmDesc d;
+    memset(&d, 0, sizeof(d));
+    d.M = s.M; d.N = s.N; d.K = s.K;
+    d.amode = s.amode; d.bmode = s.bmode; d.pro_a = s.pro_a; d.pro_b = PRO_NONE;
+    d.nsrc = 1;
+    d.a[0] = A;
+    d.lda[0] = s.amode == AMODE_COL ? s.M : (s.amode == AMODE_SHIFT3 ? s.cin : s.K);
+    d.kbeg[0] = 0; d.kbeg[1] = s.K;
+    d.a_scale = s.pro_a ? sc : nullptr;
+    d.a_shift = s.pro_a ? sh : nullptr;
+    d.b = B;
+    d.ldb = s.bmode == BMODE_NT ? s.K : (s.bmode == BMODE_NN_SHIFT3 ? s.cin : s.N);
+    d.H = s.H; d.W = s.W; d.cin = s.cin;
+    d.c = C; d.ldc = s.N;
+    d.stats = s.stats ? st : nullptr;
+    d.allow_split = s.split;
+    d.adt = d.bdt = d.cdt = ACC_F32;
+    const double us = timeit([&] {
+      int r = accunet_gemm(&d, ws, wse, 0);
+      if (r) { fprintf(stderr, "accunet_gemm rc %d (%s)\n", r, s.name); exit(1); }
+    }, iters);
+    const double tf = 2.0 * s.M * s.N * (double)s.K / us / 1e6;
+    printf("%-54s %9.2f us %7.1f TF/s (%.3f of 157.3)\n", s.name, us, tf, tf / 157.3);
+    fflush(stdout);
+  }
+  CK(hipDeviceSynchronize());
+  return 0;
+}
