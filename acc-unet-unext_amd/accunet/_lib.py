@@ -91,7 +91,8 @@ _SIGS = {
     "accunet_group_relayout": [P, P, I, I, I, IP, I, P],
     "accunet_se_save_elems": [I, I, I],
     "accunet_se_ws_elems": [I, I, I, I],
-    "accunet_se_fwd": [P, P, P, I, I, I, I, I, P, P, P, P, P, P, P, P, P, F, F, I, P, P, P, P, S, I, P],
+    "accunet_se_fwd": [P, P, P, I, I, I, I, I, P, P, P, P, P, P, P, P, P, F, F, I, P, P, P, P, P, S, I,
+                       P],
     "accunet_se_stats_rows": [I, I, I],
     "accunet_se_bwd": [P, P, P, P, I, I, I, I, I, P, P, P, I, P, P, P, P, P, P, P, P, P, S, I, P],
     "accunet_se_bwd_pro": [P, P, P, I, P, I, I, I, I, I, P, P, P, I, P, P, P, P, P, P, P, P, P, P,

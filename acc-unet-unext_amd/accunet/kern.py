@@ -371,13 +371,16 @@ def se_stats_rows(B, HW, C) -> int:
 
 
 def se_fwd(z, sc, sh, act, B, HW, C, Cr, w1, b1, w2, b2, gamma, beta, rmean, rvar, nbt, momentum,
-           eps, training, out, save, ostats=None):
+           eps, training, out, save, ostats=None, res=None):
+    """res: out = SE(z) + res (the fused residual add, see accunet_se_fwd)."""
     n = se_ws_elems(B, HW, C, Cr)
     ws = workspace(n, z.device)
+    if res is not None and (res.shape != z.shape or res.dtype != z.dtype or not res.is_contiguous()):
+        raise ValueError("se_fwd: res must be a contiguous tensor shaped and typed like z")
     call("accunet_se_fwd", _p(z), _p(sc), _p(sh), int(act), B, HW, C, Cr, _p(w1), _p(b1), _p(w2),
          _p(b2), _p(gamma), _p(beta), _p(rmean), _p(rvar), _p(nbt), float(momentum), float(eps),
-         1 if training else 0, _p(out), _p(save), _p(ostats), _p(ws), n, _same_dt(z, out),
-         _stream())
+         1 if training else 0, _p(out), _p(res), _p(save), _p(ostats), _p(ws), n,
+         _same_dt(z, out), _stream())
     return ws
 
 

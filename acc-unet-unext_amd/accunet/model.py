@@ -52,8 +52,9 @@ class ChannelSELayer(nn.Module):
         self.sigmoid = nn.Sigmoid()
         self.bn = nn.BatchNorm2d(num_channels)
 
-    def run(self, x, consumer_bn=None):
-        return ops.se(x, self, consumer_bn=consumer_bn)
+    def run(self, x, consumer_bn=None, res=None, res_slot=None):
+        """res: return SE(x) + res with the add fused into the SE (see ops.se)."""
+        return ops.se(x, self, consumer_bn=consumer_bn, res=res, res_slot=res_slot)
 
     def forward(self, inp):
         return _nchw_out(self.run(_nchw_in(inp)))
@@ -99,12 +100,13 @@ class Conv2d_batchnorm(nn.Module):
             raise NotImplementedError("Conv2d_batchnorm: only the 1x1 / stride-1 form ACC-UNet uses")
 
     def run(self, srcs, *, w_off=0, ups=(), weight=None, consumer_bn=None, slots=None,
-            wslot=None):
+            wslot=None, res=None, res_slot=None):
+        """res: return sqe(...) + res, the add fused into the SE (the MLFC merge)."""
         self._check()
         w = self.conv1.weight if weight is None else weight
         z = ops.pw_conv(srcs, w, self.conv1.bias, w_off=w_off, ups=ups,
                         consumer_bn=self.batchnorm, slots=slots, wslot=wslot)
-        return self.sqe.run(z, consumer_bn=consumer_bn)
+        return self.sqe.run(z, consumer_bn=consumer_bn, res=res, res_slot=res_slot)
 
     def forward(self, x):
         return _nchw_out(self.run([_nchw_in(x)]))
@@ -183,11 +185,9 @@ class ResPath(nn.Module):
             sl = slot if (i == 0 and slot is not None) else ops.GradSlot()
             z = ops.conv3x3(x, self.convs[i].weight, self.convs[i].bias, consumer_bn=self.bns[i],
                             slot=sl)
-            v = self.sqes[i].run(z)
+            # x + sqes[i](act(bns[i](z))) (:326): the add fused into the SE's apply pass
             nxt = self.bn if i == n - 1 else None
-            x = ops.bn_act_add(v, res=x, consumer_bn=nxt, act_after=ACT_LRELU, res_slot=sl)
-            if i < n - 1:
-                x = x.z
+            x = self.sqes[i].run(z, consumer_bn=nxt, res=x, res_slot=sl)
         if n == 0:
             x = ops.bn_act_add(x, consumer_bn=self.bn, act_after=ACT_LRELU, want_stats=True)
         # sqe(act(bn(x)))
@@ -234,8 +234,10 @@ class MLFC(nn.Module):
         self.sqe3 = ChannelSELayer(in_filters3)
         self.sqe4 = ChannelSELayer(in_filters4)
 
-    def _merge(self, m, xl, bn, slot=None):
-        return ops.bn_act_add(m, res=xl, consumer_bn=bn, act_after=ACT_LRELU, res_slot=slot)
+    def _merge(self, mrg, srcs, wm, slots, xl, bn, slot):
+        """x_c_l = LReLU(bns_mrg(cnv_mrg(interleave(x_c_l, x_l)) + x_l)) (:489-520): the
+        residual add fused into cnv_mrg's SE (the SE output is never written)."""
+        return mrg.run(srcs, weight=wm, slots=slots, consumer_bn=bn, res=xl, res_slot=slot)
 
     def run(self, x1, x2, x3, x4):
         xs = (x1, x2, x3, x4)
@@ -271,9 +273,8 @@ class MLFC(nn.Module):
                 f = fs[l]
                 # interleaved merge channels: 2c = x_c[c], 2c+1 = x_l[c] (:492)
                 wm = ops.group_relayout(mrg.conv1.weight.reshape(f, 2 * f), 2, (0, 1))
-                v2 = mrg.run([xcs[l], xs[l]], weight=wm, slots=[None, sl[(l, l)]])
-                finals[l] = self._merge(v2, xs[l], getattr(self, f"bns_mrg{l + 1}")[i],
-                                        sl[(l, l)])
+                finals[l] = self._merge(mrg, [xcs[l], xs[l]], wm, [None, sl[(l, l)]], xs[l],
+                                        getattr(self, f"bns_mrg{l + 1}")[i], sl[(l, l)])
         return tuple(getattr(self, f"sqe{l + 1}").run(finals[l]) for l in range(4))
 
     def forward(self, x1, x2, x3, x4):
@@ -286,8 +287,11 @@ class MLFC_W(MLFC):
 
     _weighted = True
 
-    def _merge(self, m, xl, bn, slot=None):
-        return ops.wmerge(m, xl, self.W, consumer_bn=bn)  # x_l's gradient: autograd adds it
+    def _merge(self, mrg, srcs, wm, slots, xl, bn, slot):
+        # cnv_mrg(...) * W + x_l * (1 - W) (ACC_UNet_w.py:497-522); x_l's gradient:
+        # autograd adds it
+        m = mrg.run(srcs, weight=wm, slots=slots)
+        return ops.wmerge(m, xl, self.W, consumer_bn=bn)
 
 
 class MLFC_Lite(MLFC):

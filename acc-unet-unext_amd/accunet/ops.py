@@ -873,11 +873,13 @@ class _SECfg:
     C: int
     Cr: int
     want_stats: bool = False
+    has_res: bool = False  # out = SE(x) + res (the fused residual add)
+    res_slot: object = None  # GradSlot collecting res's gradient
 
 
 class _SEFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, cfg: _SECfg, z, pro_g, pro_b, w1, b1, w2, b2, g, b):
+    def forward(ctx, cfg: _SECfg, z, pro_g, pro_b, w1, b1, w2, b2, g, b, res):
         B, HW, C, Cr = cfg.B, cfg.HW, cfg.C, cfg.Cr
         pro = cfg.pro
         out = torch.empty_like(z)
@@ -893,7 +895,7 @@ class _SEFn(torch.autograd.Function):
                         b2, g, b, bn.running_mean if bn.track_running_stats else None,
                         bn.running_var if bn.track_running_stats else None,
                         bn.num_batches_tracked if (tr and bn.track_running_stats) else None,
-                        mom, bn.eps, tr, out, save, ostats)
+                        mom, bn.eps, tr, out, save, ostats, res=res if cfg.has_res else None)
         ctx.cfg = cfg
         ctx.save_for_backward(z, pro_g, w1, w2, g, save)
         if ostats is None:
@@ -905,10 +907,16 @@ class _SEFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout, _dst):
         if dout is None:  # output unused: every input gradient is zero
-            return (None,) * 10
+            sl = ctx.cfg.res_slot
+            return (None,) * 10 + (sl.done() if sl is not None else None,)
         cfg = ctx.cfg
         z, pro_g, w1, w2, g, save = ctx.saved_tensors
         dout = dout.contiguous()
+        # the fused residual add: res's gradient is dout itself
+        dres = dout if cfg.has_res else None
+        if cfg.res_slot is not None:  # dout joins the shared buffer as a read-only addend
+            cfg.res_slot.give(dout)
+            dres = cfg.res_slot.done()
         B, HW, C, Cr = cfg.B, cfg.HW, cfg.C, cfg.Cr
         pro = cfg.pro
         dw1 = torch.empty_like(w1)
@@ -928,15 +936,18 @@ class _SEFn(torch.autograd.Function):
                             dbeta, dsum)
             if dsum is not None:
                 pro.bslot.t = dsum
-            return None, dz, dpg, dpb, dw1, db1, dw2, db2, dg, dbeta
+            return None, dz, dpg, dpb, dw1, db1, dw2, db2, dg, dbeta, dres
         da = torch.empty_like(z)
         kern.se_bwd(z, dout, None, None, pro.act, B, HW, C, Cr, w1, w2, g, cfg.training, save,
                     da, dw1, db1, dw2, db2, dg, dbeta)
-        return None, da, None, None, dw1, db1, dw2, db2, dg, dbeta
+        return None, da, None, None, dw1, db1, dw2, db2, dg, dbeta, dres
 
 
-def se(x, mod, *, consumer_bn=None):
-    """ChannelSELayer `mod` (fc1, fc2, bn) applied to x (Pending or tensor).
+def se(x, mod, *, consumer_bn=None, res=None, res_slot=None):
+    """ChannelSELayer `mod` (fc1, fc2, bn) applied to x (Pending or tensor), plus `res`
+    when given: the residual add that follows the SE in ResPath and in the MLFC merge
+    (ACC_UNet.py:326, :489-520), fused into the SE's apply pass, so the SE output is
+    never written. res_slot: GradSlot collecting res's gradient.
 
     Returns the materialised output tensor, or (when consumer_bn is given) a
     Pending(out, consumer_bn) carrying the output's statistics."""
@@ -947,10 +958,13 @@ def se(x, mod, *, consumer_bn=None):
     bn = mod.bn
     tr = bn.training or not bn.track_running_stats
     want = _want_stats(consumer_bn)
-    cfg = _SECfg(pro, bn, tr, B, H * W, C, Cr, want)
+    if res is not None:
+        res = res.contiguous()
+    cfg = _SECfg(pro, bn, tr, B, H * W, C, Cr, want, res is not None,
+                 _slot_reg(res_slot) if res is not None else None)
     pg, pb = _bn_params(x)
     out, ostats = _SEFn.apply(cfg, x.z, pg, pb, mod.fc1.weight, mod.fc1.bias, mod.fc2.weight,
-                              mod.fc2.bias, bn.weight, bn.bias)
+                              mod.fc2.bias, bn.weight, bn.bias, res)
     if consumer_bn is None:
         return out
     return Pending(out, consumer_bn, ACT_LRELU, ostats if want else None,

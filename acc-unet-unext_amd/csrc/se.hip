@@ -250,12 +250,15 @@ __global__ void __launch_bounds__(256) se_mid_bn_kernel(SeGeom g, SeMid m) {
   se_mid_bn_body(g, m, blockIdx.x * blockDim.x + threadIdx.x);
 }
 
-// pass 2 forward: out = lrelu(alpha[b,c]*a + betap[c]); SAUX: store cache policy
-template <int V, typename T, bool PRO, int SAUX = ACC_STREAM_STORE_AUX>
+// pass 2 forward: out = lrelu(alpha[b,c]*a + betap[c]) (+ res: the residual add that
+// follows the SE in ResPath, ACC_UNet.py:326, and in the MLFC merge, :489-520, fused
+// so the SE output itself is never written: the sum is, as rnd(rnd(y) + res), the
+// value the separate add would have stored)
+template <int V, typename T, bool PRO, bool RES>
 __global__ void __launch_bounds__(256)
 se_apply_kernel(const T* __restrict__ z, const float* __restrict__ sc,
                 const float* __restrict__ sh, int act, SeGeom g, const float* __restrict__ alpha,
-                const float* __restrict__ betap, T* __restrict__ out,
+                const float* __restrict__ betap, const T* __restrict__ res, T* __restrict__ out,
                 double* __restrict__ ostats) {
   ChanTile t = chan_tile<V>(g.C);
   const int b = blockIdx.x / g.NCH, ch = blockIdx.x % g.NCH;
@@ -273,33 +276,43 @@ se_apply_kernel(const T* __restrict__ z, const float* __restrict__ sc,
       al[j] = alpha[b * g.C + t.c0 + j];
       be[j] = betap[t.c0 + j];
     }
+    const bool st = ostats != nullptr;
+    auto elem = [&](bool ok, const float (&x)[V], const float (&rv)[V], float (&v)[V]) {
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const float a = PRO ? apply_act(x[j] * s[j] + h[j], act) : x[j];
+        v[j] = rnd<T>(lrelu(al[j] * a + be[j]));  // statistics of the stored value
+        if (RES) v[j] = rnd<T>(v[j] + rv[j]);
+        const double y = (st && ok) ? (double)v[j] : 0.0;
+        o1[j] += y;
+        o2[j] += y * y;
+      }
+    };
     if constexpr (V == 4) {
       const long nr = r1 > r0 ? r1 - r0 : 0;
       const __amdgpu_buffer_rsrc_t ro = acc_rsrc(out + r0 * g.C, (unsigned)(nr * g.C * sizeof(T)));
-      const bool st = ostats != nullptr;
-      quad_rows1<8>(z + r0 * g.C, nr, t.rg, t.RG, g.C, t.c0, [&](bool ok, float4 x4, unsigned off) {
-        float v[4] = {x4.x, x4.y, x4.z, x4.w};
-#pragma unroll
-        for (int j = 0; j < V; ++j) {
-          float x = PRO ? apply_act(v[j] * s[j] + h[j], act) : v[j];
-          v[j] = rnd<T>(lrelu(al[j] * x + be[j]));  // statistics of the stored value
-          const double y = (st && ok) ? (double)v[j] : 0.0;
-          o1[j] += y;
-          o2[j] += y * y;
-        }
-        bufq_st<SAUX>(ro, off, make_float4(v[0], v[1], v[2], v[3]), (T*)nullptr);
-      });
+      auto body = [&](bool ok, float4 x4, float4 r4, unsigned off) {
+        const float x[4] = {x4.x, x4.y, x4.z, x4.w}, rv[4] = {r4.x, r4.y, r4.z, r4.w};
+        float v[4];
+        elem(ok, x, rv, v);
+        bufq_st<ACC_STREAM_STORE_AUX>(ro, off, make_float4(v[0], v[1], v[2], v[3]), (T*)nullptr);
+      };
+      if (RES)
+        quad_rows2<8>(z + r0 * g.C, res + r0 * g.C, nr, t.rg, t.RG, g.C, t.c0, body);
+      else
+        quad_rows1<8>(z + r0 * g.C, nr, t.rg, t.RG, g.C, t.c0, [&](bool ok, float4 x4, unsigned off) {
+          body(ok, x4, make_float4(0.f, 0.f, 0.f, 0.f), off);
+        });
     } else {
       for (long r = r0 + t.rg; r < r1; r += t.RG) {
-        float v[V];
-        ldv<V>(z + r * g.C + t.c0, v);
+        float x[V], rv[V], v[V];
+        ldv<V>(z + r * g.C + t.c0, x);
+        if (RES) ldv<V>(res + r * g.C + t.c0, rv);
+        else {
 #pragma unroll
-        for (int j = 0; j < V; ++j) {
-          float x = PRO ? apply_act(v[j] * s[j] + h[j], act) : v[j];
-          v[j] = rnd<T>(lrelu(al[j] * x + be[j]));
-          o1[j] += v[j];
-          o2[j] += (double)v[j] * v[j];
+          for (int j = 0; j < V; ++j) rv[j] = 0.f;
         }
+        elem(true, x, rv, v);
         stv<V>(out + r * g.C + t.c0, v);
       }
     }
@@ -845,8 +858,9 @@ extern "C" int accunet_se_fwd(const void* z, const float* sc, const float* sh, i
                               int HW, int C, int Cr, const float* w1, const float* b1,
                               const float* w2, const float* b2, const float* gamma,
                               const float* beta, float* rmean, float* rvar, long long* nbt,
-                              float momentum, float eps, int training, void* out, float* save,
-                              double* ostats, float* ws, size_t ws_elems, int dt, void* stream) {
+                              float momentum, float eps, int training, void* out,
+                              const void* res, float* save, double* ostats, float* ws,
+                              size_t ws_elems, int dt, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (dt != ACC_F32 && dt != ACC_BF16) return ACC_EBADARG;
   if (ws_elems < accunet_se_ws_elems(B, HW, C, Cr)) return ACC_EBADARG;
@@ -880,32 +894,19 @@ extern "C" int accunet_se_fwd(const void* z, const float* sc, const float* sh, i
   const float* betap = alpha + (size_t)B * C;
   with_dt(dt, [&](auto tag) {
     using T = decltype(tag);
-    static int nts = -1;
-    if (nts < 0) {
-      const char* e = getenv("ACCUNET_SE_NT");  // tuning knob: non-temporal SE output stores
-      nts = e ? atoi(e) : 0;
-    }
-    if (V == 4) {
-      if (pro && nts)
-        hipLaunchKernelGGL((se_apply_kernel<4, T, true, 2>), grid, dim3(256), 0, s, (const T*)z, sc,
-                           sh, act, g, alpha, betap, (T*)out, ostats);
-      else if (pro)
-        hipLaunchKernelGGL((se_apply_kernel<4, T, true>), grid, dim3(256), 0, s, (const T*)z, sc,
-                           sh, act, g, alpha, betap, (T*)out, ostats);
-      else if (nts)
-        hipLaunchKernelGGL((se_apply_kernel<4, T, false, 2>), grid, dim3(256), 0, s, (const T*)z, sc,
-                           sh, act, g, alpha, betap, (T*)out, ostats);
-      else
-        hipLaunchKernelGGL((se_apply_kernel<4, T, false>), grid, dim3(256), 0, s, (const T*)z, sc,
-                           sh, act, g, alpha, betap, (T*)out, ostats);
-    } else {
-      if (pro)
-        hipLaunchKernelGGL((se_apply_kernel<1, T, true>), grid, dim3(256), 0, s, (const T*)z, sc,
-                           sh, act, g, alpha, betap, (T*)out, ostats);
-      else
-        hipLaunchKernelGGL((se_apply_kernel<1, T, false>), grid, dim3(256), 0, s, (const T*)z, sc,
-                           sh, act, g, alpha, betap, (T*)out, ostats);
-    }
+    auto go = [&](auto kv, auto kp, auto kr) {
+      hipLaunchKernelGGL((se_apply_kernel<decltype(kv)::value, T, decltype(kp)::value,
+                                          decltype(kr)::value>),
+                         grid, dim3(256), 0, s, (const T*)z, sc, sh, act, g, alpha, betap,
+                         (const T*)res, (T*)out, ostats);
+    };
+    using I4 = std::integral_constant<int, 4>;
+    using I1 = std::integral_constant<int, 1>;
+    using BT = std::true_type;
+    using BF = std::false_type;
+    auto by_res = [&](auto kv, auto kp) { res ? go(kv, kp, BT{}) : go(kv, kp, BF{}); };
+    if (V == 4) pro ? by_res(I4{}, BT{}) : by_res(I4{}, BF{});
+    else pro ? by_res(I1{}, BT{}) : by_res(I1{}, BF{});
   });
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }

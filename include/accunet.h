@@ -221,8 +221,12 @@ int accunet_se_fwd(const void* z, const float* sc, const float* sh, int act, int
                    int C, int Cr, const float* w1, const float* b1, const float* w2,
                    const float* b2, const float* gamma, const float* beta, float* rmean,
                    float* rvar, long long* nbt, float momentum, float eps, int training,
-                   void* out, float* save, double* ostats, float* ws, size_t ws_elems, int dt,
-                   void* stream);
+                   void* out, const void* res, float* save, double* ostats, float* ws,
+                   size_t ws_elems, int dt, void* stream);
+/* res (optional, same shape and storage as z): out = SE(z) + res, the residual add
+ * that follows the SE in ResPath (ACC_UNet/ACC_UNet.py:326) and in the MLFC merge
+ * (:489-520), fused into the apply pass so the SE output itself is never written;
+ * ostats then describe out. */
 int accunet_se_bwd(const void* z, const void* dout, const float* sc, const float* sh, int act,
                    int B, int HW, int C, int Cr, const float* w1, const float* w2,
                    const float* gamma, int training, const float* save, void* da, float* dw1,

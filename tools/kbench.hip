@@ -229,7 +229,7 @@ int main(int argc, char** argv) {
     }
     report("K3 se_fwd 16x65536x32 pro",
            timeit([&] { CA(accunet_se_fwd(z, sc, sh, 1, B, HW, C, Cr, w1, b1, w2, b2, g, be, rm, rv,
-                                          nullptr, 0.1f, 1e-5f, 1, out, save, nullptr, ws, wse, ACC_F32, 0)); }, iters),
+                                          nullptr, 0.1f, 1e-5f, 1, out, nullptr, save, nullptr, ws, wse, ACC_F32, 0)); }, iters),
            bytes);
     report("K3' se_bwd 16x65536x32 pro (2 rd + 1 rd/wr)",
            timeit([&] { CA(accunet_se_bwd(z, dout, sc, sh, 1, B, HW, C, Cr, w1, w2, g, 1, save, da,
