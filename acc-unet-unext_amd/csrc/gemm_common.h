@@ -29,6 +29,14 @@ enum { AM_ROW = 0, AM_COL = 1, AM_SHIFT3 = 2 };
 enum { BM_NT = 0, BM_NN = 1, BM_NN_SHIFT3 = 2 };
 
 #define GEMM_PAD 4
+// cache policy (buffer aux bits: 2 = nt, 16 = sc1) of the vector epilogue's streams:
+// the BatchNorm-backward input bz (read once) and the C stores
+#ifndef GEMM_EPI_ZB_AUX
+#define GEMM_EPI_ZB_AUX 0
+#endif
+#ifndef GEMM_EPI_ST_AUX
+#define GEMM_EPI_ST_AUX 2
+#endif
 #define GEMM_THREADS 256
 
 struct GemmParams {
@@ -66,6 +74,7 @@ struct GemmParams {
   int kchunk;    // K range per blockIdx.z (split-K); >= K means no split
   size_t zstride;  // element stride between split-K partial slabs
   int evec;      // epilogue may use quad (4-element) accesses (host-checked alignment)
+  int ngrp;      // N tiles per raster group (0: plain N-fastest order; see gemm_tile)
 };
 
 template <int PRO>
@@ -95,7 +104,11 @@ constexpr int gemm_epi_floats() {
 // a weight panel) while it is hot. Workgroups are dealt round-robin to the 8 XCDs, so
 // when the tile count is a multiple of 8 each XCD takes a contiguous run of tiles and
 // an A panel is fetched into one XCD's L2 once, not once per N tile.
-ACC_DEV void gemm_tile(int& mt, int& nt) {
+// ngrp > 0 (wide B: many N tiles x long K): the N tiles are cut into groups of ngrp
+// and the order is group-major (M panels within a group, N-fastest inside): the B
+// panels of one group stay in the XCD's L2 while every M panel passes, instead of the
+// whole B being evicted by the epilogue streams and re-fetched for every M panel.
+ACC_DEV void gemm_tile(int& mt, int& nt, int ngrp) {
   const int gy = gridDim.y;
   if (gridDim.z > 1 || gy == 1) {
     mt = blockIdx.x;
@@ -105,6 +118,16 @@ ACC_DEV void gemm_tile(int& mt, int& nt) {
   const int T = gridDim.x * gy;
   int bid = blockIdx.x + gridDim.x * blockIdx.y;  // dispatch order
   if ((T & 7) == 0) bid = (bid & 7) * (T >> 3) + (bid >> 3);
+  if (ngrp > 0 && ngrp < gy) {
+    const int per = gridDim.x * ngrp;  // tiles of one full group
+    const int g = bid / per;
+    const int gn0 = g * ngrp;
+    const int gw = min(ngrp, gy - gn0);
+    const int r = bid - g * per;
+    mt = r / gw;
+    nt = gn0 + (r - mt * gw);
+    return;
+  }
   nt = bid % gy;
   mt = bid / gy;
 }
@@ -501,7 +524,7 @@ ACC_DEV void gemm_epilogue_vec(const GemmParams& p, floatx16 (&acc)[TM][TN], flo
       int m;
       const bool ok = row_of(t, c, m);
       if (EPI & EPI_BNB)
-        L[c].zb = bufq_ld<0>(rZ, ok ? (unsigned)(((m - m0) * ldc + nq) * SZ) : ACC_OOB, (const TC*)nullptr);
+        L[c].zb = bufq_ld<GEMM_EPI_ZB_AUX>(rZ, ok ? (unsigned)(((m - m0) * ldc + nq) * SZ) : ACC_OOB, (const TC*)nullptr);
       if (EPI & (EPI_PYR | EPI_UPS)) {
         int b, h, w;
         gemm_pix(p, ok ? m : m0, b, h, w);
@@ -601,7 +624,7 @@ ACC_DEV void gemm_epilogue_vec(const GemmParams& p, floatx16 (&acc)[TM][TN], flo
           }
         }
       }
-      bufq_st<2>(rC, ok ? (unsigned)(((m - m0) * ldc + nq) * SZ) : ACC_OOB,
+      bufq_st<GEMM_EPI_ST_AUX>(rC, ok ? (unsigned)(((m - m0) * ldc + nq) * SZ) : ACC_OOB,
                  make_float4(v[0], v[1], v[2], v[3]), (TC*)nullptr);
     }
   }

@@ -46,7 +46,7 @@ gemm_f32_kernel(const GemmParams p) {
   const int lh = lane >> 5;
 
   int mt, nt;
-  gemm_tile(mt, nt);
+  gemm_tile(mt, nt, p.ngrp);
   const int m0 = mt * BM;
   const int n0 = nt * BN;
   const int M = p.M, N = p.N, K = p.K;

@@ -150,6 +150,19 @@ static long split_target() {
   return v;
 }
 
+// raster groups for wide-B GEMMs (gemm_tile): B bytes per group in KB
+// (ACCUNET_GEMM_NGRP_KB, tuning knob; 0 = plain N-fastest order). 1 MB groups cut the
+// pyramid data gradient's fetch (65536x4352x128) from 3.23 to 2.46 GB per launch at
+// the same time; the whole step is neutral (profiles/r03_gemm_lab.txt)
+static long ngrp_kb() {
+  static long v = -1;
+  if (v < 0) {
+    const char* e = getenv("ACCUNET_GEMM_NGRP_KB");
+    v = e ? atol(e) : 1024;
+  }
+  return v;
+}
+
 static int smallk_tile() {
   static int v = -2;
   if (v == -2) {
@@ -270,6 +283,13 @@ int gemm_run(GemmParams p, int amode, int bmode, int pro_a, int pro_b, bool allo
     for (int u = 0; u < p.nup; ++u)
       if ((p.upld[u] % 4) || ((uintptr_t)p.up[u] & cal)) ev = false;
     p.evec = ev ? 1 : 0;
+  }
+  p.ngrp = 0;
+  if (S == 1 && gy > 1 && ngrp_kb() > 0) {
+    const long per_tile = (long)p.K * BN * (bdt == ACC_BF16 ? 2 : 4);  // B bytes per N tile
+    long g = ngrp_kb() * 1024 / per_tile;
+    if (g < 1) g = 1;
+    if (g < gy) p.ngrp = (int)g;
   }
   dim3 grid(gx, gy, S);
   gemm_kfn kfn = tab[t];

@@ -52,6 +52,7 @@ static double timeit(F f, int iters) {
 struct Shape {
   const char* name;
   int M, N, K, amode, bmode, pro_a, stats, split, H, W, cin;
+  int pyr = 0;  // HANCLayer pyramid backward + BatchNorm-backward statistics epilogue
 };
 
 int main(int argc, char** argv) {
@@ -62,6 +63,7 @@ int main(int argc, char** argv) {
       {"cnv12 conv1 fwd   1048576x96x32 NT stats", 1048576, 96, 32, AMODE_ROW, BMODE_NT, PRO_NONE, 1, 0, 0, 0, 0},
       {"cnv32 hnc fwd      262144x128x384 NT proA stats", 262144, 128, 384, AMODE_ROW, BMODE_NT, PRO_AFFINE_LRELU, 1, 0, 0, 0, 0},
       {"cnv72 x dgrad       65536x4352x128 NN", 65536, 4352, 128, AMODE_ROW, BMODE_NN, PRO_NONE, 0, 0, 0, 0, 0},
+      {"cnv72 pyr dgrad     65536x4352x128 NN bnb+pyr", 65536, 4352, 128, AMODE_ROW, BMODE_NN, PRO_NONE, 1, 0, 64, 64, 0, 1},
       {"cnv72 x wgrad       4352x128x65536 COL NN split", 4352, 128, 65536, AMODE_COL, BMODE_NN, PRO_NONE, 0, 1, 0, 0, 0},
       {"rspth1 3x3 fwd   1048576x32x288 SHIFT3 stats", 1048576, 32, 288, AMODE_SHIFT3, BMODE_NT, PRO_NONE, 1, 0, 256, 256, 32},
       {"rspth1 3x3 wgrad    32x288x1048576 COL SHIFT3 split", 32, 288, 1048576, AMODE_COL, BMODE_NN_SHIFT3, PRO_NONE, 0, 1, 256, 256, 32},
@@ -77,7 +79,21 @@ int main(int argc, char** argv) {
   // 65536/32 x 2 x 4352 x 8 B (142 MB) bounds any tile choice (ACCUNET_GEMM_TILE)
   double* st;
   CK(hipMalloc(&st, (size_t)160 << 20));
+  // pyramid-backward operands of the 65536x4352 data gradient (16 x 64 x 64 pixels):
+  // bz [M][N], dP2 [M/4][2N], dP4 [M/16][2N], codes [M/4][N], [M/16][N]
+  const size_t PM = 65536, PN = 4352;
+  float* bz = dalloc(PM * PN);
+  float* bst = dalloc(4 * PN, 0.5f);
+  float* pd2 = dalloc(PM / 4 * 2 * PN, 0.1f);
+  float* pd4 = dalloc(PM / 16 * 2 * PN, 0.1f);
+  unsigned char *mk2, *mk4;
+  CK(hipMalloc(&mk2, PM / 4 * PN));
+  CK(hipMalloc(&mk4, PM / 16 * PN));
+  CK(hipMemset(mk2, 1, PM / 4 * PN));
+  CK(hipMemset(mk4, 5, PM / 16 * PN));
+  const char* only = getenv("GB_ONLY");  // run only the shapes whose name contains this
   for (const Shape& s : shapes) {
+    if (only && !strstr(s.name, only)) continue;
     AccGemmDesc d;
     memset(&d, 0, sizeof(d));
     d.M = s.M; d.N = s.N; d.K = s.K;
@@ -95,6 +111,10 @@ int main(int argc, char** argv) {
     d.stats = s.stats ? st : nullptr;
     d.allow_split = s.split;
     d.adt = d.bdt = d.cdt = ACC_F32;
+    if (s.pyr) {
+      d.bz = bz; d.bst = bst; d.bact = 1;
+      d.pd2 = pd2; d.pd4 = pd4; d.mk2 = mk2; d.mk4 = mk4;
+    }
     const double us = timeit([&] {
       int r = accunet_gemm(&d, ws, wse, 0);
       if (r) { fprintf(stderr, "accunet_gemm rc %d (%s)\n", r, s.name); exit(1); }
