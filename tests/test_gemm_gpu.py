@@ -100,6 +100,33 @@ def test_col_nn_wgrad_splitk(P, Co, Ci, pro):
     assert rel(dW, ref) < 1e-5
 
 
+@pytest.mark.parametrize("M,N,K,ldc,off", [(256, 1152, 131072, 1152, 0), (96, 290, 200003, 301, 7),
+                                           (128, 640, 65536, 1000, 333), (200, 136, 40000, 136, 0)])
+def test_splitk_many_slabs_into_slice(M, N, K, ldc, off):
+    """Tiled split-K weight gradients (more than 3 output tiles, tens of slabs): quad and
+    non-quad N, output into a column slice of a wider row (unaligned, columns outside the
+    slice untouched), ragged M; bitwise reproducible (fixed slab order); against fp64."""
+    torch.manual_seed(6)
+    A = torch.randn(K, M, device=DEV)
+    B = torch.randn(K, N, device=DEV)
+    C = torch.full((M + 1, ldc), 7.0, device=DEV)  # (one spare row: the slice is offset)
+
+    def run(c):
+        kern.gemm(M, N, K, a=[A], lda=[M], amode=_lib.AMODE_COL, b=B, ldb=N,
+                  bmode=_lib.BMODE_NN, c=c, ldc=ldc, c_offset=off, allow_split=True)
+    run(C)
+    got = torch.as_strided(C.view(-1)[off:], (M, N), (ldc, 1))
+    ref = A.double().t() @ B.double()
+    assert rel(got, ref) < 2e-5
+    mask = torch.ones((M + 1) * ldc, dtype=torch.bool, device=DEV)
+    idx = off + torch.arange(M, device=DEV)[:, None] * ldc + torch.arange(N, device=DEV)[None, :]
+    mask[idx.reshape(-1)] = False
+    assert bool((C.view(-1)[mask] == 7.0).all())
+    C2 = torch.full((M + 1, ldc), 7.0, device=DEV)
+    run(C2)
+    assert torch.equal(C, C2)
+
+
 @pytest.mark.parametrize("B,H,W,Ci,Co", [(2, 32, 32, 32, 32), (1, 16, 64, 64, 64), (2, 8, 8, 256, 256)])
 def test_conv3x3_fwd_dgrad_wgrad(B, H, W, Ci, Co):
     torch.manual_seed(4)
