@@ -21,6 +21,7 @@ stamped with the git commit and K1's source hash (accunet.probe.src_hash):
                               FETCH / WRITE for the top-5 GEMMs
   {r}_gemm_census.txt         tools/gemm_census.py (every GEMM of one step)
   {r}_kbench.txt              tools/kbench (kernels + float4 copy ceilings)
+  {r}_gputests.txt            the -m gpu suite: counts, mapped .so files, source hash
 """
 import collections
 import csv
@@ -236,6 +237,24 @@ def main():
     if os.path.exists(cen):
         open(os.path.join(PROF, f"{r}_gemm_census.txt"), "w").write(
             f"# python tools/gemm_census.py --top 200 ({st})\n" + open(cen).read())
+    # the -m gpu suite of this tree: pass counts, the in-tree .so files the test process
+    # mapped (tests/conftest.py writes gputests_stamp.json) and the product-source hash,
+    # checked against this checkout's sources
+    gs = os.path.join(OUT, "gputests_stamp.json")
+    gl = os.path.join(OUT, "gputests.log")
+    if os.path.exists(gs) and os.path.exists(gl):
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from conftest import product_src_hash
+        d = json.load(open(gs))
+        here = product_src_hash()
+        tail = [l.rstrip() for l in open(gl) if l.strip()][-1]
+        txt = (f"# python -m pytest tests -m gpu on one MI355X ({st})\n"
+               f"product sources (csrc, accunet, include) sha {d['product_src_sha']} on the box, "
+               f"{here} in this checkout: {'MATCH' if d['product_src_sha'] == here else 'DIFFERENT'}\n"
+               f"device: {d.get('device')}\nexit status: {d['exitstatus']}\ncounts: {json.dumps(d['counts'])}\n"
+               f"native libraries mapped by the test process: {', '.join(d['native_so_loaded'])}\n"
+               f"pytest summary: {tail}\n")
+        open(os.path.join(PROF, f"{r}_gputests.txt"), "w").write(txt)
     kb = os.path.join(OUT, "kbench.txt")
     if os.path.exists(kb):
         open(os.path.join(PROF, f"{r}_kbench.txt"), "w").write(f"# tools/kbench 20 ({st})\n" + open(kb).read())
