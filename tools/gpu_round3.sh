@@ -18,6 +18,8 @@ timeout -k 10 300 python bench.py --dtype bf16 --no-cpu-baseline > gpurun_out/be
 grep '^{"metric' gpurun_out/bench_bf16.log | cut -c1-200
 timeout -k 10 300 python bench.py --model unext > gpurun_out/bench_unext.log 2>&1
 grep '^{"metric' gpurun_out/bench_unext.log | cut -c1-200
+timeout -k 10 300 python bench.py --variant w --size 512 --batch 4 --no-cpu-baseline > gpurun_out/bench_w512.log 2>&1
+grep '^{"metric' gpurun_out/bench_w512.log | cut -c1-200
 rm -rf gpurun_out/prof_bench
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/prof_bench.log 2>&1
 echo "kernel trace done"

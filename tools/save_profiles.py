@@ -186,7 +186,8 @@ def main():
     os.makedirs(PROF, exist_ok=True)
     # bench lines
     for log, name in (("bench_full.log", f"{r}_bench_line.json"), ("bench_bf16.log", f"{r}_bench_line_bf16.json"),
-                      ("bench_unext.log", f"{r}_unext_bench_line.json")):
+                      ("bench_unext.log", f"{r}_unext_bench_line.json"),
+                      ("bench_w512.log", f"{r}_bench_line_w512.json")):
         p = os.path.join(OUT, log)
         if os.path.exists(p):
             for line in open(p):
