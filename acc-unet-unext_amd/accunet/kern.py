@@ -275,8 +275,9 @@ def stream_ticket_bank(stream, bank: int) -> None:
     call("accunet_stream_ticket_bank", ctypes.c_void_p(stream.cuda_stream), int(bank))
 
 
-def dw3x3_rows(B, H, W, C) -> int:
-    return int(_lib_raw().accunet_dw3x3_rows(B, H, W, C))
+def dw3x3_rows(B, H, W, C, like: torch.Tensor) -> int:
+    """rows of the forward's statistics partials for this shape and like's storage dtype"""
+    return int(_lib_raw().accunet_dw3x3_rows(B, H, W, C, _dt(like)))
 
 
 _DW_NAMES = {2: "dw3x3_span_fwd_kernel", 1: "dw3x3_tile_fwd_kernel", 0: "dw3x3_fwd_kernel"}
@@ -299,7 +300,7 @@ def dw3x3_fwd(x, wt, bias, sc, sh, act, flip, z, stats, B, H, W, C, bnb=None):
 
 
 def dw3x3_wgrad(x, dz, sc, sh, act, dw, db, B, H, W, C):
-    n = int(_lib_raw().accunet_dw3x3_wgrad_ws(B, H, W, C))
+    n = int(_lib_raw().accunet_dw3x3_wgrad_ws(B, H, W, C, _same_dt(x, dz)))
     ws = workspace(n, x.device)
     call("accunet_dw3x3_wgrad", _p(x), _p(dz), _p(sc), _p(sh), int(act), _p(dw), _p(db), B, H, W,
          C, _p(ws), n, _same_dt(x, dz), _stream())

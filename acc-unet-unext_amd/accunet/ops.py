@@ -564,7 +564,7 @@ class _DWConvFn(torch.autograd.Function):
         Z = _act((B, H, W, C), z)
         stats = None
         if cfg.want_stats:
-            stats = _stats((kern.dw3x3_rows(B, H, W, C), 2, C), z)
+            stats = _stats((kern.dw3x3_rows(B, H, W, C, z), 2, C), z)
         pro = cfg.pro
         # csrc/dwconv.hip picks the LDS-tiled kernel whenever C % 32 == 0
         kname = kern.dw3x3_kernel_name(B, H, W, C)
@@ -600,7 +600,7 @@ class _DWConvFn(torch.autograd.Function):
         part = R = None
         if pro.active:
             # norm1's backward reduce rides in the data-gradient kernel's epilogue
-            R = kern.dw3x3_rows(B, H, W, C)
+            R = kern.dw3x3_rows(B, H, W, C, dZ)
             part = _bnb_part(pro, B * H * W, C, z, R)
             kern.dw3x3_fwd(dZ, weight, None, None, None, ACT_NONE, 1, dA, part, B, H, W, C,
                            bnb=(z, pro.st, pro.act))
@@ -624,7 +624,7 @@ def dw_conv(x, weight, bias, *, consumer_bn=None):
     pg, pb = _bn_params(x)
     Z, stats = _DWConvFn.apply(cfg, x.z, pg, pb, weight.reshape(C, 9), bias)
     return Pending(Z, consumer_bn, ACT_LRELU, stats if want else None,
-                   kern.dw3x3_rows(B, H, W, C) if want else 0)
+                   kern.dw3x3_rows(B, H, W, C, x.z) if want else 0)
 
 
 # --------------------------------------------------------------------------

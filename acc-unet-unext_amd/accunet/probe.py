@@ -100,7 +100,7 @@ def k1_dw3x3(B, H, W, C, weight, bias, iters=20, device="cuda", dtype=torch.floa
     sc = (torch.rand(C, generator=g) + 0.5).to(device)
     sh = (torch.randn(C, generator=g) * 0.1).to(device)
     z = torch.empty_like(x)
-    st = torch.empty(kern.dw3x3_rows(B, H, W, C), 2, C, dtype=torch.float64, device=device)
+    st = torch.empty(kern.dw3x3_rows(B, H, W, C, x), 2, C, dtype=torch.float64, device=device)
     w = weight.detach().contiguous()
     b = bias.detach().contiguous()
 

@@ -1171,12 +1171,22 @@ static DwSGeom dw_sgeom_wgrad(int B, int H, int W, int C, int nt, dim3* grid) {
   return g;
 }
 
-// tile-kernel selection: 0 = none (register-window kernel), else TCQ
-static int dw_tile_tcq(int H, int W, int C) {
+// tile-kernel selection: 0 = none (register-window kernel), else TCQ. 64-channel tiles
+// (TCQ 16) for narrow images, and in bf16 wherever C % 64 == 0: a bf16 pixel segment is
+// then one whole 128-B line (16 x 256 x 256 x 192 bf16: 253 -> 227 us, bf16 step +0.8 %;
+// fp32 keeps 32-channel tiles: step -0.2 %, profiles/r03_tcq16_ab.txt).
+// ACCUNET_DW_TCQ16 (tuning knob): 0 = narrow images only, 1 = wherever C % 64 == 0.
+static int dw_tile_tcq(int H, int W, int C, int dt) {
   if (C % 32) return 0;
   if ((long)H * W * C * 4 >= (1L << 31)) return 0;  // one image per 32-bit buffer descriptor
   int CQ = C / 4;
-  if (W <= 16 && CQ % 16 == 0) return 16;
+  static int t16 = -2;
+  if (t16 == -2) {
+    const char* e = getenv("ACCUNET_DW_TCQ16");
+    t16 = e ? atoi(e) : -1;
+  }
+  const bool wide = t16 == 1 || (t16 < 0 && dt == ACC_BF16);
+  if ((W <= 16 || wide) && CQ % 16 == 0) return 16;
   return 8;
 }
 
@@ -1263,16 +1273,16 @@ static DwGeom dw_geom(int B, int H, int W, int C, int V, dim3* grid) {
 extern "C" int accunet_dw3x3_variant(int B, int H, int W, int C) {
   (void)B;
   if (dw_span_nt(H, W, C)) return 2;
-  return dw_tile_tcq(H, W, C) ? 1 : 0;
+  return dw_tile_tcq(H, W, C, ACC_F32) ? 1 : 0;
 }
 
-extern "C" int accunet_dw3x3_rows(int B, int H, int W, int C) {
+extern "C" int accunet_dw3x3_rows(int B, int H, int W, int C, int dt) {
   dim3 grid;
   if (const int nt = dw_span_nt(H, W, C)) {
     dw_sgeom(B, H, W, C, nt, &grid);
     return (int)grid.x;
   }
-  int tcq = dw_tile_tcq(H, W, C);
+  int tcq = dw_tile_tcq(H, W, C, dt);
   if (tcq) dw_tgeom(B, H, W, C, tcq, &grid, dw_rch_max());
   else dw_geom(B, H, W, C, (C % 4 == 0) ? 4 : 1, &grid);
   return (int)grid.x;
@@ -1317,7 +1327,7 @@ extern "C" int accunet_dw3x3_fwd(const void* x, const float* wt, const float* bi
       return ACC_EBADARG;
     return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
   }
-  int tcq = dw_tile_tcq(H, W, C);
+  int tcq = dw_tile_tcq(H, W, C, dt);
   if (tcq) {
     DwTGeom tg = dw_tgeom(B, H, W, C, tcq, &grid, dw_rch_max());
     // non-temporal loads only for inputs above the Infinity Cache (bytes as stored)
@@ -1374,24 +1384,26 @@ extern "C" int accunet_dw3x3_fwd(const void* x, const float* wt, const float* bi
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 
-static int dw_wgrad_rows(int B, int H, int W, int C) {
+static int dw_wgrad_rows(int B, int H, int W, int C, int dt) {
   dim3 grid;
   if (const int nt = dw_span_nt(H, W, C, 1)) {
     dw_sgeom_wgrad(B, H, W, C, nt, &grid);
     return (int)grid.x;
   }
-  int tcq = dw_tile_tcq(H, W, C);
+  int tcq = dw_tile_tcq(H, W, C, dt);
   if (tcq) dw_tgeom(B, H, W, C, tcq, &grid);
   else dw_geom(B, H, W, C, (C % 4 == 0) ? 4 : 1, &grid);
   return (int)grid.x;
 }
 
-size_t dw_wgrad_ws(int B, int H, int W, int C) {
-  int R = dw_wgrad_rows(B, H, W, C);
+size_t dw_wgrad_ws(int B, int H, int W, int C, int dt) {
+  int R = dw_wgrad_rows(B, H, W, C, dt);
   return (size_t)R * 10 * C + accunet_partials_ws_elems(R, 10 * C) + 10 * (size_t)C;
 }
 
-extern "C" size_t accunet_dw3x3_wgrad_ws(int B, int H, int W, int C) { return dw_wgrad_ws(B, H, W, C); }
+extern "C" size_t accunet_dw3x3_wgrad_ws(int B, int H, int W, int C, int dt) {
+  return dw_wgrad_ws(B, H, W, C, dt);
+}
 
 extern "C" int accunet_dw3x3_wgrad(const void* x, const void* dz, const float* sc,
                                    const float* sh, int act, float* dw, float* db, int B, int H,
@@ -1399,13 +1411,13 @@ extern "C" int accunet_dw3x3_wgrad(const void* x, const void* dz, const float* s
   hipStream_t s = (hipStream_t)stream;
   int V = (C % 4 == 0) ? 4 : 1;
   dim3 grid;
-  int tcq = dw_tile_tcq(H, W, C);
+  int tcq = dw_tile_tcq(H, W, C, dt);
   DwTGeom tg;
   DwGeom g;
   if (tcq) tg = dw_tgeom(B, H, W, C, tcq, &grid);
   else g = dw_geom(B, H, W, C, V, &grid);
   int R = (int)grid.x;
-  if (ws_elems < dw_wgrad_ws(B, H, W, C)) return ACC_EBADARG;
+  if (ws_elems < dw_wgrad_ws(B, H, W, C, dt)) return ACC_EBADARG;
   float* part = ws;
   float* scratch = ws + (size_t)R * 10 * C;
   float* sums = scratch + accunet_partials_ws_elems(R, 10 * C);
@@ -1413,7 +1425,7 @@ extern "C" int accunet_dw3x3_wgrad(const void* x, const void* dz, const float* s
     dim3 sgrid;
     const DwSGeom sg = dw_sgeom_wgrad(B, H, W, C, nt, &sgrid);
     R = (int)sgrid.x;
-    if (ws_elems < dw_wgrad_ws(B, H, W, C)) return ACC_EBADARG;
+    if (ws_elems < dw_wgrad_ws(B, H, W, C, dt)) return ACC_EBADARG;
     part = ws;
     scratch = ws + (size_t)R * 10 * C;
     if (with_dt(dt, [&](auto tag) {

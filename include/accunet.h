@@ -153,7 +153,9 @@ int accunet_reduce_stats(const double* part, int R, int C, double* out2C, double
  * `stats` then receives the BatchNorm-backward partials (sum g, sum g*(bz - mean)),
  * g = out * act'(bz*scale + shift), for accunet_bn_bwd_part. wgrad writes dW [C][1][3][3] and db [C].
  * ------------------------------------------------------------------------- */
-int accunet_dw3x3_rows(int B, int H, int W, int C);
+/* rows of `stats` ([rows][2][C] fp64) the forward writes for this shape and storage
+ * dtype dt (bf16 runs 64-channel tiles where C % 64 == 0). */
+int accunet_dw3x3_rows(int B, int H, int W, int C, int dt);
 /* Which forward kernel runs for the shape: 2 = whole-pixel span kernel (C % 8 == 0,
  * C <= 256), 1 = LDS tile kernel (other C % 32 == 0), 0 = register-window kernel. */
 int accunet_dw3x3_variant(int B, int H, int W, int C);
@@ -161,7 +163,7 @@ int accunet_dw3x3_fwd(const void* x, const float* wt, const float* bias, const f
                       const float* sh, int act, int flip, void* z, double* stats, int B, int H,
                       int W, int C, const void* bz, const float* bst, int bact, int dt,
                       void* stream);
-size_t accunet_dw3x3_wgrad_ws(int B, int H, int W, int C);
+size_t accunet_dw3x3_wgrad_ws(int B, int H, int W, int C, int dt);
 int accunet_dw3x3_wgrad(const void* x, const void* dz, const float* sc, const float* sh,
                         int act, float* dw, float* db, int B, int H, int W, int C, float* ws,
                         size_t ws_elems, int dt, void* stream);

@@ -294,6 +294,9 @@ def test_abi_host_side_contract_without_a_device():
     # longest with >= 3072 blocks) -> 16 * 8 * 8 = 1024 statistics rows; cnv11's 9
     # channels the register kernel
     assert lib.accunet_dw3x3_variant(16, 256, 256, 96) == 1
-    assert lib.accunet_dw3x3_rows(16, 256, 256, 96) == 1024
+    assert lib.accunet_dw3x3_rows(16, 256, 256, 96, 0) == 1024
+    # bf16 (dt 1) runs 64-channel tiles where C % 64 == 0: 16-pixel tiles, twice the rows
+    assert lib.accunet_dw3x3_rows(16, 128, 128, 192, 0) * 2 == lib.accunet_dw3x3_rows(16, 128, 128, 192, 1)
+    assert lib.accunet_dw3x3_rows(16, 256, 256, 96, 1) == 1024
     assert lib.accunet_dw3x3_variant(16, 64, 64, 4352) == 1
     assert lib.accunet_dw3x3_variant(16, 256, 256, 9) == 0

@@ -70,7 +70,7 @@ def test_dw3x3_fwd_stats_wgrad_vs_fp64(B, H, W, C, pro):
 
     f = lambda t: t.float().contiguous().to(DEV)  # noqa: E731
     xd, wd, bd, scd, shd, dzd = f(x), f(wt), f(bias), f(sc), f(sh), f(dz)
-    rows = kern.dw3x3_rows(B, H, W, C)
+    rows = kern.dw3x3_rows(B, H, W, C, xd)
     st = torch.zeros(rows, 2 * C, dtype=torch.float64, device=DEV)
     z = torch.empty(B, H, W, C, device=DEV)
     act = 1 if pro else 0

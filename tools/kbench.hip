@@ -112,7 +112,7 @@ int main(int argc, char** argv) {
     size_t n = (size_t)B * H * W * C;
     float *x = dalloc(n), *z = dalloc(n), *wt = dalloc(9 * C, 0.3f), *bi = dalloc(C, 0.1f);
     float *sc = dalloc(C, 1.f), *sh = dalloc(C, 0.1f);
-    int rows = accunet_dw3x3_rows(B, H, W, C);
+    int rows = accunet_dw3x3_rows(B, H, W, C, ACC_F32);  // (C = 96: the bf16 rows are the same)
     double* st;
     CK(hipMalloc(&st, (size_t)rows * 2 * C * sizeof(double)));
     double bytes = 2.0 * 4 * n;
@@ -150,7 +150,7 @@ int main(int argc, char** argv) {
            bytes / 2);
     {  // cnv91 forward in the bf16 mode: 16x256x256x192 bf16 = the same buffers' bytes
       const int C2 = 2 * C;
-      int rows2 = accunet_dw3x3_rows(B, H, W, C2);
+      int rows2 = accunet_dw3x3_rows(B, H, W, C2, ACC_BF16);
       double* st2;
       CK(hipMalloc(&st2, (size_t)rows2 * 2 * C2 * sizeof(double)));
       float *wt2 = dalloc(9 * C2, 0.3f), *bi2 = dalloc(C2, 0.1f), *sc2 = dalloc(C2, 1.f),
@@ -166,7 +166,7 @@ int main(int argc, char** argv) {
     report("K1 dw3x3_fwd flip (dgrad) no pro/stats",
            timeit([&] { CA(accunet_dw3x3_fwd(x, wt, nullptr, nullptr, nullptr, 0, 1, z, nullptr, B, H, W, C, nullptr, nullptr, 0, ACC_F32, 0)); }, iters),
            bytes);
-    size_t wse = accunet_dw3x3_wgrad_ws(B, H, W, C);
+    size_t wse = std::max(accunet_dw3x3_wgrad_ws(B, H, W, C, ACC_F32), accunet_dw3x3_wgrad_ws(B, H, W, C, ACC_BF16));
     float* ws = dalloc(wse);
     float *dw = dalloc(9 * C), *db = dalloc(C);
     report("K1' dw3x3_wgrad 16x256x256x96 pro",
@@ -183,7 +183,7 @@ int main(int argc, char** argv) {
       size_t n = (size_t)B * H * W * C;
       float *x = dalloc(n), *z = dalloc(n), *wt = dalloc(9 * C, 0.3f), *bi = dalloc(C, 0.1f);
       float *sc = dalloc(C, 1.f), *sh = dalloc(C, 0.1f);
-      int rows = accunet_dw3x3_rows(B, H, W, C);
+      int rows = accunet_dw3x3_rows(B, H, W, C, ACC_F32);
       double* st;
       CK(hipMalloc(&st, (size_t)rows * 2 * C * sizeof(double)));
       char name[96];
