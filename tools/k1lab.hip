@@ -264,6 +264,56 @@ __global__ void __launch_bounds__(256) strip_lds(const float* x, float* z) {
   }
 }
 
+// cross-lane geometry (a K1 without an LDS halo): a wave = 64 consecutive pixels of one
+// row x NQ channel quads (lane = pixel), walking R rows down the image: each row's NQ
+// quads are loaded once per lane (vertical window in registers), the left / right
+// neighbours come from lanes -1 / +1 (ds_bpermute here; DPP wave shifts in a kernel), and
+// the two halo pixels of the wave are loaded by the edge lanes. Stores its own quads.
+template <int NQ, int R, int AUX>
+__global__ void __launch_bounds__(256) pix_xlane(const float* x, float* z) {
+  constexpr int NG = CQ / NQ;  // channel groups
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int bid = blockIdx.x;
+  const int per = gridDim.x >> 3;
+  bid = (bid & 7) * per + (bid >> 3);
+  // block = 4 waves: 4 channel groups (or fewer) of the same 64-pixel segment
+  const int segs = W / 64;
+  const int g0 = (bid % ((NG + 3) / 4)) * 4 + wv;
+  int t = bid / ((NG + 3) / 4);
+  const int sg = t % segs;
+  t /= segs;
+  const int th = t % (H / R);
+  const int b = t / (H / R);
+  const bool on = g0 < NG;
+  const int w = sg * 64 + lane, c0 = g0 * NQ * 4;
+  const auto rx = rsrc(x + (long)b * H * W * C, IMG), rz = rsrc(z + (long)b * H * W * C, IMG);
+  u32x4 acc = {0u, 0u, 0u, 0u};
+  for (int r = 0; r < R; ++r) {
+    const int h = th * R + r;
+    u32x4 v[NQ];
+#pragma unroll
+    for (int k = 0; k < NQ; ++k)
+      v[k] = ld<AUX>(rx, on ? (unsigned)(((h * W + w) * C + c0 + 4 * k) * 4) : OOB);
+    // halo pixels of the wave (lane 0: w - 1, lane 63: w + 1)
+    const int hw = lane == 0 ? w - 1 : w + 1;
+    const bool hon = on && (lane == 0 || lane == 63) && hw >= 0 && hw < W;
+    u32x4 hv = ld<AUX>(rx, hon ? (unsigned)(((h * W + hw) * C + c0) * 4) : OOB);
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) {
+      // neighbours' quads (left, right) through the cross-lane network
+      u32x4 lft, rgt;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        lft[e] = __builtin_amdgcn_ds_bpermute(((lane + 63) & 63) * 4, (int)v[k][e]);
+        rgt[e] = __builtin_amdgcn_ds_bpermute(((lane + 1) & 63) * 4, (int)v[k][e]);
+      }
+      acc ^= lft ^ rgt ^ hv;  // consumed, so the exchange is not optimised away
+      st<AUX>(rz, on ? (unsigned)(((h * W + w) * C + c0 + 4 * k) * 4) : OOB, v[k]);
+    }
+  }
+  if (acc[0] == 0x12345678u && acc[1] == 0x9abcdef0u) z[0] = 1.f;  // (never)
+}
+
 __global__ void fill(float* p, long n) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
     p[i] = (float)((i * 2654435761u) % 1000) / 1000.f;
@@ -333,6 +383,11 @@ int main(int argc, char** argv) {
   rep("span_reg R4 nt", [&] { hipLaunchKernelGGL((span_reg<4, 2>), dim3(B * 64 * 26), dim3(256), 0, 0, x, z); });
   rep("row_reg R1 nt", [&] { hipLaunchKernelGGL((row_reg<1, 2>), dim3(B * H), dim3(256), 0, 0, x, z); });
   rep("row_reg R2 nt", [&] { hipLaunchKernelGGL((row_reg<2, 2>), dim3(B * H / 2), dim3(256), 0, 0, x, z); });
+  // 64-pixel segments x channel groups of NQ quads, 4 groups per block
+  rep("pix_xlane NQ4 R8 nt", [&] { hipLaunchKernelGGL((pix_xlane<4, 8, 2>), dim3(B * (H / 8) * (W / 64) * ((CQ / 4 + 3) / 4)), dim3(256), 0, 0, x, z); });
+  rep("pix_xlane NQ8 R8 nt", [&] { hipLaunchKernelGGL((pix_xlane<8, 8, 2>), dim3(B * (H / 8) * (W / 64) * ((CQ / 8 + 3) / 4)), dim3(256), 0, 0, x, z); });
+  rep("pix_xlane NQ4 R32 nt", [&] { hipLaunchKernelGGL((pix_xlane<4, 32, 2>), dim3(B * (H / 32) * (W / 64) * ((CQ / 4 + 3) / 4)), dim3(256), 0, 0, x, z); });
+  rep("pix_xlane NQ8 R32 default", [&] { hipLaunchKernelGGL((pix_xlane<8, 32, 0>), dim3(B * (H / 32) * (W / 64) * ((CQ / 8 + 3) / 4)), dim3(256), 0, 0, x, z); });
   CK(hipFree(x));
   CK(hipFree(z));
   return 0;
