@@ -46,9 +46,83 @@ splitk_reduce_kernel(const float* __restrict__ ws, float* __restrict__ C, int M,
   }
 }
 
+// Quad form (N % 4 == 0): a 256-thread block = (256 / G) output quads x G slab groups;
+// thread (quad, g) sums slabs g, g + G, ... as float4 (8 loads in flight), then the G
+// group sums are added in group order (deterministic). G grows with S so that deep
+// splits of small outputs still spread over many lanes.
+template <int G>
+__global__ void __launch_bounds__(256)
+splitk_reduce4_kernel(const float* __restrict__ ws, float* __restrict__ C, int M, int N, int ldc,
+                      int S, size_t zstride) {
+  constexpr int QC = 256 / G;
+  __shared__ float4 part[G][QC];
+  const int qc = threadIdx.x % QC, g = threadIdx.x / QC;
+  const long nq = (long)M * N / 4;
+  const long i = (long)blockIdx.x * QC + qc;  // output quad
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i < nq) {
+    const float4* src = reinterpret_cast<const float4*>(ws) + i;
+    const size_t zs = zstride / 4;
+    int z = g;
+    for (; z + 7 * G < S; z += 8 * G) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = src[(size_t)(z + u * G) * zs];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) { acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w; }
+    }
+    for (; z < S; z += G) {
+      const float4 v = src[(size_t)z * zs];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+  }
+  if (G > 1) {
+    part[g][qc] = acc;
+    __syncthreads();
+    if (g != 0) return;
+    acc = part[0][qc];
+#pragma unroll
+    for (int k = 1; k < G; ++k) {
+      const float4 v = part[k][qc];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+  }
+  if (i >= nq) return;
+  const long e = 4 * i;
+  const int m = (int)(e / N), n = (int)(e - (long)m * N);
+  float* dst = C + (size_t)m * ldc + n;
+  if ((ldc & 3) == 0 && ((uintptr_t)C & 15) == 0) {
+    *reinterpret_cast<float4*>(dst) = acc;
+  } else {
+    dst[0] = acc.x; dst[1] = acc.y; dst[2] = acc.z; dst[3] = acc.w;
+  }
+}
+
+static int splitk_v4_on() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ACCUNET_SPLITK_V4");  // A/B knob: 0 = the scalar reduce only
+    v = e ? atoi(e) : 1;
+  }
+  return v;
+}
+
 static void splitk_reduce(const float* ws, float* C, int M, int N, int ldc, int S, size_t zstride,
                           hipStream_t stream) {
   const long total = (long)M * N;
+  if (splitk_v4_on() && (N & 3) == 0 && (zstride & 3) == 0 && ((uintptr_t)ws & 15) == 0) {
+    const long nq = total / 4;
+    auto go = [&](auto kfn, int G) {
+      const int QC = 256 / G;
+      hipLaunchKernelGGL(kfn, dim3((unsigned)((nq + QC - 1) / QC)), dim3(256), 0, stream, ws, C, M,
+                         N, ldc, S, zstride);
+    };
+    // slab groups: enough lanes for the deep splits of small outputs
+    if (S >= 64 && nq < 65536) go(splitk_reduce4_kernel<16>, 16);
+    else if (S >= 16) go(splitk_reduce4_kernel<4>, 4);
+    else go(splitk_reduce4_kernel<1>, 1);
+    return;
+  }
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((total + SPLITK_COLS - 1) / SPLITK_COLS)),
                      dim3(SPLITK_COLS * SPLITK_GROUPS), 0, stream, ws, C, M, N, ldc, S, zstride);
 }
