@@ -219,7 +219,9 @@ static long split_target() {
   static long v = -1;
   if (v < 0) {
     const char* e = getenv("ACCUNET_SPLIT_TARGET");
-    v = e ? atol(e) : 1024;
+    // 768 with the float4 reduce (fp32 step +0.6 % over 1024, bf16 equal:
+    // profiles/r03_split_target_ab.txt)
+    v = e ? atol(e) : 768;
   }
   return v;
 }
