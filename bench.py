@@ -5,6 +5,12 @@
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
+`--gpus N` (N > 1) without a launcher around it (no WORLD_SIZE in the environment)
+starts `python -m torch.distributed.run --nnodes 1 --nproc-per-node N` on this same
+command line as a child process before anything touches the GPU, relays rank 0's
+JSON line and exits with the launcher's status (non-zero if any rank failed). Under
+a launcher the world size must equal --gpus.
+
 One step = forward + WeightedDiceBCE(0.5, 0.5) + backward (+ RCCL bucketed
 all-reduce for N > 1) + Adam(lr 1e-3) step of the canonical ACC_UNet (16.77 M
 params, ACC_UNet/ACC_UNet.py) on a per-GPU batch of 16 x 3 x 256 x 256 fp32
@@ -27,13 +33,18 @@ Extra objects on the line:
                  HBM3E peak; `rooflines` adds K3 (cnv12's SE) and the largest MFMA
                  GEMM (cnv72's HANC x-branch) (see DESIGN.md 3, accunet/probe.py);
   cpu_baseline — the CPU oracle (oracle/accunet_oracle.py, plain PyTorch-CPU, same op
-                 sequence as the reference) timed on this host on a bounded sample.
+                 sequence as the reference) timed on this host on a bounded sample;
+                 its `parity` object runs the HIP model and the CPU path on the same
+                 fixed inputs (Cfg1 Lite 1x3x128^2, canonical 1x3x256^2, eval mode) and
+                 reports max |prob| difference, _show_dice and dice_on_batch of both.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -66,15 +77,75 @@ def parse():
     ap.add_argument("--eager", action="store_true",
                     help="launch every kernel from Python (default: replay one HIP graph per step)")
     ap.add_argument("--no-probe", action="store_true", help="skip the roofline probes")
+    ap.add_argument("--no-parity", action="store_true",
+                    help="skip the same-run forward parity vs the CPU path (cpu_baseline.parity)")
     ap.add_argument("--cpu-sample", type=int, default=None,
                     help="images in the CPU sample (3; unext 16)")
     return ap.parse_args()
 
 
-def cpu_baseline(variant, size, n_img, model="acc_unet"):
-    """Time the CPU oracle (fwd + loss + bwd) on n_img images of the same workload."""
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launcher_cmd(argv, gpus, port=None):
+    """The torch.distributed.run command that runs this bench on `gpus` ranks of one
+    node (Experiments/Train_one_epoch.py:107,126-129 is the reference's single-process
+    caller; the reference has no DP launcher at all). None when no child launch is due:
+    --gpus 1, or already under a launcher (WORLD_SIZE set)."""
+    if gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1",
+            "--nproc-per-node", str(gpus), "--master-addr", "127.0.0.1",
+            "--master-port", str(port or _free_port()),
+            os.path.abspath(__file__)] + list(argv)
+
+
+def relay(cmd) -> int:
+    """Run the launcher as a child (never exec: see the module docstring), stream its
+    stderr through, print exactly one JSON line (rank 0's) and return its exit status."""
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    lines = []
+    for ln in p.stdout:
+        if ln.startswith('{"metric"'):
+            lines.append(ln.strip())
+        else:
+            sys.stderr.write(ln)
+    rc = p.wait()
+    if rc == 0 and len(lines) != 1:
+        sys.stderr.write(f"bench launcher: expected one JSON line from rank 0, got {len(lines)}\n")
+        rc = 1
+    if rc == 0:
+        print(lines[0], flush=True)
+    return rc
+
+
+def _oracle():
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import accunet_oracle as O
+    return O
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(variant, size, n_img, model="acc_unet"):
+    """Time the CPU oracle (fwd + loss + bwd) on n_img images of the same workload."""
+    O = _oracle()
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
     torch.set_num_threads(threads)
     spec = O.unext_param_spec(3, 1) if model == "unext" else O.param_spec(variant, 3, 1, 32)
@@ -93,28 +164,78 @@ def cpu_baseline(variant, size, n_img, model="acc_unet"):
     loss.backward()
     dt = time.perf_counter() - t0
     del params
-    cpu = "unknown"
-    try:
-        with open("/proc/cpuinfo") as f:
-            for line in f:
-                if line.startswith("model name"):
-                    cpu = line.split(":", 1)[1].strip()
-                    break
-    except OSError:
-        pass
     return {"value": n_img / dt, "unit": "images/s", "cores": threads, "kind": "port",
             "sample": f"{n_img} image(s) {variant} 3x{size}x{size} fwd+loss+bwd (no optimizer), "
-                      f"fp32, torch-CPU oracle, {dt:.1f} s", "cpu_model": cpu}
+                      f"fp32, torch-CPU oracle, {dt:.1f} s", "cpu_model": _cpu_model()}
+
+
+PARITY_CASES = (("lite", 128), ("canonical", 256))  # BASELINE configs[0], then configs[1]'s image
+PARITY_TOL = 1e-4  # north_star: forward Dice on fixed inputs within 1e-4 of the CPU path, fp32
+
+
+def forward_parity(dev, cases=PARITY_CASES, n_filts=32):
+    """Same-run forward parity against the reference CPU path (north_star):
+    for each (variant, size) one fixed 1x3xSxS image and mask, the HIP model (fp32, eval
+    mode, the oracle's deterministic weights) and the CPU oracle (fp32, the reference's
+    op sequence) are run on the same input, and the line reports
+    max|prob_hip - prob_cpu|, the logged Dice (WeightedDiceBCE._show_dice,
+    Experiments/utils.py:149-158) and dice_on_batch (utils.py:503-519) of both sides,
+    with the CPU forward's time and thread count. The probabilities are the sharp
+    check: for sigmoid-output presets both Dice values are degenerate (the reference
+    applies a second sigmoid, so every pixel thresholds to 1)."""
+    O = _oracle()
+    from accunet import model as M
+    from accunet.loss import WeightedDiceBCE
+    from accunet.trainer import dice_on_batch
+    threads = torch.get_num_threads()
+    rows = []
+    for variant, S in cases:
+        sd = O.det_state_dict(O.param_spec(variant, 3, 1, n_filts), seed=0)
+        x = O.det_input((1, 3, S, S), f"bench-parity-x-{S}")
+        mask = O.det_mask((1, 1, S, S), f"bench-parity-mask-{S}", p=0.3)
+        net = M.VARIANTS[variant](3, 1, n_filts=n_filts)
+        net.load_state_dict(sd)
+        net = net.to(dev).eval()
+        with torch.no_grad():
+            p_hip = net(x.to(dev)).float()
+            torch.cuda.synchronize()
+            crit = WeightedDiceBCE(0.5, 0.5)
+            sd_hip = float(crit._show_dice(p_hip, mask.to(dev).clone()))
+            db_hip = dice_on_batch(mask.to(dev), p_hip)
+            p_hip = p_hip.cpu()
+        del net
+        t0 = time.perf_counter()
+        with torch.no_grad():
+            p_cpu = O.forward(sd, x, variant, training=False)
+        t_cpu = time.perf_counter() - t0
+        sd_cpu = float(O.show_dice(p_cpu, mask.clone()))
+        db_cpu = O.dice_on_batch(mask, p_cpu)
+        row = {"case": f"{variant} n_filts {n_filts} 1x3x{S}x{S} eval",
+               "max_abs_prob": float((p_hip - p_cpu).abs().max()),
+               # the probabilities' own range: the scale the difference is read against
+               "prob_spread": float(p_cpu.max() - p_cpu.min()),
+               "show_dice": [sd_hip, sd_cpu], "dice_on_batch": [db_hip, db_cpu],
+               "cpu_forward_s": round(t_cpu, 3)}
+        row["ok"] = (row["max_abs_prob"] <= PARITY_TOL and abs(sd_hip - sd_cpu) <= PARITY_TOL
+                     and abs(db_hip - db_cpu) <= PARITY_TOL)
+        rows.append(row)
+    return {"tol": PARITY_TOL, "cores": threads, "cpu_model": _cpu_model(), "cases": rows,
+            "ok": all(r["ok"] for r in rows)}
 
 
 def main():
     args = parse()
+    cmd = launcher_cmd(sys.argv[1:], args.gpus)
+    if cmd is not None:  # before any GPU call: the ranks are children of this process
+        sys.exit(relay(cmd))
     from accunet import dist as adist
     from accunet import model as M
     from accunet import profile as prof
     from accunet.train import TrainStep
 
     rank, world = adist.init_from_env()
+    if world != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but the launcher started {world} rank(s)")
     local = adist.local_device()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -163,10 +284,13 @@ def main():
     t1 = time.perf_counter()
     prof.enable(False)
     dt = t1 - t0
+    per_rank = [dt]
     if world > 1:
-        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
+        tt = torch.zeros(world, dtype=torch.float64, device=dev)
+        tt[rank] = dt
+        dist.all_reduce(tt, op=dist.ReduceOp.SUM)  # every rank's time, in rank order
+        per_rank = tt.tolist()
+        dt = max(per_rank)
     imgs = B * world * args.steps
     line = {
         "metric": METRIC_UNEXT if unext else METRIC,
@@ -193,6 +317,8 @@ def main():
                    "global_batch": B * world, "per_gpu_batch": B, "image": [3, S, S],
                    "parallelism": f"dp{world}"},
         "final_loss": float(loss.item()),
+        "ranks_seen": world,
+        "ms_per_step_per_rank": [round(1000.0 * t / args.steps, 3) for t in per_rank],
     }
     # roofline: K1, the HANC depthwise stage at the north-star instance (cnv12's
     # dw3x3 over B x 256^2 x 96; cnv92 has the same shape), SURVEY.md 8(d), plus K3
@@ -221,6 +347,8 @@ def main():
     line["mode"] = "eager" if args.eager else "hipgraph"
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.variant, S, args.cpu_sample, args.model)
+        if not unext and not args.no_parity:
+            line["cpu_baseline"]["parity"] = forward_parity(dev)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -60,6 +60,27 @@ def test_world2_bench_line():
 
 
 @pytest.mark.gpu
+def test_bench_gpus2_direct_launches_two_ranks():
+    """`python bench.py --gpus 2` with no launcher around it (the driver's command form):
+    bench.py starts torch.distributed.run itself and relays rank 0's line, which must
+    report two ranks."""
+    env = dict(os.environ, ACCUNET_DIST_BACKEND="gloo", OMP_NUM_THREADS="4")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1",
+                        "--batch", "2", "--size", "64", "--no-probe"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1 and lines[0].startswith('{"metric"'), r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["ranks_seen"] == 2 and d["config"]["global_batch"] == 4
+    assert len(d["ms_per_step_per_rank"]) == 2
+    assert abs(d["ms_per_step"] - max(d["ms_per_step_per_rank"])) < 1e-2
+
+
+@pytest.mark.gpu
 def test_graph_event_nodes_gate_side_stream():
     """The graph-mode all-reduce gating (accunet/train.py _GraphBuckets): a marker left
     in a captured graph gets an event-record node behind it (kern.GraphEvent.attach on

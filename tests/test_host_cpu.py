@@ -300,3 +300,33 @@ def test_abi_host_side_contract_without_a_device():
     assert lib.accunet_dw3x3_rows(16, 256, 256, 96, 1) == 1024
     assert lib.accunet_dw3x3_variant(16, 64, 64, 4352) == 1
     assert lib.accunet_dw3x3_variant(16, 256, 256, 9) == 0
+
+
+def test_bench_launcher_argument_logic(monkeypatch):
+    """bench.py --gpus N: with no launcher around it (no WORLD_SIZE) and N > 1 it builds
+    one torch.distributed.run child command on 127.0.0.1 with N ranks and the same
+    arguments; --gpus 1, or a run already under a launcher, starts no child."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(os.path.dirname(HERE),
+                                                                             "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    argv = ["--gpus", "8", "--steps", "5", "--warmup", "2"]
+    cmd = bench.launcher_cmd(argv, 8, port=29555)
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert cmd[cmd.index("--nproc-per-node") + 1] == "8"
+    assert cmd[cmd.index("--nnodes") + 1] == "1"
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[cmd.index("--master-port") + 1] == "29555"
+    assert cmd[-len(argv) - 1].endswith("bench.py") and cmd[-len(argv):] == argv
+    assert bench.launcher_cmd(["--gpus", "1"], 1) is None
+    monkeypatch.setenv("WORLD_SIZE", "8")
+    assert bench.launcher_cmd(argv, 8) is None
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    # relay: rank 0's one JSON line passes through, other output goes to stderr, and a
+    # failing launcher's status comes back non-zero
+    ok = bench.relay([sys.executable, "-c", "print('log'); print('{\"metric\": \"m\"}')"])
+    assert ok == 0
+    assert bench.relay([sys.executable, "-c", "import sys; sys.exit(3)"]) == 3
+    assert bench.relay([sys.executable, "-c", "print('no line')"]) == 1
