@@ -169,30 +169,36 @@ def cpu_baseline(variant, size, n_img, model="acc_unet"):
                       f"fp32, torch-CPU oracle, {dt:.1f} s", "cpu_model": _cpu_model()}
 
 
-PARITY_CASES = (("lite", 128), ("canonical", 256))  # BASELINE configs[0], then configs[1]'s image
+# (variant, image size, weight seed, input key): configs[0] is the reference's own
+# golden case (tests/golden/cfg1_lite.npz holds the reference's output for it), then
+# configs[1]'s image at batch 1
+PARITY_CASES = (("lite", 128, 1, "cfg1"), ("canonical", 256, 0, "bench-parity-256"))
 PARITY_TOL = 1e-4  # north_star: forward Dice on fixed inputs within 1e-4 of the CPU path, fp32
 
 
 def forward_parity(dev, cases=PARITY_CASES, n_filts=32):
-    """Same-run forward parity against the reference CPU path (north_star):
-    for each (variant, size) one fixed 1x3xSxS image and mask, the HIP model (fp32, eval
-    mode, the oracle's deterministic weights) and the CPU oracle (fp32, the reference's
-    op sequence) are run on the same input, and the line reports
+    """Same-run forward parity against the reference CPU path (north_star; SURVEY 8(c),
+    8(d) Cfg1): for each case one fixed 1x3xSxS image and mask; the HIP model (fp32,
+    eval mode, the oracle's deterministic weights) and the CPU oracle (fp32, the
+    reference's op sequence) run on the same input, and the line reports
     max|prob_hip - prob_cpu|, the logged Dice (WeightedDiceBCE._show_dice,
     Experiments/utils.py:149-158) and dice_on_batch (utils.py:503-519) of both sides,
-    with the CPU forward's time and thread count. The probabilities are the sharp
-    check: for sigmoid-output presets both Dice values are degenerate (the reference
-    applies a second sigmoid, so every pixel thresholds to 1)."""
+    with the CPU forward's time and thread count. For the Cfg1 case the reference's own
+    output (tests/golden/cfg1_lite.npz, recorded by importing the reference) is compared
+    too. The probabilities are the sharp check: for sigmoid-output presets both Dice
+    values are degenerate (the reference applies a second sigmoid, so every pixel
+    thresholds to 1)."""
+    import numpy as np
     O = _oracle()
     from accunet import model as M
     from accunet.loss import WeightedDiceBCE
     from accunet.trainer import dice_on_batch
     threads = torch.get_num_threads()
     rows = []
-    for variant, S in cases:
-        sd = O.det_state_dict(O.param_spec(variant, 3, 1, n_filts), seed=0)
-        x = O.det_input((1, 3, S, S), f"bench-parity-x-{S}")
-        mask = O.det_mask((1, 1, S, S), f"bench-parity-mask-{S}", p=0.3)
+    for variant, S, seed, key in cases:
+        sd = O.det_state_dict(O.param_spec(variant, 3, 1, n_filts), seed=seed)
+        x = O.det_input((1, 3, S, S), f"{key}-x")
+        mask = O.det_mask((1, 1, S, S), f"{key}-mask", p=0.5)
         net = M.VARIANTS[variant](3, 1, n_filts=n_filts)
         net.load_state_dict(sd)
         net = net.to(dev).eval()
@@ -216,8 +222,15 @@ def forward_parity(dev, cases=PARITY_CASES, n_filts=32):
                "prob_spread": float(p_cpu.max() - p_cpu.min()),
                "show_dice": [sd_hip, sd_cpu], "dice_on_batch": [db_hip, db_cpu],
                "cpu_forward_s": round(t_cpu, 3)}
-        row["ok"] = (row["max_abs_prob"] <= PARITY_TOL and abs(sd_hip - sd_cpu) <= PARITY_TOL
-                     and abs(db_hip - db_cpu) <= PARITY_TOL)
+        ok = (row["max_abs_prob"] <= PARITY_TOL and abs(sd_hip - sd_cpu) <= PARITY_TOL
+              and abs(db_hip - db_cpu) <= PARITY_TOL)
+        gold = os.path.join(ROOT, "tests", "golden", "cfg1_lite.npz")
+        if key == "cfg1" and os.path.exists(gold):
+            g = np.load(gold)
+            row["max_abs_prob_vs_reference_golden"] = float(
+                np.abs(p_hip.double().numpy() - g["probs_eval"]).max())
+            ok = ok and row["max_abs_prob_vs_reference_golden"] <= PARITY_TOL
+        row["ok"] = ok
         rows.append(row)
     return {"tol": PARITY_TOL, "cores": threads, "cpu_model": _cpu_model(), "cases": rows,
             "ok": all(r["ok"] for r in rows)}
