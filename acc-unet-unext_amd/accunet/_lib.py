@@ -67,6 +67,8 @@ _SIGS = {
     "accunet_gemm_stats_rows": [I, I, I, I, I, I],
     "accunet_stream_rows": [L, I],
     "accunet_stream_ticket_bank": [P, I],
+    "accunet_stream_ticket_unregister": [P],
+    "accunet_abi_hash": [],
     "accunet_bn_finalize": [P, I, I, D, P, P, P, P, P, F, F, I, P, P, P],
     "accunet_affine_act_fwd": [P, P, P, I, P, P, L, I, P, IP, I, P],
     "accunet_bn_bwd_ws_elems": [L, I],
@@ -139,6 +141,9 @@ _SIZE_FNS = {"accunet_bn_bwd_ws_elems", "accunet_bn_bwd_part_ws_elems", "accunet
              "accunet_head_ws_elems", "accunet_loss_ws_elems", "accunet_dwconvk_wgrad_ws",
              "accunet_dwconvk_dgrad_ws"}
 
+_LL_FNS = {"accunet_abi_hash"}
+HEADER = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "accunet.h")
+
 _lib = None
 
 
@@ -155,14 +160,41 @@ def load():
             f"libaccunet_hip.so not found at {LIB_PATH}; build it with "
             "`make -C acc-unet-unext_amd -j8` (or __graft_entry__.build())")
     lib = ctypes.CDLL(LIB_PATH)
+    check_abi(lib)
     for name, args in _SIGS.items():
-        if LIB_PATH != _DEFAULT_LIB and not hasattr(lib, name):
-            continue  # A/B against an older build: entry points it predates stay unbound
         fn = getattr(lib, name)
         fn.argtypes = args
-        fn.restype = c_size_t if name in _SIZE_FNS else c_int
+        fn.restype = (c_size_t if name in _SIZE_FNS else c_longlong if name in _LL_FNS
+                      else c_int)
     _lib = lib
     return lib
+
+
+def header_abi_hash(path: str = HEADER) -> int:
+    """The ABI identity the Makefile bakes into the library: the first 15 hex digits
+    of include/accunet.h's sha256 (csrc/abi.hip)."""
+    import hashlib
+    with open(path, "rb") as fh:
+        return int(hashlib.sha256(fh.read()).hexdigest()[:15], 16)
+
+
+def check_abi(lib) -> None:
+    """Refuse a library built from another header (an ACCUNET_LIB_OVERRIDE A/B build of
+    older sources, or a stale in-tree build): its entry points would be called with
+    this binding's argument lists, shifted wherever a signature changed."""
+    if not hasattr(lib, "accunet_abi_hash"):
+        raise AccError(f"{LIB_PATH} predates the ABI hash (accunet_abi_hash): rebuild it")
+    lib.accunet_abi_hash.argtypes = []
+    lib.accunet_abi_hash.restype = c_longlong
+    got = int(lib.accunet_abi_hash())
+    if os.path.exists(HEADER):
+        want = header_abi_hash()
+        if got != want:
+            raise AccError(f"{LIB_PATH} was built from another include/accunet.h (ABI hash "
+                           f"{got:#x}, header {want:#x}): rebuild it with "
+                           "`make -C acc-unet-unext_amd`")
+    elif LIB_PATH != _DEFAULT_LIB:
+        raise AccError("ACCUNET_LIB_OVERRIDE needs include/accunet.h to check the ABI")
 
 
 def declared_symbols():

@@ -152,6 +152,19 @@ extern "C" int accunet_stream_ticket_bank(void* stream, int bank) {
   return ACC_OK;
 }
 
+extern "C" int accunet_stream_ticket_unregister(void* stream) {
+  if (!stream) return ACC_EBADARG;
+  std::lock_guard<std::mutex> lk(g_bank_mu);
+  for (int i = 0; i < g_bank_n; ++i)
+    if (g_bank_stream[i] == (hipStream_t)stream) {
+      g_bank_stream[i] = g_bank_stream[g_bank_n - 1];
+      g_bank_of[i] = g_bank_of[g_bank_n - 1];
+      --g_bank_n;
+      return ACC_OK;
+    }
+  return ACC_EBADARG;
+}
+
 static int stream_bank(hipStream_t s) {
   if (!s) return 0;
   std::lock_guard<std::mutex> lk(g_bank_mu);

@@ -1041,8 +1041,8 @@ static int dw_span_nt(int H, int W, int C, int bit = 2) {
   if (!(dw_span_on() & bit) || C % 8) return 0;  // CQ even (bf16 fill units are quad pairs)
   if ((long)H * W * C * 4 >= (1L << 31)) return 0;
   const int CQ = C / 4;
-  // (512-thread blocks, CQ 33..64, hold 102 KB of LDS, one block per CU: in the model
-  // the tile kernel is as fast there, so they run only for the forward knob)
+  // the weight gradient runs 256-thread spans (CQ <= 32) only; 512-thread blocks (CQ
+  // 33..64) hold 102 KB of LDS, one block per CU, and run only for the forward knob
   if (bit == 1) return CQ <= 32 ? 256 : 0;
   return CQ <= 32 ? 256 : (CQ <= 64 ? 512 : 0);
 }
@@ -1446,14 +1446,12 @@ extern "C" int accunet_dw3x3_wgrad(const void* x, const void* dz, const float* s
     if (ws_elems < dw_wgrad_ws(B, H, W, C, dt)) return ACC_EBADARG;
     part = ws;
     scratch = ws + (size_t)R * 10 * C;
+    // dw_span_nt(.., 1) is 256 or 0: the weight gradient runs 256-thread spans only
+    if (nt != 256) return ACC_EBADARG;
     if (with_dt(dt, [&](auto tag) {
           using T = decltype(tag);
-          if (nt == 256)
-            hipLaunchKernelGGL((dw3x3_span_wgrad_kernel<256, 0, T>), sgrid, dim3(256), 0, s,
-                               (const T*)x, (const T*)dz, sc, sh, act, part, sg);
-          else
-            hipLaunchKernelGGL((dw3x3_span_wgrad_kernel<512, 0, T>), sgrid, dim3(512), 0, s,
-                               (const T*)x, (const T*)dz, sc, sh, act, part, sg);
+          hipLaunchKernelGGL((dw3x3_span_wgrad_kernel<256, 0, T>), sgrid, dim3(256), 0, s,
+                             (const T*)x, (const T*)dz, sc, sh, act, part, sg);
         }))
       return ACC_EBADARG;
   } else if (with_dt(dt, [&](auto tag) {

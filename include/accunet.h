@@ -117,6 +117,14 @@ int accunet_stream_rows(long P, int C);
  * 0..1, a null stream or a full table (64 streams). No reference counterpart (the
  * reference's reductions are ATen's). */
 int accunet_stream_ticket_bank(void* stream, int bank);
+/* Drop a stream's registration (call before destroying a registered stream, so a
+ * later stream that reuses the handle does not inherit its bank). Returns 0, or -2
+ * for a null or unregistered stream. */
+int accunet_stream_ticket_unregister(void* stream);
+/* ABI identity: the first 15 hex digits of this header's sha256, fixed when the
+ * library was built. The Python binding refuses a library whose hash differs from
+ * the header it binds against. */
+long long accunet_abi_hash(void);
 int accunet_bn_finalize(const double* part, int R, int C, double count, const float* gamma,
                         const float* beta, float* rmean, float* rvar, long long* nbt,
                         float momentum, float eps, int training, float* st, double* ws,
@@ -156,8 +164,9 @@ int accunet_reduce_stats(const double* part, int R, int C, double* out2C, double
 /* rows of `stats` ([rows][2][C] fp64) the forward writes for this shape and storage
  * dtype dt (bf16 runs 64-channel tiles where C % 64 == 0). */
 int accunet_dw3x3_rows(int B, int H, int W, int C, int dt);
-/* Which forward kernel runs for the shape: 2 = whole-pixel span kernel (C % 8 == 0,
- * C <= 256), 1 = LDS tile kernel (other C % 32 == 0), 0 = register-window kernel. */
+/* Which forward kernel runs for the shape: 1 = LDS tile kernel (C % 32 == 0),
+ * 0 = register-window kernel; 2 = whole-pixel span kernel, only with the tuning knob
+ * ACCUNET_DW_SPAN bit 2 set (off by default) and then for C % 8 == 0, C/4 <= 64. */
 int accunet_dw3x3_variant(int B, int H, int W, int C);
 int accunet_dw3x3_fwd(const void* x, const float* wt, const float* bias, const float* sc,
                       const float* sh, int act, int flip, void* z, double* stats, int B, int H,

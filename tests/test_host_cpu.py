@@ -23,7 +23,7 @@ from accunet.model import VARIANTS  # noqa: E402
 
 def header_symbols():
     h = open(os.path.join(ROOT, "include", "accunet.h")).read()
-    return sorted(set(re.findall(r"\b(?:int|size_t)\s+(accunet_\w+)\s*\(", h)))
+    return sorted(set(re.findall(r"\b(?:int|size_t|long long)\s+(accunet_\w+)\s*\(", h)))
 
 
 def test_library_loads_and_exports_every_header_symbol():
@@ -285,6 +285,11 @@ def test_abi_host_side_contract_without_a_device():
     assert lib.accunet_stream_ticket_bank(fake, 2) == -2  # out of range
     assert lib.accunet_stream_ticket_bank(fake, -1) == -2
     assert lib.accunet_stream_ticket_bank(None, 1) == -2  # null stream is always bank 0
+    assert lib.accunet_stream_ticket_unregister(fake) == 0  # the fake handle leaves the table
+    assert lib.accunet_stream_ticket_unregister(fake) == -2  # no longer registered
+    assert lib.accunet_stream_ticket_unregister(None) == -2
+    # the library was built from this header (the binding refuses any other)
+    assert lib.accunet_abi_hash() == _lib.header_abi_hash()
     # bz without its BatchNorm state / statistics buffer: rejected before any launch
     one = ctypes.c_void_p(16)
     assert lib.accunet_dw3x3_fwd(one, one, None, None, None, 0, 1, one, None, 1, 8, 8, 32,

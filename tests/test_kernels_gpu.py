@@ -4,8 +4,10 @@ ACC_UNet/ACC_UNet.py:240-247,273-275, and ChannelSELayer :37-49), called through
 the C ABI (accunet.kern) so every tile variant / fallback path is exercised:
     dw3x3: forward / data gradient on the LDS-tiled TCQ=8 / TCQ=16 kernels
            (C % 32 == 0) or the register-window fallback (incl. cnv11's C = 9); the
-           weight gradient on the whole-pixel span kernel (C % 8 == 0, C <= 256; 256-
-           and 512-thread blocks, ragged spans and row bands) or the tile kernels."""
+           weight gradient on the whole-pixel span kernel (C % 8 == 0, C <= 128:
+           256-thread blocks, ragged spans and row bands) or the tile kernels. The
+           span FORWARD kernel (ACCUNET_DW_SPAN bit 2, off by default; 256- and 512-
+           thread blocks) runs the same checks in a child process with the knob set."""
 import os
 import sys
 
@@ -35,8 +37,8 @@ DW_SHAPES = [
     (1, 13, 35, 32),     # ragged everything
     (3, 8, 8, 128),      # W < TP / PX
     (1, 13, 35, 96),     # wgrad span, ragged H (13) and W (35 = 3 x 10 + 5)
-    (2, 9, 21, 192),     # wgrad span, 512 threads (PX 10)
-    (1, 8, 17, 256),     # wgrad span, 512 threads (PX 8)
+    (2, 9, 21, 192),     # tile kernels (span forward knob: 512 threads, PX 10)
+    (1, 8, 17, 256),     # tile kernels (span forward knob: 512 threads, PX 8)
     (2, 6, 300, 8),      # register kernel; wgrad span with 2 quads per pixel (PX 128)
     (2, 16, 24, 384),    # TCQ 8 tile (C > 256, wgrad too)
     (2, 16, 16, 320),    # TCQ 16 tile (W <= 16)
@@ -93,6 +95,28 @@ def test_dw3x3_fwd_stats_wgrad_vs_fp64(B, H, W, C, pro):
     assert (dw.double().cpu() - gw).abs().max().item() <= 1e-5 * gw.abs().max().item() + 1e-5
     gb = b_req.grad
     assert (db.double().cpu() - gb).abs().max().item() <= 1e-5 * gb.abs().max().item() + 1e-5
+
+
+def test_dw3x3_span_forward_knob_vs_fp64():
+    """The span forward / data-gradient kernel ships behind ACCUNET_DW_SPAN bit 2 (read
+    once per process by the library): a child process with ACCUNET_DW_SPAN=3 runs the
+    forward + statistics + flipped-kernel + weight-gradient checks above on shapes that
+    select it with 256-thread (C/4 <= 32) and 512-thread (C/4 33..64) blocks."""
+    import subprocess
+    code = (
+        "import sys; sys.path.insert(0, %r); import test_kernels_gpu as T\n"
+        "from accunet import _lib\n"
+        "lib = _lib.load()\n"
+        "for (B, H, W, C) in [(2, 16, 16, 96), (1, 13, 35, 96), (2, 6, 300, 8), (2, 9, 21, 192),\n"
+        "                     (1, 8, 17, 256), (2, 24, 40, 64)]:\n"
+        "    assert lib.accunet_dw3x3_variant(B, H, W, C) == 2, (B, H, W, C)\n"
+        "    for pro in (False, True):\n"
+        "        T.test_dw3x3_fwd_stats_wgrad_vs_fp64(B, H, W, C, pro)\n"
+        "print('SPAN_OK')\n") % HERE
+    env = dict(os.environ, ACCUNET_DW_SPAN="3")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=240, cwd=HERE)
+    assert r.returncode == 0 and "SPAN_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
 
 
 @pytest.mark.parametrize("B,H,C", [(4, 16, 64), (2, 8, 32), (16, 32, 256), (3, 5, 40)])
