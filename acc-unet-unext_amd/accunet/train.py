@@ -65,14 +65,21 @@ class _GraphBuckets:
     world > 1; see the module docstring). Built before capture; its hooks run only
     while the backward is being captured."""
 
-    def __init__(self, params, bucket_mb, device):
+    def __init__(self, params, bucket_mb, device, comm_dtype=None):
         self.params = params
         total = sum(p.numel() for p in params)
         self.flat = torch.zeros(total, dtype=torch.float32, device=device)
-        self.views, offs, o = [], [], 0
+        # comm_dtype bf16: the buckets travel as bf16 (half the bytes over xGMI; the
+        # gradients are rounded once when packed, RCCL sums in bf16) and are widened back
+        # into the fp32 views the optimizer reads, bucket by bucket, behind each reduce
+        self.comm_dtype = comm_dtype
+        self.wire = (torch.zeros(total, dtype=comm_dtype, device=device)
+                     if comm_dtype not in (None, torch.float32) else self.flat)
+        self.views, self.wviews, offs, o = [], [], [], 0
         for p in params:
             offs.append(o)
             self.views.append(self.flat[o:o + p.numel()].view_as(p))
+            self.wviews.append(self.wire[o:o + p.numel()].view_as(p))
             o += p.numel()
         self.buckets = cut_buckets([p.numel() for p in params], bucket_mb)
         self.range = [(min(offs[i] for i in b), max(offs[i] + params[i].numel() for i in b))
@@ -89,7 +96,7 @@ class _GraphBuckets:
         self._sealed[k] = True
         live = [i for i in self.buckets[k] if self.params[i].grad is not None]
         if live:
-            torch._foreach_copy_([self.views[i] for i in live], [self.params[i].grad for i in live])
+            torch._foreach_copy_([self.wviews[i] for i in live], [self.params[i].grad for i in live])
         kern.GraphEvent.mark(k)
 
     def _hook(self, i):
@@ -124,17 +131,24 @@ class _GraphBuckets:
         """enqueue every bucket's all-reduce behind its event (no host wait for RCCL)"""
         nccl = dist.get_backend(pg) == "nccl"
         main = torch.cuda.current_stream()
+        narrow = self.wire is not self.flat
         if not nccl:  # gloo (tests): host-synchronous collectives on finished buckets
             for k, (lo, hi) in enumerate(self.range):
                 self.events[k].synchronize()
-                all_reduce_mean(self.flat[lo:hi], pg)
+                all_reduce_mean(self.wire[lo:hi], pg)
+                if narrow:
+                    self.flat[lo:hi].copy_(self.wire[lo:hi])
             return
         works = []
         with torch.cuda.stream(self.stream):
             for k, (lo, hi) in enumerate(self.range):
                 self.events[k].wait(self.stream)
-                works.append(dist.all_reduce(self.flat[lo:hi], op=dist.ReduceOp.AVG, group=pg,
-                                             async_op=True))
+                w = dist.all_reduce(self.wire[lo:hi], op=dist.ReduceOp.AVG, group=pg,
+                                    async_op=True)
+                if narrow:  # widen this bucket on the side stream once RCCL is done with it
+                    w.wait()
+                    self.flat[lo:hi].copy_(self.wire[lo:hi])
+                works.append(w)
         for w in works:  # the main stream (Adam) waits on RCCL's stream
             w.wait()
         main.wait_stream(self.stream)
@@ -142,7 +156,8 @@ class _GraphBuckets:
 
 class TrainStep:
     def __init__(self, model, lr=1e-3, reducer=None, dice_weight=0.5, bce_weight=0.5,
-                 graph=False, process_group=None, precision=None, bucket_mb=16.0):
+                 graph=False, process_group=None, precision=None, bucket_mb=16.0,
+                 comm_dtype=None):
         if graph and reducer is not None:
             raise ValueError("graph mode does its own single-bucket all-reduce; pass no reducer")
         if precision is not None:  # "fp32" / "bf16": see ACC_UNet.set_precision
@@ -164,6 +179,13 @@ class TrainStep:
         self.opt = FusedAdam(self.params, lr=lr)
         self._g = None
         self.bucket_mb = bucket_mb
+        # graph-mode DP gradient wire format: None / torch.float32, or torch.bfloat16
+        # (BASELINE configs[2]: 33.5 MB instead of 67 MB per step over xGMI)
+        if comm_dtype == "bf16":
+            comm_dtype = torch.bfloat16
+        if comm_dtype not in (None, torch.float32, torch.bfloat16):
+            raise ValueError(f"comm_dtype: None, torch.float32 or torch.bfloat16, got {comm_dtype}")
+        self.comm_dtype = comm_dtype
         if graph and self.dp:
             # identical replicas to start from (what DDP / GradBucketReducer do at wrap time)
             with torch.no_grad():
@@ -220,7 +242,8 @@ class TrainStep:
 
         self._buckets = None
         if self.dp:
-            self._buckets = _GraphBuckets(self.params, self.bucket_mb, self._x.device)
+            self._buckets = _GraphBuckets(self.params, self.bucket_mb, self._x.device,
+                                          self.comm_dtype)
             self._buckets.stream = torch.cuda.Stream()
             self._buckets.arm()
         g = torch.cuda.CUDAGraph(keep_graph=self._buckets is not None)

@@ -73,6 +73,9 @@ def parse():
                     help="activation storage: fp32 (configs[1], the reference's precision) or "
                          "bf16 (configs[2]: bf16 activations, fp32 master weights / Adam / "
                          "BN statistics)")
+    ap.add_argument("--comm-dtype", default=None, choices=["fp32", "bf16"],
+                    help="gradient all-reduce wire format for N > 1 (default: bf16 with --dtype "
+                         "bf16, else fp32)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true",
                     help="launch every kernel from Python (default: replay one HIP graph per step)")
@@ -273,7 +276,10 @@ def main():
         reducer = adist.GradBucketReducer(model) if world > 1 else None
         step = TrainStep(model, lr=1e-3, reducer=reducer, precision=prec)
     else:
-        step = TrainStep(model, lr=1e-3, graph=True, precision=prec)
+        # configs[2]: bf16 activations AND bf16 gradient buckets over xGMI (--comm-dtype)
+        wire = args.comm_dtype or ("bf16" if args.dtype == "bf16" else "fp32")
+        step = TrainStep(model, lr=1e-3, graph=True, precision=prec,
+                         comm_dtype="bf16" if wire == "bf16" else None)
 
     g = torch.Generator(device="cpu").manual_seed(1000 + rank)
     B, S = args.batch, args.size
@@ -328,7 +334,10 @@ def main():
                    "model": ("UNext (1.47M)" if unext else
                              "ACC_UNet (16.77M)" if args.variant == "canonical" else args.variant),
                    "global_batch": B * world, "per_gpu_batch": B, "image": [3, S, S],
-                   "parallelism": f"dp{world}"},
+                   "parallelism": f"dp{world}",
+                   "grad_allreduce": (None if world == 1 or args.eager else
+                                      args.comm_dtype or ("bf16" if args.dtype == "bf16"
+                                                          else "fp32"))},
         "final_loss": float(loss.item()),
         "ranks_seen": world,
         "ms_per_step_per_rank": [round(1000.0 * t / args.steps, 3) for t in per_rank],

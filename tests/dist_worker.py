@@ -11,6 +11,8 @@ data-parallel code path is the one bench.py runs over RCCL on a node:
      with backward through post-accumulate-grad hooks), same start, same data.
   3. the epoch loop: Trainer(reducer=GradBucketReducer) over the same batches.
   4./5. graph and eager again in bf16 storage (BASELINE configs[2]'s precision).
+  6. graph mode with bf16 gradient buckets on the wire (TrainStep(comm_dtype="bf16"),
+     fp32 storage): within bf16 rounding of the fp32-bucket run.
 Checks: parameters identical on both ranks after each mode (bitwise), graph and eager
 identical to each other (bitwise, fp32 and bf16: the same kernels in the same order,
 and a world-2 sum is order-free), the epoch loop equal to eager, and the parameters
@@ -41,6 +43,9 @@ def run(mode, sd, data, dev):
     m.load_state_dict(sd)
     m = m.to(dev).train()
     prec = None
+    wire = None
+    if mode.endswith("_wire16"):
+        mode, wire = mode[:-7], "bf16"
     if mode.endswith("_bf16"):
         mode, prec = mode[:-5], "bf16"
     if mode == "trainer":  # the epoch loop with the bucketed reducer (Trainer(reducer=))
@@ -51,7 +56,8 @@ def run(mode, sd, data, dev):
         torch.cuda.synchronize()
         return flat_params(m), [h["loss"] for h in tr.history]
     if mode == "graph":
-        step = TrainStep(m, lr=1e-3, graph=True, bucket_mb=0.25, precision=prec)
+        step = TrainStep(m, lr=1e-3, graph=True, bucket_mb=0.25, precision=prec,
+                         comm_dtype=wire)
     else:
         step = TrainStep(m, lr=1e-3, reducer=adist.GradBucketReducer(m, bucket_mb=0.25),
                          precision=prec)
@@ -62,6 +68,8 @@ def run(mode, sd, data, dev):
     if mode == "graph":
         nb = len(step._buckets.buckets)
         assert nb >= 3, f"graph mode ran {nb} bucket(s); the multi-bucket path needs >= 3"
+        want = torch.bfloat16 if wire else torch.float32
+        assert step._buckets.wire.dtype == want, step._buckets.wire.dtype
         print(f"graph{'_' + prec if prec else ''}: {nb} buckets", flush=True)
     return flat_params(m), losses
 
@@ -78,7 +86,7 @@ def main():
     data = [(torch.randn(2, 3, 32, 32, generator=g).to(dev),
              (torch.rand(2, 1, 32, 32, generator=g) < 0.3).float().to(dev)) for _ in range(3)]
     out = {}
-    for mode in ("graph", "eager", "trainer", "graph_bf16", "eager_bf16"):
+    for mode in ("graph", "eager", "trainer", "graph_bf16", "eager_bf16", "graph_wire16"):
         p, losses = run(mode, sd, data, dev)
         other = [torch.empty_like(p) for _ in range(world)]
         dist.all_gather(other, p)
@@ -98,6 +106,14 @@ def main():
     d = float((out["trainer"][0] - out["eager"][0]).abs().max())
     print(f"rank {rank} trainer vs eager max|dp| {d:.3e}", flush=True)
     assert d < 1e-5, d
+    # bf16 buckets: every gradient rounded once to bf16 and summed in bf16; after 3 Adam
+    # steps (lr 1e-3, updates ~lr * g / |g|) the parameters sit within a few bf16
+    # relative roundings of an lr-sized update from the fp32-bucket run
+    d = float((out["graph_wire16"][0] - out["graph"][0]).abs().max())
+    dl = max(abs(a - b) for a, b in zip(out["graph_wire16"][1], out["graph"][1]))
+    print(f"rank {rank} graph_wire16 vs graph max|dp| {d:.3e} max|dloss| {dl:.3e}", flush=True)
+    assert d <= 3 * 1e-3 * 2 ** -4, d
+    assert dl <= 1e-3 * abs(out["graph"][1][-1]) + 1e-6, dl
     dist.barrier()
     dist.destroy_process_group()
     if rank == 0:
