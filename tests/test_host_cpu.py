@@ -335,3 +335,23 @@ def test_bench_launcher_argument_logic(monkeypatch):
     assert ok == 0
     assert bench.relay([sys.executable, "-c", "import sys; sys.exit(3)"]) == 3
     assert bench.relay([sys.executable, "-c", "print('no line')"]) == 1
+
+
+def test_host_abi_under_address_sanitizer():
+    """the host side of the C ABI built with -fsanitize=address (host pass
+    only; acc-unet-unext_amd/Makefile target `asan`) and driven by tools/asan_abi,
+    which calls every entry point that answers without a device: geometry and workspace
+    queries over the BASELINE shapes and ragged ones, the 64-entry ticket-bank table
+    (filled, overflowed, unregistered in every position), the ABI hash, and the
+    argument checks that return -2 before any launch. AddressSanitizer aborts on any
+    invalid host access; the driver exits 0 only if every result matches the header."""
+    import subprocess
+    root = os.path.dirname(HERE)
+    exe = os.path.join(root, "tools", "asan_abi")
+    r = subprocess.run(["make", "-C", os.path.join(root, "acc-unet-unext_amd"), "-j8", "asan"],
+                       capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0 and "0 failure(s)" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "AddressSanitizer" not in r.stderr, r.stderr[-4000:]
