@@ -653,6 +653,263 @@ dw3x3_tile_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
   }
 }
 
+// ----------------------------------------------------------------------------
+// K1 with LDS-DMA staging (fp32, 32-channel tiles, no BN-backward epilogue; the
+// default forward of those shapes, ACCUNET_DW_DMA). Same tile geometry and strips as
+// dw3x3_tile_fwd_kernel, but input rows go HBM -> LDS by `global_load_lds_dwordx4`
+// (no VGPR destination), so the prefetch depth is bounded by LDS, not by registers:
+// a 12-slot ring holds three 4-row chunks -- the one being computed, the next (landed,
+// being activated) and the one after (in flight) -- 52 KB per block, 3 blocks per CU,
+// so ~100 KB of input rows per CU stay in flight (the register-staged strip keeps one
+// chunk, ~52 KB per CU).
+// Ring row layout (272 float4): pixels 0..31 of the tile x 8 quads, then the left and
+// right halo pixels x 8 quads. One wave owns one row of a chunk: 4 DMA instructions
+// of 1 KB (the interior, lane-linear) + 1 of 16 lanes (the two halo pixels).
+// Out-of-image pixels and rows load a clamped in-image address and are zeroed when
+// the wave that loaded them applies the prologue (BN scale/shift + LeakyReLU) in
+// place, after its own DMA has landed (counted vmcnt) and before the barrier that
+// publishes the chunk. The 3x3 window is a pair of rolling row accumulators carried
+// across chunks (each input row read once per thread: left, centre, right quad), in
+// the same FMA order as a whole-window sum (bias, then taps row-major).
+// ----------------------------------------------------------------------------
+// s_waitcnt vmcnt(N) with every other counter left alone (gfx9 encoding)
+template <int N>
+ACC_DEV void dw_wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+#define DWD_ROW 272
+#define DWD_SLOTS 12
+
+template <bool NT>
+ACC_DEV void dwd_dma16(const float* src, unsigned lds_byte) {
+  unsigned keep;
+  if (NT)
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src), "s"(lds_byte)
+                 : "memory");
+  else
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src), "s"(lds_byte)
+                 : "memory");
+}
+
+template <bool NT>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
+dw3x3_dma_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
+                     const float* __restrict__ bias, const float* __restrict__ sc,
+                     const float* __restrict__ sh, int act, int flip, float* __restrict__ z,
+                     double* __restrict__ stats, DwTGeom g) {
+  constexpr int TCQ = 8, TP = 32, CR = 4;
+  __shared__ float4 ring[DWD_SLOTS * DWD_ROW];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int q = tid % TCQ, p = tid / TCQ;
+  int t = dw_tile_id(g);
+  int cg = blockIdx.y;
+  if (g.cgf) {
+    cg = t % g.cgf;
+    t /= g.cgf;
+  }
+  const int srow = g.cgf ? t : (int)blockIdx.x;
+  const int c0 = cg * TCQ * 4;
+  const int c = c0 + 4 * q;
+  const int tw = t % g.tilesW;
+  t /= g.tilesW;
+  const int th = t % g.tilesH;
+  const int b = t / g.tilesH;
+  const int hbeg = th * DW_TR * g.rch, w0 = tw * TP;
+  const int hend = min(g.H, hbeg + DW_TR * g.rch);
+  const int nch = (hend - hbeg + CR - 1) / CR;
+  const float* ximg = x + (long)b * g.H * g.W * g.C;
+  const long img = (long)b * g.H * g.W * g.C;
+  const __amdgpu_buffer_rsrc_t rz = acc_rsrc(z + img, (unsigned)(g.H * g.W * g.C * 4));
+  const unsigned ring_lds =
+      (unsigned)(size_t)(__attribute__((address_space(3))) float4*)ring;
+  // the DMA lane map: interior piece i (0..3): pixel 8 i + lane / 8, quad lane % 8;
+  // halo piece (lanes 0..15): pixel -1 (lanes 0..7) / 32 (lanes 8..15)
+  const int lq = lane & 7;
+  const int hip = lane < 8 ? -1 : TP;
+  // chunk j >= -1 = input rows hbeg + 1 + 4j .. +3 (j = -1: rows hbeg-3 .. hbeg, of which
+  // hbeg-1 and hbeg start the window); wave wv owns row hbeg + 1 + 4j + wv, ring slot
+  // (4 (j + 1) + wv) % 12
+  auto issue = [&](int j) {
+    const int R = hbeg + 1 + CR * j + wv;
+    const int Rl = max(0, min(R, min(hend, g.H - 1)));  // rows past the strip: a re-read
+    const int slot = (CR * (j + 1) + wv) % DWD_SLOTS;
+    const float* rowp = ximg + (long)Rl * g.W * g.C + c0 + 4 * lq;
+    const unsigned base = ring_lds + (unsigned)(slot * DWD_ROW) * 16u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int wp = min(w0 + 8 * i + (lane >> 3), g.W - 1);
+      dwd_dma16<NT>(rowp + (long)wp * g.C, base + i * 1024u);
+    }
+    if (lane < 16) {
+      const int wp = max(0, min(w0 + hip, g.W - 1));
+      dwd_dma16<NT>(rowp + (long)wp * g.C, base + 4096u);
+    }
+  };
+  const bool pro = sc != nullptr;
+  const float4 ps = pro ? ld4(sc + c0 + 4 * lq) : make_float4(1.f, 1.f, 1.f, 1.f);
+  const float4 pb = pro ? ld4(sh + c0 + 4 * lq) : make_float4(0.f, 0.f, 0.f, 0.f);
+  // prologue (BN+act, in-image only; zero padding after the activation) of the wave's
+  // own pieces of chunk j, in place
+  auto activate = [&](int j) {
+    const int R = hbeg + 1 + CR * j + wv;
+    const int slot = (CR * (j + 1) + wv) % DWD_SLOTS;
+    const bool rin = R >= 0 && R < g.H;
+    float4* rw = ring + slot * DWD_ROW;
+    auto fix = [&](float4 v, bool in) {
+      if (pro) {
+        v.x = apply_act(v.x * ps.x + pb.x, act);
+        v.y = apply_act(v.y * ps.y + pb.y, act);
+        v.z = apply_act(v.z * ps.z + pb.z, act);
+        v.w = apply_act(v.w * ps.w + pb.w, act);
+      }
+      return in ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = 64 * i + lane;
+      rw[e] = fix(rw[e], rin && w0 + 8 * i + (lane >> 3) < g.W);
+    }
+    if (lane < 16) {
+      const int wp = w0 + hip;
+      rw[256 + lane] = fix(rw[256 + lane], rin && wp >= 0 && wp < g.W);
+    }
+  };
+  issue(-1);
+  issue(0);
+  issue(1);
+  // weights: the quad's 4 channels x 9 taps are 36 contiguous floats of wt ([C][9])
+  float k[9][4], bi[4];
+  {
+    float wvv[36];
+#pragma unroll
+    for (int e = 0; e < 9; ++e) {
+      const float4 w4 = ld4(wt + c * 9 + 4 * e);
+      wvv[4 * e] = w4.x; wvv[4 * e + 1] = w4.y; wvv[4 * e + 2] = w4.z; wvv[4 * e + 3] = w4.w;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int tp = 0; tp < 9; ++tp) k[tp][j] = wvv[j * 9 + (flip ? 8 - tp : tp)];
+    const float4 b4 = bias ? ld4(bias + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    bi[0] = b4.x; bi[1] = b4.y; bi[2] = b4.z; bi[3] = b4.w;
+  }
+  // everything issued so far has landed (chunks -1, 0, 1 and the weights): activate the
+  // two chunks the window starts from, publish, read the first two rows, and let every
+  // wave pass them before chunk -1's slots are refilled
+  __builtin_amdgcn_s_waitcnt(0);
+  activate(-1);
+  activate(0);
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+  __builtin_amdgcn_s_barrier();
+  // reads the thread's 3 quads (tile pixels p-1, p, p+1) of input row R (chunk j, row rr)
+  auto rdrow = [&](int slot, float (&row)[3][4]) {
+    const float4* rw = ring + slot * DWD_ROW;
+    const int e = p * TCQ + q;
+    const float4 l = rw[p == 0 ? 256 + q : e - TCQ];
+    const float4 m = rw[e];
+    const float4 r = rw[p == TP - 1 ? 264 + q : e + TCQ];
+    row[0][0] = l.x; row[0][1] = l.y; row[0][2] = l.z; row[0][3] = l.w;
+    row[1][0] = m.x; row[1][1] = m.y; row[1][2] = m.z; row[1][3] = m.w;
+    row[2][0] = r.x; row[2][1] = r.y; row[2][2] = r.z; row[2][3] = r.w;
+  };
+  float a0[4], a1[4];
+  {
+    float row[3][4];
+    rdrow(2, row);  // input row hbeg - 1
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float acc = bi[j];
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) acc = fmaf(k[dx][j], row[dx][j], acc);
+      a0[j] = acc;
+    }
+    rdrow(3, row);  // input row hbeg
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float acc = a0[j], nxt = bi[j];
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) {
+        acc = fmaf(k[3 + dx][j], row[dx][j], acc);
+        nxt = fmaf(k[dx][j], row[dx][j], nxt);
+      }
+      a0[j] = acc;
+      a1[j] = nxt;
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_s_barrier();
+  double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+  const int w = w0 + p;
+  const bool wok = w < g.W;
+  for (int kc = 0; kc < nch; ++kc) {
+    issue(kc + 2);  // into chunk kc-1's slots, free since the last barrier
+    const int r0 = hbeg + CR * kc;
+    const int nr = min(CR, hend - r0);
+    float c1[4] = {0.f, 0.f, 0.f, 0.f}, c2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < CR; ++r) {
+      const bool on = wok && r < nr;
+      float row[3][4];
+      rdrow((CR * (kc + 1) + r) % DWD_SLOTS, row);
+      float o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float acc = a0[j], mid = a1[j], nxt = bi[j];
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) {
+          acc = fmaf(k[6 + dx][j], row[dx][j], acc);
+          mid = fmaf(k[3 + dx][j], row[dx][j], mid);
+          nxt = fmaf(k[dx][j], row[dx][j], nxt);
+        }
+        a0[j] = mid;
+        a1[j] = nxt;
+        o[j] = acc;
+        const float am = on ? acc : 0.f;
+        c1[j] += am;
+        c2[j] = fmaf(am, am, c2[j]);
+      }
+      const unsigned off = on ? (unsigned)((((r0 + r) * g.W + w) * g.C + c) * 4) : ACC_OOB;
+      bufq_st<2>(rz, off, make_float4(o[0], o[1], o[2], o[3]), (float*)nullptr);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      s1[j] += (double)c1[j];
+      s2[j] += (double)c2[j];
+    }
+    // chunk kc+1's DMA (issued one iteration ago) has landed once only the 5 DMA pieces
+    // of chunk kc+2 and the 4 + 4 stores of chunks kc-1, kc are younger (chunk 1 was
+    // drained in the prologue)
+    if (kc == 0) dw_wait_vm<9>();
+    else dw_wait_vm<13>();
+    activate(kc + 1);
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_s_barrier();
+  }
+  // the ring becomes the reduction buffer: no DMA may still be writing it
+  __builtin_amdgcn_s_waitcnt(0);
+  if (stats) {
+    __syncthreads();
+    double v[8] = {s1[0], s1[1], s1[2], s1[3], s2[0], s2[1], s2[2], s2[3]};
+    if (block_slot_reduce<TCQ, 8, double>(v, reinterpret_cast<double*>(ring))) {
+      const long row = (long)srow * 2 * g.C;
+      const int cc = c0 + 4 * threadIdx.x;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        stats[row + cc + j] = v[j];
+        stats[row + g.C + cc + j] = v[4 + j];
+      }
+    }
+  }
+}
+
 template <int TCQ, typename T>
 __global__ void __launch_bounds__(256)
 dw3x3_tile_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dz,
@@ -1230,6 +1487,18 @@ static int dw_cgfast() {
   return v;
 }
 
+// K1 staging: 1 = LDS-DMA ring (dw3x3_dma_fwd_kernel) for the fp32 32-channel tiles
+// without a BN-backward epilogue, 0 = the register-staged strip for every shape
+// (ACCUNET_DW_DMA, tuning knob / A/B)
+static int dw_dma() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ACCUNET_DW_DMA");
+    v = e ? atoi(e) : 0;
+  }
+  return v;
+}
+
 static int dw_rch_max() {
   static int v = -1;
   if (v < 0) {
@@ -1357,6 +1626,15 @@ extern "C" int accunet_dw3x3_fwd(const void* x, const float* wt, const float* bi
     if (dw_cgfast() && grid.y > 1) {
       tg.cgf = (int)grid.y;
       grid = dim3(grid.x * grid.y, 1);
+    }
+    if (dt == ACC_F32 && tcq == 8 && !bz && dw_dma()) {
+      if (tg.ntl)
+        hipLaunchKernelGGL((dw3x3_dma_fwd_kernel<true>), grid, dim3(256), 0, s, (const float*)x, wt,
+                           bias, sc, sh, act, flip, (float*)z, stats, tg);
+      else
+        hipLaunchKernelGGL((dw3x3_dma_fwd_kernel<false>), grid, dim3(256), 0, s, (const float*)x,
+                           wt, bias, sc, sh, act, flip, (float*)z, stats, tg);
+      return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
     }
     // both fixed-function choices (channel-group width, nt loads) are template arguments
     auto launch = [&](auto tag, auto tcqc, auto bnbc, auto auxc) {

@@ -432,6 +432,9 @@ struct EpiRow {
 // by a vmcnt(0) (the generic path pays about one L2/HBM round trip per chunk).
 // Descriptors cover one block's rows (wave-uniform bases from m0), so tensors of
 // any size stay within 32-bit offsets.
+#ifndef GEMM_PYR_EC
+#define GEMM_PYR_EC 1
+#endif
 template <typename TC, int EPI, int WM, int TM, int TN>
 ACC_DEV void gemm_epilogue_vec(const GemmParams& p, floatx16 (&acc)[TM][TN], float* smem, int m0,
                                int n0) {
@@ -444,7 +447,9 @@ ACC_DEV void gemm_epilogue_vec(const GemmParams& p, floatx16 (&acc)[TM][TN], flo
   constexpr int SC = BN + 4;
   constexpr int NR = PR / RPP;
   constexpr bool LOADS = (EPI & (EPI_BNB | EPI_PYR | EPI_UPS)) != 0;
-  constexpr int EC = LOADS ? 2 : NR;  // rows per chunk; two chunks of operands in flight
+  // rows per chunk; two chunks of operands in flight (the BN-backward + pyramid epilogue
+  // gathers 6 operands per row: one row per chunk keeps it within 3 waves per SIMD)
+  constexpr int EC = ((EPI & EPI_PYR) && (EPI & EPI_BNB)) ? GEMM_PYR_EC : LOADS ? 2 : NR;
   constexpr int NCH = NR / EC;
   constexpr int NT = TM * NCH;        // chunks of the whole tile
   constexpr int SZ = (int)sizeof(TC);

@@ -64,8 +64,12 @@ ACC_DEV void gg_wait_vm() {
 template <int R>
 ACC_DEV int kmaj_swz(int k) { return R >= 64 ? ((k >> 2) & 1) << 5 : 0; }
 
+#ifndef GG_PYR_WAVES
+#define GG_PYR_WAVES 3
+#endif
 template <int AMODE, int BMODE, int PRO_A, int PRO_B, int WM, int TM, int TN, int EPI>
 __global__ void __launch_bounds__(GEMM_THREADS)
+__attribute__((amdgpu_waves_per_eu(((EPI & EPI_PYR) && (EPI & EPI_BNB)) ? GG_PYR_WAVES : 1)))
 gemm_f32g_kernel(const GemmParams p) {
   constexpr int WN = 4 / WM;
   constexpr int BM = WM * TM * 32;

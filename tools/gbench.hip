@@ -64,6 +64,10 @@ int main(int argc, char** argv) {
       {"cnv32 hnc fwd      262144x128x384 NT proA stats", 262144, 128, 384, AMODE_ROW, BMODE_NT, PRO_AFFINE_LRELU, 1, 0, 0, 0, 0},
       {"cnv72 x dgrad       65536x4352x128 NN", 65536, 4352, 128, AMODE_ROW, BMODE_NN, PRO_NONE, 0, 0, 0, 0, 0},
       {"cnv72 pyr dgrad     65536x4352x128 NN bnb+pyr", 65536, 4352, 128, AMODE_ROW, BMODE_NN, PRO_NONE, 1, 0, 64, 64, 0, 1},
+      {"cnv91 pyr dgrad   1048576x192x64 NN bnb+pyr", 1048576, 192, 64, AMODE_ROW, BMODE_NN, PRO_NONE, 1, 0, 256, 256, 0, 1},
+      {"cnv81 pyr dgrad    262144x192x64 NN bnb+pyr", 262144, 192, 64, AMODE_ROW, BMODE_NN, PRO_NONE, 1, 0, 128, 128, 0, 1},
+      {"cnv92 pyr dgrad   1048576x96x32 NN bnb+pyr", 1048576, 96, 32, AMODE_ROW, BMODE_NN, PRO_NONE, 1, 0, 256, 256, 0, 1},
+      {"cnv32 pyr dgrad    262144x384x128 NN bnb+pyr", 262144, 384, 128, AMODE_ROW, BMODE_NN, PRO_NONE, 1, 0, 128, 128, 0, 1},
       {"cnv72 x wgrad       4352x128x65536 COL NN split", 4352, 128, 65536, AMODE_COL, BMODE_NN, PRO_NONE, 0, 1, 0, 0, 0},
       {"rspth1 3x3 fwd   1048576x32x288 SHIFT3 stats", 1048576, 32, 288, AMODE_SHIFT3, BMODE_NT, PRO_NONE, 1, 0, 256, 256, 32},
       {"rspth1 3x3 wgrad    32x288x1048576 COL SHIFT3 split", 32, 288, 1048576, AMODE_COL, BMODE_NN_SHIFT3, PRO_NONE, 0, 1, 256, 256, 32},

@@ -264,6 +264,84 @@ __global__ void __launch_bounds__(256) strip_lds(const float* x, float* z) {
   }
 }
 
+
+// the strip structure with D chunks of register prefetch in flight (D = 1 is
+// strip_lds): rows for chunk kc + 1 + D are issued at chunk kc, parked at the end of
+// chunk kc + D - 1; the 10-slot ring is unchanged, so LDS per block stays 43.5 KB.
+// SR = strip rows (32: 3072 blocks, the K1 default; 128: 768 blocks)
+template <int SR, int D, int AUX>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
+strip_lds_d(const float* x, float* z) {
+  constexpr int IP = 34, IR = 10, CR = 4, NCH = SR / CR;
+  constexpr int N4 = IR * IP * 8, NL = (N4 + 255) / 256;
+  constexpr int N8 = CR * IP * 8, NL8 = (N8 + 255) / 256;
+  static_assert(NCH % D == 0, "chunks per strip divisible by D");
+  __shared__ u32x4 ring[N4];
+  int bid = blockIdx.x;
+  const int per = gridDim.x >> 3;
+  bid = (bid & 7) * per + (bid >> 3);
+  const int cg = bid % 3;
+  int t = bid / 3;
+  const int tw = t % 8;
+  t /= 8;
+  const int th = t % (H / SR);
+  const int b = t / (H / SR);
+  const int c0 = cg * 32, hbeg = th * SR;
+  const auto rx = rsrc(x + (long)b * H * W * C, IMG), rz = rsrc(z + (long)b * H * W * C, IMG);
+  auto fetch = [&](u32x4* v, int nl, int hA, int n) {
+#pragma unroll
+    for (int k = 0; k < nl; ++k) {
+      const int i = threadIdx.x + 256 * k;
+      const int q = i % 8, rp = i / 8, pp = rp % IP, r = rp / IP;
+      const int hh = hA + r, ww = tw * 32 - 1 + pp;
+      const bool in = i < n && hh >= 0 && hh < H && ww >= 0 && ww < W;
+      v[k] = ld<AUX>(rx, in ? (unsigned)(((hh * W + ww) * C + c0 + 4 * q) * 4) : OOB);
+    }
+  };
+  auto park = [&](const u32x4* v, int nl, int hA, int n) {
+#pragma unroll
+    for (int k = 0; k < nl; ++k) {
+      const int i = threadIdx.x + 256 * k;
+      if (i < n) {
+        const int q = i % 8, rp = i / 8, pp = rp % IP, r = rp / IP;
+        const int slot = (hA + r - hbeg + 1) % IR;
+        ring[(slot * IP + pp) * 8 + q] = v[k];
+      }
+    }
+  };
+  {
+    u32x4 v[NL];
+    fetch(v, NL, hbeg - 1, N4);
+    park(v, NL, hbeg - 1, N4);
+  }
+  u32x4 nx[D][NL8];
+  // chunks 1 .. D-1 ahead are issued before the loop (rows r0+9+4j for chunk j)
+#pragma unroll
+  for (int j = 0; j + 1 < D; ++j) fetch(nx[j], NL8, hbeg + 9 + CR * j, (j + 2 < NCH + 1) ? N8 : 0);
+  __syncthreads();
+  const int q = threadIdx.x % 8, p = threadIdx.x / 8;
+  for (int kb = 0; kb < NCH; kb += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const int kc = kb + d;
+      const int r0 = hbeg + CR * kc;
+      // issue the rows of chunk kc + D + 1 (r0 + 9 + 4 (D-1) ..) into buffer (d + D - 1) % D
+      const int ahead = kc + D - 1;
+      fetch(nx[(d + D - 1) % D], NL8, hbeg + 9 + CR * ahead, ahead + 1 < NCH ? N8 : 0);
+#pragma unroll
+      for (int r = 0; r < CR; ++r) {
+        const int slot = (r0 + r - hbeg + 1) % IR;
+        st<AUX>(rz, (((r0 + r) * W + tw * 32 + p) * C + c0 + 4 * q) * 4, ring[(slot * IP + p + 1) * 8 + q]);
+      }
+      if (kc + 1 < NCH) {
+        __syncthreads();
+        park(nx[d], NL8, r0 + 9, N8);
+        __syncthreads();
+      }
+    }
+  }
+}
+
 // cross-lane geometry (a K1 without an LDS halo): a wave = 64 consecutive pixels of one
 // row x NQ channel quads (lane = pixel), walking R rows down the image: each row's NQ
 // quads are loaded once per lane (vertical window in registers), the left / right
@@ -376,6 +454,12 @@ int main(int argc, char** argv) {
   rep("tile_lds R16 nt", [&] { hipLaunchKernelGGL((tile_lds<16, 2>), dim3(B * 16 * 8 * 3), dim3(256), 0, 0, x, z); });
   rep("strip_lds nt (current K1 structure)", [&] { hipLaunchKernelGGL((strip_lds<2>), dim3(B * 2 * 8 * 3), dim3(256), 0, 0, x, z); });
   rep("strip_lds default policy", [&] { hipLaunchKernelGGL((strip_lds<0>), dim3(B * 2 * 8 * 3), dim3(256), 0, 0, x, z); });
+  rep("strip_lds_d SR32 D1 nt", [&] { hipLaunchKernelGGL((strip_lds_d<32, 1, 2>), dim3(B * 8 * 8 * 3), dim3(256), 0, 0, x, z); });
+  rep("strip_lds_d SR32 D2 nt", [&] { hipLaunchKernelGGL((strip_lds_d<32, 2, 2>), dim3(B * 8 * 8 * 3), dim3(256), 0, 0, x, z); });
+  rep("strip_lds_d SR32 D4 nt", [&] { hipLaunchKernelGGL((strip_lds_d<32, 4, 2>), dim3(B * 8 * 8 * 3), dim3(256), 0, 0, x, z); });
+  rep("strip_lds_d SR64 D2 nt", [&] { hipLaunchKernelGGL((strip_lds_d<64, 2, 2>), dim3(B * 4 * 8 * 3), dim3(256), 0, 0, x, z); });
+  rep("strip_lds_d SR128 D2 nt", [&] { hipLaunchKernelGGL((strip_lds_d<128, 2, 2>), dim3(B * 2 * 8 * 3), dim3(256), 0, 0, x, z); });
+  rep("strip_lds_d SR128 D4 nt", [&] { hipLaunchKernelGGL((strip_lds_d<128, 4, 2>), dim3(B * 2 * 8 * 3), dim3(256), 0, 0, x, z); });
   rep("span_reg R8 nt", [&] { hipLaunchKernelGGL((span_reg<8, 2>), dim3(B * 32 * 26), dim3(256), 0, 0, x, z); });
   rep("span_lds R8 nt (span K1 shape)", [&] { hipLaunchKernelGGL((span_lds<8, 2>), dim3(B * 32 * 26), dim3(256), 0, 0, x, z); });
   rep("span_lds R8 nt remap", [&] { hipLaunchKernelGGL((span_lds<8, 2, true>), dim3(B * 32 * 26), dim3(256), 0, 0, x, z); });
