@@ -3,6 +3,7 @@
 Run in the build container only (needs /root/reference):
     python tests/golden/make_golden.py               # every fixture
     python tests/golden/make_golden.py --fullwidth   # only the n_filts=32 ones (6)
+    python tests/golden/make_golden.py --unext       # only the UNeXt ones (7)
 It imports the reference modules from /root/reference (read-only), fills them
 with the oracle's deterministic, version-independent parameters
 (oracle/accunet_oracle.py: det_state_dict), runs them on deterministic inputs
@@ -50,6 +51,81 @@ def ref_models():
 def ref_utils():
     sys.modules.setdefault("cv2", types.ModuleType("cv2"))  # imported, never called (utils.py:9)
     return load_module("ref_utils", os.path.join(REF, "Experiments/utils.py"))
+
+
+def ref_unext(U):
+    """Experiments/nets/UNext.py with import shims for the packages this image lacks.
+    Its forward path is the reference's own code plus torch; what the shims stand for:
+      torchvision (transforms, utils.save_image): imported at :4,8-9, never called;
+      timm.models.layers (:17): to_2tuple (:169-170) restated as timm defines it (an int
+        -> (x, x)); trunc_normal_ (:58,131,184, weight init only, overwritten by
+        load_state_dict) = torch.nn.init.trunc_normal_, the same algorithm; DropPath is
+        only built for drop_path > 0 (:123; UNext's default drop_path_rate is 0), so the
+        shim raises if it is ever constructed;
+      `from utils import *` (:13): Experiments/utils.py itself (cv2 shim as above)."""
+    import torch.nn as nn
+    sys.modules["utils"] = U
+    tv = types.ModuleType("torchvision")
+    tv.transforms = types.ModuleType("torchvision.transforms")
+    tvu = types.ModuleType("torchvision.utils")
+    tvu.save_image = None
+    tv.utils = tvu
+    timm = types.ModuleType("timm")
+    tmod = types.ModuleType("timm.models")
+    layers = types.ModuleType("timm.models.layers")
+
+    class DropPath(nn.Module):
+        def __init__(self, *a, **k):
+            raise RuntimeError("DropPath is not on the path at drop_path_rate 0")
+
+    layers.DropPath = DropPath
+    layers.to_2tuple = lambda x: tuple(x) if isinstance(x, (tuple, list)) else (x, x)
+    layers.trunc_normal_ = nn.init.trunc_normal_
+    timm.models = tmod
+    tmod.layers = layers
+    sys.modules.update({"torchvision": tv, "torchvision.transforms": tv.transforms,
+                        "torchvision.utils": tvu, "timm": timm, "timm.models": tmod,
+                        "timm.models.layers": layers})
+    return load_module("ref_unext", os.path.join(REF, "Experiments/nets/UNext.py")).UNext
+
+
+def unext(U):
+    """7) UNeXt (BASELINE configs[4]; Experiments/nets/UNext.py:201-358), reference-run:
+    2x3x64x64 train fwd + WeightedDiceBCE(0.5, 0.5) + bwd (outputs, loss, gradient
+    summaries, running-stat sums) and eval output, plus the eval output of one
+    1x3x224x224 image (the Cfg5 resolution)."""
+    cls = ref_unext(U)
+    spec = O.unext_param_spec(3, 1)
+    res = {}
+    for name, shape, mode in (("s64", (2, 3, 64, 64), "both"), ("s224", (1, 3, 224, 224), "eval")):
+        m = cls(num_classes=1, input_channels=3, img_size=shape[-1])
+        assert [k for k, _ in spec] == list(m.state_dict().keys())
+        sd = O.det_state_dict(spec, seed=5)
+        x = O.det_input(shape, f"unext-x-{name}")
+        m.load_state_dict(sd)
+        m.eval()
+        with torch.no_grad():
+            res[f"out_eval_{name}"] = m(x).numpy()
+        if mode == "both":
+            mk = O.det_mask((shape[0], 1) + shape[2:], f"unext-mask-{name}", p=0.3)
+            m.load_state_dict(sd)
+            m.train()
+            out = m(x)
+            crit = U.WeightedDiceBCE(dice_weight=0.5, BCE_weight=0.5)
+            loss = crit(out, mk.clone())
+            m.zero_grad()
+            loss.backward()
+            names, s1, s2, s3, samp = grad_summary(m)
+            bufs = {k: t.detach().numpy() for k, t in m.state_dict().items()
+                    if k.endswith("running_mean") or k.endswith("running_var")}
+            rm = sorted(bufs)
+            res.update({f"out_train_{name}": out.detach().numpy(),
+                        f"loss_{name}": np.array(loss.item()), "grad_names": np.array(names),
+                        "grad_sum": s1, "grad_abs": s2, "grad_sq": s3, "grad_samples": samp,
+                        "buf_names": np.array(rm),
+                        "buf_sums": np.array([bufs[k].astype(np.float64).sum() for k in rm])})
+            print("unext", name, "loss", loss.item())
+    np.savez_compressed(os.path.join(HERE, "unext.npz"), **res)
 
 
 def grad_summary(model):
@@ -114,6 +190,9 @@ def main():
     U = ref_utils()
     if "--fullwidth" in sys.argv:
         fullwidth(models, U)
+        return
+    if "--unext" in sys.argv:
+        unext(U)
         return
     meta = {}
 
@@ -225,6 +304,7 @@ def main():
         json.dump(meta, f, indent=1)
 
     fullwidth(models, U)
+    unext(U)
 
 
 if __name__ == "__main__":

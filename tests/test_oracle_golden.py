@@ -181,3 +181,49 @@ def test_fullwidth_nf32_at_256_matches_reference(variant):
     for i, n in enumerate(list(g["buf_names"])):
         assert abs(sd[n].double().sum().item() - float(g["buf_sums"][i])) < 1e-4 * max(1.0, abs(float(g["buf_sums"][i]))), n
     assert abs(O.show_dice(out.detach(), mask.clone()).item() - float(g["show_dice"])) < 1e-6
+
+
+def test_unext_matches_reference():
+    """UNeXt (BASELINE configs[4], Experiments/nets/UNext.py:201-358): the oracle's
+    restatement (oracle/accunet_oracle.py: unext_forward) against the reference module
+    itself, run by tests/golden/make_golden.py with import shims for the absent timm /
+    torchvision (to_2tuple restated, trunc_normal_ = torch's, DropPath never built at
+    drop_path_rate 0): 2x3x64x64 train fwd + WeightedDiceBCE + bwd (output, loss, every
+    parameter gradient's summary, running statistics) and eval outputs at 64^2 and at
+    the Cfg5 resolution 224^2 (tests/golden/unext.npz)."""
+    g = np.load(os.path.join(GOLD, "unext.npz"))
+    spec = O.unext_param_spec(3, 1)
+    sd0 = O.det_state_dict(spec, seed=5)
+    for name, shape in (("s64", (2, 3, 64, 64)), ("s224", (1, 3, 224, 224))):
+        x = O.det_input(shape, f"unext-x-{name}")
+        with torch.no_grad():
+            oe = O.unext_forward({k: v.clone() for k, v in sd0.items()}, x, training=False)
+        np.testing.assert_allclose(oe.numpy(), g[f"out_eval_{name}"], rtol=0, atol=2e-5)
+    sd = {k: v.clone() for k, v in sd0.items()}
+    x = O.det_input((2, 3, 64, 64), "unext-x-s64")
+    mask = O.det_mask((2, 1, 64, 64), "unext-mask-s64", p=0.3)
+    params = oracle_params(sd)
+    out = O.unext_forward(sd, x, training=True)
+    np.testing.assert_allclose(out.detach().numpy(), g["out_train_s64"], rtol=0, atol=2e-5)
+    loss = O.dice_bce_loss(out, mask.clone())
+    assert abs(loss.item() - float(g["loss_s64"])) < 1e-5
+    loss.backward()
+    # the encoder / decoder conv biases feed a training-mode BatchNorm (UNext.py:257-330):
+    # structurally zero gradients, rounding noise on both sides
+    bn_fed = {f"encoder{i}.bias" for i in (1, 2, 3)} | {f"decoder{i}.bias" for i in (1, 2, 3, 4)}
+    names = list(g["grad_names"])
+    assert names == list(params)
+    per = g["grad_abs"] / np.array([params[n].numel() for n in names])
+    med = float(np.median(per[per > 0]))
+    for i, n in enumerate(names):
+        gr = params[n].grad.detach().double().flatten()
+        if n in bn_fed:
+            assert gr.abs().mean().item() < 1e-3 * med and per[i] < 1e-3 * med, n
+            continue
+        ref = float(g["grad_abs"][i])
+        assert abs(gr.abs().sum().item() - ref) <= 2e-3 * ref + 1e-4 * med * gr.numel(), n
+        idx = torch.linspace(0, gr.numel() - 1, 8).long()
+        np.testing.assert_allclose(gr[idx].numpy(), g["grad_samples"][i], rtol=0,
+                                   atol=2e-3 * gr.abs().max().item() + 1e-4 * med, err_msg=n)
+    for i, n in enumerate(list(g["buf_names"])):
+        assert abs(sd[n].double().sum().item() - float(g["buf_sums"][i])) < 1e-4, n

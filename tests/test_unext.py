@@ -1,10 +1,14 @@
 """UNeXt (Experiments/nets/UNext.py) on the HIP kernels (accunet/unext.py) against the
 oracle restatement (oracle/accunet_oracle.py: unext_forward).
 
-The reference module imports timm / torchvision, which this image lacks, so no
-reference fixture pins it (parity unpinned by the reference); the oracle follows the
-source line by line and its pieces are cross-checked against torch here (shift vs
-an independent index formula, bilinear x2 vs F.interpolate). The HIP path is held to
+The reference module imports timm / torchvision, which this image lacks; the fixture
+tests/golden/unext.npz was recorded by running the reference module itself with import
+shims for them (tests/golden/make_golden.py: ref_unext; to_2tuple restated, init-only
+trunc_normal_, DropPath never built at drop_path_rate 0), and pins the oracle
+(test_oracle_golden.py: test_unext_matches_reference) and, below, the HIP model's eval
+output at 64^2 and at the Cfg5 resolution 224^2. The oracle's pieces are also
+cross-checked against torch here (shift vs an independent index formula, bilinear x2
+vs F.interpolate). The HIP path is held to
 the fp64 oracle within 4x the reference's own fp32 error (the oracle run in fp32 on
 one-rounding-perturbed inputs) plus 1e-4 of each tensor's scale, like the ACC-UNet
 whole-model tests."""
@@ -141,6 +145,24 @@ def test_unext_ops_match_torch():
     ref = torch.zeros(x.shape)
     ref[:, ::2, ::2] = 1
     assert torch.equal(x.grad.cpu(), ref)
+
+
+@pytest.mark.gpu
+def test_unext_eval_matches_reference_golden():
+    """The HIP UNeXt in eval mode against the reference module's own fp32 output
+    (tests/golden/unext.npz) at 2x3x64x64 and 1x3x224x224, within 1e-4 (the north-star
+    bound on probabilities)."""
+    from accunet.unext import UNext
+    g = np.load(os.path.join(HERE, "golden", "unext.npz"))
+    sd = O.det_state_dict(O.unext_param_spec(3, 1), seed=5)
+    for name, shape in (("s64", (2, 3, 64, 64)), ("s224", (1, 3, 224, 224))):
+        m = UNext(3, 1, img_size=shape[-1])
+        m.load_state_dict(sd)
+        m = m.cuda().eval()
+        with torch.no_grad():
+            out = m(O.det_input(shape, f"unext-x-{name}").cuda())
+        d = np.abs(out.double().cpu().numpy() - g[f"out_eval_{name}"]).max()
+        assert d < 1e-4, (name, d)
 
 
 @pytest.mark.gpu
