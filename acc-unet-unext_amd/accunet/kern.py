@@ -280,15 +280,16 @@ def dw3x3_rows(B, H, W, C, like: torch.Tensor) -> int:
     return int(_lib_raw().accunet_dw3x3_rows(B, H, W, C, _dt(like)))
 
 
-_DW_NAMES = {2: "dw3x3_span_fwd_kernel", 1: "dw3x3_tile_fwd_kernel", 0: "dw3x3_fwd_kernel"}
+_DW_NAMES = {3: "dw3x3_dma_fwd_kernel", 2: "dw3x3_span_fwd_kernel", 1: "dw3x3_tile_fwd_kernel",
+             0: "dw3x3_fwd_kernel"}
 
 
-def dw3x3_kernel_name(B, H, W, C) -> str:
-    """the forward depthwise kernel accunet_dw3x3_fwd launches for this shape"""
+def dw3x3_kernel_name(B, H, W, C, like=None) -> str:
+    """the forward depthwise kernel accunet_dw3x3_fwd launches for this shape (and the
+    storage dtype of `like`, fp32 if None)"""
     lib = _lib_raw()
-    if not hasattr(lib, "accunet_dw3x3_variant"):  # an older build (A/B runs)
-        return _DW_NAMES[1 if C % 32 == 0 else 0]
-    return _DW_NAMES[int(lib.accunet_dw3x3_variant(B, H, W, C))]
+    dt = _dt(like) if like is not None else _lib.ACC_F32
+    return _DW_NAMES[int(lib.accunet_dw3x3_variant(B, H, W, C, dt))]
 
 
 def dw3x3_fwd(x, wt, bias, sc, sh, act, flip, z, stats, B, H, W, C, bnb=None):

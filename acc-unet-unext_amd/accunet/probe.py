@@ -107,7 +107,7 @@ def k1_dw3x3(B, H, W, C, weight, bias, iters=20, device="cuda", dtype=torch.floa
     def run():
         kern.dw3x3_fwd(x, w, b, sc, sh, 1, 0, z, st, B, H, W, C)
     t = _time(run, iters)
-    name = kern.dw3x3_kernel_name(B, H, W, C)
+    name = kern.dw3x3_kernel_name(B, H, W, C, x)
     return _hbm_row(name, f"{B}x{H}x{W}x{C}", 2.0 * x.element_size() * B * H * W * C, t, iters)
 
 

@@ -1555,12 +1555,15 @@ static DwGeom dw_geom(int B, int H, int W, int C, int V, dim3* grid) {
   return g;
 }
 
-// which forward kernel accunet_dw3x3_fwd runs for this shape: 2 = span, 1 = tile,
-// 0 = register window (profiling names / the bench probe)
-extern "C" int accunet_dw3x3_variant(int B, int H, int W, int C) {
+// which forward kernel accunet_dw3x3_fwd runs for this shape and storage dtype without
+// a BN-backward epilogue: 3 = LDS-DMA ring, 2 = span, 1 = tile, 0 = register window
+// (profiling names / the bench probe)
+extern "C" int accunet_dw3x3_variant(int B, int H, int W, int C, int dt) {
   (void)B;
   if (dw_span_nt(H, W, C)) return 2;
-  return dw_tile_tcq(H, W, C, ACC_F32) ? 1 : 0;
+  const int tcq = dw_tile_tcq(H, W, C, dt);
+  if (tcq == 8 && dt == ACC_F32 && dw_dma()) return 3;
+  return tcq ? 1 : 0;
 }
 
 extern "C" int accunet_dw3x3_rows(int B, int H, int W, int C, int dt) {

@@ -109,7 +109,7 @@ def test_dw3x3_span_forward_knob_vs_fp64():
         "lib = _lib.load()\n"
         "for (B, H, W, C) in [(2, 16, 16, 96), (1, 13, 35, 96), (2, 6, 300, 8), (2, 9, 21, 192),\n"
         "                     (1, 8, 17, 256), (2, 24, 40, 64)]:\n"
-        "    assert lib.accunet_dw3x3_variant(B, H, W, C) == 2, (B, H, W, C)\n"
+        "    assert lib.accunet_dw3x3_variant(B, H, W, C, 0) == 2, (B, H, W, C)\n"
         "    for pro in (False, True):\n"
         "        T.test_dw3x3_fwd_stats_wgrad_vs_fp64(B, H, W, C, pro)\n"
         "print('SPAN_OK')\n") % HERE
