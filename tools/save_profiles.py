@@ -35,7 +35,9 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "gpurun_out")
 PROF = os.path.join(ROOT, "profiles")
-K1 = "dw3x3_tile_fwd_kernel<8, false,"
+# the fp32 K1 kernel of 16x256x256x96: the LDS-DMA ring (accunet_dw3x3_variant 3) or,
+# with ACCUNET_DW_DMA=0, the register-staged strip
+K1 = os.environ.get("K1_KERNEL", "dw3x3_dma_fwd_kernel<")
 K1_GRID = 3072 * 256  # 1024 tiles (32-row strips) x 3 channel groups, 256 threads (16x256x256x96)
 K3 = ["se_reduce_kernel<4, float, true>", "se_mid_sample_kernel", "se_mid_bn_kernel",
       "se_apply_kernel<4, float, true,"]
@@ -115,22 +117,38 @@ def step_breakdown(rows, st):
 
 
 def k1_trace(rows, st):
-    k = [r for r in rows if K1 in r["Kernel_Name"] and "float>" in r["Kernel_Name"] and grid(r) == K1_GRID]
-    probe = k[-20:]
+    """K1 dispatches of the kernel trace. The probe is the last 20 dispatches (after the
+    final Adam). In-model dispatches are matched by SHAPE through their position in the
+    step, not by grid: several depthwise layers launch the same kernel with the same
+    3072-workgroup grid (16x128^2x96 / x192, 16x64^2x384, ...), but in every step the
+    forward depthwise layers run in model order (cnv12, cnv21, ..., cnv92; cnv11's 9
+    channels and the 16^2 level use other kernels, every data gradient another template),
+    so cnv12 and cnv92 (16x256x256x96) are the first and the last K1 dispatch of a step."""
+    adam = [i for i, r in enumerate(rows) if "adam" in r["Kernel_Name"]]
+    # (the DMA kernel is fp32-only; the strip kernel's fp32 instance ends "float>")
+    isk1 = lambda r: K1 in r["Kernel_Name"] and ("dma" in K1 or "float>" in r["Kernel_Name"])
+    k = [r for r in rows if isk1(r) and grid(r) == K1_GRID]
+    probe = [r for r in rows[adam[-1] + 1:] if isk1(r)][-20:]
+    inm, other = [], []
+    for a, b in zip(adam[:-1], adam[1:]):
+        seq = [r for r in rows[a + 1:b + 1] if isk1(r)]
+        if len(seq) >= 2:
+            ends = [seq[0], seq[-1]]
+            inm += [r for r in ends if grid(r) == K1_GRID]
+            other += [r for r in seq[1:-1] if grid(r) == K1_GRID]
     pavg = sum(dur(r) for r in probe) / len(probe)
-    inm = [r for r in k[:-20] if dur(r) > 0.5 * pavg]
-    other = [r for r in k[:-20] if dur(r) <= 0.5 * pavg]
     avg = lambda rs: sum(dur(r) for r in rs) / max(len(rs), 1) / 1e3
     pd = sorted(dur(r) for r in probe)
     lines = [f"rocprofv3 --kernel-trace of `python bench.py --steps 5 --warmup 2 --no-cpu-baseline` ({st})",
              f"{K1} ..., {K1_GRID // 256} workgroups (16x256x256x96: cnv12 / cnv92 forward)",
-             f"  last 20 dispatches = bench.py roofline probe: avg {avg(probe):.2f} us, median "
-             f"{pd[len(pd) // 2] / 1e3:.2f} us ({805306368 / (avg(probe) * 1e-6) / 1e9:.0f} GB/s at the avg)",
-             f"  in-model dispatches of the same shape (cnv12 / cnv92 forward inside the "
-             f"graph-replayed steps): {len(inm)}, avg {avg(inm):.2f} us",
-             f"  same grid, other shape: {len(other)}, avg {avg(other):.2f} us", "",
-             "  dispatch durations (us):"]
-    lab = lambda r: "probe" if r in probe else ("in-model cnv12/92" if r in inm else "other shape")
+             f"  last 20 dispatches = bench.py roofline probe: avg {pavg / 1e3:.2f} us, median "
+             f"{pd[len(pd) // 2] / 1e3:.2f} us ({805306368 / (pavg * 1e-9) / 1e9:.0f} GB/s at the avg)",
+             f"  in-model dispatches of the same shape (the first and last K1 dispatch of each "
+             f"graph-replayed step = cnv12 / cnv92 forward): {len(inm)}, avg {avg(inm):.2f} us",
+             f"  same kernel and grid, other shapes (cnv21 ... cnv82 forward): {len(other)}, "
+             f"avg {avg(other):.2f} us", "", "  dispatch durations (us):"]
+    lab = lambda r: ("probe" if r in probe else "in-model cnv12/92" if r in inm else
+                     "other shape" if r in other else "warm-up / capture")
     lines += [f"    {dur(r) / 1e3:8.2f}  {lab(r)}" for r in k]
     return "\n".join(lines) + "\n"
 
@@ -208,7 +226,8 @@ def main():
         open(os.path.join(PROF, f"{r}_k1_trace.txt"), "w").write(k1_trace(rows, st))
     # PMC: K1 and K3 traffic
     if glob.glob(os.path.join(OUT, "pmc_fetch", "**", "*counter_collection.csv"), recursive=True):
-        k1rows = [x for x in pmc_rows(K1, grid_size=K1_GRID) if "float>" in x["Kernel_Name"]]
+        k1rows = [x for x in pmc_rows(K1, grid_size=K1_GRID)
+                  if "dma" in K1 or "float>" in x["Kernel_Name"]]
         write_csv(os.path.join(PROF, f"{r}_pmc_k1.csv"), k1rows)
         t1 = traffic(K1, K1_GRID, "16x256x256x96")
         t1["source"] = f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE of bench.py --eager ({st}); {r}_pmc_k1.csv"
