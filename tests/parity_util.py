@@ -115,6 +115,23 @@ def compare_vs_reference_fp32(hip: dict, ref64: dict, ref32: dict, factor=4.0, r
     return rows
 
 
+def per_tensor_norm_rows(hip: dict, ref64: dict, ref32_runs, keys, factor=4.0, rel_floor=1e-6):
+    """Per-tensor NORM check without absolute floors: ||hip - ref64|| <= factor *
+    max_runs ||ref32 - ref64|| + rel_floor * ||ref64||, for every tensor in keys. A norm
+    is far less noisy than a max, so this catches a small tensor whose gradient is
+    wrong as a whole (which the max-based check's absolute floors could let pass).
+    Returns rows (name, err_hip, err_ref32, tol, ok)."""
+    rows = []
+    for k in keys:
+        r64 = ref64[k].detach().double().cpu()
+        e_h = float((hip[k].detach().double().cpu() - r64).norm())
+        e_r = max(float((run[k].detach().double().cpu() - r64).norm()) for run in ref32_runs
+                  if k in run)
+        tol = factor * e_r + rel_floor * float(r64.norm()) + 1e-12
+        rows.append((k, e_h, e_r, tol, e_h <= tol))
+    return rows
+
+
 def global_rel_err(hip: dict, ref: dict, keys):
     num = sum(float((hip[k].detach().double().cpu() - ref[k].detach().double().cpu()).norm() ** 2)
               for k in keys)

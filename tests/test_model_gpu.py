@@ -127,6 +127,10 @@ def test_whole_model_train_step_matches_oracle(variant):
     rows = PU.compare_vs_reference_fp32(hip, r64, r32, abs_floor=floor, ref32_extra=ens)
     bad = [r for r in rows if not r[4]]
     assert not bad, sorted(bad, key=lambda r: -r[1] / r[3])[:8]
+    # and per tensor in norm, with no absolute floor: no gradient may be wrong as a whole
+    rows = PU.per_tensor_norm_rows(hip, r64, [r32] + list(ens), gkeys)
+    bad = [r for r in rows if not r[4]]
+    assert not bad, sorted(bad, key=lambda r: -r[1] / r[3])[:8]
     # eval mode uses the (updated) running statistics
     m.eval()
     with torch.no_grad():
