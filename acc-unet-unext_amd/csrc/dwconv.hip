@@ -770,7 +770,7 @@ dw3x3_dma_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
         v.z = apply_act(v.z * ps.z + pb.z, act);
         v.w = apply_act(v.w * ps.w + pb.w, act);
       }
-      return in ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+      return make_float4(in ? v.x : 0.f, in ? v.y : 0.f, in ? v.z : 0.f, in ? v.w : 0.f);
     };
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -894,6 +894,243 @@ dw3x3_dma_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
     __builtin_amdgcn_s_barrier();
   }
   // the ring becomes the reduction buffer: no DMA may still be writing it
+  __builtin_amdgcn_s_waitcnt(0);
+  if (stats) {
+    __syncthreads();
+    double v[8] = {s1[0], s1[1], s1[2], s1[3], s2[0], s2[1], s2[2], s2[3]};
+    if (block_slot_reduce<TCQ, 8, double>(v, reinterpret_cast<double*>(ring))) {
+      const long row = (long)srow * 2 * g.C;
+      const int cc = c0 + 4 * threadIdx.x;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        stats[row + cc + j] = v[j];
+        stats[row + g.C + cc + j] = v[4 + j];
+      }
+    }
+  }
+}
+
+// bf16 storage: the same LDS-DMA pipeline, but the DMA'd rows are raw bf16 (a 16-B
+// piece = 2 channel quads) in a raw ring of two chunks (the next, landed, and the one
+// after, in flight), and the activation widens each wave's own pieces into an fp32
+// ring (the window arithmetic stays fp32, as in the register-staged kernel): ACTC = 2
+// chunk slots there (one barrier per chunk: the next chunk is activated while this one
+// is read) for 32-channel tiles, 1 slot (two barriers per chunk) for 64-channel tiles,
+// whose rows are longer. LDS per block: TCQ 8 52 KB, TCQ 16 37 KB.
+template <int TCQ, bool NT>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
+dw3x3_dma_bf16_fwd_kernel(const bf16_t* __restrict__ x, const float* __restrict__ wt,
+                          const float* __restrict__ bias, const float* __restrict__ sc,
+                          const float* __restrict__ sh, int act, int flip,
+                          bf16_t* __restrict__ z, double* __restrict__ stats, DwTGeom g) {
+  constexpr int TP = 256 / TCQ, CR = 4;
+  constexpr int ROWQ = 256 + 2 * TCQ;     // quads per row: interior, then left / right halo
+  constexpr int RAWB = ROWQ * 8;          // bytes per raw bf16 row
+  constexpr int ACTC = TCQ == 8 ? 2 : 1;  // fp32 chunk slots
+  __shared__ float4 ring[ACTC * CR * ROWQ];
+  __shared__ __attribute__((aligned(16))) unsigned char raw[2 * CR * RAWB];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int q = tid % TCQ, p = tid / TCQ;
+  int t = dw_tile_id(g);
+  int cg = blockIdx.y;
+  if (g.cgf) {
+    cg = t % g.cgf;
+    t /= g.cgf;
+  }
+  const int srow = g.cgf ? t : (int)blockIdx.x;
+  const int c0 = cg * TCQ * 4;
+  const int c = c0 + 4 * q;
+  const int tw = t % g.tilesW;
+  t /= g.tilesW;
+  const int th = t % g.tilesH;
+  const int b = t / g.tilesH;
+  const int hbeg = th * DW_TR * g.rch, w0 = tw * TP;
+  const int hend = min(g.H, hbeg + DW_TR * g.rch);
+  const int nch = (hend - hbeg + CR - 1) / CR;
+  const long img = (long)b * g.H * g.W * g.C;
+  const bf16_t* ximg = x + img;
+  const __amdgpu_buffer_rsrc_t rz = acc_rsrc(z + img, (unsigned)(g.H * g.W * g.C * 2));
+  const unsigned raw_lds = (unsigned)(size_t)(__attribute__((address_space(3))) unsigned char*)raw;
+  // a lane's 16-B pieces: interior piece i (0, 1) = quads 128 i + 2 lane, +1, i.e. pixel
+  // (128 i + 2 lane) / TCQ, quad pair lq = (2 lane) % TCQ; halo (lanes < TCQ) = quads
+  // 2 lane, +1 of [left | right], pixel -1 / TP
+  const int lq = (2 * lane) % TCQ;
+  const int hside = (2 * lane) / TCQ;  // halo lanes: 0 left, 1 right
+  const int hip = hside ? TP : -1;
+  auto issue = [&](int j) {  // chunk j >= -1: rows hbeg + 1 + 4j .. +3, wave wv owns one
+    const int R = hbeg + 1 + CR * j + wv;
+    const int Rl = max(0, min(R, min(hend, g.H - 1)));
+    const int slot = ((j + 2) & 1) * CR + wv;
+    const bf16_t* rowp = ximg + (long)Rl * g.W * g.C + c0 + 4 * lq;
+    const unsigned base = raw_lds + (unsigned)(slot * RAWB);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int wp = min(w0 + (128 * i + 2 * lane) / TCQ, g.W - 1);
+      dwd_dma16<NT>(reinterpret_cast<const float*>(rowp + (long)wp * g.C), base + i * 1024u);
+    }
+    if (lane < TCQ) {
+      const int wp = max(0, min(w0 + hip, g.W - 1));
+      dwd_dma16<NT>(reinterpret_cast<const float*>(rowp + (long)wp * g.C), base + 2048u);
+    }
+  };
+  const bool pro = sc != nullptr;
+  float4 ps[2], pb[2];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    ps[e] = pro ? ld4(sc + c0 + 4 * (lq + e)) : make_float4(1.f, 1.f, 1.f, 1.f);
+    pb[e] = pro ? ld4(sh + c0 + 4 * (lq + e)) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  // widen + prologue (in-image only, zero padding after the activation) of the wave's
+  // own raw pieces of chunk j into the fp32 ring
+  auto activate = [&](int j) {
+    const int R = hbeg + 1 + CR * j + wv;
+    const int rslot = ((j + 2) & 1) * CR + wv;
+    const int aslot = (ACTC == 2 ? ((j + 2) & 1) * CR : 0) + wv;
+    const bool rin = R >= 0 && R < g.H;
+    const uint4* rr = reinterpret_cast<const uint4*>(raw + rslot * RAWB);
+    float4* aw = ring + aslot * ROWQ;
+    auto fix = [&](uint4 u, bool in, int e0) {
+      float4 v0 = make_float4(bflo(u.x), bfhi(u.x), bflo(u.y), bfhi(u.y));
+      float4 v1 = make_float4(bflo(u.z), bfhi(u.z), bflo(u.w), bfhi(u.w));
+      v0.x = apply_act(v0.x * ps[0].x + pb[0].x, act); v0.y = apply_act(v0.y * ps[0].y + pb[0].y, act);
+      v0.z = apply_act(v0.z * ps[0].z + pb[0].z, act); v0.w = apply_act(v0.w * ps[0].w + pb[0].w, act);
+      v1.x = apply_act(v1.x * ps[1].x + pb[1].x, act); v1.y = apply_act(v1.y * ps[1].y + pb[1].y, act);
+      v1.z = apply_act(v1.z * ps[1].z + pb[1].z, act); v1.w = apply_act(v1.w * ps[1].w + pb[1].w, act);
+      // component-wise selects (a select of whole float4 values lands in scratch)
+      aw[e0] = make_float4(in ? v0.x : 0.f, in ? v0.y : 0.f, in ? v0.z : 0.f, in ? v0.w : 0.f);
+      aw[e0 + 1] = make_float4(in ? v1.x : 0.f, in ? v1.y : 0.f, in ? v1.z : 0.f, in ? v1.w : 0.f);
+    };
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int qq = 128 * i + 2 * lane;
+      fix(rr[64 * i + lane], rin && w0 + qq / TCQ < g.W, qq);
+    }
+    if (lane < TCQ) {
+      const int wp = w0 + hip;
+      fix(rr[128 + lane], rin && wp >= 0 && wp < g.W, 256 + 2 * lane);
+    }
+  };
+  issue(-1);
+  issue(0);
+  float k[9][4], bi[4];
+  {
+    float wvv[36];
+#pragma unroll
+    for (int e = 0; e < 9; ++e) {
+      const float4 w4 = ld4(wt + c * 9 + 4 * e);
+      wvv[4 * e] = w4.x; wvv[4 * e + 1] = w4.y; wvv[4 * e + 2] = w4.z; wvv[4 * e + 3] = w4.w;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int tp = 0; tp < 9; ++tp) k[tp][j] = wvv[j * 9 + (flip ? 8 - tp : tp)];
+    const float4 b4 = bias ? ld4(bias + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    bi[0] = b4.x; bi[1] = b4.y; bi[2] = b4.z; bi[3] = b4.w;
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  // ACTC 1: chunk -1 widened, its two window rows read, then chunk 0 into the same slot
+  auto rdrow = [&](int aslot, float (&row)[3][4]) {
+    const float4* rw = ring + aslot * ROWQ;
+    const int e = p * TCQ + q;
+    const float4 l = rw[p == 0 ? 256 + q : e - TCQ];
+    const float4 m = rw[e];
+    const float4 r = rw[p == TP - 1 ? 256 + TCQ + q : e + TCQ];
+    row[0][0] = l.x; row[0][1] = l.y; row[0][2] = l.z; row[0][3] = l.w;
+    row[1][0] = m.x; row[1][1] = m.y; row[1][2] = m.z; row[1][3] = m.w;
+    row[2][0] = r.x; row[2][1] = r.y; row[2][2] = r.z; row[2][3] = r.w;
+  };
+  activate(-1);
+  if (ACTC == 2) activate(0);
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_s_barrier();
+  float a0[4], a1[4];
+  {
+    const int am1 = ACTC == 2 ? CR : 0;  // chunk -1's act slot
+    float row[3][4];
+    rdrow(am1 + 2, row);  // input row hbeg - 1
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float acc = bi[j];
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) acc = fmaf(k[dx][j], row[dx][j], acc);
+      a0[j] = acc;
+    }
+    rdrow(am1 + 3, row);  // input row hbeg
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float acc = a0[j], nxt = bi[j];
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) {
+        acc = fmaf(k[3 + dx][j], row[dx][j], acc);
+        nxt = fmaf(k[dx][j], row[dx][j], nxt);
+      }
+      a0[j] = acc;
+      a1[j] = nxt;
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_s_barrier();
+  if (ACTC == 1) {  // chunk 0 into the slot chunk -1 leaves
+    activate(0);
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_s_barrier();
+  }
+  issue(1);  // into chunk -1's raw slot, free since chunk -1 was widened
+  double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+  const int w = w0 + p;
+  const bool wok = w < g.W;
+  for (int kc = 0; kc < nch; ++kc) {
+    issue(kc + 2);  // into chunk kc's raw slot (widened in the previous iteration)
+    const int r0 = hbeg + CR * kc;
+    const int nr = min(CR, hend - r0);
+    const int ab = ACTC == 2 ? (kc & 1) * CR : 0;
+    float c1[4] = {0.f, 0.f, 0.f, 0.f}, c2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < CR; ++r) {
+      const bool on = wok && r < nr;
+      float row[3][4];
+      rdrow(ab + r, row);
+      float o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float acc = a0[j], mid = a1[j], nxt = bi[j];
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) {
+          acc = fmaf(k[6 + dx][j], row[dx][j], acc);
+          mid = fmaf(k[3 + dx][j], row[dx][j], mid);
+          nxt = fmaf(k[dx][j], row[dx][j], nxt);
+        }
+        a0[j] = mid;
+        a1[j] = nxt;
+        acc = rnd<bf16_t>(acc);  // statistics of the stored value
+        o[j] = acc;
+        const float am = on ? acc : 0.f;
+        c1[j] += am;
+        c2[j] = fmaf(am, am, c2[j]);
+      }
+      const unsigned off = on ? (unsigned)((((r0 + r) * g.W + w) * g.C + c) * 2) : ACC_OOB;
+      bufq_st<2>(rz, off, make_float4(o[0], o[1], o[2], o[3]), (bf16_t*)nullptr);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      s1[j] += (double)c1[j];
+      s2[j] += (double)c2[j];
+    }
+    // chunk kc+1's raw DMA has landed once only chunk kc+2's 3 pieces and the stores of
+    // chunks kc-1 and kc (4 each) are younger (kc = 0: chunk 1 was issued after the
+    // prologue, behind no stores)
+    if (kc == 0) dw_wait_vm<7>();
+    else dw_wait_vm<11>();
+    if (ACTC == 1) {  // every wave is done reading chunk kc's slot
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_s_barrier();
+    }
+    activate(kc + 1);
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_s_barrier();
+  }
   __builtin_amdgcn_s_waitcnt(0);
   if (stats) {
     __syncthreads();
@@ -1487,9 +1724,10 @@ static int dw_cgfast() {
   return v;
 }
 
-// K1 staging: 1 = LDS-DMA ring (dw3x3_dma_fwd_kernel) for the fp32 32-channel tiles
-// without a BN-backward epilogue, 0 = the register-staged strip for every shape
-// (ACCUNET_DW_DMA, tuning knob / A/B)
+// K1 staging (ACCUNET_DW_DMA, tuning knob / A/B): bit 0 = LDS-DMA ring for the fp32
+// 32-channel tiles (dw3x3_dma_fwd_kernel), bit 1 = LDS-DMA ring for bf16 tiles
+// (dw3x3_dma_bf16_fwd_kernel), both without a BN-backward epilogue; 0 = the
+// register-staged strip for every shape
 static int dw_dma() {
   static int v = -1;
   if (v < 0) {
@@ -1562,7 +1800,8 @@ extern "C" int accunet_dw3x3_variant(int B, int H, int W, int C, int dt) {
   (void)B;
   if (dw_span_nt(H, W, C)) return 2;
   const int tcq = dw_tile_tcq(H, W, C, dt);
-  if (tcq == 8 && dt == ACC_F32 && dw_dma()) return 3;
+  if ((tcq == 8 && dt == ACC_F32 && (dw_dma() & 1)) || (tcq && dt == ACC_BF16 && (dw_dma() & 2)))
+    return 3;
   return tcq ? 1 : 0;
 }
 
@@ -1630,7 +1869,24 @@ extern "C" int accunet_dw3x3_fwd(const void* x, const float* wt, const float* bi
       tg.cgf = (int)grid.y;
       grid = dim3(grid.x * grid.y, 1);
     }
-    if (dt == ACC_F32 && tcq == 8 && !bz && dw_dma()) {
+    if (dt == ACC_BF16 && !bz && (dw_dma() & 2)) {
+      auto lb = [&](auto tcqc, auto ntc) {
+        hipLaunchKernelGGL((dw3x3_dma_bf16_fwd_kernel<decltype(tcqc)::value, decltype(ntc)::value>),
+                           grid, dim3(256), 0, s, (const bf16_t*)x, wt, bias, sc, sh, act, flip,
+                           (bf16_t*)z, stats, tg);
+      };
+      using I16 = std::integral_constant<int, 16>;
+      using I8 = std::integral_constant<int, 8>;
+      using NTT = std::integral_constant<bool, true>;
+      using NTF = std::integral_constant<bool, false>;
+      if (tcq == 16) {
+        if (tg.ntl) lb(I16{}, NTT{}); else lb(I16{}, NTF{});
+      } else {
+        if (tg.ntl) lb(I8{}, NTT{}); else lb(I8{}, NTF{});
+      }
+      return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+    }
+    if (dt == ACC_F32 && tcq == 8 && !bz && (dw_dma() & 1)) {
       if (tg.ntl)
         hipLaunchKernelGGL((dw3x3_dma_fwd_kernel<true>), grid, dim3(256), 0, s, (const float*)x, wt,
                            bias, sc, sh, act, flip, (float*)z, stats, tg);

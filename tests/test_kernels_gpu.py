@@ -97,6 +97,46 @@ def test_dw3x3_fwd_stats_wgrad_vs_fp64(B, H, W, C, pro):
     assert (db.double().cpu() - gb).abs().max().item() <= 1e-5 * gb.abs().max().item() + 1e-5
 
 
+@pytest.mark.parametrize("B,H,W,C", [(2, 16, 64, 96), (1, 13, 35, 96), (2, 24, 40, 192),
+                                     (1, 16, 16, 64), (2, 9, 20, 128)])
+@pytest.mark.parametrize("pro", [False, True])
+def test_dw3x3_bf16_fwd_vs_fp64(B, H, W, C, pro):
+    """bf16 storage (BASELINE configs[2]): the depthwise forward reads bf16 x, computes
+    in fp32 (prologue, 9 taps) and stores z rounded to bf16; its norm2 statistics are
+    those of the stored values. Against an fp64 restatement of the same rounding: z
+    within one bf16 rounding (2^-8 relative, plus the fp32 arithmetic), statistics of
+    the stored z within fp32 accumulation noise. Covers 32- and 64-channel tiles
+    (C % 64 == 0) and ragged images, on whichever kernel the library selects (the
+    LDS-DMA ring with ACCUNET_DW_DMA bit 1, else the register-staged strip)."""
+    kern = _kern()
+    g = torch.Generator().manual_seed(B * 7 + H * 3 + C)
+    x = torch.randn(B, H, W, C, generator=g).to(torch.bfloat16)
+    wt = torch.randn(C, 1, 3, 3, generator=g, dtype=torch.float64) * 0.3
+    bias = torch.randn(C, generator=g, dtype=torch.float64) * 0.1
+    sc = torch.rand(C, generator=g, dtype=torch.float64) + 0.5
+    sh = torch.randn(C, generator=g, dtype=torch.float64) * 0.2
+    xd = x.double()
+    a = _lrelu(xd * sc.float().double() + sh.float().double()) if pro else xd
+    z_ref = F.conv2d(a.permute(0, 3, 1, 2), wt.float().double(), bias.float().double(), padding=1,
+                     groups=C).permute(0, 2, 3, 1)
+    xg = x.to(DEV)
+    wd = wt.float().to(DEV)
+    rows = kern.dw3x3_rows(B, H, W, C, xg)
+    st = torch.zeros(rows, 2, C, dtype=torch.float64, device=DEV)
+    z = torch.empty(B, H, W, C, device=DEV, dtype=torch.bfloat16)
+    kern.dw3x3_fwd(xg, wd, bias.float().to(DEV), sc.float().to(DEV) if pro else None,
+                   sh.float().to(DEV) if pro else None, 1 if pro else 0, 0, z, st, B, H, W, C)
+    torch.cuda.synchronize()
+    zh = z.double().cpu()
+    scale = z_ref.abs().max().item()
+    assert (zh - z_ref).abs().max().item() <= 2.0 ** -8 * z_ref.abs().max().item() * 1.01 + 1e-6 * scale
+    # statistics describe the stored (rounded) values
+    s_ = st.sum(0).cpu()
+    zr = zh.reshape(-1, C)
+    assert torch.allclose(s_[:C], zr.sum(0), rtol=1e-6, atol=1e-6 * zr.abs().sum(0).max().item())
+    assert torch.allclose(s_[C:], (zr * zr).sum(0), rtol=1e-6)
+
+
 def test_dw3x3_span_forward_knob_vs_fp64():
     """The span forward / data-gradient kernel ships behind ACCUNET_DW_SPAN bit 2 (read
     once per process by the library): a child process with ACCUNET_DW_SPAN=3 runs the
