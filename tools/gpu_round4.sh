@@ -1,0 +1,38 @@
+#!/bin/bash
+# Round-4 profile pass: parity tests, the bench lines (fp32 headline, bf16, UNeXt,
+# ACC_UNet_W at 512^2), a rocprofv3 kernel trace (+ stats) of the fp32 bench and of the
+# bf16 bench, the FETCH_SIZE / WRITE_SIZE passes (separate runs) that give K1's and K3's
+# HBM traffic, and tools/kbench. Every GPU step has its own time limit; the first
+# failure ends the pass. SKIP_TESTS=1 skips the suite.
+set -e -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+if [ -z "${SKIP_TESTS:-}" ]; then
+  timeout -k 10 900 python -u -m pytest tests -q -m gpu --timeout 240 --timeout-method thread > gpurun_out/gputests.log 2>&1 || { tail -30 gpurun_out/gputests.log; exit 1; }
+  tail -n 1 gpurun_out/gputests.log
+fi
+timeout -k 10 400 python bench.py > gpurun_out/bench_full.log 2>&1
+grep '^{"metric' gpurun_out/bench_full.log | cut -c1-300
+timeout -k 10 300 python bench.py --dtype bf16 --no-cpu-baseline > gpurun_out/bench_bf16.log 2>&1
+grep '^{"metric' gpurun_out/bench_bf16.log | cut -c1-300
+timeout -k 10 300 python bench.py --model unext > gpurun_out/bench_unext.log 2>&1
+grep '^{"metric' gpurun_out/bench_unext.log | cut -c1-200
+timeout -k 10 300 python bench.py --variant w --size 512 --batch 4 --no-cpu-baseline > gpurun_out/bench_w512.log 2>&1
+grep '^{"metric' gpurun_out/bench_w512.log | cut -c1-200
+for dt in fp32 bf16; do
+  d=prof_bench; [ $dt = bf16 ] && d=prof_bench_bf16
+  rm -rf gpurun_out/$d
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$d -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-parity --dtype $dt > gpurun_out/$d.log 2>&1
+  python tools/step_profile.py gpurun_out/$d --last 4 --top 45 > gpurun_out/step_$dt.txt
+  head -n 3 gpurun_out/step_$dt.txt
+done
+echo "kernel traces done"
+rm -rf gpurun_out/pmc_fetch gpurun_out/pmc_write
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python bench.py --eager --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/pmc_fetch.log 2>&1
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python bench.py --eager --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/pmc_write.log 2>&1
+# keep only the probe dispatches (the last 300 dispatch ids cover K1, K3 and the GEMM probe)
+python tools/save_profiles.py --shrink-pmc gpurun_out/pmc_fetch gpurun_out/pmc_write
+echo "pmc done"
+timeout -k 10 120 tools/kbench 20 > gpurun_out/kbench.txt 2>&1
+echo "kbench done"
