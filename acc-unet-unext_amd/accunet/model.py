@@ -149,11 +149,16 @@ class HANCBlock(nn.Module):
 
     def run(self, inp: torch.Tensor) -> torch.Tensor:
         """inp: materialised NHWC tensor -> NHWC output of the block's SE."""
-        z1 = ops.pw_conv([inp], self.conv1.weight, self.conv1.bias, consumer_bn=self.norm1)
+        # inp feeds conv1 and the residual add: its two gradient contributions meet in
+        # one buffer (the residual's, handed over as it is, is added in conv1's
+        # data-gradient epilogue) instead of an autograd elementwise add
+        sl = ops.GradSlot()
+        z1 = ops.pw_conv([inp], self.conv1.weight, self.conv1.bias, consumer_bn=self.norm1,
+                         slots=[sl])
         z2 = ops.dw_conv(z1, self.conv2.weight, self.conv2.bias, consumer_bn=self.norm2)
         z3 = self.hnc.run(z2)
         # x = norm(lrelu(hnc.bn(z3)) + inp)   (ACC_UNet.py:279; no activation after norm)
-        r = ops.bn_act_add(z3, res=inp, consumer_bn=self.norm, act_after=ACT_NONE)
+        r = ops.bn_act_add(z3, res=inp, consumer_bn=self.norm, act_after=ACT_NONE, res_slot=sl)
         z4 = ops.pw_conv([r], self.conv3.weight, self.conv3.bias, consumer_bn=self.norm3)
         return self.sqe.run(z4)
 
