@@ -26,6 +26,14 @@ ACC_F32, ACC_BF16 = 0, 1
 ACC_AUG_F32, ACC_AUG_U8 = 0, 1  # accunet_aug_geom element types
 
 
+class AccRelayout(Structure):
+    _fields_ = [
+        ("inp", c_void_p), ("out", c_void_p), ("total", c_longlong), ("kind", c_int),
+        ("blk0", c_int), ("d", c_int * 4), ("s", c_longlong * 4), ("flip", c_int * 4),
+        ("N", c_int), ("C", c_int), ("J", c_int), ("order", c_int * 8),
+    ]
+
+
 class AccGemmDesc(Structure):
     _fields_ = [
         ("M", c_int), ("N", c_int), ("K", c_int),
@@ -69,6 +77,8 @@ _SIGS = {
     "accunet_stream_ticket_bank": [P, I],
     "accunet_stream_ticket_unregister": [P],
     "accunet_abi_hash": [],
+    "accunet_relayout_blocks": [L],
+    "accunet_relayout_batch": [P, I, I, P],
     "accunet_bn_finalize": [P, I, I, D, P, P, P, P, P, F, F, I, P, P, P],
     "accunet_affine_act_fwd": [P, P, P, I, P, P, L, I, P, IP, I, P],
     "accunet_bn_bwd_ws_elems": [L, I],

@@ -354,6 +354,15 @@ def permute4(inp, out, dims, strides, flips=None, accumulate=False):
          _dt(out), _stream())
 
 
+def relayout_blocks(total: int) -> int:
+    return int(_lib_raw().accunet_relayout_blocks(int(total)))
+
+
+def relayout_batch(items_dev: torch.Tensor, n: int, nblocks: int):
+    """one launch for n AccRelayout items already in device memory (WeightPrep)"""
+    call("accunet_relayout_batch", _p(items_dev), int(n), int(nblocks), _stream())
+
+
 def group_relayout(inp, out, N, C, J, order, inverse=False):
     o = (ctypes.c_int * 8)(*([int(v) for v in order] + [0] * (8 - len(order))))
     call("accunet_group_relayout", _p(inp), _p(out), int(N), int(C), int(J), o,

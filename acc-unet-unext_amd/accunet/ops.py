@@ -16,13 +16,15 @@ used for allocation, views and autograd bookkeeping.
 """
 from __future__ import annotations
 
+import contextlib
+
 import os
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
 
 import torch
 
-from . import kern
+from . import _lib, kern
 from . import profile as _prof
 from ._lib import (ACT_LRELU, ACT_NONE, AMODE_COL, AMODE_SHIFT3, BMODE_NN, BMODE_NN_SHIFT3,
                    PRO_AFFINE, PRO_AFFINE_LRELU, PRO_NONE)
@@ -266,6 +268,108 @@ def _slot_reg(slot):
     if slot is None or not _SLOTS_ON or not torch.is_grad_enabled():
         return None
     return slot.register()
+
+
+# --------------------------------------------------------------------------
+# Forward-layout weight copies made ahead of time (graph mode)
+# --------------------------------------------------------------------------
+_PREP = None  # {(weight data_ptr, tag): tensor} while a WeightPrep is active
+
+
+def _prepared(weight, tag):
+    """the forward-layout copy of `weight` made by the active WeightPrep, or None (then
+    the op makes it itself)"""
+    if _PREP is None:
+        return None
+    return _PREP.get((weight.data_ptr(), tag))
+
+
+class WeightPrep:
+    """Every forward-layout weight copy of a model -- HANCLayer's grouped columns
+    (ACC_UNet.py:96-106,138), the MLFC merge de-interleave (:492), the ResPath 3x3 and
+    its flipped data-gradient form (:317-318), the ConvTranspose2d [ci][tap][co] form
+    (:578-590) -- made by ONE launch (accunet_relayout_batch) into persistent buffers.
+
+    The graph-mode TrainStep runs it before each replay and captures its graph inside
+    `active()`, so the captured ops read these buffers instead of launching ~54 small
+    relayouts per step. Outside `active()` every op makes its own copy, so an eager
+    forward (validation, tests) never reads a copy older than the weights."""
+
+    def __init__(self, model):
+        from torch import nn
+        from .model import HANCLayer, MLFC, MLFC_Lite, ResPath
+        items, bufs, keep = [], {}, []
+
+        def add(w, tag, out_shape, kind, **kw):
+            key = (w.data_ptr(), tag)
+            if key in bufs:
+                return
+            out = torch.empty(out_shape, dtype=torch.float32, device=w.device)
+            it = _lib.AccRelayout()
+            it.inp, it.out = w.data_ptr(), out.data_ptr()
+            it.total, it.kind = out.numel(), kind
+            if kind == 0:
+                for a in range(4):
+                    it.d[a], it.s[a] = kw["d"][a], kw["s"][a]
+                    it.flip[a] = kw.get("flip", (0, 0, 0, 0))[a]
+            else:
+                it.N, it.C, it.J = kw["N"], kw["C"], kw["J"]
+                for j in range(8):
+                    it.order[j] = kw["order"][j] if j < kw["J"] else j
+            items.append(it)
+            bufs[key] = out
+            keep.append(w)
+
+        for m in model.modules():
+            if isinstance(m, HANCLayer):
+                w = m.cnv.weight
+                N, K = w.shape[0], w.shape[1]
+                J = 2 * m.k - 1
+                add(w, "hanc", (N, K), 1, N=N, C=K // J, J=J, order=_HANC_ORDER[m.k])
+            elif isinstance(m, MLFC) and not isinstance(m, MLFC_Lite):
+                for name, ch in m.named_children():
+                    if name.startswith("cnv_mrg"):
+                        for blk in ch:
+                            w = blk.conv1.weight
+                            f = w.shape[0]
+                            add(w, "grp", (f, 2 * f), 1, N=f, C=f, J=2, order=(0, 1))
+            elif isinstance(m, ResPath):
+                for conv in m.convs:
+                    w = conv.weight
+                    Co, Ci = w.shape[0], w.shape[1]
+                    add(w, "c3", (Co, 9 * Ci), 0, d=(Co, 3, 3, Ci), s=(9 * Ci, 3, 1, 9))
+                    add(w, "c3f", (Ci, 9 * Co), 0, d=(Ci, 3, 3, Co), s=(9, 3, 1, 9 * Ci),
+                        flip=(0, 1, 1, 0))
+            elif isinstance(m, nn.ConvTranspose2d) and tuple(m.kernel_size) == (2, 2):
+                w = m.weight
+                Ci, Co = w.shape[0], w.shape[1]
+                add(w, "ct", (Ci, 4 * Co), 0, d=(Ci, 2, 2, Co), s=(4 * Co, 2, 1, 4))
+        blk = 0
+        for it in items:
+            it.blk0 = blk
+            blk += kern.relayout_blocks(it.total)
+        self.n, self.nblocks = len(items), blk
+        self.bufs = bufs
+        self._weights = keep
+        self._items = items
+        if items:
+            raw = bytes((_lib.AccRelayout * len(items))(*items))
+            dev = keep[0].device
+            self.table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev)
+
+    def run(self):
+        """(re)make every copy from the current weights, on the current stream"""
+        if self.n:
+            kern.relayout_batch(self.table, self.n, self.nblocks)
+
+    @contextlib.contextmanager
+    def active(self):
+        global _PREP
+        prev, _PREP = _PREP, self.bufs
+        try:
+            yield self
+        finally:
+            _PREP = prev
 
 
 def as_pending(x) -> Pending:
@@ -660,8 +764,10 @@ class _HancLayerFn(torch.autograd.Function):
         pro = cfg.pro
         sc = pro.st[2] if pro.active else None
         sh = pro.st[3] if pro.active else None
-        Wp = _f32((N, J * C), z)
-        kern.group_relayout(weight, Wp, N, C, J, _HANC_ORDER[k])
+        Wp = _prepared(weight, "hanc")
+        if Wp is None:
+            Wp = _f32((N, J * C), z)
+            kern.group_relayout(weight, Wp, N, C, J, _HANC_ORDER[k])
         ups = []
         p2 = p4 = g2 = g4 = mk2 = mk4 = None
         if k >= 2:
@@ -991,8 +1097,10 @@ class _Conv3x3Fn(torch.autograd.Function):
     def forward(ctx, cfg: _C3Cfg, x, weight, bias):
         B, H, W, Ci, Co = cfg.B, cfg.H, cfg.W, cfg.Cin, cfg.Cout
         P = B * H * W
-        Wr = _f32((Co, 9 * Ci), x)  # [co][tap][ci]
-        kern.permute4(weight, Wr, (Co, 3, 3, Ci), (9 * Ci, 3, 1, 9))
+        Wr = _prepared(weight, "c3")
+        if Wr is None:
+            Wr = _f32((Co, 9 * Ci), x)  # [co][tap][ci]
+            kern.permute4(weight, Wr, (Co, 3, 3, Ci), (9 * Ci, 3, 1, 9))
         Z = _act((B, H, W, Co), x)
         stats = _stats((kern.gemm_stats_rows(P, Co, 9 * Ci), 2, Co), x) if cfg.want_stats else None
         kern.gemm(P, Co, 9 * Ci, a=[x], lda=[Ci], amode=AMODE_SHIFT3, b=Wr, ldb=9 * Ci, c=Z,
@@ -1025,8 +1133,10 @@ class _Conv3x3Fn(torch.autograd.Function):
                                   allow_split=True))
             kern.permute4(dWr, dW, (Co, Ci, 3, 3), (9 * Ci, 1, 3 * Ci, Ci))
         if ctx.needs_input_grad[1]:
-            Wf = _f32((Ci, 9 * Co), x)  # [ci][tap'][co] = W[co][ci][8-tap']
-            kern.permute4(weight, Wf, (Ci, 3, 3, Co), (9, 3, 1, 9 * Ci), flips=(0, 1, 1, 0))
+            Wf = _prepared(weight, "c3f")
+            if Wf is None:
+                Wf = _f32((Ci, 9 * Co), x)  # [ci][tap'][co] = W[co][ci][8-tap']
+                kern.permute4(weight, Wf, (Ci, 3, 3, Co), (9, 3, 1, 9 * Ci), flips=(0, 1, 1, 0))
             if cfg.slot is None:
                 dx, adds = torch.empty_like(x), []
             else:  # shared gradient buffer: earlier contributions are epilogue addends
@@ -1064,8 +1174,10 @@ class _ConvT2Fn(torch.autograd.Function):
         B, H, W, Ci = x.shape
         Co = weight.shape[1]
         P = B * H * W
-        Wr = _f32((Ci, 4 * Co), x)  # [ci][d][co], d = di*2+dj
-        kern.permute4(weight, Wr, (Ci, 2, 2, Co), (4 * Co, 2, 1, 4))
+        Wr = _prepared(weight, "ct")
+        if Wr is None:
+            Wr = _f32((Ci, 4 * Co), x)  # [ci][d][co], d = di*2+dj
+            kern.permute4(weight, Wr, (Ci, 2, 2, Co), (4 * Co, 2, 1, 4))
         T = _act((B, H, W, 4 * Co), x)
         kern.gemm(P, 4 * Co, Ci, a=[x], lda=[Ci], b=Wr, ldb=4 * Co, bmode=BMODE_NN, c=T,
                   ldc=4 * Co)
@@ -1260,9 +1372,12 @@ class _GroupRelayoutFn(torch.autograd.Function):
     def forward(ctx, w2, J, order):
         N, K = w2.shape
         C = K // J
+        ctx.meta = (N, C, J, list(order))
+        pre = _prepared(w2, "grp") if (J, tuple(order)) == (2, (0, 1)) else None
+        if pre is not None:  # made by the step's WeightPrep launch (a view: the buffer stays plain)
+            return pre.view(N, K)
         out = _f32((N, K), w2)
         kern.group_relayout(w2, out, N, C, J, order)
-        ctx.meta = (N, C, J, list(order))
         return out
 
     @staticmethod

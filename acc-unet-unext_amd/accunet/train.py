@@ -35,7 +35,9 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
-from . import kern
+import os
+
+from . import kern, ops
 from .dist import all_reduce_mean
 from .loss import WeightedDiceBCE
 from .optim import FusedAdam
@@ -240,6 +242,12 @@ class TrainStep:
             p.grad = None
         torch.cuda.synchronize()
 
+        # every forward-layout weight copy in one launch before each replay, read by the
+        # captured ops (ops.WeightPrep; ACCUNET_WEIGHT_PREP=0: each op relayouts itself)
+        self._prep = None
+        if os.environ.get("ACCUNET_WEIGHT_PREP", "1") != "0":
+            self._prep = ops.WeightPrep(self.model)
+            self._prep.run()
         self._buckets = None
         if self.dp:
             self._buckets = _GraphBuckets(self.params, self.bucket_mb, self._x.device,
@@ -249,7 +257,11 @@ class TrainStep:
         g = torch.cuda.CUDAGraph(keep_graph=self._buckets is not None)
         try:
             with torch.cuda.graph(g):
-                loss = self._fwd_bwd(self._x, self._m)
+                if self._prep is not None:
+                    with self._prep.active():
+                        loss = self._fwd_bwd(self._x, self._m)
+                else:
+                    loss = self._fwd_bwd(self._x, self._m)
         finally:
             if self._buckets is not None:
                 self._buckets.disarm()
@@ -285,6 +297,8 @@ class TrainStep:
             self._x.copy_(images)
         if masks.data_ptr() != self._m.data_ptr():
             self._m.copy_(masks)
+        if self._prep is not None:
+            self._prep.run()  # from the weights the last Adam step left
         self._g.replay()
         if self.dp:
             self._buckets.reduce(self.pg)

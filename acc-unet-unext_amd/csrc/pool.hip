@@ -603,3 +603,59 @@ extern "C" int accunet_group_relayout(const float* in, float* out, int N, int C,
                      (hipStream_t)stream, in, out, N, C, J, o, inverse);
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
+
+// ---------------------------------------------------------------------------
+// Batched weight relayouts: every forward-layout weight copy of a training step in one
+// launch (accunet/ops.py: WeightPrep, used by the graph-mode TrainStep before each
+// replay) instead of one small launch per layer. Item i (AccRelayout, device memory)
+// owns blocks [blk0_i, blk0_{i+1}); kind 0 = accunet_permute4's gather, kind 1 =
+// accunet_group_relayout's forward; the same index arithmetic, so the copies are the
+// ones the per-layer launches make.
+// ---------------------------------------------------------------------------
+#define RL_EPT 4
+__global__ void __launch_bounds__(256)
+relayout_batch_kernel(const AccRelayout* __restrict__ items, int n) {
+  // the item of this block: the last one whose blk0 <= blockIdx.x (blk0 ascending)
+  int lo = 0, hi = n - 1;
+  const int bid = (int)blockIdx.x;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (items[mid].blk0 <= bid) lo = mid; else hi = mid - 1;
+  }
+  const AccRelayout& it = items[lo];
+  const long base = ((long)(bid - it.blk0) * 256 + threadIdx.x) * RL_EPT;
+#pragma unroll
+  for (int e = 0; e < RL_EPT; ++e) {
+    const long i = base + e;
+    if (i >= it.total) break;
+    long src;
+    if (it.kind == 0) {
+      long r = i;
+      src = 0;
+      for (int a = 3; a >= 0; --a) {
+        int ia = (int)(r % it.d[a]);
+        r /= it.d[a];
+        if (it.flip[a]) ia = it.d[a] - 1 - ia;
+        src += ia * it.s[a];
+      }
+    } else {
+      const int c = (int)(i % it.C);
+      const long t = i / it.C;
+      const int jj = (int)(t % it.J);
+      const int nn = (int)(t / it.J);
+      src = (long)nn * it.C * it.J + (long)c * it.J + it.order[jj];
+    }
+    it.out[i] = it.in[src];
+  }
+}
+
+extern "C" int accunet_relayout_blocks(long long total) {
+  return (int)((total + 256L * RL_EPT - 1) / (256L * RL_EPT));
+}
+
+extern "C" int accunet_relayout_batch(const void* items_dev, int n, int nblocks, void* stream) {
+  if (!items_dev || n <= 0 || nblocks <= 0) return ACC_EBADARG;
+  hipLaunchKernelGGL(relayout_batch_kernel, dim3(nblocks), dim3(256), 0, (hipStream_t)stream,
+                     (const AccRelayout*)items_dev, n);
+  return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+}

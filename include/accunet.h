@@ -180,6 +180,29 @@ int accunet_dw3x3_wgrad(const void* x, const void* dz, const float* sc, const fl
                         size_t ws_elems, int dt, void* stream);
 
 /* ------------------------------------------------------------------------- *
+ * Batched forward-layout weight copies (the graph-mode training step makes them all
+ * in one launch before each replay, accunet/ops.py WeightPrep): `items_dev` is a
+ * device array of n AccRelayout, blk0 ascending from 0, item i owning blocks
+ * [blk0_i, blk0_{i+1}) with accunet_relayout_blocks(total_i) blocks; nblocks = their
+ * sum. kind 0 = the gather of accunet_permute4 (d, s, flip), kind 1 = the forward of
+ * accunet_group_relayout (N, C, J, order). fp32 weights only.
+ * ------------------------------------------------------------------------- */
+typedef struct AccRelayout {
+  const float* in;
+  float* out;
+  long long total;
+  int kind;
+  int blk0;
+  int d[4];
+  long long s[4];
+  int flip[4];
+  int N, C, J;
+  int order[8];
+} AccRelayout;
+int accunet_relayout_blocks(long long total);
+int accunet_relayout_batch(const void* items_dev, int n, int nblocks, void* stream);
+
+/* ------------------------------------------------------------------------- *
  * HANCLayer neighbourhood pyramid (ACC_UNet/ACC_UNet.py:86-106): from
  * a = act(x*sc+sh): P2 = [avg2 a | max2 a] at H/2, P4 = [avg4 a | max4 a] at H/4
  * (k = 3) in one read. mk2 / mk4 (optional, uint8 [P/4][C] / [P/16][C]) receive the

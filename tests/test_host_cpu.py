@@ -357,3 +357,71 @@ def test_host_abi_under_address_sanitizer():
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode == 0 and "0 failure(s)" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
     assert "AddressSanitizer" not in r.stderr, r.stderr[-4000:]
+
+
+def _emulate_relayout(it, src):
+    """numpy restatement of relayout_batch_kernel's index arithmetic for one item"""
+    out = np.empty(it.total, dtype=np.float32)
+    i = np.arange(it.total, dtype=np.int64)
+    if it.kind == 0:
+        r, off = i.copy(), np.zeros_like(i)
+        for a in (3, 2, 1, 0):
+            ia = r % it.d[a]
+            r //= it.d[a]
+            if it.flip[a]:
+                ia = it.d[a] - 1 - ia
+            off += ia * it.s[a]
+    else:
+        c = i % it.C
+        t = i // it.C
+        jj = t % it.J
+        nn = t // it.J
+        order = np.array(list(it.order), dtype=np.int64)
+        off = nn * it.C * it.J + c * it.J + order[jj]
+    out[:] = src[off]
+    return out
+
+
+def test_weight_prep_items_reproduce_the_per_op_layouts():
+    """ops.WeightPrep (the graph step's one-launch weight relayout): the AccRelayout
+    items it builds for a full ACC_UNet (18 HANC grouped-column, 12 MLFC merge, 10 + 10
+    ResPath 3x3 / flipped, 4 ConvT copies), fed through a numpy restatement of the
+    kernel's index arithmetic, give exactly the layouts the per-op relayouts make
+    (torch permutes of the reference weights), with ascending block ranges."""
+    from accunet import ops
+    from accunet._lib import AccRelayout
+    from accunet.model import ACC_UNet
+    assert ctypes.sizeof(AccRelayout) == 144
+    torch.manual_seed(0)
+    m = ACC_UNet(3, 1, n_filts=8)
+    prep = ops.WeightPrep(m)
+    assert prep.n == 18 + 12 + 20 + 4
+    blk = [it.blk0 for it in prep._items]
+    assert blk[0] == 0 and all(a < b for a, b in zip(blk, blk[1:]))
+    want = {}
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.Conv2d) and mod.kernel_size == (3, 3) and mod.groups == 1:
+            w = mod.weight.detach()
+            Co, Ci = w.shape[:2]
+            want[(w.data_ptr(), "c3")] = w.permute(0, 2, 3, 1).reshape(Co, 9 * Ci)
+            want[(w.data_ptr(), "c3f")] = w.flip(2, 3).permute(1, 2, 3, 0).reshape(Ci, 9 * Co)
+        elif isinstance(mod, torch.nn.ConvTranspose2d):
+            w = mod.weight.detach()
+            want[(w.data_ptr(), "ct")] = w.permute(0, 2, 3, 1).reshape(w.shape[0], -1)
+    for name, mod in m.named_modules():
+        if name.endswith(".hnc"):
+            w = mod.cnv.weight.detach()
+            N, K = w.shape[:2]
+            J = 2 * mod.k - 1
+            order = list(ops._HANC_ORDER[mod.k])
+            want[(w.data_ptr(), "hanc")] = w.reshape(N, K // J, J)[:, :, order].permute(0, 2, 1).reshape(N, K)
+        if ".cnv_mrg" in name and name.endswith(".conv1"):
+            w = mod.weight.detach()
+            f = w.shape[0]
+            want[(w.data_ptr(), "grp")] = w.reshape(f, f, 2).permute(0, 2, 1).reshape(f, 2 * f)
+    assert set(want) == set(prep.bufs)
+    ptr2w = {p.data_ptr(): p.detach().reshape(-1).numpy() for p in m.parameters()}
+    for it, (key, buf) in zip(prep._items, prep.bufs.items()):
+        assert it.out == buf.data_ptr() and it.inp == key[0]
+        got = _emulate_relayout(it, ptr2w[it.inp])
+        np.testing.assert_array_equal(got, want[key].reshape(-1).numpy(), err_msg=str(key))
