@@ -57,6 +57,9 @@ int main() {
   }
   for (int b = 1; b <= 32; b *= 2) sink += (long)accunet_loss_ws_elems(b);
   EXPECT(accunet_adam_chunk_elems() > 0);
+  EXPECT(accunet_relayout_blocks(1) == 1 && accunet_relayout_blocks(1024) == 1 &&
+         accunet_relayout_blocks(1025) == 2);
+  EXPECT(accunet_relayout_batch(nullptr, 4, 4, nullptr) == -2);
   // dwconv2d geometry: every odd k of the reference's test.py, both paddings
   for (int k = 3; k <= 31; k += 2)
     for (int rep = 0; rep < 2; ++rep) {
