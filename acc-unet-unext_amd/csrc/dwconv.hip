@@ -1303,6 +1303,164 @@ dw3x3_xl_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
   }
 }
 
+// ----------------------------------------------------------------------------
+// K1 one-shot block tiles (ACCUNET_DW_BLK = R): a block loads its whole (R+2)-row halo
+// tile of 34 px x 8 quads at once (every load in flight together), activates it into
+// LDS, takes ONE barrier and computes its R output rows (rolling row accumulators, the
+// FMA order and 4-row statistics grouping of the strip kernel: bit-identical). No ring,
+// no per-chunk barriers; the blocks of a CU overlap one another's load and compute
+// phases instead (tools/k1lab tile_lds R16: +3-5 points of HBM over the strip structure
+// without arithmetic). R = 16: 78 KB of LDS, 2 blocks per CU; R = 8: 43.5 KB, 3.
+// ----------------------------------------------------------------------------
+template <int R, int AUX, typename T>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R >= 16 ? 2 : 3)))
+dw3x3_blk_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
+                     const float* __restrict__ bias, const float* __restrict__ sc,
+                     const float* __restrict__ sh, int act, int flip, T* __restrict__ z,
+                     double* __restrict__ stats, DwTGeom g) {
+  constexpr int TCQ = 8, TP = 32, IP = TP + 2, IRB = R + 2, CR = 4;
+  constexpr int QL = Raw16<T>::QL;
+  constexpr int NQ = IRB * IP * TCQ;         // quads of the halo tile
+  constexpr int NL = (NQ / QL + 255) / 256;  // 16-byte loads per thread
+  typedef typename Raw16<T>::type RawL;
+  __shared__ float4 tile[NQ];
+  const int tid = threadIdx.x;
+  const int q = tid % TCQ, p = tid / TCQ;
+  int t = dw_tile_id(g);
+  int cg = blockIdx.y;
+  if (g.cgf) {
+    cg = t % g.cgf;
+    t /= g.cgf;
+  }
+  const int srow = g.cgf ? t : (int)blockIdx.x;
+  const int c0 = cg * TCQ * 4;
+  const int c = c0 + 4 * q;
+  const int tw = t % g.tilesW;
+  t /= g.tilesW;
+  const int th = t % g.tilesH;
+  const int b = t / g.tilesH;
+  const int hbeg = th * DW_TR * g.rch, w0 = tw * TP;
+  const int hend = min(g.H, hbeg + DW_TR * g.rch);
+  const long img = (long)b * g.H * g.W * g.C;
+  const unsigned ibytes = (unsigned)(g.H * g.W * g.C * (int)sizeof(T));
+  const __amdgpu_buffer_rsrc_t rx = acc_rsrc(x + img, ibytes);
+  const __amdgpu_buffer_rsrc_t rz = acc_rsrc(z + img, ibytes);
+  const bool pro = sc != nullptr;
+  float4 ps[QL], pb[QL];
+  dw_stage_pro<TCQ, QL>(sc, sh, c0, ps, pb);
+  {
+    RawL v[NL];
+#pragma unroll
+    for (int k = 0; k < NL; ++k) {
+      const int i = (tid + 256 * k) * QL;
+      const int rp = i / TCQ, qq = i % TCQ;
+      const int pp = rp % IP, r = rp / IP;
+      const int hh = hbeg - 1 + r, ww = w0 - 1 + pp;
+      const bool in = i < NQ && hh >= 0 && hh < g.H && ww >= 0 && ww < g.W;
+      v[k] = buf16_ld<AUX>(rx, in ? (unsigned)(((hh * g.W + ww) * g.C + c0 + 4 * qq) * (int)sizeof(T))
+                                  : ACC_OOB, (const T*)nullptr);
+    }
+#pragma unroll
+    for (int k = 0; k < NL; ++k) {
+      const int i = (tid + 256 * k) * QL;
+      if (i < NQ) {
+        const int rp = i / TCQ;
+        const int pp = rp % IP, r = rp / IP;
+        const int hh = hbeg - 1 + r, ww = w0 - 1 + pp;
+        const bool in = hh >= 0 && hh < g.H && ww >= 0 && ww < g.W;
+#pragma unroll
+        for (int j = 0; j < QL; ++j) {
+          float4 a = r16q(v[k], j);
+          if (pro) {
+            a.x = apply_act(a.x * ps[j].x + pb[j].x, act);
+            a.y = apply_act(a.y * ps[j].y + pb[j].y, act);
+            a.z = apply_act(a.z * ps[j].z + pb[j].z, act);
+            a.w = apply_act(a.w * ps[j].w + pb[j].w, act);
+          }
+          tile[i + j] = make_float4(in ? a.x : 0.f, in ? a.y : 0.f, in ? a.z : 0.f, in ? a.w : 0.f);
+        }
+      }
+    }
+  }
+  float k[9][4], bi[4];
+  {
+    float wvv[36];
+#pragma unroll
+    for (int e = 0; e < 9; ++e) {
+      const float4 w4 = ld4(wt + c * 9 + 4 * e);
+      wvv[4 * e] = w4.x; wvv[4 * e + 1] = w4.y; wvv[4 * e + 2] = w4.z; wvv[4 * e + 3] = w4.w;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int tp = 0; tp < 9; ++tp) k[tp][j] = wvv[j * 9 + (flip ? 8 - tp : tp)];
+    const float4 b4 = bias ? ld4(bias + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    bi[0] = b4.x; bi[1] = b4.y; bi[2] = b4.z; bi[3] = b4.w;
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  const int w = w0 + p;
+  const bool wok = w < g.W;
+  float a0[4] = {0.f, 0.f, 0.f, 0.f}, a1[4] = {0.f, 0.f, 0.f, 0.f};
+  double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+  float c1[4] = {0.f, 0.f, 0.f, 0.f}, c2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int r = 0; r < IRB; ++r) {
+    float row[3][4];
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx) {
+      const float4 a = tile[(r * IP + p + dx) * TCQ + q];
+      row[dx][0] = a.x; row[dx][1] = a.y; row[dx][2] = a.z; row[dx][3] = a.w;
+    }
+    const int ho = hbeg + r - 2;  // output row input row r completes (r >= 2)
+    const bool on = wok && r >= 2 && ho < hend;
+    float o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float acc = a0[e], mid = a1[e], nxt = bi[e];
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) {
+        acc = fmaf(k[6 + dx][e], row[dx][e], acc);
+        mid = fmaf(k[3 + dx][e], row[dx][e], mid);
+        nxt = fmaf(k[dx][e], row[dx][e], nxt);
+      }
+      a0[e] = mid;
+      a1[e] = nxt;
+      acc = rnd<T>(acc);  // statistics of the stored value
+      o[e] = acc;
+      const float am = on ? acc : 0.f;
+      c1[e] += am;
+      c2[e] = fmaf(am, am, c2[e]);
+    }
+    if (r >= 2) {
+      const unsigned off = on ? (unsigned)(((ho * g.W + w) * g.C + c) * (int)sizeof(T)) : ACC_OOB;
+      bufq_st<2>(rz, off, make_float4(o[0], o[1], o[2], o[3]), (T*)nullptr);
+      if ((r - 2) % CR == CR - 1 || r == IRB - 1) {  // the strip kernel's 4-row groups
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          s1[e] += (double)c1[e];
+          s2[e] += (double)c2[e];
+          c1[e] = 0.f;
+          c2[e] = 0.f;
+        }
+      }
+    }
+  }
+  if (stats) {
+    __syncthreads();
+    double v[8] = {s1[0], s1[1], s1[2], s1[3], s2[0], s2[1], s2[2], s2[3]};
+    if (block_slot_reduce<TCQ, 8, double>(v, reinterpret_cast<double*>(tile))) {
+      const long row = (long)srow * 2 * g.C;
+      const int cc = c0 + 4 * threadIdx.x;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        stats[row + cc + e] = v[e];
+        stats[row + g.C + cc + e] = v[4 + e];
+      }
+    }
+  }
+}
+
 template <int TCQ, typename T>
 __global__ void __launch_bounds__(256)
 dw3x3_tile_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dz,
@@ -1904,6 +2062,20 @@ static int dw_xl() {
   return v;
 }
 
+// K1 one-shot block tiles (dw3x3_blk_fwd_kernel): 0 = off, 8 or 16 = output rows per
+// block for the 32-channel tiles (ACCUNET_DW_BLK, tuning knob / A/B). The strip length of
+// every forward-type launch of those shapes (the BN-backward data gradient too, so the
+// statistics rows agree) is then R.
+static int dw_blk() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ACCUNET_DW_BLK");
+    v = e ? atoi(e) : 0;
+    if (v != 8 && v != 16) v = 0;
+  }
+  return v;
+}
+
 static int dw_rch_max() {
   static int v = -1;
   if (v < 0) {
@@ -1925,6 +2097,8 @@ static DwTGeom dw_tgeom(int B, int H, int W, int C, int tcq, dim3* grid, int rch
   static const char* force = getenv("ACCUNET_DW_RCH_FORCE");  // tuning knob (tools/kbench)
   if (force && rch_max > 1) {
     rch = atoi(force) > 0 ? atoi(force) : 1;
+  } else if (rch_max > 1 && tcq == 8 && dw_blk()) {
+    rch = dw_blk() / DW_TR;  // one-shot block tiles
   } else {
       // the longest strips (powers of two) that still give >= 4 rounds of 3 resident
       // blocks per CU (3072 blocks): 16x256x256x96 fp32 rch 1/2/4/8/16 = 180/159/154/155/
@@ -1967,6 +2141,7 @@ extern "C" int accunet_dw3x3_variant(int B, int H, int W, int C, int dt) {
   (void)B;
   if (dw_span_nt(H, W, C)) return 2;
   const int tcq = dw_tile_tcq(H, W, C, dt);
+  if (tcq == 8 && dw_blk()) return 5;
   if (tcq == 8 && dt == ACC_F32 && dw_xl()) return 4;
   if ((tcq == 8 && dt == ACC_F32 && (dw_dma() & 1)) || (tcq && dt == ACC_BF16 && (dw_dma() & 2)))
     return 3;
@@ -2036,6 +2211,27 @@ extern "C" int accunet_dw3x3_fwd(const void* x, const float* wt, const float* bi
     if (dw_cgfast() && grid.y > 1) {
       tg.cgf = (int)grid.y;
       grid = dim3(grid.x * grid.y, 1);
+    }
+    if (tcq == 8 && !bz && dw_blk() && tg.rch * DW_TR == dw_blk()) {
+      auto lb = [&](auto tag, auto rc, auto auxc) {
+        using T = decltype(tag);
+        hipLaunchKernelGGL((dw3x3_blk_fwd_kernel<decltype(rc)::value, decltype(auxc)::value, T>),
+                           grid, dim3(256), 0, s, (const T*)x, wt, bias, sc, sh, act, flip, (T*)z,
+                           stats, tg);
+      };
+      using R16 = std::integral_constant<int, 16>;
+      using R8 = std::integral_constant<int, 8>;
+      using A2 = std::integral_constant<int, 2>;
+      using A0 = std::integral_constant<int, 0>;
+      if (with_dt(dt, [&](auto tag) {
+            if (dw_blk() == 16) {
+              if (tg.ntl) lb(tag, R16{}, A2{}); else lb(tag, R16{}, A0{});
+            } else {
+              if (tg.ntl) lb(tag, R8{}, A2{}); else lb(tag, R8{}, A0{});
+            }
+          }))
+        return ACC_EBADARG;
+      return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
     }
     if (dt == ACC_F32 && tcq == 8 && !bz && dw_xl()) {
       if (tg.ntl)
