@@ -1148,162 +1148,6 @@ dw3x3_dma_bf16_fwd_kernel(const bf16_t* __restrict__ x, const float* __restrict_
 }
 
 // ----------------------------------------------------------------------------
-// K1 cross-lane strip (ACCUNET_DW_XL): the tile of the strip kernel (32 px x 32 ch x a
-// strip of rows), but each wave owns 8 pixels x 8 channel quads (a 128-B segment per
-// pixel: 8 whole lines per load) and walks the strip on its own, PF input rows of loads
-// in flight in registers (its 64 quads + the two halo pixels on lanes 0..15). Per input
-// row the wave activates what it loaded (prologue BN + LeakyReLU, zero padding after the
-// activation), parks it in its own 10-pixel LDS row and reads back the left / right
-// neighbours: LDS operations of one wave execute in order, so no block barrier is ever
-// taken inside the strip (the strip kernel takes two per 4-row chunk). The 3x3 window
-// is a pair of rolling row accumulators (bias, then taps row-major: the FMA order of
-// the strip kernel, whose results and statistics this kernel reproduces bit for bit).
-// ----------------------------------------------------------------------------
-template <int PF, int AUX>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
-dw3x3_xl_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
-                    const float* __restrict__ bias, const float* __restrict__ sc,
-                    const float* __restrict__ sh, int act, int flip, float* __restrict__ z,
-                    double* __restrict__ stats, DwTGeom g) {
-  constexpr int TCQ = 8, TP = 32, CR = 4;
-  __shared__ float4 xrow[4 * 80];  // per wave: 10 pixels x 8 quads (activated)
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wv = tid >> 6;
-  const int p = lane >> 3, q = lane & 7;
-  int t = dw_tile_id(g);
-  int cg = blockIdx.y;
-  if (g.cgf) {
-    cg = t % g.cgf;
-    t /= g.cgf;
-  }
-  const int srow = g.cgf ? t : (int)blockIdx.x;
-  const int c0 = cg * TCQ * 4;
-  const int c = c0 + 4 * q;
-  const int tw = t % g.tilesW;
-  t /= g.tilesW;
-  const int th = t % g.tilesH;
-  const int b = t / g.tilesH;
-  const int hbeg = th * DW_TR * g.rch, w0 = tw * TP;
-  const int hend = min(g.H, hbeg + DW_TR * g.rch);
-  const long img = (long)b * g.H * g.W * g.C;
-  const unsigned ibytes = (unsigned)(g.H * g.W * g.C * 4);
-  const __amdgpu_buffer_rsrc_t rx = acc_rsrc(x + img, ibytes);
-  const __amdgpu_buffer_rsrc_t rz = acc_rsrc(z + img, ibytes);
-  const int w = w0 + 8 * wv + p;  // this lane's pixel
-  const bool wok = w < g.W;
-  const int hpx = lane < 8 ? w0 + 8 * wv - 1 : w0 + 8 * wv + 8;  // halo lanes' pixel
-  const bool hok = lane < 16 && hpx >= 0 && hpx < g.W;
-  const bool pro = sc != nullptr;
-  const float4 ps = pro ? ld4(sc + c) : make_float4(1.f, 1.f, 1.f, 1.f);
-  const float4 pb = pro ? ld4(sh + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-  float k[9][4], bi[4];
-  {
-    float wvv[36];
-#pragma unroll
-    for (int e = 0; e < 9; ++e) {
-      const float4 w4 = ld4(wt + c * 9 + 4 * e);
-      wvv[4 * e] = w4.x; wvv[4 * e + 1] = w4.y; wvv[4 * e + 2] = w4.z; wvv[4 * e + 3] = w4.w;
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int tp = 0; tp < 9; ++tp) k[tp][j] = wvv[j * 9 + (flip ? 8 - tp : tp)];
-    const float4 b4 = bias ? ld4(bias + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-    bi[0] = b4.x; bi[1] = b4.y; bi[2] = b4.z; bi[3] = b4.w;
-  }
-  // input rows hbeg - 1 .. hend (n_in of them); row i = hbeg - 1 + i
-  const int n_in = hend - hbeg + 2;
-  auto ldrow = [&](int i, float4& m, float4& hv) {
-    const int h = hbeg - 1 + i;
-    const bool rin = i < n_in && h >= 0 && h < g.H;
-    m = bufq_ld<AUX>(rx, (rin && wok) ? (unsigned)(((h * g.W + w) * g.C + c) * 4) : ACC_OOB,
-                     (const float*)nullptr);
-    hv = bufq_ld<AUX>(rx, (rin && hok) ? (unsigned)(((h * g.W + hpx) * g.C + c) * 4) : ACC_OOB,
-                      (const float*)nullptr);
-  };
-  float4 mm[PF], hh[PF];
-#pragma unroll
-  for (int j = 0; j < PF; ++j) ldrow(j, mm[j], hh[j]);
-  // retire the weight / prologue loads now (left pending they would be merged into the
-  // loop's wait state and drain the prefetched rows at the first use), not the rows
-  __builtin_amdgcn_s_waitcnt((2 * PF & 15) | (((2 * PF) >> 4) << 14) | (7 << 4) | (15 << 8));
-  auto actv = [&](float4 v, bool in) {
-    v.x = apply_act(v.x * ps.x + pb.x, act);
-    v.y = apply_act(v.y * ps.y + pb.y, act);
-    v.z = apply_act(v.z * ps.z + pb.z, act);
-    v.w = apply_act(v.w * ps.w + pb.w, act);
-    return make_float4(in ? v.x : 0.f, in ? v.y : 0.f, in ? v.z : 0.f, in ? v.w : 0.f);
-  };
-  float4* xr = xrow + wv * 80;
-  float a0[4] = {0.f, 0.f, 0.f, 0.f}, a1[4] = {0.f, 0.f, 0.f, 0.f};
-  double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
-  float c1[4] = {0.f, 0.f, 0.f, 0.f}, c2[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int i0 = 0; i0 < n_in; i0 += PF) {
-#pragma unroll
-    for (int j = 0; j < PF; ++j) {
-      const int i = i0 + j;
-      const int h = hbeg - 1 + i;
-      const bool rin = i < n_in && h >= 0 && h < g.H;
-      const float4 m = actv(mm[j], rin && wok);
-      const float4 hv = actv(hh[j], rin && hok);
-      ldrow(i + PF, mm[j], hh[j]);  // the row PF ahead into the freed registers
-      xr[(p + 1) * 8 + q] = m;
-      if (lane < 16) xr[(lane < 8 ? 0 : 72) + q] = hv;
-      const float4 lf = xr[p * 8 + q], rt = xr[(p + 2) * 8 + q];
-      const float row[3][4] = {{lf.x, lf.y, lf.z, lf.w}, {m.x, m.y, m.z, m.w},
-                               {rt.x, rt.y, rt.z, rt.w}};
-      // input row i completes output row h - 1 (i >= 2), advances h, starts h + 1
-      const int ho = h - 1;
-      const bool on = wok && i >= 2 && ho < hend;
-      float o[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float acc = a0[e], mid = a1[e], nxt = bi[e];
-#pragma unroll
-        for (int dx = 0; dx < 3; ++dx) {
-          acc = fmaf(k[6 + dx][e], row[dx][e], acc);
-          mid = fmaf(k[3 + dx][e], row[dx][e], mid);
-          nxt = fmaf(k[dx][e], row[dx][e], nxt);
-        }
-        a0[e] = mid;
-        a1[e] = nxt;
-        o[e] = acc;
-        const float am = on ? acc : 0.f;
-        c1[e] += am;
-        c2[e] = fmaf(am, am, c2[e]);
-      }
-      const unsigned off = on ? (unsigned)(((ho * g.W + w) * g.C + c) * 4) : ACC_OOB;
-      bufq_st<2>(rz, off, make_float4(o[0], o[1], o[2], o[3]), (float*)nullptr);
-      // the strip kernel folds its fp32 statistics into fp64 once per 4-row chunk of
-      // output rows (rows hbeg + 4k .. +3): the same grouping here
-      if (i >= 2 && ((ho - hbeg) % CR == CR - 1 || ho == hend - 1)) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          s1[e] += (double)c1[e];
-          s2[e] += (double)c2[e];
-          c1[e] = 0.f;
-          c2[e] = 0.f;
-        }
-      }
-    }
-  }
-  __builtin_amdgcn_s_waitcnt(0);
-  if (stats) {
-    __syncthreads();
-    double v[8] = {s1[0], s1[1], s1[2], s1[3], s2[0], s2[1], s2[2], s2[3]};
-    if (block_slot_reduce<TCQ, 8, double>(v, reinterpret_cast<double*>(xrow))) {
-      const long row = (long)srow * 2 * g.C;
-      const int cc = c0 + 4 * threadIdx.x;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        stats[row + cc + e] = v[e];
-        stats[row + g.C + cc + e] = v[4 + e];
-      }
-    }
-  }
-}
-
-// ----------------------------------------------------------------------------
 // K1 one-shot block tiles (ACCUNET_DW_BLK = R): a block loads its whole (R+2)-row halo
 // tile of 34 px x 8 quads at once (every load in flight together), activates it into
 // LDS, takes ONE barrier and computes its R output rows (rolling row accumulators, the
@@ -2051,17 +1895,6 @@ static int dw_dma() {
   return v;
 }
 
-// K1 cross-lane strip (dw3x3_xl_fwd_kernel) for the fp32 32-channel tiles without a
-// BN-backward epilogue (ACCUNET_DW_XL, tuning knob / A/B; default off)
-static int dw_xl() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("ACCUNET_DW_XL");
-    v = e ? atoi(e) : 0;
-  }
-  return v;
-}
-
 // K1 one-shot block tiles (dw3x3_blk_fwd_kernel): 0 = off, 8 or 16 = output rows per
 // block for the 32-channel tiles (ACCUNET_DW_BLK, tuning knob / A/B). The strip length of
 // every forward-type launch of those shapes (the BN-backward data gradient too, so the
@@ -2142,7 +1975,6 @@ extern "C" int accunet_dw3x3_variant(int B, int H, int W, int C, int dt) {
   if (dw_span_nt(H, W, C)) return 2;
   const int tcq = dw_tile_tcq(H, W, C, dt);
   if (tcq == 8 && dw_blk()) return 5;
-  if (tcq == 8 && dt == ACC_F32 && dw_xl()) return 4;
   if ((tcq == 8 && dt == ACC_F32 && (dw_dma() & 1)) || (tcq && dt == ACC_BF16 && (dw_dma() & 2)))
     return 3;
   return tcq ? 1 : 0;
@@ -2231,15 +2063,6 @@ extern "C" int accunet_dw3x3_fwd(const void* x, const float* wt, const float* bi
             }
           }))
         return ACC_EBADARG;
-      return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
-    }
-    if (dt == ACC_F32 && tcq == 8 && !bz && dw_xl()) {
-      if (tg.ntl)
-        hipLaunchKernelGGL((dw3x3_xl_fwd_kernel<4, 2>), grid, dim3(256), 0, s, (const float*)x, wt,
-                           bias, sc, sh, act, flip, (float*)z, stats, tg);
-      else
-        hipLaunchKernelGGL((dw3x3_xl_fwd_kernel<4, 0>), grid, dim3(256), 0, s, (const float*)x, wt,
-                           bias, sc, sh, act, flip, (float*)z, stats, tg);
       return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
     }
     if (dt == ACC_BF16 && !bz && (dw_dma() & 2)) {

@@ -166,7 +166,8 @@ int accunet_reduce_stats(const double* part, int R, int C, double* out2C, double
 int accunet_dw3x3_rows(int B, int H, int W, int C, int dt);
 /* Which forward kernel runs for the shape and storage dtype dt (without bz): 1 = LDS
  * tile kernel (C % 32 == 0), 0 = register-window kernel; 3 = the LDS-DMA ring kernel
- * (fp32 32-channel tiles, ACCUNET_DW_DMA); 2 = whole-pixel span kernel, only with the
+ * (ACCUNET_DW_DMA), 5 = one-shot block tiles (ACCUNET_DW_BLK), both tuning knobs for
+ * 32-channel tiles, off by default; 2 = whole-pixel span kernel, only with the
  * tuning knob ACCUNET_DW_SPAN bit 2 set (off by default) and then for C % 8 == 0,
  * C/4 <= 64. */
 int accunet_dw3x3_variant(int B, int H, int W, int C, int dt);
