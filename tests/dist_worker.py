@@ -74,6 +74,18 @@ def run(mode, sd, data, dev):
     return flat_params(m), losses
 
 
+def grads_one_step(sd, batch, dev, wire):
+    """the all-reduced fp32 gradient vector after one graph-mode step (bucket wire format
+    `wire`): p.grad are the views of the bucket buffer the optimizer read"""
+    m = ACC_UNet(3, 1, n_filts=8)
+    m.load_state_dict(sd)
+    m = m.to(dev).train()
+    step = TrainStep(m, lr=1e-3, graph=True, bucket_mb=0.25, comm_dtype=wire)
+    step(*batch)
+    torch.cuda.synchronize()
+    return torch.cat([p.grad.detach().reshape(-1).double() for p in m.parameters()])
+
+
 def main():
     rank, world = adist.init_from_env()
     assert world == 2, world
@@ -106,14 +118,18 @@ def main():
     d = float((out["trainer"][0] - out["eager"][0]).abs().max())
     print(f"rank {rank} trainer vs eager max|dp| {d:.3e}", flush=True)
     assert d < 1e-5, d
-    # bf16 buckets: every gradient rounded once to bf16 and summed in bf16; after 3 Adam
-    # steps (lr 1e-3, updates ~lr * g / |g|) the parameters sit within a few bf16
-    # relative roundings of an lr-sized update from the fp32-bucket run
-    d = float((out["graph_wire16"][0] - out["graph"][0]).abs().max())
+    # bf16 buckets: the all-reduced gradient of one step (each rank's gradient rounded to
+    # bf16 when packed, the pair summed in bf16 by the collective, then halved) against
+    # the fp32-bucket run's: within a few bf16 roundings, in norm. (Parameters after
+    # several Adam steps are no yardstick: Adam turns the rounding of near-zero gradients
+    # into lr-sized steps of either sign.)
+    g32, g16 = grads_one_step(sd, data[0], dev, None), grads_one_step(sd, data[0], dev, "bf16")
+    rel = float((g16 - g32).norm() / g32.norm())
     dl = max(abs(a - b) for a, b in zip(out["graph_wire16"][1], out["graph"][1]))
-    print(f"rank {rank} graph_wire16 vs graph max|dp| {d:.3e} max|dloss| {dl:.3e}", flush=True)
-    assert d <= 3 * 1e-3 * 2 ** -4, d
-    assert dl <= 1e-3 * abs(out["graph"][1][-1]) + 1e-6, dl
+    print(f"rank {rank} bf16-bucket gradient vs fp32 buckets: rel {rel:.3e}; 3-step max|dloss| "
+          f"{dl:.3e}", flush=True)
+    assert 0 < rel <= 2 ** -7, rel
+    assert dl <= 1e-2 * abs(out["graph"][1][-1]), dl
     dist.barrier()
     dist.destroy_process_group()
     if rank == 0:
