@@ -9,13 +9,9 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 120 tools/k1lab 20 > gpurun_out/k1lab.txt 2>&1 || { cat gpurun_out/k1lab.txt; exit 1; }
 cat gpurun_out/k1lab.txt
-for v in 0 3 0 3; do
+for v in 0 3; do
   ACCUNET_DW_DMA=$v timeout -k 10 120 tools/kbench 20 > gpurun_out/kbench_dma$v.txt 2>&1 || { cat gpurun_out/kbench_dma$v.txt; exit 1; }
   echo "== ACCUNET_DW_DMA=$v"; grep "K1 dw3x3_fwd 16x\|K1 checksum\|copy float4\|flip\|K1 bf16" gpurun_out/kbench_dma$v.txt
-done
-for f in 2 4 8 16; do
-  ACCUNET_DW_DMA=3 ACCUNET_DW_RCH_FORCE=$f timeout -k 10 120 tools/kbench 20 > gpurun_out/kbench_dma_rch$f.txt 2>&1 || { cat gpurun_out/kbench_dma_rch$f.txt; exit 1; }
-  echo "== DMA rch $f (strip $((8 * f)) rows)"; grep "K1 dw3x3_fwd 16x\|K1 bf16" gpurun_out/kbench_dma_rch$f.txt
 done
 ACCUNET_DW_DMA=3 timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread -k "dw3x3" > gpurun_out/dw_dma_tests.log 2>&1 || { tail -30 gpurun_out/dw_dma_tests.log; exit 1; }
 tail -n 2 gpurun_out/dw_dma_tests.log
