@@ -108,7 +108,16 @@ def k1_dw3x3(B, H, W, C, weight, bias, iters=20, device="cuda", dtype=torch.floa
         kern.dw3x3_fwd(x, w, b, sc, sh, 1, 0, z, st, B, H, W, C)
     t = _time(run, iters)
     name = kern.dw3x3_kernel_name(B, H, W, C, x)
-    return _hbm_row(name, f"{B}x{H}x{W}x{C}", 2.0 * x.element_size() * B * H * W * C, t, iters)
+    row = _hbm_row(name, f"{B}x{H}x{W}x{C}", 2.0 * x.element_size() * B * H * W * C, t, iters)
+    # context for the rate: a plain device copy of the same bytes (x read once, z written
+    # once, ATen's vectorised copy) timed the same way right after K1, so the line shows
+    # what streaming reaches on this GPU in this state (the clocks under sustained load
+    # move both; tools/kbench times both on a rested GPU)
+    c_us, c_per = _time(lambda: z.copy_(x), iters)
+    row["copy_us"] = round(c_us, 2)
+    row["copy_median_us"] = round(statistics.median(c_per), 2)
+    row["frac_of_copy"] = round(c_us / t[0], 4)
+    return row
 
 
 def k3_se(B, H, W, C, se_mod, iters=20, device="cuda", dtype=torch.float32):

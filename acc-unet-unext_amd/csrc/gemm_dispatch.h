@@ -130,6 +130,11 @@ GEMM_DECLARE_TABLE(g_bgemm_col_nnsh3)
 int gemm_run(GemmParams p, int amode, int bmode, int pro_a, int pro_b, bool allow_split,
              float* ws, size_t ws_elems, int adt, int bdt, int cdt, hipStream_t stream);
 
+// ResPath 3x3 over 32 channels as a halo-tile direct convolution (csrc/conv3x3.hip):
+// ACC_OK / an error when it ran the launch, -1 when the GEMM engine should
+int conv3x3_c32_try(const GemmParams& p, int amode, int bmode, int pro_a, int pro_b, int epi,
+                    bool fp32, int tile, hipStream_t stream);
+
 // Skinny weight-gradient path (csrc/gemm_skinny.hip): returns the number of
 // [M][N] partial slabs written into ws (to be summed by the split-K reduction),
 // or 0 when the shape does not qualify.

@@ -30,6 +30,11 @@
 #ifndef GG_STAGES
 #define GG_STAGES 3
 #endif
+// narrow tiles (128x32: 8 MFMAs per wave and k-tile, 10 KB per stage) run a deeper ring,
+// so the k-tiles in flight per CU cover the load latency (A/B knob)
+#ifndef GG_STAGES_NARROW
+#define GG_STAGES_NARROW 3
+#endif
 
 static __device__ __attribute__((aligned(16))) float g_gemm_zero16[4];
 
@@ -53,6 +58,17 @@ template <int N>
 ACC_DEV void gg_wait_vm() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+// s_waitcnt vmcnt(ahead * GPW) for a run-time ahead in [0, MAXA]
+template <int GPW, int MAXA>
+ACC_DEV void gg_wait_ahead(int ahead) {
+  if constexpr (MAXA > 0) {
+    if (ahead >= MAXA) { gg_wait_vm<MAXA * GPW>(); return; }
+    gg_wait_ahead<GPW, MAXA - 1>(ahead);
+  } else {
+    gg_wait_vm<0>();
+  }
 }
 
 // LDS image of one operand tile (R = BM or BN):
@@ -80,7 +96,8 @@ gemm_f32g_kernel(const GemmParams p) {
   constexpr int AF = BM * BK, BF = BN * BK;              // floats per stage and operand
   constexpr int CF = (AMODE == AM_ROW && PRO_A != PRO_NONE) ? 2 * BK : 0;  // A prologue
   constexpr int SF = AF + BF + CF;
-  constexpr int RING = GG_STAGES * SF;
+  constexpr int STG = BN == 32 ? GG_STAGES_NARROW : GG_STAGES;
+  constexpr int RING = STG * SF;
   constexpr int EPF = gemm_epi_floats<WM, TM, TN>();
   constexpr int LDS_F = RING > EPF ? RING : EPF;
   // 16-B pieces per wave and stage (BK = 16): A: BM, B: BN
@@ -88,8 +105,8 @@ gemm_f32g_kernel(const GemmParams p) {
   constexpr int IA = (PWA + 63) / 64, IB = (PWB + 63) / 64, IC = CF ? 1 : 0;
   constexpr int GPW = IA + IB + IC;  // DMA instructions per wave and stage
   static_assert(BK == 16, "the chunk swizzle assumes 4 chunks per row");
-  static_assert(GG_STAGES >= 2 && GG_STAGES <= 4, "the vmcnt ladder covers up to 3 tiles ahead");
-  static_assert(3 * GPW < 64, "vmcnt range");
+  static_assert(STG >= 2 && STG <= 8, "the vmcnt ladder covers up to 7 tiles ahead");
+  static_assert((STG - 2) * GPW < 64, "vmcnt range");
   static_assert(PWA % 64 == 0 || PWA < 64, "A pieces per wave");
   static_assert(PWB % 64 == 0 || PWB < 64, "B pieces per wave");
   static_assert(PRO_A == PRO_NONE || AMODE == AM_ROW, "A prologue: row-major A only");
@@ -303,7 +320,7 @@ gemm_f32g_kernel(const GemmParams p) {
     }
   };
 
-  constexpr int D = GG_STAGES - 1;  // k-tiles in flight ahead of the computed one
+  constexpr int D = STG - 1;  // k-tiles in flight ahead of the computed one
   if (nkt > 0) {
 #pragma unroll
     for (int s = 0; s < D; ++s)
@@ -312,15 +329,12 @@ gemm_f32g_kernel(const GemmParams p) {
       // this wave's DMA of tile kt has landed (the up to D-1 later tiles may still be
       // in flight: their GPW instructions each are the newest in the counter) ...
       const int ahead = min(D - 1, nkt - 1 - kt);
-      if (ahead >= 3) gg_wait_vm<3 * GPW>();
-      else if (ahead == 2) gg_wait_vm<2 * GPW>();
-      else if (ahead == 1) gg_wait_vm<GPW>();
-      else gg_wait_vm<0>();
+      gg_wait_ahead<GPW, D - 1>(ahead);
       // ... and so has every wave's once all pass the barrier; the barrier also
       // retires every read of the buffer that tile kt+D overwrites (computed at kt-1)
       __builtin_amdgcn_s_barrier();
-      if (kt + D < nkt) stage(kt + D, (kt + D) % GG_STAGES);
-      compute(kt, kt % GG_STAGES);
+      if (kt + D < nkt) stage(kt + D, (kt + D) % STG);
+      compute(kt, kt % STG);
     }
   }
   gemm_epilogue<float, EPI, WM, TM, TN>(p, acc, smem, m0, n0);

@@ -360,6 +360,11 @@ int gemm_run(GemmParams p, int amode, int bmode, int pro_a, int pro_b, bool allo
       if ((p.upld[u] % 4) || ((uintptr_t)p.up[u] & cal)) ev = false;
     p.evec = ev ? 1 : 0;
   }
+  if (S == 1) {
+    const int r = conv3x3_c32_try(p, amode, bmode, pro_a, pro_b, epi,
+                                  vec && adt == ACC_F32 && bdt == ACC_F32 && cdt == ACC_F32, t, stream);
+    if (r >= 0) return r;
+  }
   p.ngrp = 0;
   if (S == 1 && gy > 1 && ngrp_kb() > 0) {
     const long per_tile = (long)p.K * BN * (bdt == ACC_BF16 ? 2 : 4);  // B bytes per N tile

@@ -159,6 +159,48 @@ def test_conv3x3_fwd_dgrad_wgrad(B, H, W, Ci, Co):
     assert rel(dw, refw) < 1e-5
 
 
+@pytest.mark.parametrize("B,H,W,Co", [(2, 64, 128, 32), (3, 40, 256, 64), (16, 256, 256, 32)])
+def test_conv3x3_halo_kernel_c32(B, H, W, Co):
+    """The halo-tile 3x3 kernel (csrc/conv3x3.hip; 32 input channels, image rows of whole
+    128-pixel tiles: the first ResPath level): forward with bias and the fp64 statistics
+    rows (one per 128-pixel tile, as the implicit GEMM's), and the data gradient
+    accumulated in place onto C (the residual's gradient), against float64 torch."""
+    torch.manual_seed(14)
+    Ci = 32
+    x = torch.randn(B, Ci, H, W, device=DEV, dtype=torch.float64, requires_grad=True)
+    w = torch.randn(Co, Ci, 3, 3, device=DEV, dtype=torch.float64, requires_grad=True) * 0.1
+    w.retain_grad()
+    bias = torch.randn(Co, device=DEV, dtype=torch.float64)
+    y = F.conv2d(x, w, bias, padding=1)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    P = B * H * W
+    xn = x.detach().permute(0, 2, 3, 1).reshape(P, Ci).float().contiguous()
+    wr = w.detach().permute(0, 2, 3, 1).reshape(Co, 9 * Ci).float().contiguous()
+    out = torch.empty(P, Co, device=DEV)
+    rows = kern.gemm_stats_rows(P, Co, 9 * Ci, _lib.AMODE_SHIFT3, _lib.BMODE_NT, Ci)
+    assert rows == P // 128  # >= 128 tiles: the engine's 128x32 tiles, the halo kernel's
+    st = torch.zeros(rows, 2, Co, device=DEV, dtype=torch.float64)
+    kern.gemm(P, Co, 9 * Ci, a=[xn], lda=[Ci], amode=_lib.AMODE_SHIFT3, b=wr, ldb=9 * Ci,
+              c=out, ldc=Co, bias=bias.float(), stats=st, H=H, W=W, cin=Ci)
+    ref = y.detach().permute(0, 2, 3, 1).reshape(P, Co)
+    assert rel(out, ref) < 1e-5
+    s = st.sum(0)
+    o = out.double()
+    assert torch.allclose(s[0], o.sum(0), rtol=1e-9, atol=1e-6)
+    assert torch.allclose(s[1], (o * o).sum(0), rtol=1e-9, atol=1e-6)
+    # data gradient (Co = 32 only: the halo kernel's input is 32-channel) onto C in place
+    if Co == 32:
+        gyn = gy.permute(0, 2, 3, 1).reshape(P, Co).float().contiguous()
+        wf = w.detach().flip(2, 3).permute(1, 2, 3, 0).reshape(Ci, 9 * Co).float().contiguous()
+        r = torch.randn(P, Ci, device=DEV)
+        dx = r.clone()
+        kern.gemm(P, Ci, 9 * Co, a=[gyn], lda=[Co], amode=_lib.AMODE_SHIFT3, b=wf, ldb=9 * Co,
+                  c=dx, ldc=Ci, H=H, W=W, cin=Co, ups=[(dx, Ci, 0, 0)])
+        refx = x.grad.permute(0, 2, 3, 1).reshape(P, Ci) + r.double()
+        assert rel(dx, refx) < 1e-5
+
+
 @pytest.mark.parametrize("M,N,K,lda,pro_b", [(32, 32, 1 << 20, 32, 0), (32, 32, 100003, 48, 1),
                                              (32, 96, 40000, 64, 2), (96, 32, 65536, 96, 0),
                                              (64, 32, 20000, 80, 2), (32, 64, 16384, 32, 1),
