@@ -8,16 +8,15 @@
 // nine times, and the 128x32 tile does 8 MFMAs per 16-k stage (0.40 of fp32 MFMA at
 // 1048576x32x288, profiles/r04_*).
 //
-// Here a workgroup owns 128 consecutive output pixels of one image row (W % 128 == 0)
-// and all 32 output channels of its column block:
-//   * the halo (3 input rows x 130 pixels x 32 channels) is staged once per tile: each
-//     input pixel goes to LDS ~3.05 times instead of 9; out-of-image slots are zeroed at
-//     staging, so the main loop has no masks;
-//   * the 36 KB weight block is read into registers per tile (9 taps x 8 channel
-//     quads: 36 float4 per lane, L2-resident), alongside the halo, which goes global ->
-//     LDS by LDS-DMA (no staging registers); workgroups are persistent over a
-//     contiguous run of tiles (neighbouring halos share input rows in L2) and the second
-//     resident workgroup of the CU computes while one stages;
+// Here a workgroup owns a column strip of 128 pixels (W % 128 == 0) of one image and a
+// run of its output rows, walked top to bottom, for 32 output channels:
+//   * a ring of 3 input rows (130 pixels x 32 channels each, padded slots) sits in LDS;
+//     each output row needs one new input row, which streams in (LDS-DMA) into the
+//     slot of the row just finished while the last row's taps and the epilogue run, so
+//     an input pixel goes to LDS ~1.02 times instead of the implicit GEMM's 9;
+//     out-of-image pixels are zero-filled at staging, so the main loop has no masks;
+//   * the 36 KB weight block stays in registers for the workgroup's life (9 taps x 8
+//     channel quads: 36 float4 per lane); two workgroups are resident per CU;
 //   * v_mfma_f32_32x32x2_f32, 4 waves x 32 pixels: a lane reads 4 consecutive channels
 //     of its pixel (one ds_read_b128, padded 36-float slots) and feeds 4 MFMAs, pairing
 //     channel 8g + t with 8g + 4 + t, the same pairing for the weights (the engine's k
@@ -41,7 +40,7 @@ static_assert(C3_DMA_LANES <= 64 && (4 * C3_DMA_ROW - 1) * C3_DMA_LANES < C3_ROW
 static __device__ __attribute__((aligned(16))) float g_c3_zero4[4];
 
 template <int EPI>
-__global__ void __launch_bounds__(256, 2) conv3x3_c32_kernel(const GemmParams p, int ntiles) {
+__global__ void __launch_bounds__(256, 2) conv3x3_c32_kernel(const GemmParams p, int rows_per) {
   __shared__ __attribute__((aligned(16))) float hal[C3_HALO_F];
   __shared__ __attribute__((aligned(16))) float epi[gemm_epi_floats<4, 1, 1>()];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -52,39 +51,34 @@ __global__ void __launch_bounds__(256, 2) conv3x3_c32_kernel(const GemmParams p,
   const float* X = (const float*)p.A[0];
   const long ldx = p.lda[0];
 
-  // this workgroup's contiguous run of 128-pixel tiles
-  const int per = (ntiles + gridDim.x - 1) / gridDim.x;
-  const int t0 = blockIdx.x * per;
-  const int t1 = min(ntiles, t0 + per);
-  if (t0 >= t1) return;
+  // this workgroup's strip: 128 columns [w0, w0 + 128) of image b, output rows
+  // [hb, he), walked top to bottom
+  const int cps = (H + rows_per - 1) / rows_per;  // row chunks per column strip
+  const int strip = blockIdx.x / cps, chunk = blockIdx.x - strip * cps;
+  const int nstrip_w = W / C3_BM;
+  const int b = strip / nstrip_w;
+  const int w0 = (strip - b * nstrip_w) * C3_BM;
+  const int hb = chunk * rows_per, he = min(H, hb + rows_per);
+  if (hb >= he) return;
 
-  // halo of tile mt -> LDS by LDS-DMA (global_load_lds_dwordx4, lane-linear 16-B
-  // pieces): piece e = (slot, k), slot = dh*130 + j holds input pixel
-  // (h + dh - 1, w0 - 1 + j) of the tile's image row, k < 8 its channel quads, k = 8 the
-  // slot's padding; the zero page outside the image and for the padding
-  auto dma = [&](int mt) {
-    const int m0 = mt * C3_BM;
-    const uint32_t q = fdiv((uint32_t)m0, p.fW);  // image row index b*H + h
-    const int w0 = m0 - (int)q * W;
-    const int h = (int)(q - fdiv(q, p.fH) * H);
-#pragma unroll
-    for (int dh = 0; dh < 3; ++dh) {  // input row by input row (waited for in that order)
-      const int hh = h + dh - 1;
-      const bool rok = hh >= 0 && hh < H;
-      const float* xrow = X + (long)((int)q + dh - 1) * W * ldx;
+  // input row r (-1 .. H) of the strip -> ring slot r mod 3 by LDS-DMA
+  // (global_load_lds_dwordx4, lane-linear 16-B pieces): piece e = (j, k), slot pixel j
+  // holds input pixel (r, w0 - 1 + j), k < 8 its channel quads, k = 8 the padding; the
+  // zero page outside the image and for the padding. Every wave issues exactly
+  // C3_DMA_ROW instructions per row (the counted waits below rely on it).
+  auto dma_row = [&](int r) {
+    const bool rok = r >= 0 && r < H;
+    const float* xrow = X + ((long)b * H + r) * W * ldx;
+    float* dst = hal + ((r + 3) % 3) * C3_ROW_PIECES * 4;
 #pragma unroll 1
-      for (int u = 0; u < C3_DMA_ROW; ++u) {
-        // C3_DMA_LANES pieces per instruction so that every wave issues exactly
-        // C3_DMA_ROW instructions per row (the counted waits below assume it)
-        const int base = (u * 4 + wave) * C3_DMA_LANES;
-        const int e = base + lane;
-        const int j = e / 9, k = e - j * 9;
-        const int ww = w0 - 1 + j;
-        const bool ok = rok && k < 8 && ww >= 0 && ww < W;
-        const float* src = ok ? xrow + (long)ww * ldx + 4 * k : g_c3_zero4;
-        if (lane < C3_DMA_LANES && e < C3_ROW_PIECES)
-          gg_dma16(src, hal + (dh * C3_ROW_PIECES + base) * 4);
-      }
+    for (int u = 0; u < C3_DMA_ROW; ++u) {
+      const int base = (u * 4 + wave) * C3_DMA_LANES;
+      const int e = base + lane;
+      const int j = e / 9, k = e - j * 9;
+      const int ww = w0 - 1 + j;
+      const bool ok = rok && k < 8 && ww >= 0 && ww < W;
+      const float* src = ok ? xrow + (long)ww * ldx + 4 * k : g_c3_zero4;
+      if (lane < C3_DMA_LANES && e < C3_ROW_PIECES) gg_dma16(src, dst + base * 4);
     }
   };
 
@@ -100,37 +94,45 @@ __global__ void __launch_bounds__(256, 2) conv3x3_c32_kernel(const GemmParams p,
         wr[tap][g] = *reinterpret_cast<const float4*>(wrow + tap * C3_CIN + 8 * g);
   }
   const int px = wave * 32 + l31;  // this lane's output pixel in the tile (A row)
-  for (int mt = t0; mt < t1; ++mt) {
-    __syncthreads();  // every read of the previous halo is done
-    dma(mt);
+
+  auto taps = [&](floatx16& acc, int dh, int r) {  // the 3 taps of input row r
+    const float* a = hal + ((r + 3) % 3) * C3_ROW_PIECES * 4 + px * C3_CS + 4 * lh;
+#pragma unroll
+    for (int dw = 0; dw < 3; ++dw) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 f = *reinterpret_cast<const float4*>(a + dw * C3_CS + 8 * g);
+        const float4 w = wr[dh * 3 + dw][g];
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(f.x, w.x, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(f.y, w.y, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(f.z, w.z, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(f.w, w.w, acc, 0, 0, 0);
+      }
+    }
+  };
+
+  dma_row(hb - 1);
+  dma_row(hb);
+  dma_row(hb + 1);
+  for (int h = hb; h < he; ++h) {
+    // rows h-1 and h have landed (row h+1 may still be in flight) ...
+    gg_wait_vm<C3_DMA_ROW>();
+    __builtin_amdgcn_s_barrier();  // ... in every wave
     floatx16 acc[1][1];
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[0][0][r] = 0.f;
-#pragma unroll
-    for (int dh = 0; dh < 3; ++dh) {
-      // input row dh of this wave has landed (the later rows' 5 instructions each may
-      // still be in flight), and every wave's once all pass the barrier: the taps of row
-      // dh run while rows dh+1.. stream in
-      if (dh == 0) gg_wait_vm<2 * C3_DMA_ROW>();
-      else if (dh == 1) gg_wait_vm<C3_DMA_ROW>();
-      else gg_wait_vm<0>();
-      __builtin_amdgcn_s_barrier();
-#pragma unroll
-      for (int dw = 0; dw < 3; ++dw) {
-        const int tap = dh * 3 + dw;
-        const float* a = hal + (dh * C3_SLOTS + px + dw) * C3_CS + 4 * lh;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const float4 f = *reinterpret_cast<const float4*>(a + 8 * g);
-          const float4 b = wr[tap][g];
-          acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.x, b.x, acc[0][0], 0, 0, 0);
-          acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.y, b.y, acc[0][0], 0, 0, 0);
-          acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.z, b.z, acc[0][0], 0, 0, 0);
-          acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.w, b.w, acc[0][0], 0, 0, 0);
-        }
-      }
-    }
-    gemm_epilogue<float, EPI, 4, 1, 1>(p, acc, epi, mt * C3_BM, n0);
+    taps(acc[0][0], 0, h - 1);
+    taps(acc[0][0], 1, h);
+    // every wave is done with row h-1's slot: row h+2 streams into it during row h+1's
+    // taps and the epilogue
+    __builtin_amdgcn_s_barrier();
+    const bool more = h + 1 < he;
+    if (more) dma_row(h + 2);
+    if (more) gg_wait_vm<C3_DMA_ROW>();
+    else gg_wait_vm<0>();
+    __builtin_amdgcn_s_barrier();  // row h+1 visible
+    taps(acc[0][0], 2, h + 1);
+    gemm_epilogue<float, EPI, 4, 1, 1>(p, acc, epi, (int)(((long)b * H + h) * W + w0), n0);
   }
 }
 
@@ -159,15 +161,19 @@ int conv3x3_c32_try(const GemmParams& p, int amode, int bmode, int pro_a, int pr
     return -1;
   if ((p.lda[0] & 3) || ((uintptr_t)p.A[0] & 15) || (p.ldb & 3) || ((uintptr_t)p.B & 15))
     return -1;
-  const int ntiles = p.M / C3_BM;
-  // two resident workgroups per CU (74.6 KB of LDS each), persistent over their tiles
-  int nwg = 512 / (p.N / 32);
-  if (nwg < 8) nwg = 8;
-  if (nwg > ntiles) nwg = ntiles;
-  dim3 grid(nwg, p.N / 32);
+  // persistent workgroups, two resident per CU (74.6 KB of LDS each): column strips of
+  // 128 pixels cut into row chunks so that there are ~512 per column block
+  const long B = p.M / ((long)p.H * p.W);
+  const long strips = B * (p.W / C3_BM);
+  const int nb = p.N / 32;
+  const long want = 512 / nb > 8 ? 512 / nb : 8;
+  int rows_per = (int)((strips * p.H + want - 1) / want);
+  if (rows_per < 1) rows_per = 1;
+  const long cps = (p.H + rows_per - 1) / rows_per;
+  dim3 grid((unsigned)(strips * cps), nb);
   if (epi & EPI_UPS)
-    hipLaunchKernelGGL(conv3x3_c32_kernel<EPI_UPS>, grid, dim3(256), 0, stream, p, ntiles);
+    hipLaunchKernelGGL(conv3x3_c32_kernel<EPI_UPS>, grid, dim3(256), 0, stream, p, rows_per);
   else
-    hipLaunchKernelGGL(conv3x3_c32_kernel<EPI_STATS>, grid, dim3(256), 0, stream, p, ntiles);
+    hipLaunchKernelGGL(conv3x3_c32_kernel<EPI_STATS>, grid, dim3(256), 0, stream, p, rows_per);
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
