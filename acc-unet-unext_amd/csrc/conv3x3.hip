@@ -177,3 +177,142 @@ int conv3x3_c32_try(const GemmParams& p, int amode, int bmode, int pro_a, int pr
     hipLaunchKernelGGL(conv3x3_c32_kernel<EPI_STATS>, grid, dim3(256), 0, stream, p, rows_per);
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
+
+// ---------------------------------------------------------------------------
+// The weight gradient of the same convolution,
+//   dW[co][tap*32 + ci] = sum_p dY[p][co] * X[shift_tap(p)][ci]      (M 32, N 288, K pixels)
+// (AM_COL x BM_NN_SHIFT3 in the engine: 0.31 of fp32 MFMA, its 32x128 tiles waste a
+// quarter of the 384 columns and re-gather X per tap). Same strips and 3-row X ring as
+// above; per output row a wave takes 32 pixels in pairs (the MFMA k): its dY values
+// (one per lane, lane (co, k)) are loaded once into 16 registers and serve all 9 taps,
+// whose X operand is one ds_read_b32 from the ring (lane (k, ci)). The 9 accumulator
+// tiles (144 registers) sum the workgroup's pixels; at the end the 4 waves are added in
+// wave order through LDS and the workgroup writes one [32][288] slab, which the split-K
+// reduction (gemm_run.hip) sums in slab order: deterministic.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256, 2)
+conv3x3_c32_wgrad_kernel(const GemmParams p, int rows_per, float* __restrict__ slabs) {
+  __shared__ __attribute__((aligned(16))) float hal[C3_HALO_F];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l31 = lane & 31, lh = lane >> 5;
+  const int H = p.H, W = p.W;
+  const float* X = (const float*)p.B;
+  const long ldx = p.ldb;
+  const float* dY = (const float*)p.A[0];
+  const long ldy = p.lda[0];
+
+  const int cps = (H + rows_per - 1) / rows_per;
+  const int strip = blockIdx.x / cps, chunk = blockIdx.x - strip * cps;
+  const int nstrip_w = W / C3_BM;
+  const int b = strip / nstrip_w;
+  const int w0 = (strip - b * nstrip_w) * C3_BM;
+  const int hb = chunk * rows_per, he = min(H, hb + rows_per);
+
+  auto dma_row = [&](int r) {  // as in the forward kernel
+    const bool rok = r >= 0 && r < H;
+    const float* xrow = X + ((long)b * H + r) * W * ldx;
+    float* dst = hal + ((r + 3) % 3) * C3_ROW_PIECES * 4;
+#pragma unroll 1
+    for (int u = 0; u < C3_DMA_ROW; ++u) {
+      const int base = (u * 4 + wave) * C3_DMA_LANES;
+      const int e = base + lane;
+      const int j = e / 9, k = e - j * 9;
+      const int ww = w0 - 1 + j;
+      const bool ok = rok && k < 8 && ww >= 0 && ww < W;
+      const float* src = ok ? xrow + (long)ww * ldx + 4 * k : g_c3_zero4;
+      if (lane < C3_DMA_LANES && e < C3_ROW_PIECES) gg_dma16(src, dst + base * 4);
+    }
+  };
+  // dY of output row h for this wave's pixel pairs: a[i] = dY[pixel w0 + 32 wave + 2i + lh][l31]
+  auto load_dy = [&](int h, float (&a)[16]) {
+    const float* row = dY + (((long)b * H + h) * W + w0 + wave * 32 + lh) * ldy + l31;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) a[i] = row[(long)(2 * i) * ldy];
+  };
+
+  floatx16 acc[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
+  // this lane's X operand: ring slot pixel 32 wave + 2i + lh + dw, channel l31
+  auto taps_row = [&](const float (&a)[16], int dh, int r) {
+    const float* xr = hal + ((r + 3) % 3) * C3_ROW_PIECES * 4 + (wave * 32 + lh) * C3_CS + l31;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+#pragma unroll
+      for (int dw = 0; dw < 3; ++dw)
+        acc[dh * 3 + dw] = __builtin_amdgcn_mfma_f32_32x32x2f32(
+            a[i], xr[(2 * i + dw) * C3_CS], acc[dh * 3 + dw], 0, 0, 0);
+  };
+
+  if (hb < he) {
+    float a[16], an[16];
+    dma_row(hb - 1);
+    dma_row(hb);
+    dma_row(hb + 1);
+    load_dy(hb, a);
+    for (int h = hb; h < he; ++h) {
+      gg_wait_vm<0>();  // rows h-1 .. h+1 and the dY loads have landed ...
+      __builtin_amdgcn_s_barrier();  // ... in every wave
+      taps_row(a, 0, h - 1);
+      __builtin_amdgcn_s_barrier();  // every wave is done with row h-1's slot
+      const bool more = h + 1 < he;
+      if (more) {
+        dma_row(h + 2);  // streams in during rows h, h+1's taps
+        load_dy(h + 1, an);
+      }
+      taps_row(a, 1, h);
+      taps_row(a, 2, h + 1);
+      if (more) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) a[i] = an[i];
+      }
+    }
+  }
+  // the 4 waves' partial tiles summed in wave order, 3 taps per round through the ring
+  __syncthreads();
+  float* slab = slabs + (size_t)blockIdx.x * (32 * 9 * C3_CIN);
+#pragma unroll
+  for (int t0 = 0; t0 < 9; t0 += 3) {
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        hal[((wave * 3 + t) * 32 + ((r & 3) + 8 * (r >> 2) + 4 * lh)) * 32 + l31] = acc[t0 + t][r];
+    __syncthreads();
+    for (int e = tid; e < 3 * 1024; e += 256) {
+      const int t = e >> 10, co = (e >> 5) & 31, ci = e & 31;
+      const float s = ((hal[((0 * 3 + t) * 32 + co) * 32 + ci] + hal[((1 * 3 + t) * 32 + co) * 32 + ci]) +
+                       hal[((2 * 3 + t) * 32 + co) * 32 + ci]) + hal[((3 * 3 + t) * 32 + co) * 32 + ci];
+      slab[co * (9 * C3_CIN) + (t0 + t) * C3_CIN + ci] = s;
+    }
+    __syncthreads();
+  }
+}
+
+// The weight-gradient launch (AM_COL dY x BM_NN_SHIFT3 X, M = 32, N = 288, no epilogue
+// features): slabs in ws, then the split-K reduction; returns the slab count, or 0 when
+// the shape is not this kernel's (the caller runs the GEMM engine).
+int conv3x3_c32_wgrad_try(const GemmParams& p, int amode, int bmode, int pro_a, int pro_b,
+                          bool fp32, float* ws, size_t ws_elems, hipStream_t stream) {
+  if (!conv3x3_c32_on() || !fp32 || amode != AM_COL || bmode != BM_NN_SHIFT3 ||
+      pro_a != PRO_NONE || pro_b != PRO_NONE || !ws)
+    return 0;
+  if (p.cin != C3_CIN || p.M != 32 || p.N != 9 * C3_CIN || p.nsrc != 1 || p.W % C3_BM ||
+      p.bias || p.nup || p.stats || p.pd2 || p.bz ||
+      (long)p.K != (long)(p.K / ((long)p.H * p.W)) * p.H * p.W)
+    return 0;
+  const long B = p.K / ((long)p.H * p.W);
+  const long strips = B * (p.W / C3_BM);
+  int rows_per = (int)((strips * p.H + 511) / 512);
+  if (rows_per < 1) rows_per = 1;
+  const long cps = (p.H + rows_per - 1) / rows_per;
+  const long nb = strips * cps;
+  if ((size_t)nb * 32 * 9 * C3_CIN > ws_elems) return 0;
+  hipLaunchKernelGGL(conv3x3_c32_wgrad_kernel, dim3((unsigned)nb), dim3(256), 0, stream, p,
+                     rows_per, ws);
+  return (int)nb;
+}

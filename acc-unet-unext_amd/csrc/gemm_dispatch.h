@@ -135,6 +135,10 @@ int gemm_run(GemmParams p, int amode, int bmode, int pro_a, int pro_b, bool allo
 int conv3x3_c32_try(const GemmParams& p, int amode, int bmode, int pro_a, int pro_b, int epi,
                     bool fp32, int tile, hipStream_t stream);
 
+// its weight gradient: the number of [M][N] slabs written into ws (0: not this shape)
+int conv3x3_c32_wgrad_try(const GemmParams& p, int amode, int bmode, int pro_a, int pro_b,
+                          bool fp32, float* ws, size_t ws_elems, hipStream_t stream);
+
 // Skinny weight-gradient path (csrc/gemm_skinny.hip): returns the number of
 // [M][N] partial slabs written into ws (to be summed by the split-K reduction),
 // or 0 when the shape does not qualify.

@@ -309,6 +309,13 @@ int gemm_run(GemmParams p, int amode, int bmode, int pro_a, int pro_b, bool allo
     if (bmode == BM_NN_SHIFT3 && (p.cin & q)) vec = false;
   }
   if (amode == AM_ROW && p.nsrc == 1) { p.kbeg[0] = 0; p.kbeg[1] = p.K; }
+  if (allow_split && vec && adt == ACC_F32 && bdt == ACC_F32 && cdt == ACC_F32) {
+    const int S = conv3x3_c32_wgrad_try(p, amode, bmode, pro_a, pro_b, true, ws, ws_elems, stream);
+    if (S > 0) {
+      splitk_reduce(ws, (float*)p.C, p.M, p.N, p.ldc, S, (size_t)p.M * p.N, stream);
+      return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+    }
+  }
   if (allow_split && cdt == ACC_F32 && adt == bdt) {
     const int S = gemm_skinny_try(p, amode, bmode, pro_a, pro_b, ws, ws_elems, adt, stream);
     if (S > 0) {

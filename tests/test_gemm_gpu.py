@@ -163,8 +163,9 @@ def test_conv3x3_fwd_dgrad_wgrad(B, H, W, Ci, Co):
 def test_conv3x3_halo_kernel_c32(B, H, W, Co):
     """The halo-tile 3x3 kernel (csrc/conv3x3.hip; 32 input channels, image rows of whole
     128-pixel tiles: the first ResPath level): forward with bias and the fp64 statistics
-    rows (one per 128-pixel tile, as the implicit GEMM's), and the data gradient
-    accumulated in place onto C (the residual's gradient), against float64 torch."""
+    rows (one per 128-pixel tile, as the implicit GEMM's), the data gradient
+    accumulated in place onto C (the residual's gradient) and the weight gradient,
+    against float64 torch."""
     torch.manual_seed(14)
     Ci = 32
     x = torch.randn(B, Ci, H, W, device=DEV, dtype=torch.float64, requires_grad=True)
@@ -199,6 +200,16 @@ def test_conv3x3_halo_kernel_c32(B, H, W, Co):
                   c=dx, ldc=Ci, H=H, W=W, cin=Co, ups=[(dx, Ci, 0, 0)])
         refx = x.grad.permute(0, 2, 3, 1).reshape(P, Ci) + r.double()
         assert rel(dx, refx) < 1e-5
+        # weight gradient (its own halo kernel: one slab per workgroup, split-K reduce)
+        def wgrad():
+            dw = torch.empty(Co, 9 * Ci, device=DEV)
+            kern.gemm(Co, 9 * Ci, P, a=[gyn], lda=[Co], amode=_lib.AMODE_COL, b=xn, ldb=Ci,
+                      bmode=_lib.BMODE_NN_SHIFT3, c=dw, ldc=9 * Ci, H=H, W=W, cin=Ci,
+                      allow_split=True)
+            return dw
+        dw = wgrad()
+        assert rel(dw, w.grad.permute(0, 2, 3, 1).reshape(Co, 9 * Ci)) < 1e-5
+        assert torch.equal(dw, wgrad())  # fixed slab order: bitwise reproducible
 
 
 @pytest.mark.parametrize("M,N,K,lda,pro_b", [(32, 32, 1 << 20, 32, 0), (32, 32, 100003, 48, 1),
