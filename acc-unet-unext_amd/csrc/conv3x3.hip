@@ -192,6 +192,11 @@ int conv3x3_c32_try(const GemmParams& p, int amode, int bmode, int pro_a, int pr
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256, 2)
 conv3x3_c32_wgrad_kernel(const GemmParams p, int rows_per, float* __restrict__ slabs) {
+  // channel block of this workgroup (blockIdx.y): output channels [co0, co0 + 32) of
+  // M = C_out, input channels [ci0, ci0 + 32) of cin (32-channel slices of wider layers,
+  // each block its own [32][9][32] part of the [M][9*cin] slab)
+  const int nci = p.cin / C3_CIN;
+  const int co0 = (blockIdx.y / nci) * 32, ci0 = (blockIdx.y % nci) * C3_CIN;
   __shared__ __attribute__((aligned(16))) float hal[C3_HALO_F];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -220,13 +225,13 @@ conv3x3_c32_wgrad_kernel(const GemmParams p, int rows_per, float* __restrict__ s
       const int j = e / 9, k = e - j * 9;
       const int ww = w0 - 1 + j;
       const bool ok = rok && k < 8 && ww >= 0 && ww < W;
-      const float* src = ok ? xrow + (long)ww * ldx + 4 * k : g_c3_zero4;
+      const float* src = ok ? xrow + (long)ww * ldx + ci0 + 4 * k : g_c3_zero4;
       if (lane < C3_DMA_LANES && e < C3_ROW_PIECES) gg_dma16(src, dst + base * 4);
     }
   };
   // dY of output row h for this wave's pixel pairs: a[i] = dY[pixel w0 + 32 wave + 2i + lh][l31]
   auto load_dy = [&](int h, float (&a)[16]) {
-    const float* row = dY + (((long)b * H + h) * W + w0 + wave * 32 + lh) * ldy + l31;
+    const float* row = dY + (((long)b * H + h) * W + w0 + wave * 32 + lh) * ldy + co0 + l31;
 #pragma unroll
     for (int i = 0; i < 16; ++i) a[i] = row[(long)(2 * i) * ldy];
   };
@@ -274,7 +279,8 @@ conv3x3_c32_wgrad_kernel(const GemmParams p, int rows_per, float* __restrict__ s
   }
   // the 4 waves' partial tiles summed in wave order, 3 taps per round through the ring
   __syncthreads();
-  float* slab = slabs + (size_t)blockIdx.x * (32 * 9 * C3_CIN);
+  const int N = 9 * p.cin;
+  float* slab = slabs + (size_t)blockIdx.x * p.M * N + (size_t)co0 * N + ci0;
 #pragma unroll
   for (int t0 = 0; t0 < 9; t0 += 3) {
 #pragma unroll
@@ -287,32 +293,35 @@ conv3x3_c32_wgrad_kernel(const GemmParams p, int rows_per, float* __restrict__ s
       const int t = e >> 10, co = (e >> 5) & 31, ci = e & 31;
       const float s = ((hal[((0 * 3 + t) * 32 + co) * 32 + ci] + hal[((1 * 3 + t) * 32 + co) * 32 + ci]) +
                        hal[((2 * 3 + t) * 32 + co) * 32 + ci]) + hal[((3 * 3 + t) * 32 + co) * 32 + ci];
-      slab[co * (9 * C3_CIN) + (t0 + t) * C3_CIN + ci] = s;
+      slab[(size_t)co * N + (t0 + t) * p.cin + ci] = s;
     }
     __syncthreads();
   }
 }
 
-// The weight-gradient launch (AM_COL dY x BM_NN_SHIFT3 X, M = 32, N = 288, no epilogue
-// features): slabs in ws, then the split-K reduction; returns the slab count, or 0 when
+// The weight-gradient launch (AM_COL dY x BM_NN_SHIFT3 X, M = C_out and cin multiples
+// of 32, N = 9 cin, image rows of whole 128-pixel strips, no epilogue features): slabs in ws, then the split-K reduction; returns the slab count, or 0 when
 // the shape is not this kernel's (the caller runs the GEMM engine).
 int conv3x3_c32_wgrad_try(const GemmParams& p, int amode, int bmode, int pro_a, int pro_b,
                           bool fp32, float* ws, size_t ws_elems, hipStream_t stream) {
   if (!conv3x3_c32_on() || !fp32 || amode != AM_COL || bmode != BM_NN_SHIFT3 ||
       pro_a != PRO_NONE || pro_b != PRO_NONE || !ws)
     return 0;
-  if (p.cin != C3_CIN || p.M != 32 || p.N != 9 * C3_CIN || p.nsrc != 1 || p.W % C3_BM ||
+  if (p.cin % C3_CIN || p.M % 32 || p.N != 9 * p.cin || p.nsrc != 1 || p.W % C3_BM ||
+      (p.lda[0] & 3) || (p.ldb & 3) ||
       p.bias || p.nup || p.stats || p.pd2 || p.bz ||
       (long)p.K != (long)(p.K / ((long)p.H * p.W)) * p.H * p.W)
     return 0;
   const long B = p.K / ((long)p.H * p.W);
   const long strips = B * (p.W / C3_BM);
-  int rows_per = (int)((strips * p.H + 511) / 512);
+  const int nblk = (p.M / 32) * (p.cin / C3_CIN);  // 32x32 channel blocks
+  const long want = 512 / nblk > 8 ? 512 / nblk : 8;  // workgroups per block
+  int rows_per = (int)((strips * p.H + want - 1) / want);
   if (rows_per < 1) rows_per = 1;
   const long cps = (p.H + rows_per - 1) / rows_per;
-  const long nb = strips * cps;
-  if ((size_t)nb * 32 * 9 * C3_CIN > ws_elems) return 0;
-  hipLaunchKernelGGL(conv3x3_c32_wgrad_kernel, dim3((unsigned)nb), dim3(256), 0, stream, p,
+  const long nb = strips * cps;  // slabs
+  if ((size_t)nb * p.M * p.N > ws_elems) return 0;
+  hipLaunchKernelGGL(conv3x3_c32_wgrad_kernel, dim3((unsigned)nb, nblk), dim3(256), 0, stream, p,
                      rows_per, ws);
   return (int)nb;
 }

@@ -212,6 +212,33 @@ def test_conv3x3_halo_kernel_c32(B, H, W, Co):
         assert torch.equal(dw, wgrad())  # fixed slab order: bitwise reproducible
 
 
+@pytest.mark.parametrize("B,H,W,Ci,Co", [(2, 24, 128, 64, 64), (1, 8, 256, 32, 96),
+                                         (2, 6, 128, 128, 64), (16, 128, 128, 64, 64)])
+def test_conv3x3_halo_wgrad_channel_blocks(B, H, W, Ci, Co):
+    """The halo weight-gradient kernel on wider layers (32x32 channel blocks per
+    workgroup, each writing its part of the [Co][9 Ci] slab): the second ResPath level
+    (16 x 128^2 x 64) and non-square channel counts, against float64 torch; bitwise
+    reproducible."""
+    torch.manual_seed(15)
+    x = torch.randn(B, Ci, H, W, device=DEV, dtype=torch.float64)
+    gy = torch.randn(B, Co, H, W, device=DEV, dtype=torch.float64)
+    w = torch.zeros(Co, Ci, 3, 3, device=DEV, dtype=torch.float64, requires_grad=True)
+    F.conv2d(x, w, padding=1).backward(gy)
+    P = B * H * W
+    xn = x.permute(0, 2, 3, 1).reshape(P, Ci).float().contiguous()
+    gyn = gy.permute(0, 2, 3, 1).reshape(P, Co).float().contiguous()
+
+    def wgrad():
+        dw = torch.empty(Co, 9 * Ci, device=DEV)
+        kern.gemm(Co, 9 * Ci, P, a=[gyn], lda=[Co], amode=_lib.AMODE_COL, b=xn, ldb=Ci,
+                  bmode=_lib.BMODE_NN_SHIFT3, c=dw, ldc=9 * Ci, H=H, W=W, cin=Ci,
+                  allow_split=True)
+        return dw
+    dw = wgrad()
+    assert rel(dw, w.grad.permute(0, 2, 3, 1).reshape(Co, 9 * Ci)) < 1e-5
+    assert torch.equal(dw, wgrad())
+
+
 @pytest.mark.parametrize("M,N,K,lda,pro_b", [(32, 32, 1 << 20, 32, 0), (32, 32, 100003, 48, 1),
                                              (32, 96, 40000, 64, 2), (96, 32, 65536, 96, 0),
                                              (64, 32, 20000, 80, 2), (32, 64, 16384, 32, 1),

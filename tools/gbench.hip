@@ -75,6 +75,7 @@ int main(int argc, char** argv) {
       {"rspth2 3x3 wgrad    64x576x262144 COL SHIFT3 split", 64, 576, 262144, AMODE_COL, BMODE_NN_SHIFT3, PRO_NONE, 0, 1, 128, 128, 64},
       {"rspth3 3x3 fwd     65536x128x1152 SHIFT3 stats", 65536, 128, 1152, AMODE_SHIFT3, BMODE_NT, PRO_NONE, 1, 0, 64, 64, 128},
       {"rspth3 3x3 wgrad   128x1152x65536 COL SHIFT3 split", 128, 1152, 65536, AMODE_COL, BMODE_NN_SHIFT3, PRO_NONE, 0, 1, 64, 64, 128},
+      {"rspth2w 3x3 wgrad   64x576x262144 COL SHIFT3 split", 64, 576, 262144, AMODE_COL, BMODE_NN_SHIFT3, PRO_NONE, 0, 1, 128, 128, 64},
       {"narrow conv 1x1 fwd 1048576x32x96 NT stats", 1048576, 32, 96, AMODE_ROW, BMODE_NT, PRO_NONE, 1, 0, 0, 0, 0},
   };
   // operand buffers sized for the largest shape (65536 x 4352 activations, 1M x 32 for B
