@@ -286,6 +286,16 @@ def main():
     x = torch.randn(B, 3, S, S, generator=g).to(dev)
     mask = (torch.rand(B, 1, S, S, generator=g) < 0.3).float().to(dev)
 
+    # K1 once more BEFORE any training step (the GPU not yet under sustained load), for
+    # context only: the line's roofline is the probe right after the timed steps
+    k1_before = None
+    if not args.no_probe and not unext:
+        from accunet import probe
+        blk = model.cnv12
+        k1_before = probe.k1_dw3x3(B, S, S, blk.conv2.weight.shape[0], blk.conv2.weight,
+                                   blk.conv2.bias, dtype=model.act_dtype)
+        torch.cuda.synchronize()
+
     for _ in range(args.warmup):
         step(x, mask)
     torch.cuda.synchronize()
@@ -362,6 +372,9 @@ def main():
                              args.dtype, probe.K1_SOURCES)
         probe.attach_traffic(rl[1], os.path.join(ROOT, "profiles", "k3_traffic.json"),
                              args.dtype, probe.K3_SOURCES)
+        if k1_before is not None:
+            rl[0]["before_steps"] = {k: k1_before[k] for k in
+                                     ("avg_us", "median_us", "frac", "copy_us", "frac_of_copy")}
         line["roofline"] = rl[0]
         line["rooflines"] = rl
     if args.eager:

@@ -18,6 +18,10 @@ import os
 import re
 import statistics
 
+# the GEMM engines and the ResPath 3x3 direct convolutions (csrc/conv3x3.hip) that a
+# replayed GEMM key may dispatch to
+GEMM_PREFIXES = ("void gemm_", "gemm_", "void conv3x3_", "conv3x3_")
+
 
 def load(path, reps):
     """{dispatch_id: {counter: value, 'name', 'dur_ns', 'grid'}} of the last reps GEMM dispatches"""
@@ -28,7 +32,7 @@ def load(path, reps):
                                                          "dur_ns": int(r["End_Timestamp"]) - int(r["Start_Timestamp"]),
                                                          "grid": int(r["Grid_Size"])})
             d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-    g = [v for k, v in rows.items() if v["name"].startswith(("void gemm_", "gemm_"))]
+    g = [v for k, v in rows.items() if v["name"].startswith(GEMM_PREFIXES)]
     return g[-reps:]
 
 
@@ -41,7 +45,7 @@ def shrink(path, reps):
     ids = []
     for r in rows:
         d = int(r["Dispatch_Id"])
-        if r["Kernel_Name"].startswith(("void gemm_", "gemm_")) and (not ids or ids[-1] != d):
+        if r["Kernel_Name"].startswith(GEMM_PREFIXES) and (not ids or ids[-1] != d):
             ids.append(d)
     keep = set(ids[-reps:])
     with open(path, "w", newline="") as f:
