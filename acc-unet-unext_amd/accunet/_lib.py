@@ -97,6 +97,7 @@ _SIGS = {
     "accunet_pool2_fwd": [P, P, I, I, I, I, I, I, P],
     "accunet_pool2_bwd": [P, P, P, P, I, I, I, I, I, I, I, P],
     "accunet_upsample_bwd": [P, I, I, P, I, I, I, I, I, I, I, I, P],
+    "accunet_upsample_bwd24": [P, I, P, I, P, I, I, I, I, I, I, P],
     "accunet_slice_copy": [P, I, I, P, I, I, L, I, I, I, P],
     "accunet_pixel_shuffle2": [P, P, P, I, I, I, I, I, I, P],
     "accunet_permute4": [P, P, IP, POINTER(c_longlong), IP, I, I, I, P],

@@ -336,6 +336,12 @@ def upsample_bwd(inp, ld_in, in_off, out, ld_out, B, H, W, C, f, accumulate=Fals
          C, int(f), 1 if accumulate else 0, _same_dt(inp, out), _stream())
 
 
+def upsample_bwd24(inp, ld_in, out2, ld_out2, out4, ld_out4, B, H, W, C):
+    """2x2 and 4x4 block sums of inp in one pass (the bits of upsample_bwd f=2 and f=4)."""
+    call("accunet_upsample_bwd24", _p(inp), int(ld_in), _p(out2), int(ld_out2), _p(out4),
+         int(ld_out4), B, H, W, C, _same_dt(inp, out2, out4), _stream())
+
+
 def slice_copy(src, ld_src, src_off, dst, ld_dst, dst_off, P, C, accumulate=False):
     call("accunet_slice_copy", _p(src), int(ld_src), int(src_off), _p(dst), int(ld_dst),
          int(dst_off), int(P), int(C), 1 if accumulate else 0, _same_dt(src, dst), _stream())

@@ -17,6 +17,7 @@ used for allocation, views and autograd bookkeeping.
 from __future__ import annotations
 
 import contextlib
+import ctypes
 
 import os
 from dataclasses import dataclass, field
@@ -370,6 +371,97 @@ class WeightPrep:
             yield self
         finally:
             _PREP = prev
+
+
+_DEFER = None  # DeferredRelayouts collecting the backward's inverse weight relayouts
+
+
+class DeferredRelayouts:
+    """The backward's inverse weight relayouts -- HANCLayer / MLFC-merge weight
+    gradients from the grouped GEMM columns back to the reference's interleave, the
+    ResPath 3x3 and ConvTranspose2d weight gradients back to the torch layout -- taken
+    out of the per-layer backward and made by ONE accunet_relayout_batch launch at the
+    end of a captured backward (graph-mode TrainStep at world 1). Inside `active()` the
+    backward ops append items instead of launching; `flush()` (still inside the capture,
+    after loss.backward(): every side-stream weight-gradient fork has joined the main
+    stream by then) captures the one launch over a preallocated item table, and
+    `upload()` fills the table after the capture (the addresses are the graph pool's,
+    fixed for every replay). Not used with data parallelism: a gradient bucket must see
+    its final values when its all-reduce starts."""
+
+    CAP = 128
+
+    def __init__(self, device):
+        self.items, self.keep = [], []
+        self.table = torch.zeros(self.CAP * ctypes.sizeof(_lib.AccRelayout), dtype=torch.uint8,
+                                 device=device)
+        self.n = self.nblocks = 0
+        self._raw = None
+
+    def full(self):
+        return len(self.items) >= self.CAP
+
+    def _add(self, src, dst, kind, total, **kw):
+        it = _lib.AccRelayout()
+        it.inp, it.out = src.data_ptr(), dst.data_ptr()
+        it.total, it.kind = int(total), kind
+        if kind == 0:
+            for a in range(4):
+                it.d[a], it.s[a] = kw["d"][a], kw["s"][a]
+                it.flip[a] = 0
+        else:
+            it.N, it.C, it.J = kw["N"], kw["C"], kw["J"]
+            for j in range(8):
+                it.order[j] = kw["order"][j] if j < kw["J"] else j
+        self.items.append(it)
+        self.keep += [src, dst]
+
+    def permute(self, src, dst, d, s):
+        self._add(src, dst, 0, dst.numel(), d=d, s=s)
+
+    def group_inverse(self, src, dst, N, C, J, order):
+        self._add(src, dst, 2, N * J * C, N=N, C=C, J=J, order=order)
+
+    def flush(self):
+        if not self.items:
+            return
+        blk = 0
+        for it in self.items:
+            it.blk0 = blk
+            blk += kern.relayout_blocks(it.total)
+        self.n, self.nblocks = len(self.items), blk
+        self._raw = bytes((_lib.AccRelayout * self.n)(*self.items))
+        kern.relayout_batch(self.table, self.n, self.nblocks)
+
+    def upload(self):
+        if self._raw:
+            self.table[:len(self._raw)].copy_(
+                torch.frombuffer(bytearray(self._raw), dtype=torch.uint8))
+
+    @contextlib.contextmanager
+    def active(self):
+        global _DEFER
+        prev, _DEFER = _DEFER, self
+        try:
+            yield self
+        finally:
+            _DEFER = prev
+
+
+def _wgrad_permute(src, dst, d, s):
+    """a weight gradient back to the torch layout (accunet_permute4), or deferred"""
+    if _DEFER is not None and not _DEFER.full():
+        _DEFER.permute(src, dst, d, s)
+    else:
+        kern.permute4(src, dst, d, s)
+
+
+def _wgrad_group_inverse(src, dst, N, C, J, order):
+    """a grouped-column weight gradient back to the reference interleave, or deferred"""
+    if _DEFER is not None and not _DEFER.full():
+        _DEFER.group_inverse(src, dst, N, C, J, order)
+    else:
+        kern.group_relayout(src, dst, N, C, J, order, inverse=True)
 
 
 def as_pending(x) -> Pending:
@@ -835,10 +927,11 @@ class _HancLayerFn(torch.autograd.Function):
         dP2 = dP4 = dG2 = dG4 = None
         if k >= 2:
             dG2 = _act((B, H // 2, W // 2, N), dZ)
-            kern.upsample_bwd(dZ, N, 0, dG2, N, B, H, W, N, 2)
-            if k == 3:
+            if k == 3:  # both pyramid sums from one read of dZ
                 dG4 = _act((B, H // 4, W // 4, N), dZ)
-                kern.upsample_bwd(dZ, N, 0, dG4, N, B, H, W, N, 4)
+                kern.upsample_bwd24(dZ, N, dG2, N, dG4, N, B, H, W, N)
+            else:
+                kern.upsample_bwd(dZ, N, 0, dG2, N, B, H, W, N, 2)
         # the three weight-gradient GEMMs on the side stream (overlap the data gradients)
         fork = _WgradFork(dZ, 2.0 * N * C * P * (1 + (1 if k >= 2 else 0) / 2 +
                                                  (1 if k == 3 else 0) / 8))
@@ -854,7 +947,7 @@ class _HancLayerFn(torch.autograd.Function):
             keep.append(kern.gemm(N, C, P, a=[dZ], lda=[N], amode=AMODE_COL, b=z, ldb=C,
                                   bmode=BMODE_NN, c=dWp, ldc=J * C, c_offset=0,
                                   pro_b=_pro_mode(pro), b_scale=sc, b_shift=sh, allow_split=True))
-            kern.group_relayout(dWp, dW, N, C, J, _HANC_ORDER[k], inverse=True)
+            _wgrad_group_inverse(dWp, dW, N, C, J, _HANC_ORDER[k])
         if k >= 2:
             dP2 = _act(p2.shape, dZ)
             keep.append(kern.gemm(P // 4, 2 * C, N, a=[dG2], lda=[N], b=Wp, ldb=J * C,
@@ -1131,7 +1224,7 @@ class _Conv3x3Fn(torch.autograd.Function):
             keep.append(kern.gemm(Co, 9 * Ci, P, a=[dZ], lda=[Co], amode=AMODE_COL, b=x, ldb=Ci,
                                   bmode=BMODE_NN_SHIFT3, c=dWr, ldc=9 * Ci, H=H, W=W, cin=Ci,
                                   allow_split=True))
-            kern.permute4(dWr, dW, (Co, Ci, 3, 3), (9 * Ci, 1, 3 * Ci, Ci))
+            _wgrad_permute(dWr, dW, (Co, Ci, 3, 3), (9 * Ci, 1, 3 * Ci, Ci))
         if ctx.needs_input_grad[1]:
             Wf = _prepared(weight, "c3f")
             if Wf is None:
@@ -1203,7 +1296,7 @@ class _ConvT2Fn(torch.autograd.Function):
         with fork:  # weight gradient on the side stream (overlaps the data gradient)
             keep.append(kern.gemm(Ci, 4 * Co, P, a=[x], lda=[Ci], amode=AMODE_COL, b=dT,
                                   ldb=4 * Co, bmode=BMODE_NN, c=dWr, ldc=4 * Co, allow_split=True))
-            kern.permute4(dWr, dW, (Ci, Co, 2, 2), (4 * Co, 1, 2 * Co, Co))
+            _wgrad_permute(dWr, dW, (Ci, Co, 2, 2), (4 * Co, 1, 2 * Co, Co))
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
             keep.append(kern.gemm(P, Ci, 4 * Co, a=[dT], lda=[4 * Co], b=Wr, ldb=4 * Co, c=dx,
@@ -1384,7 +1477,7 @@ class _GroupRelayoutFn(torch.autograd.Function):
     def backward(ctx, g):
         N, C, J, order = ctx.meta
         out = _f32((N, J * C), g)
-        kern.group_relayout(g.contiguous(), out, N, C, J, order, inverse=True)
+        _wgrad_group_inverse(g.contiguous(), out, N, C, J, order)
         return out, None, None
 
 

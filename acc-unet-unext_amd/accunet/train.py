@@ -35,6 +35,7 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
+import contextlib
 import os
 
 from . import kern, ops
@@ -218,6 +219,8 @@ class TrainStep:
         preds = self.model(x)
         loss = self.criterion(preds, m)
         loss.backward()
+        if ops._DEFER is not None:  # the deferred weight-gradient relayouts, one launch
+            ops._DEFER.flush()
         return loss
 
     def _capture(self, images, masks):
@@ -254,17 +257,25 @@ class TrainStep:
                                           self.comm_dtype)
             self._buckets.stream = torch.cuda.Stream()
             self._buckets.arm()
+        # the backward's inverse weight relayouts in one launch at its end (world 1 only:
+        # a DP gradient bucket must hold final values when its all-reduce starts)
+        self._defer = None
+        if not self.dp and os.environ.get("ACCUNET_DEFER_RELAYOUT", "1") != "0":
+            self._defer = ops.DeferredRelayouts(self._x.device)
         g = torch.cuda.CUDAGraph(keep_graph=self._buckets is not None)
         try:
             with torch.cuda.graph(g):
-                if self._prep is not None:
-                    with self._prep.active():
-                        loss = self._fwd_bwd(self._x, self._m)
-                else:
+                with contextlib.ExitStack() as es:
+                    if self._prep is not None:
+                        es.enter_context(self._prep.active())
+                    if self._defer is not None:
+                        es.enter_context(self._defer.active())
                     loss = self._fwd_bwd(self._x, self._m)
         finally:
             if self._buckets is not None:
                 self._buckets.disarm()
+        if self._defer is not None:
+            self._defer.upload()  # the item table the captured launch reads
         if self._buckets is not None:
             # an event-record node behind every bucket's marker, then instantiate
             n = kern.GraphEvent.attach(g.raw_cuda_graph(), self._buckets.events)

@@ -136,6 +136,106 @@ __global__ void __launch_bounds__(256, 2) conv3x3_c32_kernel(const GemmParams p,
   }
 }
 
+// ---------------------------------------------------------------------------
+// bf16 activation mode (BASELINE configs[2]): the same strips and ring on
+// v_mfma_f32_32x32x16_bf16. Slots hold 32 bf16 channels padded to 40 (80 B, as the
+// bf16 engine's LDS rows); a lane's A operand is one ds_read_b128 of 8 channels
+// (k = 16 g + 8 lh + j), its B operand 8 weights rounded to bf16 once (fp32 master
+// weights, round-to-nearest-even as the engine rounds them on load). Per tap the two
+// k-steps run in channel order and the taps in order 0..8: the bf16 engine's k order
+// (its 32-k stage is one tap), so the sums, and with the shared epilogue the stored
+// bf16 values, are the engine's.
+// ---------------------------------------------------------------------------
+#define C3B_CS 40                                   // bf16 per slot (32 + 8 pad)
+#define C3B_ROW_PIECES (C3_SLOTS * (C3B_CS / 8))    // 16-B pieces per ring row (650)
+#define C3B_DMA_ROW 3                               // DMA instructions per wave and row
+#define C3B_DMA_LANES ((C3B_ROW_PIECES + 4 * C3B_DMA_ROW - 1) / (4 * C3B_DMA_ROW))  // 55
+static_assert(C3B_DMA_LANES <= 64 && (4 * C3B_DMA_ROW - 1) * C3B_DMA_LANES < C3B_ROW_PIECES,
+              "every DMA instruction has live lanes");
+
+template <int EPI>
+__global__ void __launch_bounds__(256, 2) conv3x3_c32_bf16_kernel(const GemmParams p, int rows_per) {
+  __shared__ __attribute__((aligned(16))) bf16_t hal[3 * C3_SLOTS * C3B_CS];
+  __shared__ __attribute__((aligned(16))) float epi[gemm_epi_floats<4, 1, 1>()];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l31 = lane & 31, lh = lane >> 5;
+  const int n0 = blockIdx.y * 32;
+  const int H = p.H, W = p.W;
+  const bf16_t* X = (const bf16_t*)p.A[0];
+  const long ldx = p.lda[0];
+
+  const int cps = (H + rows_per - 1) / rows_per;
+  const int strip = blockIdx.x / cps, chunk = blockIdx.x - strip * cps;
+  const int nstrip_w = W / C3_BM;
+  const int b = strip / nstrip_w;
+  const int w0 = (strip - b * nstrip_w) * C3_BM;
+  const int hb = chunk * rows_per, he = min(H, hb + rows_per);
+  if (hb >= he) return;
+
+  auto dma_row = [&](int r) {  // input row r -> ring slot r mod 3 (pieces: 4 data + 1 pad)
+    const bool rok = r >= 0 && r < H;
+    const bf16_t* xrow = X + ((long)b * H + r) * W * ldx;
+    float* dst = reinterpret_cast<float*>(hal + ((r + 3) % 3) * C3_SLOTS * C3B_CS);
+#pragma unroll 1
+    for (int u = 0; u < C3B_DMA_ROW; ++u) {
+      const int base = (u * 4 + wave) * C3B_DMA_LANES;
+      const int e = base + lane;
+      const int j = e / 5, k = e - j * 5;
+      const int ww = w0 - 1 + j;
+      const bool ok = rok && k < 4 && ww >= 0 && ww < W;
+      const float* src = ok ? reinterpret_cast<const float*>(xrow + (long)ww * ldx + 8 * k) : g_c3_zero4;
+      if (lane < C3B_DMA_LANES && e < C3B_ROW_PIECES) gg_dma16(src, dst + base * 4);
+    }
+  };
+
+  // weights of output channel n0 + l31 rounded to bf16: wb[tap][g] = k 16g + 8lh .. +7
+  bf16x8_v wb[9][2];
+  {
+    const float* wrow = (const float*)p.B + (long)(n0 + l31) * p.ldb + 8 * lh;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        const uint4 u = ld8_bf(wrow + tap * C3_CIN + 16 * g);
+        wb[tap][g] = __builtin_bit_cast(bf16x8_v, u);
+      }
+  }
+  const int px = wave * 32 + l31;
+
+  auto taps = [&](floatx16& acc, int dh, int r) {
+    const bf16_t* a = hal + ((r + 3) % 3) * C3_SLOTS * C3B_CS + px * C3B_CS + 8 * lh;
+#pragma unroll
+    for (int dw = 0; dw < 3; ++dw)
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        const bf16x8_v f = *reinterpret_cast<const bf16x8_v*>(a + dw * C3B_CS + 16 * g);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f, wb[dh * 3 + dw][g], acc, 0, 0, 0);
+      }
+  };
+
+  dma_row(hb - 1);
+  dma_row(hb);
+  dma_row(hb + 1);
+  for (int h = hb; h < he; ++h) {
+    gg_wait_vm<C3B_DMA_ROW>();
+    __builtin_amdgcn_s_barrier();
+    floatx16 acc[1][1];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[0][0][r] = 0.f;
+    taps(acc[0][0], 0, h - 1);
+    taps(acc[0][0], 1, h);
+    __builtin_amdgcn_s_barrier();
+    const bool more = h + 1 < he;
+    if (more) dma_row(h + 2);
+    if (more) gg_wait_vm<C3B_DMA_ROW>();
+    else gg_wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    taps(acc[0][0], 2, h + 1);
+    gemm_epilogue<bf16_t, EPI, 4, 1, 1>(p, acc, epi, (int)(((long)b * H + h) * W + w0), n0);
+  }
+}
+
 static int conv3x3_c32_on() {
   static int v = -1;
   if (v < 0) {
@@ -150,16 +250,18 @@ static int conv3x3_c32_on() {
 // of bias / statistics / in-place addend) and returns ACC_OK, else -1 (caller runs the
 // GEMM engine). p.evec must already be set (gemm_run).
 int conv3x3_c32_try(const GemmParams& p, int amode, int bmode, int pro_a, int pro_b, int epi,
-                    bool fp32, int tile, hipStream_t stream) {
+                    int dmode, int tile, hipStream_t stream) {
   // (tile: the engine's choice; the statistics rows are per 128x32 tile, so only where
-  // the engine would run 128x32 tiles too)
-  if (!conv3x3_c32_on() || !fp32 || tile != TILE_C || amode != AM_SHIFT3 || bmode != BM_NT || pro_a != PRO_NONE ||
+  // the engine would run 128x32 tiles too. dmode: 1 fp32, 2 bf16 activations with fp32
+  // weights, 0 neither)
+  if (!conv3x3_c32_on() || !dmode || tile != TILE_C || amode != AM_SHIFT3 || bmode != BM_NT || pro_a != PRO_NONE ||
       pro_b != PRO_NONE || (epi != 0 && epi != EPI_STATS && epi != EPI_UPS))
     return -1;
   if (p.cin != C3_CIN || p.K != 9 * C3_CIN || p.nsrc != 1 || p.N % 32 || p.W % C3_BM ||
       p.M % C3_BM || (long)p.M != (long)(p.M / ((long)p.H * p.W)) * p.H * p.W)
     return -1;
-  if ((p.lda[0] & 3) || ((uintptr_t)p.A[0] & 15) || (p.ldb & 3) || ((uintptr_t)p.B & 15))
+  if ((p.lda[0] & (dmode == 2 ? 7 : 3)) || ((uintptr_t)p.A[0] & 15) || (p.ldb & 3) ||
+      ((uintptr_t)p.B & 15))
     return -1;
   // persistent workgroups, two resident per CU (74.6 KB of LDS each): column strips of
   // 128 pixels cut into row chunks so that there are ~512 per column block
@@ -171,10 +273,16 @@ int conv3x3_c32_try(const GemmParams& p, int amode, int bmode, int pro_a, int pr
   if (rows_per < 1) rows_per = 1;
   const long cps = (p.H + rows_per - 1) / rows_per;
   dim3 grid((unsigned)(strips * cps), nb);
-  if (epi & EPI_UPS)
+  if (dmode == 2) {
+    if (epi & EPI_UPS)
+      hipLaunchKernelGGL(conv3x3_c32_bf16_kernel<EPI_UPS>, grid, dim3(256), 0, stream, p, rows_per);
+    else
+      hipLaunchKernelGGL(conv3x3_c32_bf16_kernel<EPI_STATS>, grid, dim3(256), 0, stream, p, rows_per);
+  } else if (epi & EPI_UPS) {
     hipLaunchKernelGGL(conv3x3_c32_kernel<EPI_UPS>, grid, dim3(256), 0, stream, p, rows_per);
-  else
+  } else {
     hipLaunchKernelGGL(conv3x3_c32_kernel<EPI_STATS>, grid, dim3(256), 0, stream, p, rows_per);
+  }
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 

@@ -133,7 +133,7 @@ int gemm_run(GemmParams p, int amode, int bmode, int pro_a, int pro_b, bool allo
 // ResPath 3x3 over 32 channels as a halo-tile direct convolution (csrc/conv3x3.hip):
 // ACC_OK / an error when it ran the launch, -1 when the GEMM engine should
 int conv3x3_c32_try(const GemmParams& p, int amode, int bmode, int pro_a, int pro_b, int epi,
-                    bool fp32, int tile, hipStream_t stream);
+                    int dmode, int tile, hipStream_t stream);
 
 // its weight gradient: the number of [M][N] slabs written into ws (0: not this shape)
 int conv3x3_c32_wgrad_try(const GemmParams& p, int amode, int bmode, int pro_a, int pro_b,

@@ -368,8 +368,10 @@ int gemm_run(GemmParams p, int amode, int bmode, int pro_a, int pro_b, bool allo
     p.evec = ev ? 1 : 0;
   }
   if (S == 1) {
-    const int r = conv3x3_c32_try(p, amode, bmode, pro_a, pro_b, epi,
-                                  vec && adt == ACC_F32 && bdt == ACC_F32 && cdt == ACC_F32, t, stream);
+    const int dmode = !vec ? 0
+                      : (adt == ACC_F32 && bdt == ACC_F32 && cdt == ACC_F32) ? 1
+                      : (adt == ACC_BF16 && bdt == ACC_F32 && cdt == ACC_BF16) ? 2 : 0;
+    const int r = conv3x3_c32_try(p, amode, bmode, pro_a, pro_b, epi, dmode, t, stream);
     if (r >= 0) return r;
   }
   p.ngrp = 0;

@@ -443,6 +443,66 @@ extern "C" int accunet_upsample_bwd(const void* in, int ld_in, int in_off, void*
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 
+// The k = 3 HANCLayer pyramid's two backward sums from one read of in: a thread owns one
+// 4x4 pixel block of one channel, adds each 2x2 quarter in (dy, dx) order (= blocksum
+// <2>) and the 16 values in row-major order (= blocksum<4>), so both outputs carry the
+// bits of the two separate launches.
+template <typename T>
+__global__ void __launch_bounds__(256)
+blocksum24_kernel(const T* __restrict__ in, int ld_in, T* __restrict__ out2, int ld_out2,
+                  T* __restrict__ out4, int ld_out4, int B, int H, int W, int C) {
+  const int H4 = H / 4, W4 = W / 4;
+  const long total = (long)B * H4 * W4 * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const long pix = i / C;
+    const int w4 = (int)(pix % W4);
+    const long t = pix / W4;
+    const int h4 = (int)(t % H4);
+    const int b = (int)(t / H4);
+    const T* src = in + (((long)b * H + h4 * 4) * W + w4 * 4) * ld_in + c;
+    float v[16];
+#pragma unroll
+    for (int dy = 0; dy < 4; ++dy)
+#pragma unroll
+      for (int dx = 0; dx < 4; ++dx) v[dy * 4 + dx] = ld1(src + ((long)dy * W + dx) * ld_in);
+    float s4 = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s4 += v[k];
+    st1(out4 + pix * ld_out4 + c, s4);
+    const int H2 = H / 2, W2 = W / 2;
+#pragma unroll
+    for (int qy = 0; qy < 2; ++qy)
+#pragma unroll
+      for (int qx = 0; qx < 2; ++qx) {
+        float s2 = 0.f;
+        s2 += v[(2 * qy) * 4 + 2 * qx];
+        s2 += v[(2 * qy) * 4 + 2 * qx + 1];
+        s2 += v[(2 * qy + 1) * 4 + 2 * qx];
+        s2 += v[(2 * qy + 1) * 4 + 2 * qx + 1];
+        const long p2 = ((long)b * H2 + h4 * 2 + qy) * W2 + w4 * 2 + qx;
+        st1(out2 + p2 * ld_out2 + c, s2);
+      }
+  }
+}
+
+extern "C" int accunet_upsample_bwd24(const void* in, int ld_in, void* out2, int ld_out2,
+                                      void* out4, int ld_out4, int B, int H, int W, int C, int dt,
+                                      void* stream) {
+  if (H % 4 || W % 4) return ACC_EBADSHAPE;
+  if (!in || !out2 || !out4) return ACC_EBADARG;
+  const long total = (long)B * (H / 4) * (W / 4) * C;
+  if (with_dt(dt, [&](auto tag) {
+        using T = decltype(tag);
+        hipLaunchKernelGGL(blocksum24_kernel<T>, dim3(grid_for(total)), dim3(256), 0,
+                           (hipStream_t)stream, (const T*)in, ld_in, (T*)out2, ld_out2, (T*)out4,
+                           ld_out4, B, H, W, C);
+      }))
+    return ACC_EBADARG;
+  return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+}
+
 // ---------------------------------------------------------------------------
 // Strided channel-slice copy: dst[p, dst_off + c] (+)= src[p, src_off + c], c < C
 // ---------------------------------------------------------------------------
@@ -609,7 +669,8 @@ extern "C" int accunet_group_relayout(const float* in, float* out, int N, int C,
 // launch (accunet/ops.py: WeightPrep, used by the graph-mode TrainStep before each
 // replay) instead of one small launch per layer. Item i (AccRelayout, device memory)
 // owns blocks [blk0_i, blk0_{i+1}); kind 0 = accunet_permute4's gather, kind 1 =
-// accunet_group_relayout's forward; the same index arithmetic, so the copies are the
+// accunet_group_relayout's forward, kind 2 its inverse (the backward's weight
+// gradients, ops.DeferredRelayouts); the same index arithmetic, so the copies are the
 // ones the per-layer launches make.
 // ---------------------------------------------------------------------------
 #define RL_EPT 4
@@ -645,7 +706,8 @@ relayout_batch_kernel(const AccRelayout* __restrict__ items, int n) {
       const int nn = (int)(t / it.J);
       src = (long)nn * it.C * it.J + (long)c * it.J + it.order[jj];
     }
-    it.out[i] = it.in[src];
+    if (it.kind == 2) it.out[src] = it.in[i];  // the group relayout's inverse (scatter)
+    else it.out[i] = it.in[src];
   }
 }
 

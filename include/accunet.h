@@ -186,7 +186,9 @@ int accunet_dw3x3_wgrad(const void* x, const void* dz, const float* sc, const fl
  * device array of n AccRelayout, blk0 ascending from 0, item i owning blocks
  * [blk0_i, blk0_{i+1}) with accunet_relayout_blocks(total_i) blocks; nblocks = their
  * sum. kind 0 = the gather of accunet_permute4 (d, s, flip), kind 1 = the forward of
- * accunet_group_relayout (N, C, J, order). fp32 weights only.
+ * accunet_group_relayout (N, C, J, order), kind 2 = its inverse (the backward's weight
+ * gradients back into the reference layout, ops.DeferredRelayouts; total = N*J*C).
+ * fp32 weights only.
  * ------------------------------------------------------------------------- */
 typedef struct AccRelayout {
   const float* in;
@@ -235,6 +237,12 @@ int accunet_pool2_bwd(const void* x, const void* y, const void* dy, void* dx, in
                       int W, int C, int mode, int accumulate, int dt, void* stream);
 int accunet_upsample_bwd(const void* in, int ld_in, int in_off, void* out, int ld_out, int B,
                          int H, int W, int C, int f, int accumulate, int dt, void* stream);
+/* Both backward sums of a k = 3 HANCLayer's pyramid (ACC_UNet.py:96-106: the 2x and 4x
+ * nearest upsamples of the pooled branches) in one pass over in: out2 = 2x2 block sums,
+ * out4 = 4x4 block sums, each added in the order accunet_upsample_bwd adds them (the
+ * same bits as its f = 2 and f = 4 launches). H, W multiples of 4. */
+int accunet_upsample_bwd24(const void* in, int ld_in, void* out2, int ld_out2, void* out4,
+                           int ld_out4, int B, int H, int W, int C, int dt, void* stream);
 int accunet_slice_copy(const void* src, int ld_src, int src_off, void* dst, int ld_dst,
                        int dst_off, long P, int C, int accumulate, int dt, void* stream);
 int accunet_pixel_shuffle2(const void* t, const float* bias, void* y, int B, int Hi, int Wi,

@@ -212,6 +212,25 @@ def test_conv3x3_halo_kernel_c32(B, H, W, Co):
         assert torch.equal(dw, wgrad())  # fixed slab order: bitwise reproducible
 
 
+def test_conv3x3_halo_matches_engine_bitwise(tmp_path):
+    """The halo-tile forward / data-gradient kernels (fp32 and bf16 activation mode) use
+    the implicit GEMM's MFMA, k pairing, k order and epilogue, so their outputs and fp64
+    statistics rows are bit-identical to the engine's (ACCUNET_CONV3_HALO=0), each run in
+    a child process (the knob is read once per process)."""
+    import os
+    import subprocess
+    import sys
+    outs = {}
+    for v in ("1", "0"):
+        env = dict(os.environ, ACCUNET_CONV3_HALO=v)
+        path = tmp_path / f"c3_{v}.pt"
+        subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "conv3x3_worker.py"),
+                        str(path)], env=env, check=True, timeout=240)
+        outs[v] = torch.load(path, weights_only=True)
+    for k in outs["1"]:
+        assert torch.equal(outs["1"][k], outs["0"][k]), k
+
+
 @pytest.mark.parametrize("B,H,W,Ci,Co", [(2, 24, 128, 64, 64), (1, 8, 256, 32, 96),
                                          (2, 6, 128, 128, 64), (16, 128, 128, 64, 64)])
 def test_conv3x3_halo_wgrad_channel_blocks(B, H, W, Ci, Co):

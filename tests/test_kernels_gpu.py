@@ -202,3 +202,25 @@ def test_se_layer_vs_fp64_oracle(B, H, C):
     rows = PU.compare_vs_reference_fp32(hip, a64, a32, factor=4.0, rel_floor=1e-5)
     bad = [r for r in rows if not r[4]]
     assert not bad, bad
+
+
+@pytest.mark.parametrize("B,H,W,C,dt", [(2, 16, 32, 32, torch.float32), (3, 8, 12, 20, torch.float32),
+                                        (16, 256, 256, 32, torch.float32),
+                                        (2, 16, 32, 64, torch.bfloat16)])
+def test_upsample_bwd24_matches_two_blocksums(B, H, W, C, dt):
+    """The k = 3 HANCLayer backward's fused pyramid sums (one read of dZ) carry the bits
+    of the two separate f = 2 / f = 4 block-sum launches, and match float64."""
+    from accunet import kern
+    torch.manual_seed(31)
+    dz = torch.randn(B, H, W, C, device=DEV).to(dt)
+    g2 = torch.empty(B, H // 2, W // 2, C, device=DEV, dtype=dt)
+    g4 = torch.empty(B, H // 4, W // 4, C, device=DEV, dtype=dt)
+    kern.upsample_bwd24(dz, C, g2, C, g4, C, B, H, W, C)
+    r2, r4 = torch.empty_like(g2), torch.empty_like(g4)
+    kern.upsample_bwd(dz, C, 0, r2, C, B, H, W, C, 2)
+    kern.upsample_bwd(dz, C, 0, r4, C, B, H, W, C, 4)
+    assert torch.equal(g2, r2) and torch.equal(g4, r4)
+    d = dz.double()
+    ref4 = d.view(B, H // 4, 4, W // 4, 4, C).sum((2, 4))
+    tol = 1e-5 if dt == torch.float32 else 2e-2
+    assert ((g4.double() - ref4).abs().max() / ref4.abs().max()).item() < tol

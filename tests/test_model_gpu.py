@@ -285,7 +285,9 @@ def test_hip_graph_train_step_equals_eager(variant):
     atomics), so 3 graph steps must reproduce 3 eager steps bit for bit: losses,
     parameters, BatchNorm running statistics and num_batches_tracked. The graph step
     reads the forward-layout weight copies of the one-launch WeightPrep (remade before
-    every replay from the weights Adam left), the eager step makes them per op."""
+    every replay from the weights Adam left) and makes the backward's inverse weight
+    relayouts in one launch at the end of the backward (ops.DeferredRelayouts); the
+    eager step makes both per op."""
     from accunet.train import TrainStep
     nf, B, S = 8, 2, 64
     sd = O.det_state_dict(O.param_spec(variant, 3, 1, nf), seed=0)

@@ -1,11 +1,12 @@
 #!/bin/bash
-# halo-tile 3x3 kernel (csrc/conv3x3.hip): parity tests, gbench A/B against the implicit
-# GEMM (ACCUNET_CONV3_HALO=0), then the suite and a bench line
+# halo-tile 3x3 kernels (csrc/conv3x3.hip): parity tests (incl. bitwise vs the implicit
+# GEMM), gbench A/B against the implicit GEMM (ACCUNET_CONV3_HALO=0), the suite, then
+# bench lines fp32 / bf16 with the knob on and off
 set -e -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_gemm_gpu.py -x -q --timeout 120 --timeout-method thread -k "conv3x3" > gpurun_out/c3_tests.log 2>&1 || { tail -30 gpurun_out/c3_tests.log; exit 1; }
+timeout -k 10 400 python -u -m pytest tests/test_gemm_gpu.py -x -q --timeout 240 --timeout-method thread -k "conv3x3" > gpurun_out/c3_tests.log 2>&1 || { tail -30 gpurun_out/c3_tests.log; exit 1; }
 tail -n 2 gpurun_out/c3_tests.log
 : > gpurun_out/c3_ab.txt
 for rep in 1 2; do
@@ -17,7 +18,10 @@ done
 cat gpurun_out/c3_ab.txt
 timeout -k 10 900 python -u -m pytest tests -q -m gpu -x --timeout 240 --timeout-method thread > gpurun_out/gputests.log 2>&1 || { tail -30 gpurun_out/gputests.log; exit 1; }
 tail -n 1 gpurun_out/gputests.log
-for v in 1 0; do
-  ACCUNET_CONV3_HALO=$v timeout -k 10 400 python bench.py --no-cpu-baseline > gpurun_out/bench_c3_$v.log 2>&1
-  echo "halo=$v"; grep '^{"metric' gpurun_out/bench_c3_$v.log | cut -c1-260
+for dt in fp32 bf16; do
+  for v in 1 0; do
+    ACCUNET_CONV3_HALO=$v timeout -k 10 400 python bench.py --dtype $dt --no-cpu-baseline > gpurun_out/bench_c3_${dt}_$v.log 2>&1
+    echo "$dt halo=$v"; grep '^{"metric' gpurun_out/bench_c3_${dt}_$v.log | cut -c1-200
+  done
 done
+grep -o '"before_steps": {[^}]*}' gpurun_out/bench_c3_fp32_1.log || true

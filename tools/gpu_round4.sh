@@ -36,3 +36,11 @@ python tools/save_profiles.py --shrink-pmc gpurun_out/pmc_fetch gpurun_out/pmc_w
 echo "pmc done"
 timeout -k 10 120 tools/kbench 20 > gpurun_out/kbench.txt 2>&1
 echo "kbench done"
+if [ -n "${PMC_GEMM:-}" ]; then
+  # GEMM census of one step and the PMC passes of the ResPath 3x3 (halo kernels) and the
+  # pyramid data gradient at the final sources
+  timeout -k 10 300 python tools/gemm_census.py --top 200 > gpurun_out/census_full.txt 2>&1
+  head -n 3 gpurun_out/census_full.txt
+  KEYS="32,288,1048576,1,2 1048576,32,288,2,0 65536,4352,128,0,1" timeout -k 10 900 bash tools/pmc_gemm.sh > gpurun_out/pmc_gemm.log 2>&1
+  cat gpurun_out/pmc_gemm/report.txt
+fi
