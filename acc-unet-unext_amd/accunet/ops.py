@@ -414,7 +414,11 @@ class DeferredRelayouts:
             for j in range(8):
                 it.order[j] = kw["order"][j] if j < kw["J"] else j
         self.items.append(it)
-        self.keep += [src, dst]
+        # the source stays alive here; the destination is the gradient autograd hands to
+        # the parameter: an extra reference would make AccumulateGrad clone it (copy the
+        # still-unfilled buffer) instead of taking it, so only its address is kept, and
+        # TrainStep checks after the capture that every one became a parameter's .grad
+        self.keep.append(src)
 
     def permute(self, src, dst, d, s):
         self._add(src, dst, 0, dst.numel(), d=d, s=s)
@@ -432,6 +436,9 @@ class DeferredRelayouts:
         self.n, self.nblocks = len(self.items), blk
         self._raw = bytes((_lib.AccRelayout * self.n)(*self.items))
         kern.relayout_batch(self.table, self.n, self.nblocks)
+
+    def destinations(self):
+        return [int(it.out) for it in self.items]
 
     def upload(self):
         if self._raw:

@@ -275,6 +275,13 @@ class TrainStep:
             if self._buckets is not None:
                 self._buckets.disarm()
         if self._defer is not None:
+            # every deferred relayout must write a buffer autograd took as a parameter's
+            # .grad (not a copy of it, which would have been read before the launch)
+            grads = {p.grad.data_ptr() for p in self.params if p.grad is not None}
+            lost = [a for a in self._defer.destinations() if a not in grads]
+            if lost:
+                raise RuntimeError(f"deferred weight-gradient relayouts: {len(lost)} "
+                                   f"destination(s) are not parameter gradients")
             self._defer.upload()  # the item table the captured launch reads
         if self._buckets is not None:
             # an event-record node behind every bucket's marker, then instantiate
