@@ -115,22 +115,29 @@ __global__ void __launch_bounds__(256, 2) conv3x3_c32_kernel(const GemmParams p,
   dma_row(hb);
   dma_row(hb + 1);
   for (int h = hb; h < he; ++h) {
-    // rows h-1 and h have landed (row h+1 may still be in flight) ...
-    gg_wait_vm<C3_DMA_ROW>();
-    __builtin_amdgcn_s_barrier();  // ... in every wave
+    // Rows h-1 .. h+1 are needed. Past the first row they are in place: each new row
+    // was issued during the previous row's taps and drained by that row's epilogue
+    // (its barriers wait for all memory), so only the first row waits here: rows
+    // hb-1 and hb have landed (hb+1 may still be in flight) in every wave.
+    if (h == hb) {
+      gg_wait_vm<C3_DMA_ROW>();
+      __builtin_amdgcn_s_barrier();
+    }
     floatx16 acc[1][1];
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[0][0][r] = 0.f;
     taps(acc[0][0], 0, h - 1);
-    taps(acc[0][0], 1, h);
-    // every wave is done with row h-1's slot: row h+2 streams into it during row h+1's
-    // taps and the epilogue
+    // every wave is done with row h-1's slot: row h+2 streams into it during the taps
+    // of rows h, h+1 and the epilogue
     __builtin_amdgcn_s_barrier();
     const bool more = h + 1 < he;
     if (more) dma_row(h + 2);
-    if (more) gg_wait_vm<C3_DMA_ROW>();
-    else gg_wait_vm<0>();
-    __builtin_amdgcn_s_barrier();  // row h+1 visible
+    taps(acc[0][0], 1, h);
+    if (h == hb) {  // row hb+1 (the prologue's third row) visible
+      if (more) gg_wait_vm<C3_DMA_ROW>();
+      else gg_wait_vm<0>();
+      __builtin_amdgcn_s_barrier();
+    }
     taps(acc[0][0], 2, h + 1);
     gemm_epilogue<float, EPI, 4, 1, 1>(p, acc, epi, (int)(((long)b * H + h) * W + w0), n0);
   }
@@ -217,20 +224,24 @@ __global__ void __launch_bounds__(256, 2) conv3x3_c32_bf16_kernel(const GemmPara
   dma_row(hb - 1);
   dma_row(hb);
   dma_row(hb + 1);
-  for (int h = hb; h < he; ++h) {
-    gg_wait_vm<C3B_DMA_ROW>();
-    __builtin_amdgcn_s_barrier();
+  for (int h = hb; h < he; ++h) {  // the same schedule as the fp32 kernel
+    if (h == hb) {
+      gg_wait_vm<C3B_DMA_ROW>();
+      __builtin_amdgcn_s_barrier();
+    }
     floatx16 acc[1][1];
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[0][0][r] = 0.f;
     taps(acc[0][0], 0, h - 1);
-    taps(acc[0][0], 1, h);
     __builtin_amdgcn_s_barrier();
     const bool more = h + 1 < he;
     if (more) dma_row(h + 2);
-    if (more) gg_wait_vm<C3B_DMA_ROW>();
-    else gg_wait_vm<0>();
-    __builtin_amdgcn_s_barrier();
+    taps(acc[0][0], 1, h);
+    if (h == hb) {
+      if (more) gg_wait_vm<C3B_DMA_ROW>();
+      else gg_wait_vm<0>();
+      __builtin_amdgcn_s_barrier();
+    }
     taps(acc[0][0], 2, h + 1);
     gemm_epilogue<bf16_t, EPI, 4, 1, 1>(p, acc, epi, (int)(((long)b * H + h) * W + w0), n0);
   }
