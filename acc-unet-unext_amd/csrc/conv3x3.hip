@@ -378,14 +378,17 @@ conv3x3_c32_wgrad_kernel(const GemmParams p, int rows_per, float* __restrict__ s
     dma_row(hb);
     dma_row(hb + 1);
     load_dy(hb, a);
+    gg_wait_vm<0>();  // the first three rows and the first dY row have landed ...
+    __builtin_amdgcn_s_barrier();  // ... in every wave
     for (int h = hb; h < he; ++h) {
-      gg_wait_vm<0>();  // rows h-1 .. h+1 and the dY loads have landed ...
-      __builtin_amdgcn_s_barrier();  // ... in every wave
       taps_row(a, 0, h - 1);
-      __builtin_amdgcn_s_barrier();  // every wave is done with row h-1's slot
+      // row h+1 (issued during the previous row) has landed in this wave, and after the
+      // barrier in every wave, which is also done with row h-1's slot
+      gg_wait_vm<0>();
+      __builtin_amdgcn_s_barrier();
       const bool more = h + 1 < he;
       if (more) {
-        dma_row(h + 2);  // streams in during rows h, h+1's taps
+        dma_row(h + 2);  // streams in during the taps of rows h, h+1 and the next h-1
         load_dy(h + 1, an);
       }
       taps_row(a, 1, h);

@@ -10,7 +10,7 @@ tail -n 2 gpurun_out/c3_tests.log
 for rep in 1 2; do
   for v in 1 0; do
     echo "== ACCUNET_CONV3_HALO=$v" >> gpurun_out/c3_ab.txt
-    ACCUNET_CONV3_HALO=$v GB_ONLY=rspth1 timeout -k 10 120 tools/gbench 20 >> gpurun_out/c3_ab.txt 2>&1
+    ACCUNET_CONV3_HALO=$v GB_ONLY=rspth timeout -k 10 120 tools/gbench 20 >> gpurun_out/c3_ab.txt 2>&1
   done
 done
 cat gpurun_out/c3_ab.txt
