@@ -8,11 +8,10 @@
 //   pass 1 (se_reduce): per-(b,c) S = sum_hw a, Q = sum_hw a^2      [reads z once]
 //   mid   (se_mid_sample, one block per sample): S, Q from the chunk partials,
 //                      m = S/HW, s = sigmoid(fc2(lrelu(fc1(m))))
-//   pass 2 (se_apply): BN stats of y = a*s derived exactly from (S, Q, s) per channel
-//                      (se_bn_coef, by every block for its channels, no launch of its
-//                      own): mean = sum_b s*S / n,  E[y^2] = sum_b s^2*Q / n -> per-(b,c)
-//                      alpha = gamma*rstd*s, per-c beta' = beta - gamma*rstd*mean;
-//                      out = lrelu(alpha*a + beta')                [reads z, writes out]
+//   mid   (se_mid_bn, one thread per channel): BN stats of y = a*s derived exactly
+//                      from (S, Q, s): mean = sum_b s*S / n,  E[y^2] = sum_b s^2*Q / n
+//                      -> per-(b,c) alpha = gamma*rstd*s, per-c beta' = beta - gamma*rstd*mean
+//   pass 2 (se_apply): out = lrelu(alpha*a + beta')                [reads z, writes out]
 // so neither a nor y = a*s is ever materialised.
 //
 // Backward:
@@ -184,49 +183,42 @@ ACC_DEV void se_mid_sample_body(const double* __restrict__ part, const SeGeom& g
   }
 }
 
-// The middle step's channel part, evaluated inside the apply pass (no launch of its
-// own): each apply thread derives alpha[b,c] and beta'[c] of its channels from the saved
-// (S, Q, s) (fp64, sample order, so every block gets the same bits); the first block (sample 0, chunk 0) also stores the saved
-// mean / rstd / alpha / beta' for the backward and updates the running statistics.
-ACC_DEV void se_bn_coef(const SeGeom& g, const SeMid& m, int c, int b, bool store, float& al,
-                        float& be) {
+// middle step, part 2, channel c: BatchNorm statistics of y = a*s derived from
+// (S, Q, s), running-stat update, per-(b,c) coefficients.
+ACC_DEV void se_mid_bn_body(const SeGeom& g, const SeMid& m, int c) {
   const int B = g.B, C = g.C;
+  if (m.nbt && c == 0) *m.nbt += 1;  // num_batches_tracked (training only; null otherwise)
+  if (c >= C) return;
   SeSave sv = se_save_view(m.save, B, C, m.Cr);
   const double n = (double)B * g.HW;
   float mu, var;
   if (m.training) {
     double m1 = 0.0, m2 = 0.0;
 #pragma unroll 8
-    for (int bb = 0; bb < B; ++bb) {
-      double s = *(sv.sg + bb * C + c);
-      m1 += s * *(sv.S + bb * C + c);
-      m2 += s * s * *(sv.Q + bb * C + c);
+    for (int b = 0; b < B; ++b) {
+      double s = *(sv.sg + b * C + c);
+      m1 += s * *(sv.S + b * C + c);
+      m2 += s * s * *(sv.Q + b * C + c);
     }
     m1 /= n;
     m2 = m2 / n - m1 * m1;
     if (m2 < 0.0) m2 = 0.0;
     mu = (float)m1;
     var = (float)m2;
-    if (store) {
-      if (m.rmean) m.rmean[c] = (1.f - m.momentum) * m.rmean[c] + m.momentum * mu;
-      if (m.rvar)
-        m.rvar[c] = (1.f - m.momentum) * m.rvar[c] + m.momentum * (float)(m2 * n / (n - 1.0));
-    }
+    if (m.rmean) m.rmean[c] = (1.f - m.momentum) * m.rmean[c] + m.momentum * mu;
+    if (m.rvar)
+      m.rvar[c] = (1.f - m.momentum) * m.rvar[c] + m.momentum * (float)(m2 * n / (n - 1.0));
   } else {
     mu = m.rmean[c];
     var = m.rvar[c];
   }
-  const float rs = 1.f / sqrtf(var + m.eps);
-  const float k = m.gamma[c] * rs;
-  al = k * *(sv.sg + b * C + c);
-  be = m.beta[c] - k * mu;
-  if (store) {
-    sv.mean[c] = mu;
-    sv.rstd[c] = rs;
-    sv.betap[c] = be;
+  float rs = 1.f / sqrtf(var + m.eps);
+  float k = m.gamma[c] * rs;
+  sv.mean[c] = mu;
+  sv.rstd[c] = rs;
+  sv.betap[c] = m.beta[c] - k * mu;
 #pragma unroll 8
-    for (int bb = 0; bb < B; ++bb) sv.alpha[bb * C + c] = k * *(sv.sg + bb * C + c);
-  }
+  for (int b = 0; b < B; ++b) sv.alpha[b * C + c] = k * *(sv.sg + b * C + c);
 }
 
 // pass 1 forward: partials part[(b*NCH + chunk)][2][C] of (sum a, sum a^2).
@@ -254,6 +246,9 @@ se_mid_sample_kernel(const double* __restrict__ part, SeGeom g, SeMid m) {
   extern __shared__ __attribute__((aligned(16))) float se_dyn[];
   se_mid_sample_body(part, g, m, blockIdx.x, se_dyn);
 }
+__global__ void __launch_bounds__(256) se_mid_bn_kernel(SeGeom g, SeMid m) {
+  se_mid_bn_body(g, m, blockIdx.x * blockDim.x + threadIdx.x);
+}
 
 // pass 2 forward: out = lrelu(alpha[b,c]*a + betap[c]) (+ res: the residual add that
 // follows the SE in ResPath, ACC_UNet.py:326, and in the MLFC merge, :489-520, fused
@@ -262,12 +257,11 @@ se_mid_sample_kernel(const double* __restrict__ part, SeGeom g, SeMid m) {
 template <int V, typename T, bool PRO, bool RES>
 __global__ void __launch_bounds__(256)
 se_apply_kernel(const T* __restrict__ z, const float* __restrict__ sc,
-                const float* __restrict__ sh, int act, SeGeom g, SeMid m,
-                const T* __restrict__ res, T* __restrict__ out, double* __restrict__ ostats) {
+                const float* __restrict__ sh, int act, SeGeom g, const float* __restrict__ alpha,
+                const float* __restrict__ betap, const T* __restrict__ res, T* __restrict__ out,
+                double* __restrict__ ostats) {
   ChanTile t = chan_tile<V>(g.C);
   const int b = blockIdx.x / g.NCH, ch = blockIdx.x % g.NCH;
-  // num_batches_tracked (training only; null otherwise), once
-  if (m.nbt && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *m.nbt += 1;
   long r0 = (long)b * g.HW + ch * g.rows_per;
   long r1 = min((long)b * g.HW + g.HW, r0 + g.rows_per);
   double o1[V], o2[V];
@@ -279,7 +273,8 @@ se_apply_kernel(const T* __restrict__ z, const float* __restrict__ sc,
     for (int j = 0; j < V; ++j) {
       s[j] = PRO ? sc[t.c0 + j] : 1.f;
       h[j] = PRO ? sh[t.c0 + j] : 0.f;
-      se_bn_coef(g, m, t.c0 + j, b, blockIdx.x == 0 && t.rg == 0, al[j], be[j]);
+      al[j] = alpha[b * g.C + t.c0 + j];
+      be[j] = betap[t.c0 + j];
     }
     const bool st = ostats != nullptr;
     auto elem = [&](bool ok, const float (&x)[V], const float (&rv)[V], float (&v)[V]) {
@@ -891,16 +886,18 @@ extern "C" int accunet_se_fwd(const void* z, const float* sc, const float* sh, i
     if (V == 4) pro ? go(I4{}, std::true_type{}) : go(I4{}, std::false_type{});
     else pro ? go(I1{}, std::true_type{}) : go(I1{}, std::false_type{});
   });
-  // S, Q and the gate per sample; the BN-of-gated statistics per channel are derived
-  // inside the apply pass (se_bn_coef)
+  // S, Q and the gate per sample, then the BN-of-gated statistics per channel
   hipLaunchKernelGGL(se_mid_sample_kernel, dim3(B), dim3(256), (C + Cr) * sizeof(float), s, part,
                      g, m);
+  hipLaunchKernelGGL(se_mid_bn_kernel, dim3(ceil_div(C, 256)), dim3(256), 0, s, g, m);
+  const float* alpha = save + se_alpha_offset(B, C, Cr);
+  const float* betap = alpha + (size_t)B * C;
   with_dt(dt, [&](auto tag) {
     using T = decltype(tag);
     auto go = [&](auto kv, auto kp, auto kr) {
       hipLaunchKernelGGL((se_apply_kernel<decltype(kv)::value, T, decltype(kp)::value,
                                           decltype(kr)::value>),
-                         grid, dim3(256), 0, s, (const T*)z, sc, sh, act, g, m,
+                         grid, dim3(256), 0, s, (const T*)z, sc, sh, act, g, alpha, betap,
                          (const T*)res, (T*)out, ostats);
     };
     using I4 = std::integral_constant<int, 4>;

@@ -39,7 +39,7 @@ PROF = os.path.join(ROOT, "profiles")
 # with ACCUNET_DW_DMA=0, the register-staged strip
 K1 = os.environ.get("K1_KERNEL", "dw3x3_tile_fwd_kernel<8, false,")
 K1_GRID = 3072 * 256  # 1024 tiles (32-row strips) x 3 channel groups, 256 threads (16x256x256x96)
-K3 = ["se_reduce_kernel<4, float, true>", "se_mid_sample_kernel",
+K3 = ["se_reduce_kernel<4, float, true>", "se_mid_sample_kernel", "se_mid_bn_kernel",
       "se_apply_kernel<4, float, true,"]
 
 FAMILIES = ["gemm_f32g", "gemm_f32", "gemm_bf16", "splitk", "dw3x3", "reduce_finish", "bn_bwd",
