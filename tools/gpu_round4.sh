@@ -41,6 +41,6 @@ if [ -n "${PMC_GEMM:-}" ]; then
   # pyramid data gradient at the final sources
   timeout -k 10 300 python tools/gemm_census.py --top 200 > gpurun_out/census_full.txt 2>&1
   head -n 3 gpurun_out/census_full.txt
-  KEYS="32,288,1048576,1,2 1048576,32,288,2,0 65536,4352,128,0,1" timeout -k 10 900 bash tools/pmc_gemm.sh > gpurun_out/pmc_gemm.log 2>&1
+  KEYS="32,288,1048576,1,2 1048576,32,288,2,0 64,576,262144,1,2 65536,4352,128,0,1" timeout -k 10 900 bash tools/pmc_gemm.sh > gpurun_out/pmc_gemm.log 2>&1
   cat gpurun_out/pmc_gemm/report.txt
 fi
