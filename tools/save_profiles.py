@@ -12,6 +12,7 @@ stamped with the git commit and K1's source hash (accunet.probe.src_hash):
   {r}_bench_kernel_stats.csv  rocprofv3 --stats of bench.py --steps 5 --warmup 2
   {r}_bench_kstats.txt        per-kernel totals of that trace (tools/kstats.py)
   {r}_step_breakdown.txt      one graph-replayed step: time by kernel family, launches,
+                              (and {r}_step_breakdown_bf16.txt for the bf16 mode)
                               inter-kernel gaps
   {r}_k1_trace.txt            K1 dispatches: the 20-launch roofline probe (agrees with
                               the bench line's roofline.avg_us) and the in-model ones
@@ -67,8 +68,8 @@ def family(name):
     return name.split("(")[0][:40]
 
 
-def trace_rows():
-    f = glob.glob(os.path.join(OUT, "prof_bench", "**", "*kernel_trace.csv"), recursive=True)[0]
+def trace_rows(d="prof_bench"):
+    f = glob.glob(os.path.join(OUT, d, "**", "*kernel_trace.csv"), recursive=True)[0]
     rows = list(csv.DictReader(open(f)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     return rows
@@ -223,6 +224,10 @@ def main():
         open(os.path.join(PROF, f"{r}_bench_kstats.txt"), "w").write(f"# {st}\n" + ks)
         rows = trace_rows()
         open(os.path.join(PROF, f"{r}_step_breakdown.txt"), "w").write(step_breakdown(rows, st))
+        # the bf16 activation mode's step (BASELINE configs[2]) from its own trace
+        if glob.glob(os.path.join(OUT, "prof_bench_bf16", "**", "*kernel_trace.csv"), recursive=True):
+            open(os.path.join(PROF, f"{r}_step_breakdown_bf16.txt"), "w").write(
+                step_breakdown(trace_rows("prof_bench_bf16"), st + ", --dtype bf16"))
         open(os.path.join(PROF, f"{r}_k1_trace.txt"), "w").write(k1_trace(rows, st))
     # PMC: K1 and K3 traffic
     if glob.glob(os.path.join(OUT, "pmc_fetch", "**", "*counter_collection.csv"), recursive=True):
