@@ -378,7 +378,10 @@ def _emulate_relayout(it, src):
         nn = t // it.J
         order = np.array(list(it.order), dtype=np.int64)
         off = nn * it.C * it.J + c * it.J + order[jj]
-    out[:] = src[off]
+    if it.kind == 2:  # the group relayout's inverse: scatter
+        out[off] = src[i]
+    else:
+        out[:] = src[off]
     return out
 
 
@@ -425,3 +428,36 @@ def test_weight_prep_items_reproduce_the_per_op_layouts():
         assert it.out == buf.data_ptr() and it.inp == key[0]
         got = _emulate_relayout(it, ptr2w[it.inp])
         np.testing.assert_array_equal(got, want[key].reshape(-1).numpy(), err_msg=str(key))
+
+
+def test_deferred_weight_gradient_relayouts_items():
+    """ops.DeferredRelayouts (the captured backward's one-launch inverse relayouts): the
+    items the backward helpers append for a HANC grouped-column weight gradient (kind 2,
+    the inverse scatter), a ResPath 3x3 and a ConvT weight gradient (kind 0 permutes),
+    fed through the numpy restatement of the kernel's index arithmetic, give the torch
+    layouts the per-op relayouts produce; outside active() the helpers launch per op."""
+    from accunet import ops
+    torch.manual_seed(3)
+    d = ops.DeferredRelayouts("cpu")
+    k, N, C = 3, 6, 4
+    J = 2 * k - 1
+    order = list(ops._HANC_ORDER[k])
+    w = torch.randn(N, C * J)  # reference layout [n][c*J + j]
+    fwd = w.reshape(N, C, J)[:, :, order].permute(0, 2, 1).reshape(N, J * C)  # GEMM layout
+    Co, Ci = 5, 3
+    w3 = torch.randn(Co, Ci, 3, 3)
+    g3 = w3.permute(0, 2, 3, 1).reshape(Co, 9 * Ci)  # [co][tap][ci]
+    wt = torch.randn(Ci, Co, 2, 2)
+    gt = wt.permute(0, 2, 3, 1).reshape(Ci, 4 * Co)  # [ci][d][co]
+    outs = [torch.empty_like(w), torch.empty_like(w3), torch.empty_like(wt)]
+    with d.active():
+        assert ops._DEFER is d
+        ops._wgrad_group_inverse(fwd, outs[0], N, C, J, order)
+        ops._wgrad_permute(g3, outs[1], (Co, Ci, 3, 3), (9 * Ci, 1, 3 * Ci, Ci))
+        ops._wgrad_permute(gt, outs[2], (Ci, Co, 2, 2), (4 * Co, 1, 2 * Co, Co))
+    assert ops._DEFER is None and len(d.items) == 3
+    assert [it.kind for it in d.items] == [2, 0, 0]
+    assert d.destinations() == [o.data_ptr() for o in outs]
+    for it, src, want in zip(d.items, (fwd, g3, gt), (w, w3, wt)):
+        got = _emulate_relayout(it, src.reshape(-1).numpy())
+        np.testing.assert_array_equal(got, want.reshape(-1).numpy())
