@@ -260,8 +260,16 @@ static int pick_tile(int M, int N, int K, int bmode, int cin, bool can_split) {
   // epilogue-dominated, so smaller tiles (more resident waves to hide its gathers)
   const int sk = smallk_tile();
   // (128x32 tiles for 64 < N <= 96: 1Mx96x32 pyramid dgrad 368 vs 447 us; N = 64 is
-  // slower with them: 262144x64x64 +10 us)
-  if (sk >= 0 && K <= 64 && M >= 65536 && N > 32) return (N > 64 && N <= 96) ? TILE_C : sk;
+  // slower with them: 262144x64x64 +10 us. 128x64 tiles for N > 96: at K = 64, N = 192
+  // the forward is 11-14 % faster, the pyramid data gradient 3-8 %, the plain data
+  // gradient 5 % than with 64x64, profiles/r04_k64_tile_ab.txt)
+  static int wide = -1;
+  if (wide < 0) {
+    const char* e = getenv("ACCUNET_K64_TILE_B");  // A/B knob: 0 = 64x64 for N > 96 too
+    wide = e ? atoi(e) : 1;
+  }
+  if (sk >= 0 && K <= 64 && M >= 65536 && N > 32)
+    return (N > 64 && N <= 96) ? TILE_C : (wide && N > 96) ? TILE_B : sk;
   if (M <= 32) t = TILE_D;
   else if (M <= 64) t = TILE_E;
   else if (N <= 32) t = TILE_C;

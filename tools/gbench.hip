@@ -64,8 +64,8 @@ int main(int argc, char** argv) {
       {"cnv32 hnc fwd      262144x128x384 NT proA stats", 262144, 128, 384, AMODE_ROW, BMODE_NT, PRO_AFFINE_LRELU, 1, 0, 0, 0, 0},
       {"cnv72 x dgrad       65536x4352x128 NN", 65536, 4352, 128, AMODE_ROW, BMODE_NN, PRO_NONE, 0, 0, 0, 0, 0},
       {"cnv72 pyr dgrad     65536x4352x128 NN bnb+pyr", 65536, 4352, 128, AMODE_ROW, BMODE_NN, PRO_NONE, 1, 0, 64, 64, 0, 1},
-      {"cnv91 pyr dgrad   1048576x192x64 NN bnb+pyr", 1048576, 192, 64, AMODE_ROW, BMODE_NN, PRO_NONE, 1, 0, 256, 256, 0, 1},
-      {"cnv81 pyr dgrad    262144x192x64 NN bnb+pyr", 262144, 192, 64, AMODE_ROW, BMODE_NN, PRO_NONE, 1, 0, 128, 128, 0, 1},
+      {"k64 cnv91 pyr dgrad   1048576x192x64 NN bnb+pyr", 1048576, 192, 64, AMODE_ROW, BMODE_NN, PRO_NONE, 1, 0, 256, 256, 0, 1},
+      {"k64 cnv81 pyr dgrad    262144x192x64 NN bnb+pyr", 262144, 192, 64, AMODE_ROW, BMODE_NN, PRO_NONE, 1, 0, 128, 128, 0, 1},
       {"cnv92 pyr dgrad   1048576x96x32 NN bnb+pyr", 1048576, 96, 32, AMODE_ROW, BMODE_NN, PRO_NONE, 1, 0, 256, 256, 0, 1},
       {"cnv32 pyr dgrad    262144x384x128 NN bnb+pyr", 262144, 384, 128, AMODE_ROW, BMODE_NN, PRO_NONE, 1, 0, 128, 128, 0, 1},
       {"cnv72 x wgrad       4352x128x65536 COL NN split", 4352, 128, 65536, AMODE_COL, BMODE_NN, PRO_NONE, 0, 1, 0, 0, 0},
@@ -76,6 +76,9 @@ int main(int argc, char** argv) {
       {"rspth3 3x3 fwd     65536x128x1152 SHIFT3 stats", 65536, 128, 1152, AMODE_SHIFT3, BMODE_NT, PRO_NONE, 1, 0, 64, 64, 128},
       {"rspth3 3x3 wgrad   128x1152x65536 COL SHIFT3 split", 128, 1152, 65536, AMODE_COL, BMODE_NN_SHIFT3, PRO_NONE, 0, 1, 64, 64, 128},
       {"rspth2w 3x3 wgrad   64x576x262144 COL SHIFT3 split", 64, 576, 262144, AMODE_COL, BMODE_NN_SHIFT3, PRO_NONE, 0, 1, 128, 128, 64},
+      {"k64 cnv91 conv1-like fwd 1048576x192x64 NT stats", 1048576, 192, 64, AMODE_ROW, BMODE_NT, PRO_NONE, 1, 0, 0, 0, 0},
+      {"k64 cnv81 conv1-like fwd  262144x192x64 NT stats", 262144, 192, 64, AMODE_ROW, BMODE_NT, PRO_NONE, 1, 0, 0, 0, 0},
+      {"k64 dgrad 1048576x192x64 NN", 1048576, 192, 64, AMODE_ROW, BMODE_NN, PRO_NONE, 0, 0, 0, 0, 0},
       {"narrow conv 1x1 fwd 1048576x32x96 NT stats", 1048576, 32, 96, AMODE_ROW, BMODE_NT, PRO_NONE, 1, 0, 0, 0, 0},
   };
   // operand buffers sized for the largest shape (65536 x 4352 activations, 1M x 32 for B
