@@ -276,12 +276,20 @@ static int pick_tile(int M, int N, int K, int bmode, int cin, bool can_split) {
   else if (N <= 64) t = TILE_B;
   else t = TILE_A;
   // too few output tiles to occupy the 256 CUs (small-M layers: UNeXt's 14x14 / 28x28
-  // token stages, ACC-UNet's 16x16 level): 64x64 tiles give 2-4x the workgroups.
+  // token stages, ACC-UNet's 16x16 and 32x32 levels): 64x64 tiles give 2-4x the workgroups.
   // Not for split-K GEMMs (weight gradients): their K split already fills the chip
   // and the larger tile needs fewer operand loads per MFMA.
+  // (below 256 tiles: 128 left the 16x16-level GEMMs -- 4096x512x1536, 16384x128x256 --
+  // on 128x128 tiles over half the CUs; 256: -0.25 ms of GEMM time per step, step +0.35 %,
+  // profiles/r04_few_tiles_ab.txt)
+  static long few = -1;
+  if (few < 0) {
+    const char* e = getenv("ACCUNET_FEW_TILES");  // tuning knob: the tile-count threshold
+    few = e ? atol(e) : 256;
+  }
   if (!can_split && t != TILE_D && t != TILE_E && M > 64) {
     const long tiles = (long)ceil_div(M, tile_bm(t)) * ceil_div(N, tile_bn(t));
-    if (tiles < 128) t = TILE_E;
+    if (tiles < few) t = TILE_E;
   }
   (void)bmode;
   (void)cin;
