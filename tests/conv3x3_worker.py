@@ -15,7 +15,7 @@ from accunet import _lib, kern  # noqa: E402
 def main(out_path):
     torch.manual_seed(21)
     dev = "cuda"
-    B, H, W, C = 2, 64, 128, 32
+    B, H, W, C = 4, 64, 128, 32  # 256 tiles of 128 pixels: the halo kernels run
     P = B * H * W
     res = {}
     for dt in (torch.float32, torch.bfloat16):

@@ -159,7 +159,7 @@ def test_conv3x3_fwd_dgrad_wgrad(B, H, W, Ci, Co):
     assert rel(dw, refw) < 1e-5
 
 
-@pytest.mark.parametrize("B,H,W,Co", [(2, 64, 128, 32), (3, 40, 256, 64), (16, 256, 256, 32)])
+@pytest.mark.parametrize("B,H,W,Co", [(2, 128, 128, 32), (4, 32, 256, 32), (16, 256, 256, 32)])
 def test_conv3x3_halo_kernel_c32(B, H, W, Co):
     """The halo-tile 3x3 kernel (csrc/conv3x3.hip; 32 input channels, image rows of whole
     128-pixel tiles: the first ResPath level): forward with bias and the fp64 statistics
@@ -180,7 +180,9 @@ def test_conv3x3_halo_kernel_c32(B, H, W, Co):
     wr = w.detach().permute(0, 2, 3, 1).reshape(Co, 9 * Ci).float().contiguous()
     out = torch.empty(P, Co, device=DEV)
     rows = kern.gemm_stats_rows(P, Co, 9 * Ci, _lib.AMODE_SHIFT3, _lib.BMODE_NT, Ci)
-    assert rows == P // 128  # >= 128 tiles: the engine's 128x32 tiles, the halo kernel's
+    # >= 256 tiles of 128x32: the engine's tile there and the halo kernel's (fewer run
+    # 64x64 tiles on the engine, pick_tile)
+    assert rows == P // 128
     st = torch.zeros(rows, 2, Co, device=DEV, dtype=torch.float64)
     kern.gemm(P, Co, 9 * Ci, a=[xn], lda=[Ci], amode=_lib.AMODE_SHIFT3, b=wr, ldb=9 * Ci,
               c=out, ldc=Co, bias=bias.float(), stats=st, H=H, W=W, cin=Ci)
