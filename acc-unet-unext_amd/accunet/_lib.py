@@ -77,6 +77,7 @@ _SIGS = {
     "accunet_stream_ticket_bank": [P, I],
     "accunet_stream_ticket_unregister": [P],
     "accunet_abi_hash": [],
+    "accunet_conv3x3_halo_launches": [I],
     "accunet_relayout_blocks": [L],
     "accunet_relayout_batch": [P, I, I, P],
     "accunet_bn_finalize": [P, I, I, D, P, P, P, P, P, F, F, I, P, P, P],
@@ -152,7 +153,7 @@ _SIZE_FNS = {"accunet_bn_bwd_ws_elems", "accunet_bn_bwd_part_ws_elems", "accunet
              "accunet_head_ws_elems", "accunet_loss_ws_elems", "accunet_dwconvk_wgrad_ws",
              "accunet_dwconvk_dgrad_ws"}
 
-_LL_FNS = {"accunet_abi_hash"}
+_LL_FNS = {"accunet_abi_hash", "accunet_conv3x3_halo_launches"}
 HEADER = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "accunet.h")
 
 _lib = None

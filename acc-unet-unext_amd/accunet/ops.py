@@ -380,14 +380,17 @@ class DeferredRelayouts:
     """The backward's inverse weight relayouts -- HANCLayer / MLFC-merge weight
     gradients from the grouped GEMM columns back to the reference's interleave, the
     ResPath 3x3 and ConvTranspose2d weight gradients back to the torch layout -- taken
-    out of the per-layer backward and made by ONE accunet_relayout_batch launch at the
-    end of a captured backward (graph-mode TrainStep at world 1). Inside `active()` the
-    backward ops append items instead of launching; `flush()` (still inside the capture,
-    after loss.backward(): every side-stream weight-gradient fork has joined the main
-    stream by then) captures the one launch over a preallocated item table, and
-    `upload()` fills the table after the capture (the addresses are the graph pool's,
-    fixed for every replay). Not used with data parallelism: a gradient bucket must see
-    its final values when its all-reduce starts."""
+    out of the per-layer backward and made by batched accunet_relayout_batch launches
+    in a captured backward (graph-mode TrainStep). Inside `active()` the backward ops
+    append items instead of launching; each `flush()` captures one launch over the items
+    added since the previous flush, reading its own segment of a preallocated item
+    table, and `upload()` fills every segment after the capture (the addresses are the
+    graph pool's, fixed for every replay). At world 1 there is one flush, after
+    loss.backward() (every side-stream weight-gradient fork has joined the main stream by
+    then). With data parallelism a gradient bucket must hold final values when it is
+    packed for its all-reduce, so the bucket's seal flushes first (train._GraphBuckets):
+    one launch per sealed bucket instead of one per layer (the ops join their forks
+    before they return, so every pending item's source is final at a seal)."""
 
     CAP = 128
 
@@ -395,8 +398,9 @@ class DeferredRelayouts:
         self.items, self.keep = [], []
         self.table = torch.zeros(self.CAP * ctypes.sizeof(_lib.AccRelayout), dtype=torch.uint8,
                                  device=device)
-        self.n = self.nblocks = 0
-        self._raw = None
+        self.done = 0        # items already captured by a flush
+        self.segments = []   # (byte offset in the table, item bytes) per flush
+        self.launches = 0
 
     def full(self):
         return len(self.items) >= self.CAP
@@ -427,23 +431,29 @@ class DeferredRelayouts:
         self._add(src, dst, 2, N * J * C, N=N, C=C, J=J, order=order)
 
     def flush(self):
-        if not self.items:
+        """one launch for the items added since the last flush (none: no launch)"""
+        new = self.items[self.done:]
+        if not new:
             return
         blk = 0
-        for it in self.items:
+        for it in new:
             it.blk0 = blk
             blk += kern.relayout_blocks(it.total)
-        self.n, self.nblocks = len(self.items), blk
-        self._raw = bytes((_lib.AccRelayout * self.n)(*self.items))
-        kern.relayout_batch(self.table, self.n, self.nblocks)
+        sz = ctypes.sizeof(_lib.AccRelayout)
+        off = self.done * sz
+        raw = bytes((_lib.AccRelayout * len(new))(*new))
+        self.segments.append((off, raw))
+        kern.relayout_batch(self.table[off:], len(new), blk)
+        self.done = len(self.items)
+        self.launches += 1
 
     def destinations(self):
         return [int(it.out) for it in self.items]
 
     def upload(self):
-        if self._raw:
-            self.table[:len(self._raw)].copy_(
-                torch.frombuffer(bytearray(self._raw), dtype=torch.uint8))
+        for off, raw in self.segments:
+            self.table[off:off + len(raw)].copy_(
+                torch.frombuffer(bytearray(raw), dtype=torch.uint8))
 
     @contextlib.contextmanager
     def active(self):

@@ -97,6 +97,8 @@ class _GraphBuckets:
         if self._sealed[k]:
             return
         self._sealed[k] = True
+        if ops._DEFER is not None:  # pending inverse weight relayouts: final values first
+            ops._DEFER.flush()
         live = [i for i in self.buckets[k] if self.params[i].grad is not None]
         if live:
             torch._foreach_copy_([self.wviews[i] for i in live], [self.params[i].grad for i in live])
@@ -144,14 +146,17 @@ class _GraphBuckets:
             return
         works = []
         with torch.cuda.stream(self.stream):
+            # every reduce first, each behind its own bucket's event only: RCCL's stream
+            # waits on this side stream when a collective is enqueued, so a widening copy
+            # issued between two reduces would hold the next reduce back
             for k, (lo, hi) in enumerate(self.range):
                 self.events[k].wait(self.stream)
-                w = dist.all_reduce(self.wire[lo:hi], op=dist.ReduceOp.AVG, group=pg,
-                                    async_op=True)
-                if narrow:  # widen this bucket on the side stream once RCCL is done with it
+                works.append(dist.all_reduce(self.wire[lo:hi], op=dist.ReduceOp.AVG, group=pg,
+                                             async_op=True))
+            if narrow:  # widen each bucket on the side stream once RCCL is done with it
+                for (lo, hi), w in zip(self.range, works):
                     w.wait()
                     self.flat[lo:hi].copy_(self.wire[lo:hi])
-                works.append(w)
         for w in works:  # the main stream (Adam) waits on RCCL's stream
             w.wait()
         main.wait_stream(self.stream)
@@ -257,10 +262,11 @@ class TrainStep:
                                           self.comm_dtype)
             self._buckets.stream = torch.cuda.Stream()
             self._buckets.arm()
-        # the backward's inverse weight relayouts in one launch at its end (world 1 only:
-        # a DP gradient bucket must hold final values when its all-reduce starts)
+        # the backward's inverse weight relayouts batched: one launch at its end at world 1;
+        # with data parallelism one launch per sealed bucket (a gradient bucket must hold
+        # final values when it is packed for its all-reduce, _GraphBuckets._seal)
         self._defer = None
-        if not self.dp and os.environ.get("ACCUNET_DEFER_RELAYOUT", "1") != "0":
+        if os.environ.get("ACCUNET_DEFER_RELAYOUT", "1") != "0":
             self._defer = ops.DeferredRelayouts(self._x.device)
         g = torch.cuda.CUDAGraph(keep_graph=self._buckets is not None)
         try:

@@ -26,6 +26,8 @@
 //     runs unchanged: statistics rows and results are indexed exactly as the engine's.
 #include "gemm_dispatch.h"
 
+#include <atomic>
+
 #define C3_CIN 32
 #define C3_BM 128
 #define C3_SLOTS (C3_BM + 2)
@@ -115,10 +117,10 @@ __global__ void __launch_bounds__(256, 2) conv3x3_c32_kernel(const GemmParams p,
   dma_row(hb);
   dma_row(hb + 1);
   for (int h = hb; h < he; ++h) {
-    // Rows h-1 .. h+1 are needed. Past the first row they are in place: each new row
-    // was issued during the previous row's taps and drained by that row's epilogue
-    // (its barriers wait for all memory), so only the first row waits here: rows
-    // hb-1 and hb have landed (hb+1 may still be in flight) in every wave.
+    // Rows h-1 .. h+1 are needed. Past the first row, rows h-1 and h are in place and
+    // row h+1 (issued during the previous row's taps) is waited for explicitly after
+    // taps(0, h-1) below; at the first row: rows hb-1 and hb have landed (hb+1 may
+    // still be in flight) in every wave.
     if (h == hb) {
       gg_wait_vm<C3_DMA_ROW>();
       __builtin_amdgcn_s_barrier();
@@ -127,6 +129,9 @@ __global__ void __launch_bounds__(256, 2) conv3x3_c32_kernel(const GemmParams p,
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[0][0][r] = 0.f;
     taps(acc[0][0], 0, h - 1);
+    // past the first row, row h+1 (issued during the previous row) must have landed in
+    // every wave before taps(2, h+1): an explicit wait here, not the epilogue's drain
+    if (h > hb) gg_wait_vm<0>();
     // every wave is done with row h-1's slot: row h+2 streams into it during the taps
     // of rows h, h+1 and the epilogue
     __builtin_amdgcn_s_barrier();
@@ -233,6 +238,7 @@ __global__ void __launch_bounds__(256, 2) conv3x3_c32_bf16_kernel(const GemmPara
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[0][0][r] = 0.f;
     taps(acc[0][0], 0, h - 1);
+    if (h > hb) gg_wait_vm<0>();  // row h+1 landed in every wave (as the fp32 kernel)
     __builtin_amdgcn_s_barrier();
     const bool more = h + 1 < he;
     if (more) dma_row(h + 2);
@@ -245,6 +251,14 @@ __global__ void __launch_bounds__(256, 2) conv3x3_c32_bf16_kernel(const GemmPara
     taps(acc[0][0], 2, h + 1);
     gemm_epilogue<bf16_t, EPI, 4, 1, 1>(p, acc, epi, (int)(((long)b * H + h) * W + w0), n0);
   }
+}
+
+// host-side launch counts (accunet_conv3x3_halo_launches): [0] forward / data gradient,
+// [1] weight gradient
+static std::atomic<long long> g_c3_launches[2];
+
+extern "C" long long accunet_conv3x3_halo_launches(int wgrad) {
+  return g_c3_launches[wgrad ? 1 : 0].load();
 }
 
 static int conv3x3_c32_on() {
@@ -294,6 +308,7 @@ int conv3x3_c32_try(const GemmParams& p, int amode, int bmode, int pro_a, int pr
   } else {
     hipLaunchKernelGGL(conv3x3_c32_kernel<EPI_STATS>, grid, dim3(256), 0, stream, p, rows_per);
   }
+  g_c3_launches[0]++;
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 
@@ -445,5 +460,6 @@ int conv3x3_c32_wgrad_try(const GemmParams& p, int amode, int bmode, int pro_a, 
   if ((size_t)nb * p.M * p.N > ws_elems) return 0;
   hipLaunchKernelGGL(conv3x3_c32_wgrad_kernel, dim3((unsigned)nb, nblk), dim3(256), 0, stream, p,
                      rows_per, ws);
+  g_c3_launches[1]++;
   return (int)nb;
 }

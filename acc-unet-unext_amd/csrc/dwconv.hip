@@ -653,658 +653,6 @@ dw3x3_tile_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
   }
 }
 
-// ----------------------------------------------------------------------------
-// K1 with LDS-DMA staging (fp32, 32-channel tiles, no BN-backward epilogue; the
-// default forward of those shapes, ACCUNET_DW_DMA). Same tile geometry and strips as
-// dw3x3_tile_fwd_kernel, but input rows go HBM -> LDS by `global_load_lds_dwordx4`
-// (no VGPR destination), so the prefetch depth is bounded by LDS, not by registers:
-// a 12-slot ring holds three 4-row chunks -- the one being computed, the next (landed,
-// being activated) and the one after (in flight) -- 52 KB per block, 3 blocks per CU,
-// so ~100 KB of input rows per CU stay in flight (the register-staged strip keeps one
-// chunk, ~52 KB per CU).
-// Ring row layout (272 float4): pixels 0..31 of the tile x 8 quads, then the left and
-// right halo pixels x 8 quads. One wave owns one row of a chunk: 4 DMA instructions
-// of 1 KB (the interior, lane-linear) + 1 of 16 lanes (the two halo pixels).
-// Out-of-image pixels and rows load a clamped in-image address and are zeroed when
-// the wave that loaded them applies the prologue (BN scale/shift + LeakyReLU) in
-// place, after its own DMA has landed (counted vmcnt) and before the barrier that
-// publishes the chunk. The 3x3 window is a pair of rolling row accumulators carried
-// across chunks (each input row read once per thread: left, centre, right quad), in
-// the same FMA order as a whole-window sum (bias, then taps row-major).
-// ----------------------------------------------------------------------------
-// s_waitcnt vmcnt(N) with every other counter left alone (gfx9 encoding)
-template <int N>
-ACC_DEV void dw_wait_vm() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
-}
-
-#define DWD_ROW 272
-#define DWD_SLOTS 12
-
-template <bool NT>
-ACC_DEV void dwd_dma16(const float* src, unsigned lds_byte) {
-  unsigned keep;
-  if (NT)
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(src), "s"(lds_byte)
-                 : "memory");
-  else
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(src), "s"(lds_byte)
-                 : "memory");
-}
-
-template <bool NT>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
-dw3x3_dma_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
-                     const float* __restrict__ bias, const float* __restrict__ sc,
-                     const float* __restrict__ sh, int act, int flip, float* __restrict__ z,
-                     double* __restrict__ stats, DwTGeom g) {
-  constexpr int TCQ = 8, TP = 32, CR = 4;
-  __shared__ float4 ring[DWD_SLOTS * DWD_ROW];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int q = tid % TCQ, p = tid / TCQ;
-  int t = dw_tile_id(g);
-  int cg = blockIdx.y;
-  if (g.cgf) {
-    cg = t % g.cgf;
-    t /= g.cgf;
-  }
-  const int srow = g.cgf ? t : (int)blockIdx.x;
-  const int c0 = cg * TCQ * 4;
-  const int c = c0 + 4 * q;
-  const int tw = t % g.tilesW;
-  t /= g.tilesW;
-  const int th = t % g.tilesH;
-  const int b = t / g.tilesH;
-  const int hbeg = th * DW_TR * g.rch, w0 = tw * TP;
-  const int hend = min(g.H, hbeg + DW_TR * g.rch);
-  const int nch = (hend - hbeg + CR - 1) / CR;
-  const float* ximg = x + (long)b * g.H * g.W * g.C;
-  const long img = (long)b * g.H * g.W * g.C;
-  const __amdgpu_buffer_rsrc_t rz = acc_rsrc(z + img, (unsigned)(g.H * g.W * g.C * 4));
-  const unsigned ring_lds =
-      (unsigned)(size_t)(__attribute__((address_space(3))) float4*)ring;
-  // the DMA lane map: interior piece i (0..3): pixel 8 i + lane / 8, quad lane % 8;
-  // halo piece (lanes 0..15): pixel -1 (lanes 0..7) / 32 (lanes 8..15)
-  const int lq = lane & 7;
-  const int hip = lane < 8 ? -1 : TP;
-  // chunk j >= -1 = input rows hbeg + 1 + 4j .. +3 (j = -1: rows hbeg-3 .. hbeg, of which
-  // hbeg-1 and hbeg start the window); wave wv owns row hbeg + 1 + 4j + wv, ring slot
-  // (4 (j + 1) + wv) % 12
-  auto issue = [&](int j) {
-    const int R = hbeg + 1 + CR * j + wv;
-    const int Rl = max(0, min(R, min(hend, g.H - 1)));  // rows past the strip: a re-read
-    const int slot = (CR * (j + 1) + wv) % DWD_SLOTS;
-    const float* rowp = ximg + (long)Rl * g.W * g.C + c0 + 4 * lq;
-    const unsigned base = ring_lds + (unsigned)(slot * DWD_ROW) * 16u;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int wp = min(w0 + 8 * i + (lane >> 3), g.W - 1);
-      dwd_dma16<NT>(rowp + (long)wp * g.C, base + i * 1024u);
-    }
-    if (lane < 16) {
-      const int wp = max(0, min(w0 + hip, g.W - 1));
-      dwd_dma16<NT>(rowp + (long)wp * g.C, base + 4096u);
-    }
-  };
-  const bool pro = sc != nullptr;
-  const float4 ps = pro ? ld4(sc + c0 + 4 * lq) : make_float4(1.f, 1.f, 1.f, 1.f);
-  const float4 pb = pro ? ld4(sh + c0 + 4 * lq) : make_float4(0.f, 0.f, 0.f, 0.f);
-  // prologue (BN+act, in-image only; zero padding after the activation) of the wave's
-  // own pieces of chunk j, in place
-  auto activate = [&](int j) {
-    const int R = hbeg + 1 + CR * j + wv;
-    const int slot = (CR * (j + 1) + wv) % DWD_SLOTS;
-    const bool rin = R >= 0 && R < g.H;
-    float4* rw = ring + slot * DWD_ROW;
-    auto fix = [&](float4 v, bool in) {
-      if (pro) {
-        v.x = apply_act(v.x * ps.x + pb.x, act);
-        v.y = apply_act(v.y * ps.y + pb.y, act);
-        v.z = apply_act(v.z * ps.z + pb.z, act);
-        v.w = apply_act(v.w * ps.w + pb.w, act);
-      }
-      return make_float4(in ? v.x : 0.f, in ? v.y : 0.f, in ? v.z : 0.f, in ? v.w : 0.f);
-    };
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int e = 64 * i + lane;
-      rw[e] = fix(rw[e], rin && w0 + 8 * i + (lane >> 3) < g.W);
-    }
-    if (lane < 16) {
-      const int wp = w0 + hip;
-      rw[256 + lane] = fix(rw[256 + lane], rin && wp >= 0 && wp < g.W);
-    }
-  };
-  issue(-1);
-  issue(0);
-  issue(1);
-  // weights: the quad's 4 channels x 9 taps are 36 contiguous floats of wt ([C][9])
-  float k[9][4], bi[4];
-  {
-    float wvv[36];
-#pragma unroll
-    for (int e = 0; e < 9; ++e) {
-      const float4 w4 = ld4(wt + c * 9 + 4 * e);
-      wvv[4 * e] = w4.x; wvv[4 * e + 1] = w4.y; wvv[4 * e + 2] = w4.z; wvv[4 * e + 3] = w4.w;
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int tp = 0; tp < 9; ++tp) k[tp][j] = wvv[j * 9 + (flip ? 8 - tp : tp)];
-    const float4 b4 = bias ? ld4(bias + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-    bi[0] = b4.x; bi[1] = b4.y; bi[2] = b4.z; bi[3] = b4.w;
-  }
-  // everything issued so far has landed (chunks -1, 0, 1 and the weights): activate the
-  // two chunks the window starts from, publish, read the first two rows, and let every
-  // wave pass them before chunk -1's slots are refilled
-  __builtin_amdgcn_s_waitcnt(0);
-  activate(-1);
-  activate(0);
-  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-  __builtin_amdgcn_s_barrier();
-  // reads the thread's 3 quads (tile pixels p-1, p, p+1) of input row R (chunk j, row rr)
-  auto rdrow = [&](int slot, float (&row)[3][4]) {
-    const float4* rw = ring + slot * DWD_ROW;
-    const int e = p * TCQ + q;
-    const float4 l = rw[p == 0 ? 256 + q : e - TCQ];
-    const float4 m = rw[e];
-    const float4 r = rw[p == TP - 1 ? 264 + q : e + TCQ];
-    row[0][0] = l.x; row[0][1] = l.y; row[0][2] = l.z; row[0][3] = l.w;
-    row[1][0] = m.x; row[1][1] = m.y; row[1][2] = m.z; row[1][3] = m.w;
-    row[2][0] = r.x; row[2][1] = r.y; row[2][2] = r.z; row[2][3] = r.w;
-  };
-  float a0[4], a1[4];
-  {
-    float row[3][4];
-    rdrow(2, row);  // input row hbeg - 1
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float acc = bi[j];
-#pragma unroll
-      for (int dx = 0; dx < 3; ++dx) acc = fmaf(k[dx][j], row[dx][j], acc);
-      a0[j] = acc;
-    }
-    rdrow(3, row);  // input row hbeg
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float acc = a0[j], nxt = bi[j];
-#pragma unroll
-      for (int dx = 0; dx < 3; ++dx) {
-        acc = fmaf(k[3 + dx][j], row[dx][j], acc);
-        nxt = fmaf(k[dx][j], row[dx][j], nxt);
-      }
-      a0[j] = acc;
-      a1[j] = nxt;
-    }
-  }
-  __builtin_amdgcn_s_waitcnt(0xc07f);
-  __builtin_amdgcn_s_barrier();
-  double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
-  const int w = w0 + p;
-  const bool wok = w < g.W;
-  for (int kc = 0; kc < nch; ++kc) {
-    issue(kc + 2);  // into chunk kc-1's slots, free since the last barrier
-    const int r0 = hbeg + CR * kc;
-    const int nr = min(CR, hend - r0);
-    float c1[4] = {0.f, 0.f, 0.f, 0.f}, c2[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int r = 0; r < CR; ++r) {
-      const bool on = wok && r < nr;
-      float row[3][4];
-      rdrow((CR * (kc + 1) + r) % DWD_SLOTS, row);
-      float o[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float acc = a0[j], mid = a1[j], nxt = bi[j];
-#pragma unroll
-        for (int dx = 0; dx < 3; ++dx) {
-          acc = fmaf(k[6 + dx][j], row[dx][j], acc);
-          mid = fmaf(k[3 + dx][j], row[dx][j], mid);
-          nxt = fmaf(k[dx][j], row[dx][j], nxt);
-        }
-        a0[j] = mid;
-        a1[j] = nxt;
-        o[j] = acc;
-        const float am = on ? acc : 0.f;
-        c1[j] += am;
-        c2[j] = fmaf(am, am, c2[j]);
-      }
-      const unsigned off = on ? (unsigned)((((r0 + r) * g.W + w) * g.C + c) * 4) : ACC_OOB;
-      bufq_st<2>(rz, off, make_float4(o[0], o[1], o[2], o[3]), (float*)nullptr);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      s1[j] += (double)c1[j];
-      s2[j] += (double)c2[j];
-    }
-    // chunk kc+1's DMA (issued one iteration ago) has landed once only the 5 DMA pieces
-    // of chunk kc+2 and the 4 + 4 stores of chunks kc-1, kc are younger (chunk 1 was
-    // drained in the prologue)
-    if (kc == 0) dw_wait_vm<9>();
-    else dw_wait_vm<13>();
-    activate(kc + 1);
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_s_barrier();
-  }
-  // the ring becomes the reduction buffer: no DMA may still be writing it
-  __builtin_amdgcn_s_waitcnt(0);
-  if (stats) {
-    __syncthreads();
-    double v[8] = {s1[0], s1[1], s1[2], s1[3], s2[0], s2[1], s2[2], s2[3]};
-    if (block_slot_reduce<TCQ, 8, double>(v, reinterpret_cast<double*>(ring))) {
-      const long row = (long)srow * 2 * g.C;
-      const int cc = c0 + 4 * threadIdx.x;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        stats[row + cc + j] = v[j];
-        stats[row + g.C + cc + j] = v[4 + j];
-      }
-    }
-  }
-}
-
-// bf16 storage: the same LDS-DMA pipeline, but the DMA'd rows are raw bf16 (a 16-B
-// piece = 2 channel quads) in a raw ring of two chunks (the next, landed, and the one
-// after, in flight), and the activation widens each wave's own pieces into an fp32
-// ring (the window arithmetic stays fp32, as in the register-staged kernel): ACTC = 2
-// chunk slots there (one barrier per chunk: the next chunk is activated while this one
-// is read) for 32-channel tiles, 1 slot (two barriers per chunk) for 64-channel tiles,
-// whose rows are longer. LDS per block: TCQ 8 52 KB, TCQ 16 37 KB.
-template <int TCQ, bool NT>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
-dw3x3_dma_bf16_fwd_kernel(const bf16_t* __restrict__ x, const float* __restrict__ wt,
-                          const float* __restrict__ bias, const float* __restrict__ sc,
-                          const float* __restrict__ sh, int act, int flip,
-                          bf16_t* __restrict__ z, double* __restrict__ stats, DwTGeom g) {
-  constexpr int TP = 256 / TCQ, CR = 4;
-  constexpr int ROWQ = 256 + 2 * TCQ;     // quads per row: interior, then left / right halo
-  constexpr int RAWB = ROWQ * 8;          // bytes per raw bf16 row
-  constexpr int ACTC = TCQ == 8 ? 2 : 1;  // fp32 chunk slots
-  __shared__ float4 ring[ACTC * CR * ROWQ];
-  __shared__ __attribute__((aligned(16))) unsigned char raw[2 * CR * RAWB];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int q = tid % TCQ, p = tid / TCQ;
-  int t = dw_tile_id(g);
-  int cg = blockIdx.y;
-  if (g.cgf) {
-    cg = t % g.cgf;
-    t /= g.cgf;
-  }
-  const int srow = g.cgf ? t : (int)blockIdx.x;
-  const int c0 = cg * TCQ * 4;
-  const int c = c0 + 4 * q;
-  const int tw = t % g.tilesW;
-  t /= g.tilesW;
-  const int th = t % g.tilesH;
-  const int b = t / g.tilesH;
-  const int hbeg = th * DW_TR * g.rch, w0 = tw * TP;
-  const int hend = min(g.H, hbeg + DW_TR * g.rch);
-  const int nch = (hend - hbeg + CR - 1) / CR;
-  const long img = (long)b * g.H * g.W * g.C;
-  const bf16_t* ximg = x + img;
-  const __amdgpu_buffer_rsrc_t rz = acc_rsrc(z + img, (unsigned)(g.H * g.W * g.C * 2));
-  const unsigned raw_lds = (unsigned)(size_t)(__attribute__((address_space(3))) unsigned char*)raw;
-  // a lane's 16-B pieces: interior piece i (0, 1) = quads 128 i + 2 lane, +1, i.e. pixel
-  // (128 i + 2 lane) / TCQ, quad pair lq = (2 lane) % TCQ; halo (lanes < TCQ) = quads
-  // 2 lane, +1 of [left | right], pixel -1 / TP
-  const int lq = (2 * lane) % TCQ;
-  const int hside = (2 * lane) / TCQ;  // halo lanes: 0 left, 1 right
-  const int hip = hside ? TP : -1;
-  auto issue = [&](int j) {  // chunk j >= -1: rows hbeg + 1 + 4j .. +3, wave wv owns one
-    const int R = hbeg + 1 + CR * j + wv;
-    const int Rl = max(0, min(R, min(hend, g.H - 1)));
-    const int slot = ((j + 2) & 1) * CR + wv;
-    const bf16_t* rowp = ximg + (long)Rl * g.W * g.C + c0 + 4 * lq;
-    const unsigned base = raw_lds + (unsigned)(slot * RAWB);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int wp = min(w0 + (128 * i + 2 * lane) / TCQ, g.W - 1);
-      dwd_dma16<NT>(reinterpret_cast<const float*>(rowp + (long)wp * g.C), base + i * 1024u);
-    }
-    if (lane < TCQ) {
-      const int wp = max(0, min(w0 + hip, g.W - 1));
-      dwd_dma16<NT>(reinterpret_cast<const float*>(rowp + (long)wp * g.C), base + 2048u);
-    }
-  };
-  const bool pro = sc != nullptr;
-  float4 ps[2], pb[2];
-#pragma unroll
-  for (int e = 0; e < 2; ++e) {
-    ps[e] = pro ? ld4(sc + c0 + 4 * (lq + e)) : make_float4(1.f, 1.f, 1.f, 1.f);
-    pb[e] = pro ? ld4(sh + c0 + 4 * (lq + e)) : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  // widen + prologue (in-image only, zero padding after the activation) of the wave's
-  // own raw pieces of chunk j into the fp32 ring
-  auto activate = [&](int j) {
-    const int R = hbeg + 1 + CR * j + wv;
-    const int rslot = ((j + 2) & 1) * CR + wv;
-    const int aslot = (ACTC == 2 ? ((j + 2) & 1) * CR : 0) + wv;
-    const bool rin = R >= 0 && R < g.H;
-    const uint4* rr = reinterpret_cast<const uint4*>(raw + rslot * RAWB);
-    float4* aw = ring + aslot * ROWQ;
-    auto fix = [&](uint4 u, bool in, int e0) {
-      float4 v0 = make_float4(bflo(u.x), bfhi(u.x), bflo(u.y), bfhi(u.y));
-      float4 v1 = make_float4(bflo(u.z), bfhi(u.z), bflo(u.w), bfhi(u.w));
-      v0.x = apply_act(v0.x * ps[0].x + pb[0].x, act); v0.y = apply_act(v0.y * ps[0].y + pb[0].y, act);
-      v0.z = apply_act(v0.z * ps[0].z + pb[0].z, act); v0.w = apply_act(v0.w * ps[0].w + pb[0].w, act);
-      v1.x = apply_act(v1.x * ps[1].x + pb[1].x, act); v1.y = apply_act(v1.y * ps[1].y + pb[1].y, act);
-      v1.z = apply_act(v1.z * ps[1].z + pb[1].z, act); v1.w = apply_act(v1.w * ps[1].w + pb[1].w, act);
-      // component-wise selects (a select of whole float4 values lands in scratch)
-      aw[e0] = make_float4(in ? v0.x : 0.f, in ? v0.y : 0.f, in ? v0.z : 0.f, in ? v0.w : 0.f);
-      aw[e0 + 1] = make_float4(in ? v1.x : 0.f, in ? v1.y : 0.f, in ? v1.z : 0.f, in ? v1.w : 0.f);
-    };
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int qq = 128 * i + 2 * lane;
-      fix(rr[64 * i + lane], rin && w0 + qq / TCQ < g.W, qq);
-    }
-    if (lane < TCQ) {
-      const int wp = w0 + hip;
-      fix(rr[128 + lane], rin && wp >= 0 && wp < g.W, 256 + 2 * lane);
-    }
-  };
-  issue(-1);
-  issue(0);
-  float k[9][4], bi[4];
-  {
-    float wvv[36];
-#pragma unroll
-    for (int e = 0; e < 9; ++e) {
-      const float4 w4 = ld4(wt + c * 9 + 4 * e);
-      wvv[4 * e] = w4.x; wvv[4 * e + 1] = w4.y; wvv[4 * e + 2] = w4.z; wvv[4 * e + 3] = w4.w;
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int tp = 0; tp < 9; ++tp) k[tp][j] = wvv[j * 9 + (flip ? 8 - tp : tp)];
-    const float4 b4 = bias ? ld4(bias + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-    bi[0] = b4.x; bi[1] = b4.y; bi[2] = b4.z; bi[3] = b4.w;
-  }
-  __builtin_amdgcn_s_waitcnt(0);
-  // ACTC 1: chunk -1 widened, its two window rows read, then chunk 0 into the same slot
-  auto rdrow = [&](int aslot, float (&row)[3][4]) {
-    const float4* rw = ring + aslot * ROWQ;
-    const int e = p * TCQ + q;
-    const float4 l = rw[p == 0 ? 256 + q : e - TCQ];
-    const float4 m = rw[e];
-    const float4 r = rw[p == TP - 1 ? 256 + TCQ + q : e + TCQ];
-    row[0][0] = l.x; row[0][1] = l.y; row[0][2] = l.z; row[0][3] = l.w;
-    row[1][0] = m.x; row[1][1] = m.y; row[1][2] = m.z; row[1][3] = m.w;
-    row[2][0] = r.x; row[2][1] = r.y; row[2][2] = r.z; row[2][3] = r.w;
-  };
-  activate(-1);
-  if (ACTC == 2) activate(0);
-  __builtin_amdgcn_s_waitcnt(0xc07f);
-  __builtin_amdgcn_s_barrier();
-  float a0[4], a1[4];
-  {
-    const int am1 = ACTC == 2 ? CR : 0;  // chunk -1's act slot
-    float row[3][4];
-    rdrow(am1 + 2, row);  // input row hbeg - 1
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float acc = bi[j];
-#pragma unroll
-      for (int dx = 0; dx < 3; ++dx) acc = fmaf(k[dx][j], row[dx][j], acc);
-      a0[j] = acc;
-    }
-    rdrow(am1 + 3, row);  // input row hbeg
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float acc = a0[j], nxt = bi[j];
-#pragma unroll
-      for (int dx = 0; dx < 3; ++dx) {
-        acc = fmaf(k[3 + dx][j], row[dx][j], acc);
-        nxt = fmaf(k[dx][j], row[dx][j], nxt);
-      }
-      a0[j] = acc;
-      a1[j] = nxt;
-    }
-  }
-  __builtin_amdgcn_s_waitcnt(0xc07f);
-  __builtin_amdgcn_s_barrier();
-  if (ACTC == 1) {  // chunk 0 into the slot chunk -1 leaves
-    activate(0);
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_s_barrier();
-  }
-  issue(1);  // into chunk -1's raw slot, free since chunk -1 was widened
-  double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
-  const int w = w0 + p;
-  const bool wok = w < g.W;
-  for (int kc = 0; kc < nch; ++kc) {
-    issue(kc + 2);  // into chunk kc's raw slot (widened in the previous iteration)
-    const int r0 = hbeg + CR * kc;
-    const int nr = min(CR, hend - r0);
-    const int ab = ACTC == 2 ? (kc & 1) * CR : 0;
-    float c1[4] = {0.f, 0.f, 0.f, 0.f}, c2[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int r = 0; r < CR; ++r) {
-      const bool on = wok && r < nr;
-      float row[3][4];
-      rdrow(ab + r, row);
-      float o[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float acc = a0[j], mid = a1[j], nxt = bi[j];
-#pragma unroll
-        for (int dx = 0; dx < 3; ++dx) {
-          acc = fmaf(k[6 + dx][j], row[dx][j], acc);
-          mid = fmaf(k[3 + dx][j], row[dx][j], mid);
-          nxt = fmaf(k[dx][j], row[dx][j], nxt);
-        }
-        a0[j] = mid;
-        a1[j] = nxt;
-        acc = rnd<bf16_t>(acc);  // statistics of the stored value
-        o[j] = acc;
-        const float am = on ? acc : 0.f;
-        c1[j] += am;
-        c2[j] = fmaf(am, am, c2[j]);
-      }
-      const unsigned off = on ? (unsigned)((((r0 + r) * g.W + w) * g.C + c) * 2) : ACC_OOB;
-      bufq_st<2>(rz, off, make_float4(o[0], o[1], o[2], o[3]), (bf16_t*)nullptr);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      s1[j] += (double)c1[j];
-      s2[j] += (double)c2[j];
-    }
-    // chunk kc+1's raw DMA has landed once only chunk kc+2's 3 pieces and the stores of
-    // chunks kc-1 and kc (4 each) are younger (kc = 0: chunk 1 was issued after the
-    // prologue, behind no stores)
-    if (kc == 0) dw_wait_vm<7>();
-    else dw_wait_vm<11>();
-    if (ACTC == 1) {  // every wave is done reading chunk kc's slot
-      __builtin_amdgcn_s_waitcnt(0xc07f);
-      __builtin_amdgcn_s_barrier();
-    }
-    activate(kc + 1);
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_s_barrier();
-  }
-  __builtin_amdgcn_s_waitcnt(0);
-  if (stats) {
-    __syncthreads();
-    double v[8] = {s1[0], s1[1], s1[2], s1[3], s2[0], s2[1], s2[2], s2[3]};
-    if (block_slot_reduce<TCQ, 8, double>(v, reinterpret_cast<double*>(ring))) {
-      const long row = (long)srow * 2 * g.C;
-      const int cc = c0 + 4 * threadIdx.x;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        stats[row + cc + j] = v[j];
-        stats[row + g.C + cc + j] = v[4 + j];
-      }
-    }
-  }
-}
-
-// ----------------------------------------------------------------------------
-// K1 one-shot block tiles (ACCUNET_DW_BLK = R): a block loads its whole (R+2)-row halo
-// tile of 34 px x 8 quads at once (every load in flight together), activates it into
-// LDS, takes ONE barrier and computes its R output rows (rolling row accumulators, the
-// FMA order and 4-row statistics grouping of the strip kernel: bit-identical). No ring,
-// no per-chunk barriers; the blocks of a CU overlap one another's load and compute
-// phases instead (tools/k1lab tile_lds R16: +3-5 points of HBM over the strip structure
-// without arithmetic). R = 16: 78 KB of LDS, 2 blocks per CU; R = 8: 43.5 KB, 3.
-// ----------------------------------------------------------------------------
-template <int R, int AUX, typename T>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R >= 16 ? 2 : 3)))
-dw3x3_blk_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
-                     const float* __restrict__ bias, const float* __restrict__ sc,
-                     const float* __restrict__ sh, int act, int flip, T* __restrict__ z,
-                     double* __restrict__ stats, DwTGeom g) {
-  constexpr int TCQ = 8, TP = 32, IP = TP + 2, IRB = R + 2, CR = 4;
-  constexpr int QL = Raw16<T>::QL;
-  constexpr int NQ = IRB * IP * TCQ;         // quads of the halo tile
-  constexpr int NL = (NQ / QL + 255) / 256;  // 16-byte loads per thread
-  typedef typename Raw16<T>::type RawL;
-  __shared__ float4 tile[NQ];
-  const int tid = threadIdx.x;
-  const int q = tid % TCQ, p = tid / TCQ;
-  int t = dw_tile_id(g);
-  int cg = blockIdx.y;
-  if (g.cgf) {
-    cg = t % g.cgf;
-    t /= g.cgf;
-  }
-  const int srow = g.cgf ? t : (int)blockIdx.x;
-  const int c0 = cg * TCQ * 4;
-  const int c = c0 + 4 * q;
-  const int tw = t % g.tilesW;
-  t /= g.tilesW;
-  const int th = t % g.tilesH;
-  const int b = t / g.tilesH;
-  const int hbeg = th * DW_TR * g.rch, w0 = tw * TP;
-  const int hend = min(g.H, hbeg + DW_TR * g.rch);
-  const long img = (long)b * g.H * g.W * g.C;
-  const unsigned ibytes = (unsigned)(g.H * g.W * g.C * (int)sizeof(T));
-  const __amdgpu_buffer_rsrc_t rx = acc_rsrc(x + img, ibytes);
-  const __amdgpu_buffer_rsrc_t rz = acc_rsrc(z + img, ibytes);
-  const bool pro = sc != nullptr;
-  float4 ps[QL], pb[QL];
-  dw_stage_pro<TCQ, QL>(sc, sh, c0, ps, pb);
-  {
-    RawL v[NL];
-#pragma unroll
-    for (int k = 0; k < NL; ++k) {
-      const int i = (tid + 256 * k) * QL;
-      const int rp = i / TCQ, qq = i % TCQ;
-      const int pp = rp % IP, r = rp / IP;
-      const int hh = hbeg - 1 + r, ww = w0 - 1 + pp;
-      const bool in = i < NQ && hh >= 0 && hh < g.H && ww >= 0 && ww < g.W;
-      v[k] = buf16_ld<AUX>(rx, in ? (unsigned)(((hh * g.W + ww) * g.C + c0 + 4 * qq) * (int)sizeof(T))
-                                  : ACC_OOB, (const T*)nullptr);
-    }
-#pragma unroll
-    for (int k = 0; k < NL; ++k) {
-      const int i = (tid + 256 * k) * QL;
-      if (i < NQ) {
-        const int rp = i / TCQ;
-        const int pp = rp % IP, r = rp / IP;
-        const int hh = hbeg - 1 + r, ww = w0 - 1 + pp;
-        const bool in = hh >= 0 && hh < g.H && ww >= 0 && ww < g.W;
-#pragma unroll
-        for (int j = 0; j < QL; ++j) {
-          float4 a = r16q(v[k], j);
-          if (pro) {
-            a.x = apply_act(a.x * ps[j].x + pb[j].x, act);
-            a.y = apply_act(a.y * ps[j].y + pb[j].y, act);
-            a.z = apply_act(a.z * ps[j].z + pb[j].z, act);
-            a.w = apply_act(a.w * ps[j].w + pb[j].w, act);
-          }
-          tile[i + j] = make_float4(in ? a.x : 0.f, in ? a.y : 0.f, in ? a.z : 0.f, in ? a.w : 0.f);
-        }
-      }
-    }
-  }
-  float k[9][4], bi[4];
-  {
-    float wvv[36];
-#pragma unroll
-    for (int e = 0; e < 9; ++e) {
-      const float4 w4 = ld4(wt + c * 9 + 4 * e);
-      wvv[4 * e] = w4.x; wvv[4 * e + 1] = w4.y; wvv[4 * e + 2] = w4.z; wvv[4 * e + 3] = w4.w;
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int tp = 0; tp < 9; ++tp) k[tp][j] = wvv[j * 9 + (flip ? 8 - tp : tp)];
-    const float4 b4 = bias ? ld4(bias + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-    bi[0] = b4.x; bi[1] = b4.y; bi[2] = b4.z; bi[3] = b4.w;
-  }
-  __builtin_amdgcn_s_waitcnt(0);
-  __syncthreads();
-  const int w = w0 + p;
-  const bool wok = w < g.W;
-  float a0[4] = {0.f, 0.f, 0.f, 0.f}, a1[4] = {0.f, 0.f, 0.f, 0.f};
-  double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
-  float c1[4] = {0.f, 0.f, 0.f, 0.f}, c2[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int r = 0; r < IRB; ++r) {
-    float row[3][4];
-#pragma unroll
-    for (int dx = 0; dx < 3; ++dx) {
-      const float4 a = tile[(r * IP + p + dx) * TCQ + q];
-      row[dx][0] = a.x; row[dx][1] = a.y; row[dx][2] = a.z; row[dx][3] = a.w;
-    }
-    const int ho = hbeg + r - 2;  // output row input row r completes (r >= 2)
-    const bool on = wok && r >= 2 && ho < hend;
-    float o[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float acc = a0[e], mid = a1[e], nxt = bi[e];
-#pragma unroll
-      for (int dx = 0; dx < 3; ++dx) {
-        acc = fmaf(k[6 + dx][e], row[dx][e], acc);
-        mid = fmaf(k[3 + dx][e], row[dx][e], mid);
-        nxt = fmaf(k[dx][e], row[dx][e], nxt);
-      }
-      a0[e] = mid;
-      a1[e] = nxt;
-      acc = rnd<T>(acc);  // statistics of the stored value
-      o[e] = acc;
-      const float am = on ? acc : 0.f;
-      c1[e] += am;
-      c2[e] = fmaf(am, am, c2[e]);
-    }
-    if (r >= 2) {
-      const unsigned off = on ? (unsigned)(((ho * g.W + w) * g.C + c) * (int)sizeof(T)) : ACC_OOB;
-      bufq_st<2>(rz, off, make_float4(o[0], o[1], o[2], o[3]), (T*)nullptr);
-      if ((r - 2) % CR == CR - 1 || r == IRB - 1) {  // the strip kernel's 4-row groups
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          s1[e] += (double)c1[e];
-          s2[e] += (double)c2[e];
-          c1[e] = 0.f;
-          c2[e] = 0.f;
-        }
-      }
-    }
-  }
-  if (stats) {
-    __syncthreads();
-    double v[8] = {s1[0], s1[1], s1[2], s1[3], s2[0], s2[1], s2[2], s2[3]};
-    if (block_slot_reduce<TCQ, 8, double>(v, reinterpret_cast<double*>(tile))) {
-      const long row = (long)srow * 2 * g.C;
-      const int cc = c0 + 4 * threadIdx.x;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        stats[row + cc + e] = v[e];
-        stats[row + g.C + cc + e] = v[4 + e];
-      }
-    }
-  }
-}
-
 template <int TCQ, typename T>
 __global__ void __launch_bounds__(256)
 dw3x3_tile_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dz,
@@ -1882,33 +1230,6 @@ static int dw_cgfast() {
   return v;
 }
 
-// K1 staging (ACCUNET_DW_DMA, tuning knob / A/B): bit 0 = LDS-DMA ring for the fp32
-// 32-channel tiles (dw3x3_dma_fwd_kernel), bit 1 = LDS-DMA ring for bf16 tiles
-// (dw3x3_dma_bf16_fwd_kernel), both without a BN-backward epilogue; 0 = the
-// register-staged strip for every shape
-static int dw_dma() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("ACCUNET_DW_DMA");
-    v = e ? atoi(e) : 0;
-  }
-  return v;
-}
-
-// K1 one-shot block tiles (dw3x3_blk_fwd_kernel): 0 = off, 8 or 16 = output rows per
-// block for the 32-channel tiles (ACCUNET_DW_BLK, tuning knob / A/B). The strip length of
-// every forward-type launch of those shapes (the BN-backward data gradient too, so the
-// statistics rows agree) is then R.
-static int dw_blk() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("ACCUNET_DW_BLK");
-    v = e ? atoi(e) : 0;
-    if (v != 8 && v != 16) v = 0;
-  }
-  return v;
-}
-
 static int dw_rch_max() {
   static int v = -1;
   if (v < 0) {
@@ -1930,8 +1251,6 @@ static DwTGeom dw_tgeom(int B, int H, int W, int C, int tcq, dim3* grid, int rch
   static const char* force = getenv("ACCUNET_DW_RCH_FORCE");  // tuning knob (tools/kbench)
   if (force && rch_max > 1) {
     rch = atoi(force) > 0 ? atoi(force) : 1;
-  } else if (rch_max > 1 && tcq == 8 && dw_blk()) {
-    rch = dw_blk() / DW_TR;  // one-shot block tiles
   } else {
       // the longest strips (powers of two) that still give >= 4 rounds of 3 resident
       // blocks per CU (3072 blocks): 16x256x256x96 fp32 rch 1/2/4/8/16 = 180/159/154/155/
@@ -1968,15 +1287,12 @@ static DwGeom dw_geom(int B, int H, int W, int C, int V, dim3* grid) {
 }
 
 // which forward kernel accunet_dw3x3_fwd runs for this shape and storage dtype without
-// a BN-backward epilogue: 3 = LDS-DMA ring, 2 = span, 1 = tile, 0 = register window
-// (profiling names / the bench probe)
+// a BN-backward epilogue: 2 = span, 1 = tile (strip), 0 = register window (profiling
+// names / the bench probe); it follows the same two choices the launch below makes
 extern "C" int accunet_dw3x3_variant(int B, int H, int W, int C, int dt) {
   (void)B;
   if (dw_span_nt(H, W, C)) return 2;
   const int tcq = dw_tile_tcq(H, W, C, dt);
-  if (tcq == 8 && dw_blk()) return 5;
-  if ((tcq == 8 && dt == ACC_F32 && (dw_dma() & 1)) || (tcq && dt == ACC_BF16 && (dw_dma() & 2)))
-    return 3;
   return tcq ? 1 : 0;
 }
 
@@ -2043,53 +1359,6 @@ extern "C" int accunet_dw3x3_fwd(const void* x, const float* wt, const float* bi
     if (dw_cgfast() && grid.y > 1) {
       tg.cgf = (int)grid.y;
       grid = dim3(grid.x * grid.y, 1);
-    }
-    if (tcq == 8 && !bz && dw_blk() && tg.rch * DW_TR == dw_blk()) {
-      auto lb = [&](auto tag, auto rc, auto auxc) {
-        using T = decltype(tag);
-        hipLaunchKernelGGL((dw3x3_blk_fwd_kernel<decltype(rc)::value, decltype(auxc)::value, T>),
-                           grid, dim3(256), 0, s, (const T*)x, wt, bias, sc, sh, act, flip, (T*)z,
-                           stats, tg);
-      };
-      using R16 = std::integral_constant<int, 16>;
-      using R8 = std::integral_constant<int, 8>;
-      using A2 = std::integral_constant<int, 2>;
-      using A0 = std::integral_constant<int, 0>;
-      if (with_dt(dt, [&](auto tag) {
-            if (dw_blk() == 16) {
-              if (tg.ntl) lb(tag, R16{}, A2{}); else lb(tag, R16{}, A0{});
-            } else {
-              if (tg.ntl) lb(tag, R8{}, A2{}); else lb(tag, R8{}, A0{});
-            }
-          }))
-        return ACC_EBADARG;
-      return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
-    }
-    if (dt == ACC_BF16 && !bz && (dw_dma() & 2)) {
-      auto lb = [&](auto tcqc, auto ntc) {
-        hipLaunchKernelGGL((dw3x3_dma_bf16_fwd_kernel<decltype(tcqc)::value, decltype(ntc)::value>),
-                           grid, dim3(256), 0, s, (const bf16_t*)x, wt, bias, sc, sh, act, flip,
-                           (bf16_t*)z, stats, tg);
-      };
-      using I16 = std::integral_constant<int, 16>;
-      using I8 = std::integral_constant<int, 8>;
-      using NTT = std::integral_constant<bool, true>;
-      using NTF = std::integral_constant<bool, false>;
-      if (tcq == 16) {
-        if (tg.ntl) lb(I16{}, NTT{}); else lb(I16{}, NTF{});
-      } else {
-        if (tg.ntl) lb(I8{}, NTT{}); else lb(I8{}, NTF{});
-      }
-      return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
-    }
-    if (dt == ACC_F32 && tcq == 8 && !bz && (dw_dma() & 1)) {
-      if (tg.ntl)
-        hipLaunchKernelGGL((dw3x3_dma_fwd_kernel<true>), grid, dim3(256), 0, s, (const float*)x, wt,
-                           bias, sc, sh, act, flip, (float*)z, stats, tg);
-      else
-        hipLaunchKernelGGL((dw3x3_dma_fwd_kernel<false>), grid, dim3(256), 0, s, (const float*)x,
-                           wt, bias, sc, sh, act, flip, (float*)z, stats, tg);
-      return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
     }
     // both fixed-function choices (channel-group width, nt loads) are template arguments
     auto launch = [&](auto tag, auto tcqc, auto bnbc, auto auxc) {

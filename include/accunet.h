@@ -125,6 +125,11 @@ int accunet_stream_ticket_unregister(void* stream);
  * library was built. The Python binding refuses a library whose hash differs from
  * the header it binds against. */
 long long accunet_abi_hash(void);
+/* Diagnostic: how many launches of the ResPath halo-tile 3x3 kernels (forward / data
+ * gradient, and weight gradient) accunet_gemm has made in this process since it was
+ * loaded (host-side counts; a launch captured into a graph counts once). Lets a test
+ * prove which implementation ran. No reference counterpart. */
+long long accunet_conv3x3_halo_launches(int wgrad);
 int accunet_bn_finalize(const double* part, int R, int C, double count, const float* gamma,
                         const float* beta, float* rmean, float* rvar, long long* nbt,
                         float momentum, float eps, int training, float* st, double* ws,
@@ -165,11 +170,9 @@ int accunet_reduce_stats(const double* part, int R, int C, double* out2C, double
  * dtype dt (bf16 runs 64-channel tiles where C % 64 == 0). */
 int accunet_dw3x3_rows(int B, int H, int W, int C, int dt);
 /* Which forward kernel runs for the shape and storage dtype dt (without bz): 1 = LDS
- * tile kernel (C % 32 == 0), 0 = register-window kernel; 3 = the LDS-DMA ring kernel
- * (ACCUNET_DW_DMA), 5 = one-shot block tiles (ACCUNET_DW_BLK), both tuning knobs for
- * 32-channel tiles, off by default; 2 = whole-pixel span kernel, only with the
- * tuning knob ACCUNET_DW_SPAN bit 2 set (off by default) and then for C % 8 == 0,
- * C/4 <= 64. */
+ * strip kernel (C % 32 == 0), 0 = register-window kernel; 2 = whole-pixel span kernel,
+ * only with the tuning knob ACCUNET_DW_SPAN bit 2 set (off by default) and then for
+ * C % 8 == 0, C/4 <= 64. */
 int accunet_dw3x3_variant(int B, int H, int W, int C, int dt);
 int accunet_dw3x3_fwd(const void* x, const float* wt, const float* bias, const float* sc,
                       const float* sh, int act, int flip, void* z, double* stats, int B, int H,

@@ -413,9 +413,10 @@ def convT(x, sd, p):
     return q(F.conv_transpose2d(q(x), qw(sd[p + ".weight"]), sd[p + ".bias"], stride=2))
 
 
-def forward(sd, x, variant="canonical", training=True, n_classes=1):
+def forward(sd, x, variant="canonical", training=True, n_classes=1, return_logits=False):
     """ACC_UNet.forward, ACC_UNet/ACC_UNet.py:601-659 (script variant returns logits,
-    Experiments/nets/ACC_UNet.py:654-655)."""
+    Experiments/nets/ACC_UNet.py:654-655). return_logits=True returns the head's pre-sigmoid
+    output for every variant (a diagnostic the reference does not expose)."""
     t = training
     x = q(x)
     x2 = hanc_block(hanc_block(x, sd, "cnv11", 3, t), sd, "cnv12", 3, t)
@@ -443,7 +444,7 @@ def forward(sd, x, variant="canonical", training=True, n_classes=1):
         logits = F.conv2d(x10, sd["out.weight"], sd["out.bias"])
     else:
         logits = conv(x10, sd, "out")
-    if variant != "script" and n_classes == 1:
+    if variant != "script" and n_classes == 1 and not return_logits:
         return torch.sigmoid(logits)
     return logits
 

@@ -9,7 +9,10 @@ each all-reduced (AVG) by RCCL on the side stream behind its in-graph event
 (_GraphBuckets.reduce, nccl branch), then the fused Adam reads the flat buffer. At
 world 1 RCCL's AVG is an identity, so after 3 steps the parameters must equal, bit
 for bit, those of the plain world-1 graph step (no process group, no buckets) on the
-same data -- in fp32 and in bf16 storage.
+same data -- in fp32 and in bf16 storage. With the bf16 wire (comm_dtype="bf16", the
+bench default for --dtype bf16) every bucket travels as bf16 and is widened back on the
+side stream after its reduce: at world 1 the gradient Adam reads must be the graph's
+fp32 gradient rounded to bf16 and widened, bit for bit, for every parameter.
 """
 import os
 import sys
@@ -36,6 +39,30 @@ def run(sd, data, dev, pg, prec):
     m = m.to(dev).train()
     kw = dict(process_group=pg, bucket_mb=0.25) if pg is not None else {}
     step = TrainStep(m, lr=1e-3, graph=True, precision=prec, **kw)
+    return _steps(step, m, data)
+
+
+def wire16(sd, data, dev, pg, prec):
+    """graph DP step over RCCL with bf16 gradient buckets: after each step the fp32
+    gradients the optimizer read == bf16(graph gradient) widened, every parameter"""
+    m = ACC_UNet(3, 1, n_filts=8)
+    m.load_state_dict(sd)
+    m = m.to(dev).train()
+    step = TrainStep(m, lr=1e-3, graph=True, precision=prec, process_group=pg, bucket_mb=0.25,
+                     comm_dtype="bf16")
+    nb = 0
+    for x, y in data:
+        step(x, y)
+        torch.cuda.synchronize()
+        nb = len(step._buckets.buckets)
+        for p, g in zip(step.params, step._graph_grads):
+            assert p.grad.data_ptr() != g.data_ptr()
+            want = g.to(torch.bfloat16).float()
+            assert torch.equal(p.grad, want), float((p.grad - want).abs().max())
+    return nb
+
+
+def _steps(step, m, data):
     losses = [float(step(x, y)) for x, y in data]
     torch.cuda.synchronize()
     nb = len(step._buckets.buckets) if step._buckets is not None else 0
@@ -61,6 +88,9 @@ def main():
         assert nb >= 3 and nb1 == 0, (nb, nb1)
         assert torch.equal(p_dp, p_1), d
         assert l_dp == l_1
+        nb16 = wire16(sd, data, dev, dist.group.WORLD, prec)
+        print(f"{prec}: bf16-wire buckets {nb16}: reduced gradient == bf16(gradient)", flush=True)
+        assert nb16 >= 3
     dist.destroy_process_group()
     print("RCCL_OK", flush=True)
 

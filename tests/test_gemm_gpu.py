@@ -229,6 +229,9 @@ def test_conv3x3_halo_matches_engine_bitwise(tmp_path):
         subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "conv3x3_worker.py"),
                         str(path)], env=env, check=True, timeout=240)
         outs[v] = torch.load(path, weights_only=True)
+    # the knob-on run really took the halo kernels (every launch), the knob-off run never
+    assert int(outs["1"].pop("halo_launches")) == 8
+    assert int(outs["0"].pop("halo_launches")) == 0
     for k in outs["1"]:
         assert torch.equal(outs["1"][k], outs["0"][k]), k
 
@@ -255,7 +258,10 @@ def test_conv3x3_halo_wgrad_channel_blocks(B, H, W, Ci, Co):
                   bmode=_lib.BMODE_NN_SHIFT3, c=dw, ldc=9 * Ci, H=H, W=W, cin=Ci,
                   allow_split=True)
         return dw
+    lib = _lib.load()
+    n0 = lib.accunet_conv3x3_halo_launches(1)
     dw = wgrad()
+    assert lib.accunet_conv3x3_halo_launches(1) == n0 + 1  # the halo weight-gradient kernel ran
     assert rel(dw, w.grad.permute(0, 2, 3, 1).reshape(Co, 9 * Ci)) < 1e-5
     assert torch.equal(dw, wgrad())
 

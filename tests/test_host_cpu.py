@@ -298,9 +298,8 @@ def test_abi_host_side_contract_without_a_device():
     # 16x256x256x96: the tile kernel, 8 tiles of 32 pixels per row, 32-row strips (the
     # longest with >= 3072 blocks) -> 16 * 8 * 8 = 1024 statistics rows; cnv11's 9
     # channels the register kernel
-    # fp32: the LDS-DMA ring (3) or, with ACCUNET_DW_DMA=0, the register strip (1)
-    assert lib.accunet_dw3x3_variant(16, 256, 256, 96, 0) in (1, 3)
-    assert lib.accunet_dw3x3_variant(16, 256, 256, 96, 1) == 1  # bf16: the register strip
+    assert lib.accunet_dw3x3_variant(16, 256, 256, 96, 0) == 1  # the register-staged strip
+    assert lib.accunet_dw3x3_variant(16, 256, 256, 96, 1) == 1
     assert lib.accunet_dw3x3_rows(16, 256, 256, 96, 0) == 1024
     # bf16 (dt 1) runs 64-channel tiles where C % 64 == 0: 16-pixel tiles, twice the rows
     assert lib.accunet_dw3x3_rows(16, 128, 128, 192, 0) * 2 == lib.accunet_dw3x3_rows(16, 128, 128, 192, 1)

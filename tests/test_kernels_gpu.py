@@ -106,8 +106,7 @@ def test_dw3x3_bf16_fwd_vs_fp64(B, H, W, C, pro):
     those of the stored values. Against an fp64 restatement of the same rounding: z
     within one bf16 rounding (2^-8 relative, plus the fp32 arithmetic), statistics of
     the stored z within fp32 accumulation noise. Covers 32- and 64-channel tiles
-    (C % 64 == 0) and ragged images, on whichever kernel the library selects (the
-    LDS-DMA ring with ACCUNET_DW_DMA bit 1, else the register-staged strip)."""
+    (C % 64 == 0) and ragged images (the register-staged strip kernel)."""
     kern = _kern()
     g = torch.Generator().manual_seed(B * 7 + H * 3 + C)
     x = torch.randn(B, H, W, C, generator=g).to(torch.bfloat16)

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-4 profile pass: parity tests, the bench lines (fp32 headline, bf16, UNeXt,
+# Round profile pass (the final-source pass of a round): parity tests, the bench lines (fp32 headline, bf16, UNeXt,
 # ACC_UNet_W at 512^2), a rocprofv3 kernel trace (+ stats) of the fp32 bench and of the
 # bf16 bench, the FETCH_SIZE / WRITE_SIZE passes (separate runs) that give K1's and K3's
 # HBM traffic, and tools/kbench. Every GPU step has its own time limit; the first

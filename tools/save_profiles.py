@@ -36,8 +36,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "gpurun_out")
 PROF = os.path.join(ROOT, "profiles")
-# the fp32 K1 kernel of 16x256x256x96: the LDS-DMA ring (accunet_dw3x3_variant 3) or,
-# with ACCUNET_DW_DMA=0, the register-staged strip
+# the fp32 K1 kernel of 16x256x256x96: the register-staged LDS strip
 K1 = os.environ.get("K1_KERNEL", "dw3x3_tile_fwd_kernel<8, false,")
 K1_GRID = 3072 * 256  # 1024 tiles (32-row strips) x 3 channel groups, 256 threads (16x256x256x96)
 K3 = ["se_reduce_kernel<4, float, true>", "se_mid_sample_kernel", "se_mid_bn_kernel",
