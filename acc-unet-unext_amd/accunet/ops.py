@@ -394,22 +394,25 @@ class DeferredRelayouts:
 
     CAP = 128
 
-    def __init__(self, device):
+    def __init__(self, device, cap=None):
+        self.cap = cap or self.CAP
         self.items, self.keep = [], []
-        self.table = torch.zeros(self.CAP * ctypes.sizeof(_lib.AccRelayout), dtype=torch.uint8,
+        self.table = torch.zeros(self.cap * ctypes.sizeof(_lib.AccRelayout), dtype=torch.uint8,
                                  device=device)
         self.done = 0        # items already captured by a flush
         self.segments = []   # (byte offset in the table, item bytes) per flush
         self.launches = 0
 
     def full(self):
-        return len(self.items) >= self.CAP
+        return len(self.items) >= self.cap
 
     def _add(self, src, dst, kind, total, **kw):
         it = _lib.AccRelayout()
         it.inp, it.out = src.data_ptr(), dst.data_ptr()
         it.total, it.kind = int(total), kind
-        if kind == 0:
+        if kind in (3, 4):
+            pass
+        elif kind == 0:
             for a in range(4):
                 it.d[a], it.s[a] = kw["d"][a], kw["s"][a]
                 it.flip[a] = 0
@@ -429,6 +432,13 @@ class DeferredRelayouts:
 
     def group_inverse(self, src, dst, N, C, J, order):
         self._add(src, dst, 2, N * J * C, N=N, C=C, J=J, order=order)
+
+    def copy(self, src, dst):
+        """flat copy of a contiguous fp32 tensor into dst (fp32, or bf16 rounded to
+        nearest even): kinds 3 / 4, the data-parallel bucket packing"""
+        if src.dtype != torch.float32 or dst.numel() != src.numel():
+            raise ValueError("copy: fp32 source of dst's size")
+        self._add(src, dst, 4 if dst.dtype == torch.bfloat16 else 3, src.numel())
 
     def flush(self):
         """one launch for the items added since the last flush (none: no launch)"""

@@ -90,6 +90,10 @@ class _GraphBuckets:
         self.bucket_of = {i: k for k, b in enumerate(self.buckets) for i in b}
         self.events = [kern.GraphEvent() for _ in self.buckets]
         self._handles = []
+        # every sealed bucket is packed by ONE batched copy launch (fp32, or rounded to
+        # bf16 for the bf16 wire) instead of _foreach_copy_ (a mixed-dtype foreach copy
+        # falls back to one launch per tensor: ~900 graph nodes per step)
+        self.packer = ops.DeferredRelayouts(device, cap=len(params))
 
     # ------------------------------------------------------------ capture side
     def _seal(self, k):
@@ -99,9 +103,11 @@ class _GraphBuckets:
         self._sealed[k] = True
         if ops._DEFER is not None:  # pending inverse weight relayouts: final values first
             ops._DEFER.flush()
-        live = [i for i in self.buckets[k] if self.params[i].grad is not None]
-        if live:
-            torch._foreach_copy_([self.wviews[i] for i in live], [self.params[i].grad for i in live])
+        for i in self.buckets[k]:
+            g = self.params[i].grad
+            if g is not None:
+                self.packer.copy(g.contiguous(), self.wviews[i])
+        self.packer.flush()
         kern.GraphEvent.mark(k)
 
     def _hook(self, i):
@@ -290,6 +296,7 @@ class TrainStep:
                                    f"destination(s) are not parameter gradients")
             self._defer.upload()  # the item table the captured launch reads
         if self._buckets is not None:
+            self._buckets.packer.upload()  # the bucket-packing item tables
             # an event-record node behind every bucket's marker, then instantiate
             n = kern.GraphEvent.attach(g.raw_cuda_graph(), self._buckets.events)
             if n != len(self._buckets.buckets):

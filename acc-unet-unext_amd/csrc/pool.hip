@@ -671,7 +671,9 @@ extern "C" int accunet_group_relayout(const float* in, float* out, int N, int C,
 // owns blocks [blk0_i, blk0_{i+1}); kind 0 = accunet_permute4's gather, kind 1 =
 // accunet_group_relayout's forward, kind 2 its inverse (the backward's weight
 // gradients, ops.DeferredRelayouts); the same index arithmetic, so the copies are the
-// ones the per-layer launches make.
+// ones the per-layer launches make. kind 3 / 4 = flat copies into a gradient bucket
+// (fp32 / rounded to bf16 like torch's .to(bfloat16): the graph-mode data-parallel
+// step packs each sealed bucket in one launch, accunet/train.py _GraphBuckets).
 // ---------------------------------------------------------------------------
 #define RL_EPT 4
 __global__ void __launch_bounds__(256)
@@ -689,6 +691,11 @@ relayout_batch_kernel(const AccRelayout* __restrict__ items, int n) {
   for (int e = 0; e < RL_EPT; ++e) {
     const long i = base + e;
     if (i >= it.total) break;
+    if (it.kind >= 3) {  // flat copy (data-parallel bucket packing): fp32, or rounded to bf16
+      if (it.kind == 3) it.out[i] = it.in[i];
+      else reinterpret_cast<bf16_t*>(it.out)[i] = f2bf(it.in[i]);
+      continue;
+    }
     long src;
     if (it.kind == 0) {
       long r = i;

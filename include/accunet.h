@@ -190,8 +190,9 @@ int accunet_dw3x3_wgrad(const void* x, const void* dz, const float* sc, const fl
  * [blk0_i, blk0_{i+1}) with accunet_relayout_blocks(total_i) blocks; nblocks = their
  * sum. kind 0 = the gather of accunet_permute4 (d, s, flip), kind 1 = the forward of
  * accunet_group_relayout (N, C, J, order), kind 2 = its inverse (the backward's weight
- * gradients back into the reference layout, ops.DeferredRelayouts; total = N*J*C).
- * fp32 weights only.
+ * gradients back into the reference layout, ops.DeferredRelayouts; total = N*J*C),
+ * kind 3 = flat copy in -> out (fp32), kind 4 = flat copy with `out` a bf16 array
+ * (round to nearest even): the data-parallel gradient-bucket packing. `in` is fp32.
  * ------------------------------------------------------------------------- */
 typedef struct AccRelayout {
   const float* in;

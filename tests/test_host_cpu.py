@@ -362,6 +362,11 @@ def _emulate_relayout(it, src):
     """numpy restatement of relayout_batch_kernel's index arithmetic for one item"""
     out = np.empty(it.total, dtype=np.float32)
     i = np.arange(it.total, dtype=np.int64)
+    if it.kind in (3, 4):  # flat copy (bucket packing), kind 4 rounded to bf16
+        out[:] = src
+        if it.kind == 4:
+            out[:] = torch.from_numpy(out).to(torch.bfloat16).float().numpy()
+        return out
     if it.kind == 0:
         r, off = i.copy(), np.zeros_like(i)
         for a in (3, 2, 1, 0):
@@ -382,6 +387,27 @@ def _emulate_relayout(it, src):
     else:
         out[:] = src[off]
     return out
+
+
+def test_bucket_packing_items():
+    """The graph-mode data-parallel step packs each sealed gradient bucket with one
+    batched launch (ops.DeferredRelayouts.copy, kinds 3 / 4): flat copies into the
+    fp32 or bf16 wire; several flushes use consecutive segments of one item table."""
+    from accunet import ops
+    torch.manual_seed(4)
+    d = ops.DeferredRelayouts("cpu", cap=4)
+    src = [torch.randn(5, 7), torch.randn(33)]
+    dst = [torch.empty(35), torch.empty(33, dtype=torch.bfloat16)]
+    d.copy(src[0], dst[0])
+    d.copy(src[1], dst[1])
+    assert [it.kind for it in d.items] == [3, 4]
+    for it, s_, d_ in zip(d.items, src, dst):
+        assert it.inp == s_.data_ptr() and it.out == d_.data_ptr() and it.total == s_.numel()
+        got = _emulate_relayout(it, s_.reshape(-1).numpy())
+        want = s_.reshape(-1).to(d_.dtype).float().numpy()
+        np.testing.assert_array_equal(got, want)
+    with pytest.raises(ValueError):
+        d.copy(torch.randn(3, dtype=torch.float64), torch.empty(3))
 
 
 def test_weight_prep_items_reproduce_the_per_op_layouts():

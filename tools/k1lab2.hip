@@ -210,6 +210,173 @@ colx(const float* __restrict__ x, const float* __restrict__ wt, const float* __r
   }
 }
 
+// os<R, DMA>: one-shot tiles. A block owns R output rows x 32 pixels x 8 quads and
+// is gone after one tile (no walk), so the resident blocks of a CU cover neighbouring
+// tiles and every block's loads are issued at once (the lab's fastest shapes).
+// DMA = false: each thread loads its own pixel-quad column (R + 2 rows) into registers
+// and lanes < 16 (R + 2) load the two halo pixels; the activated values go to an LDS
+// exchange tile, of which a thread reads back only its left / right neighbours.
+// DMA = true: the whole (R + 2) x 34 x 8 input tile goes HBM -> LDS by
+// global_load_lds_dwordx4 (zero page outside the image), every thread applies the
+// prologue to the three quads of each row it reads (in-image only).
+// Weights / bias / prologue vectors are issued before the tile loads.
+__device__ __attribute__((aligned(16))) float g_zero4[4] = {0.f, 0.f, 0.f, 0.f};
+ACC_DEV void dma16(const float* src, float4* lds_dst) {
+  const unsigned dst = __builtin_amdgcn_readfirstlane(
+      (unsigned)(size_t)(__attribute__((address_space(3))) float4*)lds_dst);
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(dst)
+               : "memory");
+}
+
+template <int R, bool DMA, int WPE, int PH = 1>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
+os(const float* __restrict__ x, const float* __restrict__ wt, const float* __restrict__ bias,
+   const float* __restrict__ sc, const float* __restrict__ sh, float* __restrict__ z,
+   double* __restrict__ stats, int remap) {
+  constexpr int IP = TP + 2, IR = R + 2;
+  static_assert(IR % PH == 0 && (!DMA || PH == 1), "phases split the input rows");
+  constexpr int XR = IR / PH;  // exchange rows per phase (PH = 2: half the LDS)
+  __shared__ float4 xb[XR][IP][TCQ];
+  const int tid = threadIdx.x;
+  const int q = tid % TCQ, p = tid / TCQ;
+  int bid = blockIdx.x;
+  if (remap) {
+    const int per = gridDim.x >> 3;
+    bid = (bid & 7) * per + (bid >> 3);
+  }
+  const int cg = bid % NCG;
+  int t = bid / NCG;
+  const int srow = t;
+  const int tw = t % (W / TP);
+  t /= (W / TP);
+  const int th = t % (H / R);
+  const int b = t / (H / R);
+  const int c0 = cg * TCQ * 4, c = c0 + 4 * q;
+  const int w0 = tw * TP, w = w0 + p, h0 = th * R;
+  const long img = (long)b * H * W * C;
+  const auto rx = acc_rsrc(x + img, IMG), rz = acc_rsrc(z + img, IMG);
+  float k[9][4], bi[4];
+  float4 ps, pb;
+  {
+    float wv[36];
+#pragma unroll
+    for (int e = 0; e < 9; ++e) {
+      const float4 w4 = ld4(wt + c * 9 + 4 * e);
+      wv[4 * e] = w4.x; wv[4 * e + 1] = w4.y; wv[4 * e + 2] = w4.z; wv[4 * e + 3] = w4.w;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int tp = 0; tp < 9; ++tp) k[tp][j] = wv[j * 9 + tp];
+    const float4 b4 = ld4(bias + c);
+    bi[0] = b4.x; bi[1] = b4.y; bi[2] = b4.z; bi[3] = b4.w;
+    ps = ld4(sc + c); pb = ld4(sh + c);
+  }
+  float4 own[IR], hv[PH];
+  // halo lanes: per phase 2 pixels x 8 quads x XR rows, lane tid < 16 XR: row tid / 16
+  const bool hl = tid < 16 * XR;
+  const int hr = tid >> 4, hs = (tid >> 3) & 1;
+  const int hw = hs ? w0 + TP : w0 - 1;
+  if (DMA) {
+    constexpr int NE = IR * IP * TCQ, NI = (NE + 63) / 64;
+    const int lane = tid & 63, wave = tid >> 6;
+    for (int u = wave; u < NI; u += 4) {
+      const int e = u * 64 + lane;
+      const int r = e / (IP * TCQ), pp = (e / TCQ) % IP, qq = e % TCQ;
+      const int hh = h0 - 1 + r, ww = w0 - 1 + pp;
+      const bool ok = e < NE && hh >= 0 && hh < H && ww >= 0 && ww < W;
+      const float* src = ok ? x + img + ((long)(hh * W + ww) * C + c0 + 4 * qq) : g_zero4;
+      if (e < NE) dma16(src, &xb[0][0][0] + u * 64);
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+  } else {
+#pragma unroll
+    for (int r = 0; r < IR; ++r) {
+      const int i = h0 - 1 + r;
+      const bool rin = i >= 0 && i < H;
+      own[r] = bufq_ld<2>(rx, rin ? (unsigned)(((i * W + w) * C + c) * 4) : ACC_OOB, (const float*)nullptr);
+    }
+#pragma unroll
+    for (int ph = 0; ph < PH; ++ph) {
+      const int hrow = h0 - 1 + ph * XR + hr;
+      const bool hin = hl && hw >= 0 && hw < W && hrow >= 0 && hrow < H;
+      hv[ph] = bufq_ld<2>(rx, hin ? (unsigned)(((hrow * W + hw) * C + c) * 4) : ACC_OOB,
+                          (const float*)nullptr);
+    }
+  }
+  float a0[4] = {0.f, 0.f, 0.f, 0.f}, a1[4] = {0.f, 0.f, 0.f, 0.f};
+  float c1[4] = {0.f, 0.f, 0.f, 0.f}, c2[4] = {0.f, 0.f, 0.f, 0.f};
+  const bool lin = w - 1 >= 0, rinw = w + 1 < W;
+#pragma unroll
+  for (int ph = 0; ph < PH; ++ph) {
+    if (!DMA) {
+      if (ph > 0) __syncthreads();  // every thread is done with the previous phase's rows
+#pragma unroll
+      for (int rr = 0; rr < XR; ++rr) {
+        const int r = ph * XR + rr, i = h0 - 1 + r;
+        own[r] = (i >= 0 && i < H) ? act4(own[r], ps, pb) : make_float4(0.f, 0.f, 0.f, 0.f);
+        xb[rr][p + 1][q] = own[r];
+      }
+      if (hl) {
+        const int hrow = h0 - 1 + ph * XR + hr;
+        const bool hin = hw >= 0 && hw < W && hrow >= 0 && hrow < H;
+        xb[hr][hs ? IP - 1 : 0][q] = hin ? act4(hv[ph], ps, pb) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int rr = 0; rr < XR; ++rr) {
+      const int r = ph * XR + rr, i = h0 - 1 + r;
+      float4 L = xb[rr][p][q], Cc, Rr = xb[rr][p + 2][q];
+      if (DMA) {
+        const bool rin = i >= 0 && i < H;
+        Cc = xb[rr][p + 1][q];
+        Cc = rin ? act4(Cc, ps, pb) : make_float4(0.f, 0.f, 0.f, 0.f);
+        L = (rin && lin) ? act4(L, ps, pb) : make_float4(0.f, 0.f, 0.f, 0.f);
+        Rr = (rin && rinw) ? act4(Rr, ps, pb) : make_float4(0.f, 0.f, 0.f, 0.f);
+      } else {
+        Cc = own[r];
+      }
+      const float vL[4] = {L.x, L.y, L.z, L.w};
+      const float vC[4] = {Cc.x, Cc.y, Cc.z, Cc.w};
+      const float vR[4] = {Rr.x, Rr.y, Rr.z, Rr.w};
+      float o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float t0 = a0[j], t1 = a1[j], t2 = bi[j];
+        t0 = fmaf(k[6][j], vL[j], t0); t0 = fmaf(k[7][j], vC[j], t0); t0 = fmaf(k[8][j], vR[j], t0);
+        t1 = fmaf(k[3][j], vL[j], t1); t1 = fmaf(k[4][j], vC[j], t1); t1 = fmaf(k[5][j], vR[j], t1);
+        t2 = fmaf(k[0][j], vL[j], t2); t2 = fmaf(k[1][j], vC[j], t2); t2 = fmaf(k[2][j], vR[j], t2);
+        o[j] = t0;
+        a0[j] = t1;
+        a1[j] = t2;
+        if (r >= 2) {
+          c1[j] += t0;
+          c2[j] = fmaf(t0, t0, c2[j]);
+        }
+      }
+      if (r >= 2)
+        bufq_st<2>(rz, (unsigned)((((i - 1) * W + w) * C + c) * 4), make_float4(o[0], o[1], o[2], o[3]),
+                   (float*)nullptr);
+    }
+  }
+  __syncthreads();
+  double v[8] = {c1[0], c1[1], c1[2], c1[3], c2[0], c2[1], c2[2], c2[3]};
+  if (block_slot_reduce<TCQ, 8, double>(v, reinterpret_cast<double*>(&xb[0][0][0]))) {
+    const long row = (long)srow * 2 * C;
+    const int cc = c0 + 4 * threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      stats[row + cc + j] = v[j];
+      stats[row + C + cc + j] = v[4 + j];
+    }
+  }
+}
+
 __global__ void fill(float* p, long n, unsigned salt, float lo, float span) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
     p[i] = lo + span * (float)(((i + salt) * 2654435761u) % 10007) / 10007.f;
@@ -252,7 +419,8 @@ int main(int argc, char** argv) {
   hipLaunchKernelGGL(fill, dim3(1), dim3(256), 0, 0, sh, (long)C, 9u, -0.2f, 0.4f);
   const int rows = accunet_dw3x3_rows(B, H, W, C, ACC_F32);
   double *st, *str;
-  CK(hipMalloc(&st, (size_t)std::max(rows, NT) * 2 * C * 8));
+  const int st_cap = std::max(rows, 8 * NT);  // rows of the largest grid (R = 4 tiles)
+  CK(hipMalloc(&st, (size_t)st_cap * 2 * C * 8));
   CK(hipMalloc(&str, (size_t)rows * 2 * C * 8));
   CK(hipDeviceSynchronize());
   auto totals = [&](const double* d, int R) {
@@ -280,6 +448,7 @@ int main(int argc, char** argv) {
   const std::vector<double> sref = totals(str, rows);
   std::vector<unsigned> hz(n), hr(n);
   CK(hipMemcpy(hr.data(), zr, n * 4, hipMemcpyDeviceToHost));
+  int stat_rows = NT;
   auto check = [&](const char* name, bool arith) {
     CK(hipDeviceSynchronize());
     CK(hipMemcpy(hz.data(), z, n * 4, hipMemcpyDeviceToHost));
@@ -288,7 +457,7 @@ int main(int argc, char** argv) {
       for (size_t i = 0; i < n; ++i) bad += hz[i] != hr[i];
     double es = 0.0;
     if (arith) {
-      const std::vector<double> s = totals(st, NT);
+      const std::vector<double> s = totals(st, stat_rows);
       for (int e = 0; e < 2 * C; ++e) es = std::max(es, fabs(s[e] - sref[e]) / (fabs(sref[e]) + 1e-30));
     }
     printf("  %-42s z %s (%ld differ), stats max rel %.2e\n", name,
@@ -305,12 +474,27 @@ int main(int argc, char** argv) {
     CK(hipGetLastError());                                                                    \
     check(NAME, AR);                                                                          \
   }
-  RUN(4, true, true, "colx CR4 DB");
+#define RUNOS(R, DMA, WPE, REMAP, NAME) RUNOSP(R, DMA, WPE, REMAP, 1, NAME)
+#define RUNOSP(R, DMA, WPE, REMAP, PH, NAME)                                                   \
+  {                                                                                            \
+    stat_rows = B * (H / R) * (W / TP);                                                        \
+    if (stat_rows > st_cap) { fprintf(stderr, "stats rows %d > %d\n", stat_rows, st_cap); exit(3); } \
+    auto f = [&] { hipLaunchKernelGGL((os<R, DMA, WPE, PH>), dim3(stat_rows * NCG), dim3(256), 0, 0, x, wt, \
+                                      bi, sc, sh, z, st, REMAP); };                            \
+    CK(hipMemset(z, 0, n * 4));                                                                \
+    report(NAME, timeit(f, iters));                                                            \
+    CK(hipGetLastError());                                                                     \
+    check(NAME, true);                                                                         \
+    stat_rows = NT;                                                                            \
+  }
   RUN(4, false, true, "colx CR4");
-  RUN(8, false, true, "colx CR8");
-  RUN(8, true, true, "colx CR8 DB");
-  RUN(4, true, false, "colx CR4 DB no arithmetic");
-  RUN(8, false, false, "colx CR8 no arithmetic");
+  RUNOS(8, false, 3, 0, "os R8 regs");
+  RUNOSP(8, false, 4, 0, 2, "os R8 regs 2-phase exchange");
+  RUNOS(4, false, 4, 0, "os R4 regs");
+  RUNOSP(4, false, 5, 0, 2, "os R4 regs 2-phase exchange");
+  RUNOSP(16, false, 3, 0, 2, "os R16 regs 2-phase exchange");
+  RUNOS(8, false, 3, 0, "os R8 regs (again)");
+  RUNOS(16, true, 2, 0, "os R16 DMA");
   report("K1 product (again)", timeit(prod, iters));
   report("copy x4 nt (again)", timeit([&] {
     hipLaunchKernelGGL(copy_x4_nt, dim3(n4 / 1024), dim3(256), 0, 0, (const v4f*)x, (v4f*)z); }, iters));
