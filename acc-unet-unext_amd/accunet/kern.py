@@ -280,7 +280,7 @@ def dw3x3_rows(B, H, W, C, like: torch.Tensor) -> int:
     return int(_lib_raw().accunet_dw3x3_rows(B, H, W, C, _dt(like)))
 
 
-_DW_NAMES = {2: "dw3x3_span_fwd_kernel", 1: "dw3x3_tile_fwd_kernel", 0: "dw3x3_fwd_kernel"}
+_DW_NAMES = {3: "dw3x3_os_fwd_kernel", 2: "dw3x3_span_fwd_kernel", 1: "dw3x3_tile_fwd_kernel", 0: "dw3x3_fwd_kernel"}
 
 
 def dw3x3_kernel_name(B, H, W, C, like=None) -> str:

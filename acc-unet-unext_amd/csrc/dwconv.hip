@@ -653,6 +653,222 @@ dw3x3_tile_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
   }
 }
 
+// ----------------------------------------------------------------------------
+// K1 one-shot tiles (forward, data gradient, BN-backward data gradient). A block owns
+// R output rows x TP = 256/TCQ pixels x TCQ channel quads of one image and exits after
+// it: every load of the tile is issued at once, and the blocks resident on a CU at any
+// moment cover neighbouring tiles (the strip kernel above walks long column strips, so
+// its resident blocks are spread over the whole tensor; tools/k1lab2: one-shot tiles
+// 3-4 % faster with identical z). Each thread loads ITS OWN pixel-quad column (R + 2
+// rows) into registers; lanes t < 2 TCQ XR of each phase also load the two halo
+// pixels. The prologue (pending BN + LeakyReLU) is applied once per element, the
+// activated quads go to an LDS exchange tile, and a thread reads back only its left and
+// right neighbours (PH = 2: in two halves of XR = (R + 2) / 2 rows, half the LDS).
+// Three rolling accumulators carry the output rows (an arriving input row completes
+// the row above it, continues its own and starts the one below): per output the sum is
+// bias, then the taps row-major, the strip kernel's FMA order, so z is bit-identical.
+// Statistics: fp32 per thread over its R rows, fp64 across the block (one partial row
+// per tile); BNB (data gradient, flip = 1): the BatchNorm-backward partials
+// (sum g, sum g*(bz - mean)), g = out * act'(bz*scale + shift), in fp64 per element.
+// Blocks are dispatched channel group fastest, then tiles in row-major image order.
+// ----------------------------------------------------------------------------
+struct DwOGeom {
+  int B, H, W, C;
+  int tilesW, tilesH, ncg;
+  int ntl;  // non-temporal input loads
+};
+
+template <int TCQ, int R, int PH, bool BNB, int AUX, typename T, int WPE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
+dw3x3_os_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
+                    const float* __restrict__ bias, const float* __restrict__ sc,
+                    const float* __restrict__ sh, int act, int flip, T* __restrict__ z,
+                    double* __restrict__ stats, DwOGeom g, const T* __restrict__ bz,
+                    const float* __restrict__ bst, int bact) {
+  constexpr int TP = 256 / TCQ, IP = TP + 2, IR = R + 2;
+  static_assert(IR % PH == 0, "phases split the input rows");
+  constexpr int XR = IR / PH;                    // exchange rows per phase
+  constexpr int NH = (2 * TCQ * XR + 255) / 256;  // halo loads per lane and phase
+  typedef typename QuadRaw<T>::type RawQ;
+  __shared__ float4 xb[XR][IP][TCQ];
+  const int tid = threadIdx.x;
+  const int q = tid % TCQ, p = tid / TCQ;
+  int t = (int)blockIdx.x;
+  const int cg = t % g.ncg;
+  t /= g.ncg;
+  const int srow = t;  // statistics partial row of this tile
+  const int tw = t % g.tilesW;
+  t /= g.tilesW;
+  const int th = t % g.tilesH;
+  const int b = t / g.tilesH;
+  const int c0 = cg * TCQ * 4, c = c0 + 4 * q;
+  const int w0 = tw * TP, w = w0 + p, h0 = th * R;
+  const long img = (long)b * g.H * g.W * g.C;
+  const unsigned ibytes = (unsigned)(g.H * g.W * g.C * (int)sizeof(T));
+  const __amdgpu_buffer_rsrc_t rx = acc_rsrc(x + img, ibytes);
+  const __amdgpu_buffer_rsrc_t rz = acc_rsrc(z + img, ibytes);
+  const __amdgpu_buffer_rsrc_t rb = acc_rsrc(BNB ? bz + img : x + img, BNB ? ibytes : 0u);
+  const bool pro = sc != nullptr;
+  const bool win = w < g.W;
+  // weights, bias, prologue and BatchNorm vectors first: in flight with the tile
+  float k[9][4], bi[4];
+  float4 ps = make_float4(1.f, 1.f, 1.f, 1.f), pb = make_float4(0.f, 0.f, 0.f, 0.f);
+  float bmu[4] = {0.f, 0.f, 0.f, 0.f}, bsc[4] = {0.f, 0.f, 0.f, 0.f}, bsh[4] = {0.f, 0.f, 0.f, 0.f};
+  {
+    float wv[36];
+#pragma unroll
+    for (int e = 0; e < 9; ++e) {
+      const float4 w4 = ld4(wt + c * 9 + 4 * e);
+      wv[4 * e] = w4.x; wv[4 * e + 1] = w4.y; wv[4 * e + 2] = w4.z; wv[4 * e + 3] = w4.w;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int tp = 0; tp < 9; ++tp) k[tp][j] = wv[j * 9 + (flip ? 8 - tp : tp)];
+    const float4 b4 = bias ? ld4(bias + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    bi[0] = b4.x; bi[1] = b4.y; bi[2] = b4.z; bi[3] = b4.w;
+    if (pro) {
+      ps = ld4(sc + c);
+      pb = ld4(sh + c);
+    }
+    if (BNB) {
+      const float4 m4 = ld4(bst + BN_MEAN * g.C + c), s4 = ld4(bst + BN_SCALE * g.C + c),
+                   h4 = ld4(bst + BN_SHIFT * g.C + c);
+      bmu[0] = m4.x; bmu[1] = m4.y; bmu[2] = m4.z; bmu[3] = m4.w;
+      bsc[0] = s4.x; bsc[1] = s4.y; bsc[2] = s4.z; bsc[3] = s4.w;
+      bsh[0] = h4.x; bsh[1] = h4.y; bsh[2] = h4.z; bsh[3] = h4.w;
+    }
+  }
+  // the whole tile: own column (R + 2 rows) and the halo pixels
+  RawQ own[IR], hv[PH][NH], zb[BNB ? R : 1];
+#pragma unroll
+  for (int r = 0; r < IR; ++r) {
+    const int i = h0 - 1 + r;
+    const bool in = win && i >= 0 && i < g.H;
+    own[r] = bufq_ld<AUX>(rx, in ? (unsigned)(((i * g.W + w) * g.C + c) * (int)sizeof(T)) : ACC_OOB,
+                          (const T*)nullptr);
+  }
+  auto halo = [&](int ph, int m, int& hr, int& hs, int& hq, int& hw, int& hi) {
+    const int e = tid + 256 * m;  // halo element of this phase: (row, side, quad)
+    hr = e / (2 * TCQ);
+    hs = (e / TCQ) & 1;
+    hq = e % TCQ;
+    hw = hs ? w0 + TP : w0 - 1;
+    hi = h0 - 1 + ph * XR + hr;
+    return e < 2 * TCQ * XR && hw >= 0 && hw < g.W && hi >= 0 && hi < g.H;
+  };
+#pragma unroll
+  for (int ph = 0; ph < PH; ++ph)
+#pragma unroll
+    for (int m = 0; m < NH; ++m) {
+      int hr, hs, hq, hw, hi;
+      const bool in = halo(ph, m, hr, hs, hq, hw, hi);
+      hv[ph][m] = bufq_ld<AUX>(rx, in ? (unsigned)(((hi * g.W + hw) * g.C + c0 + 4 * hq) * (int)sizeof(T))
+                                      : ACC_OOB, (const T*)nullptr);
+    }
+  auto activate = [&](float4 a, float4 s4, float4 t4) {
+    if (pro) {
+      a.x = apply_act(a.x * s4.x + t4.x, act);
+      a.y = apply_act(a.y * s4.y + t4.y, act);
+      a.z = apply_act(a.z * s4.z + t4.z, act);
+      a.w = apply_act(a.w * s4.w + t4.w, act);
+    }
+    return a;
+  };
+  float a0[4] = {0.f, 0.f, 0.f, 0.f}, a1[4] = {0.f, 0.f, 0.f, 0.f};
+  float c1[4] = {0.f, 0.f, 0.f, 0.f}, c2[4] = {0.f, 0.f, 0.f, 0.f};
+  double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+  float4 cen[IR];
+#pragma unroll
+  for (int ph = 0; ph < PH; ++ph) {
+    if (ph > 0) __syncthreads();  // every thread is done with the previous phase's rows
+#pragma unroll
+    for (int rr = 0; rr < XR; ++rr) {
+      const int r = ph * XR + rr, i = h0 - 1 + r;
+      const bool in = win && i >= 0 && i < g.H;
+      cen[r] = in ? activate(q2f(own[r]), ps, pb) : make_float4(0.f, 0.f, 0.f, 0.f);
+      xb[rr][p + 1][q] = cen[r];
+    }
+#pragma unroll
+    for (int m = 0; m < NH; ++m) {
+      int hr, hs, hq, hw, hi;
+      const bool in = halo(ph, m, hr, hs, hq, hw, hi);
+      // (256 % TCQ == 0: a halo lane's quad hq is its own quad q, so its prologue too)
+      if (tid + 256 * m < 2 * TCQ * XR)
+        xb[hr][hs ? IP - 1 : 0][hq] = in ? activate(q2f(hv[ph][m]), ps, pb)
+                                         : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    __syncthreads();
+    if (BNB && ph == 0) {  // the pre-BN rows, issued once the raw tile has been consumed
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int h = h0 + r;
+        const bool in = win && h < g.H;
+        zb[r] = bufq_ld<0>(rb, in ? (unsigned)(((h * g.W + w) * g.C + c) * (int)sizeof(T)) : ACC_OOB,
+                           (const T*)nullptr);
+      }
+    }
+#pragma unroll
+    for (int rr = 0; rr < XR; ++rr) {
+      const int r = ph * XR + rr;
+      const float4 L = xb[rr][p][q], Rr = xb[rr][p + 2][q];
+      const float vL[4] = {L.x, L.y, L.z, L.w};
+      const float vC[4] = {cen[r].x, cen[r].y, cen[r].z, cen[r].w};
+      const float vR[4] = {Rr.x, Rr.y, Rr.z, Rr.w};
+      const int h = h0 + r - 2;  // output row completed by input row h0 - 1 + r
+      const bool on = r >= 2 && win && h < g.H;
+      float o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float t0 = a0[j], t1 = a1[j], t2 = bi[j];
+        t0 = fmaf(k[6][j], vL[j], t0); t0 = fmaf(k[7][j], vC[j], t0); t0 = fmaf(k[8][j], vR[j], t0);
+        t1 = fmaf(k[3][j], vL[j], t1); t1 = fmaf(k[4][j], vC[j], t1); t1 = fmaf(k[5][j], vR[j], t1);
+        t2 = fmaf(k[0][j], vL[j], t2); t2 = fmaf(k[1][j], vC[j], t2); t2 = fmaf(k[2][j], vR[j], t2);
+        a0[j] = t1;
+        a1[j] = t2;
+        t0 = rnd<T>(t0);  // statistics of the stored value
+        o[j] = t0;
+        const float am = on ? t0 : 0.f;
+        if (BNB) {
+          if (r >= 2) {
+            const float zz = f4get(q2f(zb[r >= 2 ? r - 2 : 0]), j);
+            float gg = am;
+            if (bact == ACT_LRELU) gg *= lrelu_d(zz * bsc[j] + bsh[j]);
+            s1[j] += gg;
+            s2[j] += (double)gg * ((double)zz - bmu[j]);
+          }
+        } else {
+          c1[j] += am;
+          c2[j] = fmaf(am, am, c2[j]);
+        }
+      }
+      if (r >= 2)
+        bufq_st<2>(rz, on ? (unsigned)(((h * g.W + w) * g.C + c) * (int)sizeof(T)) : ACC_OOB,
+                   make_float4(o[0], o[1], o[2], o[3]), (T*)nullptr);
+    }
+  }
+  if (stats) {
+    __syncthreads();  // the exchange tile is reused as the reduction buffer
+    if (!BNB) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        s1[j] = (double)c1[j];
+        s2[j] = (double)c2[j];
+      }
+    }
+    double v[8] = {s1[0], s1[1], s1[2], s1[3], s2[0], s2[1], s2[2], s2[3]};
+    if (block_slot_reduce<TCQ, 8, double>(v, reinterpret_cast<double*>(&xb[0][0][0]))) {
+      const long row = (long)srow * 2 * g.C;
+      const int cc = c0 + 4 * threadIdx.x;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        stats[row + cc + j] = v[j];
+        stats[row + g.C + cc + j] = v[4 + j];
+      }
+    }
+  }
+}
+
 template <int TCQ, typename T>
 __global__ void __launch_bounds__(256)
 dw3x3_tile_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dz,
@@ -1230,6 +1446,30 @@ static int dw_cgfast() {
   return v;
 }
 
+// K1 tile structure (ACCUNET_DW_OS, A/B knob this round): 0 = the register-staged strip
+// kernel, 1 = one-shot 8-row tiles (dw3x3_os_fwd_kernel), 2 = one-shot 8-row tiles with a
+// two-phase exchange (half the LDS, 4 blocks per CU)
+static int dw_os() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ACCUNET_DW_OS");
+    v = e ? atoi(e) : 1;
+  }
+  return v;
+}
+#define DW_OS_R 8
+
+static DwOGeom dw_ogeom(int B, int H, int W, int C, int tcq, dim3* grid) {
+  DwOGeom g;
+  g.B = B; g.H = H; g.W = W; g.C = C;
+  g.tilesW = ceil_div(W, 256 / tcq);
+  g.tilesH = ceil_div(H, DW_OS_R);
+  g.ncg = C / 4 / tcq;
+  g.ntl = 0;
+  *grid = dim3((unsigned)((long)B * g.tilesH * g.tilesW * g.ncg));
+  return g;
+}
+
 static int dw_rch_max() {
   static int v = -1;
   if (v < 0) {
@@ -1293,6 +1533,7 @@ extern "C" int accunet_dw3x3_variant(int B, int H, int W, int C, int dt) {
   (void)B;
   if (dw_span_nt(H, W, C)) return 2;
   const int tcq = dw_tile_tcq(H, W, C, dt);
+  if (tcq && dw_os()) return 3;
   return tcq ? 1 : 0;
 }
 
@@ -1303,6 +1544,10 @@ extern "C" int accunet_dw3x3_rows(int B, int H, int W, int C, int dt) {
     return (int)grid.x;
   }
   int tcq = dw_tile_tcq(H, W, C, dt);
+  if (tcq && dw_os()) {
+    const DwOGeom og = dw_ogeom(B, H, W, C, tcq, &grid);
+    return B * og.tilesH * og.tilesW;
+  }
   if (tcq) dw_tgeom(B, H, W, C, tcq, &grid, dw_rch_max());
   else dw_geom(B, H, W, C, (C % 4 == 0) ? 4 : 1, &grid);
   return (int)grid.x;
@@ -1348,6 +1593,47 @@ extern "C" int accunet_dw3x3_fwd(const void* x, const float* wt, const float* bi
     return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
   }
   int tcq = dw_tile_tcq(H, W, C, dt);
+  if (tcq && dw_os()) {
+    DwOGeom og = dw_ogeom(B, H, W, C, tcq, &grid);
+    // non-temporal loads only for inputs above the Infinity Cache and whole-line segments
+    const int seg = tcq * 4 * (dt == ACC_BF16 ? 2 : 4);
+    og.ntl = seg % 128 == 0 ? dw_ntl((long)B * H * W * C * (dt == ACC_BF16 ? 2 : 4)) : 0;
+    auto launch = [&](auto tag, auto tcqc, auto bnbc, auto auxc, auto phc) {
+      using T = decltype(tag);
+      constexpr int PH = decltype(phc)::value;
+      hipLaunchKernelGGL((dw3x3_os_fwd_kernel<decltype(tcqc)::value, DW_OS_R, PH,
+                                              decltype(bnbc)::value, decltype(auxc)::value, T,
+                                              PH == 2 ? 4 : 3>),
+                         grid, dim3(256), 0, s, (const T*)x, wt, bias, sc, sh, act, flip, (T*)z,
+                         stats, og, (const T*)bz, bst, bact);
+    };
+    using I16 = std::integral_constant<int, 16>;
+    using I8 = std::integral_constant<int, 8>;
+    using BT = std::integral_constant<bool, true>;
+    using BF = std::integral_constant<bool, false>;
+    using A2 = std::integral_constant<int, 2>;
+    using A0 = std::integral_constant<int, 0>;
+    using P1 = std::integral_constant<int, 1>;
+    using P2 = std::integral_constant<int, 2>;
+    if (with_dt(dt, [&](auto tag) {
+          auto by_ph = [&](auto tc, auto bn, auto ax) {
+            if (dw_os() == 2) launch(tag, tc, bn, ax, P2{});
+            else launch(tag, tc, bn, ax, P1{});
+          };
+          auto by_aux = [&](auto tc, auto bn) {
+            if (og.ntl) by_ph(tc, bn, A2{});
+            else by_ph(tc, bn, A0{});
+          };
+          auto by_bnb = [&](auto tc) {
+            if (bz) by_aux(tc, BT{});
+            else by_aux(tc, BF{});
+          };
+          if (tcq == 16) by_bnb(I16{});
+          else by_bnb(I8{});
+        }))
+      return ACC_EBADARG;
+    return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+  }
   if (tcq) {
     DwTGeom tg = dw_tgeom(B, H, W, C, tcq, &grid, dw_rch_max());
     // non-temporal loads only for inputs above the Infinity Cache (bytes as stored)

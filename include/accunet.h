@@ -169,10 +169,11 @@ int accunet_reduce_stats(const double* part, int R, int C, double* out2C, double
 /* rows of `stats` ([rows][2][C] fp64) the forward writes for this shape and storage
  * dtype dt (bf16 runs 64-channel tiles where C % 64 == 0). */
 int accunet_dw3x3_rows(int B, int H, int W, int C, int dt);
-/* Which forward kernel runs for the shape and storage dtype dt (without bz): 1 = LDS
- * strip kernel (C % 32 == 0), 0 = register-window kernel; 2 = whole-pixel span kernel,
- * only with the tuning knob ACCUNET_DW_SPAN bit 2 set (off by default) and then for
- * C % 8 == 0, C/4 <= 64. */
+/* Which forward kernel runs for the shape and storage dtype dt (without bz): 3 = one-shot
+ * 8-row tiles (C % 32 == 0), 1 = the LDS strip kernel (the same shapes with
+ * ACCUNET_DW_OS=0), 0 = register-window kernel; 2 = whole-pixel span kernel, only with
+ * the tuning knob ACCUNET_DW_SPAN bit 2 set (off by default) and then for C % 8 == 0,
+ * C/4 <= 64. */
 int accunet_dw3x3_variant(int B, int H, int W, int C, int dt);
 int accunet_dw3x3_fwd(const void* x, const float* wt, const float* bias, const float* sc,
                       const float* sh, int act, int flip, void* z, double* stats, int B, int H,

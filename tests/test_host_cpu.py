@@ -295,16 +295,17 @@ def test_abi_host_side_contract_without_a_device():
     assert lib.accunet_dw3x3_fwd(one, one, None, None, None, 0, 1, one, None, 1, 8, 8, 32,
                                  one, None, 0, 0, None) == -2
     assert lib.accunet_gemm(None, None, 0, None) == -2
-    # 16x256x256x96: the tile kernel, 8 tiles of 32 pixels per row, 32-row strips (the
-    # longest with >= 3072 blocks) -> 16 * 8 * 8 = 1024 statistics rows; cnv11's 9
-    # channels the register kernel
-    assert lib.accunet_dw3x3_variant(16, 256, 256, 96, 0) == 1  # the register-staged strip
-    assert lib.accunet_dw3x3_variant(16, 256, 256, 96, 1) == 1
-    assert lib.accunet_dw3x3_rows(16, 256, 256, 96, 0) == 1024
+    # 16x256x256x96: one-shot tiles of 8 rows x 32 pixels -> 16 * 32 * 8 = 4096 statistics
+    # rows (the strip kernel, ACCUNET_DW_OS=0: 32-row strips, 1024); cnv11's 9 channels
+    # the register kernel
+    os_on = os.environ.get("ACCUNET_DW_OS", "1") != "0"
+    assert lib.accunet_dw3x3_variant(16, 256, 256, 96, 0) == (3 if os_on else 1)
+    assert lib.accunet_dw3x3_variant(16, 256, 256, 96, 1) == (3 if os_on else 1)
+    assert lib.accunet_dw3x3_rows(16, 256, 256, 96, 0) == (4096 if os_on else 1024)
     # bf16 (dt 1) runs 64-channel tiles where C % 64 == 0: 16-pixel tiles, twice the rows
     assert lib.accunet_dw3x3_rows(16, 128, 128, 192, 0) * 2 == lib.accunet_dw3x3_rows(16, 128, 128, 192, 1)
-    assert lib.accunet_dw3x3_rows(16, 256, 256, 96, 1) == 1024
-    assert lib.accunet_dw3x3_variant(16, 64, 64, 4352, 1) == 1
+    assert lib.accunet_dw3x3_rows(16, 256, 256, 96, 1) == (4096 if os_on else 1024)
+    assert lib.accunet_dw3x3_variant(16, 64, 64, 4352, 1) == (3 if os_on else 1)
     assert lib.accunet_dw3x3_variant(16, 256, 256, 9, 0) == 0
 
 
