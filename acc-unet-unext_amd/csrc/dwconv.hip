@@ -676,6 +676,7 @@ struct DwOGeom {
   int B, H, W, C;
   int tilesW, tilesH, ncg;
   int ntl;  // non-temporal input loads
+  int xcd;  // channel groups of a tile on one XCD (tiles % 8 == 0): blocks 8 apart
 };
 
 template <int TCQ, int R, int PH, bool BNB, int AUX, typename T, int WPE>
@@ -693,9 +694,18 @@ dw3x3_os_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
   __shared__ float4 xb[XR][IP][TCQ];
   const int tid = threadIdx.x;
   const int q = tid % TCQ, p = tid / TCQ;
-  int t = (int)blockIdx.x;
-  const int cg = t % g.ncg;
-  t /= g.ncg;
+  int t = (int)blockIdx.x, cg;
+  if (g.xcd) {
+    // workgroups are dealt round-robin over the 8 XCDs (b and b + 8 share one): the ncg
+    // channel groups of a tile run 8 apart, on one XCD, so 64-B (bf16) pixel segments
+    // that share a 128-B line are fetched into one L2; tiles stay in dispatch order
+    const int xs = t & 7, j = t >> 3;
+    cg = j % g.ncg;
+    t = (j / g.ncg) * 8 + xs;
+  } else {
+    cg = t % g.ncg;
+    t /= g.ncg;
+  }
   const int srow = t;  // statistics partial row of this tile
   const int tw = t % g.tilesW;
   t /= g.tilesW;
@@ -1466,6 +1476,7 @@ static DwOGeom dw_ogeom(int B, int H, int W, int C, int tcq, dim3* grid) {
   g.tilesH = ceil_div(H, DW_OS_R);
   g.ncg = C / 4 / tcq;
   g.ntl = 0;
+  g.xcd = 0;
   *grid = dim3((unsigned)((long)B * g.tilesH * g.tilesW * g.ncg));
   return g;
 }
@@ -1598,6 +1609,9 @@ extern "C" int accunet_dw3x3_fwd(const void* x, const float* wt, const float* bi
     // non-temporal loads only for inputs above the Infinity Cache and whole-line segments
     const int seg = tcq * 4 * (dt == ACC_BF16 ? 2 : 4);
     og.ntl = seg % 128 == 0 ? dw_ntl((long)B * H * W * C * (dt == ACC_BF16 ? 2 : 4)) : 0;
+    // half-line pixel segments (bf16, 32 channels): the channel groups sharing a line on
+    // one XCD (ACCUNET_DW_OS=3 forces this order for every dtype, A/B)
+    og.xcd = ((seg % 128 != 0 && og.ncg > 1) || dw_os() == 3) && (long)B * og.tilesH * og.tilesW % 8 == 0;
     auto launch = [&](auto tag, auto tcqc, auto bnbc, auto auxc, auto phc) {
       using T = decltype(tag);
       constexpr int PH = decltype(phc)::value;
