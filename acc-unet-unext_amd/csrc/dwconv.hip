@@ -1332,22 +1332,28 @@ dw3x3_span_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dz,
   for (int it = 0; it < nrt; ++it) {
     const int h0 = (tb * nrt + it) * R;
     if (h0 >= g.H) break;  // block-uniform
+    RawQ dr[R];
+    auto issue_dz = [&]() {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const bool in = lane_on && h0 + r < g.H;
+        dr[r] = bufq_ld<0>(rd_, in ? (unsigned)(((h0 + r) * L + s0 + tid) * QB) : ACC_OOB,
+                           (const T*)nullptr);
+      }
+    };
     {
       DwsFill<NT, AUX, T> fill;
       fill.issue(rx, g, h0, s0, sc, sh);
+      // bf16: the dz rows (8 B per lane and row) fit beside the fill registers, so they
+      // are issued with the tile and one memory round trip covers both
+      if constexpr (sizeof(T) == 2) issue_dz();
       if (it > 0) __syncthreads();  // every lane is done with the previous tile
       fill.park(tile, g, pro, act);
     }
-    __builtin_amdgcn_sched_barrier(0);  // keep the dz loads behind the park (registers)
-    // this lane's dz rows, issued once the fill registers are free (in flight across
-    // the barrier)
-    RawQ dr[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const bool in = lane_on && h0 + r < g.H;
-      dr[r] = bufq_ld<0>(rd_, in ? (unsigned)(((h0 + r) * L + s0 + tid) * QB) : ACC_OOB,
-                         (const T*)nullptr);
-    }
+    __builtin_amdgcn_sched_barrier(0);  // keep the fp32 dz loads behind the park (registers)
+    // fp32: this lane's dz rows, issued once the fill registers are free (in flight
+    // across the barrier)
+    if constexpr (sizeof(T) != 2) issue_dz();
     __syncthreads();
     if (tid < NA) {
       float win[3][3][4];

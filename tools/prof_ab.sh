@@ -14,6 +14,8 @@ for v in $VARIANTS; do
   timeout -k 10 300 env ${envs//,/ } rocprofv3 --kernel-trace --output-format csv -d gpurun_out/pa_$name -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-probe --dtype ${DT:-fp32} > gpurun_out/pa_$name.log 2>&1
   python tools/step_profile.py gpurun_out/pa_$name --last 4 --top ${TOP:-60} > gpurun_out/step_$name.txt
   python tools/kstats.py gpurun_out/pa_$name --steps 7 --top 80 > gpurun_out/kstats_$name.txt
+  python tools/splitk_census.py gpurun_out/pa_$name --steps 7 > gpurun_out/splitk_$name.txt
+  for fam in ${KGRID:-}; do python tools/kgrid.py gpurun_out/pa_$name $fam > gpurun_out/kgrid_${name}_$fam.txt; done
   rm -rf gpurun_out/pa_$name
   echo "== $name"; head -24 gpurun_out/step_$name.txt
 done
