@@ -78,6 +78,7 @@ _SIGS = {
     "accunet_stream_ticket_unregister": [P],
     "accunet_abi_hash": [],
     "accunet_conv3x3_halo_launches": [I],
+    "accunet_copy_nt": [P, P, L, P],
     "accunet_relayout_blocks": [L],
     "accunet_relayout_batch": [P, I, I, P],
     "accunet_bn_finalize": [P, I, I, D, P, P, P, P, P, F, F, I, P, P, P],

@@ -291,6 +291,14 @@ def dw3x3_kernel_name(B, H, W, C, like=None) -> str:
     return _DW_NAMES[int(lib.accunet_dw3x3_variant(B, H, W, C, dt))]
 
 
+def copy_nt(src: torch.Tensor, dst: torch.Tensor):
+    """non-temporal float4 copy of src's bytes into dst (the probes' streaming ceiling)"""
+    n = src.numel() * src.element_size()
+    if dst.numel() * dst.element_size() < n:
+        raise _lib.AccError("copy_nt: destination smaller than the source")
+    call("accunet_copy_nt", _p(src), _p(dst), int(n), _stream())
+
+
 def dw3x3_fwd(x, wt, bias, sc, sh, act, flip, z, stats, B, H, W, C, bnb=None):
     """bnb = (bz, bst, bact): `stats` receives BatchNorm-backward partials (see
     accunet_dw3x3_fwd in include/accunet.h)."""

@@ -109,11 +109,12 @@ def k1_dw3x3(B, H, W, C, weight, bias, iters=20, device="cuda", dtype=torch.floa
     t = _time(run, iters)
     name = kern.dw3x3_kernel_name(B, H, W, C, x)
     row = _hbm_row(name, f"{B}x{H}x{W}x{C}", 2.0 * x.element_size() * B * H * W * C, t, iters)
-    # context for the rate: a plain device copy of the same bytes (x read once, z written
-    # once, ATen's vectorised copy) timed the same way right after K1, so the line shows
+    # context for the rate: the fastest device copy of the same bytes (x read once, z
+    # written once; non-temporal float4 loads and stores, 4 per thread: accunet_copy_nt,
+    # tools/kbench "x4/thread nt") timed the same way right after K1, so the line shows
     # what streaming reaches on this GPU in this state (the clocks under sustained load
-    # move both; tools/kbench times both on a rested GPU)
-    c_us, c_per = _time(lambda: z.copy_(x), iters)
+    # move both)
+    c_us, c_per = _time(lambda: kern.copy_nt(x, z), iters)
     row["copy_us"] = round(c_us, 2)
     row["copy_median_us"] = round(statistics.median(c_per), 2)
     row["frac_of_copy"] = round(c_us / t[0], 4)

@@ -660,10 +660,9 @@ dw3x3_tile_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
 // moment cover neighbouring tiles (the strip kernel above walks long column strips, so
 // its resident blocks are spread over the whole tensor; tools/k1lab2: one-shot tiles
 // 3-4 % faster with identical z). Each thread loads ITS OWN pixel-quad column (R + 2
-// rows) into registers; lanes t < 2 TCQ XR of each phase also load the two halo
-// pixels. The prologue (pending BN + LeakyReLU) is applied once per element, the
-// activated quads go to an LDS exchange tile, and a thread reads back only its left and
-// right neighbours (PH = 2: in two halves of XR = (R + 2) / 2 rows, half the LDS).
+// rows) into registers; lanes t < 2 TCQ (R + 2) also load the two halo pixels. The
+// prologue (pending BN + LeakyReLU) is applied once per element, the activated quads go
+// to an LDS exchange tile, and a thread reads back only its left and right neighbours.
 // Three rolling accumulators carry the output rows (an arriving input row completes
 // the row above it, continues its own and starts the one below): per output the sum is
 // bias, then the taps row-major, the strip kernel's FMA order, so z is bit-identical.
@@ -679,19 +678,17 @@ struct DwOGeom {
   int xcd;  // channel groups of a tile on one XCD (tiles % 8 == 0): blocks 8 apart
 };
 
-template <int TCQ, int R, int PH, bool BNB, int AUX, typename T, int WPE>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
+template <int TCQ, int R, bool BNB, int AUX, typename T>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
 dw3x3_os_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
                     const float* __restrict__ bias, const float* __restrict__ sc,
                     const float* __restrict__ sh, int act, int flip, T* __restrict__ z,
                     double* __restrict__ stats, DwOGeom g, const T* __restrict__ bz,
                     const float* __restrict__ bst, int bact) {
   constexpr int TP = 256 / TCQ, IP = TP + 2, IR = R + 2;
-  static_assert(IR % PH == 0, "phases split the input rows");
-  constexpr int XR = IR / PH;                    // exchange rows per phase
-  constexpr int NH = (2 * TCQ * XR + 255) / 256;  // halo loads per lane and phase
+  constexpr int NH = (2 * TCQ * IR + 255) / 256;  // halo loads per lane
   typedef typename QuadRaw<T>::type RawQ;
-  __shared__ float4 xb[XR][IP][TCQ];
+  __shared__ float4 xb[IR][IP][TCQ];
   const int tid = threadIdx.x;
   const int q = tid % TCQ, p = tid / TCQ;
   int t = (int)blockIdx.x, cg;
@@ -750,7 +747,7 @@ dw3x3_os_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
     }
   }
   // the whole tile: own column (R + 2 rows) and the halo pixels
-  RawQ own[IR], hv[PH][NH], zb[BNB ? R : 1];
+  RawQ own[IR], hv[NH], zb[BNB ? R : 1];
 #pragma unroll
   for (int r = 0; r < IR; ++r) {
     const int i = h0 - 1 + r;
@@ -758,24 +755,22 @@ dw3x3_os_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
     own[r] = bufq_ld<AUX>(rx, in ? (unsigned)(((i * g.W + w) * g.C + c) * (int)sizeof(T)) : ACC_OOB,
                           (const T*)nullptr);
   }
-  auto halo = [&](int ph, int m, int& hr, int& hs, int& hq, int& hw, int& hi) {
-    const int e = tid + 256 * m;  // halo element of this phase: (row, side, quad)
+  auto halo = [&](int m, int& hr, int& hs, int& hq, int& hw, int& hi) {
+    const int e = tid + 256 * m;  // halo element: (row, side, quad)
     hr = e / (2 * TCQ);
     hs = (e / TCQ) & 1;
     hq = e % TCQ;
     hw = hs ? w0 + TP : w0 - 1;
-    hi = h0 - 1 + ph * XR + hr;
-    return e < 2 * TCQ * XR && hw >= 0 && hw < g.W && hi >= 0 && hi < g.H;
+    hi = h0 - 1 + hr;
+    return e < 2 * TCQ * IR && hw >= 0 && hw < g.W && hi >= 0 && hi < g.H;
   };
 #pragma unroll
-  for (int ph = 0; ph < PH; ++ph)
-#pragma unroll
-    for (int m = 0; m < NH; ++m) {
-      int hr, hs, hq, hw, hi;
-      const bool in = halo(ph, m, hr, hs, hq, hw, hi);
-      hv[ph][m] = bufq_ld<AUX>(rx, in ? (unsigned)(((hi * g.W + hw) * g.C + c0 + 4 * hq) * (int)sizeof(T))
-                                      : ACC_OOB, (const T*)nullptr);
-    }
+  for (int m = 0; m < NH; ++m) {
+    int hr, hs, hq, hw, hi;
+    const bool in = halo(m, hr, hs, hq, hw, hi);
+    hv[m] = bufq_ld<AUX>(rx, in ? (unsigned)(((hi * g.W + hw) * g.C + c0 + 4 * hq) * (int)sizeof(T))
+                                : ACC_OOB, (const T*)nullptr);
+  }
   auto activate = [&](float4 a, float4 s4, float4 t4) {
     if (pro) {
       a.x = apply_act(a.x * s4.x + t4.x, act);
@@ -790,72 +785,66 @@ dw3x3_os_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
   double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
   float4 cen[IR];
 #pragma unroll
-  for (int ph = 0; ph < PH; ++ph) {
-    if (ph > 0) __syncthreads();  // every thread is done with the previous phase's rows
+  for (int r = 0; r < IR; ++r) {
+    const int i = h0 - 1 + r;
+    const bool in = win && i >= 0 && i < g.H;
+    cen[r] = in ? activate(q2f(own[r]), ps, pb) : make_float4(0.f, 0.f, 0.f, 0.f);
+    xb[r][p + 1][q] = cen[r];
+  }
 #pragma unroll
-    for (int rr = 0; rr < XR; ++rr) {
-      const int r = ph * XR + rr, i = h0 - 1 + r;
-      const bool in = win && i >= 0 && i < g.H;
-      cen[r] = in ? activate(q2f(own[r]), ps, pb) : make_float4(0.f, 0.f, 0.f, 0.f);
-      xb[rr][p + 1][q] = cen[r];
+  for (int m = 0; m < NH; ++m) {
+    int hr, hs, hq, hw, hi;
+    const bool in = halo(m, hr, hs, hq, hw, hi);
+    // (256 % TCQ == 0: a halo lane's quad hq is its own quad q, so its prologue too)
+    if (tid + 256 * m < 2 * TCQ * IR)
+      xb[hr][hs ? IP - 1 : 0][hq] = in ? activate(q2f(hv[m]), ps, pb) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  __syncthreads();
+  if (BNB) {  // the pre-BN rows, issued once the raw tile has been consumed (registers)
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int h = h0 + r;
+      const bool in = win && h < g.H;
+      zb[r] = bufq_ld<0>(rb, in ? (unsigned)(((h * g.W + w) * g.C + c) * (int)sizeof(T)) : ACC_OOB,
+                         (const T*)nullptr);
     }
+  }
 #pragma unroll
-    for (int m = 0; m < NH; ++m) {
-      int hr, hs, hq, hw, hi;
-      const bool in = halo(ph, m, hr, hs, hq, hw, hi);
-      // (256 % TCQ == 0: a halo lane's quad hq is its own quad q, so its prologue too)
-      if (tid + 256 * m < 2 * TCQ * XR)
-        xb[hr][hs ? IP - 1 : 0][hq] = in ? activate(q2f(hv[ph][m]), ps, pb)
-                                         : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    __syncthreads();
-    if (BNB && ph == 0) {  // the pre-BN rows, issued once the raw tile has been consumed
+  for (int r = 0; r < IR; ++r) {
+    const float4 L = xb[r][p][q], Rr = xb[r][p + 2][q];
+    const float vL[4] = {L.x, L.y, L.z, L.w};
+    const float vC[4] = {cen[r].x, cen[r].y, cen[r].z, cen[r].w};
+    const float vR[4] = {Rr.x, Rr.y, Rr.z, Rr.w};
+    const int h = h0 + r - 2;  // output row completed by input row h0 - 1 + r
+    const bool on = r >= 2 && win && h < g.H;
+    float o[4];
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const int h = h0 + r;
-        const bool in = win && h < g.H;
-        zb[r] = bufq_ld<0>(rb, in ? (unsigned)(((h * g.W + w) * g.C + c) * (int)sizeof(T)) : ACC_OOB,
-                           (const T*)nullptr);
-      }
-    }
-#pragma unroll
-    for (int rr = 0; rr < XR; ++rr) {
-      const int r = ph * XR + rr;
-      const float4 L = xb[rr][p][q], Rr = xb[rr][p + 2][q];
-      const float vL[4] = {L.x, L.y, L.z, L.w};
-      const float vC[4] = {cen[r].x, cen[r].y, cen[r].z, cen[r].w};
-      const float vR[4] = {Rr.x, Rr.y, Rr.z, Rr.w};
-      const int h = h0 + r - 2;  // output row completed by input row h0 - 1 + r
-      const bool on = r >= 2 && win && h < g.H;
-      float o[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float t0 = a0[j], t1 = a1[j], t2 = bi[j];
-        t0 = fmaf(k[6][j], vL[j], t0); t0 = fmaf(k[7][j], vC[j], t0); t0 = fmaf(k[8][j], vR[j], t0);
-        t1 = fmaf(k[3][j], vL[j], t1); t1 = fmaf(k[4][j], vC[j], t1); t1 = fmaf(k[5][j], vR[j], t1);
-        t2 = fmaf(k[0][j], vL[j], t2); t2 = fmaf(k[1][j], vC[j], t2); t2 = fmaf(k[2][j], vR[j], t2);
-        a0[j] = t1;
-        a1[j] = t2;
-        t0 = rnd<T>(t0);  // statistics of the stored value
-        o[j] = t0;
-        const float am = on ? t0 : 0.f;
-        if (BNB) {
-          if (r >= 2) {
-            const float zz = f4get(q2f(zb[r >= 2 ? r - 2 : 0]), j);
-            float gg = am;
-            if (bact == ACT_LRELU) gg *= lrelu_d(zz * bsc[j] + bsh[j]);
-            s1[j] += gg;
-            s2[j] += (double)gg * ((double)zz - bmu[j]);
-          }
-        } else {
-          c1[j] += am;
-          c2[j] = fmaf(am, am, c2[j]);
+    for (int j = 0; j < 4; ++j) {
+      float t0 = a0[j], t1 = a1[j], t2 = bi[j];
+      t0 = fmaf(k[6][j], vL[j], t0); t0 = fmaf(k[7][j], vC[j], t0); t0 = fmaf(k[8][j], vR[j], t0);
+      t1 = fmaf(k[3][j], vL[j], t1); t1 = fmaf(k[4][j], vC[j], t1); t1 = fmaf(k[5][j], vR[j], t1);
+      t2 = fmaf(k[0][j], vL[j], t2); t2 = fmaf(k[1][j], vC[j], t2); t2 = fmaf(k[2][j], vR[j], t2);
+      a0[j] = t1;
+      a1[j] = t2;
+      t0 = rnd<T>(t0);  // statistics of the stored value
+      o[j] = t0;
+      const float am = on ? t0 : 0.f;
+      if (BNB) {
+        if (r >= 2) {
+          const float zz = f4get(q2f(zb[r >= 2 ? r - 2 : 0]), j);
+          float gg = am;
+          if (bact == ACT_LRELU) gg *= lrelu_d(zz * bsc[j] + bsh[j]);
+          s1[j] += gg;
+          s2[j] += (double)gg * ((double)zz - bmu[j]);
         }
+      } else {
+        c1[j] += am;
+        c2[j] = fmaf(am, am, c2[j]);
       }
-      if (r >= 2)
-        bufq_st<2>(rz, on ? (unsigned)(((h * g.W + w) * g.C + c) * (int)sizeof(T)) : ACC_OOB,
-                   make_float4(o[0], o[1], o[2], o[3]), (T*)nullptr);
     }
+    if (r >= 2)
+      bufq_st<2>(rz, on ? (unsigned)(((h * g.W + w) * g.C + c) * (int)sizeof(T)) : ACC_OOB,
+                 make_float4(o[0], o[1], o[2], o[3]), (T*)nullptr);
   }
   if (stats) {
     __syncthreads();  // the exchange tile is reused as the reduction buffer
@@ -1462,9 +1451,12 @@ static int dw_cgfast() {
   return v;
 }
 
-// K1 tile structure (ACCUNET_DW_OS, A/B knob this round): 0 = the register-staged strip
-// kernel, 1 = one-shot 8-row tiles (dw3x3_os_fwd_kernel), 2 = one-shot 8-row tiles with a
-// two-phase exchange (half the LDS, 4 blocks per CU)
+// Forward-type tile kernel (ACCUNET_DW_OS): 1 (default) = one-shot 8-row tiles
+// (dw3x3_os_fwd_kernel) for fp32 storage and the strip kernel for bf16, 2 = one-shot
+// tiles for both, 0 = the strip kernel for both. Every forward-type launch of a shape
+// (forward, data gradient, BN-backward data gradient) takes the same kernel, so the
+// statistics rows agree (accunet_dw3x3_rows). tests/test_kernels_gpu.py runs all three
+// settings bit for bit against each other.
 static int dw_os() {
   static int v = -1;
   if (v < 0) {
@@ -1473,6 +1465,7 @@ static int dw_os() {
   }
   return v;
 }
+static bool dw_os_on(int dt) { return dw_os() == 2 || (dw_os() == 1 && dt == ACC_F32); }
 #define DW_OS_R 8
 
 static DwOGeom dw_ogeom(int B, int H, int W, int C, int tcq, dim3* grid) {
@@ -1550,7 +1543,7 @@ extern "C" int accunet_dw3x3_variant(int B, int H, int W, int C, int dt) {
   (void)B;
   if (dw_span_nt(H, W, C)) return 2;
   const int tcq = dw_tile_tcq(H, W, C, dt);
-  if (tcq && dw_os()) return 3;
+  if (tcq && dw_os_on(dt)) return 3;
   return tcq ? 1 : 0;
 }
 
@@ -1561,7 +1554,7 @@ extern "C" int accunet_dw3x3_rows(int B, int H, int W, int C, int dt) {
     return (int)grid.x;
   }
   int tcq = dw_tile_tcq(H, W, C, dt);
-  if (tcq && dw_os()) {
+  if (tcq && dw_os_on(dt)) {
     const DwOGeom og = dw_ogeom(B, H, W, C, tcq, &grid);
     return B * og.tilesH * og.tilesW;
   }
@@ -1610,20 +1603,18 @@ extern "C" int accunet_dw3x3_fwd(const void* x, const float* wt, const float* bi
     return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
   }
   int tcq = dw_tile_tcq(H, W, C, dt);
-  if (tcq && dw_os()) {
+  if (tcq && dw_os_on(dt)) {
     DwOGeom og = dw_ogeom(B, H, W, C, tcq, &grid);
     // non-temporal loads only for inputs above the Infinity Cache and whole-line segments
     const int seg = tcq * 4 * (dt == ACC_BF16 ? 2 : 4);
     og.ntl = seg % 128 == 0 ? dw_ntl((long)B * H * W * C * (dt == ACC_BF16 ? 2 : 4)) : 0;
     // half-line pixel segments (bf16, 32 channels): the channel groups sharing a line on
-    // one XCD (ACCUNET_DW_OS=3 forces this order for every dtype, A/B)
-    og.xcd = ((seg % 128 != 0 && og.ncg > 1) || dw_os() == 3) && (long)B * og.tilesH * og.tilesW % 8 == 0;
-    auto launch = [&](auto tag, auto tcqc, auto bnbc, auto auxc, auto phc) {
+    // one XCD
+    og.xcd = seg % 128 != 0 && og.ncg > 1 && (long)B * og.tilesH * og.tilesW % 8 == 0;
+    auto launch = [&](auto tag, auto tcqc, auto bnbc, auto auxc) {
       using T = decltype(tag);
-      constexpr int PH = decltype(phc)::value;
-      hipLaunchKernelGGL((dw3x3_os_fwd_kernel<decltype(tcqc)::value, DW_OS_R, PH,
-                                              decltype(bnbc)::value, decltype(auxc)::value, T,
-                                              PH == 2 ? 4 : 3>),
+      hipLaunchKernelGGL((dw3x3_os_fwd_kernel<decltype(tcqc)::value, DW_OS_R,
+                                              decltype(bnbc)::value, decltype(auxc)::value, T>),
                          grid, dim3(256), 0, s, (const T*)x, wt, bias, sc, sh, act, flip, (T*)z,
                          stats, og, (const T*)bz, bst, bact);
     };
@@ -1633,16 +1624,10 @@ extern "C" int accunet_dw3x3_fwd(const void* x, const float* wt, const float* bi
     using BF = std::integral_constant<bool, false>;
     using A2 = std::integral_constant<int, 2>;
     using A0 = std::integral_constant<int, 0>;
-    using P1 = std::integral_constant<int, 1>;
-    using P2 = std::integral_constant<int, 2>;
     if (with_dt(dt, [&](auto tag) {
-          auto by_ph = [&](auto tc, auto bn, auto ax) {
-            if (dw_os() == 2) launch(tag, tc, bn, ax, P2{});
-            else launch(tag, tc, bn, ax, P1{});
-          };
           auto by_aux = [&](auto tc, auto bn) {
-            if (og.ntl) by_ph(tc, bn, A2{});
-            else by_ph(tc, bn, A0{});
+            if (og.ntl) launch(tag, tc, bn, A2{});
+            else launch(tag, tc, bn, A0{});
           };
           auto by_bnb = [&](auto tc) {
             if (bz) by_aux(tc, BT{});

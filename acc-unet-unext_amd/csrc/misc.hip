@@ -568,6 +568,31 @@ struct MakeMarkers<0, I...> {
 };
 typedef MakeMarkers<ACC_MAX_MARKERS>::type Markers;
 
+// The probes' streaming ceiling (include/accunet.h accunet_copy_nt): one 16-KB chunk per
+// 256-thread block, 4 float4 per thread, non-temporal both ways.
+typedef float acc_v4f __attribute__((ext_vector_type(4)));
+__global__ void __launch_bounds__(256) copy_nt_kernel(const acc_v4f* __restrict__ a,
+                                                      acc_v4f* __restrict__ b, long n) {
+  const long base = (long)blockIdx.x * 1024 + threadIdx.x;
+  acc_v4f v[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (base + 256 * k < n) v[k] = __builtin_nontemporal_load(&a[base + 256 * k]);
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (base + 256 * k < n) __builtin_nontemporal_store(v[k], &b[base + 256 * k]);
+}
+
+extern "C" int accunet_copy_nt(const void* src, void* dst, long long n_bytes, void* stream) {
+  if (!src || !dst || n_bytes < 0 || (n_bytes & 15) || (((uintptr_t)src | (uintptr_t)dst) & 15))
+    return ACC_EBADARG;
+  const long n = (long)(n_bytes / 16);
+  if (n == 0) return ACC_OK;
+  hipLaunchKernelGGL(copy_nt_kernel, dim3((unsigned)((n + 1023) / 1024)), dim3(256), 0,
+                     (hipStream_t)stream, (const acc_v4f*)src, (acc_v4f*)dst, n);
+  return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+}
+
 extern "C" int accunet_graph_marker(int id, void* stream) {
   if (id < 0 || id >= ACC_MAX_MARKERS) return ACC_EBADARG;
   if (hipLaunchKernel(Markers::get(id), dim3(1), dim3(1), nullptr, 0, (hipStream_t)stream) !=

@@ -358,6 +358,14 @@ int accunet_stream_wait_event(void* stream, void* ev);
 int accunet_event_synchronize(void* ev);
 
 /* ------------------------------------------------------------------------- *
+ * Streaming ceiling for the roofline probes (accunet/probe.py): copies n_bytes
+ * (a multiple of 16, 16-B aligned buffers) from src to dst with non-temporal float4
+ * loads and stores, four per thread per 16-KB block -- the fastest copy form measured
+ * on MI355X (tools/kbench "x4/thread nt"). Not on the model path.
+ * ------------------------------------------------------------------------- */
+int accunet_copy_nt(const void* src, void* dst, long long n_bytes, void* stream);
+
+/* ------------------------------------------------------------------------- *
  * Input preparation (csrc/data.hip). Replaces the per-image host work of
  * ImageToImage2D.__getitem__, Experiments/Load_Dataset.py:453-487, for a whole
  * batch: image_prep takes N raw channel planes [N][Hin][Win] (fp32) and writes

@@ -19,7 +19,8 @@ SHAPES = [(2, 16, 64, 96), (1, 13, 35, 96), (2, 9, 21, 192), (2, 16, 16, 128), (
 def main(out_path):
     dev = "cuda"
     lib = _lib.load()
-    res = {"variant": torch.tensor(lib.accunet_dw3x3_variant(2, 16, 64, 96, 0))}
+    res = {"variant": torch.tensor(lib.accunet_dw3x3_variant(2, 16, 64, 96, 0)),
+           "variant_bf16": torch.tensor(lib.accunet_dw3x3_variant(2, 16, 64, 96, 1))}
     for (B, H, W, C) in SHAPES:
         for dt in (torch.float32, torch.bfloat16):
             g = torch.Generator().manual_seed(B * 100 + H * 7 + C)

@@ -97,25 +97,29 @@ def test_dw3x3_fwd_stats_wgrad_vs_fp64(B, H, W, C, pro):
     assert (db.double().cpu() - gb).abs().max().item() <= 1e-5 * gb.abs().max().item() + 1e-5
 
 
-def test_dw3x3_one_shot_matches_strip_bitwise(tmp_path):
-    """The one-shot tile kernel (ACCUNET_DW_OS=1, the default for C % 32 == 0) and the
-    strip kernel (ACCUNET_DW_OS=0) sum every output in the same order (bias, then the
-    taps row-major), so forward z, the flipped-kernel data gradient and the
-    BatchNorm-backward data gradient are bit-identical in fp32 and bf16, and their
-    statistics totals (the partial rows are cut differently: one per 8-row tile vs one
-    per 32-row strip) agree to fp64 summation order. Each run in a child process (the
-    knob is read once per process; tests/dw_os_worker.py)."""
+@pytest.mark.parametrize("setting", ["1", "2"])
+def test_dw3x3_one_shot_matches_strip_bitwise(tmp_path, setting):
+    """The one-shot tile kernel and the strip kernel sum every output in the same order
+    (bias, then the taps row-major), so forward z, the flipped-kernel data gradient and
+    the BatchNorm-backward data gradient are bit-identical, and their statistics totals
+    (the partial rows are cut differently: one per 8-row tile vs one per 32-row strip)
+    agree to summation order. ACCUNET_DW_OS=1 (the default: one-shot tiles for fp32,
+    the strip for bf16) and 2 (one-shot tiles for both) against 0 (the strip for both),
+    fp32 and bf16, each in a child process (the knob is read once per process;
+    tests/dw_os_worker.py)."""
     import subprocess
     outs = {}
-    for v in ("1", "0"):
+    for v in (setting, "0"):
         env = dict(os.environ, ACCUNET_DW_OS=v)
         path = tmp_path / f"dw_{v}.pt"
         subprocess.run([sys.executable, os.path.join(HERE, "dw_os_worker.py"), str(path)], env=env,
                        check=True, timeout=240)
         outs[v] = torch.load(path, weights_only=True)
-    assert int(outs["1"].pop("variant")) == 3 and int(outs["0"].pop("variant")) == 1
-    for k in outs["1"]:
-        a, b = outs["1"][k], outs["0"][k]
+    assert int(outs[setting].pop("variant")) == 3 and int(outs["0"].pop("variant")) == 1
+    assert int(outs[setting].pop("variant_bf16")) == (3 if setting == "2" else 1)
+    outs["0"].pop("variant_bf16")
+    for k in outs[setting]:
+        a, b = outs[setting][k], outs["0"][k]
         if k.endswith("_sb"):  # BN-backward partials: fp64 per element in both kernels
             assert torch.allclose(a, b, rtol=1e-9, atol=1e-9 * float(b.abs().max())), k
         elif k.endswith("_st"):  # (sum z, sum z^2): fp32 over 4-row chunks vs 8-row tiles

@@ -166,6 +166,17 @@ int main(int argc, char** argv) {
     report("K1 dw3x3_fwd flip (dgrad) no pro/stats",
            timeit([&] { CA(accunet_dw3x3_fwd(x, wt, nullptr, nullptr, nullptr, 0, 1, z, nullptr, B, H, W, C, nullptr, nullptr, 0, ACC_F32, 0)); }, iters),
            bytes);
+    {  // the BatchNorm-backward data gradient (flip, bz / bst, BN-backward partials):
+       // reads dz and bz, writes dA -- 3 x B*H*W*C*4 bytes
+      float *bz = dalloc(n), *bst = dalloc(4 * C, 1.f);
+      report("K1 dw3x3_fwd BN-backward dgrad (flip, bz, partials)",
+             timeit([&] { CA(accunet_dw3x3_fwd(x, wt, nullptr, nullptr, nullptr, 0, 1, z, st, B, H, W, C, bz, bst, 1, ACC_F32, 0)); }, iters),
+             1.5 * bytes);
+      report("K1 bf16 BN-backward dgrad (flip, bz, partials)",
+             timeit([&] { CA(accunet_dw3x3_fwd(x, wt, nullptr, nullptr, nullptr, 0, 1, z, st, B, H, W, C, bz, bst, 1, ACC_BF16, 0)); }, iters),
+             0.75 * bytes);
+      CK(hipFree(bz)); CK(hipFree(bst));
+    }
     size_t wse = std::max(accunet_dw3x3_wgrad_ws(B, H, W, C, ACC_F32), accunet_dw3x3_wgrad_ws(B, H, W, C, ACC_BF16));
     float* ws = dalloc(wse);
     float *dw = dalloc(9 * C), *db = dalloc(C);
