@@ -231,7 +231,7 @@ ACC_DEV void dma16(const float* src, float4* lds_dst) {
                : "memory");
 }
 
-template <int R, bool DMA, int WPE, int PH = 1>
+template <int R, bool DMA, int WPE, int PH = 1, bool FULL = false, int AUXL = 2, int AUXS = 2>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 os(const float* __restrict__ x, const float* __restrict__ wt, const float* __restrict__ bias,
    const float* __restrict__ sc, const float* __restrict__ sh, float* __restrict__ z,
@@ -239,7 +239,10 @@ os(const float* __restrict__ x, const float* __restrict__ wt, const float* __res
   constexpr int IP = TP + 2, IR = R + 2;
   static_assert(IR % PH == 0 && (!DMA || PH == 1), "phases split the input rows");
   constexpr int XR = IR / PH;  // exchange rows per phase (PH = 2: half the LDS)
-  __shared__ float4 xb[XR][IP][TCQ];
+  // FULL: an exchange row per input row (no reuse across phases: one barrier per phase,
+  // and phase 0 waits only for its own rows, issued first)
+  constexpr int LR = FULL ? IR : XR;
+  __shared__ float4 xb[LR][IP][TCQ];
   const int tid = threadIdx.x;
   const int q = tid % TCQ, p = tid / TCQ;
   int bid = blockIdx.x;
@@ -252,8 +255,9 @@ os(const float* __restrict__ x, const float* __restrict__ wt, const float* __res
   const int srow = t;
   const int tw = t % (W / TP);
   t /= (W / TP);
-  const int th = t % (H / R);
-  const int b = t / (H / R);
+  constexpr int NTH = (H + R - 1) / R;
+  const int th = t % NTH;
+  const int b = t / NTH;
   const int c0 = cg * TCQ * 4, c = c0 + 4 * q;
   const int w0 = tw * TP, w = w0 + p, h0 = th * R;
   const long img = (long)b * H * W * C;
@@ -295,17 +299,17 @@ os(const float* __restrict__ x, const float* __restrict__ wt, const float* __res
     __syncthreads();
   } else {
 #pragma unroll
-    for (int r = 0; r < IR; ++r) {
-      const int i = h0 - 1 + r;
-      const bool rin = i >= 0 && i < H;
-      own[r] = bufq_ld<2>(rx, rin ? (unsigned)(((i * W + w) * C + c) * 4) : ACC_OOB, (const float*)nullptr);
-    }
-#pragma unroll
     for (int ph = 0; ph < PH; ++ph) {
+#pragma unroll
+      for (int rr = 0; rr < XR; ++rr) {
+        const int r = ph * XR + rr, i = h0 - 1 + r;
+        const bool rin = i >= 0 && i < H;
+        own[r] = bufq_ld<AUXL>(rx, rin ? (unsigned)(((i * W + w) * C + c) * 4) : ACC_OOB, (const float*)nullptr);
+      }
       const int hrow = h0 - 1 + ph * XR + hr;
       const bool hin = hl && hw >= 0 && hw < W && hrow >= 0 && hrow < H;
-      hv[ph] = bufq_ld<2>(rx, hin ? (unsigned)(((hrow * W + hw) * C + c) * 4) : ACC_OOB,
-                          (const float*)nullptr);
+      hv[ph] = bufq_ld<AUXL>(rx, hin ? (unsigned)(((hrow * W + hw) * C + c) * 4) : ACC_OOB,
+                             (const float*)nullptr);
     }
   }
   float a0[4] = {0.f, 0.f, 0.f, 0.f}, a1[4] = {0.f, 0.f, 0.f, 0.f};
@@ -314,27 +318,28 @@ os(const float* __restrict__ x, const float* __restrict__ wt, const float* __res
 #pragma unroll
   for (int ph = 0; ph < PH; ++ph) {
     if (!DMA) {
-      if (ph > 0) __syncthreads();  // every thread is done with the previous phase's rows
+      if (ph > 0 && !FULL) __syncthreads();  // every thread is done with the previous phase's rows
 #pragma unroll
       for (int rr = 0; rr < XR; ++rr) {
         const int r = ph * XR + rr, i = h0 - 1 + r;
         own[r] = (i >= 0 && i < H) ? act4(own[r], ps, pb) : make_float4(0.f, 0.f, 0.f, 0.f);
-        xb[rr][p + 1][q] = own[r];
+        xb[FULL ? r : rr][p + 1][q] = own[r];
       }
       if (hl) {
         const int hrow = h0 - 1 + ph * XR + hr;
         const bool hin = hw >= 0 && hw < W && hrow >= 0 && hrow < H;
-        xb[hr][hs ? IP - 1 : 0][q] = hin ? act4(hv[ph], ps, pb) : make_float4(0.f, 0.f, 0.f, 0.f);
+        xb[FULL ? ph * XR + hr : hr][hs ? IP - 1 : 0][q] = hin ? act4(hv[ph], ps, pb) : make_float4(0.f, 0.f, 0.f, 0.f);
       }
       __syncthreads();
     }
 #pragma unroll
     for (int rr = 0; rr < XR; ++rr) {
       const int r = ph * XR + rr, i = h0 - 1 + r;
-      float4 L = xb[rr][p][q], Cc, Rr = xb[rr][p + 2][q];
+      const int xr = FULL ? r : rr;
+      float4 L = xb[xr][p][q], Cc, Rr = xb[xr][p + 2][q];
       if (DMA) {
         const bool rin = i >= 0 && i < H;
-        Cc = xb[rr][p + 1][q];
+        Cc = xb[xr][p + 1][q];
         Cc = rin ? act4(Cc, ps, pb) : make_float4(0.f, 0.f, 0.f, 0.f);
         L = (rin && lin) ? act4(L, ps, pb) : make_float4(0.f, 0.f, 0.f, 0.f);
         Rr = (rin && rinw) ? act4(Rr, ps, pb) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -354,13 +359,13 @@ os(const float* __restrict__ x, const float* __restrict__ wt, const float* __res
         o[j] = t0;
         a0[j] = t1;
         a1[j] = t2;
-        if (r >= 2) {
+        if (r >= 2 && i - 1 < H) {
           c1[j] += t0;
           c2[j] = fmaf(t0, t0, c2[j]);
         }
       }
-      if (r >= 2)
-        bufq_st<2>(rz, (unsigned)((((i - 1) * W + w) * C + c) * 4), make_float4(o[0], o[1], o[2], o[3]),
+      if (r >= 2 && i - 1 < H)
+        bufq_st<AUXS>(rz, (unsigned)((((i - 1) * W + w) * C + c) * 4), make_float4(o[0], o[1], o[2], o[3]),
                    (float*)nullptr);
     }
   }
@@ -475,6 +480,18 @@ int main(int argc, char** argv) {
     check(NAME, AR);                                                                          \
   }
 #define RUNOS(R, DMA, WPE, REMAP, NAME) RUNOSP(R, DMA, WPE, REMAP, 1, NAME)
+#define RUNOSX(R, WPE, PH, FULL, AL, AS, NAME)                                                 \
+  {                                                                                            \
+    stat_rows = B * ((H + R - 1) / R) * (W / TP);                                              \
+    if (stat_rows > st_cap) { fprintf(stderr, "stats rows %d > %d\n", stat_rows, st_cap); exit(3); } \
+    auto f = [&] { hipLaunchKernelGGL((os<R, false, WPE, PH, FULL, AL, AS>), dim3(stat_rows * NCG), dim3(256), 0, 0, \
+                                      x, wt, bi, sc, sh, z, st, 0); };                          \
+    CK(hipMemset(z, 0, n * 4));                                                                \
+    report(NAME, timeit(f, iters));                                                            \
+    CK(hipGetLastError());                                                                     \
+    check(NAME, true);                                                                         \
+    stat_rows = NT;                                                                            \
+  }
 #define RUNOSP(R, DMA, WPE, REMAP, PH, NAME)                                                   \
   {                                                                                            \
     stat_rows = B * (H / R) * (W / TP);                                                        \
@@ -487,14 +504,13 @@ int main(int argc, char** argv) {
     check(NAME, true);                                                                         \
     stat_rows = NT;                                                                            \
   }
-  RUN(4, false, true, "colx CR4");
   RUNOS(8, false, 3, 0, "os R8 regs");
-  RUNOSP(8, false, 4, 0, 2, "os R8 regs 2-phase exchange");
-  RUNOS(4, false, 4, 0, "os R4 regs");
-  RUNOSP(4, false, 5, 0, 2, "os R4 regs 2-phase exchange");
-  RUNOSP(16, false, 3, 0, 2, "os R16 regs 2-phase exchange");
+  RUNOSX(8, 3, 2, true, 2, 2, "os R8 split barrier (full LDS)");
+  RUNOSX(8, 3, 1, false, 0, 2, "os R8 default-policy loads");
+  RUNOSX(8, 3, 1, false, 2, 0, "os R8 default-policy stores");
+  RUNOSX(6, 4, 1, false, 2, 2, "os R6 (4 blocks/CU)");
+  RUNOSX(6, 4, 2, true, 2, 2, "os R6 split barrier");
   RUNOS(8, false, 3, 0, "os R8 regs (again)");
-  RUNOS(16, true, 2, 0, "os R16 DMA");
   report("K1 product (again)", timeit(prod, iters));
   report("copy x4 nt (again)", timeit([&] {
     hipLaunchKernelGGL(copy_x4_nt, dim3(n4 / 1024), dim3(256), 0, 0, (const v4f*)x, (v4f*)z); }, iters));
