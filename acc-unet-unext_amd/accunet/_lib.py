@@ -87,7 +87,7 @@ _SIGS = {
     "accunet_bn_bwd": [P, P, P, P, I, I, L, I, P, I, P, P, P, P, S, I, P],
     "accunet_colsum": [P, L, I, P, P, S, I, P],
     "accunet_reduce_stats": [P, I, I, P, P, P],
-    "accunet_dw3x3_rows": [I, I, I, I, I],
+    "accunet_dw3x3_rows": [I, I, I, I, I, I],
     "accunet_dw3x3_variant": [I, I, I, I, I],
     "accunet_dw3x3_fwd": [P, P, P, P, P, I, I, P, P, I, I, I, I, P, P, I, I, P],
     "accunet_bn_bwd_part_ws_elems": [L, I, I],

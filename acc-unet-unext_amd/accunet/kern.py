@@ -275,9 +275,10 @@ def stream_ticket_bank(stream, bank: int) -> None:
     call("accunet_stream_ticket_bank", ctypes.c_void_p(stream.cuda_stream), int(bank))
 
 
-def dw3x3_rows(B, H, W, C, like: torch.Tensor) -> int:
-    """rows of the forward's statistics partials for this shape and like's storage dtype"""
-    return int(_lib_raw().accunet_dw3x3_rows(B, H, W, C, _dt(like)))
+def dw3x3_rows(B, H, W, C, like: torch.Tensor, bnb: bool = False) -> int:
+    """rows of the statistics partials accunet_dw3x3_fwd writes for this shape and like's
+    storage dtype: the forward's (bnb False) or the BN-backward data gradient's"""
+    return int(_lib_raw().accunet_dw3x3_rows(B, H, W, C, _dt(like), 1 if bnb else 0))
 
 
 _DW_NAMES = {3: "dw3x3_os_fwd_kernel", 2: "dw3x3_span_fwd_kernel", 1: "dw3x3_tile_fwd_kernel", 0: "dw3x3_fwd_kernel"}

@@ -823,7 +823,7 @@ class _DWConvFn(torch.autograd.Function):
         part = R = None
         if pro.active:
             # norm1's backward reduce rides in the data-gradient kernel's epilogue
-            R = kern.dw3x3_rows(B, H, W, C, dZ)
+            R = kern.dw3x3_rows(B, H, W, C, dZ, bnb=True)
             part = _bnb_part(pro, B * H * W, C, z, R)
             kern.dw3x3_fwd(dZ, weight, None, None, None, ACT_NONE, 1, dA, part, B, H, W, C,
                            bnb=(z, pro.st, pro.act))

@@ -1451,11 +1451,15 @@ static int dw_cgfast() {
   return v;
 }
 
-// Forward-type tile kernel (ACCUNET_DW_OS): 1 (default) = one-shot 8-row tiles
-// (dw3x3_os_fwd_kernel) for fp32 storage and the strip kernel for bf16, 2 = one-shot
-// tiles for both, 0 = the strip kernel for both. Every forward-type launch of a shape
-// (forward, data gradient, BN-backward data gradient) takes the same kernel, so the
-// statistics rows agree (accunet_dw3x3_rows). tests/test_kernels_gpu.py runs all three
+// Which forward-type tile kernel a launch takes (ACCUNET_DW_OS): 1 (default) = one-shot
+// 8-row tiles (dw3x3_os_fwd_kernel) for the fp32 forward and plain data gradient of
+// inputs above the 256 MB Infinity Cache (the K1 shapes, 16 x 256^2 x 96 / 192), the
+// strip kernel for everything else; 2 = one-shot tiles for every tile shape, dtype and
+// launch kind; 0 = the strip kernel everywhere. Single-stream traces of the step
+// (profiles/r05_dw_os_ab.txt): one-shot tiles are faster only on the streamed (> 256 MB)
+// shapes; the BN-backward data gradient (a second pre-BN operand per output) and the
+// cached 64^2..128^2 shapes run faster as strips. The statistics rows follow the kernel
+// (accunet_dw3x3_rows takes the launch kind). tests/test_kernels_gpu.py runs the three
 // settings bit for bit against each other.
 static int dw_os() {
   static int v = -1;
@@ -1465,7 +1469,11 @@ static int dw_os() {
   }
   return v;
 }
-static bool dw_os_on(int dt) { return dw_os() == 2 || (dw_os() == 1 && dt == ACC_F32); }
+static bool dw_os_on(int B, int H, int W, int C, int dt, bool bnb) {
+  if (dw_os() == 2) return true;
+  if (dw_os() != 1 || dt != ACC_F32 || bnb) return false;
+  return (long)B * H * W * C * 4 > (256L << 20);
+}
 #define DW_OS_R 8
 
 static DwOGeom dw_ogeom(int B, int H, int W, int C, int tcq, dim3* grid) {
@@ -1540,21 +1548,20 @@ static DwGeom dw_geom(int B, int H, int W, int C, int V, dim3* grid) {
 // a BN-backward epilogue: 2 = span, 1 = tile (strip), 0 = register window (profiling
 // names / the bench probe); it follows the same two choices the launch below makes
 extern "C" int accunet_dw3x3_variant(int B, int H, int W, int C, int dt) {
-  (void)B;
   if (dw_span_nt(H, W, C)) return 2;
   const int tcq = dw_tile_tcq(H, W, C, dt);
-  if (tcq && dw_os_on(dt)) return 3;
+  if (tcq && dw_os_on(B, H, W, C, dt, false)) return 3;
   return tcq ? 1 : 0;
 }
 
-extern "C" int accunet_dw3x3_rows(int B, int H, int W, int C, int dt) {
+extern "C" int accunet_dw3x3_rows(int B, int H, int W, int C, int dt, int bnb) {
   dim3 grid;
   if (const int nt = dw_span_nt(H, W, C)) {
     dw_sgeom(B, H, W, C, nt, &grid);
     return (int)grid.x;
   }
   int tcq = dw_tile_tcq(H, W, C, dt);
-  if (tcq && dw_os_on(dt)) {
+  if (tcq && dw_os_on(B, H, W, C, dt, bnb != 0)) {
     const DwOGeom og = dw_ogeom(B, H, W, C, tcq, &grid);
     return B * og.tilesH * og.tilesW;
   }
@@ -1603,7 +1610,7 @@ extern "C" int accunet_dw3x3_fwd(const void* x, const float* wt, const float* bi
     return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
   }
   int tcq = dw_tile_tcq(H, W, C, dt);
-  if (tcq && dw_os_on(dt)) {
+  if (tcq && dw_os_on(B, H, W, C, dt, bz != nullptr)) {
     DwOGeom og = dw_ogeom(B, H, W, C, tcq, &grid);
     // non-temporal loads only for inputs above the Infinity Cache and whole-line segments
     const int seg = tcq * 4 * (dt == ACC_BF16 ? 2 : 4);

@@ -166,14 +166,16 @@ int accunet_reduce_stats(const double* part, int R, int C, double* out2C, double
  * `stats` then receives the BatchNorm-backward partials (sum g, sum g*(bz - mean)),
  * g = out * act'(bz*scale + shift), for accunet_bn_bwd_part. wgrad writes dW [C][1][3][3] and db [C].
  * ------------------------------------------------------------------------- */
-/* rows of `stats` ([rows][2][C] fp64) the forward writes for this shape and storage
- * dtype dt (bf16 runs 64-channel tiles where C % 64 == 0). */
-int accunet_dw3x3_rows(int B, int H, int W, int C, int dt);
+/* rows of `stats` ([rows][2][C] fp64) accunet_dw3x3_fwd writes for this shape and
+ * storage dtype dt (bf16 runs 64-channel tiles where C % 64 == 0): the forward's norm2
+ * partials (bnb = 0) or the BN-backward data gradient's (bnb = 1, bz given); the two
+ * launch kinds may run different tile kernels. */
+int accunet_dw3x3_rows(int B, int H, int W, int C, int dt, int bnb);
 /* Which forward kernel runs for the shape and storage dtype dt (without bz): 3 = one-shot
- * 8-row tiles (C % 32 == 0), 1 = the LDS strip kernel (the same shapes with
- * ACCUNET_DW_OS=0), 0 = register-window kernel; 2 = whole-pixel span kernel, only with
- * the tuning knob ACCUNET_DW_SPAN bit 2 set (off by default) and then for C % 8 == 0,
- * C/4 <= 64. */
+ * 8-row tiles (fp32, C % 32 == 0, inputs above 256 MB), 1 = the LDS strip kernel (the
+ * other C % 32 == 0 shapes), 0 = register-window kernel; 2 = whole-pixel span kernel,
+ * only with the tuning knob ACCUNET_DW_SPAN bit 2 set (off by default) and then for
+ * C % 8 == 0, C/4 <= 64. */
 int accunet_dw3x3_variant(int B, int H, int W, int C, int dt);
 int accunet_dw3x3_fwd(const void* x, const float* wt, const float* bias, const float* sc,
                       const float* sh, int act, int flip, void* z, double* stats, int B, int H,

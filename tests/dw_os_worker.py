@@ -14,6 +14,8 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
 from accunet import _lib, kern  # noqa: E402
 
 SHAPES = [(2, 16, 64, 96), (1, 13, 35, 96), (2, 9, 21, 192), (2, 16, 16, 128), (1, 24, 40, 64)]
+if os.environ.get("DW_WORKER_K1"):  # the north-star K1 shape (402 MB fp32: one-shot by default)
+    SHAPES = [(16, 256, 256, 96)]
 
 
 def main(out_path):
@@ -22,7 +24,8 @@ def main(out_path):
     res = {"variant": torch.tensor(lib.accunet_dw3x3_variant(2, 16, 64, 96, 0)),
            "variant_bf16": torch.tensor(lib.accunet_dw3x3_variant(2, 16, 64, 96, 1))}
     for (B, H, W, C) in SHAPES:
-        for dt in (torch.float32, torch.bfloat16):
+        for dt in ((torch.float32,) if os.environ.get("DW_WORKER_K1") else
+                   (torch.float32, torch.bfloat16)):
             g = torch.Generator().manual_seed(B * 100 + H * 7 + C)
             x = torch.randn(B, H, W, C, generator=g).to(dev, dt)
             bz = torch.randn(B, H, W, C, generator=g).to(dev, dt)
@@ -37,12 +40,13 @@ def main(out_path):
             bst[3] = sh
             rows = kern.dw3x3_rows(B, H, W, C, x)
             st = torch.zeros(rows, 2, C, dtype=torch.float64, device=dev)
+            rows_b = kern.dw3x3_rows(B, H, W, C, x, bnb=True)
             z = torch.empty_like(x)
             kern.dw3x3_fwd(x, wt, bias, sc, sh, 1, 0, z, st, B, H, W, C)
             zf = torch.empty_like(x)
             kern.dw3x3_fwd(x, wt, None, None, None, 0, 1, zf, None, B, H, W, C)
             zb = torch.empty_like(x)
-            sb = torch.zeros(rows, 2, C, dtype=torch.float64, device=dev)
+            sb = torch.zeros(rows_b, 2, C, dtype=torch.float64, device=dev)
             kern.dw3x3_fwd(x, wt, None, None, None, 0, 1, zb, sb, B, H, W, C, bnb=(bz, bst, 1))
             torch.cuda.synchronize()
             tag = f"{'f32' if dt == torch.float32 else 'bf16'}_{B}x{H}x{W}x{C}"

@@ -299,19 +299,23 @@ def test_abi_host_side_contract_without_a_device():
     # rows (the strip kernel, ACCUNET_DW_OS=0: 32-row strips, 1024); cnv11's 9 channels
     # the register kernel
     os_knob = os.environ.get("ACCUNET_DW_OS", "1")
-    os_on, os_bf = os_knob != "0", os_knob == "2"  # one-shot tiles for fp32 / for bf16 too
+    # one-shot tiles (8 rows x 32 pixels -> 16 * 32 * 8 = 4096 rows) for the fp32 forward
+    # above 256 MB by default, for every tile launch with ACCUNET_DW_OS=2; else 32-row
+    # strips (1024 rows)
+    os_on, os_all = os_knob != "0", os_knob == "2"
     assert lib.accunet_dw3x3_variant(16, 256, 256, 96, 0) == (3 if os_on else 1)
-    assert lib.accunet_dw3x3_variant(16, 256, 256, 96, 1) == (3 if os_bf else 1)
-    assert lib.accunet_dw3x3_rows(16, 256, 256, 96, 0) == (4096 if os_on else 1024)
+    assert lib.accunet_dw3x3_variant(16, 256, 256, 96, 1) == (3 if os_all else 1)
+    assert lib.accunet_dw3x3_rows(16, 256, 256, 96, 0, 0) == (4096 if os_on else 1024)
+    # the BN-backward data gradient of the same shape: strips unless ACCUNET_DW_OS=2
+    assert lib.accunet_dw3x3_rows(16, 256, 256, 96, 0, 1) == (4096 if os_all else 1024)
+    # 16 x 128^2 x 192 fp32 (201 MB, cached): strips by default
+    assert lib.accunet_dw3x3_variant(16, 128, 128, 192, 0) == (3 if os_all else 1)
     # bf16 (dt 1) runs 64-channel tiles where C % 64 == 0: 16-pixel tiles, twice the rows
     # of the same kernel's 32-pixel fp32 tiles
-    r32, r16 = (lib.accunet_dw3x3_rows(16, 128, 128, 192, d) for d in (0, 1))
-    if os_on == os_bf:
-        assert r32 * 2 == r16
-    if os_on:  # one-shot tiles: 8 rows x 32 pixels (fp32)
-        assert r32 == 16 * (128 // 8) * (128 // 32)
-    assert lib.accunet_dw3x3_rows(16, 256, 256, 96, 1) == (4096 if os_bf else 1024)
-    assert lib.accunet_dw3x3_variant(16, 64, 64, 4352, 1) == (3 if os_bf else 1)
+    r32, r16 = (lib.accunet_dw3x3_rows(16, 128, 128, 192, d, 0) for d in (0, 1))
+    assert r32 * 2 == r16
+    assert lib.accunet_dw3x3_rows(16, 256, 256, 96, 1, 0) == (4096 if os_all else 1024)
+    assert lib.accunet_dw3x3_variant(16, 64, 64, 4352, 1) == (3 if os_all else 1)
     assert lib.accunet_dw3x3_variant(16, 256, 256, 9, 0) == 0
 
 

@@ -97,39 +97,58 @@ def test_dw3x3_fwd_stats_wgrad_vs_fp64(B, H, W, C, pro):
     assert (db.double().cpu() - gb).abs().max().item() <= 1e-5 * gb.abs().max().item() + 1e-5
 
 
-@pytest.mark.parametrize("setting", ["1", "2"])
-def test_dw3x3_one_shot_matches_strip_bitwise(tmp_path, setting):
-    """The one-shot tile kernel and the strip kernel sum every output in the same order
-    (bias, then the taps row-major), so forward z, the flipped-kernel data gradient and
-    the BatchNorm-backward data gradient are bit-identical, and their statistics totals
-    (the partial rows are cut differently: one per 8-row tile vs one per 32-row strip)
-    agree to summation order. ACCUNET_DW_OS=1 (the default: one-shot tiles for fp32,
-    the strip for bf16) and 2 (one-shot tiles for both) against 0 (the strip for both),
-    fp32 and bf16, each in a child process (the knob is read once per process;
-    tests/dw_os_worker.py)."""
-    import subprocess
-    outs = {}
-    for v in (setting, "0"):
-        env = dict(os.environ, ACCUNET_DW_OS=v)
-        path = tmp_path / f"dw_{v}.pt"
-        subprocess.run([sys.executable, os.path.join(HERE, "dw_os_worker.py"), str(path)], env=env,
-                       check=True, timeout=240)
-        outs[v] = torch.load(path, weights_only=True)
-    assert int(outs[setting].pop("variant")) == 3 and int(outs["0"].pop("variant")) == 1
-    assert int(outs[setting].pop("variant_bf16")) == (3 if setting == "2" else 1)
-    outs["0"].pop("variant_bf16")
-    for k in outs[setting]:
-        a, b = outs[setting][k], outs["0"][k]
+def _dw_compare(outs, a_key, b_key):
+    for k in outs[a_key]:
+        a, b = outs[a_key][k], outs[b_key][k]
         if k.endswith("_sb"):  # BN-backward partials: fp64 per element in both kernels
             assert torch.allclose(a, b, rtol=1e-9, atol=1e-9 * float(b.abs().max())), k
         elif k.endswith("_st"):  # (sum z, sum z^2): fp32 over 4-row chunks vs 8-row tiles
             C = a.shape[-1]
-            zabs = outs["0"][k[:-3] + "_z"].double().abs().reshape(-1, C).sum(0)
-            assert torch.allclose(a[0], b[0], rtol=1e-6, atol=0) or \
-                bool(((a[0] - b[0]).abs() <= 1e-6 * zabs).all()), k
+            zabs = outs[b_key][k[:-3] + "_z"].double().abs().reshape(-1, C).sum(0)
+            assert bool(((a[0] - b[0]).abs() <= 1e-6 * zabs).all()), k
             assert torch.allclose(a[1], b[1], rtol=1e-6), k
         else:
             assert torch.equal(a, b), (k, float((a - b).abs().max()))
+
+
+def _dw_runs(tmp_path, settings, extra_env=None):
+    import subprocess
+    outs = {}
+    for v in settings:
+        env = dict(os.environ, ACCUNET_DW_OS=v, **(extra_env or {}))
+        path = tmp_path / f"dw_{v}.pt"
+        subprocess.run([sys.executable, os.path.join(HERE, "dw_os_worker.py"), str(path)], env=env,
+                       check=True, timeout=240)
+        outs[v] = torch.load(path, weights_only=True)
+    return outs
+
+
+def test_dw3x3_one_shot_k1_shape_matches_strip(tmp_path):
+    """The default kernel choice at the north-star K1 shape (16 x 256^2 x 96 fp32, 402 MB:
+    one-shot tiles for the forward and the plain data gradient, the strip for the
+    BN-backward data gradient) against the strip everywhere (ACCUNET_DW_OS=0): z and
+    both data gradients bit for bit, statistics totals to summation order."""
+    outs = _dw_runs(tmp_path, ("1", "0"), {"DW_WORKER_K1": "1"})
+    assert int(outs["1"].pop("variant")) == 1  # (the worker's 2 x 16 x 64 probe shape)
+    outs["0"].pop("variant")
+    outs["1"].pop("variant_bf16")
+    outs["0"].pop("variant_bf16")
+    _dw_compare(outs, "1", "0")
+
+
+def test_dw3x3_one_shot_matches_strip_bitwise(tmp_path):
+    """The one-shot tile kernel and the strip kernel sum every output in the same order
+    (bias, then the taps row-major), so forward z, the flipped-kernel data gradient and
+    the BatchNorm-backward data gradient are bit-identical, and their statistics totals
+    (the partial rows are cut differently: one per 8-row tile vs one per 32-row strip)
+    agree to summation order. ACCUNET_DW_OS=2 (one-shot tiles for every tile shape,
+    dtype and launch kind) against 0 (the strip everywhere) on ragged and channel-group
+    shapes, fp32 and bf16, each in a child process (the knob is read once per process;
+    tests/dw_os_worker.py)."""
+    outs = _dw_runs(tmp_path, ("2", "0"))
+    assert int(outs["2"].pop("variant")) == 3 and int(outs["0"].pop("variant")) == 1
+    assert int(outs["2"].pop("variant_bf16")) == 3 and int(outs["0"].pop("variant_bf16")) == 1
+    _dw_compare(outs, "2", "0")
 
 
 @pytest.mark.parametrize("B,H,W,C", [(2, 16, 64, 96), (1, 13, 35, 96), (2, 24, 40, 192),

@@ -34,7 +34,7 @@ int main() {
   long sink = 0;
   for (auto& s : shapes) {
     for (int dt = 0; dt < 2; ++dt) {
-      const int r = accunet_dw3x3_rows(s[0], s[1], s[2], s[3], dt);
+      const int r = accunet_dw3x3_rows(s[0], s[1], s[2], s[3], dt, dt);
       EXPECT(r > 0);
       sink += r;
       sink += (long)accunet_dw3x3_wgrad_ws(s[0], s[1], s[2], s[3], dt);

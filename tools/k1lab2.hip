@@ -422,7 +422,7 @@ int main(int argc, char** argv) {
   hipLaunchKernelGGL(fill, dim3(1), dim3(256), 0, 0, bi, (long)C, 3u, -0.1f, 0.2f);
   hipLaunchKernelGGL(fill, dim3(1), dim3(256), 0, 0, sc, (long)C, 5u, 0.5f, 1.f);
   hipLaunchKernelGGL(fill, dim3(1), dim3(256), 0, 0, sh, (long)C, 9u, -0.2f, 0.4f);
-  const int rows = accunet_dw3x3_rows(B, H, W, C, ACC_F32);
+  const int rows = accunet_dw3x3_rows(B, H, W, C, ACC_F32, 0);
   double *st, *str;
   const int st_cap = std::max(rows, 8 * NT);  // rows of the largest grid (R = 4 tiles)
   CK(hipMalloc(&st, (size_t)st_cap * 2 * C * 8));

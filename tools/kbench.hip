@@ -112,7 +112,9 @@ int main(int argc, char** argv) {
     size_t n = (size_t)B * H * W * C;
     float *x = dalloc(n), *z = dalloc(n), *wt = dalloc(9 * C, 0.3f), *bi = dalloc(C, 0.1f);
     float *sc = dalloc(C, 1.f), *sh = dalloc(C, 0.1f);
-    int rows = accunet_dw3x3_rows(B, H, W, C, ACC_F32);  // (C = 96: the bf16 rows are the same)
+    // (forward and BN-backward partials, fp32 and bf16: the largest)
+    int rows = std::max(std::max(accunet_dw3x3_rows(B, H, W, C, ACC_F32, 0), accunet_dw3x3_rows(B, H, W, C, ACC_F32, 1)),
+                        std::max(accunet_dw3x3_rows(B, H, W, C, ACC_BF16, 0), accunet_dw3x3_rows(B, H, W, C, ACC_BF16, 1)));
     double* st;
     CK(hipMalloc(&st, (size_t)rows * 2 * C * sizeof(double)));
     double bytes = 2.0 * 4 * n;
@@ -150,7 +152,7 @@ int main(int argc, char** argv) {
            bytes / 2);
     {  // cnv91 forward in the bf16 mode: 16x256x256x192 bf16 = the same buffers' bytes
       const int C2 = 2 * C;
-      int rows2 = accunet_dw3x3_rows(B, H, W, C2, ACC_BF16);
+      int rows2 = accunet_dw3x3_rows(B, H, W, C2, ACC_BF16, 0);
       double* st2;
       CK(hipMalloc(&st2, (size_t)rows2 * 2 * C2 * sizeof(double)));
       float *wt2 = dalloc(9 * C2, 0.3f), *bi2 = dalloc(C2, 0.1f), *sc2 = dalloc(C2, 1.f),
@@ -194,7 +196,7 @@ int main(int argc, char** argv) {
       size_t n = (size_t)B * H * W * C;
       float *x = dalloc(n), *z = dalloc(n), *wt = dalloc(9 * C, 0.3f), *bi = dalloc(C, 0.1f);
       float *sc = dalloc(C, 1.f), *sh = dalloc(C, 0.1f);
-      int rows = accunet_dw3x3_rows(B, H, W, C, ACC_F32);
+      int rows = accunet_dw3x3_rows(B, H, W, C, ACC_F32, 0);
       double* st;
       CK(hipMalloc(&st, (size_t)rows * 2 * C * sizeof(double)));
       char name[96];
