@@ -14,7 +14,9 @@ if [ -z "${SKIP_TESTS:-}" ]; then
 fi
 timeout -k 10 400 python bench.py > gpurun_out/bench_full.log 2>&1
 grep '^{"metric' gpurun_out/bench_full.log | cut -c1-300
-timeout -k 10 300 python bench.py --dtype bf16 --no-cpu-baseline > gpurun_out/bench_bf16.log 2>&1
+timeout -k 10 400 python bench.py --dp-path --no-cpu-baseline --no-parity > gpurun_out/bench_dp32.log 2>&1
+grep '^{"metric' gpurun_out/bench_dp32.log | grep -o '"dp_path": {[^}]*}'
+timeout -k 10 300 python bench.py --dtype bf16 --no-cpu-baseline --dp-path > gpurun_out/bench_bf16.log 2>&1
 grep '^{"metric' gpurun_out/bench_bf16.log | cut -c1-300
 timeout -k 10 300 python bench.py --model unext > gpurun_out/bench_unext.log 2>&1
 grep '^{"metric' gpurun_out/bench_unext.log | cut -c1-200
@@ -36,6 +38,11 @@ python tools/save_profiles.py --shrink-pmc gpurun_out/pmc_fetch gpurun_out/pmc_w
 echo "pmc done"
 timeout -k 10 120 tools/kbench 20 > gpurun_out/kbench.txt 2>&1
 echo "kbench done"
+# K1 instruction-level PMC beside the lab structures, and a single-stream trace of the
+# step (split-K reduce census, depthwise per-grid table: no cross-stream stretch)
+timeout -k 10 600 bash tools/pmc_k1.sh > gpurun_out/pmc_k1.log 2>&1
+KGRID="splitk dw3x3" VARIANTS="ss:-" timeout -k 10 600 bash tools/prof_ab.sh > gpurun_out/prof_ss.log 2>&1
+echo "pmc_k1 / single-stream trace done"
 if [ -n "${PMC_GEMM:-}" ]; then
   # GEMM census of one step and the PMC passes of the ResPath 3x3 (halo kernels) and the
   # pyramid data gradient at the final sources

@@ -204,6 +204,7 @@ def main():
     os.makedirs(PROF, exist_ok=True)
     # bench lines
     for log, name in (("bench_full.log", f"{r}_bench_line.json"), ("bench_bf16.log", f"{r}_bench_line_bf16.json"),
+                      ("bench_dp32.log", f"{r}_bench_line_dp32.json"),
                       ("bench_unext.log", f"{r}_unext_bench_line.json"),
                       ("bench_w512.log", f"{r}_bench_line_w512.json")):
         p = os.path.join(OUT, log)
@@ -279,6 +280,18 @@ def main():
                f"native libraries mapped by the test process: {', '.join(d['native_so_loaded'])}\n"
                f"pytest summary: {tail}\n")
         open(os.path.join(PROF, f"{r}_gputests.txt"), "w").write(txt)
+    # K1 instruction-level PMC beside the lab structures (tools/pmc_k1.sh) and the
+    # single-stream trace's split-K census / depthwise per-grid table (tools/prof_ab.sh)
+    rep = os.path.join(OUT, "pmc_k1", "report.txt")
+    if os.path.exists(rep):
+        open(os.path.join(PROF, f"{r}_pmc_k1_insts.txt"), "w").write(
+            f"# tools/pmc_k1.sh + tools/pmc_k1_report.py ({st})\n" + open(rep).read())
+    parts = [os.path.join(OUT, f) for f in ("splitk_ss.txt", "kgrid_ss_splitk.txt", "kgrid_ss_dw3x3.txt",
+                                             "step_ss.txt")]
+    if all(os.path.exists(f) for f in parts[:1]):
+        open(os.path.join(PROF, f"{r}_single_stream.txt"), "w").write(
+            f"# single-stream step trace (ACCUNET_WGRAD_STREAM=0, tools/prof_ab.sh; {st})\n" +
+            "\n".join(open(f).read() for f in parts if os.path.exists(f)))
     kb = os.path.join(OUT, "kbench.txt")
     if os.path.exists(kb):
         open(os.path.join(PROF, f"{r}_kbench.txt"), "w").write(f"# tools/kbench 20 ({st})\n" + open(kb).read())
