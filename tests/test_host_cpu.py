@@ -78,6 +78,35 @@ def test_lr_schedule_matches_reference():
     np.testing.assert_allclose(lrs, g["lrs"], rtol=1e-12)
 
 
+def test_adam_step_counter_host_logic(monkeypatch):
+    # host side only: the launch is stubbed, the step counter bookkeeping is real
+    from accunet import optim
+    calls = []
+    monkeypatch.setattr(optim.kern, "adam_step", lambda *a: calls.append(a[-1]))
+    ps = [torch.nn.Parameter(torch.zeros(3)) for _ in range(4)]
+    for p in ps:
+        p.grad = torch.zeros(3)
+    opt = optim.FusedAdam(ps, lr=1e-3)
+    monkeypatch.setattr(opt, "_table", lambda gi, params: (None, None, None, 0))
+    for _ in range(3):
+        opt.step()
+    assert calls == [1, 2, 3]
+    assert all(float(opt.state[p]["step"]) == 3.0 for p in ps)
+    # a checkpoint round trip (separate step tensors after load) keeps counting
+    sd = opt.state_dict()
+    opt2 = optim.FusedAdam(ps, lr=1e-3)
+    opt2.load_state_dict(sd)
+    for p in ps:
+        opt2.state[p]["step"] = torch.tensor(float(opt2.state[p]["step"]))
+    monkeypatch.setattr(opt2, "_table", lambda gi, params: (None, None, None, 0))
+    opt2.step()
+    assert calls[-1] == 4 and float(opt2.state[ps[0]]["step"]) == 4.0
+    # mismatched counters are refused, as before
+    opt2.state[ps[1]]["step"] = torch.tensor(9.0)
+    with pytest.raises(RuntimeError):
+        opt2.step()
+
+
 def test_host_tensors_fail_loudly():
     # no CPU fallback: a host tensor reaching a kernel wrapper raises
     a = torch.zeros(4, 4)
