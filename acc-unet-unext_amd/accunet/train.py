@@ -70,7 +70,13 @@ class _GraphBuckets:
 
     def __init__(self, params, bucket_mb, device, comm_dtype=None):
         self.params = params
-        total = sum(p.numel() for p in params)
+        # each view starts at a multiple of 4 elements, so the packing copies move whole
+        # 16-byte (fp32) / 8-byte (bf16) quads; the pads stay zero
+        offs, o = [], 0
+        for p in params:
+            offs.append(o)
+            o += -(-p.numel() // 4) * 4
+        total = max(o, 1)
         self.flat = torch.zeros(total, dtype=torch.float32, device=device)
         # comm_dtype bf16: the buckets travel as bf16 (half the bytes over xGMI; the
         # gradients are rounded once when packed, RCCL sums in bf16) and are widened back
@@ -78,12 +84,10 @@ class _GraphBuckets:
         self.comm_dtype = comm_dtype
         self.wire = (torch.zeros(total, dtype=comm_dtype, device=device)
                      if comm_dtype not in (None, torch.float32) else self.flat)
-        self.views, self.wviews, offs, o = [], [], [], 0
-        for p in params:
-            offs.append(o)
+        self.views, self.wviews = [], []
+        for p, o in zip(params, offs):
             self.views.append(self.flat[o:o + p.numel()].view_as(p))
             self.wviews.append(self.wire[o:o + p.numel()].view_as(p))
-            o += p.numel()
         self.buckets = cut_buckets([p.numel() for p in params], bucket_mb)
         self.range = [(min(offs[i] for i in b), max(offs[i] + params[i].numel() for i in b))
                       for b in self.buckets]

@@ -70,7 +70,9 @@ ACC_DEV void ordered_strided_sum(T (&s)[N], int r, int r1, int st, L load) {
   }
 }
 
-ACC_DEV float lrelu(float x) { return x > 0.f ? x : x * LRELU_SLOPE; }
+// LeakyReLU as max(x, slope*x): bit-identical to x > 0 ? x : slope*x for 0 < slope < 1
+// (signed zeros and infinities included), 2 VALU ops (v_mul + v_max) instead of 3
+ACC_DEV float lrelu(float x) { return __builtin_fmaxf(x, x * LRELU_SLOPE); }
 // torch LeakyReLU backward: grad * (input > 0 ? 1 : slope)
 ACC_DEV float lrelu_d(float pre) { return pre > 0.f ? 1.f : LRELU_SLOPE; }
 
@@ -253,7 +255,9 @@ ACC_DEV float f4get(const float4& v, int i) {
 }
 
 
-ACC_DEV float apply_act(float v, int act) { return act == ACT_LRELU ? lrelu(v) : v; }
+// the activation as a slope (ACT_NONE: max(v, 1*v) = v), so a runtime act costs no select
+ACC_DEV float act_slope(int act) { return act == ACT_LRELU ? LRELU_SLOPE : 1.f; }
+ACC_DEV float apply_act(float v, int act) { return __builtin_fmaxf(v, v * act_slope(act)); }
 
 // Per-channel BatchNorm state block produced by bn_finalize:
 //   st[0*C + c] = mean, st[1*C + c] = rstd, st[2*C + c] = scale (= gamma*rstd),

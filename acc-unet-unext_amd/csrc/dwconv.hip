@@ -19,6 +19,40 @@
 
 #define DW_TR 8  // output rows per thread strip
 
+// The tile prologue a = act(x*scale + shift) of one channel quad on packed pairs
+// (v_pk_fma_f32 / v_pk_mul_f32), LeakyReLU as max(v, slope*v). Without a prologue it
+// is the identity bit for bit: scale 1, shift -0 (x + -0 = x for every x), slope 1.
+typedef float dwf2 __attribute__((ext_vector_type(2)));
+struct DwPro {
+  dwf2 s01, s23, t01, t23;
+  float sl;
+};
+ACC_DEV DwPro dw_pro(float4 ps, float4 pb, bool pro, int act) {
+  DwPro P;
+  if (!pro) {
+    ps = make_float4(1.f, 1.f, 1.f, 1.f);
+    pb = make_float4(-0.f, -0.f, -0.f, -0.f);
+  }
+  P.s01 = dwf2{ps.x, ps.y};
+  P.s23 = dwf2{ps.z, ps.w};
+  P.t01 = dwf2{pb.x, pb.y};
+  P.t23 = dwf2{pb.z, pb.w};
+  P.sl = pro ? act_slope(act) : 1.f;
+  return P;
+}
+ACC_DEV float4 dw_act(const DwPro& P, float4 a) {
+  dwf2 lo = {a.x, a.y}, hi = {a.z, a.w};
+  lo = lo * P.s01 + P.t01;
+  hi = hi * P.s23 + P.t23;
+  const dwf2 ml = lo * P.sl, mh = hi * P.sl;
+  return make_float4(__builtin_fmaxf(lo.x, ml.x), __builtin_fmaxf(lo.y, ml.y),
+                     __builtin_fmaxf(hi.x, mh.x), __builtin_fmaxf(hi.y, mh.y));
+}
+// component-wise keep-or-zero (a float4 ?: can be lowered through a scratch slot)
+ACC_DEV float4 dw_keep(bool in, float4 v) {
+  return make_float4(in ? v.x : 0.f, in ? v.y : 0.f, in ? v.z : 0.f, in ? v.w : 0.f);
+}
+
 template <int V>
 struct VecT;
 template <>
@@ -379,8 +413,7 @@ ACC_DEV void dw_fetch_rows(typename Raw16<TX>::type (&v)[NKK], __amdgpu_buffer_r
 // Activate (prologue BN+act, in-image elements only) and park fetched rows in the ring.
 template <int TCQ, int NKK, int QL, typename R>
 ACC_DEV void dw_park_rows(float4* __restrict__ ring, const R (&v)[NKK], const DwTGeom& g,
-                          int hA, int n, int w0, int hbeg, bool pro, const float4 (&ps)[QL],
-                          const float4 (&pb)[QL], int act) {
+                          int hA, int n, int w0, int hbeg, const DwPro (&P)[QL]) {
   typedef DwT<TCQ> G;
   const int tid = threadIdx.x;
 #pragma unroll
@@ -393,16 +426,8 @@ ACC_DEV void dw_park_rows(float4* __restrict__ ring, const R (&v)[NKK], const Dw
       const bool in = hh >= 0 && hh < g.H && ww >= 0 && ww < g.W;
       const int slot = (hh - hbeg + 1) % G::IR;
 #pragma unroll
-      for (int j = 0; j < QL; ++j) {
-        float4 a = r16q(v[k], j);
-        if (pro && in) {
-          a.x = apply_act(a.x * ps[j].x + pb[j].x, act);
-          a.y = apply_act(a.y * ps[j].y + pb[j].y, act);
-          a.z = apply_act(a.z * ps[j].z + pb[j].z, act);
-          a.w = apply_act(a.w * ps[j].w + pb[j].w, act);
-        }
-        ring[(slot * G::IP + p) * TCQ + q + j] = a;
-      }
+      for (int j = 0; j < QL; ++j)  // out-of-image quads loaded as zeros stay zero
+        ring[(slot * G::IP + p) * TCQ + q + j] = dw_keep(in, dw_act(P[j], r16q(v[k], j)));
     }
   }
 }
@@ -417,8 +442,10 @@ ACC_DEV void dw_fill_tile(float4* __restrict__ tile, const TX* __restrict__ x,
   constexpr int NL = (G::N4 / QL + 255) / 256;  // 16-byte loads per thread
   const int tid = threadIdx.x;
   float4 ps[QL], pb[QL];
-  const bool pro = sc != nullptr;
   dw_stage_pro<TCQ, QL>(sc, sh, c0, ps, pb);
+  DwPro P[QL];
+#pragma unroll
+  for (int j = 0; j < QL; ++j) P[j] = dw_pro(ps[j], pb[j], sc != nullptr, act);
   // raw, unconditional loads (out-of-image quads read the image origin and are zeroed
   // at the LDS write): all NL in flight together, bf16 widened only when parked
   typedef typename Raw16<TX>::type RawL;
@@ -438,16 +465,7 @@ ACC_DEV void dw_fill_tile(float4* __restrict__ tile, const TX* __restrict__ x,
     const int i = (tid + 256 * k) * QL;
     if (i < G::N4) {
 #pragma unroll
-      for (int j = 0; j < QL; ++j) {
-        float4 a = r16q(v[k], j);
-        if (pro) {
-          a.x = apply_act(a.x * ps[j].x + pb[j].x, act);
-          a.y = apply_act(a.y * ps[j].y + pb[j].y, act);
-          a.z = apply_act(a.z * ps[j].z + pb[j].z, act);
-          a.w = apply_act(a.w * ps[j].w + pb[j].w, act);
-        }
-        tile[i + j] = in[k] ? a : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
+      for (int j = 0; j < QL; ++j) tile[i + j] = dw_keep(in[k], dw_act(P[j], r16q(v[k], j)));
     }
   }
 }
@@ -502,13 +520,17 @@ dw3x3_tile_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
   const __amdgpu_buffer_rsrc_t rx = acc_rsrc(x + img, ibytes);
   const __amdgpu_buffer_rsrc_t rz = acc_rsrc(z + img, ibytes);
   const __amdgpu_buffer_rsrc_t rb = acc_rsrc(BNB ? bz + img : x + img, BNB ? ibytes : 0u);
-  const bool pro = sc != nullptr;
-  float4 ps[QL], pb[QL];
-  dw_stage_pro<TCQ, QL>(sc, sh, c0, ps, pb);
+  DwPro P[QL];
+  {
+    float4 ps[QL], pb[QL];
+    dw_stage_pro<TCQ, QL>(sc, sh, c0, ps, pb);
+#pragma unroll
+    for (int j = 0; j < QL; ++j) P[j] = dw_pro(ps[j], pb[j], sc != nullptr, act);
+  }
   {
     RawL v[NL];
     dw_fetch_rows<TCQ, NL, AUX, T>(v, rx, g, hbeg - 1, G::N4, w0, c0);
-    dw_park_rows<TCQ, NL, QL>(tile, v, g, hbeg - 1, G::N4, w0, hbeg, pro, ps, pb, act);
+    dw_park_rows<TCQ, NL, QL>(tile, v, g, hbeg - 1, G::N4, w0, hbeg, P);
   }
   // the quad's 4 channels x 9 taps are 36 contiguous floats of wt ([C][9], 16-B aligned
   // since c % 4 == 0): 9 float4 loads instead of 36 scalar ones
@@ -630,7 +652,7 @@ dw3x3_tile_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
     }
     if (more) {
       __syncthreads();  // every thread is done with rows r0-1 .. r0+CR-2
-      dw_park_rows<TCQ, NL8, QL>(tile, nx, g, r0 + 9, G::N8, w0, hbeg, pro, ps, pb, act);
+      dw_park_rows<TCQ, NL8, QL>(tile, nx, g, r0 + 9, G::N8, w0, hbeg, P);
       __syncthreads();
     }
     if (BNB) {
@@ -771,33 +793,40 @@ dw3x3_os_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
     hv[m] = bufq_ld<AUX>(rx, in ? (unsigned)(((hi * g.W + hw) * g.C + c0 + 4 * hq) * (int)sizeof(T))
                                 : ACC_OOB, (const T*)nullptr);
   }
-  auto activate = [&](float4 a, float4 s4, float4 t4) {
-    if (pro) {
-      a.x = apply_act(a.x * s4.x + t4.x, act);
-      a.y = apply_act(a.y * s4.y + t4.y, act);
-      a.z = apply_act(a.z * s4.z + t4.z, act);
-      a.w = apply_act(a.w * s4.w + t4.w, act);
-    }
-    return a;
-  };
+  typedef dwf2 f2v;
+  const DwPro P = dw_pro(ps, pb, pro, act);
+  auto activate = [&](float4 a) { return dw_act(P, a); };
+  auto keep = dw_keep;
+  // interior tile (block-uniform): every input row and pixel of the tile is inside the
+  // image and every output row is stored, so no per-element masking
+  const bool interior = h0 >= 1 && h0 + R + 1 <= g.H && w0 + TP <= g.W;
   float a0[4] = {0.f, 0.f, 0.f, 0.f}, a1[4] = {0.f, 0.f, 0.f, 0.f};
-  float c1[4] = {0.f, 0.f, 0.f, 0.f}, c2[4] = {0.f, 0.f, 0.f, 0.f};
+  f2v c1[2] = {{0.f, 0.f}, {0.f, 0.f}}, c2[2] = {{0.f, 0.f}, {0.f, 0.f}};
   double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
   float4 cen[IR];
+  if (interior) {
 #pragma unroll
-  for (int r = 0; r < IR; ++r) {
-    const int i = h0 - 1 + r;
-    const bool in = win && i >= 0 && i < g.H;
-    cen[r] = in ? activate(q2f(own[r]), ps, pb) : make_float4(0.f, 0.f, 0.f, 0.f);
-    xb[r][p + 1][q] = cen[r];
+    for (int r = 0; r < IR; ++r) {
+      cen[r] = activate(q2f(own[r]));
+      xb[r][p + 1][q] = cen[r];
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < IR; ++r) {
+      const int i = h0 - 1 + r;
+      const bool in = win && i >= 0 && i < g.H;
+      cen[r] = keep(in, activate(q2f(own[r])));
+      xb[r][p + 1][q] = cen[r];
+    }
   }
 #pragma unroll
   for (int m = 0; m < NH; ++m) {
     int hr, hs, hq, hw, hi;
     const bool in = halo(m, hr, hs, hq, hw, hi);
     // (256 % TCQ == 0: a halo lane's quad hq is its own quad q, so its prologue too)
-    if (tid + 256 * m < 2 * TCQ * IR)
-      xb[hr][hs ? IP - 1 : 0][hq] = in ? activate(q2f(hv[m]), ps, pb) : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (tid + 256 * m < 2 * TCQ * IR) {
+      xb[hr][hs ? IP - 1 : 0][hq] = keep(in, activate(q2f(hv[m])));
+    }
   }
   __syncthreads();
   if (BNB) {  // the pre-BN rows, issued once the raw tile has been consumed (registers)
@@ -809,51 +838,63 @@ dw3x3_os_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
                          (const T*)nullptr);
     }
   }
+  auto taps = [&](auto interior_c) {
+    constexpr bool IN = decltype(interior_c)::value;
 #pragma unroll
-  for (int r = 0; r < IR; ++r) {
-    const float4 L = xb[r][p][q], Rr = xb[r][p + 2][q];
-    const float vL[4] = {L.x, L.y, L.z, L.w};
-    const float vC[4] = {cen[r].x, cen[r].y, cen[r].z, cen[r].w};
-    const float vR[4] = {Rr.x, Rr.y, Rr.z, Rr.w};
-    const int h = h0 + r - 2;  // output row completed by input row h0 - 1 + r
-    const bool on = r >= 2 && win && h < g.H;
-    float o[4];
+    for (int r = 0; r < IR; ++r) {
+      const float4 L = xb[r][p][q], Rr = xb[r][p + 2][q];
+      const float vL[4] = {L.x, L.y, L.z, L.w};
+      const float vC[4] = {cen[r].x, cen[r].y, cen[r].z, cen[r].w};
+      const float vR[4] = {Rr.x, Rr.y, Rr.z, Rr.w};
+      const int h = h0 + r - 2;  // output row completed by input row h0 - 1 + r
+      const bool on = r >= 2 && (IN || (win && h < g.H));
+      float o[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float t0 = a0[j], t1 = a1[j], t2 = bi[j];
-      t0 = fmaf(k[6][j], vL[j], t0); t0 = fmaf(k[7][j], vC[j], t0); t0 = fmaf(k[8][j], vR[j], t0);
-      t1 = fmaf(k[3][j], vL[j], t1); t1 = fmaf(k[4][j], vC[j], t1); t1 = fmaf(k[5][j], vR[j], t1);
-      t2 = fmaf(k[0][j], vL[j], t2); t2 = fmaf(k[1][j], vC[j], t2); t2 = fmaf(k[2][j], vR[j], t2);
-      a0[j] = t1;
-      a1[j] = t2;
-      t0 = rnd<T>(t0);  // statistics of the stored value
-      o[j] = t0;
-      const float am = on ? t0 : 0.f;
+      for (int j = 0; j < 4; ++j) {
+        float t0 = a0[j], t1 = a1[j], t2 = bi[j];
+        t0 = fmaf(k[6][j], vL[j], t0); t0 = fmaf(k[7][j], vC[j], t0); t0 = fmaf(k[8][j], vR[j], t0);
+        t1 = fmaf(k[3][j], vL[j], t1); t1 = fmaf(k[4][j], vC[j], t1); t1 = fmaf(k[5][j], vR[j], t1);
+        t2 = fmaf(k[0][j], vL[j], t2); t2 = fmaf(k[1][j], vC[j], t2); t2 = fmaf(k[2][j], vR[j], t2);
+        a0[j] = t1;
+        a1[j] = t2;
+        o[j] = rnd<T>(t0);  // statistics of the stored value
+      }
+      if (r < 2) continue;
       if (BNB) {
-        if (r >= 2) {
-          const float zz = f4get(q2f(zb[r >= 2 ? r - 2 : 0]), j);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float am = on ? o[j] : 0.f;
+          const float zz = f4get(q2f(zb[r - 2]), j);
           float gg = am;
           if (bact == ACT_LRELU) gg *= lrelu_d(zz * bsc[j] + bsh[j]);
           s1[j] += gg;
           s2[j] += (double)gg * ((double)zz - bmu[j]);
         }
       } else {
-        c1[j] += am;
-        c2[j] = fmaf(am, am, c2[j]);
+        // fp32 per-thread sums on packed pairs (same adds and fmas as the scalar form)
+        f2v m01 = {o[0], o[1]}, m23 = {o[2], o[3]};
+        if (!IN) {
+          m01 = on ? m01 : f2v{0.f, 0.f};
+          m23 = on ? m23 : f2v{0.f, 0.f};
+        }
+        c1[0] += m01;
+        c1[1] += m23;
+        c2[0] = m01 * m01 + c2[0];
+        c2[1] = m23 * m23 + c2[1];
       }
-    }
-    if (r >= 2)
       bufq_st<2>(rz, on ? (unsigned)(((h * g.W + w) * g.C + c) * (int)sizeof(T)) : ACC_OOB,
                  make_float4(o[0], o[1], o[2], o[3]), (T*)nullptr);
-  }
+    }
+  };
+  if (!BNB && interior)  // (the BN-backward form keeps one copy: registers are tight)
+    taps(std::true_type{});
+  else
+    taps(std::false_type{});
   if (stats) {
     __syncthreads();  // the exchange tile is reused as the reduction buffer
     if (!BNB) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        s1[j] = (double)c1[j];
-        s2[j] = (double)c2[j];
-      }
+      s1[0] = (double)c1[0].x; s1[1] = (double)c1[0].y; s1[2] = (double)c1[1].x; s1[3] = (double)c1[1].y;
+      s2[0] = (double)c2[0].x; s2[1] = (double)c2[0].y; s2[2] = (double)c2[1].x; s2[3] = (double)c2[1].y;
     }
     double v[8] = {s1[0], s1[1], s1[2], s1[3], s2[0], s2[1], s2[2], s2[3]};
     if (block_slot_reduce<TCQ, 8, double>(v, reinterpret_cast<double*>(&xb[0][0][0]))) {
@@ -1047,22 +1088,16 @@ struct DwsFill {
     asm volatile("" : "+v"(tid));
     const int RW = (g.PX + 2) * g.CQ, NF = g.PX * g.CQ / QL;
     const int nunits = (R + 2) * RW / QL;
+    DwPro P[QL];
+#pragma unroll
+    for (int j = 0; j < QL; ++j) P[j] = dw_pro(ps[j], pb[j], pro, act);
 #pragma unroll
     for (int k = 0; k < DwS<NT>::NLMAX; ++k) {
       const int u = tid + NF * k;
       if (tid < NF && u < nunits) {
         const bool in = (inb >> k) & 1u;
 #pragma unroll
-        for (int j = 0; j < QL; ++j) {
-          float4 a = r16q(v[k], j);
-          if (pro) {
-            a.x = apply_act(a.x * ps[j].x + pb[j].x, act);
-            a.y = apply_act(a.y * ps[j].y + pb[j].y, act);
-            a.z = apply_act(a.z * ps[j].z + pb[j].z, act);
-            a.w = apply_act(a.w * ps[j].w + pb[j].w, act);
-          }
-          tile[u * QL + j] = in ? a : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
+        for (int j = 0; j < QL; ++j) tile[u * QL + j] = dw_keep(in, dw_act(P[j], r16q(v[k], j)));
       }
     }
   }

@@ -687,6 +687,26 @@ relayout_batch_kernel(const AccRelayout* __restrict__ items, int n) {
   }
   const AccRelayout& it = items[lo];
   const long base = ((long)(bid - it.blk0) * 256 + threadIdx.x) * RL_EPT;
+  static_assert(RL_EPT == 4, "the flat copies move one float4 per thread");
+  if (it.kind >= 3 && base + 3 < it.total) {
+    // flat copy, whole quad: one 16-byte load, one 16-byte (fp32) / 8-byte (bf16) store
+    // where both ends are aligned (the bucket views start at 4-element offsets)
+    const float* src = it.in + base;
+    const bool k3 = it.kind == 3;
+    const uintptr_t dst = k3 ? (uintptr_t)(it.out + base) : (uintptr_t)(reinterpret_cast<bf16_t*>(it.out) + base);
+    if ((((uintptr_t)src) & 15) == 0 && (dst & (k3 ? 15 : 7)) == 0) {
+      const float4 v = *reinterpret_cast<const float4*>(src);
+      if (k3) {
+        *reinterpret_cast<float4*>(dst) = v;
+      } else {
+        uint2 u;
+        u.x = (unsigned)f2bf(v.x) | ((unsigned)f2bf(v.y) << 16);
+        u.y = (unsigned)f2bf(v.z) | ((unsigned)f2bf(v.w) << 16);
+        *reinterpret_cast<uint2*>(dst) = u;
+      }
+      return;
+    }
+  }
 #pragma unroll
   for (int e = 0; e < RL_EPT; ++e) {
     const long i = base + e;

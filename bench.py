@@ -82,6 +82,9 @@ def parse():
     ap.add_argument("--no-probe", action="store_true", help="skip the roofline probes")
     ap.add_argument("--no-parity", action="store_true",
                     help="skip the same-run forward parity vs the CPU path (cpu_baseline.parity)")
+    ap.add_argument("--dp-world1", action="store_true",
+                    help="time the data-parallel step itself (world-1 RCCL group) as the main "
+                         "step, for kernel traces of the DP path; not a headline line")
     ap.add_argument("--dp-path", action="store_true",
                     help="N = 1 only: also time the data-parallel step (graph-mode event-gated "
                          "gradient buckets all-reduced by RCCL over a world-1 process group) "
@@ -422,7 +425,14 @@ def main():
     else:
         # configs[2]: bf16 activations AND bf16 gradient buckets over xGMI (--comm-dtype)
         wire = args.comm_dtype or ("bf16" if args.dtype == "bf16" else "fp32")
-        step = TrainStep(model, lr=1e-3, graph=True, precision=prec,
+        pg = None
+        if args.dp_world1:
+            if world > 1 or args.dp_path:
+                raise SystemExit("--dp-world1: N = 1, without --dp-path")
+            dist.init_process_group("nccl", rank=0, world_size=1,
+                                    init_method=f"tcp://127.0.0.1:{_free_port()}")
+            pg = dist.group.WORLD
+        step = TrainStep(model, lr=1e-3, graph=True, precision=prec, process_group=pg,
                          comm_dtype="bf16" if wire == "bf16" else None)
 
     g = torch.Generator(device="cpu").manual_seed(1000 + rank)
@@ -492,7 +502,7 @@ def main():
                              "ACC_UNet (16.77M)" if args.variant == "canonical" else args.variant),
                    "global_batch": B * world, "per_gpu_batch": B, "image": [3, S, S],
                    "parallelism": f"dp{world}",
-                   "grad_allreduce": (None if world == 1 or args.eager else
+                   "grad_allreduce": (None if (world == 1 and not args.dp_world1) or args.eager else
                                       args.comm_dtype or ("bf16" if args.dtype == "bf16"
                                                           else "fp32"))},
         "final_loss": float(loss.item()),

@@ -168,6 +168,13 @@ int main(int argc, char** argv) {
     report("K1 dw3x3_fwd flip (dgrad) no pro/stats",
            timeit([&] { CA(accunet_dw3x3_fwd(x, wt, nullptr, nullptr, nullptr, 0, 1, z, nullptr, B, H, W, C, nullptr, nullptr, 0, ACC_F32, 0)); }, iters),
            bytes);
+    // what K1's prologue and statistics cost, one at a time (same tile kernel)
+    report("K1 dw3x3_fwd pro, no stats",
+           timeit([&] { CA(accunet_dw3x3_fwd(x, wt, bi, sc, sh, 1, 0, z, nullptr, B, H, W, C, nullptr, nullptr, 0, ACC_F32, 0)); }, iters),
+           bytes);
+    report("K1 dw3x3_fwd stats, no pro",
+           timeit([&] { CA(accunet_dw3x3_fwd(x, wt, bi, nullptr, nullptr, 0, 0, z, st, B, H, W, C, nullptr, nullptr, 0, ACC_F32, 0)); }, iters),
+           bytes);
     {  // the BatchNorm-backward data gradient (flip, bz / bst, BN-backward partials):
        // reads dz and bz, writes dA -- 3 x B*H*W*C*4 bytes
       float *bz = dalloc(n), *bst = dalloc(4 * C, 1.f);

@@ -11,7 +11,7 @@ for v in $VARIANTS; do
   IFS=: read -r name lib envs <<< "$v"
   if [ "$lib" = "-" ]; then unset ACCUNET_LIB_OVERRIDE; else export ACCUNET_LIB_OVERRIDE=$PWD/$lib/libaccunet_hip.so; fi
   rm -rf gpurun_out/pa_$name
-  timeout -k 10 300 env ${envs//,/ } rocprofv3 --kernel-trace --output-format csv -d gpurun_out/pa_$name -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-probe --dtype ${DT:-fp32} > gpurun_out/pa_$name.log 2>&1
+  timeout -k 10 300 env ${envs//,/ } rocprofv3 --kernel-trace --output-format csv -d gpurun_out/pa_$name -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-probe --dtype ${DT:-fp32} ${BENCH_ARGS:-} > gpurun_out/pa_$name.log 2>&1
   python tools/step_profile.py gpurun_out/pa_$name --last 4 --top ${TOP:-60} > gpurun_out/step_$name.txt
   python tools/kstats.py gpurun_out/pa_$name --steps 7 --top 80 > gpurun_out/kstats_$name.txt
   python tools/splitk_census.py gpurun_out/pa_$name --steps 7 > gpurun_out/splitk_$name.txt
