@@ -890,12 +890,36 @@ dw3x3_os_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
     taps(std::true_type{});
   else
     taps(std::false_type{});
+  if (stats && !BNB) {
+    // forward statistics: the fp32 per-thread sums (R rows) are added over the wave's
+    // pixels in fp32 (shuffles), then over the 4 waves in fp64 through a small slab of
+    // its own -- no barrier before it, the exchange tile stays untouched (tools/k1lab2:
+    // 2-3 us of K1's 150 against the block reduction through the tile)
+    constexpr int WL = TCQ < 64 ? TCQ : 64;
+    __shared__ double sw[4][WL][8];
+    float f[8] = {c1[0].x, c1[0].y, c1[1].x, c1[1].y, c2[0].x, c2[0].y, c2[1].x, c2[1].y};
+#pragma unroll
+    for (int off = TCQ; off < 64; off <<= 1)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] += __shfl_xor(f[e], off);
+    const int lane = tid & 63, wave = tid >> 6;
+    if (lane < WL) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sw[wave][lane][e] = (double)f[e];
+    }
+    __syncthreads();
+    if (tid < TCQ) {  // (TCQ <= 64: every wave holds every quad)
+      const long row = (long)srow * 2 * g.C;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const double v = ((sw[0][tid][e] + sw[1][tid][e]) + sw[2][tid][e]) + sw[3][tid][e];
+        stats[row + (e >> 2) * g.C + c0 + 4 * tid + (e & 3)] = v;
+      }
+    }
+    return;
+  }
   if (stats) {
     __syncthreads();  // the exchange tile is reused as the reduction buffer
-    if (!BNB) {
-      s1[0] = (double)c1[0].x; s1[1] = (double)c1[0].y; s1[2] = (double)c1[1].x; s1[3] = (double)c1[1].y;
-      s2[0] = (double)c2[0].x; s2[1] = (double)c2[0].y; s2[2] = (double)c2[1].x; s2[3] = (double)c2[1].y;
-    }
     double v[8] = {s1[0], s1[1], s1[2], s1[3], s2[0], s2[1], s2[2], s2[3]};
     if (block_slot_reduce<TCQ, 8, double>(v, reinterpret_cast<double*>(&xb[0][0][0]))) {
       const long row = (long)srow * 2 * g.C;

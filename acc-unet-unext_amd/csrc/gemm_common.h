@@ -163,7 +163,9 @@ ACC_DEV void gemm_epilogue_generic(const GemmParams& p, floatx16 (&acc)[TM][TN],
   // rows per load chunk (more for the gather-heavy data-gradient epilogues)
   // (2-row chunks pay for the pyramid gathers of the 128-row tiles; the 64x64 small-K
   // tiles keep 1 for occupancy: tools/gemm_census.py)
-  constexpr int ECMAX = ((EPI & EPI_PYR) && TM == 2) ? 2 : (EPI & (EPI_PYR | EPI_BNB)) ? 1 : 2;
+  // (the BN-backward + pyramid form keeps 1: with 2 its 128x128 instance spills)
+  constexpr int ECMAX = ((EPI & EPI_PYR) && !(EPI & EPI_BNB) && TM == 2) ? 2
+                        : (EPI & (EPI_PYR | EPI_BNB)) ? 1 : 2;
   constexpr int EC = NR < ECMAX ? NR : ECMAX;
   static_assert(PR % RPP == 0, "pass rows must split evenly over the sweeps");
   static_assert(GEMM_THREADS % CQN == 0, "BN/4 must divide the block");
@@ -449,7 +451,12 @@ ACC_DEV void gemm_epilogue_vec(const GemmParams& p, floatx16 (&acc)[TM][TN], flo
   constexpr bool LOADS = (EPI & (EPI_BNB | EPI_PYR | EPI_UPS)) != 0;
   // rows per chunk; two chunks of operands in flight (the BN-backward + pyramid epilogue
   // gathers 6 operands per row: one row per chunk keeps it within 3 waves per SIMD)
-  constexpr int EC = ((EPI & EPI_PYR) && (EPI & EPI_BNB)) ? GEMM_PYR_EC : LOADS ? 2 : NR;
+  // pyramid data gradient (EPI_PYR): a thread's rows come in horizontal pixel pairs
+  // (w even, w + 1: tile rows 2k, 2k + 1, since m0 and W are even), which share their
+  // 2x2 and 4x4 windows, so each pair issues ONE set of pyramid gathers (6 loads)
+  // beside its two BN-backward rows
+  constexpr bool PAIR = (EPI & EPI_PYR) != 0;
+  constexpr int EC = PAIR ? 2 : ((EPI & EPI_PYR) && (EPI & EPI_BNB)) ? GEMM_PYR_EC : LOADS ? 2 : NR;
   constexpr int NCH = NR / EC;
   constexpr int NT = TM * NCH;        // chunks of the whole tile
   constexpr int SZ = (int)sizeof(TC);
@@ -516,10 +523,14 @@ ACC_DEV void gemm_epilogue_vec(const GemmParams& p, floatx16 (&acc)[TM][TN], flo
       bsh4[e] = p.bst[BN_SHIFT * N + n];
     }
   }
+  // tile row (of the pass's PR rows) of chunk t's row c
+  auto tile_row = [&](int t, int c) {
+    return PAIR ? 2 * (rr0 + (t % NCH) * RPP) + c : rr0 + ((t % NCH) * EC + c) * RPP;
+  };
   // rows of chunk t (pass t / NCH): C row and in-range flag of its row c
   auto row_of = [&](int t, int c, int& m) {
-    const int i = t / NCH, r = (t % NCH) * EC + c;
-    const int rr = rr0 + r * RPP;
+    const int i = t / NCH;
+    const int rr = tile_row(t, c);
     m = m0 + (rr >> 5) * TM * 32 + i * 32 + (rr & 31);
     return m < M && nq < N;
   };
@@ -533,7 +544,7 @@ ACC_DEV void gemm_epilogue_vec(const GemmParams& p, floatx16 (&acc)[TM][TN], flo
       if (EPI & (EPI_PYR | EPI_UPS)) {
         int b, h, w;
         gemm_pix(p, ok ? m : m0, b, h, w);
-        if (EPI & EPI_PYR) {
+        if ((EPI & EPI_PYR) && c == 0) {  // (PAIR: row c = 1 shares row 0's windows)
           const unsigned i2 = (unsigned)(gemm_pix_lg(p, b, h, w, 1) - q2a);
           const unsigned i4 = (unsigned)(gemm_pix_lg(p, b, h, w, 2) - q4a);
           const unsigned o2 = ok ? (i2 * 2 * N + nq) * SZ : ACC_OOB;
@@ -579,7 +590,7 @@ ACC_DEV void gemm_epilogue_vec(const GemmParams& p, floatx16 (&acc)[TM][TN], flo
     for (int c = 0; c < EC; ++c) {
       int m;
       const bool ok = row_of(t, c, m);
-      const int rr = rr0 + ((t % NCH) * EC + c) * RPP;
+      const int rr = tile_row(t, c);
       const float4 a4 = *reinterpret_cast<const float4*>(smem + rr * SC + 4 * cq);
       float v[4] = {a4.x + bq[0], a4.y + bq[1], a4.z + bq[2], a4.w + bq[3]};
       if ((EPI & EPI_PYR) && p.pd2) {
@@ -587,15 +598,16 @@ ACC_DEV void gemm_epilogue_vec(const GemmParams& p, floatx16 (&acc)[TM][TN], flo
           int b, h, w;
           gemm_pix(p, ok ? m : m0, b, h, w);
           const unsigned pos2 = (h & 1) * 2 + (w & 1), pos4 = (h & 3) * 4 + (w & 3);
-          const float4 av2 = q2f(R[c].av2), mx2 = q2f(R[c].mx2);
-          const float4 av4 = q2f(R[c].av4), mx4 = q2f(R[c].mx4);
+          const EpiRow<TC>& G = R[0];  // the pair's windows
+          const float4 av2 = q2f(G.av2), mx2 = q2f(G.mx2);
+          const float4 av4 = q2f(G.av4), mx4 = q2f(G.mx4);
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             float g = f4get(av2, e) * 0.25f;
-            if (((R[c].k2 >> (8 * e)) & 255u) == pos2) g += f4get(mx2, e);
+            if (((G.k2 >> (8 * e)) & 255u) == pos2) g += f4get(mx2, e);
             if (p.pd4) {
               g += f4get(av4, e) * (1.f / 16.f);
-              if (((R[c].k4 >> (8 * e)) & 255u) == pos4) g += f4get(mx4, e);
+              if (((G.k4 >> (8 * e)) & 255u) == pos4) g += f4get(mx4, e);
             }
             v[e] += g;
           }

@@ -231,7 +231,12 @@ ACC_DEV void dma16(const float* src, float4* lds_dst) {
                : "memory");
 }
 
-template <int R, bool DMA, int WPE, int PH = 1, bool FULL = false, int AUXL = 2, int AUXS = 2>
+// STM (statistics): 0 none, 1 fp32 per thread + fp64 block reduce through the exchange
+// tile (the product), 2 fp32 in-wave shuffles + fp64 across the 4 waves in a separate LDS
+// slab (no barrier before it), 3 per-thread sums only (lanes p == 0 write theirs: the
+// accumulation without the reduction), 4 fp64 in-wave shuffles, one partial row per wave
+template <int R, bool DMA, int WPE, int PH = 1, bool FULL = false, int AUXL = 2, int AUXS = 2,
+          int STM = 1>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 os(const float* __restrict__ x, const float* __restrict__ wt, const float* __restrict__ bias,
    const float* __restrict__ sc, const float* __restrict__ sh, float* __restrict__ z,
@@ -359,7 +364,7 @@ os(const float* __restrict__ x, const float* __restrict__ wt, const float* __res
         o[j] = t0;
         a0[j] = t1;
         a1[j] = t2;
-        if (r >= 2 && i - 1 < H) {
+        if (STM && r >= 2 && i - 1 < H) {
           c1[j] += t0;
           c2[j] = fmaf(t0, t0, c2[j]);
         }
@@ -368,6 +373,54 @@ os(const float* __restrict__ x, const float* __restrict__ wt, const float* __res
         bufq_st<AUXS>(rz, (unsigned)((((i - 1) * W + w) * C + c) * 4), make_float4(o[0], o[1], o[2], o[3]),
                    (float*)nullptr);
     }
+  }
+  if (STM == 0) return;
+  if (STM == 3) {
+    if (p == 0) {
+      const long row = (long)srow * 2 * C;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        stats[row + c + j] = c1[j];
+        stats[row + C + c + j] = c2[j];
+      }
+    }
+    return;
+  }
+  if (STM == 2) {
+    __shared__ double sw[4][TCQ][8];
+    float f[8] = {c1[0], c1[1], c1[2], c1[3], c2[0], c2[1], c2[2], c2[3]};
+#pragma unroll
+    for (int off = TCQ; off < 64; off <<= 1)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] += __shfl_xor(f[e], off);
+    const int lane = tid & 63, wave = tid >> 6;
+    if (lane < TCQ)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sw[wave][lane][e] = (double)f[e];
+    __syncthreads();
+    if (tid < TCQ) {
+      const long row = (long)srow * 2 * C;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const double v = ((sw[0][tid][e] + sw[1][tid][e]) + sw[2][tid][e]) + sw[3][tid][e];
+        stats[row + (e >> 2) * C + c0 + 4 * tid + (e & 3)] = v;
+      }
+    }
+    return;
+  }
+  if (STM == 4) {
+    double v[8] = {c1[0], c1[1], c1[2], c1[3], c2[0], c2[1], c2[2], c2[3]};
+#pragma unroll
+    for (int off = TCQ; off < 64; off <<= 1)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += __shfl_xor(v[e], off);
+    const int lane = tid & 63, wave = tid >> 6;
+    if (lane < TCQ) {
+      const long row = ((long)srow * 4 + wave) * 2 * C;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) stats[row + (e >> 2) * C + c0 + 4 * lane + (e & 3)] = v[e];
+    }
+    return;
   }
   __syncthreads();
   double v[8] = {c1[0], c1[1], c1[2], c1[3], c2[0], c2[1], c2[2], c2[3]};
@@ -424,7 +477,7 @@ int main(int argc, char** argv) {
   hipLaunchKernelGGL(fill, dim3(1), dim3(256), 0, 0, sh, (long)C, 9u, -0.2f, 0.4f);
   const int rows = accunet_dw3x3_rows(B, H, W, C, ACC_F32, 0);
   double *st, *str;
-  const int st_cap = std::max(rows, 8 * NT);  // rows of the largest grid (R = 4 tiles)
+  const int st_cap = std::max(rows, 16 * NT);  // rows of the largest grid (R = 8, a row per wave)
   CK(hipMalloc(&st, (size_t)st_cap * 2 * C * 8));
   CK(hipMalloc(&str, (size_t)rows * 2 * C * 8));
   CK(hipDeviceSynchronize());
@@ -504,12 +557,26 @@ int main(int argc, char** argv) {
     check(NAME, true);                                                                         \
     stat_rows = NT;                                                                            \
   }
+#define RUNOSS(STM, NAME)                                                                       \
+  {                                                                                            \
+    stat_rows = B * (H / 8) * (W / TP);                                                        \
+    const int srows = STM == 4 ? 4 * stat_rows : stat_rows;                                    \
+    if (srows > st_cap) { fprintf(stderr, "stats rows %d > %d\n", srows, st_cap); exit(3); }   \
+    auto f = [&] { hipLaunchKernelGGL((os<8, false, 3, 1, false, 2, 2, STM>), dim3(stat_rows * NCG), dim3(256), 0, 0, \
+                                      x, wt, bi, sc, sh, z, st, 0); };                          \
+    CK(hipMemset(z, 0, n * 4));                                                                \
+    report(NAME, timeit(f, iters));                                                            \
+    CK(hipGetLastError());                                                                     \
+    stat_rows = srows;                                                                         \
+    check(NAME, STM == 1 || STM == 2 || STM == 4);                                             \
+    stat_rows = NT;                                                                            \
+  }
   RUNOS(8, false, 3, 0, "os R8 regs");
-  RUNOSX(8, 3, 2, true, 2, 2, "os R8 split barrier (full LDS)");
-  RUNOSX(8, 3, 1, false, 0, 2, "os R8 default-policy loads");
-  RUNOSX(8, 3, 1, false, 2, 0, "os R8 default-policy stores");
-  RUNOSX(6, 4, 1, false, 2, 2, "os R6 (4 blocks/CU)");
-  RUNOSX(6, 4, 2, true, 2, 2, "os R6 split barrier");
+  RUNOSS(0, "os R8 stats: none");
+  RUNOSS(3, "os R8 stats: per-thread sums only");
+  RUNOSS(2, "os R8 stats: fp32 wave shuffles + fp64 slab");
+  RUNOSS(4, "os R8 stats: fp64 shuffles, row per wave");
+  RUNOSS(1, "os R8 stats: product form");
   RUNOS(8, false, 3, 0, "os R8 regs (again)");
   report("K1 product (again)", timeit(prod, iters));
   report("copy x4 nt (again)", timeit([&] {

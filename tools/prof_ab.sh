@@ -16,6 +16,7 @@ for v in $VARIANTS; do
   python tools/kstats.py gpurun_out/pa_$name --steps 7 --top 80 > gpurun_out/kstats_$name.txt
   python tools/splitk_census.py gpurun_out/pa_$name --steps 7 > gpurun_out/splitk_$name.txt
   for fam in ${KGRID:-}; do python tools/kgrid.py gpurun_out/pa_$name $fam > gpurun_out/kgrid_${name}_$fam.txt; done
+  if [ -n "${SEQ:-}" ]; then python tools/step_seq.py gpurun_out/pa_$name $SEQ > gpurun_out/seq_$name.txt; fi
   rm -rf gpurun_out/pa_$name
   echo "== $name"; head -24 gpurun_out/step_$name.txt
 done
