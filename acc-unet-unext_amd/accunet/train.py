@@ -44,7 +44,7 @@ from .loss import WeightedDiceBCE
 from .optim import FusedAdam
 
 
-def cut_buckets(numels, bucket_mb):
+def cut_buckets(numels, bucket_mb, tail_mb=1.0):
     """Parameter indices per bucket, in reverse registration order (backward finishes
     the output layer first); each bucket but the last holds >= bucket_mb of fp32. One
     graph marker per bucket, and accunet_graph_marker takes MAX_GRAPH_MARKERS ids, so
@@ -60,6 +60,20 @@ def cut_buckets(numels, bucket_mb):
             cur, n = [], 0
     if cur:
         buckets.append(cur)
+    # The last bucket seals when the backward ends, so its reduce (and, with the bf16
+    # wire, its widening copy) is the exposed tail of the step: its first-registered
+    # parameters (the encoder's first blocks, whose gradients come last) go into a
+    # bucket of their own of at most tail_mb, and the rest seals earlier, while those
+    # blocks' backward still runs.
+    tail = max(1, int(tail_mb * (1 << 20) / 4))
+    last = buckets[-1] if buckets else []
+    if len(buckets) < kern.MAX_GRAPH_MARKERS and sum(numels[i] for i in last) > tail:
+        k, n = len(last), 0
+        while k > 1 and n + numels[last[k - 1]] <= tail:
+            k -= 1
+            n += numels[last[k]]
+        if k < len(last):
+            buckets[-1:] = [last[:k], last[k:]]
     return buckets
 
 

@@ -1517,7 +1517,10 @@ static int dw_cgfast() {
 // launch kind; 0 = the strip kernel everywhere. Single-stream traces of the step
 // (profiles/r05_dw_os_ab.txt): one-shot tiles are faster only on the streamed (> 256 MB)
 // shapes; the BN-backward data gradient (a second pre-BN operand per output) and the
-// cached 64^2..128^2 shapes run faster as strips. The statistics rows follow the kernel
+// cached 64^2..128^2 shapes run faster as strips. Per shape (tools/kbench KB_DWSWEEP,
+// profiles/r05_dw_sweep.txt): one-shot 4-7 % faster at C = 96 / 192 / 384, 10 % slower
+// at cnv72's 64^2 x 4352 (a tile's 136 channel groups, vertical neighbours 272 blocks
+// apart), so C > 1024 keeps the strips. The statistics rows follow the kernel
 // (accunet_dw3x3_rows takes the launch kind). tests/test_kernels_gpu.py runs the three
 // settings bit for bit against each other.
 static int dw_os() {
@@ -1531,7 +1534,7 @@ static int dw_os() {
 static bool dw_os_on(int B, int H, int W, int C, int dt, bool bnb) {
   if (dw_os() == 2) return true;
   if (dw_os() != 1 || dt != ACC_F32 || bnb) return false;
-  return (long)B * H * W * C * 4 > (256L << 20);
+  return (long)B * H * W * C * 4 > (256L << 20) && C <= 1024;
 }
 #define DW_OS_R 8
 

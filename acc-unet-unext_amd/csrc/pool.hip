@@ -678,12 +678,21 @@ extern "C" int accunet_group_relayout(const float* in, float* out, int N, int C,
 #define RL_EPT 4
 __global__ void __launch_bounds__(256)
 relayout_batch_kernel(const AccRelayout* __restrict__ items, int n) {
-  // the item of this block: the last one whose blk0 <= blockIdx.x (blk0 ascending)
+  // the item of this block: the last one whose blk0 <= blockIdx.x (blk0 ascending),
+  // searched in LDS (the blk0 column fetched in one parallel round trip instead of a
+  // chain of ~log2(n) dependent loads per block: the bucket packs run thousands of blocks)
+  constexpr int RL_LDS = 1024;
+  __shared__ int sblk[RL_LDS];
+  const bool in_lds = n <= RL_LDS;  // (uniform)
+  if (in_lds) {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) sblk[i] = items[i].blk0;
+    __syncthreads();
+  }
   int lo = 0, hi = n - 1;
   const int bid = (int)blockIdx.x;
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
-    if (items[mid].blk0 <= bid) lo = mid; else hi = mid - 1;
+    if ((in_lds ? sblk[mid] : items[mid].blk0) <= bid) lo = mid; else hi = mid - 1;
   }
   const AccRelayout& it = items[lo];
   const long base = ((long)(bid - it.blk0) * 256 + threadIdx.x) * RL_EPT;

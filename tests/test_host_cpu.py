@@ -299,6 +299,12 @@ def test_graph_buckets_respect_the_marker_table():
         assert lo <= len(b) <= hi, (mb, len(b))
         flat = [i for k in b for i in k]
         assert flat == list(reversed(range(len(numels))))
+    # the bucket that seals last (the step's exposed reduce) holds at most tail_mb,
+    # unless its first parameter alone is larger
+    b = cut_buckets(numels, 16.0)
+    assert len(b) == 5 and sum(numels[i] for i in b[-1]) * 4 <= 1 << 20
+    b = cut_buckets([3, 400000, 5, 7], 16.0, tail_mb=0.001)
+    assert b == [[3, 2, 1], [0]]
 
 
 def test_abi_host_side_contract_without_a_device():
@@ -339,6 +345,9 @@ def test_abi_host_side_contract_without_a_device():
     assert lib.accunet_dw3x3_rows(16, 256, 256, 96, 0, 1) == (4096 if os_all else 1024)
     # 16 x 128^2 x 192 fp32 (201 MB, cached): strips by default
     assert lib.accunet_dw3x3_variant(16, 128, 128, 192, 0) == (3 if os_all else 1)
+    # cnv72's 16 x 64^2 x 4352 (1.1 GB, but 136 channel groups per tile): strips by default
+    assert lib.accunet_dw3x3_variant(16, 64, 64, 4352, 0) == (3 if os_all else 1)
+    assert lib.accunet_dw3x3_variant(16, 128, 128, 384, 0) == (3 if os_on else 1)
     # bf16 (dt 1) runs 64-channel tiles where C % 64 == 0: 16-pixel tiles, twice the rows
     # of the same kernel's 32-pixel fp32 tiles
     r32, r16 = (lib.accunet_dw3x3_rows(16, 128, 128, 192, d, 0) for d in (0, 1))

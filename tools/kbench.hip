@@ -103,8 +103,40 @@ static void report(const char* name, double us, double bytes) {
          100.0 * bytes / us / 1e3 / 8000.0);
 }
 
+// KB_DWSWEEP=1: the step's large depthwise shapes only (forward with prologue + statistics,
+// and the flipped data gradient), with whatever kernel the library picks (ACCUNET_DW_OS
+// decides between one-shot tiles and strips: run twice to compare)
+static void dw_sweep(int iters) {
+  struct S { int B, H, W, C; const char* what; };
+  const S shapes[] = {{16, 256, 256, 96, "cnv12/92 (K1)"}, {16, 256, 256, 192, "cnv91 (C 192)"},
+                      {16, 128, 128, 192, "cnv22/82"}, {16, 128, 128, 384, "cnv81"},
+                      {16, 64, 64, 4352, "cnv72 (inv_fctr 34)"}, {16, 64, 64, 384, "cnv32/71"}};
+  size_t nmax = 0;
+  for (const S& s : shapes) nmax = std::max(nmax, (size_t)s.B * s.H * s.W * s.C);
+  float *x = dalloc(nmax), *z = dalloc(nmax), *wt = dalloc(9 * 4352, 0.3f), *bi = dalloc(4352, 0.1f);
+  float *sc = dalloc(4352, 1.f), *sh = dalloc(4352, 0.1f);
+  for (const S& s : shapes) {
+    const int rows = accunet_dw3x3_rows(s.B, s.H, s.W, s.C, ACC_F32, 0);
+    double* st;
+    CK(hipMalloc(&st, (size_t)rows * 2 * s.C * sizeof(double)));
+    const double bytes = 2.0 * 4 * s.B * s.H * s.W * s.C;
+    char name[96];
+    snprintf(name, sizeof name, "dw fwd %dx%dx%dx%d %s v%d", s.B, s.H, s.W, s.C, s.what,
+             accunet_dw3x3_variant(s.B, s.H, s.W, s.C, ACC_F32));
+    report(name, timeit([&] { CA(accunet_dw3x3_fwd(x, wt, bi, sc, sh, 1, 0, z, st, s.B, s.H, s.W, s.C, nullptr, nullptr, 0, ACC_F32, 0)); }, iters), bytes);
+    snprintf(name, sizeof name, "dw dgrad %dx%dx%dx%d %s", s.B, s.H, s.W, s.C, s.what);
+    report(name, timeit([&] { CA(accunet_dw3x3_fwd(x, wt, nullptr, nullptr, nullptr, 0, 1, z, nullptr, s.B, s.H, s.W, s.C, nullptr, nullptr, 0, ACC_F32, 0)); }, iters), bytes);
+    CK(hipFree(st));
+  }
+  CK(hipFree(x)); CK(hipFree(z)); CK(hipFree(wt)); CK(hipFree(bi)); CK(hipFree(sc)); CK(hipFree(sh));
+}
+
 int main(int argc, char** argv) {
   int iters = argc > 1 ? atoi(argv[1]) : 30;
+  if (getenv("KB_DWSWEEP") && atoi(getenv("KB_DWSWEEP"))) {
+    dw_sweep(iters);
+    return 0;
+  }
   const int B = 16, H = 256, W = 256;
   // ---- K1: cnv12 depthwise, C = 96 ----
   {
