@@ -30,7 +30,7 @@ class AccRelayout(Structure):
     _fields_ = [
         ("inp", c_void_p), ("out", c_void_p), ("total", c_longlong), ("kind", c_int),
         ("blk0", c_int), ("d", c_int * 4), ("s", c_longlong * 4), ("flip", c_int * 4),
-        ("N", c_int), ("C", c_int), ("J", c_int), ("order", c_int * 8),
+        ("N", c_int), ("C", c_int), ("J", c_int), ("order", c_int * 8), ("scale", c_float),
     ]
 
 

@@ -411,7 +411,7 @@ class DeferredRelayouts:
         it.inp, it.out = src.data_ptr(), dst.data_ptr()
         it.total, it.kind = int(total), kind
         if kind in (3, 4):
-            pass
+            it.scale = kw.get("scale", 1.0)
         elif kind == 0:
             for a in range(4):
                 it.d[a], it.s[a] = kw["d"][a], kw["s"][a]
@@ -433,12 +433,12 @@ class DeferredRelayouts:
     def group_inverse(self, src, dst, N, C, J, order):
         self._add(src, dst, 2, N * J * C, N=N, C=C, J=J, order=order)
 
-    def copy(self, src, dst):
-        """flat copy of a contiguous fp32 tensor into dst (fp32, or bf16 rounded to
-        nearest even): kinds 3 / 4, the data-parallel bucket packing"""
+    def copy(self, src, dst, scale=1.0):
+        """flat copy of a contiguous fp32 tensor times `scale` into dst (fp32, or bf16
+        rounded to nearest even): kinds 3 / 4, the data-parallel bucket packing"""
         if src.dtype != torch.float32 or dst.numel() != src.numel():
             raise ValueError("copy: fp32 source of dst's size")
-        self._add(src, dst, 4 if dst.dtype == torch.bfloat16 else 3, src.numel())
+        self._add(src, dst, 4 if dst.dtype == torch.bfloat16 else 3, src.numel(), scale=scale)
 
     def flush(self):
         """one launch for the items added since the last flush (none: no launch)"""

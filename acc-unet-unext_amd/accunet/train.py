@@ -21,8 +21,8 @@ Two execution modes, same arithmetic:
       event-record node is added behind each marker (accunet_graph_events_after_
       markers on the kept hipGraph_t, then instantiate). Each step the host replays
       the graph and, without waiting, enqueues per bucket on a side stream:
-      wait(bucket event) -> RCCL all_reduce(AVG) of that slice. The collectives
-      therefore run over xGMI while the graph is still computing the rest of
+      wait(bucket event) -> RCCL all_reduce(SUM) of that slice (packed pre-divided
+      by the world, so the sum is the mean). The collectives therefore run over xGMI while the graph is still computing the rest of
       backward; only the last bucket's reduce is exposed before the one-launch Adam.
       The collectives themselves are not captured (they run on RCCL's own stream).
       Capture happens on the first call: no autograd graph of an earlier eager
@@ -39,7 +39,6 @@ import contextlib
 import os
 
 from . import kern, ops
-from .dist import all_reduce_mean
 from .loss import WeightedDiceBCE
 from .optim import FusedAdam
 
@@ -82,8 +81,13 @@ class _GraphBuckets:
     world > 1; see the module docstring). Built before capture; its hooks run only
     while the backward is being captured."""
 
-    def __init__(self, params, bucket_mb, device, comm_dtype=None):
+    def __init__(self, params, bucket_mb, device, comm_dtype=None, world=1):
         self.params = params
+        # the packed gradients are pre-divided by the world (exact for power-of-two
+        # worlds), so the all-reduce is a plain SUM -- RCCL's PreMulSum form of AVG, which
+        # at world 1 also leaves no reduce kernel behind -- and the reduced buffer holds
+        # the mean, as with AVG
+        self.scale = 1.0 / world
         # each view starts at a multiple of 4 elements, so the packing copies move whole
         # 16-byte (fp32) / 8-byte (bf16) quads; the pads stay zero
         offs, o = [], 0
@@ -112,21 +116,36 @@ class _GraphBuckets:
         # bf16 for the bf16 wire) instead of _foreach_copy_ (a mixed-dtype foreach copy
         # falls back to one launch per tensor: ~900 graph nodes per step)
         self.packer = ops.DeferredRelayouts(device, cap=len(params))
+        self.seal_stream = None
 
     # ------------------------------------------------------------ capture side
     def _seal(self, k):
-        """pack bucket k's gradients into the flat buffer, then mark it ready"""
+        """pack bucket k's gradients into the flat buffer, then mark it ready -- on a
+        stream of its own, forked from the backward at this point, so the packing
+        launches run beside the rest of the backward instead of in its chain (every
+        source is final here and stays referenced: parameter gradients, the deferred
+        relayouts' kept sources); the backward joins it before the capture ends"""
         if self._sealed[k]:
             return
         self._sealed[k] = True
-        if ops._DEFER is not None:  # pending inverse weight relayouts: final values first
-            ops._DEFER.flush()
-        for i in self.buckets[k]:
-            g = self.params[i].grad
-            if g is not None:
-                self.packer.copy(g.contiguous(), self.wviews[i])
-        self.packer.flush()
-        kern.GraphEvent.mark(k)
+        main = torch.cuda.current_stream()
+        if self.seal_stream is None:
+            self.seal_stream = torch.cuda.Stream(device=main.device)
+        self.seal_stream.wait_stream(main)
+        with torch.cuda.stream(self.seal_stream):
+            if ops._DEFER is not None:  # pending inverse weight relayouts: final values first
+                ops._DEFER.flush()
+            for i in self.buckets[k]:
+                g = self.params[i].grad
+                if g is not None:
+                    self.packer.copy(g.contiguous(), self.wviews[i], scale=self.scale)
+            self.packer.flush()
+            kern.GraphEvent.mark(k)
+
+    def join(self):
+        """the capturing stream waits for the packing stream (before the capture ends)"""
+        if self.seal_stream is not None:
+            torch.cuda.current_stream().wait_stream(self.seal_stream)
 
     def _hook(self, i):
         def hook(p):
@@ -164,7 +183,7 @@ class _GraphBuckets:
         if not nccl:  # gloo (tests): host-synchronous collectives on finished buckets
             for k, (lo, hi) in enumerate(self.range):
                 self.events[k].synchronize()
-                all_reduce_mean(self.wire[lo:hi], pg)
+                dist.all_reduce(self.wire[lo:hi], op=dist.ReduceOp.SUM, group=pg)
                 if narrow:
                     self.flat[lo:hi].copy_(self.wire[lo:hi])
             return
@@ -175,7 +194,7 @@ class _GraphBuckets:
             # issued between two reduces would hold the next reduce back
             for k, (lo, hi) in enumerate(self.range):
                 self.events[k].wait(self.stream)
-                works.append(dist.all_reduce(self.wire[lo:hi], op=dist.ReduceOp.AVG, group=pg,
+                works.append(dist.all_reduce(self.wire[lo:hi], op=dist.ReduceOp.SUM, group=pg,
                                              async_op=True))
             if narrow:  # widen each bucket on the side stream once RCCL is done with it
                 for (lo, hi), w in zip(self.range, works):
@@ -250,6 +269,8 @@ class TrainStep:
         loss.backward()
         if ops._DEFER is not None:  # the deferred weight-gradient relayouts, one launch
             ops._DEFER.flush()
+        if getattr(self, "_buckets", None) is not None:
+            self._buckets.join()
         return loss
 
     def _capture(self, images, masks):
@@ -283,8 +304,9 @@ class TrainStep:
         self._buckets = None
         if self.dp:
             self._buckets = _GraphBuckets(self.params, self.bucket_mb, self._x.device,
-                                          self.comm_dtype)
+                                          self.comm_dtype, world=self.world)
             self._buckets.stream = torch.cuda.Stream()
+            self._buckets.seal_stream = torch.cuda.Stream()  # created outside the capture
             self._buckets.arm()
         # the backward's inverse weight relayouts batched: one launch at its end at world 1;
         # with data parallelism one launch per sealed bucket (a gradient bucket must hold

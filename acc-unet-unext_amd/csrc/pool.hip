@@ -672,8 +672,9 @@ extern "C" int accunet_group_relayout(const float* in, float* out, int N, int C,
 // accunet_group_relayout's forward, kind 2 its inverse (the backward's weight
 // gradients, ops.DeferredRelayouts); the same index arithmetic, so the copies are the
 // ones the per-layer launches make. kind 3 / 4 = flat copies into a gradient bucket
-// (fp32 / rounded to bf16 like torch's .to(bfloat16): the graph-mode data-parallel
-// step packs each sealed bucket in one launch, accunet/train.py _GraphBuckets).
+// (fp32 / rounded to bf16 like torch's .to(bfloat16), times `scale` = 1/world: the
+// graph-mode data-parallel step packs each sealed bucket in one launch and all-reduces
+// it with SUM, accunet/train.py _GraphBuckets).
 // ---------------------------------------------------------------------------
 #define RL_EPT 4
 __global__ void __launch_bounds__(256)
@@ -704,7 +705,8 @@ relayout_batch_kernel(const AccRelayout* __restrict__ items, int n) {
     const bool k3 = it.kind == 3;
     const uintptr_t dst = k3 ? (uintptr_t)(it.out + base) : (uintptr_t)(reinterpret_cast<bf16_t*>(it.out) + base);
     if ((((uintptr_t)src) & 15) == 0 && (dst & (k3 ? 15 : 7)) == 0) {
-      const float4 v = *reinterpret_cast<const float4*>(src);
+      float4 v = *reinterpret_cast<const float4*>(src);
+      v.x *= it.scale; v.y *= it.scale; v.z *= it.scale; v.w *= it.scale;
       if (k3) {
         *reinterpret_cast<float4*>(dst) = v;
       } else {
@@ -721,8 +723,8 @@ relayout_batch_kernel(const AccRelayout* __restrict__ items, int n) {
     const long i = base + e;
     if (i >= it.total) break;
     if (it.kind >= 3) {  // flat copy (data-parallel bucket packing): fp32, or rounded to bf16
-      if (it.kind == 3) it.out[i] = it.in[i];
-      else reinterpret_cast<bf16_t*>(it.out)[i] = f2bf(it.in[i]);
+      if (it.kind == 3) it.out[i] = it.in[i] * it.scale;
+      else reinterpret_cast<bf16_t*>(it.out)[i] = f2bf(it.in[i] * it.scale);
       continue;
     }
     long src;

@@ -195,7 +195,9 @@ int accunet_dw3x3_wgrad(const void* x, const void* dz, const float* sc, const fl
  * accunet_group_relayout (N, C, J, order), kind 2 = its inverse (the backward's weight
  * gradients back into the reference layout, ops.DeferredRelayouts; total = N*J*C),
  * kind 3 = flat copy in -> out (fp32), kind 4 = flat copy with `out` a bf16 array
- * (round to nearest even): the data-parallel gradient-bucket packing. `in` is fp32.
+ * (round to nearest even): the data-parallel gradient-bucket packing, each value
+ * multiplied by `scale` first (1/world: the packed gradients are pre-divided, so the
+ * RCCL all-reduce is a plain SUM, the PreMulSum form of AVG). `in` is fp32.
  * ------------------------------------------------------------------------- */
 typedef struct AccRelayout {
   const float* in;
@@ -208,6 +210,7 @@ typedef struct AccRelayout {
   int flip[4];
   int N, C, J;
   int order[8];
+  float scale; /* kinds 3 / 4 */
 } AccRelayout;
 int accunet_relayout_blocks(long long total);
 int accunet_relayout_batch(const void* items_dev, int n, int nblocks, void* stream);

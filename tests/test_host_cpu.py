@@ -411,8 +411,8 @@ def _emulate_relayout(it, src):
     """numpy restatement of relayout_batch_kernel's index arithmetic for one item"""
     out = np.empty(it.total, dtype=np.float32)
     i = np.arange(it.total, dtype=np.int64)
-    if it.kind in (3, 4):  # flat copy (bucket packing), kind 4 rounded to bf16
-        out[:] = src
+    if it.kind in (3, 4):  # flat copy (bucket packing) times scale, kind 4 rounded to bf16
+        out[:] = src * np.float32(it.scale)
         if it.kind == 4:
             out[:] = torch.from_numpy(out).to(torch.bfloat16).float().numpy()
         return out
@@ -448,12 +448,12 @@ def test_bucket_packing_items():
     src = [torch.randn(5, 7), torch.randn(33)]
     dst = [torch.empty(35), torch.empty(33, dtype=torch.bfloat16)]
     d.copy(src[0], dst[0])
-    d.copy(src[1], dst[1])
+    d.copy(src[1], dst[1], scale=0.125)  # pre-divided by the world (8): SUM = mean
     assert [it.kind for it in d.items] == [3, 4]
-    for it, s_, d_ in zip(d.items, src, dst):
+    for it, s_, d_, sc in zip(d.items, src, dst, (1.0, 0.125)):
         assert it.inp == s_.data_ptr() and it.out == d_.data_ptr() and it.total == s_.numel()
         got = _emulate_relayout(it, s_.reshape(-1).numpy())
-        want = s_.reshape(-1).to(d_.dtype).float().numpy()
+        want = (s_.reshape(-1) * sc).to(d_.dtype).float().numpy()
         np.testing.assert_array_equal(got, want)
     with pytest.raises(ValueError):
         d.copy(torch.randn(3, dtype=torch.float64), torch.empty(3))
@@ -468,7 +468,7 @@ def test_weight_prep_items_reproduce_the_per_op_layouts():
     from accunet import ops
     from accunet._lib import AccRelayout
     from accunet.model import ACC_UNet
-    assert ctypes.sizeof(AccRelayout) == 144
+    assert ctypes.sizeof(AccRelayout) == 144  # (scale fills the former tail padding)
     torch.manual_seed(0)
     m = ACC_UNet(3, 1, n_filts=8)
     prep = ops.WeightPrep(m)
