@@ -43,6 +43,15 @@ echo "kbench done"
 timeout -k 10 600 bash tools/pmc_k1.sh > gpurun_out/pmc_k1.log 2>&1
 KGRID="splitk dw3x3" VARIANTS="ss:-" timeout -k 10 600 bash tools/prof_ab.sh > gpurun_out/prof_ss.log 2>&1
 echo "pmc_k1 / single-stream trace done"
+if [ -n "${DPTRACE:-}" ]; then
+  # the data-parallel step (world-1 RCCL group) beside the plain step, bf16, two streams:
+  # one step's dispatch sequence each (tools/step_seq.py)
+  DT=bf16 ACCUNET_WGRAD_STREAM=1 SEQ="--step -2" VARIANTS="b16plain:-" timeout -k 10 300 bash tools/prof_ab.sh > gpurun_out/prof_dp.log 2>&1
+  DT=bf16 ACCUNET_WGRAD_STREAM=1 BENCH_ARGS=--dp-world1 SEQ="--step -2" VARIANTS="b16dp:-" timeout -k 10 300 bash tools/prof_ab.sh >> gpurun_out/prof_dp.log 2>&1
+  timeout -k 10 200 python tools/dp_host.py --dtype bf16 > gpurun_out/dp_host_bf16.txt 2>&1
+  timeout -k 10 200 python tools/dp_host.py --dtype fp32 > gpurun_out/dp_host_fp32.txt 2>&1
+  echo "dp traces done"
+fi
 if [ -n "${PMC_GEMM:-}" ]; then
   # GEMM census of one step and the PMC passes of the ResPath 3x3 (halo kernels) and the
   # pyramid data gradient at the final sources
