@@ -295,6 +295,23 @@ def main():
     kb = os.path.join(OUT, "kbench.txt")
     if os.path.exists(kb):
         open(os.path.join(PROF, f"{r}_kbench.txt"), "w").write(f"# tools/kbench 20 ({st})\n" + open(kb).read())
+    # the data-parallel step at world 1 (gpu_round.sh DPTRACE=1): host vs GPU time of the
+    # plain and the DP step (tools/dp_host.py), and the dispatch census of one traced step
+    # of each (tools/step_seq.py tail + tools/step_profile.py head)
+    dp = [f for f in ("dp_host_fp32.txt", "dp_host_bf16.txt", "step_b16plain.txt", "step_b16dp.txt",
+                      "seq_b16plain.txt", "seq_b16dp.txt") if os.path.exists(os.path.join(OUT, f))]
+    if dp:
+        txt = f"# data-parallel step at world 1 over RCCL ({st})\n"
+        for f in dp:
+            lines = open(os.path.join(OUT, f)).read().splitlines()
+            if f.startswith("dp_host"):
+                lines = [x for x in lines if x.startswith(("plain", "dp "))]
+            elif f.startswith("seq_"):
+                lines = [x for x in lines if x.startswith("#")]
+            else:
+                lines = lines[:16]
+            txt += f"\n## {f}\n" + "\n".join(lines) + "\n"
+        open(os.path.join(PROF, f"{r}_dp_world1.txt"), "w").write(txt)
     print("saved", r, st)
 
 
