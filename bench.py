@@ -339,7 +339,7 @@ def forward_parity(dev, cases=PARITY_CASES, n_filts=32):
             "ok": all(r["ok"] for r in rows)}
 
 
-def dp_path_overhead(args, step, x, mask, dev, prec, reps=2):
+def dp_path_overhead(args, step, x, mask, dev, prec, reps=4):
     """The per-rank cost of the data-parallel machinery, measured at world 1 on the
     hardware clock: a second model (same init) stepped by TrainStep(graph=True,
     process_group=WORLD) over a world-1 RCCL group -- bucket packing into the flat

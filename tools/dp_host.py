@@ -2,9 +2,12 @@
 RCCL group): how long the host takes to submit the replayed graph, to enqueue the bucket
 all-reduces and to prepare Adam, against the GPU time of the graph -- i.e. whether the
 all-reduces can start while the backward still runs (they are enqueued only after the
-replay call returns).
+replay call returns). Variants are built once and timed in alternating blocks.
 
-    python tools/dp_host.py [--dtype bf16] [--steps 10]
+    python tools/dp_host.py [--dtype bf16] [--steps 10] [--reps 3] [--ab-seal]
+
+--ab-seal adds the data-parallel step with the bucket packing on the backward's own
+stream (ACCUNET_DP_SEAL_STREAM=0) beside the default (a stream of its own).
 """
 import argparse
 import os
@@ -24,6 +27,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--dtype", default="bf16", choices=["fp32", "bf16"])
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--ab-seal", action="store_true")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     s = socket.socket()
@@ -34,7 +39,12 @@ def main():
     g = torch.Generator().manual_seed(1000)
     x = torch.randn(16, 3, 256, 256, generator=g).to(dev)
     m = (torch.rand(16, 1, 256, 256, generator=g) < 0.3).float().to(dev)
-    for name, pg in (("plain", None), ("dp", dist.group.WORLD)):
+    variants = [("plain", None, "1"), ("dp", dist.group.WORLD, "1")]
+    if a.ab_seal:
+        variants.append(("dp_seal_on_main", dist.group.WORLD, "0"))
+    steps, seg = {}, {}
+    for name, pg, seal in variants:
+        os.environ["ACCUNET_DP_SEAL_STREAM"] = seal  # read when the step captures
         torch.manual_seed(0)
         model = M.VARIANTS["canonical"](3, 1, n_filts=32).to(dev).train()
         st = TrainStep(model, lr=1e-3, graph=True, precision=a.dtype, process_group=pg,
@@ -42,12 +52,10 @@ def main():
         for _ in range(3):
             st(x, m)
         torch.cuda.synchronize()
-        seg = {"replay": [], "reduce": [], "opt": [], "host": [], "graph_gpu": [], "step_gpu": []}
-        g_replay, opt_step = st._g.replay, st.opt.step
-        red = st._buckets.reduce if st.dp else None
+        sg = {"replay": [], "reduce": [], "opt": [], "host": [], "graph_gpu": [], "step_gpu": []}
         ev = {}
 
-        def timed(key, fn):
+        def timed(key, fn, sg=sg, ev=ev):
             def w(*args, **kw):
                 t0 = time.perf_counter()
                 if key == "replay":
@@ -57,29 +65,33 @@ def main():
                 if key == "replay":
                     ev["b"] = torch.cuda.Event(enable_timing=True)
                     ev["b"].record()
-                seg[key].append(1e3 * (time.perf_counter() - t0))
+                sg[key].append(1e3 * (time.perf_counter() - t0))
                 return r
             return w
 
-        st._g.replay = timed("replay", g_replay)
-        st.opt.step = timed("opt", opt_step)
-        if red:
-            st._buckets.reduce = timed("reduce", red)
-        for _ in range(a.steps):
-            e0 = torch.cuda.Event(enable_timing=True)
-            e1 = torch.cuda.Event(enable_timing=True)
-            t0 = time.perf_counter()
-            e0.record()
-            st(x, m)
-            e1.record()
-            seg["host"].append(1e3 * (time.perf_counter() - t0))
-            torch.cuda.synchronize()
-            seg["graph_gpu"].append(ev["a"].elapsed_time(ev["b"]))
-            seg["step_gpu"].append(e0.elapsed_time(e1))
-        med = {k: sorted(v)[len(v) // 2] for k, v in seg.items() if v}
+        st._g.replay = timed("replay", st._g.replay)
+        st.opt.step = timed("opt", st.opt.step)
+        if st.dp:
+            st._buckets.reduce = timed("reduce", st._buckets.reduce)
+        steps[name], seg[name] = (st, ev), sg
+    for _ in range(a.reps):
+        for name, _pg, _seal in variants:
+            st, ev = steps[name]
+            sg = seg[name]
+            for _ in range(a.steps):
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                t0 = time.perf_counter()
+                e0.record()
+                st(x, m)
+                e1.record()
+                sg["host"].append(1e3 * (time.perf_counter() - t0))
+                torch.cuda.synchronize()
+                sg["graph_gpu"].append(ev["a"].elapsed_time(ev["b"]))
+                sg["step_gpu"].append(e0.elapsed_time(e1))
+    for name, _pg, _seal in variants:
+        med = {k: sorted(v)[len(v) // 2] for k, v in seg[name].items() if v}
         print(name, " ".join(f"{k} {v:.2f} ms" for k, v in med.items()), flush=True)
-        del st, model
-        torch.cuda.synchronize()
     dist.destroy_process_group()
 
 
