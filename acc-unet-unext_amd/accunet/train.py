@@ -117,8 +117,6 @@ class _GraphBuckets:
         # falls back to one launch per tensor: ~900 graph nodes per step)
         self.packer = ops.DeferredRelayouts(device, cap=len(params))
         self.seal_stream = None
-        # ACCUNET_DP_SEAL_STREAM=0 (A/B knob): pack on the backward's own stream
-        self.seal_on = os.environ.get("ACCUNET_DP_SEAL_STREAM", "1") != "0"
 
     # ------------------------------------------------------------ capture side
     def _seal(self, k):
@@ -131,10 +129,10 @@ class _GraphBuckets:
             return
         self._sealed[k] = True
         main = torch.cuda.current_stream()
-        side = self.seal_stream if self.seal_on else None
-        if side is not None:
-            side.wait_stream(main)
-        with torch.cuda.stream(side if side is not None else main):
+        if self.seal_stream is None:
+            self.seal_stream = torch.cuda.Stream(device=main.device)
+        self.seal_stream.wait_stream(main)
+        with torch.cuda.stream(self.seal_stream):
             if ops._DEFER is not None:  # pending inverse weight relayouts: final values first
                 ops._DEFER.flush()
             for i in self.buckets[k]:
@@ -146,7 +144,7 @@ class _GraphBuckets:
 
     def join(self):
         """the capturing stream waits for the packing stream (before the capture ends)"""
-        if self.seal_on and self.seal_stream is not None:
+        if self.seal_stream is not None:
             torch.cuda.current_stream().wait_stream(self.seal_stream)
 
     def _hook(self, i):

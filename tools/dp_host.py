@@ -4,10 +4,7 @@ all-reduces and to prepare Adam, against the GPU time of the graph -- i.e. wheth
 all-reduces can start while the backward still runs (they are enqueued only after the
 replay call returns). Variants are built once and timed in alternating blocks.
 
-    python tools/dp_host.py [--dtype bf16] [--steps 10] [--reps 3] [--ab-seal]
-
---ab-seal adds the data-parallel step with the bucket packing on the backward's own
-stream (ACCUNET_DP_SEAL_STREAM=0) beside the default (a stream of its own).
+    python tools/dp_host.py [--dtype bf16] [--steps 10] [--reps 3]
 """
 import argparse
 import os
@@ -28,7 +25,6 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["fp32", "bf16"])
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--ab-seal", action="store_true")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     s = socket.socket()
@@ -39,12 +35,9 @@ def main():
     g = torch.Generator().manual_seed(1000)
     x = torch.randn(16, 3, 256, 256, generator=g).to(dev)
     m = (torch.rand(16, 1, 256, 256, generator=g) < 0.3).float().to(dev)
-    variants = [("plain", None, "1"), ("dp", dist.group.WORLD, "1")]
-    if a.ab_seal:
-        variants.append(("dp_seal_on_main", dist.group.WORLD, "0"))
+    variants = [("plain", None), ("dp", dist.group.WORLD)]
     steps, seg = {}, {}
-    for name, pg, seal in variants:
-        os.environ["ACCUNET_DP_SEAL_STREAM"] = seal  # read when the step captures
+    for name, pg in variants:
         torch.manual_seed(0)
         model = M.VARIANTS["canonical"](3, 1, n_filts=32).to(dev).train()
         st = TrainStep(model, lr=1e-3, graph=True, precision=a.dtype, process_group=pg,
@@ -75,7 +68,7 @@ def main():
             st._buckets.reduce = timed("reduce", st._buckets.reduce)
         steps[name], seg[name] = (st, ev), sg
     for _ in range(a.reps):
-        for name, _pg, _seal in variants:
+        for name, _pg in variants:
             st, ev = steps[name]
             sg = seg[name]
             for _ in range(a.steps):
@@ -89,7 +82,7 @@ def main():
                 torch.cuda.synchronize()
                 sg["graph_gpu"].append(ev["a"].elapsed_time(ev["b"]))
                 sg["step_gpu"].append(e0.elapsed_time(e1))
-    for name, _pg, _seal in variants:
+    for name, _pg in variants:
         med = {k: sorted(v)[len(v) // 2] for k, v in seg[name].items() if v}
         print(name, " ".join(f"{k} {v:.2f} ms" for k, v in med.items()), flush=True)
     dist.destroy_process_group()
