@@ -1674,9 +1674,12 @@ extern "C" int accunet_dw3x3_fwd(const void* x, const float* wt, const float* bi
   int tcq = dw_tile_tcq(H, W, C, dt);
   if (tcq && dw_os_on(B, H, W, C, dt, bz != nullptr)) {
     DwOGeom og = dw_ogeom(B, H, W, C, tcq, &grid);
-    // non-temporal loads only for inputs above the Infinity Cache and whole-line segments
+    // default-policy input loads: a tile re-reads 2 of its 10 input rows and 2 of its 34
+    // pixels from its neighbours' fetches, and non-temporal loads evict those lines
+    // before the neighbour runs (kbench, same box: K1 149.0 -> 143.2 us, the flipped data
+    // gradient 143.2 -> 135.4 us without them; the strips keep nt loads above 256 MB)
     const int seg = tcq * 4 * (dt == ACC_BF16 ? 2 : 4);
-    og.ntl = seg % 128 == 0 ? dw_ntl((long)B * H * W * C * (dt == ACC_BF16 ? 2 : 4)) : 0;
+    og.ntl = 0;
     // half-line pixel segments (bf16, 32 channels): the channel groups sharing a line on
     // one XCD
     og.xcd = seg % 128 != 0 && og.ncg > 1 && (long)B * og.tilesH * og.tilesW % 8 == 0;
@@ -1691,16 +1694,11 @@ extern "C" int accunet_dw3x3_fwd(const void* x, const float* wt, const float* bi
     using I8 = std::integral_constant<int, 8>;
     using BT = std::integral_constant<bool, true>;
     using BF = std::integral_constant<bool, false>;
-    using A2 = std::integral_constant<int, 2>;
-    using A0 = std::integral_constant<int, 0>;
+    using A0 = std::integral_constant<int, 0>;  // (default-policy loads, see above)
     if (with_dt(dt, [&](auto tag) {
-          auto by_aux = [&](auto tc, auto bn) {
-            if (og.ntl) launch(tag, tc, bn, A2{});
-            else launch(tag, tc, bn, A0{});
-          };
           auto by_bnb = [&](auto tc) {
-            if (bz) by_aux(tc, BT{});
-            else by_aux(tc, BF{});
+            if (bz) launch(tag, tc, BT{}, A0{});
+            else launch(tag, tc, BF{}, A0{});
           };
           if (tcq == 16) by_bnb(I16{});
           else by_bnb(I8{});

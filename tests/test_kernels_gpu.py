@@ -277,3 +277,27 @@ def test_upsample_bwd24_matches_two_blocksums(B, H, W, C, dt):
     ref4 = d.view(B, H // 4, 4, W // 4, 4, C).sum((2, 4))
     tol = 1e-5 if dt == torch.float32 else 2e-2
     assert ((g4.double() - ref4).abs().max() / ref4.abs().max()).item() < tol
+
+
+def test_bucket_packing_copies_aligned_and_ragged():
+    """relayout_batch_kernel kinds 3 / 4 (the DP bucket packing, ops.DeferredRelayouts
+    .copy): the float4 path (16-byte aligned source and destination) and the scalar path
+    (destinations at odd element offsets, ragged lengths), times a scale, into fp32 and
+    bf16 wires -- bit-equal to torch's (src * scale).to(dtype)."""
+    from accunet import ops
+    torch.manual_seed(12)
+    d = ops.DeferredRelayouts(DEV, cap=8)
+    src = [torch.randn(n, device=DEV) for n in (4096, 1031, 7, 5000)]
+    wire32 = torch.zeros(16384, device=DEV)
+    wire16 = torch.zeros(16384, device=DEV, dtype=torch.bfloat16)
+    cases = [(src[0], wire32[0:4096], 1.0), (src[1], wire32[4097:5128], 0.125),
+             (src[2], wire16[8:15], 0.5), (src[3], wire16[5001:10001], 0.125)]
+    kern = _kern()
+    for s_, dst, sc in cases:
+        d.copy(s_, dst, scale=sc)
+    d.flush()   # (the captured launch; outside a capture its table is not filled yet)
+    d.upload()  # the item table, as TrainStep uploads it after the capture
+    kern.relayout_batch(d.table, len(d.items), sum(kern.relayout_blocks(it.total) for it in d.items))
+    torch.cuda.synchronize()
+    for s_, dst, sc in cases:
+        assert torch.equal(dst, (s_ * sc).to(dst.dtype)), (dst.dtype, dst.numel(), sc)
