@@ -65,6 +65,23 @@ __global__ void copy4_x4_nt(const float4* __restrict__ a0, float4* __restrict__ 
 #pragma unroll
   for (int k = 0; k < 4; ++k) if (base + 256 * k < n) __builtin_nontemporal_store(v[k], &b[base + 256 * k]);
 }
+// c = a + b, 4 independent float4 per thread (the byte pattern of a 2-read 1-write pass)
+__global__ void add4_x4_nt(const float4* __restrict__ a0, const float4* __restrict__ b0,
+                           float4* __restrict__ c0, long n) {
+  const v4f* a = (const v4f*)a0;
+  const v4f* b = (const v4f*)b0;
+  v4f* c = (v4f*)c0;
+  long base = (long)blockIdx.x * 1024 + threadIdx.x;
+  v4f u[4], v[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (base + 256 * k < n) {
+      u[k] = __builtin_nontemporal_load(&a[base + 256 * k]);
+      v[k] = __builtin_nontemporal_load(&b[base + 256 * k]);
+    }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) if (base + 256 * k < n) __builtin_nontemporal_store(u[k] + v[k], &c[base + 256 * k]);
+}
 
 __global__ void fill(float* p, long n, float s) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
@@ -278,6 +295,26 @@ int main(int argc, char** argv) {
              timeit([&] { CA(accunet_bn_bwd(z, dout, stb, g, 1, 1, (long)B * HW, C, da, 0, dg, dbe,
                                             nullptr, bw, bws, ACC_F32, 0)); }, iters),
              5.0 * 4 * n);
+      // the BatchNorm backward whose reduce ran in the producer's epilogue (finish + apply)
+      const int R = 64;
+      double* bpart;
+      CK(hipMalloc(&bpart, (size_t)R * 2 * C * sizeof(double)));
+      CK(hipMemset(bpart, 0, (size_t)R * 2 * C * sizeof(double)));
+      size_t pws = accunet_bn_bwd_part_ws_elems((long)B * HW, R, C);
+      float* pw = dalloc(pws);
+      report("add float4 x4/thread nt (2 rd + 1 wr)",
+             timeit([&] { hipLaunchKernelGGL(add4_x4_nt, dim3((unsigned)((n / 4 + 1023) / 1024)), dim3(256), 0, 0,
+                                             (const float4*)z, (const float4*)dout, (float4*)da, (long)(n / 4)); }, iters),
+             3.0 * 4 * n);
+      report("bn_bwd apply 16x65536x32 (2 rd + 1 wr)",
+             timeit([&] { CA(accunet_bn_bwd_part(z, dout, stb, g, 1, 1, (long)B * HW, C, bpart, R, da, dg, dbe,
+                                                 nullptr, pw, pws, ACC_F32, 0)); }, iters),
+             3.0 * 4 * n);
+      report("bn_bwd apply bf16 16x65536x32",
+             timeit([&] { CA(accunet_bn_bwd_part(z, dout, stb, g, 1, 1, (long)B * HW, C, bpart, R, da, dg, dbe,
+                                                 nullptr, pw, pws, ACC_BF16, 0)); }, iters),
+             3.0 * 2 * n);
+      CK(hipFree(bpart));
     }
     report("K3 se_fwd 16x65536x32 pro",
            timeit([&] { CA(accunet_se_fwd(z, sc, sh, 1, B, HW, C, Cr, w1, b1, w2, b2, g, be, rm, rv,
@@ -287,6 +324,43 @@ int main(int argc, char** argv) {
            timeit([&] { CA(accunet_se_bwd(z, dout, sc, sh, 1, B, HW, C, Cr, w1, w2, g, 1, save, da,
                                           dw1, db1, dw2, db2, dg, dbe, ws, wse, ACC_F32, 0)); }, iters),
            4.0 * 4 * n);
+    // the fused SE + prologue-BN backward the model runs (HANC / ResPath / MLFC)
+    float *pst = dalloc(4 * C, 1.f), *pg = dalloc(C, 1.f), *dpg = dalloc(C), *dpb = dalloc(C);
+    report("K3' se_bwd_pro 16x65536x32 (2 rd + 2 rd + 1 wr)",
+           timeit([&] { CA(accunet_se_bwd_pro(z, dout, pst, 1, pg, 1, B, HW, C, Cr, w1, w2, g, 1, save,
+                                              da, dpg, dpb, nullptr, dw1, db1, dw2, db2, dg, dbe, ws,
+                                              wse, ACC_F32, 0)); }, iters),
+           5.0 * 4 * n);
+    report("K3' bf16 se_bwd_pro 16x65536x32",
+           timeit([&] { CA(accunet_se_bwd_pro(z, dout, pst, 1, pg, 1, B, HW, C, Cr, w1, w2, g, 1, save,
+                                              da, dpg, dpb, nullptr, dw1, db1, dw2, db2, dg, dbe, ws,
+                                              wse, ACC_BF16, 0)); }, iters),
+           5.0 * 2 * n);
+  }
+  {  // cnv72's BatchNorm backward apply (16 x 64 x 64 pixels x 4352 channels)
+    const long P = 16L * 64 * 64;
+    const int C = 4352, R = 64;
+    const size_t n = (size_t)P * C;
+    float *x = dalloc(n), *dy = dalloc(n), *dx = dalloc(n);
+    float *st = dalloc(4 * C, 1.f), *ga = dalloc(C, 1.f), *dg = dalloc(C), *dbe = dalloc(C);
+    double* bpart;
+    CK(hipMalloc(&bpart, (size_t)R * 2 * C * sizeof(double)));
+    CK(hipMemset(bpart, 0, (size_t)R * 2 * C * sizeof(double)));
+    size_t pws = accunet_bn_bwd_part_ws_elems(P, R, C);
+    float* pw = dalloc(pws);
+    report("add float4 x4/thread nt 65536x4352",
+           timeit([&] { hipLaunchKernelGGL(add4_x4_nt, dim3((unsigned)((n / 4 + 1023) / 1024)), dim3(256), 0, 0,
+                                           (const float4*)x, (const float4*)dy, (float4*)dx, (long)(n / 4)); }, iters),
+           3.0 * 4 * n);
+    report("bn_bwd apply 65536x4352 (2 rd + 1 wr)",
+           timeit([&] { CA(accunet_bn_bwd_part(x, dy, st, ga, 1, 1, P, C, bpart, R, dx, dg, dbe, nullptr, pw,
+                                               pws, ACC_F32, 0)); }, iters),
+           3.0 * 4 * n);
+    report("bn_bwd apply bf16 65536x4352",
+           timeit([&] { CA(accunet_bn_bwd_part(x, dy, st, ga, 1, 1, P, C, bpart, R, dx, dg, dbe, nullptr, pw,
+                                               pws, ACC_BF16, 0)); }, iters),
+           3.0 * 2 * n);
+    CK(hipFree(x)); CK(hipFree(dy)); CK(hipFree(dx)); CK(hipFree(bpart)); CK(hipFree(pw));
   }
   CK(hipDeviceSynchronize());
   return 0;
