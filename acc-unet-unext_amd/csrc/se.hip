@@ -695,11 +695,13 @@ se_bwd_reduce_pro_kernel(const T* __restrict__ z, const T* __restrict__ dout,
   const int b = blockIdx.x / g.NCH, ch = blockIdx.x % g.NCH;
   long r0 = (long)b * g.HW + ch * g.rows_per;
   long r1 = min((long)b * g.HW + g.HW, r0 + g.rows_per);
-  double acc[SE_PRO_NQ][V];
+  // fp32 sums over the thread's rows (at most a few dozen per chunk), fp64 from the
+  // block reduction on: half the VALU work of per-element fp64 accumulation
+  float accf[SE_PRO_NQ][V];
 #pragma unroll
   for (int i = 0; i < SE_PRO_NQ; ++i)
 #pragma unroll
-    for (int j = 0; j < V; ++j) acc[i][j] = 0.0;
+    for (int j = 0; j < V; ++j) accf[i][j] = 0.f;
   if (t.active) {
     float s[V], h[V], mu[V], al[V], be[V];
 #pragma unroll
@@ -717,20 +719,18 @@ se_bwd_reduce_pro_kernel(const T* __restrict__ z, const T* __restrict__ dout,
         const float x = apply_act(pre, act);
         const float lp = act == ACT_LRELU ? lrelu_d(pre) : 1.f;
         const float g2 = d[j] * lrelu_d(al[j] * x + be[j]);
-        const double xc = (double)v[j] - mu[j];
-        const double lg = (double)lp * g2, la = (double)lp * x;
-        acc[0][j] += g2;
-        acc[1][j] += (double)g2 * x;
-        acc[2][j] += lg;
-        acc[3][j] += la;
-        acc[4][j] += lp;
-        acc[5][j] += lg * xc;
-        acc[6][j] += la * xc;
-        acc[7][j] += lp * xc;
+        const float xc = v[j] - mu[j];
+        const float lg = lp * g2, la = lp * x;
+        accf[0][j] += g2;
+        accf[1][j] = fmaf(g2, x, accf[1][j]);
+        accf[2][j] += lg;
+        accf[3][j] += la;
+        accf[4][j] += lp;
+        accf[5][j] = fmaf(lg, xc, accf[5][j]);
+        accf[6][j] = fmaf(la, xc, accf[6][j]);
+        accf[7][j] = fmaf(lp, xc, accf[7][j]);
       }
     };
-    // plain row loop: the 8 fp64 accumulators per channel already hold 64 VGPRs, and
-    // the unrolled buffer-load form (quad_rows2) costs a wave of occupancy (measured)
     for (long r = r0 + t.rg; r < r1; r += t.RG) {
       float v[V], d[V];
       ldv<V>(z + r * C + t.c0, v);
@@ -738,6 +738,11 @@ se_bwd_reduce_pro_kernel(const T* __restrict__ z, const T* __restrict__ dout,
       row(v, d);
     }
   }
+  double acc[SE_PRO_NQ][V];
+#pragma unroll
+  for (int i = 0; i < SE_PRO_NQ; ++i)
+#pragma unroll
+    for (int j = 0; j < V; ++j) acc[i][j] = (double)accf[i][j];
   block_chan_reduceN<V, SE_PRO_NQ>(t, acc, part, blockIdx.x, C);
 }
 
