@@ -8,7 +8,7 @@ GradBucketReducer is the only collective on the path: gradients are views into
 one flat fp32 buffer partitioned into ~25 MB buckets in reverse registration
 order (the order backward produces them, output layer first). A
 post-accumulate-grad hook counts ready parameters per bucket and launches an
-async all-reduce (AVG) of the bucket as soon as it is complete, so RCCL traffic
+async all-reduce (pre-divided by the world, then SUM) of the bucket as soon as it is complete, so RCCL traffic
 over xGMI overlaps the rest of backward on RCCL's own stream. A final autograd
 callback flushes buckets holding parameters that received no gradient (e.g.
 ACC_UNet_Lite's bypassed MLFC convolutions, ACC_UNet_lite.py:422-429) so every
@@ -64,6 +64,8 @@ class GradBucketReducer:
         self.module = module
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        # the fp32 value of 1/world the graph-mode packing multiplies by (AccRelayout.scale)
+        self.inv_world = float(torch.tensor(1.0 / self.world, dtype=torch.float32))
         params = [p for p in module.parameters() if p.requires_grad]
         self.params = params
         dev = params[0].device
@@ -123,9 +125,13 @@ class GradBucketReducer:
         self._launched[b] = True
         lo, hi = self.bucket_range[b]
         if self.world > 1:
-            h = dist.all_reduce(self.flat[lo:hi], op=dist.ReduceOp.AVG
-                                if dist.get_backend(self.pg) == "nccl" else dist.ReduceOp.SUM,
-                                group=self.pg, async_op=True)
+            # pre-divided by the world (fp32), then a plain SUM: the PreMulSum form of
+            # AVG the graph-mode step uses (train._GraphBuckets packs gradients times
+            # 1/world), so the two modes agree bit for bit at every world size, not only
+            # where x/world == x*(1/world) exactly (powers of two)
+            seg = self.flat[lo:hi]
+            seg.mul_(self.inv_world)
+            h = dist.all_reduce(seg, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
             self._handles.append((h, lo, hi))
 
     def _finish(self):
@@ -133,8 +139,6 @@ class GradBucketReducer:
             self._launch(b)
         for h, lo, hi in self._handles:
             h.wait()
-            if self.world > 1 and dist.get_backend(self.pg) != "nccl":
-                self.flat[lo:hi].div_(self.world)
         # ready for the next backward whether or not the caller runs prepare()
         self._reset()
 

@@ -376,10 +376,35 @@ class ACC_UNet(nn.Module):
         self.act_dtype = dt
         return self
 
-    def forward(self, x):
-        B, C, H, W = x.shape
+    # pyramid level (resolution H >> level) of every HANCBlock (ACC_UNet.py:605-651)
+    _BLOCK_LEVEL = {"cnv11": 0, "cnv12": 0, "cnv21": 1, "cnv22": 1, "cnv31": 2, "cnv32": 2,
+                    "cnv41": 3, "cnv42": 3, "cnv51": 4, "cnv52": 4, "cnv61": 3, "cnv62": 3,
+                    "cnv71": 2, "cnv72": 2, "cnv81": 1, "cnv82": 1, "cnv91": 0, "cnv92": 0}
+    # the depthwise kernels address one image of a block's hidden tensor through a 32-bit
+    # buffer descriptor (csrc/dwconv.hip: dw_image_ok)
+    DW_IMAGE_LIMIT = 1 << 31
+
+    def check_input_size(self, H, W):
+        """Raise ValueError for a spatial size this build cannot run: H, W not divisible
+        by 16 (the reference fails there too, in its pooling / cat), or a HANCBlock whose
+        depthwise input would reach 2 GiB per image (e.g. canonical cnv72's 4352 hidden
+        channels at (H/4)^2 = 352^2 fp32, an input of 1408^2; the reference accepts it)."""
         if H % 16 or W % 16:
             raise ValueError(f"ACC_UNet: H and W must be divisible by 16, got {H}x{W}")
+        elem = torch.finfo(self.act_dtype).bits // 8
+        for name, lvl in self._BLOCK_LEVEL.items():
+            hidden = getattr(self, name).conv2.weight.shape[0]
+            nbytes = (H >> lvl) * (W >> lvl) * hidden * elem
+            if nbytes >= self.DW_IMAGE_LIMIT:
+                raise ValueError(
+                    f"ACC_UNet: {name}'s depthwise input is {nbytes / 2**30:.2f} GiB per image "
+                    f"at {H}x{W} ({hidden} channels at {H >> lvl}x{W >> lvl}, "
+                    f"{self.precision}); the depthwise kernels address one image with 32-bit "
+                    f"offsets, limit 2 GiB per image")
+
+    def forward(self, x):
+        B, C, H, W = x.shape
+        self.check_input_size(H, W)
         if C != self.n_channels:
             raise ValueError(f"ACC_UNet: expected {self.n_channels} input channels, got {C}")
         x1 = ops.to_nhwc(x, self.act_dtype)

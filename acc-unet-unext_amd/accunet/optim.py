@@ -90,6 +90,14 @@ class FusedAdam(torch.optim.Optimizer):
                 shared = torch.tensor(steps.pop())
                 for p in params:
                     self.state[p]["step"] = shared
+            if len(params) != len(group["params"]):
+                # a parameter skipped this step (grad None) keeps its own count, as in
+                # torch.optim.Adam: it leaves the shared counter before the increment
+                live = {id(p) for p in params}
+                for p in group["params"]:
+                    st = self.state.get(p)
+                    if id(p) not in live and st and st.get("step") is shared:
+                        st["step"] = shared.clone()
             shared += 1
             step = int(shared)
             tab, ct, cs, n = self._table(gi, params)

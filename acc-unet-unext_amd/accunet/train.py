@@ -149,6 +149,14 @@ class _GraphBuckets:
 
     def _hook(self, i):
         def hook(p):
+            # one gradient contribution per parameter: a second AccumulateGrad add on the
+            # main stream could land after this bucket's seal (packing, and the deferred
+            # relayouts the seal stream writes into .grad) -- refuse it at capture time
+            self._fired[i] += 1
+            if self._fired[i] > 1:
+                raise RuntimeError(f"graph-mode data parallelism: parameter {i} received more "
+                                   f"than one gradient contribution; its bucket would be "
+                                   f"sealed before the last one (use graph=False)")
             if not self._queued:  # buckets with unused parameters close at the end
                 self._queued = True
                 torch.autograd.Variable._execution_engine.queue_callback(self._flush)
@@ -165,6 +173,7 @@ class _GraphBuckets:
     def arm(self):
         self._left = [len(b) for b in self.buckets]
         self._sealed = [False] * len(self.buckets)
+        self._fired = [0] * len(self.params)
         self._queued = False
         self._handles = [p.register_post_accumulate_grad_hook(self._hook(i))
                          for i, p in enumerate(self.params)]

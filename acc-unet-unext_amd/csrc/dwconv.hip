@@ -600,8 +600,12 @@ dw3x3_tile_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
     rd(1, win[1]);
     const int nr = min(CR, hend - r0);
     // forward statistics of this chunk's CR rows in fp32, folded into the fp64 sums once
-    // per chunk (K1_CHUNK_STATS; 0 = every element straight into fp64)
-    float c1[4] = {0.f, 0.f, 0.f, 0.f}, c2[4] = {0.f, 0.f, 0.f, 0.f};
+    // per chunk (K1_CHUNK_STATS; 0 = every element straight into fp64). The fp32 sums are
+    // of d = z - pv, pv = the thread's first output of the chunk (a per-thread pivot):
+    // sum d^2 stays at the scale of the spread, so a channel whose mean is large against
+    // its spread does not lose its variance to cancellation (the fold adds n pv^2 +
+    // 2 pv sum d in fp64)
+    float c1[4] = {0.f, 0.f, 0.f, 0.f}, c2[4] = {0.f, 0.f, 0.f, 0.f}, pv[4];
 #pragma unroll
     for (int r = 0; r < CR; ++r) {
       // rows past the strip end (r >= nr) read stale ring slots: computed, not kept
@@ -617,6 +621,7 @@ dw3x3_tile_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
           for (int dx = 0; dx < 3; ++dx) acc = fmaf(k[dy * 3 + dx][j], win[dy][dx][j], acc);
         acc = rnd<T>(acc);  // statistics of the stored value
         o[j] = acc;
+        if (r == 0) pv[j] = acc;  // (computed from finite values even when not kept)
         const float am = on ? acc : 0.f;
         if (BNB) {
           const float zz = f4get(q2f(zcur[r]), j);
@@ -625,8 +630,9 @@ dw3x3_tile_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
           s1[j] += gg;
           s2[j] += (double)gg * ((double)zz - bmu[j]);
         } else if (K1_CHUNK_STATS) {
-          c1[j] += am;
-          c2[j] = fmaf(am, am, c2[j]);
+          const float d = on ? acc - pv[j] : 0.f;
+          c1[j] += d;
+          c2[j] = fmaf(d, d, c2[j]);
         } else {
           s1[j] += am;
           s2[j] += (double)am * am;
@@ -644,10 +650,12 @@ dw3x3_tile_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
         }
     }
     if (!BNB && K1_CHUNK_STATS) {
+      const double n = wv ? (double)nr : 0.0;  // elements kept in this chunk
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        s1[j] += (double)c1[j];
-        s2[j] += (double)c2[j];
+        const double k0 = pv[j], d1 = c1[j];
+        s1[j] += n * k0 + d1;
+        s2[j] += (n * k0 * k0 + 2.0 * k0 * d1) + (double)c2[j];
       }
     }
     if (more) {
@@ -801,7 +809,13 @@ dw3x3_os_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
   // image and every output row is stored, so no per-element masking
   const bool interior = h0 >= 1 && h0 + R + 1 <= g.H && w0 + TP <= g.W;
   float a0[4] = {0.f, 0.f, 0.f, 0.f}, a1[4] = {0.f, 0.f, 0.f, 0.f};
-  f2v c1[2] = {{0.f, 0.f}, {0.f, 0.f}}, c2[2] = {{0.f, 0.f}, {0.f, 0.f}};
+  // forward statistics: fp32 sums of d = z - pv per thread, pv = the first output row of
+  // the wave's pixel-0 lane of the same quad (wave-uniform per quad, so the sums can be
+  // added across the wave's pixels in fp32): the squares stay at the scale of the spread
+  // (no cancellation for a channel whose mean is large against its spread); the count of
+  // kept elements rides along, and the fp64 fold restores sum z, sum z^2
+  f2v c1[2] = {{0.f, 0.f}, {0.f, 0.f}}, c2[2] = {{0.f, 0.f}, {0.f, 0.f}}, pv[2] = {{0.f, 0.f}, {0.f, 0.f}};
+  float cnt = 0.f;
   double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
   float4 cen[IR];
   if (interior) {
@@ -860,6 +874,13 @@ dw3x3_os_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
         o[j] = rnd<T>(t0);  // statistics of the stored value
       }
       if (r < 2) continue;
+      if (!BNB && r == 2) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          pv[j].x = __shfl(o[2 * j], q, 64);
+          pv[j].y = __shfl(o[2 * j + 1], q, 64);
+        }
+      }
       if (BNB) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -872,10 +893,11 @@ dw3x3_os_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
         }
       } else {
         // fp32 per-thread sums on packed pairs (same adds and fmas as the scalar form)
-        f2v m01 = {o[0], o[1]}, m23 = {o[2], o[3]};
+        f2v m01 = f2v{o[0], o[1]} - pv[0], m23 = f2v{o[2], o[3]} - pv[1];
         if (!IN) {
           m01 = on ? m01 : f2v{0.f, 0.f};
           m23 = on ? m23 : f2v{0.f, 0.f};
+          cnt += on ? 1.f : 0.f;
         }
         c1[0] += m01;
         c1[1] += m23;
@@ -897,15 +919,22 @@ dw3x3_os_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
     // 2-3 us of K1's 150 against the block reduction through the tile)
     constexpr int WL = TCQ < 64 ? TCQ : 64;
     __shared__ double sw[4][WL][8];
-    float f[8] = {c1[0].x, c1[0].y, c1[1].x, c1[1].y, c2[0].x, c2[0].y, c2[1].x, c2[1].y};
+    if (interior) cnt = (float)R;
+    float f[9] = {c1[0].x, c1[0].y, c1[1].x, c1[1].y, c2[0].x, c2[0].y, c2[1].x, c2[1].y, cnt};
 #pragma unroll
     for (int off = TCQ; off < 64; off <<= 1)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) f[e] += __shfl_xor(f[e], off);
+      for (int e = 0; e < 9; ++e) f[e] += __shfl_xor(f[e], off);
     const int lane = tid & 63, wave = tid >> 6;
     if (lane < WL) {
+      const double n = f[8];
+      const float k0[4] = {pv[0].x, pv[0].y, pv[1].x, pv[1].y};
 #pragma unroll
-      for (int e = 0; e < 8; ++e) sw[wave][lane][e] = (double)f[e];
+      for (int j = 0; j < 4; ++j) {
+        const double kk = k0[j], d1 = f[j];
+        sw[wave][lane][j] = n * kk + d1;
+        sw[wave][lane][4 + j] = (n * kk * kk + 2.0 * kk * d1) + (double)f[4 + j];
+      }
     }
     __syncthreads();
     if (tid < TCQ) {  // (TCQ <= 64: every wave holds every quad)
@@ -1632,11 +1661,21 @@ extern "C" int accunet_dw3x3_rows(int B, int H, int W, int C, int dt, int bnb) {
   return (int)grid.x;
 }
 
+// Every depthwise kernel addresses one image through a buffer descriptor whose byte
+// count and offsets are 32-bit (the masked offset ACC_OOB = 2^31 must stay out of
+// range): images of 2 GiB or more are refused (ACC_EBADSHAPE) instead of wrapping.
+// ACC_UNet.forward raises before it gets here (accunet/model.py).
+static bool dw_image_ok(int H, int W, int C, int dt) {
+  const long bytes = (long)H * W * C * (dt == ACC_BF16 ? 2 : 4);
+  return H > 0 && W > 0 && C > 0 && bytes < (1L << 31);
+}
+
 extern "C" int accunet_dw3x3_fwd(const void* x, const float* wt, const float* bias,
                                  const float* sc, const float* sh, int act, int flip, void* z,
                                  double* stats, int B, int H, int W, int C, const void* bz,
                                  const float* bst, int bact, int dt, void* stream) {
   hipStream_t s = (hipStream_t)stream;
+  if (!dw_image_ok(H, W, C, dt)) return ACC_EBADSHAPE;
   if (bz && (!bst || !stats)) return ACC_EBADARG;
   dim3 grid;
   if (const int nt = dw_span_nt(H, W, C)) {
@@ -1787,6 +1826,7 @@ extern "C" int accunet_dw3x3_wgrad(const void* x, const void* dz, const float* s
                                    const float* sh, int act, float* dw, float* db, int B, int H,
                                    int W, int C, float* ws, size_t ws_elems, int dt, void* stream) {
   hipStream_t s = (hipStream_t)stream;
+  if (!dw_image_ok(H, W, C, dt)) return ACC_EBADSHAPE;
   int V = (C % 4 == 0) ? 4 : 1;
   dim3 grid;
   int tcq = dw_tile_tcq(H, W, C, dt);

@@ -26,6 +26,8 @@
 #include <cstdlib>
 #include <type_traits>
 
+#define SE_F32_ROWS 64  // rows a thread sums in fp32 before the fp64 block reduction
+
 struct SeGeom {
   int B, HW, C, NCH;
   long rows_per;  // rows per chunk
@@ -71,6 +73,16 @@ static SeGeom se_geom(int B, int HW, int C) {
   if (maxch < 1) maxch = 1;
   g.NCH = want < maxch ? want : maxch;
   if (g.NCH < 1) g.NCH = 1;
+  // a thread walks rows_per / RG rows of its chunk (RG = 256 / min(C/V, 64) row groups,
+  // chan_tile); the backward's first pass sums them in fp32 (se_bwd_reduce_pro_kernel),
+  // so chunks are cut short enough that no thread sums more than SE_F32_ROWS rows
+  // (ACC-UNet's shapes at 256^2 / 512^2 walk at most 32 -- only larger images get
+  // more chunks)
+  const int cq = (C % 4 == 0) ? C / 4 : C;
+  const int rg = 256 / (cq < 64 ? (cq > 0 ? cq : 1) : 64);
+  const long cap = (long)SE_F32_ROWS * rg;
+  const long need = (HW + cap - 1) / cap;
+  if (need > g.NCH) g.NCH = (int)need;
   g.rows_per = (HW + g.NCH - 1) / g.NCH;
   return g;
 }
@@ -695,8 +707,8 @@ se_bwd_reduce_pro_kernel(const T* __restrict__ z, const T* __restrict__ dout,
   const int b = blockIdx.x / g.NCH, ch = blockIdx.x % g.NCH;
   long r0 = (long)b * g.HW + ch * g.rows_per;
   long r1 = min((long)b * g.HW + g.HW, r0 + g.rows_per);
-  // fp32 sums over the thread's rows (at most a few dozen per chunk), fp64 from the
-  // block reduction on: half the VALU work of per-element fp64 accumulation
+  // fp32 sums over the thread's rows (at most SE_F32_ROWS: se_geom cuts the chunks so),
+  // fp64 from the block reduction on: half the VALU work of per-element fp64 accumulation
   float accf[SE_PRO_NQ][V];
 #pragma unroll
   for (int i = 0; i < SE_PRO_NQ; ++i)

@@ -165,6 +165,8 @@ int accunet_reduce_stats(const double* part, int R, int C, double* out2C, double
  * (the data gradient); with bz/bst/bact (the pre-BN input of norm1 and its state)
  * `stats` then receives the BatchNorm-backward partials (sum g, sum g*(bz - mean)),
  * g = out * act'(bz*scale + shift), for accunet_bn_bwd_part. wgrad writes dW [C][1][3][3] and db [C].
+ * Both return -1 (bad shape) when one image, H*W*C elements as stored, reaches 2 GiB:
+ * the kernels address an image through a 32-bit buffer descriptor.
  * ------------------------------------------------------------------------- */
 /* rows of `stats` ([rows][2][C] fp64) accunet_dw3x3_fwd writes for this shape and
  * storage dtype dt (bf16 runs 64-channel tiles where C % 64 == 0): the forward's norm2

@@ -1,4 +1,4 @@
-"""Worker for tests/test_dist_gpu.py: one rank of a world-2 data-parallel run.
+"""Worker for tests/test_dist_gpu.py: one rank of a world-2 (or world-4) data-parallel run.
 
 Launched by torch.distributed.run with ACCUNET_DIST_BACKEND=gloo so that two ranks
 can share the single GPU of a test box (RCCL refuses two ranks on one device); the
@@ -16,7 +16,9 @@ data-parallel code path is the one bench.py runs over RCCL on a node:
 Checks: parameters identical on both ranks after each mode (bitwise), graph and eager
 identical to each other (bitwise, fp32 and bf16: the same kernels in the same order,
 and a world-2 sum is order-free), the epoch loop equal to eager, and the parameters
-moved.
+moved. World 4 (check_world4): every rank identical after every mode, and one step's
+reduced gradient (fp32 buckets, bf16 buckets, eager reducer) against the fp64 mean of
+the four ranks' own gradients.
 """
 import os
 import sys
@@ -86,9 +88,62 @@ def grads_one_step(sd, batch, dev, wire):
     return torch.cat([p.grad.detach().reshape(-1).double() for p in m.parameters()])
 
 
+def local_grads(sd, batch, dev):
+    """this rank's own (un-reduced) fp32 gradient of one step: plain autograd through
+    the HIP ops, no process group involved"""
+    from accunet.loss import WeightedDiceBCE
+    m = ACC_UNet(3, 1, n_filts=8)
+    m.load_state_dict(sd)
+    m = m.to(dev).train()
+    loss = WeightedDiceBCE(0.5, 0.5)(m(batch[0]), batch[1])
+    loss.backward()
+    torch.cuda.synchronize()
+    return torch.cat([p.grad.detach().reshape(-1) for p in m.parameters()])
+
+
+def eager_grads_one_step(sd, batch, dev):
+    """the all-reduced gradient after one eager step with the bucketed hook reducer"""
+    m = ACC_UNet(3, 1, n_filts=8)
+    m.load_state_dict(sd)
+    m = m.to(dev).train()
+    step = TrainStep(m, lr=1e-3, reducer=adist.GradBucketReducer(m, bucket_mb=0.25))
+    step(*batch)
+    torch.cuda.synchronize()
+    return torch.cat([p.grad.detach().reshape(-1).double() for p in m.parameters()])
+
+
+def check_world4(rank, world, sd, data, dev):
+    """world > 2: the reduced gradient of one step -- graph mode with fp32 and bf16
+    buckets (cut_buckets, 1/world pre-division, SUM), eager hook reducer -- against the
+    fp64 mean of the ranks' own fp32 gradients (all-gathered). fp32 wire and eager:
+    within fp32 rounding of a 4-addend sum; bf16 wire: each addend rounded to bf16 when
+    packed and the partial sums rounded by the collective, so within a few bf16
+    roundings (2^-8 relative) in norm."""
+    mine = local_grads(sd, data[0], dev)
+    allg = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(allg, mine)
+    ref = torch.stack([g.double() for g in allg]).mean(0)
+    ranks_differ = float(max((allg[r] - allg[0]).abs().max() for r in range(1, world)))
+    assert ranks_differ > 0, "rank-specific data should give different local gradients"
+    g32 = grads_one_step(sd, data[0], dev, None)
+    g16 = grads_one_step(sd, data[0], dev, "bf16")
+    ge = eager_grads_one_step(sd, data[0], dev)
+    rn = float(ref.norm())
+    e32 = float((g32 - ref).norm()) / rn
+    e16 = float((g16 - ref).norm()) / rn
+    ee = float((ge - ref).norm()) / rn
+    dge = float((g32 - ge).abs().max())
+    print(f"rank {rank} world {world}: reduced gradient vs fp64 mean of {world} ranks: fp32 "
+          f"buckets {e32:.3e}, eager reducer {ee:.3e}, bf16 buckets {e16:.3e}; graph vs eager "
+          f"max|dg| {dge:.3e}", flush=True)
+    assert e32 <= 1e-6 and ee <= 1e-6, (e32, ee)
+    assert 0 < e16 <= 2 ** -8, e16
+    assert dge <= 1e-6 * float(ref.abs().max()), dge
+
+
 def main():
     rank, world = adist.init_from_env()
-    assert world == 2, world
+    assert world in (2, 4), world
     dev = torch.device("cuda", adist.local_device())
     sd = O.det_state_dict(O.param_spec("canonical", 3, 1, 8), seed=0)
     m0 = ACC_UNet(3, 1, n_filts=8)
@@ -102,13 +157,22 @@ def main():
         p, losses = run(mode, sd, data, dev)
         other = [torch.empty_like(p) for _ in range(world)]
         dist.all_gather(other, p)
-        same = bool(torch.equal(other[0], other[1]))
+        same = all(bool(torch.equal(other[0], o)) for o in other[1:])
         moved = float((p - p0).abs().max())
         out[mode] = (p, losses)
         print(f"rank {rank} {mode}: losses {losses} ranks-identical {same} moved {moved:.3e}",
               flush=True)
         assert same, f"{mode}: parameters differ between ranks"
         assert moved > 1e-5, f"{mode}: parameters did not move"
+    if world > 2:
+        # a sum of 4 addends depends on the collective's order, which follows the bucket
+        # cut (graph and eager buckets differ): compared through one step's gradients
+        check_world4(rank, world, sd, data, dev)
+        dist.barrier()
+        dist.destroy_process_group()
+        if rank == 0:
+            print("DIST_OK", flush=True)
+        return
     for sfx in ("", "_bf16"):
         d = float((out["graph" + sfx][0] - out["eager" + sfx][0]).abs().max())
         print(f"rank {rank} graph{sfx} vs eager{sfx} max|dp| {d:.3e}", flush=True)

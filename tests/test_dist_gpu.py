@@ -38,6 +38,36 @@ def test_world2_graph_and_bucketed_reducer_agree():
 
 
 @pytest.mark.gpu
+def test_world4_buckets_and_wire_against_fp64_mean():
+    """World 4 (four gloo ranks on the one GPU): cut_buckets with the 1/4 pre-division,
+    the bf16 wire with 4 addends and the eager reducer, each reduced gradient against the
+    fp64 mean of the ranks' own gradients (tests/dist_worker.py: check_world4)."""
+    r = _run([os.path.join(HERE, "dist_worker.py")], nproc=4, timeout=400)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "DIST_OK" in r.stdout
+
+
+@pytest.mark.gpu
+def test_bench_gpus4_gloo_reports_four_ranks():
+    """`python bench.py --gpus 4` (gloo, four ranks sharing the GPU): one line from rank 0
+    with ranks_seen 4, the max over the ranks' step times, and 4x the per-rank batch."""
+    env = dict(os.environ, ACCUNET_DIST_BACKEND="gloo", OMP_NUM_THREADS="2")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "4", "--steps", "2", "--warmup", "1",
+                        "--batch", "2", "--size", "64", "--no-probe"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1 and lines[0].startswith('{"metric"'), r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 4 and d["ranks_seen"] == 4 and d["config"]["global_batch"] == 8
+    assert len(d["ms_per_step_per_rank"]) == 4
+    assert abs(d["ms_per_step"] - max(d["ms_per_step_per_rank"])) < 1e-2
+
+
+@pytest.mark.gpu
 def test_rccl_world1_graph_buckets():
     """The RCCL (nccl backend) branch of the graph-mode bucketed all-reduce
     (_GraphBuckets.reduce) on the box's one GPU: >= 3 buckets, fp32 and bf16, bit-equal

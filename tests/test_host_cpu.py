@@ -101,6 +101,18 @@ def test_adam_step_counter_host_logic(monkeypatch):
     monkeypatch.setattr(opt2, "_table", lambda gi, params: (None, None, None, 0))
     opt2.step()
     assert calls[-1] == 4 and float(opt2.state[ps[0]]["step"]) == 4.0
+    # a parameter without a gradient this step keeps its count (torch.optim.Adam's
+    # per-parameter step), the others advance
+    ps[3].grad = None
+    opt2.step()
+    assert float(opt2.state[ps[0]]["step"]) == 5.0
+    assert float(opt2.state[ps[3]]["step"]) == 4.0
+    ps[3].grad = torch.zeros(3)
+    with pytest.raises(RuntimeError):  # it now lags the group: refused, not silently mixed
+        opt2.step()
+    opt2.state[ps[3]]["step"] = torch.tensor(5.0)
+    opt2.step()
+    assert all(float(opt2.state[p]["step"]) == 6.0 for p in ps)
     # mismatched counters are refused, as before
     opt2.state[ps[1]]["step"] = torch.tensor(9.0)
     with pytest.raises(RuntimeError):
@@ -120,6 +132,27 @@ def test_forward_rejects_bad_spatial_size():
         m(torch.zeros(1, 3, 40, 40))
     with pytest.raises(ValueError):
         m(torch.zeros(1, 4, 32, 32))
+
+
+def test_forward_rejects_images_past_the_depthwise_limit():
+    """ACC_UNet.forward names the 2 GiB per-image limit of the depthwise kernels before
+    any launch: canonical cnv72 (4352 hidden channels at H/4) at 1408^2 fp32 is refused,
+    1344^2 passes the check, and bf16 halves the bytes (1408^2 passes)."""
+    m = VARIANTS["canonical"](3, 1)
+    with pytest.raises(ValueError, match="cnv72.*2 GiB"):
+        m.check_input_size(1408, 1408)
+    m.check_input_size(1344, 1344)
+    with pytest.raises(ValueError, match="2 GiB"):
+        m(torch.zeros(1, 3, 1408, 1408))
+    m.set_precision("bf16")
+    m.check_input_size(1408, 1408)
+    with pytest.raises(ValueError, match="cnv72"):
+        m.check_input_size(2048, 2048)
+    # the script preset (cnv72 inv_fctr 3) first hits the limit at a level-0 block
+    s = VARIANTS["script"](3, 1)
+    s.check_input_size(1408, 1408)
+    with pytest.raises(ValueError, match="cnv91"):
+        s.check_input_size(1680, 1680)
 
 
 def _reducer_worker(rank, world, port, q):
@@ -168,13 +201,17 @@ def _reducer_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_grad_bucket_reducer_gloo_world2():
+@pytest.mark.parametrize("world", [2, 3])
+def test_grad_bucket_reducer_gloo_world2(world):
+    """the bucketed hook reducer over gloo: the mean of the ranks' gradients (pre-divided
+    by the world, then summed: the graph path's PreMulSum form, also at world 3 where
+    x/3 and x*(1/3) differ)"""
     import random
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = random.randint(20000, 40000)
-    procs = [ctx.Process(target=_reducer_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_reducer_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in procs]
@@ -330,6 +367,18 @@ def test_abi_host_side_contract_without_a_device():
     assert lib.accunet_dw3x3_fwd(one, one, None, None, None, 0, 1, one, None, 1, 8, 8, 32,
                                  one, None, 0, 0, None) == -2
     assert lib.accunet_gemm(None, None, 0, None) == -2
+    # images of 2 GiB or more are refused (-1) before any launch: the depthwise kernels
+    # address one image with 32-bit offsets. Canonical cnv72 (4352 hidden channels at
+    # H/4) at a 1408^2 input: 352^2 x 4352 fp32 = 2.02 GiB; 1344^2 (336^2) is 1.83 GiB,
+    # the same tensor in bf16 1.01 GiB
+    assert lib.accunet_dw3x3_fwd(one, one, None, None, None, 0, 0, one, None, 1, 352, 352,
+                                 4352, None, None, 0, 0, None) == -1
+    assert lib.accunet_dw3x3_wgrad(one, one, None, None, 0, one, one, 1, 352, 352, 4352, one,
+                                   0, 0, None) == -1
+    assert lib.accunet_dw3x3_fwd(one, one, None, None, None, 0, 0, one, None, 1, 352, 352,
+                                 4352, one, None, 0, 1, None) == -2  # bf16: bz check next
+    assert lib.accunet_dw3x3_fwd(one, one, None, None, None, 0, 1, one, None, 1, 336, 336,
+                                 4352, one, None, 0, 0, None) == -2
     # 16x256x256x96: one-shot tiles of 8 rows x 32 pixels -> 16 * 32 * 8 = 4096 statistics
     # rows (the strip kernel, ACCUNET_DW_OS=0: 32-row strips, 1024); cnv11's 9 channels
     # the register kernel

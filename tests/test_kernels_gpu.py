@@ -301,3 +301,82 @@ def test_bucket_packing_copies_aligned_and_ragged():
     torch.cuda.synchronize()
     for s_, dst, sc in cases:
         assert torch.equal(dst, (s_ * sc).to(dst.dtype)), (dst.dtype, dst.numel(), sc)
+
+
+def _two_pass(z, C, rv0, mom=0.1, eps=1e-5):
+    """ATen's BatchNorm2d training statistics restated in fp64, two passes over the
+    stored values: mean, rstd (of the biased variance) and the running_var update with
+    the unbiased variance."""
+    zz = z.double().reshape(-1, C).cpu()
+    n = zz.shape[0]
+    m = zz.mean(0)
+    v = ((zz - m) ** 2).mean(0)
+    rstd = 1.0 / torch.sqrt(v + eps)
+    rv = (1 - mom) * rv0.double().cpu() + mom * v * n / (n - 1)
+    return m, rstd, rv, v
+
+
+def _finish_and_compare(st, rows, z, C, tag):
+    kern = _kern()
+    dev = z.device
+    P = z.numel() // C
+    gamma = torch.ones(C, device=dev)
+    beta = torch.zeros(C, device=dev)
+    rmean = torch.zeros(C, device=dev)
+    rv0 = torch.linspace(0.5, 2.0, C, device=dev)
+    rvar = rv0.clone()
+    nbt = torch.zeros((), dtype=torch.long, device=dev)
+    out = torch.empty(4, C, device=dev)
+    kern.bn_finalize(st, rows, C, float(P), gamma, beta, rmean, rvar, nbt, 0.1, 1e-5, True, out)
+    torch.cuda.synchronize()
+    m, rstd, rv, v = _two_pass(z, C, rv0)
+    # the test is only meaningful if the channels really are offset: mean >= 300 x spread
+    assert float((m.abs() / v.sqrt()).min()) >= 300, tag
+    got_m, got_r = out[0].double().cpu(), out[1].double().cpu()
+    assert float(((got_m - m) / m).abs().max()) <= 1e-6, (tag, "mean")
+    rel_r = float(((got_r - rstd) / rstd).abs().max())
+    assert rel_r <= 1e-6, (tag, "rstd", rel_r)
+    rel_v = float(((rvar.double().cpu() - rv) / rv).abs().max())
+    assert rel_v <= 1e-6, (tag, "running_var", rel_v)
+    assert int(nbt) == 1
+
+
+@pytest.mark.parametrize("B,H,W,C", [(2, 32, 48, 96), (16, 256, 256, 96)])
+def test_bn_statistics_large_mean_match_two_pass_fp64(B, H, W, C):
+    """BatchNorm statistics (ATen's two-pass fp64 BatchNorm at e.g.
+    ACC_UNet/ACC_UNet.py:274) from the producers' partial sums plus the finish kernel,
+    on channels whose mean is ~300-1000x their spread -- the case where sum z^2 - n m^2
+    from fp32 partials would cancel: K1 (the depthwise forward, strip kernel at the small
+    shape, one-shot tiles at the north-star 16x256^2x96), a GEMM epilogue and the
+    materialising affine pass. Mean, rstd and running_var within 1e-6 relative of a
+    two-pass fp64 computation over the stored values."""
+    kern = _kern()
+    g = torch.Generator().manual_seed(7)
+    P = B * H * W
+    # K1: x ~ N(0,1), weights of norm ~0.35, bias ~300 -> z ~ 300 +- 0.35 (a large bias,
+    # not a large input: the zero-padded border keeps the per-channel spread small)
+    x = torch.randn(B, H, W, C, generator=g).to(DEV)
+    wt = (1.0 / 9 + 0.02 * torch.randn(C, 1, 3, 3, generator=g)).to(DEV)
+    bias = (300.0 + 0.1 * torch.randn(C, generator=g)).to(DEV)
+    z = torch.empty_like(x)
+    rows = kern.dw3x3_rows(B, H, W, C, x)
+    st = torch.zeros(rows, 2, C, dtype=torch.float64, device=DEV)
+    kern.dw3x3_fwd(x, wt, bias, None, None, 0, 0, z, st, B, H, W, C)
+    _finish_and_compare(st, rows, z, C, f"dw3x3 {kern.dw3x3_kernel_name(B, H, W, C)}")
+    # GEMM epilogue: z = a W^T + 300, spread ~0.4
+    K, N = 64, 96
+    a = torch.randn(P, K, generator=g).to(DEV)
+    w = (0.05 * torch.randn(N, K, generator=g)).to(DEV)
+    b2 = torch.full((N,), 300.0, device=DEV)
+    zg = torch.empty(P, N, device=DEV)
+    rg = kern.gemm_stats_rows(P, N, K)
+    sg = torch.zeros(rg, 2, N, dtype=torch.float64, device=DEV)
+    kern.gemm(P, N, K, a=[a], lda=[K], b=w, ldb=K, c=zg, ldc=N, bias=b2, stats=sg)
+    _finish_and_compare(sg, rg, zg, N, "gemm epilogue")
+    # the materialising BatchNorm+act pass with statistics of its output (y = x + 300)
+    y = torch.empty_like(x)
+    ra = kern.stream_rows(P, C)
+    sa = torch.zeros(ra, 2, C, dtype=torch.float64, device=DEV)
+    ones = torch.ones(C, device=DEV)
+    kern.affine_act(x, ones, torch.full((C,), 300.0, device=DEV), 0, None, y, P, C, sa)
+    _finish_and_compare(sa, ra, y, C, "affine_act")
