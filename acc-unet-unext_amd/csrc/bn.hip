@@ -172,6 +172,7 @@ static int stream_bank(hipStream_t s) {
     if (g_bank_stream[i] == s) return g_bank_of[i];
   return 0;
 }
+int acc_stream_bank(hipStream_t s) { return stream_bank(s); }
 
 ACC_DEV void fin_column(const FinishArgs& fa, int col, double tot) {
   switch (fa.kind) {

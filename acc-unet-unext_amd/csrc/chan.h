@@ -1,5 +1,6 @@
 // Channel-tiled streaming helpers shared by the NHWC elementwise / reduction kernels.
 #pragma once
+#include <type_traits>
 #include "common.h"
 
 // --------------------------------------------------------------------------
@@ -102,10 +103,15 @@ ACC_DEV void quad_rows2(const T* base1, const T* base2, long nrows, int rg, int 
 }
 
 // Reduce per-thread (a[V], b[V]) across the RG row-groups of the block and write
-// the block's partial row out[(row)*2*C + {0,C} + c].
-template <int V, typename T>
+// the block's partial row out[(row)*2*C + {0,C} + c]. WT: write-through stores (a
+// last-arriving block of the same launch reads the row, handoff_last in common.h).
+template <typename T>
+ACC_DEV void chan_out(T* p, T v, std::false_type) { *p = v; }
+ACC_DEV void chan_out(double* p, double v, std::true_type) { st_wt(p, v); }
+template <int V, typename T, bool WT = false>
 ACC_DEV void block_chan_reduce2(const ChanTile& t, T (&a)[V], T (&b)[V], T* out, long row,
                                 int C) {
+  using W = std::integral_constant<bool, WT>;
   __shared__ T red[2][256 * 4];
   int tid = threadIdx.x;
   if ((t.TCQ & (t.TCQ - 1)) == 0) {
@@ -135,8 +141,8 @@ ACC_DEV void block_chan_reduce2(const ChanTile& t, T (&a)[V], T (&b)[V], T* out,
           sa += red[0][(w * 64 + tid) * V + j];
           sb += red[1][(w * 64 + tid) * V + j];
         }
-        out[row * 2 * C + t.c0 + j] = sa;
-        out[row * 2 * C + C + t.c0 + j] = sb;
+        chan_out(&out[row * 2 * C + t.c0 + j], sa, W{});
+        chan_out(&out[row * 2 * C + C + t.c0 + j], sb, W{});
       }
     }
     return;
@@ -156,8 +162,8 @@ ACC_DEV void block_chan_reduce2(const ChanTile& t, T (&a)[V], T (&b)[V], T* out,
         sa += red[0][(g * t.TCQ + lt) * V + j];
         sb += red[1][(g * t.TCQ + lt) * V + j];
       }
-      out[row * 2 * C + t.c0 + j] = sa;
-      out[row * 2 * C + C + t.c0 + j] = sb;
+      chan_out(&out[row * 2 * C + t.c0 + j], sa, W{});
+      chan_out(&out[row * 2 * C + C + t.c0 + j], sb, W{});
     }
   }
 }
@@ -165,8 +171,9 @@ ACC_DEV void block_chan_reduce2(const ChanTile& t, T (&a)[V], T (&b)[V], T* out,
 // N-quantity version of block_chan_reduce2: per-thread v[i][V] (i < N) reduced over
 // the block's row groups into out[(row*N + i)*C + c], one quantity at a time through
 // one LDS buffer (same deterministic order as block_chan_reduce2).
-template <int V, int N, typename T>
+template <int V, int N, typename T, bool WT = false>
 ACC_DEV void block_chan_reduceN(const ChanTile& t, T (&v)[N][V], T* out, long row, int C) {
+  using W = std::integral_constant<bool, WT>;
   __shared__ T red[256 * 4];
   const int tid = threadIdx.x;
   const bool p2 = (t.TCQ & (t.TCQ - 1)) == 0;
@@ -188,7 +195,7 @@ ACC_DEV void block_chan_reduceN(const ChanTile& t, T (&v)[N][V], T* out, long ro
         for (int j = 0; j < V; ++j) {
           T s = 0;
           for (int w = 0; w < 4; ++w) s += red[(w * 64 + tid) * V + j];
-          out[(row * N + i) * C + t.c0 + j] = s;
+          chan_out(&out[(row * N + i) * C + t.c0 + j], s, W{});
         }
       }
     } else {
@@ -201,7 +208,7 @@ ACC_DEV void block_chan_reduceN(const ChanTile& t, T (&v)[N][V], T* out, long ro
         for (int j = 0; j < V; ++j) {
           T s = 0;
           for (int g = 0; g < t.RG; ++g) s += red[(g * t.TCQ + lt) * V + j];
-          out[(row * N + i) * C + t.c0 + j] = s;
+          chan_out(&out[(row * N + i) * C + t.c0 + j], s, W{});
         }
       }
     }

@@ -47,5 +47,7 @@ struct FinishArgs {
 };
 // chunks: fp64 scratch of reduce_finish_ws(R, stride) doubles, 8-byte aligned
 size_t reduce_finish_ws(int R, int stride);
+// ticket bank (0 / 1) of launches enqueued on stream s (accunet_stream_ticket_bank)
+int acc_stream_bank(hipStream_t s);
 int reduce_finish(const void* part, bool part_f64, int R, int stride, double* chunks,
                   const FinishArgs& fa, hipStream_t s);

@@ -212,7 +212,8 @@ def test_dw3x3_span_forward_knob_vs_fp64():
     assert r.returncode == 0 and "SPAN_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
 
 
-@pytest.mark.parametrize("B,H,C", [(4, 16, 64), (2, 8, 32), (16, 32, 256), (3, 5, 40), (2, 8, 18)])
+@pytest.mark.parametrize("B,H,C", [(4, 16, 64), (2, 8, 32), (16, 32, 256), (3, 5, 40), (2, 8, 18),
+                                   (2, 8, 512), (16, 64, 32)])
 def test_se_layer_vs_fp64_oracle(B, H, C):
     """ChannelSELayer (fused GAP / gate / BN-of-gated / LeakyReLU, and its backward) vs
     the fp64 oracle; tolerance relative to the reference's own fp32 error."""
@@ -373,10 +374,10 @@ def test_bn_statistics_large_mean_match_two_pass_fp64(B, H, W, C):
     sg = torch.zeros(rg, 2, N, dtype=torch.float64, device=DEV)
     kern.gemm(P, N, K, a=[a], lda=[K], b=w, ldb=K, c=zg, ldc=N, bias=b2, stats=sg)
     _finish_and_compare(sg, rg, zg, N, "gemm epilogue")
-    # the materialising BatchNorm+act pass with statistics of its output (y = x + 300)
+    # the materialising BatchNorm+act pass with statistics of its output (y = 0.3 x + 300)
     y = torch.empty_like(x)
     ra = kern.stream_rows(P, C)
     sa = torch.zeros(ra, 2, C, dtype=torch.float64, device=DEV)
-    ones = torch.ones(C, device=DEV)
-    kern.affine_act(x, ones, torch.full((C,), 300.0, device=DEV), 0, None, y, P, C, sa)
+    kern.affine_act(x, torch.full((C,), 0.3, device=DEV), torch.full((C,), 300.0, device=DEV), 0,
+                    None, y, P, C, sa)
     _finish_and_compare(sa, ra, y, C, "affine_act")
