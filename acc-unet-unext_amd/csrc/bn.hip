@@ -213,6 +213,16 @@ ACC_DEV void fin_bn_fwd(const FinishArgs& fa, int c, double s1, double s2) {
   st[BN_SHIFT * C + c] = be - mean * sc;
 }
 
+// Bias gradient of the convolution whose output x feeds only a BatchNorm (training or
+// eval): sum_p dx with dx = k1*g + k2*(x - mean) + k3 is k1*sum g + count*k3 exactly,
+// save the k2 * sum (x - mean) term, which vanishes but for the rounding of the fp32
+// mean (the batch mean in training; eval has k2 = k3 = 0). ATen gets the same value,
+// zero up to rounding in training, as an fp32 column sum of dx; the column-sum pass and
+// its reduction are gone (ACC_UNet.py conv biases before every BatchNorm).
+ACC_DEV float bn_dsum(float k1, float k3, double s1, double count) {
+  return (float)((double)k1 * s1 + count * (double)k3);
+}
+
 // BatchNorm backward finish: (sum g, sum g*xhat | g*(x-mean)) -> dgamma, dbeta, coef
 ACC_DEV void fin_bn_bwd(const FinishArgs& fa, int c, double s1, double s2) {
   const int C = fa.ncols;
@@ -233,6 +243,10 @@ ACC_DEV void fin_bn_bwd(const FinishArgs& fa, int c, double s1, double s2) {
   fa.out_f[c] = k1;
   fa.out_f[C + c] = k2;
   fa.out_f[2 * C + c] = k3;
+  // sum_p dx = k1 sum g + k2 sum (x - mean) + count k3, and sum (x - mean) = 0 up to the
+  // rounding of the stored mean: the bias gradient of the convolution feeding this
+  // BatchNorm (bn_dsum) without a column-sum pass over dx
+  if (fa.out4) fa.out4[c] = bn_dsum(k1, k3, s1, fa.count);
 }
 
 // 256 threads = FIN_COLS columns x FIN_GROUPS row groups: with 8 loads in flight per
@@ -619,16 +633,10 @@ template <int V, typename T>
 __global__ void __launch_bounds__(256)
 bn_bwd_apply_kernel(const T* __restrict__ x, const T* __restrict__ dy,
                     const float* __restrict__ st, const float* __restrict__ coef, int act,
-                    long P, int C, T* __restrict__ dx, int accumulate,
-                    double* __restrict__ colsum) {
+                    long P, int C, T* __restrict__ dx, int accumulate) {
   ChanTile t = chan_tile<V>(C);
   long rows_per = (P + gridDim.x - 1) / gridDim.x;
   long r0 = blockIdx.x * rows_per, r1 = min(P, r0 + rows_per);
-  // optional fp64 column sums of the written d: sum_p dx = the bias gradient of the
-  // convolution that produced x (its output feeds only this BatchNorm)
-  double a[V], b[V];
-#pragma unroll
-  for (int j = 0; j < V; ++j) { a[j] = 0.0; b[j] = 0.0; }
   if (t.active) {
     float s[V], h[V], k1[V], k2[V], k3[V], mu[V];
 #pragma unroll
@@ -647,10 +655,7 @@ bn_bwd_apply_kernel(const T* __restrict__ x, const T* __restrict__ dy,
         float g = dv[j];
         if (act == ACT_LRELU) g *= lrelu_d(xv[j] * s[j] + h[j]);
         float d = k1[j] * g + k2[j] * (xv[j] - mu[j]) + k3[j];
-        // statistics describe the stored tensor (bf16: the rounded value)
-        const float dd = rnd<T>(d);
-        if (colsum && ok) a[j] += accumulate ? d : dd;
-        o[j] = accumulate ? rnd<T>(o[j] + d) : dd;
+        o[j] = accumulate ? rnd<T>(o[j] + d) : rnd<T>(d);
       }
     };
     auto plain = [&]() {
@@ -682,7 +687,16 @@ bn_bwd_apply_kernel(const T* __restrict__ x, const T* __restrict__ dy,
       plain();
     }
   }
-  if (colsum) block_chan_reduce2<V>(t, a, b, colsum, blockIdx.x, C);
+}
+
+// row blocks of the BatchNorm-backward apply pass: no block cap (it writes no partial
+// rows any more): 16x65536x32 fp32 89 -> 78 us against 1024 blocks (r05_stream_ab.txt)
+static int apply_rowblocks(long P, int C) {
+  long want = P * (long)C / (256 * 16);
+  if (want < 1) want = 1;
+  if (want > P) want = P;
+  if (want > (1L << 20)) want = 1L << 20;
+  return (int)want;
 }
 
 extern "C" size_t accunet_bn_bwd_ws_elems(long P, int C) {
@@ -690,21 +704,11 @@ extern "C" size_t accunet_bn_bwd_ws_elems(long P, int C) {
   return (size_t)nb * 2 * C * 2 + accunet_partials_ws_elems(nb, 2 * C) * 2 + 3 * (size_t)C;
 }
 
-// dsum (optional, [C]): sum over pixels of dx (fp64 partials in the apply pass, reduced
-// after it into the stats workspace, which the finalize no longer needs by then)
-static int bn_dsum_finish(double* part, int nb, int C, double* scratch, float* dsum,
-                          hipStream_t s) {
-  FinishArgs fa{};
-  fa.kind = FIN_SUM_F;
-  fa.ncols = C;
-  fa.out_f = dsum;
-  return reduce_finish(part, true, nb, 2 * C, scratch, fa, s);
-}
-
 // BatchNorm backward finish arguments (see fin_bn_bwd)
 static FinishArgs bn_bwd_fin(int C, long P, const float* st, const float* gamma, int training,
-                             float* dgamma, float* dbeta, float* coef, int xc_form) {
+                             float* dgamma, float* dbeta, float* coef, int xc_form, float* dsum) {
   FinishArgs fa{};
+  fa.out4 = dsum;
   fa.kind = FIN_BN_BWD;
   fa.ncols = C;
   fa.count = (double)P;
@@ -745,19 +749,18 @@ extern "C" int accunet_bn_bwd(const void* x, const void* dy, const float* st,
                          (const T*)dy, st, act, P, C, part);
   });
   int rc = reduce_finish(part, true, nb, 2 * C, scratch,
-                         bn_bwd_fin(C, P, st, gamma, training, dgamma, dbeta, coef, 0), s);
+                         bn_bwd_fin(C, P, st, gamma, training, dgamma, dbeta, coef, 0, dsum), s);
   if (rc != ACC_OK) return rc;
-  double* cpart = dsum ? part : nullptr;  // the reduce partials are consumed by now
+  const dim3 agrid(apply_rowblocks(P, C), grid.y);
   with_dt(dt, [&](auto tag) {
     using T = decltype(tag);
     if (V == 4)
-      hipLaunchKernelGGL((bn_bwd_apply_kernel<4, T>), grid, dim3(256), 0, s, (const T*)x,
-                         (const T*)dy, st, coef, act, P, C, (T*)dx, accumulate, cpart);
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<4, T>), agrid, dim3(256), 0, s, (const T*)x,
+                         (const T*)dy, st, coef, act, P, C, (T*)dx, accumulate);
     else
-      hipLaunchKernelGGL((bn_bwd_apply_kernel<1, T>), grid, dim3(256), 0, s, (const T*)x,
-                         (const T*)dy, st, coef, act, P, C, (T*)dx, accumulate, cpart);
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<1, T>), agrid, dim3(256), 0, s, (const T*)x,
+                         (const T*)dy, st, coef, act, P, C, (T*)dx, accumulate);
   });
-  if (dsum) return bn_dsum_finish(part, nb, C, scratch, dsum, s);
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 
@@ -795,18 +798,20 @@ extern "C" int accunet_bn_bwd_part(const void* x, const void* dy, const float* s
   double* cpart = reinterpret_cast<double*>(ws + scr_f + bn_coef_floats(C));
   double* cscr = cpart + (size_t)nb * 2 * C;
   int rc = reduce_finish(part, true, R, 2 * C, scratch,
-                         bn_bwd_fin(C, P, st, gamma, training, dgamma, dbeta, coef, 1), s);
+                         bn_bwd_fin(C, P, st, gamma, training, dgamma, dbeta, coef, 1, dsum), s);
   if (rc != ACC_OK) return rc;
+  (void)cpart;
+  (void)cscr;
+  const dim3 agrid(apply_rowblocks(P, C), grid.y);
   with_dt(dt, [&](auto tag) {
     using T = decltype(tag);
     if (V == 4)
-      hipLaunchKernelGGL((bn_bwd_apply_kernel<4, T>), grid, dim3(256), 0, s, (const T*)x,
-                         (const T*)dy, st, coef, act, P, C, (T*)dx, 0, dsum ? cpart : nullptr);
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<4, T>), agrid, dim3(256), 0, s, (const T*)x,
+                         (const T*)dy, st, coef, act, P, C, (T*)dx, 0);
     else
-      hipLaunchKernelGGL((bn_bwd_apply_kernel<1, T>), grid, dim3(256), 0, s, (const T*)x,
-                         (const T*)dy, st, coef, act, P, C, (T*)dx, 0, dsum ? cpart : nullptr);
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<1, T>), agrid, dim3(256), 0, s, (const T*)x,
+                         (const T*)dy, st, coef, act, P, C, (T*)dx, 0);
   });
-  if (dsum) return bn_dsum_finish(cpart, nb, C, cscr, dsum, s);
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 

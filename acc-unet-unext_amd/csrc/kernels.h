@@ -43,6 +43,7 @@ struct FinishArgs {
   double* out_d;     // FIN_SUM_D totals
   float* out2;       // FIN_DW / FIN_HEAD: db ; FIN_BN_BWD: dgamma
   float* out3;       // FIN_BN_BWD: dbeta
+  float* out4;       // FIN_BN_BWD: sum_p dx (the producer convolution's bias gradient), or null
   int bank;          // ticket bank (set by reduce_finish from the launch stream)
 };
 // chunks: fp64 scratch of reduce_finish_ws(R, stride) doubles, 8-byte aligned

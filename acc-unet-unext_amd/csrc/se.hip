@@ -387,6 +387,7 @@ struct SeBwdMid {
   const float *pst, *pgamma;
   int ptraining;
   float *dpg, *dpb, *pcoef;
+  float* dsum;  // sum_p dz: the bias gradient of z's producer (bn_dsum), or null
 };
 
 ACC_DEV double* se_T1(const SeGeom& g, const SeBwdMid& m) {
@@ -610,6 +611,9 @@ ACC_DEV void se_pro_coef_body(const SeGeom& g, const SeBwdMid& m, int c) {
   m.pcoef[c] = k1;
   m.pcoef[C + c] = k2;
   m.pcoef[2 * C + c] = k3;
+  // sum_p dz = k1 sum g + n k3 (+ k2 sum (z - mean1) = 0 up to the mean's rounding), as
+  // bn_dsum in csrc/bn.hip: no column-sum pass over dz
+  if (m.dsum) m.dsum[c] = (float)((double)k1 * sg + n * (double)k3);
 }
 
 // Per-sample tickets of the folded backward: [bank][sample], then one launch-wide
@@ -960,7 +964,8 @@ extern "C" int accunet_se_bwd(const void* z, const void* dout, const float* sc, 
   unsigned* tk = se_bwd_tickets(s);
   if (!tk) return ACC_ELAUNCH;
   SeBwdMid m{Cr, w1, w2, gamma, training, const_cast<float*>(save), scratch, coef,
-             dw1, db1, dw2, db2, dgamma, dbeta, nullptr, nullptr, 0, nullptr, nullptr, nullptr};
+             dw1, db1, dw2, db2, dgamma, dbeta, nullptr, nullptr, 0, nullptr, nullptr, nullptr,
+             nullptr};
   with_dt(dt, [&](auto tag) {
     using T = decltype(tag);
     if (V == 4)
@@ -1010,7 +1015,8 @@ extern "C" int accunet_se_bwd_pro(const void* z, const void* dout, const float* 
   const float* sgate = save + (size_t)B * C * 4 + (size_t)B * Cr;
   const float* mean = sgate + (size_t)B * C;
   SeBwdMid m{Cr, w1, w2, gamma, training, const_cast<float*>(save), scratch, coef,
-             dw1, db1, dw2, db2, dgamma, dbeta, pst, pgamma, ptraining, dpgamma, dpbeta, pcoef};
+             dw1, db1, dw2, db2, dgamma, dbeta, pst, pgamma, ptraining, dpgamma, dpbeta, pcoef,
+             dsum};
   if (B > SE_MAX_B) return ACC_EBADSHAPE;
   unsigned* tk = se_bwd_tickets(s);
   if (!tk) return ACC_ELAUNCH;
@@ -1023,8 +1029,7 @@ extern "C" int accunet_se_bwd_pro(const void* z, const void* dout, const float* 
       hipLaunchKernelGGL((se_bwd_reduce_pro_kernel<1, T>), grid, dim3(256), 0, s, (const T*)z,
                          (const T*)dout, pst, act, g, alpha, betap, part, m, tk);
   });
-  // the reduce-pass partials are consumed by the middle step: reuse them for dz's column sums
-  double* cpart = dsum ? part : nullptr;
+  double* cpart = nullptr;  // (dz's column sums: computed analytically, se_pro_coef_body)
   with_dt(dt, [&](auto tag) {
     using T = decltype(tag);
     if (V == 4)
@@ -1036,12 +1041,6 @@ extern "C" int accunet_se_bwd_pro(const void* z, const void* dout, const float* 
                          (const T*)dout, pst, act, g, alpha, betap, sgate, mean, coef, pcoef, (T*)dz,
                          cpart);
   });
-  if (dsum) {
-    FinishArgs fa{};
-    fa.kind = FIN_SUM_F;
-    fa.ncols = C;
-    fa.out_f = dsum;
-    return reduce_finish(cpart, true, B * g.NCH, 2 * C, dscr, fa, s);
-  }
+  (void)dscr;
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
