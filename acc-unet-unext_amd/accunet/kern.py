@@ -281,7 +281,7 @@ def dw3x3_rows(B, H, W, C, like: torch.Tensor, bnb: bool = False) -> int:
     return int(_lib_raw().accunet_dw3x3_rows(B, H, W, C, _dt(like), 1 if bnb else 0))
 
 
-_DW_NAMES = {3: "dw3x3_os_fwd_kernel", 2: "dw3x3_span_fwd_kernel", 1: "dw3x3_tile_fwd_kernel", 0: "dw3x3_fwd_kernel"}
+_DW_NAMES = {4: "dw3x3_os16_fwd_kernel", 3: "dw3x3_os_fwd_kernel", 2: "dw3x3_span_fwd_kernel", 1: "dw3x3_tile_fwd_kernel", 0: "dw3x3_fwd_kernel"}
 
 
 def dw3x3_kernel_name(B, H, W, C, like=None) -> str:

@@ -962,6 +962,205 @@ dw3x3_os_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
   }
 }
 
+// ----------------------------------------------------------------------------
+// K1 one-shot tiles of 16 rows (fp32 forward / plain data gradient; no BN-backward
+// form). A 512-thread block owns 16 output rows x TP pixels x TCQ quads as two halves of
+// 256 threads with 8 output rows each: every input row of the tile (18 with the halo) is
+// fetched once -- each half loads its own 9 rows, the rows the halves share cross through
+// the LDS exchange tile -- so a tile re-fetches 2 of 18 input rows from its neighbours'
+// fetches instead of 2 of 10, and the statistics tail (shuffles, the cross-wave slab, one
+// partial row) is paid once per 16 rows. The centre column comes from LDS too (no
+// register copy), so a thread stays within 128 VGPRs: 2 blocks = 4 waves per SIMD in
+// 2 x 78 KB of LDS. Per output the sum is bias, then the taps row-major: z bit-identical
+// to the 8-row tiles and the strip kernel.
+// ----------------------------------------------------------------------------
+template <int TCQ, typename T>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
+dw3x3_os16_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
+                      const float* __restrict__ bias, const float* __restrict__ sc,
+                      const float* __restrict__ sh, int act, int flip, T* __restrict__ z,
+                      double* __restrict__ stats, DwOGeom g) {
+  constexpr int R = 8, HR = R + 1;  // output rows / own input rows per half
+  constexpr int TP = 256 / TCQ, IP = TP + 2, IR = 2 * R + 2;
+  constexpr int NH = (2 * TCQ * IR + 511) / 512;  // halo loads per lane
+  typedef typename QuadRaw<T>::type RawQ;
+  __shared__ float4 xb[IR][IP][TCQ];
+  const int tid = threadIdx.x, half = tid >> 8, ht = tid & 255;
+  const int q = ht % TCQ, p = ht / TCQ;
+  int t = (int)blockIdx.x;
+  const int cg = t % g.ncg;
+  t /= g.ncg;
+  const int srow = t;  // statistics partial row of this tile
+  const int tw = t % g.tilesW;
+  t /= g.tilesW;
+  const int th = t % g.tilesH;
+  const int b = t / g.tilesH;
+  const int c0 = cg * TCQ * 4, c = c0 + 4 * q;
+  const int w0 = tw * TP, w = w0 + p, h0 = th * 2 * R;
+  const long img = (long)b * g.H * g.W * g.C;
+  const unsigned ibytes = (unsigned)(g.H * g.W * g.C * (int)sizeof(T));
+  const __amdgpu_buffer_rsrc_t rx = acc_rsrc(x + img, ibytes);
+  const __amdgpu_buffer_rsrc_t rz = acc_rsrc(z + img, ibytes);
+  const bool pro = sc != nullptr;
+  const bool win = w < g.W;
+  // this half's own column: input rows h0 - 1 + half*HR + r (LDS rows half*HR + r)
+  RawQ own[HR], hv[NH];
+#pragma unroll
+  for (int r = 0; r < HR; ++r) {
+    const int i = h0 - 1 + half * HR + r;
+    const bool in = win && i >= 0 && i < g.H;
+    own[r] = bufq_ld<0>(rx, in ? (unsigned)(((i * g.W + w) * g.C + c) * (int)sizeof(T)) : ACC_OOB,
+                        (const T*)nullptr);
+  }
+  auto halo = [&](int m, int& hr, int& hs, int& hq, int& hw, int& hi) {
+    const int e = tid + 512 * m;  // halo element: (row, side, quad)
+    hr = e / (2 * TCQ);
+    hs = (e / TCQ) & 1;
+    hq = e % TCQ;
+    hw = hs ? w0 + TP : w0 - 1;
+    hi = h0 - 1 + hr;
+    return e < 2 * TCQ * IR && hw >= 0 && hw < g.W && hi >= 0 && hi < g.H;
+  };
+#pragma unroll
+  for (int m = 0; m < NH; ++m) {
+    int hr, hs, hq, hw, hi;
+    const bool in = halo(m, hr, hs, hq, hw, hi);
+    hv[m] = bufq_ld<0>(rx, in ? (unsigned)(((hi * g.W + hw) * g.C + c0 + 4 * hq) * (int)sizeof(T))
+                              : ACC_OOB, (const T*)nullptr);
+  }
+  float4 ps = make_float4(1.f, 1.f, 1.f, 1.f), pb = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (pro) {
+    ps = ld4(sc + c);
+    pb = ld4(sh + c);
+  }
+  const DwPro P = dw_pro(ps, pb, pro, act);
+  const bool interior = h0 >= 1 && h0 + 2 * R + 1 <= g.H && w0 + TP <= g.W;
+  if (interior) {
+#pragma unroll
+    for (int r = 0; r < HR; ++r) xb[half * HR + r][p + 1][q] = dw_act(P, q2f(own[r]));
+  } else {
+#pragma unroll
+    for (int r = 0; r < HR; ++r) {
+      const int i = h0 - 1 + half * HR + r;
+      xb[half * HR + r][p + 1][q] = dw_keep(win && i >= 0 && i < g.H, dw_act(P, q2f(own[r])));
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < NH; ++m) {
+    int hr, hs, hq, hw, hi;
+    const bool in = halo(m, hr, hs, hq, hw, hi);
+    // (512 % TCQ == 0: a halo lane's quad hq is its own quad q, so its prologue too)
+    if (tid + 512 * m < 2 * TCQ * IR) xb[hr][hs ? IP - 1 : 0][hq] = dw_keep(in, dw_act(P, q2f(hv[m])));
+  }
+  // weights and bias (needed from the taps on; loaded behind the tile's stores)
+  float k[9][4], bi[4];
+  {
+    float wv[36];
+#pragma unroll
+    for (int e = 0; e < 9; ++e) {
+      const float4 w4 = ld4(wt + c * 9 + 4 * e);
+      wv[4 * e] = w4.x; wv[4 * e + 1] = w4.y; wv[4 * e + 2] = w4.z; wv[4 * e + 3] = w4.w;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int tp = 0; tp < 9; ++tp) k[tp][j] = wv[j * 9 + (flip ? 8 - tp : tp)];
+    const float4 b4 = bias ? ld4(bias + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    bi[0] = b4.x; bi[1] = b4.y; bi[2] = b4.z; bi[3] = b4.w;
+  }
+  __syncthreads();
+  typedef dwf2 f2v;
+  float a0[4] = {0.f, 0.f, 0.f, 0.f}, a1[4] = {0.f, 0.f, 0.f, 0.f};
+  // statistics as in dw3x3_os_fwd_kernel: fp32 sums of z - pv (pv wave-uniform per quad)
+  f2v c1[2] = {{0.f, 0.f}, {0.f, 0.f}}, c2[2] = {{0.f, 0.f}, {0.f, 0.f}}, pv[2] = {{0.f, 0.f}, {0.f, 0.f}};
+  float cnt = 0.f;
+  auto taps = [&](auto interior_c) {
+    constexpr bool IN = decltype(interior_c)::value;
+    auto row = [&](int j, float (&o)[4]) {
+      const int lr = half * R + j;  // LDS row of input row h0 - 1 + lr
+      const float4 L = xb[lr][p][q], Cm = xb[lr][p + 1][q], Rr = xb[lr][p + 2][q];
+      const float vL[4] = {L.x, L.y, L.z, L.w};
+      const float vC[4] = {Cm.x, Cm.y, Cm.z, Cm.w};
+      const float vR[4] = {Rr.x, Rr.y, Rr.z, Rr.w};
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        float t0 = a0[jj], t1 = a1[jj], t2 = bi[jj];
+        t0 = fmaf(k[6][jj], vL[jj], t0); t0 = fmaf(k[7][jj], vC[jj], t0); t0 = fmaf(k[8][jj], vR[jj], t0);
+        t1 = fmaf(k[3][jj], vL[jj], t1); t1 = fmaf(k[4][jj], vC[jj], t1); t1 = fmaf(k[5][jj], vR[jj], t1);
+        t2 = fmaf(k[0][jj], vL[jj], t2); t2 = fmaf(k[1][jj], vC[jj], t2); t2 = fmaf(k[2][jj], vR[jj], t2);
+        a0[jj] = t1;
+        a1[jj] = t2;
+        o[jj] = rnd<T>(t0);  // statistics of the stored value
+      }
+    };
+    float o[4];
+    row(0, o);  // the first two input rows only start outputs
+    row(1, o);
+    // (rolled: an unrolled loop hoists the LDS reads of every row and spills at 128 VGPRs)
+#pragma unroll 2
+    for (int j = 2; j < R + 2; ++j) {
+      row(j, o);
+      const int h = h0 + half * R + j - 2;  // output row completed by this input row
+      const bool on = IN || (win && h < g.H);
+      if (j == 2) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          pv[e].x = __shfl(o[2 * e], q, 64);
+          pv[e].y = __shfl(o[2 * e + 1], q, 64);
+        }
+      }
+      f2v m01 = f2v{o[0], o[1]} - pv[0], m23 = f2v{o[2], o[3]} - pv[1];
+      if (!IN) {
+        m01 = on ? m01 : f2v{0.f, 0.f};
+        m23 = on ? m23 : f2v{0.f, 0.f};
+        cnt += on ? 1.f : 0.f;
+      }
+      c1[0] += m01;
+      c1[1] += m23;
+      c2[0] = m01 * m01 + c2[0];
+      c2[1] = m23 * m23 + c2[1];
+      bufq_st<2>(rz, on ? (unsigned)(((h * g.W + w) * g.C + c) * (int)sizeof(T)) : ACC_OOB,
+                 make_float4(o[0], o[1], o[2], o[3]), (T*)nullptr);
+    }
+  };
+  if (interior)
+    taps(std::true_type{});
+  else
+    taps(std::false_type{});
+  if (!stats) return;
+  constexpr int WL = TCQ < 64 ? TCQ : 64;
+  if (interior) cnt = (float)R;
+  float f[9] = {c1[0].x, c1[0].y, c1[1].x, c1[1].y, c2[0].x, c2[0].y, c2[1].x, c2[1].y, cnt};
+#pragma unroll
+  for (int off = TCQ; off < 64; off <<= 1)
+#pragma unroll
+    for (int e = 0; e < 9; ++e) f[e] += __shfl_xor(f[e], off);
+  __syncthreads();  // the exchange tile is reused as the 8-wave slab
+  double* sw = reinterpret_cast<double*>(&xb[0][0][0]);  // [8 waves][WL][8]
+  const int lane = tid & 63, wave = tid >> 6;
+  if (lane < WL) {
+    const double n = f[8];
+    const float k0[4] = {pv[0].x, pv[0].y, pv[1].x, pv[1].y};
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const double kk = k0[jj], d1 = f[jj];
+      sw[(wave * WL + lane) * 8 + jj] = n * kk + d1;
+      sw[(wave * WL + lane) * 8 + 4 + jj] = (n * kk * kk + 2.0 * kk * d1) + (double)f[4 + jj];
+    }
+  }
+  __syncthreads();
+  if (tid < TCQ) {  // (TCQ <= 64: every wave holds every quad)
+    const long row = (long)srow * 2 * g.C;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      double v = 0.0;
+#pragma unroll
+      for (int wv = 0; wv < 8; ++wv) v += sw[(wv * WL + tid) * 8 + e];
+      stats[row + (e >> 2) * g.C + c0 + 4 * tid + (e & 3)] = v;
+    }
+  }
+}
+
 template <int TCQ, typename T>
 __global__ void __launch_bounds__(256)
 dw3x3_tile_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dz,
@@ -1566,12 +1765,22 @@ static bool dw_os_on(int B, int H, int W, int C, int dt, bool bnb) {
   return (long)B * H * W * C * 4 > (256L << 20) && C <= 1024;
 }
 #define DW_OS_R 8
+// ACCUNET_DW_OS16 (default 1): the one-shot launches without a BN-backward operand run
+// the 16-row, 512-thread tiles (dw3x3_os16_fwd_kernel); 0 = the 8-row tiles (A/B)
+static bool dw_os16(bool bnb) {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ACCUNET_DW_OS16");
+    v = e ? atoi(e) : 1;
+  }
+  return v != 0 && !bnb;
+}
 
-static DwOGeom dw_ogeom(int B, int H, int W, int C, int tcq, dim3* grid) {
+static DwOGeom dw_ogeom(int B, int H, int W, int C, int tcq, dim3* grid, int rows = DW_OS_R) {
   DwOGeom g;
   g.B = B; g.H = H; g.W = W; g.C = C;
   g.tilesW = ceil_div(W, 256 / tcq);
-  g.tilesH = ceil_div(H, DW_OS_R);
+  g.tilesH = ceil_div(H, rows);
   g.ncg = C / 4 / tcq;
   g.ntl = 0;
   g.xcd = 0;
@@ -1641,7 +1850,7 @@ static DwGeom dw_geom(int B, int H, int W, int C, int V, dim3* grid) {
 extern "C" int accunet_dw3x3_variant(int B, int H, int W, int C, int dt) {
   if (dw_span_nt(H, W, C)) return 2;
   const int tcq = dw_tile_tcq(H, W, C, dt);
-  if (tcq && dw_os_on(B, H, W, C, dt, false)) return 3;
+  if (tcq && dw_os_on(B, H, W, C, dt, false)) return dw_os16(false) ? 4 : 3;
   return tcq ? 1 : 0;
 }
 
@@ -1653,7 +1862,7 @@ extern "C" int accunet_dw3x3_rows(int B, int H, int W, int C, int dt, int bnb) {
   }
   int tcq = dw_tile_tcq(H, W, C, dt);
   if (tcq && dw_os_on(B, H, W, C, dt, bnb != 0)) {
-    const DwOGeom og = dw_ogeom(B, H, W, C, tcq, &grid);
+    const DwOGeom og = dw_ogeom(B, H, W, C, tcq, &grid, dw_os16(bnb != 0) ? 2 * DW_OS_R : DW_OS_R);
     return B * og.tilesH * og.tilesW;
   }
   if (tcq) dw_tgeom(B, H, W, C, tcq, &grid, dw_rch_max());
@@ -1711,6 +1920,20 @@ extern "C" int accunet_dw3x3_fwd(const void* x, const float* wt, const float* bi
     return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
   }
   int tcq = dw_tile_tcq(H, W, C, dt);
+  if (tcq && dw_os_on(B, H, W, C, dt, bz != nullptr) && dw_os16(bz != nullptr)) {
+    DwOGeom og = dw_ogeom(B, H, W, C, tcq, &grid, 2 * DW_OS_R);
+    auto launch = [&](auto tag, auto tcqc) {
+      using T = decltype(tag);
+      hipLaunchKernelGGL((dw3x3_os16_fwd_kernel<decltype(tcqc)::value, T>), grid, dim3(512), 0, s,
+                         (const T*)x, wt, bias, sc, sh, act, flip, (T*)z, stats, og);
+    };
+    if (with_dt(dt, [&](auto tag) {
+          if (tcq == 16) launch(tag, std::integral_constant<int, 16>{});
+          else launch(tag, std::integral_constant<int, 8>{});
+        }))
+      return ACC_EBADARG;
+    return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+  }
   if (tcq && dw_os_on(B, H, W, C, dt, bz != nullptr)) {
     DwOGeom og = dw_ogeom(B, H, W, C, tcq, &grid);
     // default-policy input loads: a tile re-reads 2 of its 10 input rows and 2 of its 34

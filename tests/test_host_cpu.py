@@ -387,22 +387,28 @@ def test_abi_host_side_contract_without_a_device():
     # above 256 MB by default, for every tile launch with ACCUNET_DW_OS=2; else 32-row
     # strips (1024 rows)
     os_on, os_all = os_knob != "0", os_knob == "2"
-    assert lib.accunet_dw3x3_variant(16, 256, 256, 96, 0) == (3 if os_on else 1)
-    assert lib.accunet_dw3x3_variant(16, 256, 256, 96, 1) == (3 if os_all else 1)
-    assert lib.accunet_dw3x3_rows(16, 256, 256, 96, 0, 0) == (4096 if os_on else 1024)
+    # the one-shot launches without a BN-backward operand run 16-row tiles (512 threads,
+    # 16 * 16 * 8 = 2048 rows) unless ACCUNET_DW_OS16=0 (8-row tiles: 4096 rows)
+    os16 = os.environ.get("ACCUNET_DW_OS16", "1") != "0"
+    one_shot = 4 if os16 else 3
+    assert lib.accunet_dw3x3_variant(16, 256, 256, 96, 0) == (one_shot if os_on else 1)
+    assert lib.accunet_dw3x3_variant(16, 256, 256, 96, 1) == (one_shot if os_all else 1)
+    assert lib.accunet_dw3x3_rows(16, 256, 256, 96, 0, 0) == (
+        (2048 if os16 else 4096) if os_on else 1024)
     # the BN-backward data gradient of the same shape: strips unless ACCUNET_DW_OS=2
     assert lib.accunet_dw3x3_rows(16, 256, 256, 96, 0, 1) == (4096 if os_all else 1024)
     # 16 x 128^2 x 192 fp32 (201 MB, cached): strips by default
-    assert lib.accunet_dw3x3_variant(16, 128, 128, 192, 0) == (3 if os_all else 1)
+    assert lib.accunet_dw3x3_variant(16, 128, 128, 192, 0) == (one_shot if os_all else 1)
     # cnv72's 16 x 64^2 x 4352 (1.1 GB, but 136 channel groups per tile): strips by default
-    assert lib.accunet_dw3x3_variant(16, 64, 64, 4352, 0) == (3 if os_all else 1)
-    assert lib.accunet_dw3x3_variant(16, 128, 128, 384, 0) == (3 if os_on else 1)
+    assert lib.accunet_dw3x3_variant(16, 64, 64, 4352, 0) == (one_shot if os_all else 1)
+    assert lib.accunet_dw3x3_variant(16, 128, 128, 384, 0) == (one_shot if os_on else 1)
     # bf16 (dt 1) runs 64-channel tiles where C % 64 == 0: 16-pixel tiles, twice the rows
     # of the same kernel's 32-pixel fp32 tiles
     r32, r16 = (lib.accunet_dw3x3_rows(16, 128, 128, 192, d, 0) for d in (0, 1))
     assert r32 * 2 == r16
-    assert lib.accunet_dw3x3_rows(16, 256, 256, 96, 1, 0) == (4096 if os_all else 1024)
-    assert lib.accunet_dw3x3_variant(16, 64, 64, 4352, 1) == (3 if os_all else 1)
+    assert lib.accunet_dw3x3_rows(16, 256, 256, 96, 1, 0) == (
+        (2048 if os16 else 4096) if os_all else 1024)
+    assert lib.accunet_dw3x3_variant(16, 64, 64, 4352, 1) == (one_shot if os_all else 1)
     assert lib.accunet_dw3x3_variant(16, 256, 256, 9, 0) == 0
 
 

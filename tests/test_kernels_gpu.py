@@ -123,12 +123,14 @@ def _dw_runs(tmp_path, settings, extra_env=None):
     return outs
 
 
-def test_dw3x3_one_shot_k1_shape_matches_strip(tmp_path):
+@pytest.mark.parametrize("os16", ["1", "0"])
+def test_dw3x3_one_shot_k1_shape_matches_strip(tmp_path, os16):
     """The default kernel choice at the north-star K1 shape (16 x 256^2 x 96 fp32, 402 MB:
-    one-shot tiles for the forward and the plain data gradient, the strip for the
-    BN-backward data gradient) against the strip everywhere (ACCUNET_DW_OS=0): z and
-    both data gradients bit for bit, statistics totals to summation order."""
-    outs = _dw_runs(tmp_path, ("1", "0"), {"DW_WORKER_K1": "1"})
+    one-shot tiles for the forward and the plain data gradient -- 16-row 512-thread tiles,
+    or with ACCUNET_DW_OS16=0 the 8-row tiles -- the strip for the BN-backward data
+    gradient) against the strip everywhere (ACCUNET_DW_OS=0): z and both data gradients
+    bit for bit, statistics totals to summation order."""
+    outs = _dw_runs(tmp_path, ("1", "0"), {"DW_WORKER_K1": "1", "ACCUNET_DW_OS16": os16})
     assert int(outs["1"].pop("variant")) == 1  # (the worker's 2 x 16 x 64 probe shape)
     outs["0"].pop("variant")
     outs["1"].pop("variant_bf16")
@@ -136,7 +138,8 @@ def test_dw3x3_one_shot_k1_shape_matches_strip(tmp_path):
     _dw_compare(outs, "1", "0")
 
 
-def test_dw3x3_one_shot_matches_strip_bitwise(tmp_path):
+@pytest.mark.parametrize("os16", ["1", "0"])
+def test_dw3x3_one_shot_matches_strip_bitwise(tmp_path, os16):
     """The one-shot tile kernel and the strip kernel sum every output in the same order
     (bias, then the taps row-major), so forward z, the flipped-kernel data gradient and
     the BatchNorm-backward data gradient are bit-identical, and their statistics totals
@@ -145,9 +148,10 @@ def test_dw3x3_one_shot_matches_strip_bitwise(tmp_path):
     dtype and launch kind) against 0 (the strip everywhere) on ragged and channel-group
     shapes, fp32 and bf16, each in a child process (the knob is read once per process;
     tests/dw_os_worker.py)."""
-    outs = _dw_runs(tmp_path, ("2", "0"))
-    assert int(outs["2"].pop("variant")) == 3 and int(outs["0"].pop("variant")) == 1
-    assert int(outs["2"].pop("variant_bf16")) == 3 and int(outs["0"].pop("variant_bf16")) == 1
+    outs = _dw_runs(tmp_path, ("2", "0"), {"ACCUNET_DW_OS16": os16})
+    one_shot = 4 if os16 == "1" else 3  # 16-row 512-thread tiles / 8-row tiles
+    assert int(outs["2"].pop("variant")) == one_shot and int(outs["0"].pop("variant")) == 1
+    assert int(outs["2"].pop("variant_bf16")) == one_shot and int(outs["0"].pop("variant_bf16")) == 1
     _dw_compare(outs, "2", "0")
 
 
