@@ -689,16 +689,6 @@ bn_bwd_apply_kernel(const T* __restrict__ x, const T* __restrict__ dy,
   }
 }
 
-// row blocks of the BatchNorm-backward apply pass: no block cap (it writes no partial
-// rows any more): 16x65536x32 fp32 89 -> 78 us against 1024 blocks (r05_stream_ab.txt)
-static int apply_rowblocks(long P, int C) {
-  long want = P * (long)C / (256 * 16);
-  if (want < 1) want = 1;
-  if (want > P) want = P;
-  if (want > (1L << 20)) want = 1L << 20;
-  return (int)want;
-}
-
 extern "C" size_t accunet_bn_bwd_ws_elems(long P, int C) {
   int nb = stream_rowblocks(P, C);
   return (size_t)nb * 2 * C * 2 + accunet_partials_ws_elems(nb, 2 * C) * 2 + 3 * (size_t)C;
@@ -751,7 +741,7 @@ extern "C" int accunet_bn_bwd(const void* x, const void* dy, const float* st,
   int rc = reduce_finish(part, true, nb, 2 * C, scratch,
                          bn_bwd_fin(C, P, st, gamma, training, dgamma, dbeta, coef, 0, dsum), s);
   if (rc != ACC_OK) return rc;
-  const dim3 agrid(apply_rowblocks(P, C), grid.y);
+  const dim3 agrid = grid;
   with_dt(dt, [&](auto tag) {
     using T = decltype(tag);
     if (V == 4)
@@ -802,7 +792,7 @@ extern "C" int accunet_bn_bwd_part(const void* x, const void* dy, const float* s
   if (rc != ACC_OK) return rc;
   (void)cpart;
   (void)cscr;
-  const dim3 agrid(apply_rowblocks(P, C), grid.y);
+  const dim3 agrid = grid;
   with_dt(dt, [&](auto tag) {
     using T = decltype(tag);
     if (V == 4)

@@ -1,6 +1,5 @@
 // Channel-tiled streaming helpers shared by the NHWC elementwise / reduction kernels.
 #pragma once
-#include <type_traits>
 #include "common.h"
 
 // --------------------------------------------------------------------------
@@ -103,15 +102,15 @@ ACC_DEV void quad_rows2(const T* base1, const T* base2, long nrows, int rg, int 
 }
 
 // Reduce per-thread (a[V], b[V]) across the RG row-groups of the block and write
-// the block's partial row out[(row)*2*C + {0,C} + c]. WT: write-through stores (a
-// last-arriving block of the same launch reads the row, handoff_last in common.h).
-template <typename T>
-ACC_DEV void chan_out(T* p, T v, std::false_type) { *p = v; }
-ACC_DEV void chan_out(double* p, double v, std::true_type) { st_wt(p, v); }
-template <int V, typename T, bool WT = false>
+// the block's partial row out[(row)*2*C + {0,C} + c].
+// CM (channel-major): quantity q of channel c goes to out[(q*C + c)*R + row] instead,
+// so a reader of one channel's R rows (se_bwd_chan_sum_kernel) reads contiguous memory.
+template <int V, typename T, bool CM = false>
 ACC_DEV void block_chan_reduce2(const ChanTile& t, T (&a)[V], T (&b)[V], T* out, long row,
-                                int C) {
-  using W = std::integral_constant<bool, WT>;
+                                int C, long R = 0) {
+  auto at = [&](int q, int c) -> T& {
+    return CM ? out[((long)q * C + c) * R + row] : out[row * 2 * C + (long)q * C + c];
+  };
   __shared__ T red[2][256 * 4];
   int tid = threadIdx.x;
   if ((t.TCQ & (t.TCQ - 1)) == 0) {
@@ -141,8 +140,8 @@ ACC_DEV void block_chan_reduce2(const ChanTile& t, T (&a)[V], T (&b)[V], T* out,
           sa += red[0][(w * 64 + tid) * V + j];
           sb += red[1][(w * 64 + tid) * V + j];
         }
-        chan_out(&out[row * 2 * C + t.c0 + j], sa, W{});
-        chan_out(&out[row * 2 * C + C + t.c0 + j], sb, W{});
+        at(0, t.c0 + j) = sa;
+        at(1, t.c0 + j) = sb;
       }
     }
     return;
@@ -162,8 +161,8 @@ ACC_DEV void block_chan_reduce2(const ChanTile& t, T (&a)[V], T (&b)[V], T* out,
         sa += red[0][(g * t.TCQ + lt) * V + j];
         sb += red[1][(g * t.TCQ + lt) * V + j];
       }
-      chan_out(&out[row * 2 * C + t.c0 + j], sa, W{});
-      chan_out(&out[row * 2 * C + C + t.c0 + j], sb, W{});
+      at(0, t.c0 + j) = sa;
+      at(1, t.c0 + j) = sb;
     }
   }
 }
@@ -171,9 +170,12 @@ ACC_DEV void block_chan_reduce2(const ChanTile& t, T (&a)[V], T (&b)[V], T* out,
 // N-quantity version of block_chan_reduce2: per-thread v[i][V] (i < N) reduced over
 // the block's row groups into out[(row*N + i)*C + c], one quantity at a time through
 // one LDS buffer (same deterministic order as block_chan_reduce2).
-template <int V, int N, typename T, bool WT = false>
-ACC_DEV void block_chan_reduceN(const ChanTile& t, T (&v)[N][V], T* out, long row, int C) {
-  using W = std::integral_constant<bool, WT>;
+template <int V, int N, typename T, bool CM = false>
+ACC_DEV void block_chan_reduceN(const ChanTile& t, T (&v)[N][V], T* out, long row, int C,
+                                long R = 0) {
+  auto at = [&](int q, int c) -> T& {
+    return CM ? out[((long)q * C + c) * R + row] : out[(row * N + q) * C + c];
+  };
   __shared__ T red[256 * 4];
   const int tid = threadIdx.x;
   const bool p2 = (t.TCQ & (t.TCQ - 1)) == 0;
@@ -195,7 +197,7 @@ ACC_DEV void block_chan_reduceN(const ChanTile& t, T (&v)[N][V], T* out, long ro
         for (int j = 0; j < V; ++j) {
           T s = 0;
           for (int w = 0; w < 4; ++w) s += red[(w * 64 + tid) * V + j];
-          chan_out(&out[(row * N + i) * C + t.c0 + j], s, W{});
+          at(i, t.c0 + j) = s;
         }
       }
     } else {
@@ -208,7 +210,7 @@ ACC_DEV void block_chan_reduceN(const ChanTile& t, T (&v)[N][V], T* out, long ro
         for (int j = 0; j < V; ++j) {
           T s = 0;
           for (int g = 0; g < t.RG; ++g) s += red[(g * t.TCQ + lt) * V + j];
-          chan_out(&out[(row * N + i) * C + t.c0 + j], s, W{});
+          at(i, t.c0 + j) = s;
         }
       }
     }

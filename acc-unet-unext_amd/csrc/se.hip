@@ -141,7 +141,6 @@ ACC_DEV void se_fwd_sums(const T* __restrict__ z, const float* __restrict__ sc,
 // summation order: 4 chunk groups k = grp mod 4, each in chunk order, then
 // ((g0 + g1) + g2) + g3), the channel means, fc1 (+LeakyReLU) and fc2 (+sigmoid) of
 // that sample (the reference gate, :41-45). sm: LDS m[C] | h'[Cr].
-template <bool WT>
 ACC_DEV void se_mid_sample_body(const double* __restrict__ part, const SeGeom& g, const SeMid& m,
                                 int b, float* sm) {
   __shared__ double r[2][4][64];
@@ -156,9 +155,8 @@ ACC_DEV void se_mid_sample_body(const double* __restrict__ part, const SeGeom& g
     if (c < C)
       ordered_strided_sum<8>(s2, grp, g.NCH, 4, [&](int k, double (&v)[2]) {
         const double* pr = part + ((long)(b * g.NCH + k) * 2) * C;
-        // WT: rows written by other blocks of this launch (write-through, handoff_last)
-        v[0] = WT ? ld_wt(pr + c) : *(pr + c);
-        v[1] = WT ? ld_wt(pr + C + c) : *(pr + C + c);
+        v[0] = *(pr + c);
+        v[1] = *(pr + C + c);
       });
     r[0][grp][cl] = s2[0];
     r[1][grp][cl] = s2[1];
@@ -198,15 +196,11 @@ ACC_DEV void se_mid_sample_body(const double* __restrict__ part, const SeGeom& g
 }
 
 // middle step, part 2, channel c: BatchNorm statistics of y = a*s derived from
-// (S, Q, s) -> k = gamma*rstd and beta' = beta - k*mean. Every apply block computes
-// this for its own channels (same loop, same order: identical values in every block);
-// the block `writer` also updates the running statistics and stores mean, rstd and
-// beta' for the backward.
-struct SeChanBN {
-  float k, betap;
-};
-ACC_DEV SeChanBN se_chan_bn(const SeGeom& g, const SeMid& m, int c, bool writer) {
+// (S, Q, s), running-stat update, per-(b,c) coefficients.
+ACC_DEV void se_mid_bn_body(const SeGeom& g, const SeMid& m, int c) {
   const int B = g.B, C = g.C;
+  if (m.nbt && c == 0) *m.nbt += 1;  // num_batches_tracked (training only; null otherwise)
+  if (c >= C) return;
   SeSave sv = se_save_view(m.save, B, C, m.Cr);
   const double n = (double)B * g.HW;
   float mu, var;
@@ -223,8 +217,8 @@ ACC_DEV SeChanBN se_chan_bn(const SeGeom& g, const SeMid& m, int c, bool writer)
     if (m2 < 0.0) m2 = 0.0;
     mu = (float)m1;
     var = (float)m2;
-    if (writer && m.rmean) m.rmean[c] = (1.f - m.momentum) * m.rmean[c] + m.momentum * mu;
-    if (writer && m.rvar)
+    if (m.rmean) m.rmean[c] = (1.f - m.momentum) * m.rmean[c] + m.momentum * mu;
+    if (m.rvar)
       m.rvar[c] = (1.f - m.momentum) * m.rvar[c] + m.momentum * (float)(m2 * n / (n - 1.0));
   } else {
     mu = m.rmean[c];
@@ -232,33 +226,21 @@ ACC_DEV SeChanBN se_chan_bn(const SeGeom& g, const SeMid& m, int c, bool writer)
   }
   float rs = 1.f / sqrtf(var + m.eps);
   float k = m.gamma[c] * rs;
-  SeChanBN r{k, m.beta[c] - k * mu};
-  if (writer) {
-    sv.mean[c] = mu;
-    sv.rstd[c] = rs;
-    sv.betap[c] = r.betap;
-  }
-  return r;
+  sv.mean[c] = mu;
+  sv.rstd[c] = rs;
+  sv.betap[c] = m.beta[c] - k * mu;
+#pragma unroll 8
+  for (int b = 0; b < B; ++b) sv.alpha[b * C + c] = k * *(sv.sg + b * C + c);
 }
 
-// Per-sample tickets of the folded forward (se_reduce_gate_kernel), one bank per
-// launch stream like the statistics reductions (acc_stream_bank, csrc/bn.hip).
-#define SE_MAX_B 4096
-__device__ unsigned g_se_tickets[2 * SE_MAX_B];
-
-// pass 1 forward + the gate: partials part[(b*NCH + chunk)][2][C] of (sum a, sum a^2),
-// written through; the last block of sample b to arrive (per-sample ticket) runs the
-// middle step of that sample -- S, Q, the channel means, fc1 / fc2 and the sigmoid
-// gate (se_mid_sample_body) -- while other samples' blocks still stream. Round 4 folded
-// the middle step into ONE extra launch (sample blocks + a channel step); here it rides
-// in the reduce itself and the channel step in the apply's prologue, so the layer is
-// two launches instead of four. sm (dynamic LDS): m[C] | h'[Cr].
+// pass 1 forward: partials part[(b*NCH + chunk)][2][C] of (sum a, sum a^2).
+// (The middle step stays two launches: folding it into this launch's last blocks with
+// ticketed hand-offs measured slower, as its cost is the chain of dependent memory
+// round trips, not the launches.)
 template <int V, typename T, bool PRO>
 __global__ void __launch_bounds__(256)
-se_reduce_gate_kernel(const T* __restrict__ z, const float* __restrict__ sc,
-                      const float* __restrict__ sh, int act, SeGeom g, double* __restrict__ part,
-                      SeMid m, unsigned* __restrict__ tickets) {
-  extern __shared__ __attribute__((aligned(16))) float se_dyn[];
+se_reduce_kernel(const T* __restrict__ z, const float* __restrict__ sc,
+                 const float* __restrict__ sh, int act, SeGeom g, double* __restrict__ part) {
   ChanTile t = chan_tile<V>(g.C);
   const int b = blockIdx.x / g.NCH, ch = blockIdx.x % g.NCH;
   long r0 = (long)b * g.HW + ch * g.rows_per;
@@ -267,43 +249,31 @@ se_reduce_gate_kernel(const T* __restrict__ z, const float* __restrict__ sc,
 #pragma unroll
   for (int j = 0; j < V; ++j) { a[j] = 0.0; q[j] = 0.0; }
   se_fwd_sums<V, T, PRO>(z, sc, sh, act, g, t, r0, r1, a, q);
-  block_chan_reduce2<V, double, true>(t, a, q, part, blockIdx.x, g.C);
-  if (!handoff_last(tickets + b, (unsigned)(g.NCH * gridDim.y))) return;
-  se_mid_sample_body<true>(part, g, m, b, se_dyn);
+  block_chan_reduce2<V>(t, a, q, part, blockIdx.x, g.C);
+}
+
+// middle step: per sample, then per channel
+__global__ void __launch_bounds__(256)
+se_mid_sample_kernel(const double* __restrict__ part, SeGeom g, SeMid m) {
+  extern __shared__ __attribute__((aligned(16))) float se_dyn[];
+  se_mid_sample_body(part, g, m, blockIdx.x, se_dyn);
+}
+__global__ void __launch_bounds__(256) se_mid_bn_kernel(SeGeom g, SeMid m) {
+  se_mid_bn_body(g, m, blockIdx.x * blockDim.x + threadIdx.x);
 }
 
 // pass 2 forward: out = lrelu(alpha[b,c]*a + betap[c]) (+ res: the residual add that
 // follows the SE in ResPath, ACC_UNet.py:326, and in the MLFC merge, :489-520, fused
 // so the SE output itself is never written: the sum is, as rnd(rnd(y) + res), the
-// value the separate add would have stored). Prologue: the BatchNorm-of-gated step of
-// the block's channels (se_chan_bn: alpha = k*s[b,c], beta'); the blocks of chunk 0
-// store alpha of their sample, block (0, y) the per-channel state and running stats.
-// rev: blocks walk the samples and chunks in the reverse of the reduce's order, so the
-// first re-reads are of the lines the reduce touched last.
+// value the separate add would have stored)
 template <int V, typename T, bool PRO, bool RES>
 __global__ void __launch_bounds__(256)
 se_apply_kernel(const T* __restrict__ z, const float* __restrict__ sc,
-                const float* __restrict__ sh, int act, SeGeom g, SeMid m, int rev,
-                const T* __restrict__ res, T* __restrict__ out, double* __restrict__ ostats) {
-  __shared__ float s_k[256], s_bp[256];
+                const float* __restrict__ sh, int act, SeGeom g, const float* __restrict__ alpha,
+                const float* __restrict__ betap, const T* __restrict__ res, T* __restrict__ out,
+                double* __restrict__ ostats) {
   ChanTile t = chan_tile<V>(g.C);
-  const int lin = rev ? (int)(gridDim.x - 1 - blockIdx.x) : (int)blockIdx.x;
-  const int b = lin / g.NCH, ch = lin % g.NCH;
-  {
-    const int cbase = blockIdx.y * 64 * V, ncb = min(64 * V, g.C - cbase);
-    const bool writer = lin == 0;
-    SeSave sv = se_save_view(m.save, g.B, g.C, m.Cr);
-    for (int i = threadIdx.x; i < ncb; i += 256) {
-      const int c = cbase + i;
-      const SeChanBN r = se_chan_bn(g, m, c, writer);
-      s_k[i] = r.k;
-      s_bp[i] = r.betap;
-      if (ch == 0) sv.alpha[b * g.C + c] = r.k * *(sv.sg + b * g.C + c);
-    }
-    // num_batches_tracked (training only; null otherwise)
-    if (writer && blockIdx.y == 0 && threadIdx.x == 0 && m.nbt) *m.nbt += 1;
-    __syncthreads();
-  }
+  const int b = blockIdx.x / g.NCH, ch = blockIdx.x % g.NCH;
   long r0 = (long)b * g.HW + ch * g.rows_per;
   long r1 = min((long)b * g.HW + g.HW, r0 + g.rows_per);
   double o1[V], o2[V];
@@ -311,14 +281,12 @@ se_apply_kernel(const T* __restrict__ z, const float* __restrict__ sc,
   for (int j = 0; j < V; ++j) { o1[j] = 0.0; o2[j] = 0.0; }
   if (t.active) {
     float s[V], h[V], al[V], be[V];
-    const float* sg = se_save_view(m.save, g.B, g.C, m.Cr).sg;
-    const int cl = t.c0 - (int)blockIdx.y * 64 * V;  // block-local channel of quad c0
 #pragma unroll
     for (int j = 0; j < V; ++j) {
       s[j] = PRO ? sc[t.c0 + j] : 1.f;
       h[j] = PRO ? sh[t.c0 + j] : 0.f;
-      al[j] = s_k[cl + j] * sg[b * g.C + t.c0 + j];
-      be[j] = s_bp[cl + j];
+      al[j] = alpha[b * g.C + t.c0 + j];
+      be[j] = betap[t.c0 + j];
     }
     const bool st = ostats != nullptr;
     auto elem = [&](bool ok, const float (&x)[V], const float (&rv)[V], float (&v)[V]) {
@@ -362,19 +330,54 @@ se_apply_kernel(const T* __restrict__ z, const float* __restrict__ sc,
     }
   }
   // optional statistics of the SE output (MLFC feeds it straight into bns_l, :427-487)
-  if (ostats) block_chan_reduce2<V>(t, o1, o2, ostats, lin, g.C);
+  if (ostats) block_chan_reduce2<V>(t, o1, o2, ostats, blockIdx.x, g.C);
+}
+
+// backward pass 1: partials of (T1 = sum g2, T2 = sum g2*a) per (b,c)
+template <int V, typename T>
+__global__ void __launch_bounds__(256)
+se_bwd_reduce_kernel(const T* __restrict__ z, const T* __restrict__ dout,
+                     const float* __restrict__ sc, const float* __restrict__ sh, int act,
+                     SeGeom g, const float* __restrict__ alpha, const float* __restrict__ betap,
+                     double* __restrict__ part) {
+  ChanTile t = chan_tile<V>(g.C);
+  const int b = blockIdx.x / g.NCH, ch = blockIdx.x % g.NCH;
+  long r0 = (long)b * g.HW + ch * g.rows_per;
+  long r1 = min((long)b * g.HW + g.HW, r0 + g.rows_per);
+  double t1[V], t2[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) { t1[j] = 0.0; t2[j] = 0.0; }
+  if (t.active) {
+    float s[V], h[V], al[V], be[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      s[j] = sc ? sc[t.c0 + j] : 1.f;
+      h[j] = sh ? sh[t.c0 + j] : 0.f;
+      al[j] = alpha[b * g.C + t.c0 + j];
+      be[j] = betap[t.c0 + j];
+    }
+    const bool pro = sc != nullptr;
+    for (long r = r0 + t.rg; r < r1; r += t.RG) {
+      float v[V], d[V];
+      ldv<V>(z + r * g.C + t.c0, v);
+      ldv<V>(dout + r * g.C + t.c0, d);
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        float x = pro ? apply_act(v[j] * s[j] + h[j], act) : v[j];
+        float g2 = d[j] * lrelu_d(al[j] * x + be[j]);
+        t1[j] += g2;
+        t2[j] += (double)g2 * x;
+      }
+    }
+  }
+  block_chan_reduce2<V, double, true>(t, t1, t2, part, blockIdx.x, g.C, (long)g.B * g.NCH);
 }
 
 // backward middle step. coef (fp32): A[B*C] Bc[B*C] Cc[B*C] with
 //   da = A*g2 + Bc*(a*s - mean) + Cc
 // scratch (fp64): G[C] GY[C] du[B*C] dh[B*Cr] T1[B*C] T2[B*C] (+ U1..W3 with a prologue)
-// The whole middle step rides in the first pass's launch (se_bwd_reduce_kernel /
-// se_bwd_reduce_pro_kernel): the last block of each sample to arrive adds that
-// sample's chunk partials (se_bwd_tsum), and the last of those runs the channel step,
-// the sample step and the parameter / prologue-coefficient steps for every channel and
-// sample (se_bwd_mid_all). Round 5 ran them as three more launches (a channel-sum
-// launch with one block per channel reading a column of every partial row, then the
-// sample and tail launches): 28 us per SE layer in a single-stream trace.
+// Three launches: part sums + channel step (se_bwd_chan_sum_kernel), sample step,
+// parameter + prologue-coefficient step (se_bwd_tail_kernel).
 struct SeBwdMid {
   int Cr;
   const float *w1, *w2, *gamma;
@@ -394,31 +397,23 @@ ACC_DEV double* se_T1(const SeGeom& g, const SeBwdMid& m) {
   return m.scratch + 2 * (size_t)g.C + (size_t)g.B * g.C + (size_t)g.B * m.Cr;
 }
 
-// per-sample chunk sums of the NQ quantities, T[q][b][c] = sum_k part[b*NCH + k][q][c]
-// in chunk order (whole partial rows per thread sweep: consecutive threads read
-// consecutive channels), handed on with write-through stores
-template <int NQ>
-ACC_DEV void se_bwd_tsum(const double* __restrict__ part, const SeGeom& g, const SeBwdMid& m,
-                         int b) {
-  const int C = g.C;
-  double* T = se_T1(g, m);
-  const long BC = (long)g.B * C;
-  for (int i = threadIdx.x; i < NQ * C; i += blockDim.x) {
-    const int q = i / C, c = i % C;
-    double s[1] = {0.0};
-    ordered_strided_sum<8>(s, 0, g.NCH, 1, [&](int k, double (&v)[1]) {
-      v[0] = ld_wt(part + ((long)(b * g.NCH + k) * NQ + q) * C + c);
-    });
-    st_wt(T + q * BC + (long)b * C + c, s[0]);
-  }
+// SE_LANES lanes per channel: lane l handles samples b = l, l + SE_LANES, ...; the
+// per-channel sums are reduced with an xor butterfly inside the lane group and lane 0's
+// value is broadcast, so every lane uses identical totals (deterministic). All lanes of
+// the wave take part (dead channels too).
+#define SE_LANES 16
+ACC_DEV double se_lane_sum(double v) {
+#pragma unroll
+  for (int off = 1; off < SE_LANES; off <<= 1) v += __shfl_xor(v, off);
+  return __shfl(v, (threadIdx.x & 63) & ~(SE_LANES - 1));
 }
 
-// channel step, every channel (one thread per channel, samples in order): BN backward
-// sums G = sum_b T1, GY = rstd * sum_b (s T2 - mean T1) -> dgamma, dbeta, and
-// du = ds * s * (1 - s). (Values this block hands to itself go through write-through
-// stores and L1-bypassing loads as well.)
-ACC_DEV void se_bwd_chan_all(const SeGeom& g, const SeBwdMid& m) {
+// channel step, channel c (lane `lane` of its group): BN backward sums and
+// du = ds * s * (1 - s).
+ACC_DEV void se_bwd_chan_body(const SeGeom& g, const SeBwdMid& m, int c, int lane) {
   const int B = g.B, C = g.C;
+  const bool live = c < C;
+  const int cc = live ? c : 0;
   SeSave sv = se_save_view(m.save, B, C, m.Cr);
   double* G = m.scratch;
   double* GY = G + C;
@@ -426,71 +421,129 @@ ACC_DEV void se_bwd_chan_all(const SeGeom& g, const SeBwdMid& m) {
   const double* T1 = se_T1(g, m);
   const double* T2 = T1 + (size_t)B * C;
   const double n = (double)B * g.HW;
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    const double mean = sv.mean[c], rstd = sv.rstd[c];
-    double gs = 0.0, gy = 0.0;
-    for (int b = 0; b < B; ++b) {
-      const double t1 = ld_wt(T1 + b * C + c);
+  const double mean = sv.mean[cc], rstd = sv.rstd[cc];
+  double gs = 0.0, gy = 0.0;
+  if (live)
+    for (int b = lane; b < B; b += SE_LANES) {
+      double t1 = *(T1 + b * C + c);
       gs += t1;
-      gy += (double)sv.sg[b * C + c] * ld_wt(T2 + b * C + c) - mean * t1;
+      gy += (double)sv.sg[b * C + c] * *(T2 + b * C + c) - mean * t1;
     }
-    gy *= rstd;
-    st_wt(G + c, gs);
-    st_wt(GY + c, gy);
+  gs = se_lane_sum(gs);
+  gy = se_lane_sum(gy) * rstd;
+  if (!live) return;
+  if (lane == 0) {
+    G[c] = gs;
+    GY[c] = gy;
     if (m.dgamma) m.dgamma[c] = (float)gy;
     if (m.dbeta) m.dbeta[c] = (float)gs;
-    const double k = (double)m.gamma[c] * rstd;
-    for (int b = 0; b < B; ++b) {
-      const double s = sv.sg[b * C + c];
-      const double t2 = ld_wt(T2 + b * C + c);
-      double ds;
-      if (m.training) {
-        const double yha = rstd * (s * sv.Q[b * C + c] - mean * sv.S[b * C + c]);
-        ds = k * (t2 - (gs / n) * sv.S[b * C + c] - (gy / n) * yha);
-      } else {
-        ds = k * t2;
-      }
-      st_wt(du + b * C + c, ds * s * (1.0 - s));
+  }
+  const double k = (double)m.gamma[c] * rstd;
+  for (int b = lane; b < B; b += SE_LANES) {
+    double s = sv.sg[b * C + c];
+    double t2 = *(T2 + b * C + c);
+    double ds;
+    if (m.training) {
+      double yha = rstd * (s * sv.Q[b * C + c] - mean * sv.S[b * C + c]);
+      ds = k * (t2 - (gs / n) * sv.S[b * C + c] - (gy / n) * yha);
+    } else {
+      ds = k * t2;
     }
+    du[b * C + c] = ds * s * (1.0 - s);
   }
 }
 
-// sample step, every sample: dh = lrelu'(hpre) * W2^T du, dm = W1^T dh, coefficients
-ACC_DEV void se_bwd_sample_all(const SeGeom& g, const SeBwdMid& m) {
-  const int B = g.B, C = g.C, Cr = m.Cr;
+
+// Part sums + channel step in one launch, one block per channel c: 16 lanes per
+// sample b sum the chunk partials k = lane, lane + 16, ... (every quantity's loads in
+// flight together), an xor butterfly inside the 16-lane group adds the lane sums in a
+// fixed order, lane 0 stores T[q][b, c] (fp64 scratch, read by the prologue step
+// too); then the first wave runs the channel step of c (se_bwd_chan_body). One
+// launch and two memory round trips instead of two launches.
+template <int NQ>
+__global__ void __launch_bounds__(256)
+se_bwd_chan_sum_kernel(const double* __restrict__ part, SeGeom g, SeBwdMid m) {
+  const int C = g.C, c = blockIdx.x, tid = threadIdx.x;
+  const int lane = tid % 16;
+  const long RB = (long)g.B * g.NCH;  // partial rows
+  double* T = se_T1(g, m);
+  const long BC = (long)g.B * C;
+  for (int b0 = 0; b0 < g.B; b0 += 16) {
+    const int b = b0 + tid / 16;
+    double s[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) s[q] = 0.0;
+    if (b < g.B)
+      ordered_strided_sum<4>(s, lane, g.NCH, 16, [&](int k, double (&v)[NQ]) {
+        // channel-major partials [q][c][b*NCH + k]: the 16 lanes of a sample read 16
+        // consecutive chunks, the block's samples consecutive runs of them
+        const double* pr = part + (long)c * RB + (long)b * g.NCH + k;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) v[q] = pr[(long)q * C * RB];
+      });
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) s[q] += __shfl_xor(s[q], off);
+    }
+    if (b < g.B && lane == 0) {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) T[q * BC + (long)b * C + c] = s[q];
+    }
+  }
+  __syncthreads();  // T of channel c complete (same-block global stores)
+  if (tid < 64) se_bwd_chan_body(g, m, tid < SE_LANES ? c : C, tid % SE_LANES);
+}
+
+// sample step, sample b: dh = lrelu'(hpre) * W2^T du, dm = W1^T dh, coefficients.
+// smd: LDS dh[Cr]. Ends with a barrier (smd reusable).
+ACC_DEV void se_bwd_sample_body(const SeGeom& g, const SeBwdMid& m, int b, double* smd) {
+  const int B = g.B, C = g.C, Cr = m.Cr, tid = threadIdx.x;
   SeSave sv = se_save_view(m.save, B, C, Cr);
   const double* G = m.scratch;
   const double* GY = G + C;
   const double* du = GY + C;
   double* dh = const_cast<double*>(du) + (size_t)B * C;
-  for (int i = threadIdx.x; i < B * Cr; i += blockDim.x) {
-    const int b = i / Cr, j = i % Cr;
+  for (int o = tid; o < Cr * 4; o += 256) {
+    int j = o >> 2, part_i = o & 3;
     double acc = 0.0;
 #pragma unroll 8
-    for (int c = 0; c < C; ++c) acc += (double)m.w2[(long)c * Cr + j] * ld_wt(du + b * C + c);
-    st_wt(dh + i, acc * lrelu_d(sv.hpre[b * Cr + j]));
+    for (int c = part_i; c < C; c += 4) acc += (double)m.w2[(long)c * Cr + j] * du[b * C + c];
+    acc += __shfl_xor(acc, 1);
+    acc += __shfl_xor(acc, 2);
+    if (part_i == 0) {
+      double v = acc * lrelu_d(sv.hpre[b * Cr + j]);
+      smd[j] = v;
+      dh[b * Cr + j] = v;
+    }
   }
   __syncthreads();
   const double n = (double)B * g.HW;
   float* A = m.coef;
   float* Bc = A + (size_t)B * C;
   float* Cc = Bc + (size_t)B * C;
-  for (int i = threadIdx.x; i < B * C; i += blockDim.x) {
-    const int b = i / C, c = i % C;
+  for (int c = tid; c < C; c += 256) {
     double dm = 0.0;
 #pragma unroll 8
-    for (int j = 0; j < Cr; ++j) dm += (double)m.w1[(long)j * C + c] * ld_wt(dh + b * Cr + j);
-    const double k = (double)m.gamma[c] * sv.rstd[c];
-    const double s = sv.sg[i];
-    st_wt(A + i, (float)(s * k));
+    for (int j = 0; j < Cr; ++j) dm += (double)m.w1[(long)j * C + c] * smd[j];
+    double k = (double)m.gamma[c] * sv.rstd[c];
+    double s = sv.sg[b * C + c];
+    int i = b * C + c;
+    A[i] = (float)(s * k);
     if (m.training) {
-      st_wt(Bc + i, (float)(-s * k * sv.rstd[c] * (ld_wt(GY + c) / n)));
-      st_wt(Cc + i, (float)(-s * k * (ld_wt(G + c) / n) + dm / g.HW));
+      Bc[i] = (float)(-s * k * sv.rstd[c] * (GY[c] / n));
+      Cc[i] = (float)(-s * k * (G[c] / n) + dm / g.HW);
     } else {
-      st_wt(Bc + i, 0.f);
-      st_wt(Cc + i, (float)(dm / g.HW));
+      Bc[i] = 0.f;
+      Cc[i] = (float)(dm / g.HW);
     }
   }
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(256) se_bwd_sample_kernel(SeGeom g, SeBwdMid m) {
+  extern __shared__ __attribute__((aligned(16))) double smd[];  // dh[Cr]
+  se_bwd_sample_body(g, m, blockIdx.x, smd);
 }
 
 // parameter step, output i of [dw2 | dw1 | db2 | db1] (sums over the batch)
@@ -504,29 +557,30 @@ ACC_DEV void se_bwd_param_body(const SeGeom& g, const SeBwdMid& m, long i) {
     int c = (int)(i / Cr), j = (int)(i % Cr);
     double acc = 0.0;
 #pragma unroll 8
-    for (int b = 0; b < B; ++b) acc += ld_wt(du + b * C + c) * lrelu(sv.hpre[b * Cr + j]);
+    for (int b = 0; b < B; ++b) acc += du[b * C + c] * lrelu(sv.hpre[b * Cr + j]);
     m.dw2[i] = (float)acc;
   } else if (i < 2 * nW) {  // dw1[j][c] = sum_b dh[b,j] * m[b,c]
     long t = i - nW;
     int j = (int)(t / C), c = (int)(t % C);
     double acc = 0.0;
 #pragma unroll 8
-    for (int b = 0; b < B; ++b) acc += ld_wt(dh + b * Cr + j) * (sv.S[b * C + c] / g.HW);
+    for (int b = 0; b < B; ++b) acc += dh[b * Cr + j] * (sv.S[b * C + c] / g.HW);
     m.dw1[t] = (float)acc;
   } else if (i < 2 * nW + C) {
     int c = (int)(i - 2 * nW);
     double acc = 0.0;
 #pragma unroll 8
-    for (int b = 0; b < B; ++b) acc += ld_wt(du + b * C + c);
+    for (int b = 0; b < B; ++b) acc += du[b * C + c];
     m.db2[c] = (float)acc;
   } else if (i < 2 * nW + C + Cr) {
     int j = (int)(i - 2 * nW - C);
     double acc = 0.0;
 #pragma unroll 8
-    for (int b = 0; b < B; ++b) acc += ld_wt(dh + b * Cr + j);
+    for (int b = 0; b < B; ++b) acc += dh[b * Cr + j];
     m.db1[j] = (float)acc;
   }
 }
+
 
 template <int V, typename T>
 __global__ void __launch_bounds__(256)
@@ -572,12 +626,13 @@ se_bwd_apply_kernel(const T* __restrict__ z, const T* __restrict__ dout,
 
 #define SE_PRO_NQ 8  // T1, T2, U1, U2, U3, W1, W2, W3
 
-// prologue coefficient step, channel c (samples in order): the prologue BN's backward
-// coefficients dz = k1*g + k2*(z - mean1) + k3, dgamma1 = sum g*xhat, dbeta1 = sum g,
-// from the per-(b,c) sums UW[i][B*C] (i = 0..5 -> U1 U2 U3 W1 W2 W3) and the SE
-// coefficients A, Bc, Cc.
-ACC_DEV void se_pro_coef_body(const SeGeom& g, const SeBwdMid& m, int c) {
+// prologue coefficient step, channel c (lane `lane` of its group): the prologue BN's
+// backward coefficients dz = k1*g + k2*(z - mean1) + k3, dgamma1 = sum g*xhat,
+// dbeta1 = sum g, from the per-(b,c) sums UW[i][B*C] (i = 0..5 -> U1 U2 U3 W1 W2 W3)
+// and the SE coefficients A, Bc, Cc.
+ACC_DEV void se_pro_coef_body(const SeGeom& g, const SeBwdMid& m, int c, int lane) {
   const int B = g.B, C = g.C;
+  const bool live = c < C;
   SeSave sv = se_save_view(m.save, B, C, m.Cr);
   const long BC = (long)B * C;
   const double* UW = se_T1(g, m) + 2 * BC;
@@ -585,16 +640,21 @@ ACC_DEV void se_pro_coef_body(const SeGeom& g, const SeBwdMid& m, int c) {
   const float* Bc = A + BC;
   const float* Cc = Bc + BC;
   double sg = 0.0, sgx = 0.0;
-  const double mean = sv.mean[c];
-  for (int b = 0; b < B; ++b) {
-    const long i = (long)b * C + c;
-    const double a = ld_wt(A + i), bb = ld_wt(Bc + i), s = sv.sg[i];
-    const double cst = (double)ld_wt(Cc + i) - bb * mean;
-    sg += a * ld_wt(UW + 0 * BC + i) + bb * s * ld_wt(UW + 1 * BC + i) +
-          cst * ld_wt(UW + 2 * BC + i);
-    sgx += a * ld_wt(UW + 3 * BC + i) + bb * s * ld_wt(UW + 4 * BC + i) +
-           cst * ld_wt(UW + 5 * BC + i);
+  if (live) {
+    const double mean = sv.mean[c];
+    for (int b = lane; b < B; b += SE_LANES) {
+      const long i = (long)b * C + c;
+      const double a = A[i], bb = Bc[i], s = sv.sg[i];
+      const double cst = (double)Cc[i] - bb * mean;
+      sg += a * *(UW + 0 * BC + i) + bb * s * *(UW + 1 * BC + i) +
+            cst * *(UW + 2 * BC + i);
+      sgx += a * *(UW + 3 * BC + i) + bb * s * *(UW + 4 * BC + i) +
+             cst * *(UW + 5 * BC + i);
+    }
   }
+  sg = se_lane_sum(sg);
+  sgx = se_lane_sum(sgx);
+  if (!live || lane != 0) return;
   const float rstd1 = m.pst[BN_RSTD * C + c];
   sgx *= rstd1;  // sum g*xhat
   if (m.dpg) m.dpg[c] = (float)sgx;
@@ -616,70 +676,17 @@ ACC_DEV void se_pro_coef_body(const SeGeom& g, const SeBwdMid& m, int c) {
   if (m.dsum) m.dsum[c] = (float)((double)k1 * sg + n * (double)k3);
 }
 
-// Per-sample tickets of the folded backward: [bank][sample], then one launch-wide
-// ticket per bank at [bank][SE_MAX_B]
-__device__ unsigned g_se_bwd_tickets[2 * (SE_MAX_B + 1)];
 
-// the tail of the backward's first pass: called by every block after its write-through
-// partial row; the last block of sample b sums b's chunks, the last of those runs the
-// whole middle step (channel, sample, parameter and prologue-coefficient steps)
-template <int NQ>
-ACC_DEV void se_bwd_mid_all(const double* __restrict__ part, const SeGeom& g, const SeBwdMid& m,
-                            int b, unsigned* tickets) {
-  if (!handoff_last(tickets + b, (unsigned)(g.NCH * gridDim.y))) return;
-  se_bwd_tsum<NQ>(part, g, m, b);
-  if (!handoff_last(tickets + SE_MAX_B, (unsigned)g.B)) return;
-  se_bwd_chan_all(g, m);
-  __syncthreads();
-  se_bwd_sample_all(g, m);
-  __syncthreads();
-  const long nparam = 2L * g.C * m.Cr + g.C + m.Cr;
-  for (long i = threadIdx.x; i < nparam; i += blockDim.x) se_bwd_param_body(g, m, i);
-  if (m.pcoef)
-    for (int c = threadIdx.x; c < g.C; c += blockDim.x) se_pro_coef_body(g, m, c);
-}
-
-// backward pass 1: partials of (T1 = sum g2, T2 = sum g2*a) per (b,c)
-template <int V, typename T>
-__global__ void __launch_bounds__(256)
-se_bwd_reduce_kernel(const T* __restrict__ z, const T* __restrict__ dout,
-                     const float* __restrict__ sc, const float* __restrict__ sh, int act,
-                     SeGeom g, const float* __restrict__ alpha, const float* __restrict__ betap,
-                     double* __restrict__ part, SeBwdMid m, unsigned* __restrict__ tickets) {
-  ChanTile t = chan_tile<V>(g.C);
-  const int b = blockIdx.x / g.NCH, ch = blockIdx.x % g.NCH;
-  long r0 = (long)b * g.HW + ch * g.rows_per;
-  long r1 = min((long)b * g.HW + g.HW, r0 + g.rows_per);
-  double t1[V], t2[V];
-#pragma unroll
-  for (int j = 0; j < V; ++j) { t1[j] = 0.0; t2[j] = 0.0; }
-  if (t.active) {
-    float s[V], h[V], al[V], be[V];
-#pragma unroll
-    for (int j = 0; j < V; ++j) {
-      s[j] = sc ? sc[t.c0 + j] : 1.f;
-      h[j] = sh ? sh[t.c0 + j] : 0.f;
-      al[j] = alpha[b * g.C + t.c0 + j];
-      be[j] = betap[t.c0 + j];
-    }
-    const bool pro = sc != nullptr;
-    for (long r = r0 + t.rg; r < r1; r += t.RG) {
-      float v[V], d[V];
-      ldv<V>(z + r * g.C + t.c0, v);
-      ldv<V>(dout + r * g.C + t.c0, d);
-#pragma unroll
-      for (int j = 0; j < V; ++j) {
-        float x = pro ? apply_act(v[j] * s[j] + h[j], act) : v[j];
-        float g2 = d[j] * lrelu_d(al[j] * x + be[j]);
-        t1[j] += g2;
-        t2[j] += (double)g2 * x;
-      }
-    }
+// parameter step and (prologue) coefficient step in one launch: they depend on the
+// sample step only, not on each other. Blocks [0, npb) run the parameter step.
+__global__ void __launch_bounds__(256) se_bwd_tail_kernel(SeGeom g, SeBwdMid m, int npb) {
+  if ((int)blockIdx.x < npb) {
+    se_bwd_param_body(g, m, blockIdx.x * (long)blockDim.x + threadIdx.x);
+  } else {
+    const int gid = (blockIdx.x - npb) * blockDim.x + threadIdx.x;
+    se_pro_coef_body(g, m, gid / SE_LANES, gid % SE_LANES);
   }
-  block_chan_reduce2<V, double, true>(t, t1, t2, part, blockIdx.x, g.C);
-  se_bwd_mid_all<2>(part, g, m, b, tickets);
 }
-
 
 // ---------------------------------------------------------------------------
 // SE backward fused with the backward of the BatchNorm(+act) prologue that feeds it
@@ -701,7 +708,7 @@ __global__ void __launch_bounds__(256)
 se_bwd_reduce_pro_kernel(const T* __restrict__ z, const T* __restrict__ dout,
                          const float* __restrict__ pst, int act, SeGeom g,
                          const float* __restrict__ alpha, const float* __restrict__ betap,
-                         double* __restrict__ part, SeBwdMid m, unsigned* __restrict__ tickets) {
+                         double* __restrict__ part) {
   ChanTile t = chan_tile<V>(g.C);
   const int C = g.C;
   const int b = blockIdx.x / g.NCH, ch = blockIdx.x % g.NCH;
@@ -755,8 +762,7 @@ se_bwd_reduce_pro_kernel(const T* __restrict__ z, const T* __restrict__ dout,
   for (int i = 0; i < SE_PRO_NQ; ++i)
 #pragma unroll
     for (int j = 0; j < V; ++j) acc[i][j] = (double)accf[i][j];
-  block_chan_reduceN<V, SE_PRO_NQ, double, true>(t, acc, part, blockIdx.x, C);
-  se_bwd_mid_all<SE_PRO_NQ>(part, g, m, b, tickets);
+  block_chan_reduceN<V, SE_PRO_NQ, double, true>(t, acc, part, blockIdx.x, C, (long)g.B * g.NCH);
 }
 
 template <int V, typename T>
@@ -887,39 +893,35 @@ extern "C" int accunet_se_fwd(const void* z, const float* sc, const float* sh, i
   if (!se_chunk_ok(g, dt)) return ACC_EBADSHAPE;
   int V = (C % 4 == 0) ? 4 : 1;
   dim3 grid(B * g.NCH, ceil_div(C / V, 64));
-  if (B > SE_MAX_B) return ACC_EBADSHAPE;
   double* part = reinterpret_cast<double*>(ws);
   SeMid m{Cr, w1, b1, w2, b2, gamma, beta, rmean, rvar, training ? nbt : nullptr,
           momentum, eps, training, save};
   const bool pro = sc != nullptr;
-  unsigned* tickets = nullptr;
-  if (hipGetSymbolAddress((void**)&tickets, HIP_SYMBOL(g_se_tickets)) != hipSuccess)
-    return ACC_ELAUNCH;
-  tickets += acc_stream_bank(s) * SE_MAX_B;
-  const size_t lds = (size_t)(C + Cr) * sizeof(float);
   with_dt(dt, [&](auto tag) {
     using T = decltype(tag);
     auto go = [&](auto kv, auto kp) {
       constexpr int KV = decltype(kv)::value;
       constexpr bool KP = decltype(kp)::value;
-      hipLaunchKernelGGL((se_reduce_gate_kernel<KV, T, KP>), grid, dim3(256), lds, s, (const T*)z,
-                         sc, sh, act, g, part, m, tickets);
+      hipLaunchKernelGGL((se_reduce_kernel<KV, T, KP>), grid, dim3(256), 0, s, (const T*)z, sc, sh,
+                         act, g, part);
     };
     using I4 = std::integral_constant<int, 4>;
     using I1 = std::integral_constant<int, 1>;
     if (V == 4) pro ? go(I4{}, std::true_type{}) : go(I4{}, std::false_type{});
     else pro ? go(I1{}, std::true_type{}) : go(I1{}, std::false_type{});
   });
-  static const int rev = [] {  // ACCUNET_SE_REV=0: the apply in the reduce's order (A/B)
-    const char* e = getenv("ACCUNET_SE_REV");
-    return e ? atoi(e) : 1;
-  }();
+  // S, Q and the gate per sample, then the BN-of-gated statistics per channel
+  hipLaunchKernelGGL(se_mid_sample_kernel, dim3(B), dim3(256), (C + Cr) * sizeof(float), s, part,
+                     g, m);
+  hipLaunchKernelGGL(se_mid_bn_kernel, dim3(ceil_div(C, 256)), dim3(256), 0, s, g, m);
+  const float* alpha = save + se_alpha_offset(B, C, Cr);
+  const float* betap = alpha + (size_t)B * C;
   with_dt(dt, [&](auto tag) {
     using T = decltype(tag);
     auto go = [&](auto kv, auto kp, auto kr) {
       hipLaunchKernelGGL((se_apply_kernel<decltype(kv)::value, T, decltype(kp)::value,
                                           decltype(kr)::value>),
-                         grid, dim3(256), 0, s, (const T*)z, sc, sh, act, g, m, rev,
+                         grid, dim3(256), 0, s, (const T*)z, sc, sh, act, g, alpha, betap,
                          (const T*)res, (T*)out, ostats);
     };
     using I4 = std::integral_constant<int, 4>;
@@ -933,11 +935,22 @@ extern "C" int accunet_se_fwd(const void* z, const float* sc, const float* sh, i
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }
 
-// the backward's ticket array of the launch stream's bank
-static unsigned* se_bwd_tickets(hipStream_t s) {
-  unsigned* t = nullptr;
-  if (hipGetSymbolAddress((void**)&t, HIP_SYMBOL(g_se_bwd_tickets)) != hipSuccess) return nullptr;
-  return t + acc_stream_bank(s) * (SE_MAX_B + 1);
+// the unfused backward middle step: per-(b,c) sums in scratch (from part) -> BN /
+// gate / fc backward, coef (A, Bc, Cc), fc parameter gradients (+ the prologue
+// coefficient step when m.pcoef is set)
+static void se_bwd_mid(const SeGeom& g, const SeBwdMid& m, const double* part, int nq,
+                       hipStream_t s) {
+  const int B = g.B, C = g.C, Cr = m.Cr;
+  if (nq == 2)
+    hipLaunchKernelGGL(se_bwd_chan_sum_kernel<2>, dim3(C), dim3(256), 0, s, part, g, m);
+  else
+    hipLaunchKernelGGL(se_bwd_chan_sum_kernel<SE_PRO_NQ>, dim3(C), dim3(256), 0, s, part, g, m);
+  hipLaunchKernelGGL(se_bwd_sample_kernel, dim3(B), dim3(256), (Cr > 0 ? Cr : 1) * sizeof(double),
+                     s, g, m);
+  const long nparam = 2L * C * Cr + C + Cr;
+  const int npb = ceil_div(nparam, 256);
+  const int ncb = m.pcoef ? ceil_div((long)C * SE_LANES, 256) : 0;
+  hipLaunchKernelGGL(se_bwd_tail_kernel, dim3(npb + ncb), dim3(256), 0, s, g, m, npb);
 }
 
 extern "C" int accunet_se_bwd(const void* z, const void* dout, const float* sc, const float* sh,
@@ -960,21 +973,19 @@ extern "C" int accunet_se_bwd(const void* z, const void* dout, const float* sc, 
   const float* betap = alpha + (size_t)B * C;
   const float* sgate = save + (size_t)B * C * 4 + (size_t)B * Cr;
   const float* mean = sgate + (size_t)B * C;
-  if (B > SE_MAX_B) return ACC_EBADSHAPE;
-  unsigned* tk = se_bwd_tickets(s);
-  if (!tk) return ACC_ELAUNCH;
-  SeBwdMid m{Cr, w1, w2, gamma, training, const_cast<float*>(save), scratch, coef,
-             dw1, db1, dw2, db2, dgamma, dbeta, nullptr, nullptr, 0, nullptr, nullptr, nullptr,
-             nullptr};
   with_dt(dt, [&](auto tag) {
     using T = decltype(tag);
     if (V == 4)
       hipLaunchKernelGGL((se_bwd_reduce_kernel<4, T>), grid, dim3(256), 0, s, (const T*)z,
-                         (const T*)dout, sc, sh, act, g, alpha, betap, part, m, tk);
+                         (const T*)dout, sc, sh, act, g, alpha, betap, part);
     else
       hipLaunchKernelGGL((se_bwd_reduce_kernel<1, T>), grid, dim3(256), 0, s, (const T*)z,
-                         (const T*)dout, sc, sh, act, g, alpha, betap, part, m, tk);
+                         (const T*)dout, sc, sh, act, g, alpha, betap, part);
   });
+  SeBwdMid m{Cr, w1, w2, gamma, training, const_cast<float*>(save), scratch, coef,
+             dw1, db1, dw2, db2, dgamma, dbeta, nullptr, nullptr, 0, nullptr, nullptr, nullptr,
+             nullptr};
+  se_bwd_mid(g, m, part, 2, s);
   with_dt(dt, [&](auto tag) {
     using T = decltype(tag);
     if (V == 4)
@@ -1017,18 +1028,16 @@ extern "C" int accunet_se_bwd_pro(const void* z, const void* dout, const float* 
   SeBwdMid m{Cr, w1, w2, gamma, training, const_cast<float*>(save), scratch, coef,
              dw1, db1, dw2, db2, dgamma, dbeta, pst, pgamma, ptraining, dpgamma, dpbeta, pcoef,
              dsum};
-  if (B > SE_MAX_B) return ACC_EBADSHAPE;
-  unsigned* tk = se_bwd_tickets(s);
-  if (!tk) return ACC_ELAUNCH;
   with_dt(dt, [&](auto tag) {
     using T = decltype(tag);
     if (V == 4)
       hipLaunchKernelGGL((se_bwd_reduce_pro_kernel<4, T>), grid, dim3(256), 0, s, (const T*)z,
-                         (const T*)dout, pst, act, g, alpha, betap, part, m, tk);
+                         (const T*)dout, pst, act, g, alpha, betap, part);
     else
       hipLaunchKernelGGL((se_bwd_reduce_pro_kernel<1, T>), grid, dim3(256), 0, s, (const T*)z,
-                         (const T*)dout, pst, act, g, alpha, betap, part, m, tk);
+                         (const T*)dout, pst, act, g, alpha, betap, part);
   });
+  se_bwd_mid(g, m, part, SE_PRO_NQ, s);
   double* cpart = nullptr;  // (dz's column sums: computed analytically, se_pro_coef_body)
   with_dt(dt, [&](auto tag) {
     using T = decltype(tag);

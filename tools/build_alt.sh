@@ -11,6 +11,9 @@ if [ "$REV" = WORKTREE ]; then
 else
   git archive "$REV" acc-unet-unext_amd/csrc include | tar -x -C _ab/${NAME}_src
 fi
+# ABI_HEADER=WORKTREE: stamp the working tree's header hash (a revision whose header
+# differs only in comments still loads under the current binding)
+if [ "${ABI_HEADER:-}" = WORKTREE ]; then cp include/accunet.h _ab/${NAME}_src/include/accunet.h; fi
 ABI=0x$(sha256sum _ab/${NAME}_src/include/accunet.h | cut -c1-15)
 cd _ab/${NAME}_src/acc-unet-unext_amd/csrc
 ls *.hip | xargs -P 8 -I{} sh -c "/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-result ${EXTRA_FLAGS:-} -DACCUNET_ABI_HASH=${ABI}LL -I../../include -I. -c {} -o {}.o"
