@@ -20,6 +20,8 @@ chain the blocks' NHWC `run` methods internally.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 from torch import nn
 
@@ -203,6 +205,9 @@ class ResPath(nn.Module):
         return ops.nhwc_to_nchw(self.run(_nchw_in(x)))
 
 
+_MLFC_PENDING = os.environ.get("ACCUNET_MLFC_PENDING", "1") != "0"
+
+
 def _log2(f):
     return f.bit_length() - 1
 
@@ -272,7 +277,10 @@ class MLFC(nn.Module):
                 srcs = [at[(m, l)] for m in range(l + 1)]
                 v1 = blk.run(srcs, ups=ups, consumer_bn=getattr(self, f"bns{l + 1}")[i],
                              slots=[sl[(m, l)] for m in range(l + 1)], wslot=ws)
-                xcs.append(ops.bn_act_add(v1).z)  # act(bns_l(.)) materialised
+                # act(bns_l(.)) stays pending: the merge conv applies it in its A prologue
+                # (and its backward runs bns_l's in the data-gradient epilogue), instead of
+                # a materialising pass and its backward (ACCUNET_MLFC_PENDING=0: A/B)
+                xcs.append(v1 if _MLFC_PENDING else ops.bn_act_add(v1).z)
             for l in range(4):
                 mrg = getattr(self, f"cnv_mrg{l + 1}")[i]
                 f = fs[l]
