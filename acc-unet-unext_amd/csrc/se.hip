@@ -271,9 +271,12 @@ __global__ void __launch_bounds__(256)
 se_apply_kernel(const T* __restrict__ z, const float* __restrict__ sc,
                 const float* __restrict__ sh, int act, SeGeom g, const float* __restrict__ alpha,
                 const float* __restrict__ betap, const T* __restrict__ res, T* __restrict__ out,
-                double* __restrict__ ostats) {
+                double* __restrict__ ostats, int rev) {
   ChanTile t = chan_tile<V>(g.C);
-  const int b = blockIdx.x / g.NCH, ch = blockIdx.x % g.NCH;
+  // rev: the blocks walk the chunks in the reverse of the reduce's order, so the first
+  // re-reads are of the lines the reduce fetched last (Infinity Cache residency)
+  const int lin = rev ? (int)(gridDim.x - 1 - blockIdx.x) : (int)blockIdx.x;
+  const int b = lin / g.NCH, ch = lin % g.NCH;
   long r0 = (long)b * g.HW + ch * g.rows_per;
   long r1 = min((long)b * g.HW + g.HW, r0 + g.rows_per);
   double o1[V], o2[V];
@@ -330,7 +333,7 @@ se_apply_kernel(const T* __restrict__ z, const float* __restrict__ sc,
     }
   }
   // optional statistics of the SE output (MLFC feeds it straight into bns_l, :427-487)
-  if (ostats) block_chan_reduce2<V>(t, o1, o2, ostats, blockIdx.x, g.C);
+  if (ostats) block_chan_reduce2<V>(t, o1, o2, ostats, lin, g.C);
 }
 
 // backward pass 1: partials of (T1 = sum g2, T2 = sum g2*a) per (b,c)
@@ -878,6 +881,16 @@ static bool se_chunk_ok(const SeGeom& g, int dt) {
   return g.rows_per * (long)g.C * (dt == ACC_BF16 ? 2 : 4) < (1L << 31);
 }
 
+// ACCUNET_SE_REV=1: the apply pass walks the chunks in reverse (A/B knob, default off)
+static int se_rev() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ACCUNET_SE_REV");
+    v = e ? atoi(e) : 0;
+  }
+  return v;
+}
+
 extern "C" int accunet_se_fwd(const void* z, const float* sc, const float* sh, int act, int B,
                               int HW, int C, int Cr, const float* w1, const float* b1,
                               const float* w2, const float* b2, const float* gamma,
@@ -922,7 +935,7 @@ extern "C" int accunet_se_fwd(const void* z, const float* sc, const float* sh, i
       hipLaunchKernelGGL((se_apply_kernel<decltype(kv)::value, T, decltype(kp)::value,
                                           decltype(kr)::value>),
                          grid, dim3(256), 0, s, (const T*)z, sc, sh, act, g, alpha, betap,
-                         (const T*)res, (T*)out, ostats);
+                         (const T*)res, (T*)out, ostats, se_rev());
     };
     using I4 = std::integral_constant<int, 4>;
     using I1 = std::integral_constant<int, 1>;
