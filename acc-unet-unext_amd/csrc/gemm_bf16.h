@@ -154,7 +154,9 @@ gemm_bf16_kernel(const GemmParams p) {
           aok[i] = ok;
           if (PRO_A != PRO_NONE) {  // the pending BatchNorm sits on source 0
             apro[i] = kb == 0;
-            const int kk = ok ? k : 0;
+            // coefficients exist for source 0's columns only: other sources' chunks read
+            // element 0 (unused: apro false) instead of past the end of a_scale / a_shift
+            const int kk = (ok && kb == 0) ? k : 0;
             asl[i] = ld4(p.a_scale + kk);
             asl2[i] = ld4(p.a_scale + kk + 4);
             ash[i] = ld4(p.a_shift + kk);
