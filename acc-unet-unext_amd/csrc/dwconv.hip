@@ -1765,13 +1765,16 @@ static bool dw_os_on(int B, int H, int W, int C, int dt, bool bnb) {
   return (long)B * H * W * C * 4 > (256L << 20) && C <= 1024;
 }
 #define DW_OS_R 8
-// ACCUNET_DW_OS16 (default 1): the one-shot launches without a BN-backward operand run
-// the 16-row, 512-thread tiles (dw3x3_os16_fwd_kernel); 0 = the 8-row tiles (A/B)
+// ACCUNET_DW_OS16=1: the one-shot launches without a BN-backward operand run the
+// 16-row, 512-thread tiles (dw3x3_os16_fwd_kernel). Off by default: at the K1 shape they
+// measured 160.4 us against 146.4 us for the 8-row tiles on one box (bench probe,
+// profiles/r06_os16_ab.txt) -- 4 waves per SIMD in 2 x 78 KB of LDS with the centre
+// column read from LDS lose more than the halved halo re-fetch and statistics tails gain.
 static bool dw_os16(bool bnb) {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("ACCUNET_DW_OS16");
-    v = e ? atoi(e) : 1;
+    v = e ? atoi(e) : 0;
   }
   return v != 0 && !bnb;
 }

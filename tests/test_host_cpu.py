@@ -387,9 +387,9 @@ def test_abi_host_side_contract_without_a_device():
     # above 256 MB by default, for every tile launch with ACCUNET_DW_OS=2; else 32-row
     # strips (1024 rows)
     os_on, os_all = os_knob != "0", os_knob == "2"
-    # the one-shot launches without a BN-backward operand run 16-row tiles (512 threads,
-    # 16 * 16 * 8 = 2048 rows) unless ACCUNET_DW_OS16=0 (8-row tiles: 4096 rows)
-    os16 = os.environ.get("ACCUNET_DW_OS16", "1") != "0"
+    # ACCUNET_DW_OS16=1: the one-shot launches without a BN-backward operand run 16-row
+    # tiles (512 threads, 16 * 16 * 8 = 2048 rows); by default 8-row tiles (4096 rows)
+    os16 = os.environ.get("ACCUNET_DW_OS16", "0") != "0"
     one_shot = 4 if os16 else 3
     assert lib.accunet_dw3x3_variant(16, 256, 256, 96, 0) == (one_shot if os_on else 1)
     assert lib.accunet_dw3x3_variant(16, 256, 256, 96, 1) == (one_shot if os_all else 1)

@@ -37,8 +37,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "gpurun_out")
 PROF = os.path.join(ROOT, "profiles")
 # the fp32 K1 kernel of 16x256x256x96: one-shot 8-row tiles
-K1 = os.environ.get("K1_KERNEL", "dw3x3_os16_fwd_kernel<8, float>")
-K1_GRID = 6144 * 512  # 2048 tiles (16 rows x 32 pixels) x 3 channel groups, 512 threads
+K1 = os.environ.get("K1_KERNEL", "dw3x3_os_fwd_kernel<8, 8, false, 0, float>")
+K1_GRID = 12288 * 256  # 4096 tiles (8 rows x 32 pixels) x 3 channel groups, 256 threads
 K3 = ["se_reduce_kernel<4, float, true>", "se_mid_sample_kernel", "se_mid_bn_kernel",
       "se_apply_kernel<4, float, true,"]
 
@@ -140,7 +140,7 @@ def k1_trace(rows, st):
     avg = lambda rs: sum(dur(r) for r in rs) / max(len(rs), 1) / 1e3
     pd = sorted(dur(r) for r in probe)
     lines = [f"rocprofv3 --kernel-trace of `python bench.py --steps 5 --warmup 2 --no-cpu-baseline` ({st})",
-             f"{K1} ..., {K1_GRID // 512} workgroups (16x256x256x96: cnv12 / cnv92 forward)",
+             f"{K1} ..., {K1_GRID // 256} workgroups (16x256x256x96: cnv12 / cnv92 forward)",
              f"  last 20 dispatches = bench.py roofline probe: avg {pavg / 1e3:.2f} us, median "
              f"{pd[len(pd) // 2] / 1e3:.2f} us ({805306368 / (pavg * 1e-9) / 1e9:.0f} GB/s at the avg)",
              f"  in-model dispatches of the same shape (the first and last K1 dispatch of each "
