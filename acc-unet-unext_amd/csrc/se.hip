@@ -8,10 +8,11 @@
 //   pass 1 (se_reduce): per-(b,c) S = sum_hw a, Q = sum_hw a^2      [reads z once]
 //   mid   (se_mid_sample, one block per sample): S, Q from the chunk partials,
 //                      m = S/HW, s = sigmoid(fc2(lrelu(fc1(m))))
-//   mid   (se_mid_bn, one thread per channel): BN stats of y = a*s derived exactly
-//                      from (S, Q, s): mean = sum_b s*S / n,  E[y^2] = sum_b s^2*Q / n
-//                      -> per-(b,c) alpha = gamma*rstd*s, per-c beta' = beta - gamma*rstd*mean
-//   pass 2 (se_apply): out = lrelu(alpha*a + beta')                [reads z, writes out]
+//   pass 2 (se_apply): prologue = BN stats of y = a*s derived exactly from (S, Q, s)
+//                      for the block's channels: mean = sum_b s*S / n, E[y^2] = sum_b
+//                      s^2*Q / n -> per-(b,c) alpha = gamma*rstd*s, per-c beta' = beta -
+//                      gamma*rstd*mean (se_chan_bn); then out = lrelu(alpha*a + beta')
+//                                                                  [reads z, writes out]
 // so neither a nor y = a*s is ever materialised.
 //
 // Backward:
@@ -196,11 +197,15 @@ ACC_DEV void se_mid_sample_body(const double* __restrict__ part, const SeGeom& g
 }
 
 // middle step, part 2, channel c: BatchNorm statistics of y = a*s derived from
-// (S, Q, s), running-stat update, per-(b,c) coefficients.
-ACC_DEV void se_mid_bn_body(const SeGeom& g, const SeMid& m, int c) {
+// (S, Q, s) -> k = gamma*rstd and beta' = beta - k*mean. Every apply block computes this
+// for its own channels in its prologue (same loop, same order: identical values in every
+// block, and no launch of its own); the block `writer` also updates the running
+// statistics and stores mean, rstd and beta' for the backward.
+struct SeChanBN {
+  float k, betap;
+};
+ACC_DEV SeChanBN se_chan_bn(const SeGeom& g, const SeMid& m, int c, bool writer) {
   const int B = g.B, C = g.C;
-  if (m.nbt && c == 0) *m.nbt += 1;  // num_batches_tracked (training only; null otherwise)
-  if (c >= C) return;
   SeSave sv = se_save_view(m.save, B, C, m.Cr);
   const double n = (double)B * g.HW;
   float mu, var;
@@ -217,8 +222,8 @@ ACC_DEV void se_mid_bn_body(const SeGeom& g, const SeMid& m, int c) {
     if (m2 < 0.0) m2 = 0.0;
     mu = (float)m1;
     var = (float)m2;
-    if (m.rmean) m.rmean[c] = (1.f - m.momentum) * m.rmean[c] + m.momentum * mu;
-    if (m.rvar)
+    if (writer && m.rmean) m.rmean[c] = (1.f - m.momentum) * m.rmean[c] + m.momentum * mu;
+    if (writer && m.rvar)
       m.rvar[c] = (1.f - m.momentum) * m.rvar[c] + m.momentum * (float)(m2 * n / (n - 1.0));
   } else {
     mu = m.rmean[c];
@@ -226,11 +231,13 @@ ACC_DEV void se_mid_bn_body(const SeGeom& g, const SeMid& m, int c) {
   }
   float rs = 1.f / sqrtf(var + m.eps);
   float k = m.gamma[c] * rs;
-  sv.mean[c] = mu;
-  sv.rstd[c] = rs;
-  sv.betap[c] = m.beta[c] - k * mu;
-#pragma unroll 8
-  for (int b = 0; b < B; ++b) sv.alpha[b * C + c] = k * *(sv.sg + b * C + c);
+  SeChanBN r{k, m.beta[c] - k * mu};
+  if (writer) {
+    sv.mean[c] = mu;
+    sv.rstd[c] = rs;
+    sv.betap[c] = r.betap;
+  }
+  return r;
 }
 
 // pass 1 forward: partials part[(b*NCH + chunk)][2][C] of (sum a, sum a^2).
@@ -258,9 +265,6 @@ se_mid_sample_kernel(const double* __restrict__ part, SeGeom g, SeMid m) {
   extern __shared__ __attribute__((aligned(16))) float se_dyn[];
   se_mid_sample_body(part, g, m, blockIdx.x, se_dyn);
 }
-__global__ void __launch_bounds__(256) se_mid_bn_kernel(SeGeom g, SeMid m) {
-  se_mid_bn_body(g, m, blockIdx.x * blockDim.x + threadIdx.x);
-}
 
 // pass 2 forward: out = lrelu(alpha[b,c]*a + betap[c]) (+ res: the residual add that
 // follows the SE in ResPath, ACC_UNet.py:326, and in the MLFC merge, :489-520, fused
@@ -269,14 +273,33 @@ __global__ void __launch_bounds__(256) se_mid_bn_kernel(SeGeom g, SeMid m) {
 template <int V, typename T, bool PRO, bool RES>
 __global__ void __launch_bounds__(256)
 se_apply_kernel(const T* __restrict__ z, const float* __restrict__ sc,
-                const float* __restrict__ sh, int act, SeGeom g, const float* __restrict__ alpha,
-                const float* __restrict__ betap, const T* __restrict__ res, T* __restrict__ out,
+                const float* __restrict__ sh, int act, SeGeom g, SeMid m,
+                const T* __restrict__ res, T* __restrict__ out,
                 double* __restrict__ ostats, int rev) {
+  __shared__ float s_k[256], s_bp[256];
   ChanTile t = chan_tile<V>(g.C);
   // rev: the blocks walk the chunks in the reverse of the reduce's order, so the first
   // re-reads are of the lines the reduce fetched last (Infinity Cache residency)
   const int lin = rev ? (int)(gridDim.x - 1 - blockIdx.x) : (int)blockIdx.x;
   const int b = lin / g.NCH, ch = lin % g.NCH;
+  // prologue: the BatchNorm-of-gated step of the block's channels (se_chan_bn); the
+  // blocks of chunk 0 store alpha = k*s of their sample, block (0, y) the per-channel
+  // state and the running statistics
+  const SeSave sv = se_save_view(m.save, g.B, g.C, m.Cr);
+  {
+    const int cbase = blockIdx.y * 64 * V, ncb = min(64 * V, g.C - cbase);
+    const bool writer = lin == 0;
+    for (int i = threadIdx.x; i < ncb; i += 256) {
+      const int c = cbase + i;
+      const SeChanBN r = se_chan_bn(g, m, c, writer);
+      s_k[i] = r.k;
+      s_bp[i] = r.betap;
+      if (ch == 0) sv.alpha[b * g.C + c] = r.k * *(sv.sg + b * g.C + c);
+    }
+    // num_batches_tracked (training only; null otherwise)
+    if (writer && blockIdx.y == 0 && threadIdx.x == 0 && m.nbt) *m.nbt += 1;
+    __syncthreads();
+  }
   long r0 = (long)b * g.HW + ch * g.rows_per;
   long r1 = min((long)b * g.HW + g.HW, r0 + g.rows_per);
   double o1[V], o2[V];
@@ -288,8 +311,9 @@ se_apply_kernel(const T* __restrict__ z, const float* __restrict__ sc,
     for (int j = 0; j < V; ++j) {
       s[j] = PRO ? sc[t.c0 + j] : 1.f;
       h[j] = PRO ? sh[t.c0 + j] : 0.f;
-      al[j] = alpha[b * g.C + t.c0 + j];
-      be[j] = betap[t.c0 + j];
+      const int cl = t.c0 + j - (int)blockIdx.y * 64 * V;  // block-local channel
+      al[j] = s_k[cl] * sv.sg[b * g.C + t.c0 + j];
+      be[j] = s_bp[cl];
     }
     const bool st = ostats != nullptr;
     auto elem = [&](bool ok, const float (&x)[V], const float (&rv)[V], float (&v)[V]) {
@@ -926,15 +950,13 @@ extern "C" int accunet_se_fwd(const void* z, const float* sc, const float* sh, i
   // S, Q and the gate per sample, then the BN-of-gated statistics per channel
   hipLaunchKernelGGL(se_mid_sample_kernel, dim3(B), dim3(256), (C + Cr) * sizeof(float), s, part,
                      g, m);
-  hipLaunchKernelGGL(se_mid_bn_kernel, dim3(ceil_div(C, 256)), dim3(256), 0, s, g, m);
-  const float* alpha = save + se_alpha_offset(B, C, Cr);
-  const float* betap = alpha + (size_t)B * C;
+  // (the BatchNorm-of-gated step runs in the apply's prologue, se_chan_bn)
   with_dt(dt, [&](auto tag) {
     using T = decltype(tag);
     auto go = [&](auto kv, auto kp, auto kr) {
       hipLaunchKernelGGL((se_apply_kernel<decltype(kv)::value, T, decltype(kp)::value,
                                           decltype(kr)::value>),
-                         grid, dim3(256), 0, s, (const T*)z, sc, sh, act, g, alpha, betap,
+                         grid, dim3(256), 0, s, (const T*)z, sc, sh, act, g, m,
                          (const T*)res, (T*)out, ostats, se_rev());
     };
     using I4 = std::integral_constant<int, 4>;
