@@ -809,11 +809,12 @@ dw3x3_os_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
   // image and every output row is stored, so no per-element masking
   const bool interior = h0 >= 1 && h0 + R + 1 <= g.H && w0 + TP <= g.W;
   float a0[4] = {0.f, 0.f, 0.f, 0.f}, a1[4] = {0.f, 0.f, 0.f, 0.f};
-  // forward statistics: fp32 sums of d = z - pv per thread, pv = the first output row of
-  // the wave's pixel-0 lane of the same quad (wave-uniform per quad, so the sums can be
-  // added across the wave's pixels in fp32): the squares stay at the scale of the spread
-  // (no cancellation for a channel whose mean is large against its spread); the count of
-  // kept elements rides along, and the fp64 fold restores sum z, sum z^2
+  // forward statistics: fp32 sums of d = z - pv per thread, pv = bias + (sum of the taps)
+  // * the tile's first activated input of the quad (block-uniform per quad, read from the
+  // exchange tile, so the sums can be added across the wave's pixels in fp32; a shuffle
+  // of the first output instead cost K1 ~5 %): the squares stay at the scale of the
+  // spread (no cancellation for a channel whose mean is large against its spread); the
+  // count of kept elements rides along, and the fp64 fold restores sum z, sum z^2
   f2v c1[2] = {{0.f, 0.f}, {0.f, 0.f}}, c2[2] = {{0.f, 0.f}, {0.f, 0.f}}, pv[2] = {{0.f, 0.f}, {0.f, 0.f}};
   float cnt = 0.f;
   double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
@@ -843,6 +844,20 @@ dw3x3_os_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
     }
   }
   __syncthreads();
+  if (!BNB) {  // the statistics pivot (see above): an estimate of z from one tile element
+    const float4 x0 = xb[1][1][q];
+    const float xv[4] = {x0.x, x0.y, x0.z, x0.w};
+    float pj[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float ws = k[0][j];
+#pragma unroll
+      for (int tp = 1; tp < 9; ++tp) ws += k[tp][j];
+      pj[j] = fmaf(ws, xv[j], bi[j]);
+    }
+    pv[0] = f2v{pj[0], pj[1]};
+    pv[1] = f2v{pj[2], pj[3]};
+  }
   if (BNB) {  // the pre-BN rows, issued once the raw tile has been consumed (registers)
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -874,13 +889,6 @@ dw3x3_os_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
         o[j] = rnd<T>(t0);  // statistics of the stored value
       }
       if (r < 2) continue;
-      if (!BNB && r == 2) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          pv[j].x = __shfl(o[2 * j], q, 64);
-          pv[j].y = __shfl(o[2 * j + 1], q, 64);
-        }
-      }
       if (BNB) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -1071,8 +1079,22 @@ dw3x3_os16_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
   __syncthreads();
   typedef dwf2 f2v;
   float a0[4] = {0.f, 0.f, 0.f, 0.f}, a1[4] = {0.f, 0.f, 0.f, 0.f};
-  // statistics as in dw3x3_os_fwd_kernel: fp32 sums of z - pv (pv wave-uniform per quad)
-  f2v c1[2] = {{0.f, 0.f}, {0.f, 0.f}}, c2[2] = {{0.f, 0.f}, {0.f, 0.f}}, pv[2] = {{0.f, 0.f}, {0.f, 0.f}};
+  // statistics as in dw3x3_os_fwd_kernel: fp32 sums of z - pv (pv block-uniform per quad)
+  f2v c1[2] = {{0.f, 0.f}, {0.f, 0.f}}, c2[2] = {{0.f, 0.f}, {0.f, 0.f}}, pv[2];
+  {
+    const float4 x0 = xb[1][1][q];
+    const float xv[4] = {x0.x, x0.y, x0.z, x0.w};
+    float pj[4];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      float ws = k[0][jj];
+#pragma unroll
+      for (int tp = 1; tp < 9; ++tp) ws += k[tp][jj];
+      pj[jj] = fmaf(ws, xv[jj], bi[jj]);
+    }
+    pv[0] = f2v{pj[0], pj[1]};
+    pv[1] = f2v{pj[2], pj[3]};
+  }
   float cnt = 0.f;
   auto taps = [&](auto interior_c) {
     constexpr bool IN = decltype(interior_c)::value;
@@ -1102,13 +1124,6 @@ dw3x3_os16_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
       row(j, o);
       const int h = h0 + half * R + j - 2;  // output row completed by this input row
       const bool on = IN || (win && h < g.H);
-      if (j == 2) {
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          pv[e].x = __shfl(o[2 * e], q, 64);
-          pv[e].y = __shfl(o[2 * e + 1], q, 64);
-        }
-      }
       f2v m01 = f2v{o[0], o[1]} - pv[0], m23 = f2v{o[2], o[3]} - pv[1];
       if (!IN) {
         m01 = on ? m01 : f2v{0.f, 0.f};
