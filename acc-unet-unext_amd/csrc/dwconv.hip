@@ -701,6 +701,27 @@ dw3x3_tile_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
 // (sum g, sum g*(bz - mean)), g = out * act'(bz*scale + shift), in fp64 per element.
 // Blocks are dispatched channel group fastest, then tiles in row-major image order.
 // ----------------------------------------------------------------------------
+// The statistics pivot of the one-shot tiles: output (row h0, pixel w0) of quad q --
+// bias, then the 9 taps row-major over exchange-tile rows 0..2, pixels 0..2 (the tap
+// loops' order: the value that pixel's own lane stores), rounded as stored. xb is the
+// [IR][IP][TCQ] float4 tile; every lane of the quad reads the same 9 elements.
+template <int TCQ, typename T>
+ACC_DEV void dw_os_pivot(const float4* xb, int IP, int q, const float (&k)[9][4],
+                         const float (&bi)[4], dwf2 (&pv)[2]) {
+  float t[4] = {bi[0], bi[1], bi[2], bi[3]};
+#pragma unroll
+  for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx) {
+      const float4 v = xb[(dy * IP + dx) * TCQ + q];
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) t[j] = fmaf(k[dy * 3 + dx][j], vv[j], t[j]);
+    }
+  pv[0] = dwf2{rnd<T>(t[0]), rnd<T>(t[1])};
+  pv[1] = dwf2{rnd<T>(t[2]), rnd<T>(t[3])};
+}
+
 struct DwOGeom {
   int B, H, W, C;
   int tilesW, tilesH, ncg;
@@ -809,12 +830,13 @@ dw3x3_os_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
   // image and every output row is stored, so no per-element masking
   const bool interior = h0 >= 1 && h0 + R + 1 <= g.H && w0 + TP <= g.W;
   float a0[4] = {0.f, 0.f, 0.f, 0.f}, a1[4] = {0.f, 0.f, 0.f, 0.f};
-  // forward statistics: fp32 sums of d = z - pv per thread, pv = bias + (sum of the taps)
-  // * the tile's first activated input of the quad (block-uniform per quad, read from the
-  // exchange tile, so the sums can be added across the wave's pixels in fp32; a shuffle
-  // of the first output instead cost K1 ~5 %): the squares stay at the scale of the
-  // spread (no cancellation for a channel whose mean is large against its spread); the
-  // count of kept elements rides along, and the fp64 fold restores sum z, sum z^2
+  // forward statistics: fp32 sums of d = z - pv per thread, pv = the tile's first output
+  // (row h0, pixel w0) of the quad, recomputed by every thread from the exchange tile
+  // (dw_os_pivot: block-uniform per quad, so the sums can be added across the wave's
+  // pixels in fp32; a shuffle of that lane's output inside the tap loop cost K1 ~5 %):
+  // the squares stay at the scale of the spread (no cancellation for a channel whose
+  // mean is large against its spread); the count of kept elements rides along, and the
+  // fp64 fold restores sum z, sum z^2
   f2v c1[2] = {{0.f, 0.f}, {0.f, 0.f}}, c2[2] = {{0.f, 0.f}, {0.f, 0.f}}, pv[2] = {{0.f, 0.f}, {0.f, 0.f}};
   float cnt = 0.f;
   double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
@@ -844,20 +866,7 @@ dw3x3_os_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
     }
   }
   __syncthreads();
-  if (!BNB) {  // the statistics pivot (see above): an estimate of z from one tile element
-    const float4 x0 = xb[1][1][q];
-    const float xv[4] = {x0.x, x0.y, x0.z, x0.w};
-    float pj[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float ws = k[0][j];
-#pragma unroll
-      for (int tp = 1; tp < 9; ++tp) ws += k[tp][j];
-      pj[j] = fmaf(ws, xv[j], bi[j]);
-    }
-    pv[0] = f2v{pj[0], pj[1]};
-    pv[1] = f2v{pj[2], pj[3]};
-  }
+  if (!BNB) dw_os_pivot<TCQ, T>(&xb[0][0][0], IP, q, k, bi, pv);
   if (BNB) {  // the pre-BN rows, issued once the raw tile has been consumed (registers)
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -1081,20 +1090,7 @@ dw3x3_os16_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
   float a0[4] = {0.f, 0.f, 0.f, 0.f}, a1[4] = {0.f, 0.f, 0.f, 0.f};
   // statistics as in dw3x3_os_fwd_kernel: fp32 sums of z - pv (pv block-uniform per quad)
   f2v c1[2] = {{0.f, 0.f}, {0.f, 0.f}}, c2[2] = {{0.f, 0.f}, {0.f, 0.f}}, pv[2];
-  {
-    const float4 x0 = xb[1][1][q];
-    const float xv[4] = {x0.x, x0.y, x0.z, x0.w};
-    float pj[4];
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      float ws = k[0][jj];
-#pragma unroll
-      for (int tp = 1; tp < 9; ++tp) ws += k[tp][jj];
-      pj[jj] = fmaf(ws, xv[jj], bi[jj]);
-    }
-    pv[0] = f2v{pj[0], pj[1]};
-    pv[1] = f2v{pj[2], pj[3]};
-  }
+  dw_os_pivot<TCQ, T>(&xb[0][0][0], IP, q, k, bi, pv);
   float cnt = 0.f;
   auto taps = [&](auto interior_c) {
     constexpr bool IN = decltype(interior_c)::value;
