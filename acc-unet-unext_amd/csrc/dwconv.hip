@@ -830,13 +830,12 @@ dw3x3_os_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
   // image and every output row is stored, so no per-element masking
   const bool interior = h0 >= 1 && h0 + R + 1 <= g.H && w0 + TP <= g.W;
   float a0[4] = {0.f, 0.f, 0.f, 0.f}, a1[4] = {0.f, 0.f, 0.f, 0.f};
-  // forward statistics: fp32 sums of d = z - pv per thread, pv = the tile's first output
-  // (row h0, pixel w0) of the quad, recomputed by every thread from the exchange tile
-  // (dw_os_pivot: block-uniform per quad, so the sums can be added across the wave's
-  // pixels in fp32; a shuffle of that lane's output inside the tap loop cost K1 ~5 %):
-  // the squares stay at the scale of the spread (no cancellation for a channel whose
-  // mean is large against its spread); the count of kept elements rides along, and the
-  // fp64 fold restores sum z, sum z^2
+  // forward statistics: fp32 sums of d = z - pv per thread, pv = the lane's own first
+  // output: the squares stay at the scale of the spread (no cancellation for a channel
+  // whose mean is large against its spread). At the tail the sums are re-centred on the
+  // pivot of the wave's pixel-0 lane of the quad (one shuffle, after the stores; a
+  // shuffle inside the tap loop, or recomputing that pivot from the tile, cost K1 ~5 %),
+  // added over the wave's pixels in fp32, and the fp64 fold restores sum z, sum z^2
   f2v c1[2] = {{0.f, 0.f}, {0.f, 0.f}}, c2[2] = {{0.f, 0.f}, {0.f, 0.f}}, pv[2] = {{0.f, 0.f}, {0.f, 0.f}};
   float cnt = 0.f;
   double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
@@ -866,7 +865,6 @@ dw3x3_os_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
     }
   }
   __syncthreads();
-  if (!BNB) dw_os_pivot<TCQ, T>(&xb[0][0][0], IP, q, k, bi, pv);
   if (BNB) {  // the pre-BN rows, issued once the raw tile has been consumed (registers)
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -898,6 +896,10 @@ dw3x3_os_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
         o[j] = rnd<T>(t0);  // statistics of the stored value
       }
       if (r < 2) continue;
+      if (!BNB && r == 2) {  // the lane's statistics pivot: its first output (registers)
+        pv[0] = f2v{o[0], o[1]};
+        pv[1] = f2v{o[2], o[3]};
+      }
       if (BNB) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -936,16 +938,31 @@ dw3x3_os_fwd_kernel(const T* __restrict__ x, const float* __restrict__ wt,
     // 2-3 us of K1's 150 against the block reduction through the tile)
     constexpr int WL = TCQ < 64 ? TCQ : 64;
     __shared__ double sw[4][WL][8];
-    if (interior) cnt = (float)R;
+    // re-centre on the quad's common pivot kc (lane q): sum (z - kc) = sum d + n dl,
+    // sum (z - kc)^2 = sum d^2 + dl (2 sum d + n dl), dl = pv - kc (fp32, small)
+    const float nl = interior ? (float)R : cnt;
+    f2v kc[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      kc[e].x = __shfl(pv[e].x, q, 64);
+      kc[e].y = __shfl(pv[e].y, q, 64);
+      const f2v dl = pv[e] - kc[e];
+      c2[e] = dl * (c1[e] * 2.f + dl * nl) + c2[e];
+      c1[e] = dl * nl + c1[e];
+    }
     float f[9] = {c1[0].x, c1[0].y, c1[1].x, c1[1].y, c2[0].x, c2[0].y, c2[1].x, c2[1].y, cnt};
 #pragma unroll
     for (int off = TCQ; off < 64; off <<= 1)
 #pragma unroll
-      for (int e = 0; e < 9; ++e) f[e] += __shfl_xor(f[e], off);
+      for (int e = 0; e < 8; ++e) f[e] += __shfl_xor(f[e], off);
+    if (!interior) {  // (block-uniform) the kept-element count of the wave's lanes
+#pragma unroll
+      for (int off = TCQ; off < 64; off <<= 1) f[8] += __shfl_xor(f[8], off);
+    }
     const int lane = tid & 63, wave = tid >> 6;
     if (lane < WL) {
-      const double n = f[8];
-      const float k0[4] = {pv[0].x, pv[0].y, pv[1].x, pv[1].y};
+      const double n = interior ? (double)(R * (64 / WL)) : (double)f[8];
+      const float k0[4] = {kc[0].x, kc[0].y, kc[1].x, kc[1].y};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const double kk = k0[j], d1 = f[j];
