@@ -102,6 +102,7 @@ _SIGS = {
     "accunet_upsample_bwd24": [P, I, P, I, P, I, I, I, I, I, I, P],
     "accunet_slice_copy": [P, I, I, P, I, I, L, I, I, I, P],
     "accunet_pixel_shuffle2": [P, P, P, I, I, I, I, I, I, P],
+    "accunet_convt_cat": [P, P, P, P, I, I, I, I, I, I, I, P],
     "accunet_permute4": [P, P, IP, POINTER(c_longlong), IP, I, I, I, P],
     "accunet_group_relayout": [P, P, I, I, I, IP, I, P],
     "accunet_se_save_elems": [I, I, I],

@@ -360,6 +360,16 @@ def pixel_shuffle2(t, bias, y, B, Hi, Wi, Cout, inverse=False):
          _same_dt(t, y), _stream())
 
 
+def convt_cat(t, bias, skip, y, B, Hi, Wi, Co, Cs, inverse=False):
+    """ConvT pixel shuffle (+bias) and channel concat with skip in one pass
+    (accunet_convt_cat); inverse: y is the gradient, t / skip receive theirs."""
+    for name, x in (("t", t), ("y", y), ("skip", skip)):
+        if x is not None and not x.is_contiguous():
+            raise _lib.AccError(f"convt_cat: {name} must be contiguous")
+    call("accunet_convt_cat", _p(t), _p(bias), _p(skip), _p(y), int(B), int(Hi), int(Wi), int(Co),
+         int(Cs), 1 if inverse else 0, _same_dt(t, y, skip), _stream())
+
+
 def permute4(inp, out, dims, strides, flips=None, accumulate=False):
     d = (ctypes.c_int * 4)(*[int(v) for v in dims])
     s = (ctypes.c_longlong * 4)(*[int(v) for v in strides])

@@ -431,11 +431,13 @@ class ACC_UNet(nn.Module):
         x2, x3, x4, x5 = self.mlfc1.run(x2, x3, x4, x5)
         x2, x3, x4, x5 = self.mlfc2.run(x2, x3, x4, x5)
         x2, x3, x4, x5 = self.mlfc3.run(x2, x3, x4, x5)
-        up = lambda m, t: ops.conv_transpose2x2(t, m.weight, m.bias)
-        x7 = self.cnv62.run(self.cnv61.run(ops.cat_channels(up(self.up6, x6), x5)))
-        x8 = self.cnv72.run(self.cnv71.run(ops.cat_channels(up(self.up7, x7), x4)))
-        x9 = self.cnv82.run(self.cnv81.run(ops.cat_channels(up(self.up8, x8), x3)))
-        x10 = self.cnv92.run(self.cnv91.run(ops.cat_channels(up(self.up9, x9), x2)))
+        # torch.cat([up(x), skip], dim=1): the ConvT output shuffled straight into the
+        # concatenated tensor (ops.conv_transpose2x2_cat)
+        upcat = lambda m, t, skip: ops.conv_transpose2x2_cat(t, m.weight, m.bias, skip)
+        x7 = self.cnv62.run(self.cnv61.run(upcat(self.up6, x6, x5)))
+        x8 = self.cnv72.run(self.cnv71.run(upcat(self.up7, x7, x4)))
+        x9 = self.cnv82.run(self.cnv81.run(upcat(self.up8, x8, x3)))
+        x10 = self.cnv92.run(self.cnv91.run(upcat(self.up9, x9, x2)))
         if self.out.weight.shape[0] == 1:
             y = ops.head(x10, self.out.weight, self.out.bias, self.last_activation is not None)
         else:

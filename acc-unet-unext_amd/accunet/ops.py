@@ -31,7 +31,7 @@ from ._lib import (ACT_LRELU, ACT_NONE, AMODE_COL, AMODE_SHIFT3, BMODE_NN, BMODE
                    PRO_AFFINE, PRO_AFFINE_LRELU, PRO_NONE)
 
 __all__ = ["Pending", "GradSlot", "pw_conv", "dw_conv", "hanc_layer", "bn_act_add", "se", "conv3x3",
-           "conv_transpose2x2", "pool2", "cat_channels", "head", "wmerge", "group_relayout",
+           "conv_transpose2x2", "conv_transpose2x2_cat", "pool2", "cat_channels", "head", "wmerge", "group_relayout",
            "to_nhwc", "weighted_dice_bce"]
 
 
@@ -1336,6 +1336,71 @@ class _ConvT2Fn(torch.autograd.Function):
 
 def conv_transpose2x2(x, weight, bias):
     return _ConvT2Fn.apply(x, weight, bias)
+
+
+class _ConvTCatFn(torch.autograd.Function):
+    """torch.cat([ConvTranspose2d(k=2, s=2)(x), skip], dim=1) (ACC_UNet.py:637-648): the
+    ConvT GEMM, then ONE pass that pixel-shuffles (+bias) its output into the first Co
+    channels of the concatenated tensor and copies skip into the rest (accunet_convt_cat);
+    the up-sampled tensor is never materialised on its own. Backward: one pass splits
+    the incoming gradient into dT (un-shuffled) and dskip, then the ConvT GEMMs; the bias
+    gradient is the column sums of dT ([P*4][Co])."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, skip):
+        B, H, W, Ci = x.shape
+        Co = weight.shape[1]
+        Cs = skip.shape[-1]
+        P = B * H * W
+        Wr = _prepared(weight, "ct")
+        if Wr is None:
+            Wr = _f32((Ci, 4 * Co), x)  # [ci][d][co], d = di*2+dj
+            kern.permute4(weight, Wr, (Ci, 2, 2, Co), (4 * Co, 2, 1, 4))
+        T = _act((B, H, W, 4 * Co), x)
+        kern.gemm(P, 4 * Co, Ci, a=[x], lda=[Ci], b=Wr, ldb=4 * Co, bmode=BMODE_NN, c=T,
+                  ldc=4 * Co)
+        Y = _act((B, 2 * H, 2 * W, Co + Cs), x)
+        kern.convt_cat(T, bias, skip.contiguous(), Y, B, H, W, Co, Cs)
+        ctx.save_for_backward(x, Wr)
+        ctx.shape = (B, H, W, Ci, Co, Cs)
+        return Y
+
+    @staticmethod
+    def backward(ctx, dY):
+        x, Wr = ctx.saved_tensors
+        B, H, W, Ci, Co, Cs = ctx.shape
+        P = B * H * W
+        dY = dY.contiguous()
+        dT = _act((B, H, W, 4 * Co), dY)
+        dskip = _act((B, 2 * H, 2 * W, Cs), dY) if ctx.needs_input_grad[3] else None
+        kern.convt_cat(dT, None, dskip, dY, B, H, W, Co, Cs, inverse=True)
+        keep = []
+        dx = None
+        dWr = _f32((Ci, 4 * Co), x)
+        dW = _f32((Ci, Co, 2, 2), x)
+        fork = _WgradFork(dT, 2.0 * Ci * 4 * Co * P)
+        with fork:  # weight gradient on the side stream (overlaps the data gradient)
+            keep.append(kern.gemm(Ci, 4 * Co, P, a=[x], lda=[Ci], amode=AMODE_COL, b=dT,
+                                  ldb=4 * Co, bmode=BMODE_NN, c=dWr, ldc=4 * Co, allow_split=True))
+            _wgrad_permute(dWr, dW, (Ci, Co, 2, 2), (4 * Co, 1, 2 * Co, Co))
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            keep.append(kern.gemm(P, Ci, 4 * Co, a=[dT], lda=[4 * Co], b=Wr, ldb=4 * Co, c=dx,
+                                  ldc=Ci))
+        db = _f32((Co,), x)
+        keep.append(kern.colsum(dT, P * 4, Co, db))
+        fork.join()
+        return dx, dW, db, dskip
+
+
+_CONVT_CAT = os.environ.get("ACCUNET_CONVT_CAT", "1") != "0"  # 0: ConvT, then cat (A/B)
+
+
+def conv_transpose2x2_cat(x, weight, bias, skip):
+    """torch.cat([ConvTranspose2d(x), skip], dim=1) in NHWC (the decoder's up + cat)."""
+    if not _CONVT_CAT or weight.shape[1] % 4 or skip.shape[-1] % 4:
+        return cat_channels(conv_transpose2x2(x, weight, bias), skip)
+    return _ConvTCatFn.apply(x, weight, bias, skip)
 
 
 # --------------------------------------------------------------------------

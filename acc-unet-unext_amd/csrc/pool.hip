@@ -576,6 +576,67 @@ extern "C" int accunet_pixel_shuffle2(const void* t, const float* bias, void* y,
 }
 
 // ---------------------------------------------------------------------------
+// Decoder up-sampling + channel concat in one pass (ACC_UNet.py:637-648:
+// torch.cat([ConvTranspose2d(x), skip], dim=1)): the ConvT GEMM output T [b,i,j,
+// (d*Co+co)] is pixel-shuffled (+bias) into channels [0, Co) of Y [b,ho,wo,Co+Cs] and
+// the skip tensor copied into channels [Co, Co+Cs); a block walks one output row in
+// channel quads. inverse: dY -> dT (shuffled back) and dskip (null: not wanted). The
+// shuffled values and the bias add are the pixel_shuffle2 kernel's, element for
+// element; the up-sampled tensor itself is never written (no slice copies).
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ void __launch_bounds__(256)
+convt_cat_kernel(T* __restrict__ t, const float* __restrict__ bias, T* __restrict__ skip,
+                 T* __restrict__ y, int Hi, int Wi, int Co, int Cs, int inverse) {
+  const int Ho = 2 * Hi, Wo = 2 * Wi, Ct = Co + Cs;
+  const int CQt = Ct / 4, CQo = Co / 4;
+  const int row = blockIdx.x;  // b * Ho + ho
+  const int ho = row % Ho, b = row / Ho;
+  const int di = ho & 1, hi = ho >> 1;
+  const long yrow = (long)row * Wo * Ct;
+  const long trow = ((long)b * Hi + hi) * Wi * (4 * Co);
+  const long srow = (long)row * Wo * Cs;
+  const int n = Wo * CQt;
+  for (int e = threadIdx.x; e < n; e += blockDim.x) {
+    const int wo = e / CQt, cq = e - wo * CQt;
+    T* yp = y + yrow + (long)wo * Ct + 4 * cq;
+    if (cq < CQo) {
+      const int d = di * 2 + (wo & 1), c = 4 * cq;
+      T* tp = t + trow + (long)(wo >> 1) * (4 * Co) + d * Co + c;
+      if (!inverse) {
+        float4 v = ldq(tp);
+        if (bias) {
+          const float4 bb = ld4(bias + c);
+          v.x += bb.x; v.y += bb.y; v.z += bb.z; v.w += bb.w;
+        }
+        stq(yp, v);
+      } else {
+        stq(tp, ldq(yp));
+      }
+    } else {
+      T* sp = skip ? skip + srow + (long)wo * Cs + 4 * (cq - CQo) : nullptr;
+      if (!inverse) stq(yp, ldq(sp));
+      else if (sp) stq(sp, ldq(yp));
+    }
+  }
+}
+
+extern "C" int accunet_convt_cat(void* t, const float* bias, void* skip, void* y, int B, int Hi,
+                                 int Wi, int Co, int Cs, int inverse, int dt, void* stream) {
+  if (B <= 0 || Hi <= 0 || Wi <= 0 || Co <= 0 || Cs < 0 || (Co % 4) || (Cs % 4))
+    return ACC_EBADSHAPE;
+  if (!t || !y || (!inverse && Cs > 0 && !skip)) return ACC_EBADARG;
+  if (with_dt(dt, [&](auto tag) {
+        using T = decltype(tag);
+        hipLaunchKernelGGL((convt_cat_kernel<T>), dim3(B * 2 * Hi), dim3(256), 0,
+                           (hipStream_t)stream, (T*)t, bias, (T*)skip, (T*)y, Hi, Wi, Co, Cs,
+                           inverse);
+      }))
+    return ACC_EBADARG;
+  return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
+}
+
+// ---------------------------------------------------------------------------
 // Generic 4-D permute: out[i0,i1,i2,i3] (out dims d) = in[...] with in strides
 // given per OUTPUT axis (so any permutation / flip is expressed by strides and
 // per-axis flip flags). accumulate adds into out.

@@ -259,6 +259,13 @@ int accunet_slice_copy(const void* src, int ld_src, int src_off, void* dst, int 
                        int dst_off, long P, int C, int accumulate, int dt, void* stream);
 int accunet_pixel_shuffle2(const void* t, const float* bias, void* y, int B, int Hi, int Wi,
                            int Cout, int inverse, int dt, void* stream);
+/* Decoder up-sampling and concat in one pass (ACC_UNet.py:637-648, torch.cat([up(x),
+ * skip], dim=1)): t = the ConvT GEMM output [B][Hi][Wi][4*Co] is pixel-shuffled (+bias)
+ * into channels [0, Co) of y [B][2Hi][2Wi][Co+Cs], skip [B][2Hi][2Wi][Cs] into
+ * [Co, Co+Cs). inverse = 1: y is the incoming gradient; t receives dT and skip (if not
+ * NULL) the skip's gradient. Co, Cs multiples of 4. */
+int accunet_convt_cat(void* t, const float* bias, void* skip, void* y, int B, int Hi, int Wi,
+                      int Co, int Cs, int inverse, int dt, void* stream);
 /* in_dt / out_dt: storage of in / out (e.g. NCHW fp32 input -> NHWC bf16 activations) */
 int accunet_permute4(const void* in, void* out, const int* dims, const long long* strides,
                      const int* flips, int accumulate, int in_dt, int out_dt, void* stream);
