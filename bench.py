@@ -534,6 +534,16 @@ def main():
                                      ("avg_us", "median_us", "frac", "copy_us", "frac_of_copy")}
         line["roofline"] = rl[0]
         line["rooflines"] = rl
+        # the HANC depthwise + SE reading, (bytes K1 + bytes K3) over the sum
+        # of their average launch times (two launch chains, no fused kernel)
+        k1, k3 = rl[0], rl[1]
+        by = k1["bytes_alg_per_launch"] + k3["bytes_alg_per_launch"]
+        us = k1["avg_us"] + k3["avg_us"]
+        gbs = by / (us * 1e-6) / 1e9
+        line["roofline_dw_se"] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+                                  "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+                                  "kernels": [k1["kernel"], k3["kernel"]],
+                                  "bytes_alg": by, "us": round(us, 2)}
     if args.eager:
         line["rooflines_in_model"] = prof.rooflines(HBM_PEAK_GBS)
     line["mode"] = "eager" if args.eager else "hipgraph"
