@@ -379,6 +379,10 @@ def test_abi_host_side_contract_without_a_device():
                                  4352, one, None, 0, 1, None) == -2  # bf16: bz check next
     assert lib.accunet_dw3x3_fwd(one, one, None, None, None, 0, 1, one, None, 1, 336, 336,
                                  4352, one, None, 0, 0, None) == -2
+    # the decoder's up + concat: channel counts in quads, a skip tensor in the forward
+    assert lib.accunet_convt_cat(one, None, one, one, 1, 2, 2, 6, 4, 0, 0, None) == -1
+    assert lib.accunet_convt_cat(one, None, one, one, 1, 2, 2, 8, 6, 0, 0, None) == -1
+    assert lib.accunet_convt_cat(one, None, None, one, 1, 2, 2, 8, 4, 0, 0, None) == -2
     # 16x256x256x96: one-shot tiles of 8 rows x 32 pixels -> 16 * 32 * 8 = 4096 statistics
     # rows (the strip kernel, ACCUNET_DW_OS=0: 32-row strips, 1024); cnv11's 9 channels
     # the register kernel
