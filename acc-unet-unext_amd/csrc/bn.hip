@@ -759,12 +759,10 @@ extern "C" int accunet_bn_bwd(const void* x, const void* dy, const float* st,
 // coef [3][C] floats, padded to an even count so what follows stays 8-byte aligned
 static size_t bn_coef_floats(int C) { return ((3 * (size_t)C + 1) / 2) * 2; }
 
-// ws (floats): fp64 reduce scratch (R rows) | coef [3][C] (even pad) | fp64 dsum partials
-// [nb][2][C] | fp64 dsum reduce scratch; nb = stream_rowblocks(P, C)
+// ws (floats): fp64 reduce scratch (R rows) | coef [3][C] (even pad)
 static size_t bn_bwd_part_ws(long P, int R, int C) {
-  const int nb = stream_rowblocks(P, C);
-  return accunet_partials_ws_elems(R, 2 * C) * 2 + bn_coef_floats(C) + (size_t)nb * 2 * C * 2 +
-         accunet_partials_ws_elems(nb, 2 * C) * 2;
+  (void)P;
+  return accunet_partials_ws_elems(R, 2 * C) * 2 + bn_coef_floats(C);
 }
 extern "C" size_t accunet_bn_bwd_part_ws_elems(long P, int R, int C) {
   return bn_bwd_part_ws(P, R, C);
@@ -785,13 +783,9 @@ extern "C" int accunet_bn_bwd_part(const void* x, const void* dy, const float* s
   const size_t scr_f = accunet_partials_ws_elems(R, 2 * C) * 2;
   double* scratch = reinterpret_cast<double*>(ws);
   float* coef = ws + scr_f;
-  double* cpart = reinterpret_cast<double*>(ws + scr_f + bn_coef_floats(C));
-  double* cscr = cpart + (size_t)nb * 2 * C;
   int rc = reduce_finish(part, true, R, 2 * C, scratch,
                          bn_bwd_fin(C, P, st, gamma, training, dgamma, dbeta, coef, 1, dsum), s);
   if (rc != ACC_OK) return rc;
-  (void)cpart;
-  (void)cscr;
   const dim3 agrid = grid;
   with_dt(dt, [&](auto tag) {
     using T = decltype(tag);
