@@ -1114,7 +1114,7 @@ class _SEFn(torch.autograd.Function):
         bn = cfg.bn
         mom = bn.momentum if bn.momentum is not None else 0.1
         tr = cfg.training
-        with _prof.region(f"se_fwd B{B} HW{HW} C{C}", kernel="se_reduce+se_mid_sample+se_mid_bn+se_apply",
+        with _prof.region(f"se_fwd B{B} HW{HW} C{C}", kernel="se_reduce+se_mid_sample+se_apply",
                           shape=f"{B}x{HW}x{C}", bytes_alg=2.0 * z.element_size() * B * HW * C):
             kern.se_fwd(z, pro.st[2] if pro.active else None,
                         pro.st[3] if pro.active else None, pro.act, B, HW, C, Cr, w1, b1, w2,

@@ -141,7 +141,7 @@ def k3_se(B, H, W, C, se_mod, iters=20, device="cuda", dtype=torch.float32):
                     p["fc2.bias"], p["bn.weight"], p["bn.bias"], rm, rv, None, 0.1, 1e-5, True,
                     out, save, None)
     t = _time(run, iters)
-    return _hbm_row("se_reduce+se_mid_sample+se_mid_bn+se_apply", f"{B}x{HW}x{C}",
+    return _hbm_row("se_reduce+se_mid_sample+se_apply", f"{B}x{HW}x{C}",
                     2.0 * z.element_size() * B * HW * C, t, iters)
 
 

@@ -39,7 +39,7 @@ PROF = os.path.join(ROOT, "profiles")
 # the fp32 K1 kernel of 16x256x256x96: one-shot 8-row tiles
 K1 = os.environ.get("K1_KERNEL", "dw3x3_os_fwd_kernel<8, 8, false, 0, float>")
 K1_GRID = 12288 * 256  # 4096 tiles (8 rows x 32 pixels) x 3 channel groups, 256 threads
-K3 = ["se_reduce_kernel<4, float, true>", "se_mid_sample_kernel", "se_mid_bn_kernel",
+K3 = ["se_reduce_kernel<4, float, true>", "se_mid_sample_kernel",
       "se_apply_kernel<4, float, true,"]
 
 FAMILIES = ["gemm_f32g", "gemm_f32", "gemm_bf16", "splitk", "dw3x3", "reduce_finish", "bn_bwd",
