@@ -629,7 +629,7 @@ bn_bwd_finalize_kernel(const double* __restrict__ part, int R, int C, double cou
   coef[2 * C + c] = k3;
 }
 
-template <int V, typename T>
+template <int V, int U, typename T>
 __global__ void __launch_bounds__(256)
 bn_bwd_apply_kernel(const T* __restrict__ x, const T* __restrict__ dy,
                     const float* __restrict__ st, const float* __restrict__ coef, int act,
@@ -672,7 +672,7 @@ bn_bwd_apply_kernel(const T* __restrict__ x, const T* __restrict__ dy,
       if (!accumulate) {
         const long nr = r1 > r0 ? r1 - r0 : 0;
         const __amdgpu_buffer_rsrc_t rd = acc_rsrc(dx + r0 * C, (unsigned)(nr * C * sizeof(T)));
-        quad_rows2<4>(x + r0 * C, dy + r0 * C, nr, t.rg, t.RG, C, t.c0,
+        quad_rows2<U>(x + r0 * C, dy + r0 * C, nr, t.rg, t.RG, C, t.c0,
                       [&](bool ok, float4 x4, float4 d4, unsigned off) {
                         const float xv[V] = {x4.x, x4.y, x4.z, x4.w};
                         const float dv[V] = {d4.x, d4.y, d4.z, d4.w};
@@ -687,6 +687,17 @@ bn_bwd_apply_kernel(const T* __restrict__ x, const T* __restrict__ dy,
       plain();
     }
   }
+}
+
+// rows of loads a thread of the BatchNorm-backward apply keeps in flight (per input):
+// ACCUNET_BN_APPLY_U=8 (A/B knob; default 4)
+static int bn_apply_u() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ACCUNET_BN_APPLY_U");
+    v = (e && atoi(e) == 8) ? 8 : 4;
+  }
+  return v;
 }
 
 extern "C" size_t accunet_bn_bwd_ws_elems(long P, int C) {
@@ -744,11 +755,14 @@ extern "C" int accunet_bn_bwd(const void* x, const void* dy, const float* st,
   const dim3 agrid = grid;
   with_dt(dt, [&](auto tag) {
     using T = decltype(tag);
-    if (V == 4)
-      hipLaunchKernelGGL((bn_bwd_apply_kernel<4, T>), agrid, dim3(256), 0, s, (const T*)x,
+    if (V == 4 && bn_apply_u() == 8)
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<4, 8, T>), agrid, dim3(256), 0, s, (const T*)x,
+                         (const T*)dy, st, coef, act, P, C, (T*)dx, accumulate);
+    else if (V == 4)
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<4, 4, T>), agrid, dim3(256), 0, s, (const T*)x,
                          (const T*)dy, st, coef, act, P, C, (T*)dx, accumulate);
     else
-      hipLaunchKernelGGL((bn_bwd_apply_kernel<1, T>), agrid, dim3(256), 0, s, (const T*)x,
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<1, 4, T>), agrid, dim3(256), 0, s, (const T*)x,
                          (const T*)dy, st, coef, act, P, C, (T*)dx, accumulate);
   });
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
@@ -789,11 +803,14 @@ extern "C" int accunet_bn_bwd_part(const void* x, const void* dy, const float* s
   const dim3 agrid = grid;
   with_dt(dt, [&](auto tag) {
     using T = decltype(tag);
-    if (V == 4)
-      hipLaunchKernelGGL((bn_bwd_apply_kernel<4, T>), agrid, dim3(256), 0, s, (const T*)x,
+    if (V == 4 && bn_apply_u() == 8)
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<4, 8, T>), agrid, dim3(256), 0, s, (const T*)x,
+                         (const T*)dy, st, coef, act, P, C, (T*)dx, 0);
+    else if (V == 4)
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<4, 4, T>), agrid, dim3(256), 0, s, (const T*)x,
                          (const T*)dy, st, coef, act, P, C, (T*)dx, 0);
     else
-      hipLaunchKernelGGL((bn_bwd_apply_kernel<1, T>), agrid, dim3(256), 0, s, (const T*)x,
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<1, 4, T>), agrid, dim3(256), 0, s, (const T*)x,
                          (const T*)dy, st, coef, act, P, C, (T*)dx, 0);
   });
   return hipGetLastError() == hipSuccess ? ACC_OK : ACC_ELAUNCH;
