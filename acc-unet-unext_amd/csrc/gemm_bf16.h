@@ -20,6 +20,18 @@
 
 #define GB_BK 32
 #define GB_SK (GB_BK + 8)
+// k-tiles of register-staged operands in flight: 1 (tile kt+1 loads while kt computes)
+// or 2 (tiles kt+1 and kt+2; the main loop unrolled by two so every staging slot index
+// is a compile-time constant). Depth 2 applies to the fp32-output vector instances
+// without an A prologue (split-K slabs, weight gradients), whose blocks walk long k
+// ranges: the bf16 GEMM census has those 6 % faster with it (16384 x 128 x 8704
+// split-K: 218 -> 139 us), but they run on the side stream beside the data gradients,
+// and the bf16 step did not move (profiles/r06_gb_pf_ab.txt); the bf16-output GEMMs
+// (short K, heavy epilogues) and the A-prologue instances ran slower with depth 2 (more
+// VGPRs: a wave per SIMD less). Default 1.
+#ifndef GB_PF
+#define GB_PF 1
+#endif
 
 // ---- 8-element chunks -----------------------------------------------------
 ACC_DEV void unpack8(uint4 u, float (&f)[8]) {
@@ -122,19 +134,24 @@ gemm_bf16_kernel(const GemmParams p) {
   // for the loads there, after this k-tile's MFMAs, not right after issuing them.
   // The scalar fallback paths (!VA / !VB) finish their chunk at load time.
   constexpr bool BF = sizeof(TB) == 4;  // fp32 B operand (weights): rounded at the store
-  uint4 ra[NPA], rb[NPB];
-  float4 rbl[BF ? NPB : 1], rbh[BF ? NPB : 1];
-  float4 asl[PRO_A != PRO_NONE ? NPA : 1], ash[PRO_A != PRO_NONE ? NPA : 1];
-  float4 asl2[PRO_A != PRO_NONE ? NPA : 1], ash2[PRO_A != PRO_NONE ? NPA : 1];
-  bool aok[NPA], apro[NPA], bok[NPB];
+  static_assert(GB_PF == 1 || GB_PF == 2, "register prefetch depth 1 or 2");
+  constexpr bool PF2OK = GB_PF == 2 && VA && VB && PRO_A == PRO_NONE && EPI == 0 &&
+                        sizeof(TC) == 4;
+  constexpr int PF = PF2OK ? 2 : 1;
+  uint4 ra[PF][NPA], rb[PF][NPB];
+  float4 rbl[PF][BF ? NPB : 1], rbh[PF][BF ? NPB : 1];
+  float4 asl[PF][PRO_A != PRO_NONE ? NPA : 1], ash[PF][PRO_A != PRO_NONE ? NPA : 1];
+  float4 asl2[PF][PRO_A != PRO_NONE ? NPA : 1], ash2[PF][PRO_A != PRO_NONE ? NPA : 1];
+  bool aok[PF][NPA], apro[PF][NPA], bok[PF][NPB];
 
-  auto load_tiles = [&](int k0) {
+  // sl: staging slot (compile-time after unrolling)
+  auto load_tiles = [&](int k0, int sl) {
     // ------------------------------ A ---------------------------------------
 #pragma unroll
     for (int i = 0; i < NPA; ++i) {
       const int c = tid + i * GEMM_THREADS;
-      aok[i] = false;
-      apro[i] = false;
+      aok[sl][i] = false;
+      apro[sl][i] = false;
       if (AMODE == AM_ROW) {
         const int r = c / (BK / 8), q = c % (BK / 8);
         const int g = m0 + r, k = k0 + 8 * q;
@@ -150,17 +167,17 @@ gemm_bf16_kernel(const GemmParams p) {
             if (p.nsrc > 3 && k >= p.kbeg[3]) { base = (const TA*)p.A[3]; ld = p.lda[3]; kb = p.kbeg[3]; }
           }
           const TA* src = ok ? base + (long)g * ld + (k - kb) : A0;
-          ra[i] = ld8_bf(src);
-          aok[i] = ok;
+          ra[sl][i] = ld8_bf(src);
+          aok[sl][i] = ok;
           if (PRO_A != PRO_NONE) {  // the pending BatchNorm sits on source 0
-            apro[i] = kb == 0;
+            apro[sl][i] = kb == 0;
             // coefficients exist for source 0's columns only: other sources' chunks read
             // element 0 (unused: apro false) instead of past the end of a_scale / a_shift
             const int kk = (ok && kb == 0) ? k : 0;
-            asl[i] = ld4(p.a_scale + kk);
-            asl2[i] = ld4(p.a_scale + kk + 4);
-            ash[i] = ld4(p.a_shift + kk);
-            ash2[i] = ld4(p.a_shift + kk + 4);
+            asl[sl][i] = ld4(p.a_scale + kk);
+            asl2[sl][i] = ld4(p.a_scale + kk + 4);
+            ash[sl][i] = ld4(p.a_shift + kk);
+            ash2[sl][i] = ld4(p.a_shift + kk + 4);
           }
         } else {
           uint4 v = make_uint4(0u, 0u, 0u, 0u);
@@ -182,7 +199,7 @@ gemm_bf16_kernel(const GemmParams p) {
             }
             v = pack8(f);
           }
-          ra[i] = v;
+          ra[sl][i] = v;
         }
       } else if (AMODE == AM_SHIFT3) {
         const int r = c / (BK / 8), q = c % (BK / 8);
@@ -194,8 +211,8 @@ gemm_bf16_kernel(const GemmParams p) {
           const int dh = tap / 3 - 1, dw = tap - (tap / 3) * 3 - 1;
           const int hh = a_h[i] + dh, ww = a_w[i] + dw;
           const bool ok = c < NCA && g < M && k < K && hh >= 0 && hh < p.H && ww >= 0 && ww < p.W;
-          ra[i] = ld8_bf(ok ? A0 + ((long)g + dh * p.W + dw) * lda + ci : A0);
-          aok[i] = ok;
+          ra[sl][i] = ld8_bf(ok ? A0 + ((long)g + dh * p.W + dw) * lda + ci : A0);
+          aok[sl][i] = ok;
         } else {
           uint4 v = make_uint4(0u, 0u, 0u, 0u);
           if (c < NCA && g < M) {
@@ -215,7 +232,7 @@ gemm_bf16_kernel(const GemmParams p) {
             }
             v = pack8(f);
           }
-          ra[i] = v;
+          ra[sl][i] = v;
         }
       } else {  // AM_COL (transposed): A(m,k) = A[k*lda + m], 8 consecutive m at one k
         const int kr = c % BK, cq = c / BK;
@@ -223,8 +240,8 @@ gemm_bf16_kernel(const GemmParams p) {
         const TA* src = A0 + (long)k * p.lda[0] + m;
         if (VA) {
           const bool ok = c < NCA && k < kend && m < M;
-          ra[i] = ld8_bf(ok ? src : A0);
-          aok[i] = ok;
+          ra[sl][i] = ld8_bf(ok ? src : A0);
+          aok[sl][i] = ok;
         } else {
           uint4 v = make_uint4(0u, 0u, 0u, 0u);
           if (c < NCA && k < kend) {
@@ -233,7 +250,7 @@ gemm_bf16_kernel(const GemmParams p) {
             for (int j = 0; j < 8; ++j) f[j] = (m + j < M) ? ld1(src + j) : 0.f;
             v = pack8(f);
           }
-          ra[i] = v;
+          ra[sl][i] = v;
         }
       }
     }
@@ -241,7 +258,7 @@ gemm_bf16_kernel(const GemmParams p) {
 #pragma unroll
     for (int i = 0; i < NPB; ++i) {
       const int c = tid + i * GEMM_THREADS;
-      bok[i] = false;
+      bok[sl][i] = false;
       const TB* src = Bp;
       bool vec = false;  // this chunk goes through the raw (store-time) path
       uint4 v = make_uint4(0u, 0u, 0u, 0u);
@@ -249,8 +266,8 @@ gemm_bf16_kernel(const GemmParams p) {
         const int r = c / (BK / 8), q = c % (BK / 8);
         const int n = n0 + r, k = k0 + 8 * q;
         if (VB) {
-          bok[i] = c < NCB && n < N && k < kend;
-          src = bok[i] ? Bp + (long)n * p.ldb + k : Bp;
+          bok[sl][i] = c < NCB && n < N && k < kend;
+          src = bok[sl][i] ? Bp + (long)n * p.ldb + k : Bp;
           vec = true;
         } else if (c < NCB && n < N) {
           const TB* s0 = Bp + (long)n * p.ldb + k;
@@ -263,8 +280,8 @@ gemm_bf16_kernel(const GemmParams p) {
         const int kr = c % BK, cq = c / BK;
         const int k = k0 + kr, n = n0 + 8 * cq;
         if (VB) {
-          bok[i] = c < NCB && k < kend && n < N;
-          src = bok[i] ? Bp + (long)k * p.ldb + n : Bp;
+          bok[sl][i] = c < NCB && k < kend && n < N;
+          src = bok[sl][i] ? Bp + (long)k * p.ldb + n : Bp;
           vec = true;
         } else if (c < NCB && k < kend) {
           const TB* s0 = Bp + (long)k * p.ldb + n;
@@ -289,9 +306,9 @@ gemm_bf16_kernel(const GemmParams p) {
           const int tap = (int)fdiv((uint32_t)n, p.fC);
           const int ci = n - tap * p.cin;
           const int dh = tap / 3 - 1, dw = tap - (tap / 3) * 3 - 1;
-          bok[i] = c < NCB && k < kend && n < N && hh0 + dh >= 0 && hh0 + dh < p.H &&
+          bok[sl][i] = c < NCB && k < kend && n < N && hh0 + dh >= 0 && hh0 + dh < p.H &&
                    ww0 + dw >= 0 && ww0 + dw < p.W;
-          src = bok[i] ? Bp + ((long)k + dh * p.W + dw) * p.ldb + ci : Bp;
+          src = bok[sl][i] ? Bp + ((long)k + dh * p.W + dw) * p.ldb + ci : Bp;
           vec = true;
         } else if (c < NCB && k < kend) {
           float f[8];
@@ -312,62 +329,62 @@ gemm_bf16_kernel(const GemmParams p) {
       }
       if (vec) {
         if constexpr (BF) {
-          rbl[i] = ld4((const float*)src);
-          rbh[i] = ld4((const float*)src + 4);
+          rbl[sl][i] = ld4((const float*)src);
+          rbh[sl][i] = ld4((const float*)src + 4);
         } else {
-          rb[i] = *reinterpret_cast<const uint4*>(src);
+          rb[sl][i] = *reinterpret_cast<const uint4*>(src);
         }
       } else {
-        rb[i] = v;
+        rb[sl][i] = v;
       }
     }
   };
 
   // the LDS image of A / B chunk i, finished from its raw staging registers
-  auto a_chunk = [&](int i) -> uint4 {
-    if (!VA) return ra[i];
+  auto a_chunk = [&](int i, int sl) -> uint4 {
+    if (!VA) return ra[sl][i];
     const uint4 z = make_uint4(0u, 0u, 0u, 0u);
     if (PRO_A != PRO_NONE && AMODE == AM_ROW) {
       float f[8];
-      unpack8(ra[i], f);
-      const float sc[8] = {asl[i].x, asl[i].y, asl[i].z, asl[i].w, asl2[i].x, asl2[i].y, asl2[i].z, asl2[i].w};
-      const float sh[8] = {ash[i].x, ash[i].y, ash[i].z, ash[i].w, ash2[i].x, ash2[i].y, ash2[i].z, ash2[i].w};
+      unpack8(ra[sl][i], f);
+      const float sc[8] = {asl[sl][i].x, asl[sl][i].y, asl[sl][i].z, asl[sl][i].w, asl2[sl][i].x, asl2[sl][i].y, asl2[sl][i].z, asl2[sl][i].w};
+      const float sh[8] = {ash[sl][i].x, ash[sl][i].y, ash[sl][i].z, ash[sl][i].w, ash2[sl][i].x, ash2[sl][i].y, ash2[sl][i].z, ash2[sl][i].w};
 #pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] = apro[i] ? pro_apply<PRO_A>(f[j], sc[j], sh[j]) : f[j];
-      return aok[i] ? pack8(f) : z;
+      for (int j = 0; j < 8; ++j) f[j] = apro[sl][i] ? pro_apply<PRO_A>(f[j], sc[j], sh[j]) : f[j];
+      return aok[sl][i] ? pack8(f) : z;
     }
-    return aok[i] ? ra[i] : z;
+    return aok[sl][i] ? ra[sl][i] : z;
   };
-  auto b_chunk = [&](int i) -> uint4 {
-    if (!VB) return rb[i];
+  auto b_chunk = [&](int i, int sl) -> uint4 {
+    if (!VB) return rb[sl][i];
     const uint4 z = make_uint4(0u, 0u, 0u, 0u);
     if constexpr (BF) {
-      float f[8] = {rbl[i].x, rbl[i].y, rbl[i].z, rbl[i].w, rbh[i].x, rbh[i].y, rbh[i].z, rbh[i].w};
+      float f[8] = {rbl[sl][i].x, rbl[sl][i].y, rbl[sl][i].z, rbl[sl][i].w, rbh[sl][i].x, rbh[sl][i].y, rbh[sl][i].z, rbh[sl][i].w};
       if (BMODE == BM_NN && PRO_B != PRO_NONE) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) f[j] = pro_apply<PRO_B>(f[j], bsc[i][j], bsh[i][j]);
       }
-      return bok[i] ? pack8(f) : z;
+      return bok[sl][i] ? pack8(f) : z;
     } else {
       if (BMODE == BM_NN && PRO_B != PRO_NONE) {
         float f[8];
-        unpack8(rb[i], f);
+        unpack8(rb[sl][i], f);
 #pragma unroll
         for (int j = 0; j < 8; ++j) f[j] = pro_apply<PRO_B>(f[j], bsc[i][j], bsh[i][j]);
-        return bok[i] ? pack8(f) : z;
+        return bok[sl][i] ? pack8(f) : z;
       }
-      return bok[i] ? rb[i] : z;
+      return bok[sl][i] ? rb[sl][i] : z;
     }
   };
 
-  auto store_tiles = [&](int buf) {
+  auto store_tiles = [&](int buf, int sl) {
     bf16_t* as = As + buf * BM * SK;
     bf16_t* bs = Bs + buf * BN * SK;
 #pragma unroll
     for (int i = 0; i < NPA; ++i) {
       const int c = tid + i * GEMM_THREADS;
       if (c < NCA) {
-        const uint4 v = a_chunk(i);
+        const uint4 v = a_chunk(i, sl);
         if (!TRA) {
           *reinterpret_cast<uint4*>(as + (c / (BK / 8)) * SK + 8 * (c % (BK / 8))) = v;
         } else {
@@ -381,7 +398,7 @@ gemm_bf16_kernel(const GemmParams p) {
     for (int i = 0; i < NPB; ++i) {
       const int c = tid + i * GEMM_THREADS;
       if (c < NCB) {
-        const uint4 v = b_chunk(i);
+        const uint4 v = b_chunk(i, sl);
         if (!TRB) {
           *reinterpret_cast<uint4*>(bs + (c / (BK / 8)) * SK + 8 * (c % (BK / 8))) = v;
         } else {
@@ -404,39 +421,68 @@ gemm_bf16_kernel(const GemmParams p) {
   const int am_off = (wm * TM * 32 + l31) * SK + 8 * lh;
   const int bn_off = (wn * TN * 32 + l31) * SK + 8 * lh;
 
-  if (nkt > 0) {
-    load_tiles(kstart);
-    store_tiles(0);
-    __syncthreads();
-    for (int kt = 0; kt < nkt; ++kt) {
-      const int buf = kt & 1;
-      // unconditional (the last iteration reloads its own tile, unused): no branch
-      // around the loads, so their waits are counted at the store below
-      load_tiles(kstart + min(kt + 1, nkt - 1) * BK);
-      // keep the loads ahead of this tile's MFMAs (the scheduler would otherwise sink
-      // them next to their LDS stores and expose their latency)
-      __builtin_amdgcn_sched_barrier(0);
-      const bf16_t* as = As + buf * BM * SK;
-      const bf16_t* bs = Bs + buf * BN * SK;
+  // the MFMAs of one k-tile from LDS buffer buf
+  auto compute = [&](int buf) {
+    const bf16_t* as = As + buf * BM * SK;
+    const bf16_t* bs = Bs + buf * BN * SK;
 #pragma unroll
-      for (int ks = 0; ks < BK / 16; ++ks) {
-        bf16x8_v a[TM], b[TN];
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      bf16x8_v a[TM], b[TN];
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
-          a[i] = *reinterpret_cast<const bf16x8_v*>(as + am_off + i * 32 * SK + 16 * ks);
+      for (int i = 0; i < TM; ++i)
+        a[i] = *reinterpret_cast<const bf16x8_v*>(as + am_off + i * 32 * SK + 16 * ks);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        b[j] = *reinterpret_cast<const bf16x8_v*>(bs + bn_off + j * 32 * SK + 16 * ks);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          b[j] = *reinterpret_cast<const bf16x8_v*>(bs + bn_off + j * 32 * SK + 16 * ks);
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  if constexpr (!PF2OK) {
+    if (nkt > 0) {
+      load_tiles(kstart, 0);
+      store_tiles(0, 0);
+      __syncthreads();
+      for (int kt = 0; kt < nkt; ++kt) {
+        const int buf = kt & 1;
+        // unconditional (the last iteration reloads its own tile, unused): no branch
+        // around the loads, so their waits are counted at the store below
+        load_tiles(kstart + min(kt + 1, nkt - 1) * BK, 0);
+        // keep the loads ahead of this tile's MFMAs (the scheduler would otherwise sink
+        // them next to their LDS stores and expose their latency)
+        __builtin_amdgcn_sched_barrier(0);
+        compute(buf);
+        __builtin_amdgcn_sched_barrier(0);
+        if (kt + 1 < nkt) store_tiles(buf ^ 1, 0);
+        __syncthreads();
       }
+    }
+  } else if (nkt > 0) {
+    // tile t sits in staging slot t & 1 and LDS buffer t & 1; two tiles in flight
+    load_tiles(kstart, 0);
+    load_tiles(kstart + min(1, nkt - 1) * BK, 1);
+    store_tiles(0, 0);
+    __syncthreads();
+    int kt = 0;
+    for (; kt + 1 < nkt; kt += 2) {  // tiles kt (buffer 0) and kt + 1 (buffer 1)
+      load_tiles(kstart + min(kt + 2, nkt - 1) * BK, 0);
       __builtin_amdgcn_sched_barrier(0);
-      if (kt + 1 < nkt) store_tiles(buf ^ 1);
+      compute(0);
+      __builtin_amdgcn_sched_barrier(0);
+      store_tiles(1, 1);
+      __syncthreads();
+      load_tiles(kstart + min(kt + 3, nkt - 1) * BK, 1);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(1);
+      __builtin_amdgcn_sched_barrier(0);
+      if (kt + 2 < nkt) store_tiles(0, 0);
       __syncthreads();
     }
+    if (kt < nkt) compute(0);  // odd count: the last tile is already in buffer 0
   }
   gemm_epilogue<TC, EPI, WM, TM, TN>(p, acc, reinterpret_cast<float*>(smem_raw), m0, n0);
 }
