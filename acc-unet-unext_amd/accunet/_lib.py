@@ -130,6 +130,10 @@ _SIGS = {
     "accunet_event_destroy": [P],
     "accunet_stream_wait_event": [P, P],
     "accunet_event_synchronize": [P],
+    "accunet_event_create_timed": [POINTER(c_void_p)],
+    "accunet_graph_time_markers": [P, I, I, P, P, POINTER(c_void_p)],
+    "accunet_graph_exec_event_set": [P, P, P],
+    "accunet_event_elapsed_ms": [P, P, POINTER(c_float)],
     "accunet_image_prep": [P, I, I, I, I, P, P],
     "accunet_mask_prep": [P, I, I, I, I, I, P, P],
     "accunet_aug_geom": [P, P, I, I, I, I, P, P],

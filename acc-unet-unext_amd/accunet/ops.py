@@ -790,7 +790,7 @@ class _DWConvFn(torch.autograd.Function):
             stats = _stats((kern.dw3x3_rows(B, H, W, C, z), 2, C), z)
         pro = cfg.pro
         # csrc/dwconv.hip picks the LDS-tiled kernel whenever C % 32 == 0
-        kname = kern.dw3x3_kernel_name(B, H, W, C)
+        kname = kern.dw3x3_kernel_name(B, H, W, C, z)
         with _prof.region(f"dw3x3_fwd B{B} {H}x{W} C{C}", kernel=kname,
                           shape=f"{B}x{H}x{W}x{C}",
                           bytes_alg=2.0 * z.element_size() * B * H * W * C):

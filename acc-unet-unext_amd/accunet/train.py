@@ -39,6 +39,7 @@ import contextlib
 import os
 
 from . import kern, ops
+from . import profile as _prof
 from .loss import WeightedDiceBCE
 from .optim import FusedAdam
 
@@ -323,7 +324,12 @@ class TrainStep:
         self._defer = None
         if os.environ.get("ACCUNET_DEFER_RELAYOUT", "1") != "0":
             self._defer = ops.DeferredRelayouts(self._x.device)
-        g = torch.cuda.CUDAGraph(keep_graph=self._buckets is not None)
+        # in-graph timing (accunet/profile.py, bench.py's roofline): marker ids below the
+        # bucket count are the buckets'; the timed launches' markers become event-record
+        # nodes before the graph is instantiated, so the graph is kept for that too
+        _prof.graph_reserve_markers(len(self._buckets.buckets) if self._buckets is not None else 0)
+        keep = self._buckets is not None or _prof.graph_timing_requested()
+        g = torch.cuda.CUDAGraph(keep_graph=keep)
         try:
             with torch.cuda.graph(g):
                 with contextlib.ExitStack() as es:
@@ -351,6 +357,9 @@ class TrainStep:
             if n != len(self._buckets.buckets):
                 raise RuntimeError(f"graph bucket markers: found {n}, expected "
                                    f"{len(self._buckets.buckets)}")
+        if _prof.graph_marks_pending():
+            _prof.graph_attach(g.raw_cuda_graph())
+        if keep:
             g.instantiate()
         self._g = g
         self._loss = loss.detach()
@@ -379,6 +388,7 @@ class TrainStep:
             self._m.copy_(masks)
         if self._prep is not None:
             self._prep.run()  # from the weights the last Adam step left
+        _prof.graph_before_replay(self._g)
         self._g.replay()
         if self.dp:
             self._buckets.reduce(self.pg)

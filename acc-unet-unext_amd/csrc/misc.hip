@@ -636,6 +636,95 @@ extern "C" int accunet_event_create(void** ev) {
   return ACC_OK;
 }
 
+extern "C" int accunet_event_create_timed(void** ev) {
+  if (!ev) return ACC_EBADARG;
+  hipEvent_t e;
+  if (hipEventCreate(&e) != hipSuccess) return ACC_ELAUNCH;
+  *ev = (void*)e;
+  return ACC_OK;
+}
+
+// the one kernel node of graph g that launches marker id (nullptr: none or several)
+static hipGraphNode_t find_marker(hipGraph_t g, int id) {
+  size_t nn = 0;
+  if (hipGraphGetNodes(g, nullptr, &nn) != hipSuccess || nn == 0) return nullptr;
+  hipGraphNode_t* nodes = (hipGraphNode_t*)malloc(sizeof(hipGraphNode_t) * nn);
+  if (!nodes) return nullptr;
+  hipGraphNode_t hit = nullptr;
+  int count = 0;
+  if (hipGraphGetNodes(g, nodes, &nn) == hipSuccess) {
+    for (size_t k = 0; k < nn; ++k) {
+      hipGraphNodeType t;
+      if (hipGraphNodeGetType(nodes[k], &t) != hipSuccess || t != hipGraphNodeTypeKernel) continue;
+      hipKernelNodeParams kp;
+      if (hipGraphKernelNodeGetParams(nodes[k], &kp) != hipSuccess) continue;
+      if (kp.func == Markers::get(id)) {
+        hit = nodes[k];
+        ++count;
+      }
+    }
+  }
+  free(nodes);
+  return count == 1 ? hit : nullptr;
+}
+
+// event-record node in place of marker node m: same dependencies, same dependents;
+// the marker is removed only once the new node is wired (a failure leaves a valid graph)
+static int replace_marker(hipGraph_t g, hipGraphNode_t m, hipEvent_t ev, hipGraphNode_t* out) {
+  size_t np = 0, ns = 0;
+  if (hipGraphNodeGetDependencies(m, nullptr, &np) != hipSuccess ||
+      hipGraphNodeGetDependentNodes(m, nullptr, &ns) != hipSuccess)
+    return ACC_ELAUNCH;
+  hipGraphNode_t* pr = (hipGraphNode_t*)malloc(sizeof(hipGraphNode_t) * (np + ns + 1));
+  if (!pr) return ACC_EBADARG;
+  hipGraphNode_t* su = pr + np;
+  int rc = ACC_OK;
+  if ((np && hipGraphNodeGetDependencies(m, pr, &np) != hipSuccess) ||
+      (ns && hipGraphNodeGetDependentNodes(m, su, &ns) != hipSuccess))
+    rc = ACC_ELAUNCH;
+  hipGraphNode_t e = nullptr;
+  if (rc == ACC_OK && hipGraphAddEventRecordNode(&e, g, np ? pr : nullptr, np, ev) != hipSuccess)
+    rc = ACC_ELAUNCH;
+  for (size_t k = 0; rc == ACC_OK && k < ns; ++k)
+    if (hipGraphAddDependencies(g, &e, &su[k], 1) != hipSuccess) rc = ACC_ELAUNCH;
+  if (rc == ACC_OK && hipGraphDestroyNode(m) != hipSuccess) rc = ACC_ELAUNCH;
+  free(pr);
+  if (rc == ACC_OK) *out = e;
+  return rc;
+}
+
+extern "C" int accunet_graph_time_markers(void* graph, int id_start, int id_end, void* ev_start,
+                                          void* ev_end, void** nodes) {
+  if (!graph || !ev_start || !ev_end || !nodes || id_start == id_end || id_start < 0 ||
+      id_end < 0 || id_start >= ACC_MAX_MARKERS || id_end >= ACC_MAX_MARKERS)
+    return ACC_EBADARG;
+  hipGraph_t g = (hipGraph_t)graph;
+  hipGraphNode_t ms = find_marker(g, id_start), me = find_marker(g, id_end);
+  if (!ms || !me) return ACC_EBADSHAPE;
+  hipGraphNode_t es = nullptr, ee = nullptr;
+  int rc = replace_marker(g, ms, (hipEvent_t)ev_start, &es);
+  if (rc != ACC_OK) return rc;
+  rc = replace_marker(g, me, (hipEvent_t)ev_end, &ee);
+  if (rc != ACC_OK) return rc;
+  nodes[0] = (void*)es;
+  nodes[1] = (void*)ee;
+  return ACC_OK;
+}
+
+extern "C" int accunet_graph_exec_event_set(void* exec, void* node, void* ev) {
+  if (!exec || !node || !ev) return ACC_EBADARG;
+  return hipGraphExecEventRecordNodeSetEvent((hipGraphExec_t)exec, (hipGraphNode_t)node,
+                                             (hipEvent_t)ev) == hipSuccess
+             ? ACC_OK
+             : ACC_ELAUNCH;
+}
+
+extern "C" int accunet_event_elapsed_ms(void* start, void* end, float* ms) {
+  if (!start || !end || !ms) return ACC_EBADARG;
+  return hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)end) == hipSuccess ? ACC_OK
+                                                                                   : ACC_ELAUNCH;
+}
+
 extern "C" int accunet_event_destroy(void* ev) {
   return hipEventDestroy((hipEvent_t)ev) == hipSuccess ? ACC_OK : ACC_ELAUNCH;
 }

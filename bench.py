@@ -26,12 +26,17 @@ launch; --eager launches every kernel from Python instead.
 roofline probes; accunet/unext.py).
 
 Extra objects on the line:
-  roofline     — the HANC depthwise stage (K1, `dw3x3_tile_fwd_kernel` of cnv12,
-                 B x 256^2 x 96) re-launched back-to-back at its in-model shape after
-                 the timed steps, timed with HIP events on its launch stream;
-                 algorithmic bytes (2 x B*H*W*C*4) / average launch time vs the 8 TB/s
-                 HBM3E peak; `rooflines` adds K3 (cnv12's SE) and the largest MFMA
-                 GEMM (cnv72's HANC x-branch) (see DESIGN.md 3, accunet/probe.py);
+  roofline     — the HANC depthwise stage (K1, the depthwise kernel of cnv12 and
+                 cnv92, B x 256^2 x 96) timed inside the replayed training graph of
+                 every timed step: event-record nodes stand around those launches
+                 (accunet/profile.py), on the stream they run on; algorithmic bytes
+                 (2 x B*H*W*C*4) / average launch time vs the 8 TB/s HBM3E peak.
+                 `probe`: the same kernel re-launched back-to-back at that shape after
+                 the timed steps, beside the fastest copy of the same bytes
+                 (accunet/probe.py). `rooflines` adds K3 (the SE layer, timed the
+                 same two ways) and the largest MFMA GEMM (cnv72's HANC x-branch,
+                 probe only); `roofline_dw_se` reads K1 + K3
+                 together;
   cpu_baseline — the CPU oracle (oracle/accunet_oracle.py, plain PyTorch-CPU, same op
                  sequence as the reference) timed on this host on a bounded sample;
                  its `parity` object runs the HIP model and the CPU path on the same
@@ -450,6 +455,18 @@ def main():
                                    blk.conv2.bias, dtype=model.act_dtype)
         torch.cuda.synchronize()
 
+    # K1 / K3 timed INSIDE the captured training step: the first two launches of each
+    # (cnv12's / cnv92's depthwise stage at B x 256^2 x 96, the first two SE layers at
+    # B x 256^2 x 32) get event-record nodes around them (accunet/profile.py), re-pointed
+    # at a fresh event pair for every replay of the timed region
+    in_graph = not args.eager and not unext and not args.no_probe
+    if in_graph:
+        blk = model.cnv12
+        k1_tag = f"dw3x3_fwd B{B} {S}x{S} C{blk.conv2.weight.shape[0]}"
+        k3_tag = f"se_fwd B{B} HW{S * S} C{blk.sqe.fc2.weight.shape[0]}"
+        prof.graph_time(k1_tag, 2)
+        prof.graph_time(k3_tag, 2)
+
     for _ in range(args.warmup):
         step(x, mask)
     torch.cuda.synchronize()
@@ -458,6 +475,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    prof.graph_window(True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step(x, mask)
@@ -465,7 +483,9 @@ def main():
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
+    prof.graph_window(False)
     prof.enable(False)
+    graph_rows = {r["tag"]: r for r in prof.graph_rows(HBM_PEAK_GBS)} if in_graph else {}
     dt = t1 - t0
     per_rank = [dt]
     if world > 1:
@@ -511,8 +531,10 @@ def main():
     }
     # roofline: K1, the HANC depthwise stage at the north-star instance (cnv12's
     # dw3x3 over B x 256^2 x 96; cnv92 has the same shape), SURVEY.md 8(d), plus K3
-    # (cnv12's SE) and the largest MFMA GEMM, each re-launched back-to-back at its
-    # in-model shape right after the timed steps (accunet/probe.py)
+    # (the SE layer) and the largest MFMA GEMM. K1 and K3: their in-model launches of
+    # the timed steps (event-record nodes in the graph, above); each is also
+    # re-launched back-to-back at its in-model shape right after the timed steps
+    # (accunet/probe.py: `probe`, with the copy ceiling), the GEMM only that way
     if not args.no_probe and not unext:
         from accunet import probe
         blk = model.cnv12
@@ -522,6 +544,25 @@ def main():
               probe.k3_se(B, S, S, blk.sqe.fc2.weight.shape[0], blk.sqe, dtype=adt),
               probe.hanc_gemm(B * (S // 4) ** 2, model.cnv72.hnc.cnv.weight.shape[0],
                               model.cnv72.conv1.weight.shape[0], dtype=adt)]
+        if k1_before is not None:
+            rl[0]["before_steps"] = {k: k1_before[k] for k in
+                                     ("avg_us", "median_us", "frac", "copy_us", "frac_of_copy")}
+        # K1 / K3: the launches of the timed steps are the row, the probe is kept beside
+        # it. (K3's probe re-reads one 134 MB input back to back, which can partly stay in
+        # the 256 MB Infinity Cache; in the step its launches ran ~25 % longer.)
+        notes = {0: "cnv12's and cnv92's depthwise launch", 1: "the first two SE launches of this shape"}
+        for i, tag in ((0, k1_tag if in_graph else None), (1, k3_tag if in_graph else None)):
+            row = graph_rows.get(tag)
+            if row is None:
+                continue
+            row.pop("tag")
+            row["timing"] = f"in-graph: event-record nodes around {notes[i]} in every timed step"
+            row["probe"] = {k: v for k, v in rl[i].items()
+                            if k in ("avg_us", "median_us", "frac", "launch_us", "copy_us",
+                                     "copy_median_us", "frac_of_copy", "before_steps")}
+            rl[i] = row
+        if in_graph and prof.graph_error():
+            line["graph_timing_error"] = prof.graph_error()
         # HBM traffic of K1 / K3 from the committed PMC passes of this same bench command
         # (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate runs; tools/pmc_traffic.py),
         # only when taken on this tree's kernel sources
@@ -529,9 +570,6 @@ def main():
                              args.dtype, probe.K1_SOURCES)
         probe.attach_traffic(rl[1], os.path.join(ROOT, "profiles", "k3_traffic.json"),
                              args.dtype, probe.K3_SOURCES)
-        if k1_before is not None:
-            rl[0]["before_steps"] = {k: k1_before[k] for k in
-                                     ("avg_us", "median_us", "frac", "copy_us", "frac_of_copy")}
         line["roofline"] = rl[0]
         line["rooflines"] = rl
         # the HANC depthwise + SE reading, (bytes K1 + bytes K3) over the sum
@@ -544,6 +582,10 @@ def main():
                                   "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
                                   "kernels": [k1["kernel"], k3["kernel"]],
                                   "bytes_alg": by, "us": round(us, 2)}
+        if "probe" in k1 and "probe" in k3:
+            pus = k1["probe"]["avg_us"] + k3["probe"]["avg_us"]
+            line["roofline_dw_se"]["probe"] = {"us": round(pus, 2),
+                                               "frac": round(by / (pus * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
     if args.eager:
         line["rooflines_in_model"] = prof.rooflines(HBM_PEAK_GBS)
     line["mode"] = "eager" if args.eager else "hipgraph"

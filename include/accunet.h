@@ -371,6 +371,21 @@ int accunet_event_destroy(void* ev);
 int accunet_stream_wait_event(void* stream, void* ev);
 int accunet_event_synchronize(void* ev);
 
+/* In-graph kernel timing (bench.py's roofline over the timed region; no reference
+ * counterpart). event_create_timed makes an event that records timestamps.
+ * graph_time_markers(graph, id_start, id_end, ev_start, ev_end, nodes[2]) replaces the
+ * marker kernels id_start / id_end of the un-instantiated hipGraph_t by event-record
+ * nodes with the markers' dependencies and dependents (no marker launch is left in
+ * the graph) and returns the two node handles; exec_event_set(exec, node, ev) points
+ * such a node of the instantiated graph at another event for the next launches
+ * (one event pair per replay); event_elapsed_ms(a, b, &ms) reads the time between
+ * two completed records. */
+int accunet_event_create_timed(void** ev);
+int accunet_graph_time_markers(void* graph, int id_start, int id_end, void* ev_start,
+                               void* ev_end, void** nodes);
+int accunet_graph_exec_event_set(void* exec, void* node, void* ev);
+int accunet_event_elapsed_ms(void* start, void* end, float* ms);
+
 /* ------------------------------------------------------------------------- *
  * Streaming ceiling for the roofline probes (accunet/probe.py): copies n_bytes
  * (a multiple of 16, 16-B aligned buffers) from src to dst with non-temporal float4

@@ -1,0 +1,74 @@
+"""In-graph kernel timing (accunet/profile.py graph_time / graph_attach /
+graph_before_replay / graph_rows), the measurement behind bench.py's `roofline`:
+marker kernels around the first launches of a tag are replaced by event-record
+nodes before the training graph is instantiated, and every replay of a window
+records into a fresh event pair."""
+import os
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+from parity_util import O  # noqa: E402
+from accunet import model as M  # noqa: E402
+from accunet import probe  # noqa: E402
+from accunet import profile as prof  # noqa: E402
+
+DEV = "cuda"
+
+
+def _run(sd, x, mask, nf, steps, tags=()):
+    from accunet.train import TrainStep
+    m = M.VARIANTS["canonical"](3, 1, n_filts=nf)
+    m.load_state_dict(sd)
+    m = m.to(DEV).train()
+    for t in tags:
+        prof.graph_time(t, 2)
+    step = TrainStep(m, lr=1e-3, graph=True)
+    losses = [float(step(x, mask).item())]  # capture + first replay
+    prof.graph_window(True)
+    losses += [float(step(x, mask).item()) for _ in range(steps)]
+    torch.cuda.synchronize()
+    prof.graph_window(False)
+    rows = {r["tag"]: r for r in prof.graph_rows(8000.0)}
+    return m, losses, rows
+
+
+def test_graph_timing_rows_and_unchanged_results():
+    """Timing K1 (depthwise) and K3 (SE) inside the graph: two launches of each per
+    replay are measured (6 per tag over 3 replays), their mean agrees with the same
+    kernel re-launched back-to-back at that shape (within 2x either way: clocks and
+    the other stream differ), no error is recorded, and the step's losses, parameters
+    and running statistics are bit-identical to the untimed graph's."""
+    nf, B, S = 32, 4, 128
+    sd = O.det_state_dict(O.param_spec("canonical", 3, 1, nf), seed=0)
+    x = O.det_input((B, 3, S, S), "golden-x").to(DEV)
+    mask = O.det_mask((B, 1, S, S), "golden-mask", p=0.4).to(DEV)
+    m0, l0, r0 = _run(sd, x, mask, nf, 3)
+    assert r0 == {}
+    C1 = m0.cnv12.conv2.weight.shape[0]
+    Cse = m0.cnv12.sqe.fc2.weight.shape[0]
+    k1_tag = f"dw3x3_fwd B{B} {S}x{S} C{C1}"
+    k3_tag = f"se_fwd B{B} HW{S * S} C{Cse}"
+    m1, l1, r1 = _run(sd, x, mask, nf, 3, (k1_tag, k3_tag))
+    assert prof.graph_error() is None, prof.graph_error()
+    assert l0 == l1, (l0, l1)
+    s0, s1 = m0.state_dict(), m1.state_dict()
+    for k in s0:
+        assert torch.equal(s0[k], s1[k]), k
+    assert set(r1) == {k1_tag, k3_tag}, list(r1)
+    for tag in (k1_tag, k3_tag):
+        r = r1[tag]
+        assert r["launches"] == 6, r
+        assert all(0.0 < v < 5000.0 for v in r["launch_us"]), r["launch_us"]
+    blk = m1.cnv12
+    pk1 = probe.k1_dw3x3(B, S, S, C1, blk.conv2.weight, blk.conv2.bias)
+    pk3 = probe.k3_se(B, S, S, Cse, blk.sqe)
+    for tag, p in ((k1_tag, pk1), (k3_tag, pk3)):
+        ratio = r1[tag]["avg_us"] / p["avg_us"]
+        assert 0.5 < ratio < 2.0, (tag, r1[tag]["avg_us"], p["avg_us"])
+        assert r1[tag]["shape"] == p["shape"] and r1[tag]["kernel"] == p["kernel"]
