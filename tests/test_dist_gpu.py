@@ -79,14 +79,19 @@ def test_rccl_world1_graph_buckets():
 
 @pytest.mark.gpu
 def test_world2_bench_line():
+    """World 2 with the roofline probes on: the in-graph K1 / K3 timing shares the
+    graph's marker table with the gradient buckets (ids from the top vs from 0)."""
     r = _run(["bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1", "--batch", "2",
-              "--size", "64", "--no-probe"])
+              "--size", "64"])
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith('{"metric"')]
     assert len(lines) == 1, r.stdout[-2000:]
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 4 and d["value"] > 0
     assert d["scaling"] == "weak" and "cpu_baseline" not in d
+    assert "graph_timing_error" not in d, d.get("graph_timing_error")
+    for row in d["rooflines"][:2]:
+        assert row["timing"].startswith("in-graph") and row["launches"] == 4, row
 
 
 @pytest.mark.gpu
