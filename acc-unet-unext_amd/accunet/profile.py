@@ -179,35 +179,60 @@ def graph_error():
 
 
 def graph_window(on: bool):
-    """open (collect one event pair per timed launch and replay) / close the window"""
+    """open (collect one event pair per timed launch and replay) / close the window.
+    Closing points the timing nodes back at the pairs they were created with, so later
+    replays never record into an event graph_rows() destroys."""
     global _gt_window
     if on:
         _gt_window = []
     elif _gt_window is not None:
-        _gt_window = list(_gt_window)
         _gt_closed.append(_gt_window)
         _gt_window = None
+        _restore_first()
 
 
 _gt_closed = []
+_gt_graph = None      # the torch CUDAGraph whose nodes the window re-pointed
+
+
+def _restore_first():
+    global _gt_error
+    if _gt_graph is None or not _gt_nodes:
+        return
+    import ctypes
+    from . import _lib
+    lib = _lib.load()
+    ex = ctypes.c_void_p(_gt_graph.raw_cuda_graph_exec())
+    for (tag, ns, ne), (es, ee) in zip(_gt_nodes, _gt_first):
+        if (lib.accunet_graph_exec_event_set(ex, ns, es) != 0 or
+                lib.accunet_graph_exec_event_set(ex, ne, ee) != 0):
+            # the nodes may still name a window event: keep every window's events alive
+            _gt_error = "accunet_graph_exec_event_set failed restoring the timing nodes"
+            _gt_nodes.clear()
+            return
+
+
+_gt_keep = []         # event pairs that must outlive the process's replays
 
 
 def graph_before_replay(graph) -> None:
     """point the timing nodes of `graph` (torch CUDAGraph) at fresh events for its next
     replay while a window is open"""
-    global _gt_error
+    global _gt_error, _gt_graph
     if _gt_window is None or not _gt_nodes:
         return
     import ctypes
     from . import _lib
     lib = _lib.load()
+    _gt_graph = graph
     ex = ctypes.c_void_p(graph.raw_cuda_graph_exec())
     for tag, ns, ne in _gt_nodes:
         es, ee = _timed_event(), _timed_event()
         if (lib.accunet_graph_exec_event_set(ex, ns, es) != 0 or
                 lib.accunet_graph_exec_event_set(ex, ne, ee) != 0):
             _gt_error = "accunet_graph_exec_event_set failed"
-            _gt_nodes.clear()
+            _gt_nodes.clear()  # no more re-pointing; nodes may name any event made so far,
+            _gt_keep.append((es, ee))  # so none of them is ever destroyed
             return
         _gt_window.append((tag, es, ee))
 
@@ -239,7 +264,10 @@ def graph_rows(hbm_peak_gbs: float):
                      "frac_median": round(m["bytes"] / (med * 1e-6) / 1e9 / hbm_peak_gbs, 4),
                      "launch_us": [round(v, 1) for v in us], "launches": len(us),
                      "bytes_alg_per_launch": m["bytes"], "tag": tag})
-    for lst in _gt_closed:  # the events are done with
+    # the nodes point at their first pair again (graph_window(False)): the window's
+    # events are done with once their records completed (synchronised above); after a
+    # failed re-point (graph_error) the nodes may still name one of them: keep them all
+    for lst in (_gt_closed if _gt_error is None else []):
         for _, es, ee in lst:
             lib.accunet_event_destroy(es)
             lib.accunet_event_destroy(ee)

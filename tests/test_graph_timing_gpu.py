@@ -35,7 +35,7 @@ def _run(sd, x, mask, nf, steps, tags=()):
     torch.cuda.synchronize()
     prof.graph_window(False)
     rows = {r["tag"]: r for r in prof.graph_rows(8000.0)}
-    return m, losses, rows
+    return m, losses, rows, step
 
 
 def test_graph_timing_rows_and_unchanged_results():
@@ -48,13 +48,13 @@ def test_graph_timing_rows_and_unchanged_results():
     sd = O.det_state_dict(O.param_spec("canonical", 3, 1, nf), seed=0)
     x = O.det_input((B, 3, S, S), "golden-x").to(DEV)
     mask = O.det_mask((B, 1, S, S), "golden-mask", p=0.4).to(DEV)
-    m0, l0, r0 = _run(sd, x, mask, nf, 3)
+    m0, l0, r0, _ = _run(sd, x, mask, nf, 3)
     assert r0 == {}
     C1 = m0.cnv12.conv2.weight.shape[0]
     Cse = m0.cnv12.sqe.fc2.weight.shape[0]
     k1_tag = f"dw3x3_fwd B{B} {S}x{S} C{C1}"
     k3_tag = f"se_fwd B{B} HW{S * S} C{Cse}"
-    m1, l1, r1 = _run(sd, x, mask, nf, 3, (k1_tag, k3_tag))
+    m1, l1, r1, st1 = _run(sd, x, mask, nf, 3, (k1_tag, k3_tag))
     assert prof.graph_error() is None, prof.graph_error()
     assert l0 == l1, (l0, l1)
     s0, s1 = m0.state_dict(), m1.state_dict()
@@ -72,3 +72,15 @@ def test_graph_timing_rows_and_unchanged_results():
         ratio = r1[tag]["avg_us"] / p["avg_us"]
         assert 0.5 < ratio < 2.0, (tag, r1[tag]["avg_us"], p["avg_us"])
         assert r1[tag]["shape"] == p["shape"] and r1[tag]["kernel"] == p["kernel"]
+    # replays after the window (the window's events are destroyed: the nodes must point
+    # at their first pair again), then a second window
+    for _ in range(2):
+        st1(x, mask)
+    torch.cuda.synchronize()
+    prof.graph_window(True)
+    st1(x, mask)
+    torch.cuda.synchronize()
+    prof.graph_window(False)
+    r2 = {r["tag"]: r for r in prof.graph_rows(8000.0)}
+    assert prof.graph_error() is None, prof.graph_error()
+    assert {t: r["launches"] for t, r in r2.items()} == {k1_tag: 2, k3_tag: 2}, r2
