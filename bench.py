@@ -95,7 +95,7 @@ def parse():
                          "gradient buckets all-reduced by RCCL over a world-1 process group) "
                          "against the plain step, same box, and report dp_overhead_ms")
     ap.add_argument("--cpu-sample", type=int, default=None,
-                    help="images in the CPU sample (3; unext 16)")
+                    help="images per timed CPU step (2; unext 16)")
     return ap.parse_args()
 
 
@@ -158,11 +158,15 @@ def _cpu_model():
     return "unknown"
 
 
+CPU_WARM, CPU_TIMED = 2, 3  # 2 warm + 3 timed steps
+
+
 def cpu_baseline(variant, size, n_img, model="acc_unet"):
-    """Time the CPU oracle on a bounded sample of the same workload: one untimed warm-up
-    step on 1 image (first-touch allocation, thread-pool start), then one timed step on
-    n_img images: forward + WeightedDiceBCE + backward + torch.optim.Adam(lr 1e-3) step
-    (SURVEY 8(d)'s CPU protocol, cut to one timed step to stay within ~30 s)."""
+    """Time the CPU oracle on a bounded sample of the same workload, SURVEY 8(d)'s CPU
+    protocol: two untimed warm-up steps on 1 image (first-touch allocation, thread-pool
+    start), then three timed steps of n_img images each: forward + WeightedDiceBCE +
+    backward + torch.optim.Adam(lr 1e-3) step. `value` is the images of the three steps
+    over their summed time; the per-step rates give the spread."""
     O = _oracle()
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
     torch.set_num_threads(threads)
@@ -184,16 +188,23 @@ def cpu_baseline(variant, size, n_img, model="acc_unet"):
         opt.step()
 
     t0 = time.perf_counter()
-    step(1, "bench-cpu-warm")
+    for i in range(CPU_WARM):
+        step(1, f"bench-cpu-warm{i}")
     t_warm = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    step(n_img, "bench-cpu")
-    dt = time.perf_counter() - t0
+    dts = []
+    for i in range(CPU_TIMED):
+        t0 = time.perf_counter()
+        step(n_img, f"bench-cpu{i}")
+        dts.append(time.perf_counter() - t0)
     del params, opt
-    return {"value": n_img / dt, "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"1 untimed warm-up step (1 image, {t_warm:.1f} s), then 1 timed step of "
-                      f"{n_img} image(s): {name} 3x{size}x{size} fwd + WeightedDiceBCE + bwd + "
-                      f"Adam, fp32, torch-CPU oracle, {dt:.1f} s",
+    rates = [n_img / d for d in dts]
+    return {"value": CPU_TIMED * n_img / sum(dts), "unit": "images/s", "cores": threads,
+            "kind": "port", "steps_images_per_s": [round(r, 4) for r in rates],
+            "spread": round((max(rates) - min(rates)) / (sum(rates) / len(rates)), 4),
+            "sample": f"{CPU_WARM} untimed warm-up steps (1 image each, {t_warm:.1f} s), then "
+                      f"{CPU_TIMED} timed steps of {n_img} image(s) each: {name} "
+                      f"3x{size}x{size} fwd + WeightedDiceBCE + bwd + Adam, fp32, torch-CPU "
+                      f"oracle, {sum(dts):.1f} s",
             "cpu_model": _cpu_model()}
 
 
@@ -414,7 +425,7 @@ def main():
     if args.size is None:
         args.size = 224 if unext else 256
     if args.cpu_sample is None:
-        args.cpu_sample = 16 if unext else 3
+        args.cpu_sample = 16 if unext else 2
     torch.manual_seed(0)
     if unext:
         from accunet.unext import UNext
